@@ -1,0 +1,208 @@
+/*
+ * kxcodec.h — C-ABI of the MI355X batch payload codec (libkxcodec.so).
+ *
+ * This is the drop-in boundary for Kitex's payload-codec hot path. Every entry point is plain C:
+ * pointers + sizes, no exceptions, no torch/HIP C++ types (streams travel as `void*` = hipStream_t).
+ * Device pointers are caller-owned hipMalloc'd memory unless a comment says "host".
+ *
+ * Reference interfaces each entry point replaces (paths relative to cloudwego/kitex):
+ *   kx_schema_create ............ the generated per-type FastCodec trio is driven by the IDL; the schema
+ *                                 is the flattened IDL (pkg/generic/descriptor/descriptor.go:64-80 model,
+ *                                 tool/internal_pkg/pluginmode/thriftgo/struct_tpl.go:41-391 semantics)
+ *   kx_thrift_decode_batch ...... thrift.FastCodec.FastRead (internal/mocks/thrift/k-mock.go:39-114,
+ *                                 template struct_tpl.go:41-149) applied to N records, as called from
+ *                                 fastUnmarshal (pkg/remote/codec/thrift/codec_fast.go:60-82) when the
+ *                                 message lengths are known (offsets != NULL), or as the element loop of
+ *                                 a list<Struct> (FieldFastReadList, struct_tpl.go:582-625) when the
+ *                                 records are concatenated (offsets == NULL)
+ *   kx_thrift_skip_batch ........ the skip decoder netpollSkipDecoder.SkipStruct/skipType
+ *                                 (pkg/remote/codec/thrift/codec_apache.go:166-293) over N records
+ *   kx_thrift_encoded_size_batch  thrift.FastCodec.BLength (k-mock.go:201-210; struct_tpl.go:266-391)
+ *   kx_thrift_encode_batch ...... thrift.FastCodec.FastWriteNocopy (k-mock.go:190-199; struct_tpl.go:225-264,
+ *                                 field reorder pkg tool/.../thriftgo/patcher.go:503-522)
+ *   kx_pb_decode_batch .......... proto.Unmarshal of the Kitex-Protobuf body
+ *                                 (pkg/remote/codec/protobuf/protobuf.go:209-216 -> service.go:358-365)
+ *   kx_host_decode_batch ........ fastUnmarshal end to end from host (netpoll) memory: pinned H2D ->
+ *                                 decode -> D2H (codec_fast.go:60-82 with the Next(dataLen) slice)
+ *   kx_strerror ................. error text; codes mirror pkg/remote/codec/perrors/protocol_error.go:28-36
+ */
+#ifndef KXCODEC_H_
+#define KXCODEC_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KX_ABI_VERSION 1
+
+/* ---- Thrift TType ids (gopkg protocol/thrift; pinned by pkg/protocol/bthrift/binary_test.go) ---- */
+enum {
+  KX_T_STOP = 0, KX_T_VOID = 1, KX_T_BOOL = 2, KX_T_BYTE = 3, KX_T_DOUBLE = 4,
+  KX_T_I16 = 6, KX_T_I32 = 8, KX_T_I64 = 10, KX_T_STRING = 11, KX_T_STRUCT = 12,
+  KX_T_MAP = 13, KX_T_SET = 14, KX_T_LIST = 15
+};
+
+/* ---- Thrift message types (WriteMessageBegin, binary_test.go:387-457) ---- */
+enum { KX_MSG_CALL = 1, KX_MSG_REPLY = 2, KX_MSG_EXCEPTION = 3, KX_MSG_ONEWAY = 4 };
+
+/* ---- return / status codes ----
+ * 1..6 are the thrift TProtocolException type ids (perrors/protocol_error.go:28-36):
+ * the Go shim maps any non-zero code to remote.NewTransError(remote.ProtocolError, ...)
+ * exactly as fastUnmarshal does (codec_fast.go:65,69,79). */
+enum {
+  KX_OK = 0,
+  KX_ERR_INVALID_DATA = 1,     /* unknown type id, required field missing, bad magic */
+  KX_ERR_NEGATIVE_SIZE = 2,    /* negative string/list/map length */
+  KX_ERR_SIZE_LIMIT = 3,       /* an output capacity (records / arena) is too small */
+  KX_ERR_BAD_VERSION = 4,      /* MessageBegin / Kitex-PB magic mismatch */
+  KX_ERR_NOT_IMPLEMENTED = 5,  /* schema shape not supported by this build */
+  KX_ERR_DEPTH_LIMIT = 6,      /* skip recursion depth (64, codec_apache.go:167) exceeded */
+  KX_ERR_EOF = 8,              /* record runs past the end of its buffer */
+  KX_ERR_INVALID_ARG = 100,
+  KX_ERR_HIP = 101,            /* a HIP runtime call failed */
+  KX_ERR_NO_DEVICE = 102,
+  KX_ERR_INTERNAL = 103        /* bounded spin expired / invariant broken */
+};
+
+/* ---- requiredness (thriftgo Requiredness; struct_tpl.go:55-58,313-340) ---- */
+enum { KX_REQ_DEFAULT = 0, KX_REQ_REQUIRED = 1, KX_REQ_OPTIONAL = 2 };
+
+/* ---- schema (flattened IDL) ---- */
+typedef struct kx_field_desc {
+  int16_t id;            /* thrift field id */
+  uint8_t ttype;         /* KX_T_* of the field */
+  uint8_t req;           /* KX_REQ_* */
+  uint8_t elem_ttype;    /* LIST/SET: element KX_T_* (must be a scalar, or STRING) */
+  uint8_t reserved0;
+  int16_t child;         /* STRUCT: index of the child struct in the schema's struct table; else -1 */
+  int64_t default_bits;  /* scalar default value (two's complement / IEEE bits); ignored otherwise */
+} kx_field_desc;
+
+typedef struct kx_struct_desc {
+  const kx_field_desc* fields; /* host memory, IDL order */
+  uint32_t nfields;
+  uint32_t reserved0;
+} kx_struct_desc;
+
+typedef struct kx_schema kx_schema; /* opaque */
+
+/* Column kinds produced by flattening (depth-first over the IDL, struct fields inlined). */
+enum {
+  KX_COL_FIXED = 1,   /* one value per record, width 1/2/4/8 bytes, host (little-endian) order */
+  KX_COL_BYTES = 2,   /* string/binary: u32 offsets[n+1] (bytes) + data arena */
+  KX_COL_LIST = 3     /* list/set of fixed scalars: u32 offsets[n+1] (elements) + element arena */
+};
+
+typedef struct kx_column_info {
+  uint32_t kind;        /* KX_COL_* */
+  uint32_t width;       /* FIXED: value width; LIST: element width; BYTES: 1 */
+  uint8_t ttype;        /* wire type of the field (LIST/SET for lists) */
+  uint8_t elem_ttype;   /* LIST: element wire type */
+  int16_t field_id;     /* id of the leaf field */
+  int32_t presence_bit; /* bit in the presence word for this field, or -1 */
+  uint32_t depth;       /* nesting depth (0 = root field) */
+  int16_t path[8];      /* field ids from the root to this leaf */
+} kx_column_info;
+
+/* A batch of decoded records in struct-of-arrays form. All pointers are DEVICE memory for the
+ * *_batch calls and HOST memory for kx_host_* calls. */
+typedef struct kx_column {
+  void* data;           /* FIXED: n*width bytes; BYTES/LIST: arena */
+  uint32_t* offsets;    /* BYTES/LIST: n+1 entries (arena units: bytes or elements); FIXED: NULL */
+  uint64_t capacity;    /* BYTES/LIST: arena capacity in arena units; FIXED: ignored */
+} kx_column;
+
+#define KX_MAX_COLUMNS 32
+#define KX_MAX_STRUCTS 16
+
+typedef struct kx_columns {
+  kx_column cols[KX_MAX_COLUMNS];
+  uint32_t ncols;       /* must equal kx_schema_num_columns() */
+  uint32_t reserved0;
+  uint64_t* presence;   /* n words (bit per presence-tracked field), required iff the schema has any */
+} kx_columns;
+
+/* Per-call status, written by the device (caller-owned DEVICE memory, 128 bytes, 8-aligned). */
+typedef struct kx_status {
+  int32_t code;         /* first error (lowest record index), 0 = OK */
+  int32_t reserved0;
+  uint64_t record;      /* index of the failing record */
+  uint64_t offset;      /* byte offset of the failing record's start in the input */
+  uint64_t n_records;   /* records decoded */
+  uint64_t consumed;    /* input bytes consumed (concatenated mode) */
+  uint64_t var_total[8];  /* required arena size (arena units) of the first 8 var columns */
+  uint64_t reserved1[3];
+} kx_status;
+
+typedef struct kx_ctx kx_ctx; /* opaque; one per host thread / stream */
+
+/* ---- lifecycle ---- */
+int kx_abi_version(void);
+const char* kx_strerror(int code);
+
+int kx_schema_create(const kx_struct_desc* structs, uint32_t nstructs, kx_schema** out);
+void kx_schema_destroy(kx_schema* s);
+uint32_t kx_schema_num_columns(const kx_schema* s);
+int kx_schema_column_info(const kx_schema* s, uint32_t col, kx_column_info* out);
+uint32_t kx_schema_presence_bits(const kx_schema* s);
+/* Minimum encoded size of a record (all var fields empty, optional fields unset). */
+uint64_t kx_schema_min_record_size(const kx_schema* s);
+
+int kx_ctx_create(int device, kx_ctx** out);
+void kx_ctx_destroy(kx_ctx* c);
+
+/* ---- Thrift binary: batched FastRead ----
+ * offsets != NULL : record i is in[offsets[i] .. offsets[i+1]) (u64, n+1 entries, device). Each record
+ *                   is decoded independently, trailing bytes inside the range are ignored and a read
+ *                   past the range is KX_ERR_EOF (fastUnmarshal semantics, codec_fast.go:62-71).
+ *                   record_status (optional, n bytes) receives each record's code.
+ * offsets == NULL : exactly n records are concatenated from in[0]; the boundary of each is where its
+ *                   FastRead stops (list<Struct> element loop). status->consumed = bytes used.
+ * On return the work is enqueued on `stream`; status is final when the stream reaches this point. */
+int kx_thrift_decode_batch(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len,
+                           const uint64_t* offsets, uint64_t n, const kx_columns* out,
+                           uint8_t* record_status, kx_status* status, void* stream);
+
+/* Skip decoder over n concatenated records: writes record start offsets (n+1 entries, device u64). */
+int kx_thrift_skip_batch(kx_ctx* c, const uint8_t* in, uint64_t in_len, uint64_t n,
+                         uint64_t* offsets_out, kx_status* status, void* stream);
+
+/* ---- Thrift binary: batched BLength / FastWriteNocopy ---- */
+int kx_thrift_encoded_size_batch(kx_ctx* c, const kx_schema* s, const kx_columns* in, uint64_t n,
+                                 uint64_t* sizes_out, void* stream);
+/* Writes the n encoded records back to back into out[0..). offsets_out (n+1, device, optional)
+ * receives each record's start; status->consumed receives the total size. */
+int kx_thrift_encode_batch(kx_ctx* c, const kx_schema* s, const kx_columns* in, uint64_t n,
+                           uint8_t* out, uint64_t out_cap, uint64_t* offsets_out,
+                           kx_status* status, void* stream);
+
+/* ---- Kitex-Protobuf (proto3 body) ----
+ * The schema's field ids are proto field numbers; ttype selects the proto scalar mapping
+ * (I64 = int64 varint, I32 = int32 varint, BOOL, DOUBLE = fixed64, STRING = string/bytes,
+ * LIST of a scalar = packed repeated). offsets semantics as kx_thrift_decode_batch; with
+ * offsets == NULL the input is the body of `message Batch { repeated Rec recs = 1; }`. */
+int kx_pb_decode_batch(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len,
+                       const uint64_t* offsets, uint64_t n, const kx_columns* out,
+                       uint8_t* record_status, kx_status* status, void* stream);
+
+/* ---- host-memory entry point (the netpoll buffer side) ----
+ * in / out columns / status are HOST memory (pinned or pageable). Synchronous. */
+int kx_host_decode_batch(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len,
+                         const uint64_t* offsets, uint64_t n, const kx_columns* out,
+                         kx_status* status);
+
+/* ---- Thrift MessageBegin (WriteMessageBegin / ReadMessageBegin, binary_test.go:387-457) ---- */
+uint64_t kx_thrift_message_begin_length(uint32_t name_len);
+int kx_thrift_write_message_begin(uint8_t* buf, uint64_t cap, const char* name, uint32_t name_len,
+                                  int32_t msg_type, int32_t seqid, uint64_t* written);
+int kx_thrift_read_message_begin(const uint8_t* buf, uint64_t len, const char** name,
+                                 uint32_t* name_len, int32_t* msg_type, int32_t* seqid,
+                                 uint64_t* consumed);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KXCODEC_H_ */

@@ -1,0 +1,113 @@
+"""ctypes mirror of include/kxcodec.h (the C-ABI boundary).
+
+Kept in one place so that the product binding (kitex_amd._lib) and the test-only oracle binding
+(oracle/oracle.py) describe the very same structs. Any change here must match kxcodec.h; the
+layout is checked by tests/test_abi.py against the compiled library.
+"""
+import ctypes as C
+
+KX_ABI_VERSION = 1
+
+# Thrift TType ids (gopkg protocol/thrift; pinned by pkg/protocol/bthrift/binary_test.go)
+T_STOP, T_VOID, T_BOOL, T_BYTE, T_DOUBLE = 0, 1, 2, 3, 4
+T_I16, T_I32, T_I64, T_STRING, T_STRUCT = 6, 8, 10, 11, 12
+T_MAP, T_SET, T_LIST = 13, 14, 15
+
+MSG_CALL, MSG_REPLY, MSG_EXCEPTION, MSG_ONEWAY = 1, 2, 3, 4
+
+OK = 0
+ERR_INVALID_DATA = 1
+ERR_NEGATIVE_SIZE = 2
+ERR_SIZE_LIMIT = 3
+ERR_BAD_VERSION = 4
+ERR_NOT_IMPLEMENTED = 5
+ERR_DEPTH_LIMIT = 6
+ERR_EOF = 8
+ERR_INVALID_ARG = 100
+ERR_HIP = 101
+ERR_NO_DEVICE = 102
+ERR_INTERNAL = 103
+
+REQ_DEFAULT, REQ_REQUIRED, REQ_OPTIONAL = 0, 1, 2
+FIELD_BINARY = 1  # kx_field_desc.reserved0 flag: protobuf `bytes` (no UTF-8 validation)
+
+COL_FIXED, COL_BYTES, COL_LIST = 1, 2, 3
+MAX_COLUMNS = 32
+MAX_STRUCTS = 16
+
+TYPE_SIZE = {T_BOOL: 1, T_BYTE: 1, T_I16: 2, T_I32: 4, T_I64: 8, T_DOUBLE: 8}
+
+
+class FieldDesc(C.Structure):
+    _fields_ = [
+        ("id", C.c_int16),
+        ("ttype", C.c_uint8),
+        ("req", C.c_uint8),
+        ("elem_ttype", C.c_uint8),
+        ("reserved0", C.c_uint8),
+        ("child", C.c_int16),
+        ("default_bits", C.c_int64),
+    ]
+
+
+class StructDesc(C.Structure):
+    _fields_ = [("fields", C.POINTER(FieldDesc)), ("nfields", C.c_uint32), ("reserved0", C.c_uint32)]
+
+
+class ColumnInfo(C.Structure):
+    _fields_ = [
+        ("kind", C.c_uint32),
+        ("width", C.c_uint32),
+        ("ttype", C.c_uint8),
+        ("elem_ttype", C.c_uint8),
+        ("field_id", C.c_int16),
+        ("presence_bit", C.c_int32),
+        ("depth", C.c_uint32),
+        ("path", C.c_int16 * 8),
+    ]
+
+
+class Column(C.Structure):
+    _fields_ = [("data", C.c_void_p), ("offsets", C.c_void_p), ("capacity", C.c_uint64)]
+
+
+class Columns(C.Structure):
+    _fields_ = [
+        ("cols", Column * MAX_COLUMNS),
+        ("ncols", C.c_uint32),
+        ("reserved0", C.c_uint32),
+        ("presence", C.c_void_p),
+    ]
+
+
+class Status(C.Structure):
+    _fields_ = [
+        ("code", C.c_int32),
+        ("reserved0", C.c_int32),
+        ("record", C.c_uint64),
+        ("offset", C.c_uint64),
+        ("n_records", C.c_uint64),
+        ("consumed", C.c_uint64),
+        ("var_total", C.c_uint64 * 8),
+        ("reserved1", C.c_uint64 * 3),
+    ]
+
+
+assert C.sizeof(FieldDesc) == 16
+assert C.sizeof(Status) == 128
+assert C.sizeof(Columns) == MAX_COLUMNS * 24 + 16
+
+ERROR_NAMES = {
+    OK: "ok",
+    ERR_INVALID_DATA: "invalid data",
+    ERR_NEGATIVE_SIZE: "negative size",
+    ERR_SIZE_LIMIT: "size limit",
+    ERR_BAD_VERSION: "bad version",
+    ERR_NOT_IMPLEMENTED: "not implemented",
+    ERR_DEPTH_LIMIT: "depth limit exceeded",
+    ERR_EOF: "unexpected EOF",
+    ERR_INVALID_ARG: "invalid argument",
+    ERR_HIP: "HIP runtime error",
+    ERR_NO_DEVICE: "no device",
+    ERR_INTERNAL: "internal error",
+}

@@ -1,0 +1,38 @@
+"""Shared test helpers: column-set comparison (host numpy or device torch)."""
+import numpy as np
+
+from kitex_amd import _abi as A
+
+
+def to_np(x):
+    if isinstance(x, np.ndarray):
+        return x
+    return x.detach().cpu().numpy()
+
+
+def assert_columns_equal(got, exp, infos, n, check_presence=True):
+    """Field-for-field equality of the first n records (fixed values, var bytes/elements, offsets)."""
+    for c, ci in enumerate(infos):
+        if ci.kind == A.COL_FIXED:
+            g = to_np(got.cols[c])[:n].view(np.uint8).reshape(n, -1) if n else None
+            e = to_np(exp.cols[c])[:n].view(np.uint8).reshape(n, -1) if n else None
+            if n:
+                bad = np.nonzero((g != e).any(axis=1))[0]
+                assert bad.size == 0, f"column {c} (field {ci.field_id}) differs at records {bad[:8]}"
+        else:
+            go, gd = (to_np(v) for v in got.cols[c])
+            eo, ed = (to_np(v) for v in exp.cols[c])
+            go = go.view(np.uint32)[:n + 1].astype(np.int64) - int(go.view(np.uint32)[0])
+            eo = eo.view(np.uint32)[:n + 1].astype(np.int64) - int(eo.view(np.uint32)[0])
+            lg, le = np.diff(go), np.diff(eo)
+            bad = np.nonzero(lg != le)[0]
+            assert bad.size == 0, f"var column {c} (field {ci.field_id}) lengths differ at {bad[:8]}"
+            g0 = int(to_np(got.cols[c][0]).view(np.uint32)[0])
+            e0 = int(to_np(exp.cols[c][0]).view(np.uint32)[0])
+            tot = int(eo[-1])
+            gb = gd.view(np.uint8)[g0 * gd.itemsize:(g0 + tot) * gd.itemsize]
+            eb = ed.view(np.uint8)[e0 * ed.itemsize:(e0 + tot) * ed.itemsize]
+            assert np.array_equal(gb, eb), f"var column {c} (field {ci.field_id}) payload differs"
+    if check_presence and exp.presence is not None:
+        assert got.presence is not None
+        assert np.array_equal(to_np(got.presence)[:n].view(np.uint64), to_np(exp.presence)[:n].view(np.uint64))
