@@ -1,0 +1,87 @@
+"""ctypes binding of libkxcodec.so (the product C-ABI, include/kxcodec.h).
+
+Fails loudly: there is no CPU fallback anywhere in the product path. If the shared library is
+missing or was built for another ABI version, import of the codec raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+from . import _abi as A
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libkxcodec.so")
+
+_lib = None
+
+EXPORTS = [
+    "kx_abi_version", "kx_strerror", "kx_schema_create", "kx_schema_destroy", "kx_schema_num_columns",
+    "kx_schema_column_info", "kx_schema_presence_bits", "kx_schema_min_record_size", "kx_ctx_create",
+    "kx_ctx_destroy", "kx_thrift_decode_batch", "kx_thrift_skip_batch", "kx_thrift_encoded_size_batch",
+    "kx_thrift_encode_batch", "kx_pb_decode_batch", "kx_host_decode_batch",
+    "kx_thrift_message_begin_length", "kx_thrift_write_message_begin", "kx_thrift_read_message_begin",
+]
+
+
+class KxError(RuntimeError):
+    def __init__(self, code: int, what: str = "", record: int = None, offset: int = None):
+        self.code = code
+        self.record = record
+        self.offset = offset
+        msg = f"{what}: {A.ERROR_NAMES.get(code, code)} (code {code})"
+        if record is not None:
+            msg += f" at record {record} (offset {offset})"
+        super().__init__(msg)
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"libkxcodec.so not built ({LIB_PATH}); run `python -m kitex_amd.build` "
+                          "or __graft_entry__.build()")
+    try:  # share torch's HIP runtime (same soname) when torch is around
+        import torch  # noqa: F401
+    except Exception:
+        pass
+    L = C.CDLL(LIB_PATH)
+    vp, u32, u64, i32 = C.c_void_p, C.c_uint32, C.c_uint64, C.c_int32
+    L.kx_abi_version.restype = C.c_int
+    L.kx_strerror.argtypes = [C.c_int]
+    L.kx_strerror.restype = C.c_char_p
+    L.kx_schema_create.argtypes = [C.POINTER(A.StructDesc), u32, C.POINTER(vp)]
+    L.kx_schema_destroy.argtypes = [vp]
+    L.kx_schema_destroy.restype = None
+    L.kx_schema_num_columns.argtypes = [vp]
+    L.kx_schema_num_columns.restype = u32
+    L.kx_schema_column_info.argtypes = [vp, u32, C.POINTER(A.ColumnInfo)]
+    L.kx_schema_presence_bits.argtypes = [vp]
+    L.kx_schema_presence_bits.restype = u32
+    L.kx_schema_min_record_size.argtypes = [vp]
+    L.kx_schema_min_record_size.restype = u64
+    L.kx_ctx_create.argtypes = [C.c_int, C.POINTER(vp)]
+    L.kx_ctx_destroy.argtypes = [vp]
+    L.kx_ctx_destroy.restype = None
+    dec = [vp, vp, vp, u64, vp, u64, C.POINTER(A.Columns), vp, vp, vp]
+    L.kx_thrift_decode_batch.argtypes = dec
+    L.kx_pb_decode_batch.argtypes = dec
+    L.kx_thrift_skip_batch.argtypes = [vp, vp, u64, u64, vp, vp, vp]
+    L.kx_thrift_encoded_size_batch.argtypes = [vp, vp, C.POINTER(A.Columns), u64, vp, vp]
+    L.kx_thrift_encode_batch.argtypes = [vp, vp, C.POINTER(A.Columns), u64, vp, u64, vp, vp, vp]
+    L.kx_host_decode_batch.argtypes = [vp, vp, vp, u64, vp, u64, C.POINTER(A.Columns), C.POINTER(A.Status)]
+    L.kx_thrift_message_begin_length.argtypes = [u32]
+    L.kx_thrift_message_begin_length.restype = u64
+    L.kx_thrift_write_message_begin.argtypes = [vp, u64, C.c_char_p, u32, i32, i32, C.POINTER(u64)]
+    L.kx_thrift_read_message_begin.argtypes = [vp, u64, C.POINTER(C.c_char_p), C.POINTER(u32),
+                                               C.POINTER(i32), C.POINTER(i32), C.POINTER(u64)]
+    if L.kx_abi_version() != A.KX_ABI_VERSION:
+        raise ImportError(f"libkxcodec ABI {L.kx_abi_version()} != {A.KX_ABI_VERSION}")
+    _lib = L
+    return L
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        raise KxError(rc, what)

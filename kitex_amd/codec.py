@@ -1,0 +1,235 @@
+"""Host-side mirror of Kitex's payload-codec interface over the MI355X C-ABI.
+
+Kitex (Go) plugs payload codecs in through `remote.PayloadCodec{Marshal, Unmarshal, Name}`
+(pkg/remote/payload_codec.go:29-33) and configures the Thrift one with `CodecType` bit flags
+(pkg/remote/codec/thrift/thrift.go:36-53). The classes below keep those names and meanings for a
+*batch* of same-schema records held in HBM:
+
+  ThriftCodec.Unmarshal(buf, n, offsets)  ~ n x FastRead       (codec_fast.go:60-82)
+  ThriftCodec.Marshal(columns)            ~ n x FastWriteNocopy (codec_fast.go:40-58, 85-91)
+  ThriftCodec.BLength(columns)            ~ n x BLength
+  ThriftCodec.Skip(buf, n)                ~ skipThriftStruct    (codec_apache.go:39-68,166)
+
+Errors surface as `ProtocolError` carrying the thrift TProtocolException type id, the way
+fastUnmarshal wraps them in remote.NewTransError(remote.ProtocolError, err).
+
+Every call goes through libkxcodec.so; there is no CPU path. Device buffers are torch tensors
+(torch is only the HBM allocator and stream provider here).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from enum import IntFlag
+from typing import List, Optional, Sequence
+
+from . import _abi as A
+from ._lib import KxError, check, lib
+from .columns import alloc_device, to_kx_columns
+from .schema import Schema
+from .synth import ColumnSet
+
+
+class CodecType(IntFlag):
+    """thrift.go:36-53"""
+    Basic = 0b0000
+    FastWrite = 0b0001
+    FastRead = 0b0010
+    FastReadWrite = 0b0011
+    FrugalWrite = 0b0100
+    FrugalRead = 0b1000
+    FrugalReadWrite = 0b1100
+    EnableSkipDecoder = 0b10000
+
+
+class ProtocolError(KxError):
+    """remote.NewTransError(remote.ProtocolError, err) equivalent (trans_errors.go:35)."""
+
+
+class DeviceSchema:
+    """A Schema compiled by libkxcodec (kx_schema_create)."""
+
+    def __init__(self, schema: Schema):
+        L = lib()
+        self.schema = schema
+        tab, ns = schema.struct_table()
+        h = C.c_void_p()
+        check(L.kx_schema_create(tab, ns, C.byref(h)), "kx_schema_create")
+        self.handle = h
+        self.ncols = L.kx_schema_num_columns(h)
+        self.infos: List[A.ColumnInfo] = []
+        for c in range(self.ncols):
+            ci = A.ColumnInfo()
+            check(L.kx_schema_column_info(h, c, C.byref(ci)), "kx_schema_column_info")
+            self.infos.append(ci)
+        self.npresence = L.kx_schema_presence_bits(h)
+        self.min_record_size = L.kx_schema_min_record_size(h)
+
+    def var_columns(self) -> List[int]:
+        return [c for c, ci in enumerate(self.infos) if ci.kind != A.COL_FIXED]
+
+    def __del__(self):
+        try:
+            if getattr(self, "handle", None):
+                lib().kx_schema_destroy(self.handle)
+                self.handle = None
+        except Exception:
+            pass
+
+
+class Context:
+    """kx_ctx: one per host thread / stream; owns the device workspace."""
+
+    def __init__(self, device: int = 0):
+        h = C.c_void_p()
+        check(lib().kx_ctx_create(device, C.byref(h)), "kx_ctx_create")
+        self.handle = h
+        self.device = device
+
+    def __del__(self):
+        try:
+            if getattr(self, "handle", None):
+                lib().kx_ctx_destroy(self.handle)
+                self.handle = None
+        except Exception:
+            pass
+
+
+def _stream_ptr(stream) -> int:
+    import torch
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return int(s.cuda_stream)
+
+
+def _ptr(t) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+@dataclass
+class DecodeResult:
+    columns: ColumnSet
+    status: "object"          # torch int64[16] on the device (kx_status)
+    record_status: "object"   # torch uint8[n] or None
+
+    def read_status(self) -> A.Status:
+        import torch
+        torch.cuda.current_stream().synchronize()
+        raw = self.status.cpu().numpy().tobytes()
+        st = A.Status.from_buffer_copy(raw)
+        return st
+
+
+def status_tensor(device):
+    import torch
+    return torch.zeros(16, dtype=torch.int64, device=device)
+
+
+def read_status(t) -> A.Status:
+    return A.Status.from_buffer_copy(t.cpu().numpy().tobytes())
+
+
+class ThriftCodec:
+    """Batch Thrift-binary payload codec on one MI355X (remote.PayloadCodec mirror)."""
+
+    def __init__(self, schema: Schema, codec_type: CodecType = CodecType.FastReadWrite, device: int = 0):
+        import torch
+        self.codec_type = codec_type
+        self.dschema = schema if isinstance(schema, DeviceSchema) else DeviceSchema(schema)
+        self.ctx = Context(device)
+        self.device = torch.device("cuda", device)
+
+    # -- remote.PayloadCodec --------------------------------------------------------------------
+    def Name(self) -> str:
+        return "Thrift"
+
+    def Unmarshal(self, buf, n: int, offsets=None, out: ColumnSet = None, var_caps: Sequence[int] = None,
+                  record_status: bool = False, stream=None, raise_on_error: bool = True) -> DecodeResult:
+        """Decode n records from `buf` (uint8 tensor in HBM). offsets: int64[n+1] tensor or None."""
+        import torch
+        ds = self.dschema
+        if out is None:
+            if var_caps is None:
+                var_caps = [0 if ci.kind == A.COL_FIXED else max(1, buf.numel()) for ci in ds.infos]
+            out = alloc_device(ds.infos, n, var_caps, ds.npresence, self.device)
+        kc = to_kx_columns(out, ds.infos, var_caps)
+        st = status_tensor(self.device)
+        rs = torch.empty(max(1, n), dtype=torch.uint8, device=self.device) if record_status else None
+        rc = lib().kx_thrift_decode_batch(self.ctx.handle, ds.handle, _ptr(buf), buf.numel(), _ptr(offsets), n,
+                                          C.byref(kc), _ptr(rs), _ptr(st), _stream_ptr(stream))
+        check(rc, "kx_thrift_decode_batch")
+        res = DecodeResult(out, st, rs)
+        if raise_on_error:
+            s = res.read_status()
+            if s.code:
+                raise ProtocolError(s.code, "thrift unmarshal", s.record, s.offset)
+        return res
+
+    def Marshal(self, cols: ColumnSet, with_offsets: bool = True, stream=None, out=None):
+        """Encode the columns; returns (wire uint8 tensor, record offsets int64[n+1] or None)."""
+        import torch
+        ds = self.dschema
+        n = cols.n
+        kc = to_kx_columns(cols, ds.infos)
+        if out is None:
+            sizes = self.BLength(cols, stream=stream)
+            total = int(sizes.sum().item()) if n else 0
+            out = torch.empty(max(1, total), dtype=torch.uint8, device=self.device)
+        else:
+            total = out.numel()
+        offs = torch.empty(n + 1, dtype=torch.int64, device=self.device) if with_offsets else None
+        st = status_tensor(self.device)
+        rc = lib().kx_thrift_encode_batch(self.ctx.handle, ds.handle, C.byref(kc), n, _ptr(out), out.numel(),
+                                          _ptr(offs), _ptr(st), _stream_ptr(stream))
+        check(rc, "kx_thrift_encode_batch")
+        s = read_status(st)
+        if s.code:
+            raise ProtocolError(s.code, "thrift marshal")
+        return out[:s.consumed], offs
+
+    def BLength(self, cols: ColumnSet, stream=None):
+        import torch
+        ds = self.dschema
+        kc = to_kx_columns(cols, ds.infos)
+        sizes = torch.empty(max(1, cols.n), dtype=torch.int64, device=self.device)
+        rc = lib().kx_thrift_encoded_size_batch(self.ctx.handle, ds.handle, C.byref(kc), cols.n, _ptr(sizes),
+                                                _stream_ptr(stream))
+        check(rc, "kx_thrift_encoded_size_batch")
+        return sizes[:cols.n]
+
+    def Skip(self, buf, n: int, stream=None):
+        """skipThriftStruct over n concatenated records -> int64[n+1] record offsets."""
+        import torch
+        offs = torch.empty(n + 1, dtype=torch.int64, device=self.device)
+        st = status_tensor(self.device)
+        rc = lib().kx_thrift_skip_batch(self.ctx.handle, _ptr(buf), buf.numel(), n, _ptr(offs), _ptr(st),
+                                        _stream_ptr(stream))
+        check(rc, "kx_thrift_skip_batch")
+        s = read_status(st)
+        if s.code:
+            raise ProtocolError(s.code, "skipThriftStruct", s.record, s.offset)
+        return offs
+
+    # lower-case aliases
+    name, unmarshal, marshal, blength, skip = Name, Unmarshal, Marshal, BLength, Skip
+
+
+def write_message_begin(name: str, msg_type: int, seqid: int) -> bytes:
+    """thrift.Binary.WriteMessageBegin (binary_test.go:387-457) via the C-ABI."""
+    nb = name.encode()
+    buf = (C.c_uint8 * (12 + len(nb)))()
+    w = C.c_uint64()
+    check(lib().kx_thrift_write_message_begin(buf, len(buf), nb, len(nb), msg_type, seqid, C.byref(w)),
+          "WriteMessageBegin")
+    return bytes(buf[:w.value])
+
+
+def read_message_begin(data: bytes):
+    L = lib()
+    arr = (C.c_uint8 * max(1, len(data))).from_buffer_copy(data or b"\0")
+    name, nl, t, s, u = C.c_char_p(), C.c_uint32(), C.c_int32(), C.c_int32(), C.c_uint64()
+    rc = L.kx_thrift_read_message_begin(arr, len(data), C.byref(name), C.byref(nl), C.byref(t), C.byref(s),
+                                        C.byref(u))
+    if rc:
+        raise ProtocolError(rc, "ReadMessageBegin")
+    off = C.cast(name, C.c_void_p).value - C.addressof(arr)
+    return bytes(data[off:off + nl.value]).decode(), t.value, s.value, u.value

@@ -1,0 +1,296 @@
+// kx_capi.cpp — the C-ABI of libkxcodec.so (include/kxcodec.h).
+//
+// Thin, allocation-light host layer: argument checks, per-device upload of the compiled schema,
+// a grow-only workspace per context, and kernel launches on the caller's stream. No torch types,
+// no exceptions cross the boundary.
+#include <string.h>
+
+#include <new>
+
+#include "kx_internal.h"
+
+namespace {
+
+int prog_on_device(kx_schema* s, int dev, KxProgram** out) {
+  if (dev < 0 || dev >= 64) return KX_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> g(s->mu);
+  if (!s->dev_prog[dev]) {
+    void* p = nullptr;
+    KX_HIP_CHECK(hipMalloc(&p, sizeof(KxProgram)));
+    if (hipMemcpy(p, &s->prog, sizeof(KxProgram), hipMemcpyHostToDevice) != hipSuccess) {
+      (void)hipFree(p);
+      return KX_ERR_HIP;
+    }
+    s->dev_prog[dev] = p;
+  }
+  *out = (KxProgram*)s->dev_prog[dev];
+  return KX_OK;
+}
+
+int ensure_ws(kx_ctx* c, size_t bytes, hipStream_t stream) {
+  if (c->ws_size >= bytes) return KX_OK;
+  if (c->ws) {
+    KX_HIP_CHECK(hipStreamSynchronize(stream));  // the old workspace may still be in use
+    KX_HIP_CHECK(hipFree(c->ws));
+    c->ws = nullptr;
+    c->ws_size = 0;
+  }
+  size_t sz = bytes < (1u << 20) ? (1u << 20) : bytes + bytes / 4;
+  KX_HIP_CHECK(hipMalloc(&c->ws, sz));
+  c->ws_size = sz;
+  return KX_OK;
+}
+
+int to_launch_cols(const kx_schema* s, const kx_columns* out, KxLaunchCols* lc) {
+  if (!out) return KX_ERR_INVALID_ARG;
+  if (out->ncols != s->ncols) return KX_ERR_INVALID_ARG;
+  if (s->npres && !out->presence) return KX_ERR_INVALID_ARG;
+  memset(lc, 0, sizeof *lc);
+  for (uint32_t c = 0; c < s->ncols; c++) {
+    const kx_column& k = out->cols[c];
+    if (s->info[c].kind == KX_COL_FIXED) {
+      if (!k.data) return KX_ERR_INVALID_ARG;
+    } else {
+      if (!k.offsets) return KX_ERR_INVALID_ARG;
+      if (!k.data && k.capacity) return KX_ERR_INVALID_ARG;
+    }
+    lc->data[c] = k.data;
+    lc->offs[c] = k.offsets;
+    lc->cap[c] = k.capacity;
+  }
+  lc->presence = out->presence;
+  return KX_OK;
+}
+
+int set_device(kx_ctx* c) {
+  KX_HIP_CHECK(hipSetDevice(c->device));
+  return KX_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int kx_abi_version(void) { return KX_ABI_VERSION; }
+
+const char* kx_strerror(int code) {
+  switch (code) {
+    case KX_OK: return "ok";
+    case KX_ERR_INVALID_DATA: return "invalid data";
+    case KX_ERR_NEGATIVE_SIZE: return "negative size";
+    case KX_ERR_SIZE_LIMIT: return "size limit";
+    case KX_ERR_BAD_VERSION: return "bad version";
+    case KX_ERR_NOT_IMPLEMENTED: return "not implemented";
+    case KX_ERR_DEPTH_LIMIT: return "depth limit exceeded";
+    case KX_ERR_EOF: return "unexpected EOF";
+    case KX_ERR_INVALID_ARG: return "invalid argument";
+    case KX_ERR_HIP: return "HIP runtime error";
+    case KX_ERR_NO_DEVICE: return "no device";
+    case KX_ERR_INTERNAL: return "internal error";
+    default: return "unknown error";
+  }
+}
+
+int kx_schema_create(const kx_struct_desc* structs, uint32_t nstructs, kx_schema** out) {
+  if (!out) return KX_ERR_INVALID_ARG;
+  *out = nullptr;
+  kx_schema* s = new (std::nothrow) kx_schema();
+  if (!s) return KX_ERR_INTERNAL;
+  int rc = kx_build_program(structs, nstructs, s);
+  if (rc) {
+    delete s;
+    return rc;
+  }
+  *out = s;
+  return KX_OK;
+}
+
+void kx_schema_destroy(kx_schema* s) {
+  if (!s) return;
+  for (int d = 0; d < 64; d++)
+    if (s->dev_prog[d]) {
+      (void)hipSetDevice(d);
+      (void)hipFree(s->dev_prog[d]);
+    }
+  delete s;
+}
+
+uint32_t kx_schema_num_columns(const kx_schema* s) { return s ? s->ncols : 0; }
+
+int kx_schema_column_info(const kx_schema* s, uint32_t col, kx_column_info* out) {
+  if (!s || !out || col >= s->ncols) return KX_ERR_INVALID_ARG;
+  *out = s->info[col];
+  return KX_OK;
+}
+
+uint32_t kx_schema_presence_bits(const kx_schema* s) { return s ? s->npres : 0; }
+
+uint64_t kx_schema_min_record_size(const kx_schema* s) { return s ? s->prog.fixed_min : 0; }
+
+int kx_ctx_create(int device, kx_ctx** out) {
+  if (!out) return KX_ERR_INVALID_ARG;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return KX_ERR_NO_DEVICE;
+  if (device < 0 || device >= n) return KX_ERR_INVALID_ARG;
+  kx_ctx* c = new (std::nothrow) kx_ctx();
+  if (!c) return KX_ERR_INTERNAL;
+  c->device = device;
+  *out = c;
+  return KX_OK;
+}
+
+void kx_ctx_destroy(kx_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->ws) (void)hipFree(c->ws);
+  if (c->pin) (void)hipHostFree(c->pin);
+  delete c;
+}
+
+int kx_thrift_decode_batch(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len,
+                           const uint64_t* offsets, uint64_t n, const kx_columns* out,
+                           uint8_t* record_status, kx_status* status, void* stream) {
+  if (!c || !s || !status || (!in && in_len)) return KX_ERR_INVALID_ARG;
+  int rc = set_device(c);
+  if (rc) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  KxLaunchCols lc;
+  if ((rc = to_launch_cols(s, out, &lc))) return rc;
+  if (n == 0) {
+    KX_HIP_CHECK(hipMemsetAsync(status, 0, sizeof(kx_status), st));
+    for (uint32_t k = 0; k < s->ncols; k++)
+      if (lc.offs[k]) KX_HIP_CHECK(hipMemsetAsync(lc.offs[k], 0, 4, st));
+    return KX_OK;
+  }
+  KxProgram* dp = nullptr;
+  if ((rc = prog_on_device(const_cast<kx_schema*>(s), c->device, &dp))) return rc;
+  size_t ws = kx_decode_ws_bytes(s->prog, in_len, offsets, n);
+  if ((rc = ensure_ws(c, ws, st))) return rc;
+  return kx_launch_decode(dp, s->prog, in, in_len, offsets, n, lc, record_status, status, c->ws, c->ws_size,
+                          st, false);
+}
+
+int kx_thrift_skip_batch(kx_ctx* c, const uint8_t* in, uint64_t in_len, uint64_t n, uint64_t* offsets_out,
+                         kx_status* status, void* stream) {
+  if (!c || !status || !offsets_out || (!in && in_len)) return KX_ERR_INVALID_ARG;
+  int rc = set_device(c);
+  if (rc) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  if (n == 0) {
+    KX_HIP_CHECK(hipMemsetAsync(status, 0, sizeof(kx_status), st));
+    KX_HIP_CHECK(hipMemsetAsync(offsets_out, 0, 8, st));
+    return KX_OK;
+  }
+  if ((rc = ensure_ws(c, kx_skip_ws_bytes(in_len), st))) return rc;
+  return kx_launch_skip(in, in_len, n, offsets_out, status, c->ws, c->ws_size, st);
+}
+
+int kx_thrift_encoded_size_batch(kx_ctx* c, const kx_schema* s, const kx_columns* in, uint64_t n,
+                                 uint64_t* sizes_out, void* stream) {
+  if (!c || !s || !sizes_out) return KX_ERR_INVALID_ARG;
+  int rc = set_device(c);
+  if (rc) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  KxLaunchCols lc;
+  if ((rc = to_launch_cols(s, in, &lc))) return rc;
+  if (n == 0) return KX_OK;
+  KxProgram* dp = nullptr;
+  if ((rc = prog_on_device(const_cast<kx_schema*>(s), c->device, &dp))) return rc;
+  if ((rc = ensure_ws(c, kx_encode_ws_bytes(n), st))) return rc;
+  return kx_launch_encode(dp, s->prog, lc, n, nullptr, 0, sizes_out, nullptr, nullptr, c->ws, c->ws_size, st,
+                          true);
+}
+
+int kx_thrift_encode_batch(kx_ctx* c, const kx_schema* s, const kx_columns* in, uint64_t n, uint8_t* out,
+                           uint64_t out_cap, uint64_t* offsets_out, kx_status* status, void* stream) {
+  if (!c || !s || !status || (!out && out_cap)) return KX_ERR_INVALID_ARG;
+  int rc = set_device(c);
+  if (rc) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  KxLaunchCols lc;
+  if ((rc = to_launch_cols(s, in, &lc))) return rc;
+  if (n == 0) {
+    KX_HIP_CHECK(hipMemsetAsync(status, 0, sizeof(kx_status), st));
+    if (offsets_out) KX_HIP_CHECK(hipMemsetAsync(offsets_out, 0, 8, st));
+    return KX_OK;
+  }
+  KxProgram* dp = nullptr;
+  if ((rc = prog_on_device(const_cast<kx_schema*>(s), c->device, &dp))) return rc;
+  if ((rc = ensure_ws(c, kx_encode_ws_bytes(n), st))) return rc;
+  return kx_launch_encode(dp, s->prog, lc, n, out, out_cap, nullptr, offsets_out, status, c->ws, c->ws_size,
+                          st, false);
+}
+
+int kx_pb_decode_batch(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len,
+                       const uint64_t* offsets, uint64_t n, const kx_columns* out, uint8_t* record_status,
+                       kx_status* status, void* stream) {
+  if (!c || !s || !status || (!in && in_len)) return KX_ERR_INVALID_ARG;
+  int rc = set_device(c);
+  if (rc) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  KxLaunchCols lc;
+  if ((rc = to_launch_cols(s, out, &lc))) return rc;
+  for (uint32_t f = 0; f < s->prog.nfields; f++)
+    if (s->prog.f[f].pb_wt == 7 || s->prog.ninst != 1) return KX_ERR_NOT_IMPLEMENTED;
+  if (n == 0) {
+    KX_HIP_CHECK(hipMemsetAsync(status, 0, sizeof(kx_status), st));
+    for (uint32_t k = 0; k < s->ncols; k++)
+      if (lc.offs[k]) KX_HIP_CHECK(hipMemsetAsync(lc.offs[k], 0, 4, st));
+    return KX_OK;
+  }
+  KxProgram* dp = nullptr;
+  if ((rc = prog_on_device(const_cast<kx_schema*>(s), c->device, &dp))) return rc;
+  size_t ws = kx_decode_ws_bytes(s->prog, in_len, offsets, n);
+  if ((rc = ensure_ws(c, ws, st))) return rc;
+  return kx_launch_decode(dp, s->prog, in, in_len, offsets, n, lc, record_status, status, c->ws, c->ws_size,
+                          st, true);
+}
+
+int kx_host_decode_batch(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len,
+                         const uint64_t* offsets, uint64_t n, const kx_columns* out, kx_status* status) {
+  (void)c; (void)s; (void)in; (void)in_len; (void)offsets; (void)n; (void)out; (void)status;
+  return KX_ERR_NOT_IMPLEMENTED;
+}
+
+uint64_t kx_thrift_message_begin_length(uint32_t name_len) { return 12ull + name_len; }
+
+int kx_thrift_write_message_begin(uint8_t* buf, uint64_t cap, const char* name, uint32_t name_len,
+                                  int32_t msg_type, int32_t seqid, uint64_t* written) {
+  if (!buf || (!name && name_len) || !written) return KX_ERR_INVALID_ARG;
+  uint64_t need = 12ull + name_len;
+  if (cap < need) return KX_ERR_SIZE_LIMIT;
+  uint32_t v = 0x80010000u | ((uint32_t)msg_type & 0xffu);
+  uint8_t* p = buf;
+  p[0] = v >> 24; p[1] = v >> 16; p[2] = v >> 8; p[3] = (uint8_t)v;
+  p[4] = name_len >> 24; p[5] = name_len >> 16; p[6] = name_len >> 8; p[7] = (uint8_t)name_len;
+  if (name_len) memcpy(p + 8, name, name_len);
+  uint32_t sq = (uint32_t)seqid;
+  p += 8 + name_len;
+  p[0] = sq >> 24; p[1] = sq >> 16; p[2] = sq >> 8; p[3] = (uint8_t)sq;
+  *written = need;
+  return KX_OK;
+}
+
+int kx_thrift_read_message_begin(const uint8_t* buf, uint64_t len, const char** name, uint32_t* name_len,
+                                 int32_t* msg_type, int32_t* seqid, uint64_t* consumed) {
+  if (!buf || !name || !name_len || !msg_type || !seqid || !consumed) return KX_ERR_INVALID_ARG;
+  auto be = [](const uint8_t* p) {
+    return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+  };
+  if (len < 4) return KX_ERR_EOF;
+  uint32_t v = be(buf);
+  if ((v & 0xffff0000u) != 0x80010000u) return KX_ERR_BAD_VERSION;
+  if (len < 8) return KX_ERR_EOF;
+  int32_t n = (int32_t)be(buf + 4);
+  if (n < 0) return KX_ERR_NEGATIVE_SIZE;
+  if (len < 12ull + (uint64_t)n) return KX_ERR_EOF;
+  *name = (const char*)buf + 8;
+  *name_len = (uint32_t)n;
+  *msg_type = (int32_t)(v & 0xffu);
+  *seqid = (int32_t)be(buf + 8 + n);
+  *consumed = 12ull + (uint64_t)n;
+  return KX_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,349 @@
+// kx_encode.hip — batched BLength + FastWriteNocopy (Thrift binary) on CDNA4 / gfx950.
+//
+// Reference: generated FastWriteNocopy / BLength (tool/internal_pkg/pluginmode/thriftgo/
+// struct_tpl.go:225-391, 948-1061; instance internal/mocks/thrift/k-mock.go:190-277): fields in
+// encoder order (fixed-length first, reorderStructFields patcher.go:503-522), optional fields only
+// when set, a nil struct as STOP, lists as header + elements, STOP last.
+//
+// Pipeline (the reference's size -> write structure mapped onto the GPU):
+//   1. size_kernel: one lane per record computes BLength from the columns (offset diffs, presence);
+//      per 1024-record block totals go to the workspace (sizes_out optional);
+//   2. scan_kernel: one workgroup turns block totals into block bases;
+//   3. write_kernel: each workgroup re-derives its records' sizes, scans them and writes as many
+//      records as fit into an LDS image aligned like the destination (mod 16), then streams the
+//      image to HBM with 16-byte stores. Bytes inside a record are packed into dwords in registers
+//      before they touch LDS.
+#include <hip/hip_runtime.h>
+
+#include "kx_internal.h"
+
+namespace {
+
+constexpr int NT = 256;
+constexpr int RB = 1024;             // records per block
+constexpr int OUTB = 48 * 1024;      // LDS image bytes per round
+
+struct EncParams {
+  const KxProgram* prog;
+  KxLaunchCols cols;
+  uint64_t n;
+  uint8_t* out;
+  uint64_t out_cap;
+  uint64_t* sizes_out;
+  uint64_t* offsets_out;
+  kx_status* status;
+  uint64_t* block_tot;   // workspace: per-block total size, then (after scan) block base
+  uint64_t nblocks;
+};
+
+__device__ __forceinline__ uint64_t var_len(const KxLaunchCols& C, int col, uint64_t r) {
+  return (uint64_t)C.offs[col][r + 1] - (uint64_t)C.offs[col][r];
+}
+
+// BLength (struct_tpl.go:266-391)
+__device__ uint64_t record_size(const KxProgram& P, const KxLaunchCols& C, uint64_t r) {
+  uint64_t pres = C.presence ? C.presence[r] : 0;
+  int inst = 0;
+  int f = P.inst[0].enc_first;
+  uint64_t sz = 0;
+  for (;;) {
+    if (f < 0) {
+      sz += 1;                                   // STOP
+      if (inst == 0) break;
+      f = P.inst[inst].ret_pred;
+      inst = P.inst[inst].parent;
+      continue;
+    }
+    const KxpField F = P.f[f];
+    if (F.req == KX_REQ_OPTIONAL && !((pres >> F.pbit) & 1)) { f = F.enc_next; continue; }
+    sz += 3;
+    if (F.kind == KXP_K_FIXED) sz += F.width;
+    else if (F.kind == KXP_K_BYTES) sz += 4 + var_len(C, F.col, r);
+    else if (F.kind == KXP_K_LIST) sz += 5 + var_len(C, F.col, r) * F.width;
+    else {
+      if ((pres >> F.pbit) & 1) { inst = F.child; f = P.inst[inst].enc_first; continue; }
+      sz += 1;                                   // nil *T -> STOP only (k-mock.go:190-199)
+    }
+    f = F.enc_next;
+  }
+  return sz;
+}
+
+// ---- byte sink: packs bytes into dwords before writing LDS (or global on the direct path) ----
+struct Sink {
+  uint8_t* base;   // LDS image or global output
+  uint64_t off;    // position of the first pending byte
+  uint64_t acc;    // pending bytes, first byte in bits 0..7
+  uint32_t n;      // number of pending bytes (< 8)
+
+  __device__ __forceinline__ void drain() {
+    while (n) {
+      if (off & 3) {
+        base[off] = (uint8_t)acc;
+        acc >>= 8; off += 1; n -= 1;
+      } else if (n >= 4) {
+        *(uint32_t*)(base + off) = (uint32_t)acc;
+        acc >>= 32; off += 4; n -= 4;
+      } else {
+        break;
+      }
+    }
+  }
+  // append k (1..4) bytes, first byte in bits 0..7 of v
+  __device__ __forceinline__ void put(uint32_t v, uint32_t k) {
+    acc |= (uint64_t)(k == 4 ? v : (v & ((1u << (8 * k)) - 1))) << (8 * n);
+    n += k;
+    drain();
+  }
+  __device__ __forceinline__ void flush() {
+    while (n) { base[off] = (uint8_t)acc; acc >>= 8; off += 1; n -= 1; }
+  }
+};
+
+__device__ __forceinline__ void put_be(Sink& s, uint64_t v, uint32_t w) {
+  switch (w) {
+    case 1: s.put((uint32_t)v, 1); break;
+    case 2: s.put(((uint32_t)v >> 8 & 0xff) | (((uint32_t)v & 0xff) << 8), 2); break;
+    case 4: s.put(__builtin_bswap32((uint32_t)v), 4); break;
+    default: {
+      s.put(__builtin_bswap32((uint32_t)(v >> 32)), 4);
+      s.put(__builtin_bswap32((uint32_t)v), 4);
+    }
+  }
+}
+
+__device__ __forceinline__ uint64_t load_fixed(const void* base, uint32_t w, uint64_t i) {
+  switch (w) {
+    case 1: return ((const uint8_t*)base)[i];
+    case 2: return ((const uint16_t*)base)[i];
+    case 4: return ((const uint32_t*)base)[i];
+    default: return ((const uint64_t*)base)[i];
+  }
+}
+
+// FastWriteNocopy for one record into the sink
+__device__ void write_record(const KxProgram& P, const KxLaunchCols& C, uint64_t r, Sink& s) {
+  uint64_t pres = C.presence ? C.presence[r] : 0;
+  int inst = 0;
+  int f = P.inst[0].enc_first;
+  for (;;) {
+    if (f < 0) {
+      s.put(KX_T_STOP, 1);
+      if (inst == 0) break;
+      f = P.inst[inst].ret_pred;
+      inst = P.inst[inst].parent;
+      continue;
+    }
+    const KxpField F = P.f[f];
+    if (F.req == KX_REQ_OPTIONAL && !((pres >> F.pbit) & 1)) { f = F.enc_next; continue; }
+    // WriteFieldBegin: type, id (big-endian)
+    uint32_t id = (uint16_t)F.id;
+    s.put((uint32_t)F.ttype | ((id >> 8) << 8) | ((id & 0xff) << 16), 3);
+    if (F.kind == KXP_K_FIXED) {
+      uint64_t v = load_fixed(C.data[F.col], F.width, r);
+      if (F.ttype == KX_T_BOOL) v = (v & 0xff) ? 1 : 0;
+      put_be(s, v, F.width);
+    } else if (F.kind == KXP_K_BYTES) {
+      uint64_t o = C.offs[F.col][r];
+      uint32_t len = (uint32_t)var_len(C, F.col, r);
+      put_be(s, len, 4);
+      const uint8_t* src = (const uint8_t*)C.data[F.col] + o;
+      const uint64_t sa = (uint64_t)src, se = sa + len;
+      uint32_t i = 0;
+      for (; i + 4 <= len; i += 4) {
+        // unaligned 4-byte read of the source string: aligned dwords that hold string bytes only
+        uint64_t A = (sa + i) & ~3ull;
+        uint32_t sh = (uint32_t)((sa + i) & 3);
+        uint32_t x0 = *(const uint32_t*)A;
+        uint32_t x1 = (sh && A + 4 < se) ? *(const uint32_t*)(A + 4) : 0u;
+        s.put(sh ? __builtin_amdgcn_alignbyte(x1, x0, sh) : x0, 4);
+      }
+      for (; i < len; i++) s.put(src[i], 1);
+    } else if (F.kind == KXP_K_LIST) {
+      uint64_t o = C.offs[F.col][r];
+      uint32_t cnt = (uint32_t)var_len(C, F.col, r);
+      s.put(F.elem, 1);
+      put_be(s, cnt, 4);
+      const void* src = C.data[F.col];
+      for (uint32_t i = 0; i < cnt; i++) {
+        uint64_t v = load_fixed(src, F.width, o + i);
+        if (F.elem == KX_T_BOOL) v = (v & 0xff) ? 1 : 0;
+        put_be(s, v, F.width);
+      }
+    } else {
+      if ((pres >> F.pbit) & 1) { inst = F.child; f = P.inst[inst].enc_first; continue; }
+      s.put(KX_T_STOP, 1);
+    }
+    f = F.enc_next;
+  }
+  s.flush();
+}
+
+__device__ __forceinline__ uint64_t wave_incl_scan(uint64_t v, int lane) {
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    uint64_t o = __shfl_up(v, d, 64);
+    if (lane >= d) v += o;
+  }
+  return v;
+}
+
+__device__ uint64_t block_excl_scan(uint64_t v, uint64_t* tot, uint64_t* scratch) {
+  int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint64_t inc = wave_incl_scan(v, lane);
+  __syncthreads();
+  if (lane == 63) scratch[wv] = inc;
+  __syncthreads();
+  uint64_t base = 0, t = 0;
+  for (int i = 0; i < (int)(blockDim.x >> 6); i++) {
+    uint64_t s = scratch[i];
+    if (i < wv) base += s;
+    t += s;
+  }
+  *tot = t;
+  return base + inc - v;
+}
+
+__global__ void __launch_bounds__(NT) size_kernel(EncParams ep) {
+  __shared__ uint64_t scratch[NT / 64];
+  __shared__ uint32_t progw[sizeof(KxProgram) / 4];
+  for (int i = threadIdx.x; i < (int)(sizeof(KxProgram) / 4); i += NT) progw[i] = ((const uint32_t*)ep.prog)[i];
+  __syncthreads();
+  const KxProgram& P = *reinterpret_cast<const KxProgram*>(progw);
+  uint64_t b = blockIdx.x;
+  uint64_t acc = 0;
+  for (int k = 0; k < RB / NT; k++) {
+    uint64_t r = b * RB + k * NT + threadIdx.x;
+    uint64_t sz = 0;
+    if (r < ep.n) {
+      sz = record_size(P, ep.cols, r);
+      if (ep.sizes_out) ep.sizes_out[r] = sz;
+    }
+    acc += sz;
+  }
+  uint64_t tot;
+  block_excl_scan(acc, &tot, scratch);
+  if (threadIdx.x == 0 && ep.block_tot) ep.block_tot[b] = tot;
+}
+
+__global__ void __launch_bounds__(1024) scan_kernel(EncParams ep) {
+  __shared__ uint64_t scratch[16];
+  uint64_t nb = ep.nblocks;
+  uint64_t per = (nb + 1023) / 1024;
+  uint64_t lo = threadIdx.x * per, hi = min(lo + per, nb);
+  uint64_t s = 0;
+  for (uint64_t i = lo; i < hi; i++) s += ep.block_tot[i];
+  uint64_t tot;
+  uint64_t run = block_excl_scan(s, &tot, scratch);
+  for (uint64_t i = lo; i < hi; i++) {
+    uint64_t v = ep.block_tot[i];
+    ep.block_tot[i] = run;
+    run += v;
+  }
+  if (threadIdx.x == 0) {
+    kx_status* st = ep.status;
+    st->n_records = ep.n;
+    st->consumed = tot;
+    st->code = tot > ep.out_cap ? KX_ERR_SIZE_LIMIT : 0;
+    if (ep.offsets_out && tot <= ep.out_cap) ep.offsets_out[ep.n] = tot;
+  }
+}
+
+__global__ void __launch_bounds__(NT) write_kernel(EncParams ep) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  uint8_t* img = (uint8_t*)smem_raw;                        // OUTB + 32
+  uint32_t* progw = (uint32_t*)(smem_raw + OUTB + 32);
+  uint64_t* scratch = (uint64_t*)(smem_raw + OUTB + 32 + sizeof(KxProgram));
+  __shared__ uint64_t s_take, s_round_bytes;
+  if (ep.status->code != 0) return;                         // size limit: write nothing
+  for (int i = threadIdx.x; i < (int)(sizeof(KxProgram) / 4); i += NT) progw[i] = ((const uint32_t*)ep.prog)[i];
+  __syncthreads();
+  const KxProgram& P = *reinterpret_cast<const KxProgram*>(progw);
+  const uint64_t b = blockIdx.x;
+  uint64_t r = b * RB;
+  const uint64_t rend = min(r + RB, ep.n);
+  uint64_t gpos = ep.block_tot[b];
+  while (r < rend) {
+    uint64_t my = r + threadIdx.x;
+    uint64_t sz = my < rend ? record_size(P, ep.cols, my) : 0;
+    uint64_t tot;
+    uint64_t pre = block_excl_scan(sz, &tot, scratch);
+    const uint32_t skew = (uint32_t)(((uint64_t)ep.out + gpos) & 15);
+    // records that fit entirely into this round's image (at least one)
+    bool fits = my < rend && skew + pre + sz <= OUTB;
+    if (threadIdx.x == 0) { s_take = 0; s_round_bytes = 0; }
+    __syncthreads();
+    if (fits) {
+      atomicMax((unsigned long long*)&s_take, (unsigned long long)(threadIdx.x + 1));
+      atomicMax((unsigned long long*)&s_round_bytes, (unsigned long long)(pre + sz));
+    }
+    __syncthreads();
+    uint64_t take = s_take;
+    if (take == 0) {
+      // a single record larger than the image: thread 0 writes it straight to HBM
+      if (threadIdx.x == 0) {
+        Sink s{ep.out, gpos, 0, 0};
+        write_record(P, ep.cols, r, s);
+        if (ep.offsets_out) ep.offsets_out[r] = gpos;
+        s_round_bytes = sz;
+      }
+      __syncthreads();
+      gpos += s_round_bytes;
+      r += 1;
+      __syncthreads();
+      continue;
+    }
+    if (threadIdx.x < take) {
+      Sink s{img, skew + pre, 0, 0};
+      write_record(P, ep.cols, my, s);
+      if (ep.offsets_out) ep.offsets_out[my] = gpos + pre;
+    }
+    __syncthreads();
+    // stream the image [skew, skew + bytes) to out[gpos ...): the image is congruent mod 16
+    const uint64_t bytes = s_round_bytes;
+    const uint64_t gstart = (uint64_t)ep.out + gpos;
+    const uint64_t a0 = gstart & ~15ull;                     // image byte 0 <-> a0
+    const uint64_t gend = gstart + bytes;
+    const uint64_t nch = (gend - a0 + 15) >> 4;
+    for (uint64_t c = threadIdx.x; c < nch; c += NT) {
+      uint64_t ca = a0 + c * 16;
+      if (ca >= gstart && ca + 16 <= gend) {
+        *(uint4*)ca = *(const uint4*)(img + c * 16);
+      } else {
+        for (int k = 0; k < 16; k++) {
+          uint64_t x = ca + k;
+          if (x >= gstart && x < gend) *(uint8_t*)x = img[c * 16 + k];
+        }
+      }
+    }
+    __syncthreads();
+    gpos += bytes;
+    r += take;
+  }
+}
+
+}  // namespace
+
+size_t kx_encode_ws_bytes(uint64_t n) { return ((n + RB - 1) / RB) * 8 + 256; }
+
+int kx_launch_encode(const KxProgram* dprog, const KxProgram& hprog, const KxLaunchCols& cols, uint64_t n,
+                     uint8_t* out, uint64_t out_cap, uint64_t* sizes_out, uint64_t* offsets_out,
+                     kx_status* status, void* ws, size_t ws_size, hipStream_t stream, bool sizes_only) {
+  (void)hprog;
+  EncParams ep{};
+  ep.prog = dprog; ep.cols = cols; ep.n = n; ep.out = out; ep.out_cap = out_cap;
+  ep.sizes_out = sizes_out; ep.offsets_out = offsets_out; ep.status = status;
+  ep.nblocks = (n + RB - 1) / RB;
+  if (ws_size < kx_encode_ws_bytes(n)) return KX_ERR_INVALID_ARG;
+  ep.block_tot = (uint64_t*)ws;
+  if (status) KX_HIP_CHECK(hipMemsetAsync(status, 0, sizeof(kx_status), stream));
+  hipLaunchKernelGGL(size_kernel, dim3((unsigned)ep.nblocks), dim3(NT), 0, stream, ep);
+  KX_HIP_CHECK(hipGetLastError());
+  if (sizes_only) return KX_OK;
+  hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, stream, ep);
+  KX_HIP_CHECK(hipGetLastError());
+  size_t shmem = OUTB + 32 + sizeof(KxProgram) + 8 * (NT / 64);
+  hipLaunchKernelGGL(write_kernel, dim3((unsigned)ep.nblocks), dim3(NT), shmem, stream, ep);
+  KX_HIP_CHECK(hipGetLastError());
+  return KX_OK;
+}

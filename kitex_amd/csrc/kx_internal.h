@@ -1,0 +1,65 @@
+// kx_internal.h — host-side internals shared by the C-ABI translation units.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <mutex>
+#include <vector>
+
+#include "../../include/kxcodec.h"
+#include "kx_program.h"
+
+struct kx_schema {
+  KxProgram prog;                      // host copy of the compiled schema
+  kx_column_info info[KX_MAX_COLUMNS];
+  uint32_t ncols = 0;
+  uint32_t npres = 0;
+  std::vector<kx_field_desc> fields;   // owned copy of the IDL
+  std::vector<uint32_t> struct_first, struct_n;
+  // device copies, one per device, uploaded lazily by a ctx
+  std::mutex mu;
+  void* dev_prog[64] = {nullptr};
+};
+
+struct kx_ctx {
+  int device = 0;
+  hipStream_t own_stream = nullptr;
+  // grow-only device workspace (tile descriptors + flags + counters)
+  void* ws = nullptr;
+  size_t ws_size = 0;
+  // pinned staging for kx_host_*
+  void* pin = nullptr;
+  size_t pin_size = 0;
+};
+
+// kx_schema.cpp
+int kx_build_program(const kx_struct_desc* structs, uint32_t nstructs, kx_schema* s);
+
+// device launchers (kx_decode.hip / kx_encode.hip)
+struct KxLaunchCols {
+  void* data[KX_MAX_COLUMNS];
+  uint32_t* offs[KX_MAX_COLUMNS];
+  uint64_t cap[KX_MAX_COLUMNS];
+  uint64_t* presence;
+};
+
+int kx_launch_decode(const KxProgram* dprog, const KxProgram& hprog, const uint8_t* in,
+                     uint64_t in_len, const uint64_t* offsets, uint64_t n,
+                     const KxLaunchCols& cols, uint8_t* record_status, kx_status* status,
+                     void* ws, size_t ws_size, hipStream_t stream, bool pb);
+size_t kx_decode_ws_bytes(const KxProgram& hprog, uint64_t in_len, const uint64_t* offsets, uint64_t n);
+
+int kx_launch_skip(const uint8_t* in, uint64_t in_len, uint64_t n, uint64_t* offsets_out,
+                   kx_status* status, void* ws, size_t ws_size, hipStream_t stream);
+size_t kx_skip_ws_bytes(uint64_t in_len);
+
+int kx_launch_encode(const KxProgram* dprog, const KxProgram& hprog, const KxLaunchCols& cols,
+                     uint64_t n, uint8_t* out, uint64_t out_cap, uint64_t* sizes_out,
+                     uint64_t* offsets_out, kx_status* status, void* ws, size_t ws_size,
+                     hipStream_t stream, bool sizes_only);
+size_t kx_encode_ws_bytes(uint64_t n);
+
+#define KX_HIP_CHECK(x)                       \
+  do {                                        \
+    hipError_t e_ = (x);                      \
+    if (e_ != hipSuccess) return KX_ERR_HIP;  \
+  } while (0)

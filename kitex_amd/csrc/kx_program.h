@@ -1,0 +1,83 @@
+// kx_program.h — the compiled schema ("program") the device kernels interpret.
+//
+// kx_schema_create flattens the IDL (include/kxcodec.h kx_struct_desc[]) into this fixed-size,
+// position-independent table. It is copied to HBM once per (schema, device) and staged into LDS by
+// every workgroup (≈2.5 KB), where the per-lane record parser reads it with ds_read.
+//
+// Flattening rules (identical to the CPU oracle's):
+//  * depth-first over the IDL, struct fields inlined; every struct occurrence is an "instance" with a
+//    unique set of leaf columns (non-recursive schemas only, depth < 8);
+//  * every optional / struct / container field gets a presence bit (Go nil-ability);
+//  * "flat field" index = position of a field in the instance-ordered field table (<= 64 in total),
+//    so a single 64-bit mask holds the isset state of a whole record (required-field check,
+//    struct_tpl.go:124-145).
+#pragma once
+#include <stdint.h>
+
+#define KXP_MAX_FIELDS 64
+#define KXP_MAX_INST 16
+#define KXP_MAX_COLS 32
+#define KXP_NV_MAX 8  // var (BYTES / LIST) columns per schema handled by the device kernels
+
+enum : uint8_t { KXP_K_FIXED = 1, KXP_K_BYTES = 2, KXP_K_LIST = 3, KXP_K_STRUCT = 4 };
+
+struct KxpField {      // 16 B
+  int16_t id;
+  uint8_t ttype;       // wire type (thrift TType)
+  uint8_t elem;        // LIST/SET element type
+  int8_t col;          // leaf column, -1 for STRUCT
+  int8_t child;        // STRUCT: child instance
+  int8_t pbit;         // presence bit or -1
+  int8_t enc_next;     // next flat field in this instance's encoder order, -1 at the end
+  uint8_t kind;        // KXP_K_*
+  uint8_t width;       // FIXED: value width; LIST: element width
+  uint8_t vslot;       // var slot (BYTES/LIST), 0xff otherwise
+  uint8_t inst;        // owning instance
+  uint8_t req;         // KX_REQ_*
+  uint8_t flags;       // bit0: protobuf bytes (no UTF-8 check)
+  uint8_t pb_wt;       // protobuf wire type for this field
+  uint8_t pad;
+};
+
+struct KxpInst {       // 32 B
+  uint64_t req_mask;      // required flat fields of this instance
+  uint64_t subtree_mask;  // flat fields of this instance and all descendants
+  uint64_t pres_mask;     // presence bits of fields strictly inside this instance's subtree
+  int8_t first;           // first flat field
+  int8_t nfields;
+  int8_t enc_first;       // first flat field in encoder order (-1 if no fields)
+  int8_t parent;          // parent instance, -1 for the root
+  int8_t ret_pred;        // predictor to resume with in the parent after this struct's STOP
+  int8_t self_field;      // flat field (in the parent) holding this instance
+  uint8_t vslot_mask;     // var slots inside this instance's subtree
+  int8_t pad;
+};
+
+struct KxpCol {        // 16 B
+  uint8_t kind;        // KXP_K_FIXED / BYTES / LIST
+  uint8_t width;
+  uint8_t elem;        // LIST element type (BOOL needs normalisation)
+  uint8_t vslot;       // 0xff for FIXED
+  int8_t field;        // flat field
+  uint8_t ttype;
+  uint8_t pad[2];
+  int64_t defv;        // FIXED default (bits)
+};
+
+struct KxProgram {
+  KxpField f[KXP_MAX_FIELDS];
+  KxpInst inst[KXP_MAX_INST];
+  KxpCol col[KXP_MAX_COLS];
+  uint32_t nfields, ninst, ncols, nvar;
+  uint32_t npres;
+  uint32_t sig;          // first 3 wire bytes of a canonically encoded record (little-endian packed)
+  uint32_t sig_len;      // 3, or 1 when the root encodes no fields before STOP
+  uint32_t is_pb;
+  uint8_t var_col[KXP_NV_MAX];  // var slot -> column
+  uint64_t fixed_min;    // minimum encoded record size (optional unset, var empty)
+  uint64_t pad[3];
+};
+
+static_assert(sizeof(KxpField) == 16, "KxpField layout");
+static_assert(sizeof(KxpInst) == 32, "KxpInst layout");
+static_assert(sizeof(KxpCol) == 16, "KxpCol layout");

@@ -1,0 +1,259 @@
+// kx_schema.cpp — flatten an IDL (kx_struct_desc[]) into a KxProgram (see kx_program.h).
+//
+// Semantics follow the generated FastCodec: fields are matched by id and wire type
+// (struct_tpl.go:75-101), fixed-length fields are written before the others in IDL order
+// (reorderStructFields, tool/internal_pkg/pluginmode/thriftgo/patcher.go:503-522).
+#include <string.h>
+
+#include "kx_internal.h"
+
+namespace {
+
+int type_size(uint8_t t) {
+  switch (t) {
+    case KX_T_BOOL: case KX_T_BYTE: return 1;
+    case KX_T_I16: return 2;
+    case KX_T_I32: return 4;
+    case KX_T_I64: case KX_T_DOUBLE: return 8;
+    default: return 0;
+  }
+}
+
+int pb_wire_type(uint8_t t) {
+  switch (t) {
+    case KX_T_BOOL: case KX_T_BYTE: case KX_T_I16: case KX_T_I32: case KX_T_I64: return 0;
+    case KX_T_DOUBLE: return 1;
+    case KX_T_STRING: return 2;
+    default: return 7;  // unsupported in the protobuf path
+  }
+}
+
+struct PendField {
+  const kx_field_desc* d;
+  int col;    // leaf column or -1
+  int child;  // child instance or -1
+  int pbit;
+};
+
+struct Builder {
+  const kx_struct_desc* structs;
+  uint32_t nstructs;
+  kx_schema* s;
+  std::vector<std::vector<PendField>> inst_fields;
+  std::vector<int> inst_parent, inst_self;  // self: index into parent's field list
+  int stack[8];
+
+  int rec(int sidx, int depth, int parent, int self_idx, int16_t* path, int* out) {
+    if (sidx < 0 || (uint32_t)sidx >= nstructs) return KX_ERR_INVALID_ARG;
+    if (depth >= 8) return KX_ERR_NOT_IMPLEMENTED;
+    for (int i = 0; i < depth; i++)
+      if (stack[i] == sidx) return KX_ERR_NOT_IMPLEMENTED;  // recursive type: no flat columns
+    if ((int)inst_fields.size() >= KXP_MAX_INST) return KX_ERR_NOT_IMPLEMENTED;
+    const kx_struct_desc& sd = structs[sidx];
+    if (sd.nfields && !sd.fields) return KX_ERR_INVALID_ARG;
+    int me = (int)inst_fields.size();
+    inst_fields.emplace_back();
+    inst_parent.push_back(parent);
+    inst_self.push_back(self_idx);
+    stack[depth] = sidx;
+    for (uint32_t i = 0; i < sd.nfields; i++) {
+      const kx_field_desc* f = &sd.fields[i];
+      for (uint32_t j = 0; j < i; j++)
+        if (sd.fields[j].id == f->id) return KX_ERR_INVALID_ARG;
+      if (f->req > KX_REQ_OPTIONAL) return KX_ERR_INVALID_ARG;
+      PendField pf{f, -1, -1, -1};
+      bool container = f->ttype == KX_T_STRUCT || f->ttype == KX_T_LIST || f->ttype == KX_T_SET ||
+                       f->ttype == KX_T_MAP;
+      if (f->req == KX_REQ_OPTIONAL || container) {
+        if (s->npres >= 64) return KX_ERR_NOT_IMPLEMENTED;
+        pf.pbit = (int)s->npres++;
+      }
+      path[depth] = f->id;
+      kx_column_info ci;
+      memset(&ci, 0, sizeof ci);
+      ci.ttype = f->ttype;
+      ci.field_id = f->id;
+      ci.presence_bit = pf.pbit;
+      ci.depth = (uint32_t)depth;
+      for (int d = 0; d <= depth; d++) ci.path[d] = path[d];
+      switch (f->ttype) {
+        case KX_T_BOOL: case KX_T_BYTE: case KX_T_I16: case KX_T_I32: case KX_T_I64: case KX_T_DOUBLE:
+          ci.kind = KX_COL_FIXED;
+          ci.width = (uint32_t)type_size(f->ttype);
+          break;
+        case KX_T_STRING:
+          ci.kind = KX_COL_BYTES;
+          ci.width = 1;
+          break;
+        case KX_T_LIST: case KX_T_SET:
+          if (type_size(f->elem_ttype) == 0) return KX_ERR_NOT_IMPLEMENTED;  // list<string|struct>
+          ci.kind = KX_COL_LIST;
+          ci.width = (uint32_t)type_size(f->elem_ttype);
+          ci.elem_ttype = f->elem_ttype;
+          break;
+        case KX_T_STRUCT: {
+          int child = -1;
+          // the child instance is created before this field is appended: remember the slot
+          int slot = (int)inst_fields[me].size();
+          inst_fields[me].push_back(pf);
+          int rc = rec(f->child, depth + 1, me, slot, path, &child);
+          if (rc) return rc;
+          inst_fields[me][slot].child = child;
+          continue;
+        }
+        case KX_T_MAP:
+          return KX_ERR_NOT_IMPLEMENTED;
+        default:
+          return KX_ERR_INVALID_ARG;
+      }
+      if (s->ncols >= KX_MAX_COLUMNS) return KX_ERR_NOT_IMPLEMENTED;
+      pf.col = (int)s->ncols;
+      s->info[s->ncols++] = ci;
+      inst_fields[me].push_back(pf);
+    }
+    *out = me;
+    return KX_OK;
+  }
+};
+
+}  // namespace
+
+int kx_build_program(const kx_struct_desc* structs, uint32_t nstructs, kx_schema* s) {
+  if (!structs || nstructs == 0 || nstructs > KX_MAX_STRUCTS) return KX_ERR_INVALID_ARG;
+  memset(&s->prog, 0, sizeof s->prog);
+  s->ncols = 0;
+  s->npres = 0;
+  Builder b{structs, nstructs, s, {}, {}, {}, {}};
+  int16_t path[8];
+  int root = -1;
+  int rc = b.rec(0, 0, -1, -1, path, &root);
+  if (rc) return rc;
+
+  KxProgram& P = s->prog;
+  P.ninst = (uint32_t)b.inst_fields.size();
+  // flat field indices: instances in creation order, fields contiguous per instance
+  std::vector<int> first(P.ninst);
+  int nf = 0;
+  for (uint32_t i = 0; i < P.ninst; i++) {
+    first[i] = nf;
+    nf += (int)b.inst_fields[i].size();
+  }
+  if (nf > KXP_MAX_FIELDS) return KX_ERR_NOT_IMPLEMENTED;
+  P.nfields = (uint32_t)nf;
+  P.ncols = s->ncols;
+  P.npres = s->npres;
+
+  // var slots in column order
+  int nvar = 0;
+  for (uint32_t c = 0; c < s->ncols; c++) {
+    KxpCol& kc = P.col[c];
+    const kx_column_info& ci = s->info[c];
+    kc.kind = ci.kind == KX_COL_FIXED ? KXP_K_FIXED : ci.kind == KX_COL_BYTES ? KXP_K_BYTES : KXP_K_LIST;
+    kc.width = (uint8_t)ci.width;
+    kc.elem = ci.elem_ttype;
+    kc.ttype = ci.ttype;
+    kc.vslot = 0xff;
+    if (ci.kind != KX_COL_FIXED) {
+      if (nvar >= KXP_NV_MAX) return KX_ERR_NOT_IMPLEMENTED;
+      kc.vslot = (uint8_t)nvar;
+      P.var_col[nvar++] = (uint8_t)c;
+    }
+  }
+  P.nvar = (uint32_t)nvar;
+
+  for (uint32_t i = 0; i < P.ninst; i++) {
+    KxpInst& I = P.inst[i];
+    const auto& fl = b.inst_fields[i];
+    I.first = (int8_t)first[i];
+    I.nfields = (int8_t)fl.size();
+    I.parent = (int8_t)b.inst_parent[i];
+    I.self_field = b.inst_parent[i] >= 0 ? (int8_t)(first[b.inst_parent[i]] + b.inst_self[i]) : -1;
+    // encoder order: fixed-length first, then the rest, IDL order inside each group
+    std::vector<int> order;
+    for (int pass = 0; pass < 2; pass++)
+      for (int k = 0; k < (int)fl.size(); k++)
+        if ((type_size(fl[k].d->ttype) > 0) == (pass == 0)) order.push_back(k);
+    I.enc_first = order.empty() ? -1 : (int8_t)(first[i] + order[0]);
+    for (int k = 0; k < (int)fl.size(); k++) {
+      int ff = first[i] + k;
+      KxpField& F = P.f[ff];
+      const kx_field_desc* d = fl[k].d;
+      F.id = d->id;
+      F.ttype = d->ttype;
+      F.elem = d->elem_ttype;
+      F.col = (int8_t)fl[k].col;
+      F.child = (int8_t)fl[k].child;
+      F.pbit = (int8_t)fl[k].pbit;
+      F.inst = (uint8_t)i;
+      F.req = d->req;
+      F.flags = d->reserved0;
+      F.pb_wt = (uint8_t)pb_wire_type(d->ttype);
+      F.enc_next = -1;
+      if (fl[k].col >= 0) {
+        const KxpCol& kc = P.col[fl[k].col];
+        F.kind = kc.kind;
+        F.width = kc.width;
+        F.vslot = kc.vslot;
+        P.col[fl[k].col].field = (int8_t)ff;
+        P.col[fl[k].col].defv = d->default_bits;
+      } else {
+        F.kind = KXP_K_STRUCT;
+        F.width = 0;
+        F.vslot = 0xff;
+      }
+      if (d->req == KX_REQ_REQUIRED) I.req_mask |= 1ull << ff;
+    }
+    for (size_t o = 0; o + 1 < order.size(); o++)
+      P.f[first[i] + order[o]].enc_next = (int8_t)(first[i] + order[o + 1]);
+  }
+  // subtree masks (children are created after parents: walk in reverse creation order)
+  for (int i = (int)P.ninst - 1; i >= 0; i--) {
+    KxpInst& I = P.inst[i];
+    uint64_t m = 0, pm = 0;
+    uint8_t vm = 0;
+    for (int k = 0; k < I.nfields; k++) {
+      const KxpField& F = P.f[I.first + k];
+      m |= 1ull << (I.first + k);
+      if (F.pbit >= 0) pm |= 1ull << F.pbit;
+      if (F.vslot != 0xff) vm |= (uint8_t)(1u << F.vslot);
+      if (F.child >= 0) {
+        m |= P.inst[F.child].subtree_mask;
+        pm |= P.inst[F.child].pres_mask;
+        vm |= P.inst[F.child].vslot_mask;
+      }
+    }
+    I.subtree_mask = m;
+    I.pres_mask = pm;
+    I.vslot_mask = vm;
+  }
+  for (uint32_t i = 1; i < P.ninst; i++) {
+    KxpInst& I = P.inst[i];
+    I.ret_pred = P.f[I.self_field].enc_next;
+  }
+  P.inst[0].ret_pred = -1;
+
+  // canonical first bytes of a record (speculative boundary signature)
+  const KxpInst& R = P.inst[0];
+  if (R.enc_first >= 0) {
+    const KxpField& F = P.f[R.enc_first];
+    P.sig = (uint32_t)F.ttype | ((uint32_t)((uint16_t)F.id >> 8) << 8) | ((uint32_t)(F.id & 0xff) << 16);
+    P.sig_len = 3;
+  } else {
+    P.sig = 0;
+    P.sig_len = 1;
+  }
+  // minimum encoded size: non-optional fields with empty var data, nil structs = STOP
+  uint64_t mn = 1;
+  for (int k = 0; k < R.nfields; k++) {
+    const KxpField& F = P.f[R.first + k];
+    if (F.req == KX_REQ_OPTIONAL) continue;
+    mn += 3;
+    if (F.kind == KXP_K_FIXED) mn += F.width;
+    else if (F.kind == KXP_K_BYTES) mn += 4;
+    else if (F.kind == KXP_K_LIST) mn += 5;
+    else mn += 1;
+  }
+  P.fixed_min = mn;
+  s->ncols = P.ncols;
+  return KX_OK;
+}

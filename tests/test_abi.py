@@ -1,0 +1,91 @@
+"""CPU-side checks of the drop-in boundary: libkxcodec.so loads, exports exactly the symbols
+include/kxcodec.h declares, and its host-only entry points agree with the oracle."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import pytest
+
+from kitex_amd import _abi as A
+from kitex_amd import schema as S
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "kxcodec.h")
+
+
+def declared_symbols():
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(kx_[a-z0-9_]+)\s*\(", txt)))
+
+
+@pytest.fixture(scope="module")
+def kxlib():
+    from kitex_amd import build
+    build.build()
+    from kitex_amd import _lib
+    return _lib.lib()
+
+
+def test_header_symbols_exported(kxlib):
+    syms = declared_symbols()
+    assert len(syms) >= 19
+    out = subprocess.run(["nm", "-D", "--defined-only", os.path.join(ROOT, "kitex_amd", "lib", "libkxcodec.so")],
+                         capture_output=True, text=True, check=True).stdout
+    exported = set(l.split()[-1] for l in out.splitlines() if " T " in l)
+    missing = [s for s in syms if s not in exported]
+    assert not missing, missing
+    from kitex_amd._lib import EXPORTS
+    assert sorted(EXPORTS) == syms
+
+
+def test_abi_version_and_strerror(kxlib):
+    assert kxlib.kx_abi_version() == A.KX_ABI_VERSION
+    assert kxlib.kx_strerror(A.ERR_EOF) == b"unexpected EOF"
+
+
+@pytest.mark.parametrize("name", ["r1", "r2", "r3", "pf"])
+def test_schema_columns_match_oracle(kxlib, oracle, name):
+    from kitex_amd.codec import DeviceSchema
+    sch = S.SCHEMAS[name]()
+    ds = DeviceSchema(sch)
+    rc, infos, npres = oracle.flatten(sch)
+    assert rc == 0 and ds.ncols == len(infos) and ds.npresence == npres
+    for a, b in zip(ds.infos, infos):
+        assert bytes(a) == bytes(b)
+
+
+def test_schema_min_record_size(kxlib):
+    from kitex_amd.codec import DeviceSchema
+    assert DeviceSchema(S.schema_r1()).min_record_size == 89
+    assert DeviceSchema(S.schema_r2()).min_record_size == 89 + 14
+
+
+def test_schema_rejects(kxlib):
+    from kitex_amd.codec import DeviceSchema
+    from kitex_amd._lib import KxError
+    node = S.Struct("Node", [S.Field(1, A.T_I64)])
+    node.fields.append(S.Field(2, A.T_STRUCT, child=node))
+    with pytest.raises(KxError) as e:
+        DeviceSchema(S.Schema(node))
+    assert e.value.code == A.ERR_NOT_IMPLEMENTED
+    with pytest.raises(KxError):
+        DeviceSchema(S.Schema(S.Struct("D", [S.Field(1, A.T_I64), S.Field(1, A.T_I32)])))
+
+
+@pytest.mark.parametrize("mtype", [A.MSG_CALL, A.MSG_REPLY, A.MSG_EXCEPTION, A.MSG_ONEWAY])
+def test_message_begin_matches_kat(kxlib, mtype):
+    from kitex_amd.codec import read_message_begin, write_message_begin
+    b = write_message_begin("messageBegin", mtype, 1)
+    assert b.hex() == f"8001000{mtype}0000000c6d657373616765426567696e00000001"     # binary_test.go:387-457
+    assert read_message_begin(b) == ("messageBegin", mtype, 1, 24)
+    assert kxlib.kx_thrift_message_begin_length(5) == 17
+
+
+def test_ctx_without_gpu(kxlib):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    h = C.c_void_p()
+    assert kxlib.kx_ctx_create(0, C.byref(h)) == A.ERR_NO_DEVICE
