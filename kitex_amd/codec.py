@@ -143,7 +143,8 @@ class ThriftCodec:
         return "Thrift"
 
     def Unmarshal(self, buf, n: int, offsets=None, out: ColumnSet = None, var_caps: Sequence[int] = None,
-                  record_status: bool = False, stream=None, raise_on_error: bool = True) -> DecodeResult:
+                  record_status: bool = False, stream=None, raise_on_error: bool = True,
+                  status=None) -> DecodeResult:
         """Decode n records from `buf` (uint8 tensor in HBM). offsets: int64[n+1] tensor or None."""
         import torch
         ds = self.dschema
@@ -152,7 +153,7 @@ class ThriftCodec:
                 var_caps = [0 if ci.kind == A.COL_FIXED else max(1, buf.numel()) for ci in ds.infos]
             out = alloc_device(ds.infos, n, var_caps, ds.npresence, self.device)
         kc = to_kx_columns(out, ds.infos, var_caps)
-        st = status_tensor(self.device)
+        st = status if status is not None else status_tensor(self.device)
         rs = torch.empty(max(1, n), dtype=torch.uint8, device=self.device) if record_status else None
         rc = lib().kx_thrift_decode_batch(self.ctx.handle, ds.handle, _ptr(buf), buf.numel(), _ptr(offsets), n,
                                           C.byref(kc), _ptr(rs), _ptr(st), _stream_ptr(stream))

@@ -94,7 +94,8 @@ def _buf(n: int = 256):
 
 def prim(fn: str, *args) -> bytes:
     """Call a kxo_write_* primitive and return the bytes it wrote."""
-    b = _buf(1024)
+    extra = sum(len(a) for a in args if isinstance(a, (bytes, bytearray)))
+    b = _buf(1024 + extra)
     n = getattr(lib(), fn)(b, *args)
     return bytes(b[:n])
 
