@@ -173,7 +173,7 @@ def main():
         result["host_inclusive"] = host_inclusive(cdc, wire, n, offsets, var_caps, infos, dev)
     if rank == 0 and world == 1 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(cfg, args.cpu_records)
-        if result["cpu_baseline"]:
+        if result["cpu_baseline"].get("value"):
             result["cpu_baseline"]["gpu_speedup"] = value / result["cpu_baseline"]["value"]
     if rank == 0:
         print(json.dumps(result), flush=True)
