@@ -490,10 +490,17 @@ __device__ __forceinline__ uint64_t rl64(uint64_t v, int l) {
 
 __device__ __forceinline__ uint64_t now_ns() { return __builtin_amdgcn_s_memrealtime() * 10; }  // 100 MHz
 
-// Decoupled look-back, executed by wave 0. Writes S.e_in / S.base_cnt / S.base_var.
+// Decoupled look-back, executed by wave 0 (64 predecessors per window, newest in lane 0).
+// Walks back window by window, summing aggregates, until an inclusive predecessor is found; the
+// speculative chain is verified on the way: for consecutive candidate-bearing tiles a < b,
+// exit(a) == entry(b), and the inclusive tile's exit equals the entry of the oldest candidate tile
+// after it. Tiles without a candidate pass the chain through (implied by the entry check of the
+// next candidate tile, or by the caller's own check). Any mismatch: wait for tile t-1 to publish
+// its inclusive prefix (it validates itself and repairs by a serial walk).
+// Writes S.e_in / S.base_cnt / S.base_var.
 template <int NV>
 __device__ void lookback(const DecParams& dp, Shared& S, uint64_t t, bool chain) {
-  int lane = threadIdx.x & 63;
+  const int lane = threadIdx.x & 63;
   if (t == 0) {
     if (lane == 0) {
       S.e_in = 0; S.base_cnt = 0;
@@ -502,22 +509,24 @@ __device__ void lookback(const DecParams& dp, Shared& S, uint64_t t, bool chain)
     return;
   }
   const uint64_t t0 = now_ns();
-  int64_t j = (int64_t)t - 1 - lane;
-  uint32_t f = j >= 0 ? aload32(dp.flags + j) : 2u;
-  while (__ballot(f == 0)) {
-    __builtin_amdgcn_s_sleep(2);
-    if (f == 0) f = aload32(dp.flags + j);
-    if (now_ns() - t0 > 4000000000ull) { f = 2; break; }   // bounded spin: reported below
-  }
-  uint64_t incl = __ballot(f == 2);
-  bool ok = incl != 0;
-  uint64_t E = 0, cnt = 0;
+  bool ok = true, done = false, timed_out = false;
+  bool have_pending = false, have_newest = false;
+  uint64_t pending_ent = 0, newest_ex = 0, E = 0, cnt = 0;
   uint64_t var[KXP_NV_MAX];
 #pragma unroll
   for (int v = 0; v < KXP_NV_MAX; v++) var[v] = 0;
-  if (ok) {
-    int p = __ffsll((long long)incl) - 1;
-    // every lane <= p reads its payload
+  int64_t wend = (int64_t)t;  // exclusive end of the current window
+  while (ok && !done) {
+    const int64_t j = wend - 1 - lane;
+    uint32_t f = j >= 0 ? aload32(dp.flags + j) : 2u;
+    while (__ballot(f == 0)) {
+      __builtin_amdgcn_s_sleep(1);
+      if (f == 0) f = aload32(dp.flags + j);
+      if (now_ns() - t0 > 4000000000ull) { timed_out = true; break; }
+    }
+    if (timed_out) { ok = false; break; }
+    const uint64_t incl = __ballot(f == 2);
+    const int p = incl ? __ffsll((long long)incl) - 1 : 64;
     uint64_t c = 0, en = X_NONE, ex = 0;
     uint64_t vv[KXP_NV_MAX];
 #pragma unroll
@@ -534,27 +543,52 @@ __device__ void lookback(const DecParams& dp, Shared& S, uint64_t t, bool chain)
         for (int v = 0; v < NV; v++) vv[v] = aload64(d + D_AGG_VAR + v);
       }
     }
-    E = rl64(ex, p);
-    cnt = rl64(c, p);
+    // window sums over lanes <= p (lane p: inclusive prefix)
+    uint64_t sc = lane <= p ? c : 0;
 #pragma unroll
-    for (int v = 0; v < NV; v++) var[v] = rl64(vv[v], p);
-    for (int l = p - 1; l >= 0; l--) {
-      if (E == X_ERR || E == X_DONE) break;
-      uint64_t el = rl64(en, l);
-      uint64_t xl = rl64(ex, l);
-      if (chain) {
-        uint64_t tj = t - 1 - (uint64_t)l;
-        uint64_t tend = min((tj + 1) * (uint64_t)TILE, dp.in_len);
-        if (el != X_NONE) {
-          if (E != el) { ok = false; break; }
-          E = xl;
-        } else if (E < tend) {
-          ok = false; break;
-        }
+    for (int d = 32; d >= 1; d >>= 1) sc += __shfl_xor(sc, d, 64);
+    cnt += sc;
+#pragma unroll
+    for (int v = 0; v < NV; v++) {
+      uint64_t sv = lane <= p ? vv[v] : 0;
+#pragma unroll
+      for (int d = 32; d >= 1; d >>= 1) sv += __shfl_xor(sv, d, 64);
+      var[v] += sv;
+    }
+    if (chain) {
+      // candidate-bearing AGG lanes in this window
+      const bool cand = lane < p && en != X_NONE;
+      const uint64_t cm = __ballot(cand);
+      // each candidate lane links to the next older candidate lane inside the window
+      const uint64_t older_mask = lane < 63 ? cm & ~((2ull << lane) - 1) : 0ull;
+      const int older = older_mask ? __ffsll((long long)older_mask) - 1 : -1;
+      const uint64_t older_ex = __shfl(ex, older < 0 ? lane : older, 64);
+      const bool link_bad = cand && older >= 0 && older_ex != en;
+      if (__ballot(link_bad)) ok = false;
+      if (cm) {
+        const int newest = __ffsll((long long)cm) - 1;
+        const int oldest = 63 - __clzll((long long)cm);
+        const uint64_t newest_exv = rl64(ex, newest);
+        const uint64_t oldest_en = rl64(en, oldest);
+        if (have_pending && newest_exv != pending_ent) ok = false;
+        if (!have_newest) { newest_ex = newest_exv; have_newest = true; }
+        pending_ent = oldest_en;
+        have_pending = true;
       }
-      cnt += rl64(c, l);
-#pragma unroll
-      for (int v = 0; v < NV; v++) var[v] += rl64(vv[v], l);
+    }
+    if (p < 64) {
+      const uint64_t xp = rl64(ex, p);
+      if (xp == X_ERR || xp == X_DONE) {
+        E = xp;
+      } else if (chain) {
+        if (have_pending && xp != pending_ent) ok = false;
+        E = have_newest ? newest_ex : xp;
+      } else {
+        E = xp;
+      }
+      done = true;
+    } else {
+      wend -= 64;
     }
   }
   if (!ok) {
@@ -567,7 +601,7 @@ __device__ void lookback(const DecParams& dp, Shared& S, uint64_t t, bool chain)
       if (now_ns() - t0 > 4000000000ull) break;
     }
     if (g != 2) {
-      E = X_ERR;  // give up: the chain is reported as an internal error
+      E = X_ERR;  // give up: reported as an internal error
       if (lane == 0) atomicCAS((int*)&dp.status->code, 0, KX_ERR_INTERNAL);
     } else {
       E = aload64(d + D_INC_EXIT);
@@ -822,7 +856,7 @@ __global__ void __launch_bounds__(NT) decode_kernel(DecParams dp) {
         kx_status* st = dp.status;
         st->code = KX_ERR_EOF; st->record = tot; st->offset = dp.in_len;
         st->n_records = tot; st->consumed = dp.in_len;
-        for (int v = 0; v < NV; v++) {
+        for (int v = 0; v < NV && v < (int)P.nvar; v++) {
           uint64_t vt = S.base_var[v] + S.tile_var[v];
           if (v < 8) st->var_total[v] = vt;
           if (MODE == M_THRIFT) dp.cols.offs[P.var_col[v]][tot] = (uint32_t)vt;
@@ -850,6 +884,7 @@ __global__ void __launch_bounds__(NT) decode_kernel(DecParams dp) {
     if (MODE != M_THRIFT) return;
 #pragma unroll
     for (int v = 0; v < NV; v++) {
+      if (v >= (int)P.nvar) break;
       uint32_t c = P.var_col[v];
       const KxpCol& K = P.col[c];
       dp.cols.offs[c][r] = (uint32_t)run[v];
@@ -869,6 +904,7 @@ __global__ void __launch_bounds__(NT) decode_kernel(DecParams dp) {
     st->consumed = consumed;
 #pragma unroll
     for (int v = 0; v < NV; v++) {
+      if (v >= (int)P.nvar) break;
       if (v < 8) st->var_total[v] = run[v];
       if (MODE == M_THRIFT) dp.cols.offs[P.var_col[v]][nrec] = (uint32_t)run[v];
     }
