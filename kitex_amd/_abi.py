@@ -89,7 +89,7 @@ class Status(C.Structure):
         ("n_records", C.c_uint64),
         ("consumed", C.c_uint64),
         ("var_total", C.c_uint64 * 8),
-        ("reserved1", C.c_uint64 * 3),
+        ("diag", C.c_uint64 * 3),
     ]
 
 

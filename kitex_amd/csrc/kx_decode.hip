@@ -592,6 +592,7 @@ __device__ void lookback(const DecParams& dp, Shared& S, uint64_t t, bool chain)
     }
   }
   if (!ok) {
+    if (lane == 0) atomicAdd((unsigned long long*)&dp.status->diag[1], 1ull);
     // wait for the immediate predecessor's inclusive prefix
     const uint64_t* d = dp.desc + (t - 1) * DSTRIDE;
     uint32_t g = aload32(dp.flags + t - 1);
@@ -779,6 +780,7 @@ __global__ void __launch_bounds__(NT) decode_kernel(DecParams dp) {
   __syncthreads();
 
   // ---- publish the aggregate, then look back ----
+  if (tid == 0 && !known && !S.ok) atomicAdd((unsigned long long*)&dp.status->diag[2], 1ull);
   if (tid == 0 && (known || S.ok)) {
     uint64_t words[3 + KXP_NV_MAX];
     words[0] = S.tile_cnt;
@@ -795,6 +797,7 @@ __global__ void __launch_bounds__(NT) decode_kernel(DecParams dp) {
   if (!known && !terminal) {
     bool valid = S.ok && (S.spec_ent == X_NONE ? E >= thi : E == S.spec_ent);
     if (!valid) {
+      if (tid == 0) atomicAdd((unsigned long long*)&dp.status->diag[0], 1ull);
       // serial fallback: walk from the true entry, assigning each record start to its lane
       __syncthreads();
       S.ent[tid] = X_NONE;
