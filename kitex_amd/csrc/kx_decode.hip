@@ -409,6 +409,7 @@ struct Shared {
   uint32_t tile_id;
   int32_t ok;
   int32_t first_err_lane;
+  int32_t changed;
 };
 
 // ---- block scans (256 threads = 4 waves) ----
@@ -703,11 +704,23 @@ __global__ void __launch_bounds__(NT) decode_kernel(DecParams dp) {
       const uint32_t sig = MODE == M_THRIFT ? P.sig : (uint32_t)KX_T_STOP;
       const uint32_t smask = (MODE == M_THRIFT && P.sig_len == 3) ? 0xffffffu : 0xffu;
       const uint64_t slen = (MODE == M_THRIFT && P.sig_len == 3) ? 3 : 1;
-      for (uint64_t p = seg_lo; p < seg_hi; p++) {
-        if (p + slen > dp.in_len) break;
-        if ((ld4(w, p) & smask) == sig) { ent = p; break; }
+      // one LDS dword per 4 candidate positions (the segment lies inside the LDS window)
+      const uint64_t plim = min(seg_hi, dp.in_len >= slen ? dp.in_len - slen + 1 : 0ull);
+      const uint64_t r0w = abs_in + seg_lo - wlo;   // window byte of seg_lo
+      uint32_t q = (uint32_t)(r0w >> 2);
+      uint64_t pbase = seg_lo - (r0w & 3);          // input position of window byte 4q
+      uint32_t x0 = S.win[q];
+      for (; pbase < plim; pbase += 4, q++) {
+        const uint32_t x1 = S.win[q + 1];
+        uint32_t hit = 0;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const uint64_t pp = pbase + j;
+          if (pp >= seg_lo && pp < plim && (__builtin_amdgcn_alignbyte(x1, x0, j) & smask) == sig) hit |= 1u << j;
+        }
+        if (hit) { ent = pbase + __builtin_ctz(hit); break; }
+        x0 = x1;
       }
-      if (MODE == M_SKIP && ent == X_NONE) ent = X_NONE;
     }
   }
   // (re)walk from `ent` through the segment; used for speculation and for the serial fallback
@@ -732,29 +745,65 @@ __global__ void __launch_bounds__(NT) decode_kernel(DecParams dp) {
   };
   if (!known) walk_measure(ent);
 
-  // ---- link validation (concatenated mode) ----
+  // ---- link repair (concatenated mode) ----
+  // Every lane must start walking at the first true record start in its segment. Given the exit
+  // of the previous walking lane (or the tile's entry `seed`), each lane adopts the position that
+  // exit implies and re-walks; rounds repeat until nothing changes (normally 0-1 rounds: a false
+  // signature hit is corrected by its neighbour's exit). seed == X_NONE: the tile's entry is not
+  // known yet and the first candidate lane is trusted.
   S.ent[tid] = ent;
   S.ext[tid] = ex;
-  if (tid == 0) { S.ok = 1; S.first_err_lane = NT; }
+  if (tid == 0) { S.first_err_lane = NT; S.ok = 1; }
   __syncthreads();
-  if (!known) {
-    bool has = ent != X_NONE;
-    int pc = block_excl_maxscan_i32(has ? tid : -1, S.scan_i);
-    bool lane_ok = true;
-    if (pc >= 0) {
-      uint64_t pe = S.ext[pc];
-      if (pe != X_ERR) lane_ok = has ? (pe == ent) : (seg_lo >= thi || pe >= seg_hi);
+  auto relax = [&](uint64_t seed, int max_rounds) -> int {  // rounds used, -1 if not converged
+    for (int it = 0; it <= max_rounds; it++) {
+      const bool has = ent != X_NONE;
+      const int pc = block_excl_maxscan_i32(has ? tid : -1, S.scan_i);
+      const uint64_t pe = pc >= 0 ? S.ext[pc] : seed;
+      uint64_t want = ent;
+      if (pe != X_NONE) {
+        if (pe == X_ERR || pe == X_DONE || seg_lo >= thi || pe >= seg_hi) want = X_NONE;
+        else if (pe >= seg_lo) want = pe;
+        // pe < seg_lo: an earlier lane adopts pe first; revisit next round
+      }
+      if (tid == 0) S.changed = 0;
+      __syncthreads();
+      if (want != ent) {
+        if (it == max_rounds) { S.changed = 2; }
+        else {
+          ent = want;
+          walk_measure(ent);
+          S.ent[tid] = ent;
+          S.ext[tid] = ex;
+          S.changed = 1;
+        }
+      }
+      __syncthreads();
+      const int ch = S.changed;
+      __syncthreads();
+      if (ch == 0) return it;
+      if (ch == 2) return -1;
     }
-    if (!lane_ok) atomicAnd(&S.ok, 0);
-    if (has && ex == X_ERR) atomicMin(&S.first_err_lane, tid);
+    return -1;
+  };
+  auto find_first_err = [&]() {
+    if (tid == 0) S.first_err_lane = NT;
+    __syncthreads();
+    if (ent != X_NONE && ex == X_ERR) atomicMin(&S.first_err_lane, tid);
+    __syncthreads();
+  };
+  if (!known) {
+    int r = relax(X_NONE, 16);
+    if (r != 0 && tid == 0) atomicAdd((unsigned long long*)&dp.status->diag[2], 1ull);
+    if (r < 0 && tid == 0) S.ok = 0;
+    find_first_err();
   }
-  __syncthreads();
 
   // lanes after the first failing walk hold no valid records
   uint64_t cpre = 0;
   uint64_t vpre[KXP_NV_MAX];
   auto scan_tile = [&]() {
-    bool live = known || tid <= S.first_err_lane;
+    bool live = known || (ent != X_NONE && tid <= S.first_err_lane);
     uint64_t tot;
     cpre = block_excl_scan_u64(live ? cnt : 0, &tot, S.scan_u);
     if (tid == 0) S.tile_cnt = tot;
@@ -764,23 +813,26 @@ __global__ void __launch_bounds__(NT) decode_kernel(DecParams dp) {
       if (tid == 0) S.tile_var[v] = tot;
     }
   };
+  // tile entry / exit from the lane table; `pass` is the exit when no lane holds a record start
+  auto tile_ends = [&](uint64_t pass) {
+    if (tid == 0) {
+      uint64_t se = X_NONE, sx = pass;
+      for (int i = 0; i < NT; i++)
+        if (S.ent[i] != X_NONE) { se = S.ent[i]; break; }
+      if (S.first_err_lane < NT) sx = X_ERR;
+      else
+        for (int i = NT - 1; i >= 0; i--)
+          if (S.ent[i] != X_NONE) { sx = S.ext[i]; break; }
+      S.spec_ent = se;
+      S.tile_exit = sx;
+    }
+    __syncthreads();
+  };
   scan_tile();
-  // tile exit / speculative entry (concatenated mode)
-  if (!known && tid == 0) {
-    uint64_t se = X_NONE, sx = X_NONE;
-    for (int i = 0; i < NT; i++)
-      if (S.ent[i] != X_NONE) { se = S.ent[i]; break; }
-    if (S.first_err_lane < NT) sx = X_ERR;
-    else
-      for (int i = NT - 1; i >= 0; i--)
-        if (S.ent[i] != X_NONE) { sx = S.ext[i]; break; }
-    S.spec_ent = se;
-    S.tile_exit = sx;
-  }
+  if (!known) tile_ends(X_NONE);
   __syncthreads();
 
   // ---- publish the aggregate, then look back ----
-  if (tid == 0 && !known && !S.ok) atomicAdd((unsigned long long*)&dp.status->diag[2], 1ull);
   if (tid == 0 && (known || S.ok)) {
     uint64_t words[3 + KXP_NV_MAX];
     words[0] = S.tile_cnt;
@@ -798,40 +850,35 @@ __global__ void __launch_bounds__(NT) decode_kernel(DecParams dp) {
     bool valid = S.ok && (S.spec_ent == X_NONE ? E >= thi : E == S.spec_ent);
     if (!valid) {
       if (tid == 0) atomicAdd((unsigned long long*)&dp.status->diag[0], 1ull);
-      // serial fallback: walk from the true entry, assigning each record start to its lane
-      __syncthreads();
-      S.ent[tid] = X_NONE;
-      __syncthreads();
-      if (tid == 0) {
-        uint64_t pos = E;
-        while (pos < thi && pos < dp.in_len) {
-          uint64_t lane_of = (pos - tlo) / SEG;
-          if (S.ent[lane_of] == X_NONE) S.ent[lane_of] = pos;
-          VarState<NV> vs; uint64_t pres, end;
-          int rc;
-          if (MODE == M_THRIFT) rc = thrift_record<NV, false>(w, P, S.colp, pos, dp.in_len, 0, &end, vs, pres);
-          else { end = pos; rc = dskip(w, end, dp.in_len, KX_T_STRUCT, 64); }
-          if (rc) break;
-          pos = end;
+      // repair from the true entry
+      int r = relax(E, 64);
+      if (r < 0) {
+        // last resort: one lane walks from the true entry, assigning each record start to its lane
+        __syncthreads();
+        S.ent[tid] = X_NONE;
+        __syncthreads();
+        if (tid == 0) {
+          uint64_t pos = E;
+          while (pos < thi && pos < dp.in_len) {
+            uint64_t lane_of = (pos - tlo) / SEG;
+            if (S.ent[lane_of] == X_NONE) S.ent[lane_of] = pos;
+            VarState<NV> vs; uint64_t pres, end;
+            int rc;
+            if (MODE == M_THRIFT) rc = thrift_record<NV, false>(w, P, S.colp, pos, dp.in_len, 0, &end, vs, pres);
+            else { end = pos; rc = dskip(w, end, dp.in_len, KX_T_STRUCT, 64); }
+            if (rc) break;
+            pos = end;
+          }
         }
-        S.first_err_lane = NT;
+        __syncthreads();
+        ent = S.ent[tid];
+        walk_measure(ent);
+        S.ext[tid] = ex;
+        __syncthreads();
       }
-      __syncthreads();
-      ent = S.ent[tid];
-      walk_measure(ent);
-      S.ext[tid] = ex;
-      if (ex == X_ERR && ent != X_NONE) atomicMin(&S.first_err_lane, tid);
-      __syncthreads();
+      find_first_err();
       scan_tile();
-      if (tid == 0) {
-        uint64_t sx = E;  // no record starts here: pass the entry through
-        if (S.first_err_lane < NT) sx = X_ERR;
-        else
-          for (int i = NT - 1; i >= 0; i--)
-            if (S.ent[i] != X_NONE) { sx = S.ext[i]; break; }
-        S.tile_exit = sx;
-      }
-      __syncthreads();
+      tile_ends(E);
     } else if (S.spec_ent == X_NONE && tid == 0) {
       S.tile_exit = E;  // pass-through tile
     }
@@ -875,7 +922,7 @@ __global__ void __launch_bounds__(NT) decode_kernel(DecParams dp) {
   if (!known && terminal) return;
 
   // ---- walk 2: re-parse from LDS and scatter ----
-  bool live = known || tid <= S.first_err_lane;
+  bool live = known || (ent != X_NONE && tid <= S.first_err_lane);
   if (!live) return;
   uint64_t rec = base + cpre;
   uint64_t run[KXP_NV_MAX];
