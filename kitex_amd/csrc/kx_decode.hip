@@ -21,6 +21,9 @@
 
 #include "kx_internal.h"
 
+#define LDS __attribute__((address_space(3)))
+#define GLB __attribute__((address_space(1)))
+
 namespace {
 
 constexpr int NT = 256;                 // threads per workgroup (4 waves)
@@ -68,7 +71,7 @@ struct Win {
   uint64_t in_len;
   uint64_t wlo;        // absolute address of LDS byte 0 (16-aligned)
   uint32_t wlen;       // bytes valid in LDS
-  const uint32_t* lds;
+  const LDS uint32_t* lds;
 };
 
 __device__ __forceinline__ uint32_t gld4(const Win& w, uint64_t p) {
@@ -76,8 +79,8 @@ __device__ __forceinline__ uint32_t gld4(const Win& w, uint64_t p) {
   uint64_t A = a & ~3ull;
   uint32_t sh = (uint32_t)(a & 3);
   uint64_t end = (uint64_t)w.in + w.in_len;
-  uint32_t x0 = A < end ? *(const uint32_t*)A : 0u;
-  uint32_t x1 = A + 4 < end ? *(const uint32_t*)(A + 4) : 0u;
+  uint32_t x0 = A < end ? *(const GLB uint32_t*)A : 0u;
+  uint32_t x1 = A + 4 < end ? *(const GLB uint32_t*)(A + 4) : 0u;
   return __builtin_amdgcn_alignbyte(x1, x0, sh);
 }
 
@@ -93,8 +96,8 @@ __device__ __forceinline__ uint32_t ld4(const Win& w, uint64_t p) {
 
 __device__ __forceinline__ uint32_t ld1(const Win& w, uint64_t p) {
   uint64_t r = (uint64_t)w.in + p - w.wlo;
-  if (r < w.wlen) return ((const uint8_t*)w.lds)[r];
-  return w.in[p];
+  if (r < w.wlen) return ((const LDS uint8_t*)w.lds)[r];
+  return ((const GLB uint8_t*)w.in)[p];
 }
 
 __device__ __forceinline__ uint32_t be32(const Win& w, uint64_t p) { return __builtin_bswap32(ld4(w, p)); }
@@ -254,20 +257,20 @@ struct Shared;  // fwd
 
 __device__ __forceinline__ void store_col(void* base, uint32_t width, uint64_t rec, uint64_t v) {
   switch (width) {
-    case 1: ((uint8_t*)base)[rec] = (uint8_t)v; break;
-    case 2: ((uint16_t*)base)[rec] = (uint16_t)v; break;
-    case 4: ((uint32_t*)base)[rec] = (uint32_t)v; break;
-    default: ((uint64_t*)base)[rec] = v; break;
+    case 1: ((GLB uint8_t*)base)[rec] = (uint8_t)v; break;
+    case 2: ((GLB uint16_t*)base)[rec] = (uint16_t)v; break;
+    case 4: ((GLB uint32_t*)base)[rec] = (uint32_t)v; break;
+    default: ((GLB uint64_t*)base)[rec] = v; break;
   }
 }
 
 template <int NV, bool EMIT>
-__device__ int thrift_record(const Win& w, const KxProgram& P, void* const* colp, uint64_t start,
+__device__ int thrift_record(const Win& w, const LDS KxProgram* P, void* const LDS* colp, uint64_t start,
                              uint64_t limit, uint64_t rec, uint64_t* endp, VarState<NV>& vs,
                              uint64_t& pres) {
   uint64_t pos = start;
   int inst = 0;
-  int pred = P.inst[0].enc_first;
+  int pred = P->inst[0].enc_first;
   uint64_t seen = 0;
   pres = 0;
 #pragma unroll
@@ -278,30 +281,30 @@ __device__ int thrift_record(const Win& w, const KxProgram& P, void* const* colp
     uint32_t t = h & 0xff;
     if (t == KX_T_STOP) {
       pos += 1;
-      uint64_t rq = P.inst[inst].req_mask;
+      uint64_t rq = P->inst[inst].req_mask;
       if ((seen & rq) != rq) return KX_ERR_INVALID_DATA;   // RequiredFieldNotSetError
       if (inst == 0) break;
-      pred = P.inst[inst].ret_pred;
-      inst = P.inst[inst].parent;
+      pred = P->inst[inst].ret_pred;
+      inst = P->inst[inst].parent;
       continue;
     }
     if (limit - pos < 3) return KX_ERR_EOF;
     int id = (int)(int16_t)((h & 0xff00u) | ((h >> 16) & 0xffu));
     pos += 3;
     int fi = -1;
-    if (pred >= 0 && P.f[pred].id == id) {
+    if (pred >= 0 && P->f[pred].id == id) {
       fi = pred;
     } else {
-      int f0 = P.inst[inst].first, nf = P.inst[inst].nfields;
+      int f0 = P->inst[inst].first, nf = P->inst[inst].nfields;
       for (int k = 0; k < nf; k++)
-        if (P.f[f0 + k].id == id) { fi = f0 + k; break; }
+        if (P->f[f0 + k].id == id) { fi = f0 + k; break; }
     }
-    if (fi < 0 || P.f[fi].ttype != t) {                     // default: / mismatched type -> Skip
+    if (fi < 0 || P->f[fi].ttype != t) {                     // default: / mismatched type -> Skip
       int rc = dskip(w, pos, limit, t, 64);
       if (rc) return rc;
       continue;
     }
-    const KxpField F = P.f[fi];
+    const KxpField F = P->f[fi];
     pred = F.enc_next;
     if (F.kind == KXP_K_FIXED) {
       uint32_t wd = F.width;
@@ -324,7 +327,7 @@ __device__ int thrift_record(const Win& w, const KxProgram& P, void* const* colp
       vset<NV>(vs, F.vslot, pos + 5, (uint32_t)l);
       pos += 5 + b;
     } else {                                                 // nested struct: NewX() + FastRead
-      const KxpInst& C = P.inst[F.child];
+      const KxpInst C = P->inst[F.child];
       seen &= ~C.subtree_mask;
       pres &= ~C.pres_mask;
 #pragma unroll
@@ -341,8 +344,8 @@ __device__ int thrift_record(const Win& w, const KxProgram& P, void* const* colp
   }
   if (EMIT) {
     // fields never seen (or reset by a repeated struct field) take their default
-    for (uint32_t c = 0; c < P.ncols; c++) {
-      const KxpCol& K = P.col[c];
+    for (uint32_t c = 0; c < P->ncols; c++) {
+      const KxpCol K = P->col[c];
       if (K.kind == KXP_K_FIXED && !((seen >> K.field) & 1)) store_col(colp[c], K.width, rec, (uint64_t)K.defv);
     }
   }
@@ -351,20 +354,21 @@ __device__ int thrift_record(const Win& w, const KxProgram& P, void* const* colp
 }
 
 template <int NV>
-__device__ void emit_defaults(const KxProgram& P, void* const* colp, uint64_t rec) {
-  for (uint32_t c = 0; c < P.ncols; c++) {
-    const KxpCol& K = P.col[c];
+__device__ void emit_defaults(const LDS KxProgram* P, void* const LDS* colp, uint64_t rec) {
+  for (uint32_t c = 0; c < P->ncols; c++) {
+    const KxpCol K = P->col[c];
     if (K.kind == KXP_K_FIXED) store_col(colp[c], K.width, rec, (uint64_t)K.defv);
   }
 }
 
 // copy one var field payload (n units of `width` bytes) from the input to its arena
-__device__ void copy_var(const Win& w, const KxpCol& K, uint64_t src, uint32_t n, uint8_t* dst) {
+__device__ void copy_var(const Win& w, const KxpCol& K, uint64_t src, uint32_t n, uint8_t* dst_) {
+  GLB uint8_t* dst = (GLB uint8_t*)dst_;
   if (K.kind == KXP_K_BYTES) {
     uint32_t i = 0;
     // bytes until the destination is 4-aligned, then dwords, then the tail
-    while (i < n && (((uintptr_t)(dst + i)) & 3)) { dst[i] = (uint8_t)ld1(w, src + i); i++; }
-    for (; i + 4 <= n; i += 4) *(uint32_t*)(dst + i) = ld4(w, src + i);
+    while (i < n && (((uintptr_t)(dst_ + i)) & 3)) { dst[i] = (uint8_t)ld1(w, src + i); i++; }
+    for (; i + 4 <= n; i += 4) *(GLB uint32_t*)(dst + i) = ld4(w, src + i);
     for (; i < n; i++) dst[i] = (uint8_t)ld1(w, src + i);
     return;
   }
@@ -378,14 +382,14 @@ __device__ void copy_var(const Win& w, const KxpCol& K, uint64_t src, uint32_t n
     case 2:
       for (uint32_t i = 0; i < n; i++) {
         uint32_t x = ld4(w, src + 2ull * i);
-        ((uint16_t*)dst)[i] = (uint16_t)(((x & 0xff) << 8) | ((x >> 8) & 0xff));
+        ((GLB uint16_t*)dst)[i] = (uint16_t)(((x & 0xff) << 8) | ((x >> 8) & 0xff));
       }
       break;
     case 4:
-      for (uint32_t i = 0; i < n; i++) ((uint32_t*)dst)[i] = be32(w, src + 4ull * i);
+      for (uint32_t i = 0; i < n; i++) ((GLB uint32_t*)dst)[i] = be32(w, src + 4ull * i);
       break;
     default:
-      for (uint32_t i = 0; i < n; i++) ((uint64_t*)dst)[i] = be64(w, src + 8ull * i);
+      for (uint32_t i = 0; i < n; i++) ((GLB uint64_t*)dst)[i] = be64(w, src + 8ull * i);
       break;
   }
 }
@@ -640,7 +644,8 @@ __global__ void __launch_bounds__(NT) decode_kernel(DecParams dp) {
   }
   __syncthreads();
   const uint64_t t = S.tile_id;
-  const KxProgram& P = S.prog;
+  const LDS KxProgram* P = (const LDS KxProgram*)&S.prog;
+  void* const LDS* colp = (void* const LDS*)S.colp;
 
   // ---- this tile's byte range and the LDS window ----
   uint64_t r0 = 0, r1 = 0, tlo, thi;
@@ -658,17 +663,24 @@ __global__ void __launch_bounds__(NT) decode_kernel(DecParams dp) {
   const uint64_t gend = (abs_in + dp.in_len + 15) & ~15ull;
   const uint32_t wlen = dp.in_len == 0 ? 0u : (uint32_t)min((uint64_t)WINB, gend > wlo ? gend - wlo : 0ull);
   {
-    const uint4* g = (const uint4*)wlo;
-    uint4* l = (uint4*)S.win;
+    // LDS-DMA: every 16-byte chunk goes HBM -> LDS without touching registers; all loads of the
+    // tile are in flight together (global_load_lds_dwordx4, wave-uniform LDS base + lane * 16).
+    const GLB uint8_t* g = (const GLB uint8_t*)wlo;
     const int nch = (int)(wlen >> 4);
-#pragma unroll 9
-    for (int k = 0; k < (WIN_CHUNKS + NT - 1) / NT; k++) {
-      int c = tid + k * NT;
-      if (c < nch) l[c] = g[c];
+    const int wv = tid >> 6;
+    constexpr int KW = (WIN_CHUNKS + NT - 1) / NT;
+#pragma unroll
+    for (int k = 0; k < KW; k++) {
+      const int c = tid + k * NT;
+      if (c < nch) {
+        LDS void* dst = (LDS void*)((LDS uint8_t*)S.win + (size_t)(k * NT + wv * 64) * 16);
+        __builtin_amdgcn_global_load_lds((const GLB void*)(g + (size_t)c * 16), dst, 16, 0, 0);
+      }
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
-  Win w{dp.in, dp.in_len, wlo, wlen, S.win};
+  Win w{dp.in, dp.in_len, wlo, wlen, (const LDS uint32_t*)S.win};
 
   // ---- walk 1: speculative entry + measure ----
   uint64_t ent = X_NONE, ex = X_NONE, cnt = 0;
@@ -687,7 +699,7 @@ __global__ void __launch_bounds__(NT) decode_kernel(DecParams dp) {
         err = KX_ERR_INVALID_ARG;
       } else {
         VarState<NV> vs; uint64_t pres, end;
-        if (MODE == M_THRIFT) err = thrift_record<NV, false>(w, P, S.colp, a, b, r, &end, vs, pres);
+        if (MODE == M_THRIFT) err = thrift_record<NV, false>(w, P, colp, a, b, r, &end, vs, pres);
         else { end = a; err = dskip(w, end, b, KX_T_STRUCT, 64); }
         if (!err) {
 #pragma unroll
@@ -701,9 +713,9 @@ __global__ void __launch_bounds__(NT) decode_kernel(DecParams dp) {
     seg_hi = min(seg_lo + SEG, thi);
     if (seg_lo < thi) {
       // first canonical signature in [seg_lo, seg_hi)
-      const uint32_t sig = MODE == M_THRIFT ? P.sig : (uint32_t)KX_T_STOP;
-      const uint32_t smask = (MODE == M_THRIFT && P.sig_len == 3) ? 0xffffffu : 0xffu;
-      const uint64_t slen = (MODE == M_THRIFT && P.sig_len == 3) ? 3 : 1;
+      const uint32_t sig = MODE == M_THRIFT ? P->sig : (uint32_t)KX_T_STOP;
+      const uint32_t smask = (MODE == M_THRIFT && P->sig_len == 3) ? 0xffffffu : 0xffu;
+      const uint64_t slen = (MODE == M_THRIFT && P->sig_len == 3) ? 3 : 1;
       // one LDS dword per 4 candidate positions (the segment lies inside the LDS window)
       const uint64_t plim = min(seg_hi, dp.in_len >= slen ? dp.in_len - slen + 1 : 0ull);
       const uint64_t r0w = abs_in + seg_lo - wlo;   // window byte of seg_lo
@@ -733,7 +745,7 @@ __global__ void __launch_bounds__(NT) decode_kernel(DecParams dp) {
     while (pos < seg_hi && pos < dp.in_len) {
       VarState<NV> vs; uint64_t pres, end;
       int rc;
-      if (MODE == M_THRIFT) rc = thrift_record<NV, false>(w, P, S.colp, pos, dp.in_len, 0, &end, vs, pres);
+      if (MODE == M_THRIFT) rc = thrift_record<NV, false>(w, P, colp, pos, dp.in_len, 0, &end, vs, pres);
       else { end = pos; rc = dskip(w, end, dp.in_len, KX_T_STRUCT, 64); }
       if (rc) { err = rc; ex = X_ERR; return; }
 #pragma unroll
@@ -864,7 +876,7 @@ __global__ void __launch_bounds__(NT) decode_kernel(DecParams dp) {
             if (S.ent[lane_of] == X_NONE) S.ent[lane_of] = pos;
             VarState<NV> vs; uint64_t pres, end;
             int rc;
-            if (MODE == M_THRIFT) rc = thrift_record<NV, false>(w, P, S.colp, pos, dp.in_len, 0, &end, vs, pres);
+            if (MODE == M_THRIFT) rc = thrift_record<NV, false>(w, P, colp, pos, dp.in_len, 0, &end, vs, pres);
             else { end = pos; rc = dskip(w, end, dp.in_len, KX_T_STRUCT, 64); }
             if (rc) break;
             pos = end;
@@ -906,10 +918,10 @@ __global__ void __launch_bounds__(NT) decode_kernel(DecParams dp) {
         kx_status* st = dp.status;
         st->code = KX_ERR_EOF; st->record = tot; st->offset = dp.in_len;
         st->n_records = tot; st->consumed = dp.in_len;
-        for (int v = 0; v < NV && v < (int)P.nvar; v++) {
+        for (int v = 0; v < NV && v < (int)P->nvar; v++) {
           uint64_t vt = S.base_var[v] + S.tile_var[v];
           if (v < 8) st->var_total[v] = vt;
-          if (MODE == M_THRIFT) dp.cols.offs[P.var_col[v]][tot] = (uint32_t)vt;
+          if (MODE == M_THRIFT) dp.cols.offs[P->var_col[v]][tot] = (uint32_t)vt;
         }
         if (MODE == M_SKIP) dp.skip_out[tot] = dp.in_len;
       }
@@ -934,13 +946,13 @@ __global__ void __launch_bounds__(NT) decode_kernel(DecParams dp) {
     if (MODE != M_THRIFT) return;
 #pragma unroll
     for (int v = 0; v < NV; v++) {
-      if (v >= (int)P.nvar) break;
-      uint32_t c = P.var_col[v];
-      const KxpCol& K = P.col[c];
+      if (v >= (int)P->nvar) break;
+      uint32_t c = P->var_col[v];
+      const KxpCol K = P->col[c];
       dp.cols.offs[c][r] = (uint32_t)run[v];
       uint32_t n = vs.len[v];
       if (run[v] + n <= dp.cols.cap[c]) {
-        if (n) copy_var(w, K, vs.pos[v], n, (uint8_t*)S.colp[c] + run[v] * K.width);
+        if (n) copy_var(w, K, vs.pos[v], n, (uint8_t*)colp[c] + run[v] * K.width);
       } else {
         atomicOr(dp.overflow, 1u);
       }
@@ -954,9 +966,9 @@ __global__ void __launch_bounds__(NT) decode_kernel(DecParams dp) {
     st->consumed = consumed;
 #pragma unroll
     for (int v = 0; v < NV; v++) {
-      if (v >= (int)P.nvar) break;
+      if (v >= (int)P->nvar) break;
       if (v < 8) st->var_total[v] = run[v];
-      if (MODE == M_THRIFT) dp.cols.offs[P.var_col[v]][nrec] = (uint32_t)run[v];
+      if (MODE == M_THRIFT) dp.cols.offs[P->var_col[v]][nrec] = (uint32_t)run[v];
     }
   };
 
@@ -968,11 +980,11 @@ __global__ void __launch_bounds__(NT) decode_kernel(DecParams dp) {
     uint64_t end;
     int rc = err;
     if (!rc) {
-      if (MODE == M_THRIFT) rc = thrift_record<NV, true>(w, P, S.colp, a, b, r, &end, vs, pres);
+      if (MODE == M_THRIFT) rc = thrift_record<NV, true>(w, P, colp, a, b, r, &end, vs, pres);
       else { end = a; rc = dskip(w, end, b, KX_T_STRUCT, 64); }
     }
     if (rc) {
-      if (MODE == M_THRIFT) emit_defaults<NV>(P, S.colp, r);
+      if (MODE == M_THRIFT) emit_defaults<NV>(P, colp, r);
 #pragma unroll
       for (int v = 0; v < NV; v++) vs.len[v] = 0;
       pres = 0;
@@ -990,7 +1002,7 @@ __global__ void __launch_bounds__(NT) decode_kernel(DecParams dp) {
     VarState<NV> vs;
     uint64_t end;
     int rc;
-    if (MODE == M_THRIFT) rc = thrift_record<NV, true>(w, P, S.colp, pos, dp.in_len, rec, &end, vs, pres);
+    if (MODE == M_THRIFT) rc = thrift_record<NV, true>(w, P, colp, pos, dp.in_len, rec, &end, vs, pres);
     else {
       end = pos;
       rc = dskip(w, end, dp.in_len, KX_T_STRUCT, 64);
