@@ -240,6 +240,31 @@ __device__ __noinline__ int dskip(const Win& w, uint64_t& pos, uint64_t limit, u
 // ---------------------------------------------------------------------------------------------
 // per-record FastRead. EMIT=false: measure (length, var lengths); EMIT=true: also store columns.
 // ---------------------------------------------------------------------------------------------
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// struct reads from the LDS-resident program (no implicit copy across address spaces)
+__device__ __forceinline__ KxpField ld_field(const LDS KxProgram* P, int i) {
+  u32x4 v = *(const LDS u32x4*)&P->f[i];
+  KxpField F;
+  __builtin_memcpy(&F, &v, sizeof F);
+  return F;
+}
+__device__ __forceinline__ KxpInst ld_inst(const LDS KxProgram* P, int i) {
+  u32x4 v[2];
+  v[0] = ((const LDS u32x4*)&P->inst[i])[0];
+  v[1] = ((const LDS u32x4*)&P->inst[i])[1];
+  KxpInst I;
+  __builtin_memcpy(&I, v, sizeof I);
+  return I;
+}
+__device__ __forceinline__ KxpCol ld_col(const LDS KxProgram* P, int i) {
+  u32x4 v = *(const LDS u32x4*)&P->col[i];
+  KxpCol K;
+  __builtin_memcpy(&K, &v, sizeof K);
+  return K;
+}
+
 template <int NV>
 struct VarState {
   uint64_t pos[NV > 0 ? NV : 1];
@@ -304,7 +329,7 @@ __device__ int thrift_record(const Win& w, const LDS KxProgram* P, void* const L
       if (rc) return rc;
       continue;
     }
-    const KxpField F = P->f[fi];
+    const KxpField F = ld_field(P, fi);
     pred = F.enc_next;
     if (F.kind == KXP_K_FIXED) {
       uint32_t wd = F.width;
@@ -327,7 +352,7 @@ __device__ int thrift_record(const Win& w, const LDS KxProgram* P, void* const L
       vset<NV>(vs, F.vslot, pos + 5, (uint32_t)l);
       pos += 5 + b;
     } else {                                                 // nested struct: NewX() + FastRead
-      const KxpInst C = P->inst[F.child];
+      const KxpInst C = ld_inst(P, F.child);
       seen &= ~C.subtree_mask;
       pres &= ~C.pres_mask;
 #pragma unroll
@@ -345,7 +370,7 @@ __device__ int thrift_record(const Win& w, const LDS KxProgram* P, void* const L
   if (EMIT) {
     // fields never seen (or reset by a repeated struct field) take their default
     for (uint32_t c = 0; c < P->ncols; c++) {
-      const KxpCol K = P->col[c];
+      const KxpCol K = ld_col(P, c);
       if (K.kind == KXP_K_FIXED && !((seen >> K.field) & 1)) store_col(colp[c], K.width, rec, (uint64_t)K.defv);
     }
   }
@@ -356,7 +381,7 @@ __device__ int thrift_record(const Win& w, const LDS KxProgram* P, void* const L
 template <int NV>
 __device__ void emit_defaults(const LDS KxProgram* P, void* const LDS* colp, uint64_t rec) {
   for (uint32_t c = 0; c < P->ncols; c++) {
-    const KxpCol K = P->col[c];
+    const KxpCol K = ld_col(P, c);
     if (K.kind == KXP_K_FIXED) store_col(colp[c], K.width, rec, (uint64_t)K.defv);
   }
 }
@@ -948,7 +973,7 @@ __global__ void __launch_bounds__(NT) decode_kernel(DecParams dp) {
     for (int v = 0; v < NV; v++) {
       if (v >= (int)P->nvar) break;
       uint32_t c = P->var_col[v];
-      const KxpCol K = P->col[c];
+      const KxpCol K = ld_col(P, c);
       dp.cols.offs[c][r] = (uint32_t)run[v];
       uint32_t n = vs.len[v];
       if (run[v] + n <= dp.cols.cap[c]) {
