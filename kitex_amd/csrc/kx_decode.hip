@@ -18,6 +18,7 @@
 // Known-offsets mode (fastUnmarshal with dataLen) uses the same pipeline with one record per lane.
 // No MFMA anywhere: this is byte movement, bounded by HBM bandwidth.
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 
 #include "kx_internal.h"
 
@@ -44,6 +45,9 @@ constexpr int D_INC_CNT = 11, D_INC_EXIT = 12, D_INC_VAR = 13;
 
 enum Mode { M_THRIFT = 0, M_SKIP = 1 };
 
+// opt-in phase timing (KX_PHASE_TIMING=1): cycles per phase summed over tiles, lane 0 of wave 0
+__device__ unsigned long long g_phase[10];
+
 struct DecParams {
   const uint8_t* in;
   uint64_t in_len;
@@ -60,6 +64,7 @@ struct DecParams {
   unsigned long long* errkey;  // offsets mode: min((record << 8) | code)
   uint32_t* overflow;        // an arena capacity was exceeded
   uint64_t ntiles;
+  int timing;
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -656,6 +661,14 @@ __global__ void __launch_bounds__(NT) decode_kernel(DecParams dp) {
   Shared& S = *reinterpret_cast<Shared*>(smem_raw);
   const int tid = threadIdx.x;
   const bool known = dp.offsets != nullptr;
+  uint64_t tp_last = dp.timing ? __builtin_amdgcn_s_memtime() : 0;
+  auto phase = [&](int k) {
+    if (dp.timing && tid == 0) {
+      uint64_t now = __builtin_amdgcn_s_memtime();
+      atomicAdd(&g_phase[k], (unsigned long long)(now - tp_last));
+      tp_last = now;
+    }
+  };
 
   // ---- tile id in dispatch order (forward progress of the look-back) + program into LDS ----
   if (tid == 0) S.tile_id = atomicAdd(dp.counter, 1u);
@@ -707,6 +720,7 @@ __global__ void __launch_bounds__(NT) decode_kernel(DecParams dp) {
   __syncthreads();
   Win w{dp.in, dp.in_len, wlo, wlen, (const LDS uint32_t*)S.win};
 
+  phase(0);
   // ---- walk 1: speculative entry + measure ----
   uint64_t ent = X_NONE, ex = X_NONE, cnt = 0;
   uint64_t vsum[KXP_NV_MAX];
@@ -782,6 +796,7 @@ __global__ void __launch_bounds__(NT) decode_kernel(DecParams dp) {
   };
   if (!known) walk_measure(ent);
 
+  phase(1);
   // ---- link repair (concatenated mode) ----
   // Every lane must start walking at the first true record start in its segment. Given the exit
   // of the previous walking lane (or the tile's entry `seed`), each lane adopts the position that
@@ -869,6 +884,7 @@ __global__ void __launch_bounds__(NT) decode_kernel(DecParams dp) {
   if (!known) tile_ends(X_NONE);
   __syncthreads();
 
+  phase(2);
   // ---- publish the aggregate, then look back ----
   if (tid == 0 && (known || S.ok)) {
     uint64_t words[3 + KXP_NV_MAX];
@@ -881,6 +897,7 @@ __global__ void __launch_bounds__(NT) decode_kernel(DecParams dp) {
   if (tid < 64) lookback<NV>(dp, S, t, !known);
   __syncthreads();
 
+  phase(3);
   uint64_t E = S.e_in;
   bool terminal = E == X_ERR || E == X_DONE || (!known && S.base_cnt >= dp.n);
   if (!known && !terminal) {
@@ -922,6 +939,7 @@ __global__ void __launch_bounds__(NT) decode_kernel(DecParams dp) {
   }
   __syncthreads();
 
+  phase(4);
   // ---- publish the inclusive prefix ----
   const uint64_t base = S.base_cnt;
   if (tid == 0) {
@@ -958,9 +976,11 @@ __global__ void __launch_bounds__(NT) decode_kernel(DecParams dp) {
   }
   if (!known && terminal) return;
 
+  phase(5);
   // ---- walk 2: re-parse from LDS and scatter ----
   bool live = known || (ent != X_NONE && tid <= S.first_err_lane);
-  if (!live) return;
+  if (!live) goto walk2_done;
+  {
   uint64_t rec = base + cpre;
   uint64_t run[KXP_NV_MAX];
 #pragma unroll
@@ -999,7 +1019,7 @@ __global__ void __launch_bounds__(NT) decode_kernel(DecParams dp) {
 
   if (known) {
     uint64_t r = r0 + tid;
-    if (r >= r1) return;
+    if (r >= r1) goto walk2_done;
     uint64_t a = dp.offsets[r], b = dp.offsets[r + 1];
     VarState<NV> vs;
     uint64_t end;
@@ -1018,10 +1038,10 @@ __global__ void __launch_bounds__(NT) decode_kernel(DecParams dp) {
     if (dp.rstat) dp.rstat[r] = (uint8_t)rc;
     finish_record(vs, r);
     if (r == dp.n - 1) write_final(dp.n, dp.offsets[dp.n]);
-    return;
+    goto walk2_done;
   }
 
-  if (ent == X_NONE) return;
+  if (ent == X_NONE) goto walk2_done;
   uint64_t pos = ent;
   while (pos < seg_hi && pos < dp.in_len && rec < dp.n) {
     VarState<NV> vs;
@@ -1039,7 +1059,7 @@ __global__ void __launch_bounds__(NT) decode_kernel(DecParams dp) {
       st->code = rc; st->record = rec; st->offset = pos;
       write_final(rec, pos);
       if (MODE == M_SKIP) dp.skip_out[rec] = pos;
-      return;
+      goto walk2_done;
     }
     finish_record(vs, rec);
     rec++;
@@ -1048,6 +1068,12 @@ __global__ void __launch_bounds__(NT) decode_kernel(DecParams dp) {
       write_final(dp.n, pos);
       if (MODE == M_SKIP) dp.skip_out[dp.n] = pos;
     }
+  }
+  }
+walk2_done:
+  if (dp.timing) {
+    __syncthreads();
+    phase(6);
   }
 }
 
@@ -1115,6 +1141,15 @@ size_t kx_decode_ws_bytes(const KxProgram&, uint64_t in_len, const uint64_t* off
   return ws_layout(tiles_for(in_len, offsets, n)).total;
 }
 
+// diagnostics (not part of the public ABI): read and reset the phase-timing accumulators
+extern "C" int kx_debug_phase_cycles(unsigned long long* out, int n) {
+  if (n > 10) n = 10;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase), sizeof(unsigned long long) * n) != hipSuccess) return KX_ERR_HIP;
+  unsigned long long z[10] = {0};
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_phase), z, sizeof z) != hipSuccess) return KX_ERR_HIP;
+  return KX_OK;
+}
+
 size_t kx_skip_ws_bytes(uint64_t in_len) { return ws_layout(tiles_for(in_len, nullptr, 0)).total; }
 
 int kx_launch_decode(const KxProgram* dprog, const KxProgram& hprog, const uint8_t* in, uint64_t in_len,
@@ -1122,6 +1157,9 @@ int kx_launch_decode(const KxProgram* dprog, const KxProgram& hprog, const uint8
                      kx_status* status, void* ws, size_t ws_size, hipStream_t stream, bool pb) {
   if (pb) return KX_ERR_NOT_IMPLEMENTED;
   DecParams dp{};
+  static int timing = -1;
+  if (timing < 0) { const char* e = getenv("KX_PHASE_TIMING"); timing = e && e[0] == '1'; }
+  dp.timing = timing;
   dp.in = in; dp.in_len = in_len; dp.offsets = offsets; dp.n = n; dp.prog = dprog;
   dp.cols = cols; dp.rstat = record_status; dp.status = status;
   dp.ntiles = tiles_for(in_len, offsets, n);
