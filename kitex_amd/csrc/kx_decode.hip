@@ -144,7 +144,7 @@ __device__ __forceinline__ uint32_t canon_t(uint32_t t) {
   }
 }
 
-__device__ __noinline__ int dskip(const Win& w, uint64_t& pos, uint64_t limit, uint32_t t0, int md0) {
+__device__ __forceinline__ int dskip_body(const Win& w, uint64_t& pos, uint64_t limit, uint32_t t0, int md0) {
   uint64_t stk[66];
   int sp = 0;
   auto mk = [](uint32_t t, uint32_t md) -> uint64_t { return (uint64_t)(canon_t(t) | (md << 15)); };
@@ -242,6 +242,25 @@ __device__ __noinline__ int dskip(const Win& w, uint64_t& pos, uint64_t limit, u
   return KX_OK;
 }
 
+struct SkipRes {
+  uint64_t pos;
+  int rc;
+};
+
+// (pos is passed and returned by value: a reference would pin the caller's loop-carried position
+// to scratch memory)
+__device__ __noinline__ SkipRes dskip_v(const Win w, uint64_t pos, uint64_t limit, uint32_t t0, int md0) {
+  int rc_ = dskip_body(w, pos, limit, t0, md0);
+  return SkipRes{pos, rc_};
+}
+
+__device__ __forceinline__ int dskip(const Win& w, uint64_t& pos, uint64_t limit, uint32_t t0, int md0) {
+  SkipRes r = dskip_v(w, pos, limit, t0, md0);
+  pos = r.pos;
+  return r.rc;
+}
+
+
 // ---------------------------------------------------------------------------------------------
 // per-record FastRead. EMIT=false: measure (length, var lengths); EMIT=true: also store columns.
 // ---------------------------------------------------------------------------------------------
@@ -294,6 +313,45 @@ __device__ __forceinline__ void store_col(void* base, uint32_t width, uint64_t r
   }
 }
 
+// 12 wire bytes starting at p, byte p in bits 0..7 of w0: one LDS round trip (4 independent
+// ds_read_b32 + v_alignbyte) when the bytes are in the window, global dword loads otherwise.
+struct Fetch {
+  uint32_t w0, w1, w2;
+};
+
+__device__ __forceinline__ Fetch fetch12(const Win& w, uint64_t p) {
+  uint64_t r = (uint64_t)w.in + p - w.wlo;
+  Fetch f;
+  if (r + 16 <= w.wlen) {
+    uint32_t q = (uint32_t)r >> 2, sh = (uint32_t)r & 3;
+    uint32_t x0 = w.lds[q], x1 = w.lds[q + 1], x2 = w.lds[q + 2], x3 = w.lds[q + 3];
+    f.w0 = __builtin_amdgcn_alignbyte(x1, x0, sh);
+    f.w1 = __builtin_amdgcn_alignbyte(x2, x1, sh);
+    f.w2 = __builtin_amdgcn_alignbyte(x3, x2, sh);
+  } else {
+    f.w0 = ld4(w, p);
+    f.w1 = ld4(w, p + 4);
+    f.w2 = ld4(w, p + 8);
+  }
+  return f;
+}
+
+// the field value that follows a 3-byte field header (wire bytes p+3 ...), host order
+__device__ __forceinline__ uint64_t fixed_after_header(const Fetch& f, uint32_t t) {
+  switch (t) {
+    case KX_T_BOOL: return (f.w0 >> 24) == 1 ? 1u : 0u;
+    case KX_T_BYTE: return f.w0 >> 24;
+    case KX_T_I16: return ((f.w0 >> 24) << 8) | (f.w1 & 0xff);
+    case KX_T_I32: return __builtin_bswap32(__builtin_amdgcn_alignbyte(f.w1, f.w0, 3));
+    default:
+      return ((uint64_t)__builtin_bswap32(__builtin_amdgcn_alignbyte(f.w1, f.w0, 3)) << 32) |
+             __builtin_bswap32(__builtin_amdgcn_alignbyte(f.w2, f.w1, 3));
+  }
+}
+
+// One record's FastRead. EMIT=false: measure (length, var lengths); EMIT=true: also store the
+// fixed-width columns as they are parsed. In canonical order every field costs one LDS round trip:
+// the 12 bytes at the cursor and the predicted field descriptor are fetched together.
 template <int NV, bool EMIT>
 __device__ int thrift_record(const Win& w, const LDS KxProgram* P, void* const LDS* colp, uint64_t start,
                              uint64_t limit, uint64_t rec, uint64_t* endp, VarState<NV>& vs,
@@ -307,8 +365,9 @@ __device__ int thrift_record(const Win& w, const LDS KxProgram* P, void* const L
   for (int i = 0; i < NV; i++) { vs.len[i] = 0; vs.pos[i] = 0; }
   for (;;) {
     if (pos >= limit) return KX_ERR_EOF;
-    uint32_t h = ld4(w, pos);
-    uint32_t t = h & 0xff;
+    const Fetch fx = fetch12(w, pos);
+    KxpField F = ld_field(P, pred >= 0 ? pred : 0);
+    const uint32_t t = fx.w0 & 0xff;
     if (t == KX_T_STOP) {
       pos += 1;
       uint64_t rq = P->inst[inst].req_mask;
@@ -319,43 +378,44 @@ __device__ int thrift_record(const Win& w, const LDS KxProgram* P, void* const L
       continue;
     }
     if (limit - pos < 3) return KX_ERR_EOF;
-    int id = (int)(int16_t)((h & 0xff00u) | ((h >> 16) & 0xffu));
-    pos += 3;
+    const int id = (int)(int16_t)((((fx.w0 >> 8) & 0xffu) << 8) | ((fx.w0 >> 16) & 0xffu));
     int fi = -1;
-    if (pred >= 0 && P->f[pred].id == id) {
+    if (pred >= 0 && F.id == id) {
       fi = pred;
     } else {
       int f0 = P->inst[inst].first, nf = P->inst[inst].nfields;
       for (int k = 0; k < nf; k++)
         if (P->f[f0 + k].id == id) { fi = f0 + k; break; }
+      if (fi >= 0) F = ld_field(P, fi);
     }
-    if (fi < 0 || P->f[fi].ttype != t) {                     // default: / mismatched type -> Skip
-      int rc = dskip(w, pos, limit, t, 64);
-      if (rc) return rc;
+    const uint64_t vp = pos + 3;
+    if (fi < 0 || F.ttype != t) {                            // default: / mismatched type -> Skip
+      SkipRes r = dskip_v(w, vp, limit, t, 64);
+      if (r.rc) return r.rc;
+      pos = r.pos;
       continue;
     }
-    const KxpField F = ld_field(P, fi);
     pred = F.enc_next;
     if (F.kind == KXP_K_FIXED) {
-      uint32_t wd = F.width;
-      if (limit - pos < wd) return KX_ERR_EOF;
-      if (EMIT) store_col(colp[F.col], wd, rec, load_scalar(w, pos, t));
-      pos += wd;
+      const uint32_t wd = F.width;
+      if (limit - vp < wd) return KX_ERR_EOF;
+      if (EMIT) store_col(colp[F.col], wd, rec, fixed_after_header(fx, t));
+      pos = vp + wd;
     } else if (F.kind == KXP_K_BYTES) {                      // ReadString (copies)
-      if (limit - pos < 4) return KX_ERR_EOF;
-      int32_t l = (int32_t)be32(w, pos);
+      if (limit - vp < 4) return KX_ERR_EOF;
+      const int32_t l = (int32_t)__builtin_bswap32(__builtin_amdgcn_alignbyte(fx.w1, fx.w0, 3));
       if (l < 0) return KX_ERR_NEGATIVE_SIZE;
-      if (limit - pos - 4 < (uint64_t)l) return KX_ERR_EOF;
-      vset<NV>(vs, F.vslot, pos + 4, (uint32_t)l);
-      pos += 4 + (uint64_t)l;
+      if (limit - vp - 4 < (uint64_t)l) return KX_ERR_EOF;
+      vset<NV>(vs, F.vslot, vp + 4, (uint32_t)l);
+      pos = vp + 4 + (uint64_t)l;
     } else if (F.kind == KXP_K_LIST) {                       // ReadListBegin: elem type ignored
-      if (limit - pos < 5) return KX_ERR_EOF;
-      int32_t l = (int32_t)be32(w, pos + 1);
+      if (limit - vp < 5) return KX_ERR_EOF;
+      const int32_t l = (int32_t)__builtin_bswap32(fx.w1);
       if (l < 0) return KX_ERR_NEGATIVE_SIZE;
-      uint64_t b = (uint64_t)l * F.width;
-      if (limit - pos - 5 < b) return KX_ERR_EOF;
-      vset<NV>(vs, F.vslot, pos + 5, (uint32_t)l);
-      pos += 5 + b;
+      const uint64_t b = (uint64_t)l * F.width;
+      if (limit - vp - 5 < b) return KX_ERR_EOF;
+      vset<NV>(vs, F.vslot, vp + 5, (uint32_t)l);
+      pos = vp + 5 + b;
     } else {                                                 // nested struct: NewX() + FastRead
       const KxpInst C = ld_inst(P, F.child);
       seen &= ~C.subtree_mask;
@@ -367,6 +427,7 @@ __device__ int thrift_record(const Win& w, const LDS KxProgram* P, void* const L
       if (F.pbit >= 0) pres |= 1ull << F.pbit;
       inst = F.child;
       pred = C.enc_first;
+      pos = vp;
       continue;
     }
     seen |= 1ull << fi;
@@ -392,11 +453,10 @@ __device__ void emit_defaults(const LDS KxProgram* P, void* const LDS* colp, uin
 }
 
 // copy one var field payload (n units of `width` bytes) from the input to its arena
-__device__ void copy_var(const Win& w, const KxpCol& K, uint64_t src, uint32_t n, uint8_t* dst_) {
+__device__ void copy_var_slow(const Win& w, const KxpCol& K, uint64_t src, uint32_t n, uint8_t* dst_) {
   GLB uint8_t* dst = (GLB uint8_t*)dst_;
   if (K.kind == KXP_K_BYTES) {
     uint32_t i = 0;
-    // bytes until the destination is 4-aligned, then dwords, then the tail
     while (i < n && (((uintptr_t)(dst_ + i)) & 3)) { dst[i] = (uint8_t)ld1(w, src + i); i++; }
     for (; i + 4 <= n; i += 4) *(GLB uint32_t*)(dst + i) = ld4(w, src + i);
     for (; i < n; i++) dst[i] = (uint8_t)ld1(w, src + i);
@@ -421,6 +481,68 @@ __device__ void copy_var(const Win& w, const KxpCol& K, uint64_t src, uint32_t n
     default:
       for (uint32_t i = 0; i < n; i++) ((GLB uint64_t*)dst)[i] = be64(w, src + 8ull * i);
       break;
+  }
+}
+
+// Fast path: the payload is inside the LDS window. 16 output bytes per step: 5 independent LDS
+// dwords, v_alignbyte to the source skew, byte swap for big-endian elements, one 16-byte store
+// when the destination allows it.
+__device__ void copy_var(const Win& w, const KxpCol& K, uint64_t src, uint32_t n, uint8_t* dst_) {
+  const uint64_t nbytes = (uint64_t)n * K.width;
+  const uint64_t r = (uint64_t)w.in + src - w.wlo;
+  const bool bswap = K.kind == KXP_K_LIST && K.width > 1;
+  if (r + nbytes + 20 > w.wlen || (K.kind == KXP_K_LIST && K.elem == KX_T_BOOL)) {
+    copy_var_slow(w, K, src, n, dst_);
+    return;
+  }
+  GLB uint8_t* dst = (GLB uint8_t*)dst_;
+  uint32_t i = 0;
+  if (!bswap) {
+    while (i < nbytes && (((uintptr_t)(dst_ + i)) & 15)) {
+      dst[i] = ((const LDS uint8_t*)w.lds)[r + i];
+      i++;
+    }
+  } else if (((uintptr_t)dst_) & 3) {
+    copy_var_slow(w, K, src, n, dst_);
+    return;
+  }
+  const bool a16 = ((((uintptr_t)dst_) + i) & 15) == 0;
+  const uint32_t sh = (uint32_t)((r + i) & 3);
+  uint32_t q = (uint32_t)((r + i) >> 2);
+  for (; i + 16 <= nbytes; i += 16, q += 4) {
+    uint32_t x0 = w.lds[q], x1 = w.lds[q + 1], x2 = w.lds[q + 2], x3 = w.lds[q + 3], x4 = w.lds[q + 4];
+    uint32_t a0 = __builtin_amdgcn_alignbyte(x1, x0, sh), a1 = __builtin_amdgcn_alignbyte(x2, x1, sh);
+    uint32_t a2 = __builtin_amdgcn_alignbyte(x3, x2, sh), a3 = __builtin_amdgcn_alignbyte(x4, x3, sh);
+    if (bswap) {
+      if (K.width == 8) {
+        uint32_t t0 = __builtin_bswap32(a1), t1 = __builtin_bswap32(a0);
+        uint32_t t2 = __builtin_bswap32(a3), t3 = __builtin_bswap32(a2);
+        a0 = t0; a1 = t1; a2 = t2; a3 = t3;
+      } else if (K.width == 4) {
+        a0 = __builtin_bswap32(a0); a1 = __builtin_bswap32(a1);
+        a2 = __builtin_bswap32(a2); a3 = __builtin_bswap32(a3);
+      } else {
+        a0 = __builtin_amdgcn_perm(a0, a0, 0x02030001u); a1 = __builtin_amdgcn_perm(a1, a1, 0x02030001u);
+        a2 = __builtin_amdgcn_perm(a2, a2, 0x02030001u); a3 = __builtin_amdgcn_perm(a3, a3, 0x02030001u);
+      }
+    }
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    if (a16) {
+      v4u v = {a0, a1, a2, a3};
+      *(GLB v4u*)(dst + i) = v;
+    } else {
+      GLB uint32_t* d32 = (GLB uint32_t*)(dst + i);
+      d32[0] = a0; d32[1] = a1; d32[2] = a2; d32[3] = a3;
+    }
+  }
+  if (i < nbytes) {
+    if (bswap) {
+      copy_var_slow(w, K, src + i, (uint32_t)((nbytes - i) / K.width), dst_ + i);
+    } else {
+      for (; i + 4 <= nbytes; i += 4, q++)
+        *(GLB uint32_t*)(dst + i) = __builtin_amdgcn_alignbyte(w.lds[q + 1], w.lds[q], sh);
+      for (; i < nbytes; i++) dst[i] = ((const LDS uint8_t*)w.lds)[r + i];
+    }
   }
 }
 
