@@ -77,6 +77,9 @@ struct Win {
   uint64_t wlo;        // absolute address of LDS byte 0 (16-aligned)
   uint32_t wlen;       // bytes valid in LDS
   const LDS uint32_t* lds;
+  const KxpStep* steps;  // canonical plan (global memory; uniform index -> scalar loads)
+  uint32_t nsteps;
+  uint64_t canon_pres;
 };
 
 __device__ __forceinline__ uint32_t gld4(const Win& w, uint64_t p) {
@@ -349,6 +352,51 @@ __device__ __forceinline__ uint64_t fixed_after_header(const Fetch& f, uint32_t 
   }
 }
 
+// Canonical fast path: the record is checked against the schema's canonical plan (header bytes in
+// encoder order, STOP bytes) step by step; the step is wave-uniform, so the only divergence is a
+// lane whose record deviates, which returns false and is re-parsed by the generic loop below.
+template <int NV, bool EMIT>
+__device__ __forceinline__ bool canon_record(const Win& w, void* const LDS* colp, uint64_t start, uint64_t limit,
+                                             uint64_t rec, uint64_t* endp, VarState<NV>& vs, uint64_t& pres) {
+  uint64_t pos = start;
+  const KxpStep* __restrict__ steps = w.steps;
+  for (uint32_t k = 0; k < w.nsteps; k++) {
+    const KxpStep st = steps[k];
+    const uint64_t rem = limit - pos;
+    const Fetch fx = fetch12(w, pos);
+    if (st.kind == KXP_S_END) {
+      if (rem < 1 || (fx.w0 & 0xff) != KX_T_STOP) return false;
+      pos += 1;
+      continue;
+    }
+    if (rem < 3 || (fx.w0 & 0xffffffu) != st.hdr) return false;
+    const uint64_t vp = pos + 3, vrem = rem - 3;
+    if (st.kind == KXP_S_FIXED) {
+      if (vrem < st.width) return false;
+      if (EMIT) store_col(colp[st.col], st.width, rec, fixed_after_header(fx, st.hdr & 0xff));
+      pos = vp + st.width;
+    } else if (st.kind == KXP_S_BYTES) {
+      if (vrem < 4) return false;
+      const int32_t l = (int32_t)__builtin_bswap32(__builtin_amdgcn_alignbyte(fx.w1, fx.w0, 3));
+      if (l < 0 || vrem - 4 < (uint64_t)l) return false;
+      vset<NV>(vs, st.vslot, vp + 4, (uint32_t)l);
+      pos = vp + 4 + (uint64_t)l;
+    } else if (st.kind == KXP_S_LIST) {
+      if (vrem < 5) return false;
+      const int32_t l = (int32_t)__builtin_bswap32(fx.w1);
+      const uint64_t b = (uint64_t)(l < 0 ? 0 : l) * st.width;
+      if (l < 0 || vrem - 5 < b) return false;
+      vset<NV>(vs, st.vslot, vp + 5, (uint32_t)l);
+      pos = vp + 5 + b;
+    } else {  // KXP_S_STRUCT: header only, its fields follow
+      pos = vp;
+    }
+  }
+  pres = w.canon_pres;
+  *endp = pos;
+  return true;
+}
+
 // One record's FastRead. EMIT=false: measure (length, var lengths); EMIT=true: also store the
 // fixed-width columns as they are parsed. In canonical order every field costs one LDS round trip:
 // the 12 bytes at the cursor and the predicted field descriptor are fetched together.
@@ -356,13 +404,16 @@ template <int NV, bool EMIT>
 __device__ int thrift_record(const Win& w, const LDS KxProgram* P, void* const LDS* colp, uint64_t start,
                              uint64_t limit, uint64_t rec, uint64_t* endp, VarState<NV>& vs,
                              uint64_t& pres) {
+#pragma unroll
+  for (int i = 0; i < NV; i++) { vs.len[i] = 0; vs.pos[i] = 0; }
+  if (w.nsteps && canon_record<NV, EMIT>(w, colp, start, limit, rec, endp, vs, pres)) return KX_OK;
+#pragma unroll
+  for (int i = 0; i < NV; i++) { vs.len[i] = 0; vs.pos[i] = 0; }
   uint64_t pos = start;
   int inst = 0;
   int pred = P->inst[0].enc_first;
   uint64_t seen = 0;
   pres = 0;
-#pragma unroll
-  for (int i = 0; i < NV; i++) { vs.len[i] = 0; vs.pos[i] = 0; }
   for (;;) {
     if (pos >= limit) return KX_ERR_EOF;
     const Fetch fx = fetch12(w, pos);
@@ -840,7 +891,9 @@ __global__ void __launch_bounds__(NT) decode_kernel(DecParams dp) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
-  Win w{dp.in, dp.in_len, wlo, wlen, (const LDS uint32_t*)S.win};
+  Win w{dp.in, dp.in_len, wlo, wlen, (const LDS uint32_t*)S.win,
+        MODE == M_THRIFT ? dp.prog->steps : nullptr, MODE == M_THRIFT ? dp.prog->nsteps : 0u,
+        MODE == M_THRIFT ? dp.prog->canon_pres : 0ull};
 
   phase(0);
   // ---- walk 1: speculative entry + measure ----

@@ -64,6 +64,20 @@ struct KxpCol {        // 16 B
   int64_t defv;        // FIXED default (bits)
 };
 
+// Canonical plan: the byte layout every record written by the encoder has (encoder order, all
+// non-optional fields present, nil-free structs). Executed as a straight line of steps; a record
+// that deviates at any step is re-parsed by the generic field loop.
+enum : uint8_t { KXP_S_FIXED = 1, KXP_S_BYTES = 2, KXP_S_LIST = 3, KXP_S_STRUCT = 4, KXP_S_END = 5 };
+#define KXP_MAX_STEPS 96
+
+struct KxpStep {       // 8 B
+  uint32_t hdr;        // expected field header bytes: ttype | id_hi << 8 | id_lo << 16
+  uint8_t kind;        // KXP_S_*
+  uint8_t width;       // FIXED value width / LIST element width
+  int8_t col;          // FIXED: column
+  uint8_t vslot;       // BYTES / LIST: var slot
+};
+
 struct KxProgram {
   KxpField f[KXP_MAX_FIELDS];
   KxpInst inst[KXP_MAX_INST];
@@ -75,9 +89,14 @@ struct KxProgram {
   uint32_t is_pb;
   uint8_t var_col[KXP_NV_MAX];  // var slot -> column
   uint64_t fixed_min;    // minimum encoded record size (optional unset, var empty)
-  uint64_t pad[3];
+  uint32_t nsteps;       // canonical plan length, 0 = no canonical fast path
+  uint32_t pad0;
+  uint64_t canon_pres;   // presence word of a canonical record
+  uint64_t pad[1];
+  KxpStep steps[KXP_MAX_STEPS];
 };
 
 static_assert(sizeof(KxpField) == 16, "KxpField layout");
 static_assert(sizeof(KxpInst) == 32, "KxpInst layout");
 static_assert(sizeof(KxpCol) == 16, "KxpCol layout");
+static_assert(sizeof(KxpStep) == 8, "KxpStep layout");

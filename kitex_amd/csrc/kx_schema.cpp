@@ -254,6 +254,45 @@ int kx_build_program(const kx_struct_desc* structs, uint32_t nstructs, kx_schema
     else mn += 1;
   }
   P.fixed_min = mn;
+
+  // canonical plan: depth-first in encoder order; any optional field disables the fast path
+  // (its presence varies per record), as does a plan longer than KXP_MAX_STEPS
+  struct PlanB {
+    KxProgram& P;
+    bool ok = true;
+    uint32_t n = 0;
+    uint64_t pres = 0;
+    void push(const KxpStep& st) {
+      if (n >= KXP_MAX_STEPS) { ok = false; return; }
+      P.steps[n++] = st;
+    }
+    void inst(int i) {
+      const KxpInst& I = P.inst[i];
+      for (int f = I.enc_first; f >= 0; f = P.f[f].enc_next) {
+        const KxpField& F = P.f[f];
+        if (F.req == KX_REQ_OPTIONAL) { ok = false; return; }
+        KxpStep st{};
+        st.hdr = (uint32_t)F.ttype | ((uint32_t)((uint16_t)F.id >> 8) << 8) | ((uint32_t)(F.id & 0xff) << 16);
+        st.col = F.col;
+        st.vslot = F.vslot;
+        st.width = F.width;
+        if (F.pbit >= 0) pres |= 1ull << F.pbit;
+        if (F.kind == KXP_K_FIXED) st.kind = KXP_S_FIXED;
+        else if (F.kind == KXP_K_BYTES) st.kind = KXP_S_BYTES;
+        else if (F.kind == KXP_K_LIST) st.kind = KXP_S_LIST;
+        else st.kind = KXP_S_STRUCT;
+        push(st);
+        if (F.kind == KXP_K_STRUCT) inst(F.child);
+        if (!ok) return;
+      }
+      KxpStep end{};
+      end.kind = KXP_S_END;
+      push(end);
+    }
+  } pb{P};
+  pb.inst(0);
+  P.nsteps = pb.ok ? pb.n : 0;
+  P.canon_pres = pb.pres;
   s->ncols = P.ncols;
   return KX_OK;
 }
