@@ -65,6 +65,7 @@ struct DecParams {
   uint32_t* overflow;        // an arena capacity was exceeded
   uint64_t ntiles;
   int timing;
+  int ablate;   // diagnostics only (KX_ABLATE): 1 no walk2, 2 no var copies, 4 walk2 without stores, 8 no walk1
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -1154,7 +1155,7 @@ __global__ void __launch_bounds__(NT) decode_kernel(DecParams dp) {
   phase(5);
   // ---- walk 2: re-parse from LDS and scatter ----
   bool live = known || (ent != X_NONE && tid <= S.first_err_lane);
-  if (!live) goto walk2_done;
+  if (!live || (dp.ablate & 1)) goto walk2_done;
   {
   uint64_t rec = base + cpre;
   uint64_t run[KXP_NV_MAX];
@@ -1172,7 +1173,7 @@ __global__ void __launch_bounds__(NT) decode_kernel(DecParams dp) {
       dp.cols.offs[c][r] = (uint32_t)run[v];
       uint32_t n = vs.len[v];
       if (run[v] + n <= dp.cols.cap[c]) {
-        if (n) copy_var(w, K, vs.pos[v], n, (uint8_t*)colp[c] + run[v] * K.width);
+        if (n && !(dp.ablate & 2)) copy_var(w, K, vs.pos[v], n, (uint8_t*)colp[c] + run[v] * K.width);
       } else {
         atomicOr(dp.overflow, 1u);
       }
@@ -1222,7 +1223,10 @@ __global__ void __launch_bounds__(NT) decode_kernel(DecParams dp) {
     VarState<NV> vs;
     uint64_t end;
     int rc;
-    if (MODE == M_THRIFT) rc = thrift_record<NV, true>(w, P, colp, pos, dp.in_len, rec, &end, vs, pres);
+    if (MODE == M_THRIFT) {
+      if (dp.ablate & 4) rc = thrift_record<NV, false>(w, P, colp, pos, dp.in_len, rec, &end, vs, pres);
+      else rc = thrift_record<NV, true>(w, P, colp, pos, dp.in_len, rec, &end, vs, pres);
+    }
     else {
       end = pos;
       rc = dskip(w, end, dp.in_len, KX_T_STRUCT, 64);
@@ -1332,9 +1336,11 @@ int kx_launch_decode(const KxProgram* dprog, const KxProgram& hprog, const uint8
                      kx_status* status, void* ws, size_t ws_size, hipStream_t stream, bool pb) {
   if (pb) return KX_ERR_NOT_IMPLEMENTED;
   DecParams dp{};
-  static int timing = -1;
+  static int timing = -1, ablate = -1;
   if (timing < 0) { const char* e = getenv("KX_PHASE_TIMING"); timing = e && e[0] == '1'; }
+  if (ablate < 0) { const char* e = getenv("KX_ABLATE"); ablate = e ? atoi(e) : 0; }
   dp.timing = timing;
+  dp.ablate = ablate;
   dp.in = in; dp.in_len = in_len; dp.offsets = offsets; dp.n = n; dp.prog = dprog;
   dp.cols = cols; dp.rstat = record_status; dp.status = status;
   dp.ntiles = tiles_for(in_len, offsets, n);
