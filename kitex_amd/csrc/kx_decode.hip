@@ -340,6 +340,17 @@ __device__ __forceinline__ Fetch fetch12(const Win& w, uint64_t p) {
   return f;
 }
 
+// fetch12 for a window byte offset already known to be inside the window (no branch)
+__device__ __forceinline__ Fetch fetch12_lds(const Win& w, uint32_t r) {
+  uint32_t q = r >> 2, sh = r & 3;
+  uint32_t x0 = w.lds[q], x1 = w.lds[q + 1], x2 = w.lds[q + 2], x3 = w.lds[q + 3];
+  Fetch f;
+  f.w0 = __builtin_amdgcn_alignbyte(x1, x0, sh);
+  f.w1 = __builtin_amdgcn_alignbyte(x2, x1, sh);
+  f.w2 = __builtin_amdgcn_alignbyte(x3, x2, sh);
+  return f;
+}
+
 // the field value that follows a 3-byte field header (wire bytes p+3 ...), host order
 __device__ __forceinline__ uint64_t fixed_after_header(const Fetch& f, uint32_t t) {
   switch (t) {
@@ -361,22 +372,58 @@ __device__ __forceinline__ bool canon_record(const Win& w, void* const LDS* colp
                                              uint64_t rec, uint64_t* endp, VarState<NV>& vs, uint64_t& pres) {
   uint64_t pos = start;
   const KxpStep* __restrict__ steps = w.steps;
-  for (uint32_t k = 0; k < w.nsteps; k++) {
+  uint32_t k = 0;
+  while (k < w.nsteps) {
     const KxpStep st = steps[k];
     const uint64_t rem = limit - pos;
+    if (st.kind == KXP_S_FIXED) {
+      // up to 4 consecutive fixed-width fields: positions are known without waiting for data, so
+      // all their bytes are fetched in one LDS round trip
+      const uint32_t m = min(st.hdr >> 24, 4u);
+      const KxpStep s1 = steps[k + (m > 1 ? 1 : 0)];
+      const KxpStep s2 = steps[k + (m > 2 ? 2 : 0)];
+      const KxpStep s3 = steps[k + (m > 3 ? 3 : 0)];
+      const uint32_t o1 = 3 + st.width, o2 = o1 + 3 + s1.width, o3 = o2 + 3 + s2.width;
+      const uint32_t len = m == 1 ? o1 : m == 2 ? o2 : m == 3 ? o3 : o3 + 3 + s3.width;
+      if (rem < len) return false;
+      const uint64_t r = (uint64_t)w.in + pos - w.wlo;
+      Fetch f0, f1, f2, f3;
+      if (r + o3 + 16 <= w.wlen) {
+        f0 = fetch12_lds(w, (uint32_t)r);
+        f1 = fetch12_lds(w, (uint32_t)r + o1);
+        f2 = fetch12_lds(w, (uint32_t)r + o2);
+        f3 = fetch12_lds(w, (uint32_t)r + o3);
+      } else {
+        f0 = fetch12(w, pos);
+        f1 = fetch12(w, pos + o1);
+        f2 = fetch12(w, pos + o2);
+        f3 = fetch12(w, pos + o3);
+      }
+      bool ok = (f0.w0 & 0xffffffu) == (st.hdr & 0xffffffu);
+      if (m > 1) ok &= (f1.w0 & 0xffffffu) == (s1.hdr & 0xffffffu);
+      if (m > 2) ok &= (f2.w0 & 0xffffffu) == (s2.hdr & 0xffffffu);
+      if (m > 3) ok &= (f3.w0 & 0xffffffu) == (s3.hdr & 0xffffffu);
+      if (!ok) return false;
+      if (EMIT) {
+        store_col(colp[st.col], st.width, rec, fixed_after_header(f0, st.hdr & 0xff));
+        if (m > 1) store_col(colp[s1.col], s1.width, rec, fixed_after_header(f1, s1.hdr & 0xff));
+        if (m > 2) store_col(colp[s2.col], s2.width, rec, fixed_after_header(f2, s2.hdr & 0xff));
+        if (m > 3) store_col(colp[s3.col], s3.width, rec, fixed_after_header(f3, s3.hdr & 0xff));
+      }
+      pos += len;
+      k += m;
+      continue;
+    }
     const Fetch fx = fetch12(w, pos);
+    k++;
     if (st.kind == KXP_S_END) {
       if (rem < 1 || (fx.w0 & 0xff) != KX_T_STOP) return false;
       pos += 1;
       continue;
     }
-    if (rem < 3 || (fx.w0 & 0xffffffu) != st.hdr) return false;
+    if (rem < 3 || (fx.w0 & 0xffffffu) != (st.hdr & 0xffffffu)) return false;
     const uint64_t vp = pos + 3, vrem = rem - 3;
-    if (st.kind == KXP_S_FIXED) {
-      if (vrem < st.width) return false;
-      if (EMIT) store_col(colp[st.col], st.width, rec, fixed_after_header(fx, st.hdr & 0xff));
-      pos = vp + st.width;
-    } else if (st.kind == KXP_S_BYTES) {
+    if (st.kind == KXP_S_BYTES) {
       if (vrem < 4) return false;
       const int32_t l = (int32_t)__builtin_bswap32(__builtin_amdgcn_alignbyte(fx.w1, fx.w0, 3));
       if (l < 0 || vrem - 4 < (uint64_t)l) return false;
@@ -596,6 +643,44 @@ __device__ void copy_var(const Win& w, const KxpCol& K, uint64_t src, uint32_t n
       for (; i < nbytes; i++) dst[i] = ((const LDS uint8_t*)w.lds)[r + i];
     }
   }
+}
+
+
+// First canonical record signature (3 bytes) in a lane's 128-byte segment: the segment (plus the
+// 2 bytes a match may straddle) is read with 9 x ds_read_b128 + 1 x ds_read_b32 in one round trip
+// and searched in registers, byte-equality SWAR on the first signature byte.
+__device__ __forceinline__ uint64_t scan_segment(const LDS uint32_t* win, uint32_t r0w, uint64_t seg_lo,
+                                                 uint64_t plim, uint32_t sig) {
+  typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+  const uint32_t skew = r0w & 15;
+  const LDS v4u* src = (const LDS v4u*)(win + ((r0w & ~15u) >> 2));
+  uint32_t d[37];
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    v4u v = src[i];
+    d[4 * i] = v.x; d[4 * i + 1] = v.y; d[4 * i + 2] = v.z; d[4 * i + 3] = v.w;
+  }
+  d[36] = ((const LDS uint32_t*)src)[36];
+  const uint64_t base = seg_lo - skew;  // input position of d[0] byte 0
+  const uint32_t b0 = (sig & 0xff) * 0x01010101u;
+  uint64_t found = ~0ull - 2;
+  bool done = false;
+#pragma unroll
+  for (int i = 0; i < 36; i++) {
+    const uint32_t t = d[i] ^ b0;
+    uint32_t z = (t - 0x01010101u) & ~t & 0x80808080u;   // bytes equal to the first sig byte
+    if (!done && z) {
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const uint64_t pp = base + 4 * i + j;
+        if (!done && pp >= seg_lo && pp < plim && (__builtin_amdgcn_alignbyte(d[i + 1], d[i], j) & 0xffffffu) == sig) {
+          found = pp;
+          done = true;
+        }
+      }
+    }
+  }
+  return found;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -931,22 +1016,26 @@ __global__ void __launch_bounds__(NT) decode_kernel(DecParams dp) {
       const uint32_t sig = MODE == M_THRIFT ? P->sig : (uint32_t)KX_T_STOP;
       const uint32_t smask = (MODE == M_THRIFT && P->sig_len == 3) ? 0xffffffu : 0xffu;
       const uint64_t slen = (MODE == M_THRIFT && P->sig_len == 3) ? 3 : 1;
-      // one LDS dword per 4 candidate positions (the segment lies inside the LDS window)
       const uint64_t plim = min(seg_hi, dp.in_len >= slen ? dp.in_len - slen + 1 : 0ull);
       const uint64_t r0w = abs_in + seg_lo - wlo;   // window byte of seg_lo
-      uint32_t q = (uint32_t)(r0w >> 2);
-      uint64_t pbase = seg_lo - (r0w & 3);          // input position of window byte 4q
-      uint32_t x0 = S.win[q];
-      for (; pbase < plim; pbase += 4, q++) {
-        const uint32_t x1 = S.win[q + 1];
-        uint32_t hit = 0;
+      if (slen == 3 && seg_hi - seg_lo == SEG) {
+        ent = scan_segment((const LDS uint32_t*)S.win, (uint32_t)r0w, seg_lo, plim, sig);
+      } else {
+        // short (last) segment or 1-byte signature: dword-at-a-time
+        uint32_t q = (uint32_t)(r0w >> 2);
+        uint64_t pbase = seg_lo - (r0w & 3);          // input position of window byte 4q
+        uint32_t x0 = S.win[q];
+        for (; pbase < plim; pbase += 4, q++) {
+          const uint32_t x1 = S.win[q + 1];
+          uint32_t hit = 0;
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-          const uint64_t pp = pbase + j;
-          if (pp >= seg_lo && pp < plim && (__builtin_amdgcn_alignbyte(x1, x0, j) & smask) == sig) hit |= 1u << j;
+          for (int j = 0; j < 4; j++) {
+            const uint64_t pp = pbase + j;
+            if (pp >= seg_lo && pp < plim && (__builtin_amdgcn_alignbyte(x1, x0, j) & smask) == sig) hit |= 1u << j;
+          }
+          if (hit) { ent = pbase + __builtin_ctz(hit); break; }
+          x0 = x1;
         }
-        if (hit) { ent = pbase + __builtin_ctz(hit); break; }
-        x0 = x1;
       }
     }
   }

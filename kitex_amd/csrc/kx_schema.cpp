@@ -292,6 +292,14 @@ int kx_build_program(const kx_struct_desc* structs, uint32_t nstructs, kx_schema
   } pb{P};
   pb.inst(0);
   P.nsteps = pb.ok ? pb.n : 0;
+  // top header byte of a FIXED step = length of the run of consecutive FIXED steps starting there
+  for (int k = (int)P.nsteps - 1; k >= 0; k--) {
+    if (P.steps[k].kind != KXP_S_FIXED) continue;
+    uint32_t run = 1;
+    if (k + 1 < (int)P.nsteps && P.steps[k + 1].kind == KXP_S_FIXED) run += P.steps[k + 1].hdr >> 24;
+    if (run > 255) run = 255;
+    P.steps[k].hdr = (P.steps[k].hdr & 0xffffffu) | (run << 24);
+  }
   P.canon_pres = pb.pres;
   s->ncols = P.ncols;
   return KX_OK;
