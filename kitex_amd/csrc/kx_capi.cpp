@@ -27,17 +27,42 @@ int prog_on_device(kx_schema* s, int dev, KxProgram** out) {
   return KX_OK;
 }
 
-int ensure_ws(kx_ctx* c, size_t bytes, hipStream_t stream) {
-  if (c->ws_size >= bytes) return KX_OK;
-  if (c->ws) {
-    KX_HIP_CHECK(hipStreamSynchronize(stream));  // the old workspace may still be in use
-    KX_HIP_CHECK(hipFree(c->ws));
-    c->ws = nullptr;
-    c->ws_size = 0;
+// Decode workspace: grown on demand, zeroed at allocation (tile counter 0, overflow 0, no
+// descriptor word carries a live epoch) with the error key at ~0. Returns the epoch for this call.
+int ensure_ws(kx_ctx* c, size_t bytes, hipStream_t stream, uint64_t* epoch) {
+  if (c->ws_size < bytes) {
+    if (c->ws) {
+      KX_HIP_CHECK(hipStreamSynchronize(stream));  // the old workspace may still be in use
+      KX_HIP_CHECK(hipFree(c->ws));
+      c->ws = nullptr;
+      c->ws_size = 0;
+    }
+    size_t sz = bytes < (1u << 20) ? (1u << 20) : bytes + bytes / 4;
+    KX_HIP_CHECK(hipMalloc(&c->ws, sz));
+    c->ws_size = sz;
+    c->epoch = 0xffff;  // forces the re-initialisation below
+  }
+  if (++c->epoch > 0xffff) {
+    // first use or epoch wrap: clear every descriptor word so no stale tag can match
+    KX_HIP_CHECK(hipMemsetAsync(c->ws, 0, c->ws_size, stream));
+    KX_HIP_CHECK(hipMemsetAsync((char*)c->ws + 8, 0xff, 8, stream));
+    c->epoch = 1;
+  }
+  *epoch = c->epoch;
+  return KX_OK;
+}
+
+int ensure_ews(kx_ctx* c, size_t bytes, hipStream_t stream) {
+  if (c->ews_size >= bytes) return KX_OK;
+  if (c->ews) {
+    KX_HIP_CHECK(hipStreamSynchronize(stream));
+    KX_HIP_CHECK(hipFree(c->ews));
+    c->ews = nullptr;
+    c->ews_size = 0;
   }
   size_t sz = bytes < (1u << 20) ? (1u << 20) : bytes + bytes / 4;
-  KX_HIP_CHECK(hipMalloc(&c->ws, sz));
-  c->ws_size = sz;
+  KX_HIP_CHECK(hipMalloc(&c->ews, sz));
+  c->ews_size = sz;
   return KX_OK;
 }
 
@@ -127,6 +152,15 @@ uint32_t kx_schema_presence_bits(const kx_schema* s) { return s ? s->npres : 0; 
 
 uint64_t kx_schema_min_record_size(const kx_schema* s) { return s ? s->prog.fixed_min : 0; }
 
+// diagnostics (not part of the public ABI): the decode workspace of a ctx and its current epoch
+int kx_debug_workspace(kx_ctx* c, void** ptr, size_t* size, uint64_t* epoch) {
+  if (!c || !ptr || !size || !epoch) return KX_ERR_INVALID_ARG;
+  *ptr = c->ws;
+  *size = c->ws_size;
+  *epoch = c->epoch;
+  return KX_OK;
+}
+
 int kx_ctx_create(int device, kx_ctx** out) {
   if (!out) return KX_ERR_INVALID_ARG;
   *out = nullptr;
@@ -144,6 +178,7 @@ void kx_ctx_destroy(kx_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->ws) (void)hipFree(c->ws);
+  if (c->ews) (void)hipFree(c->ews);
   if (c->pin) (void)hipHostFree(c->pin);
   delete c;
 }
@@ -166,9 +201,10 @@ int kx_thrift_decode_batch(kx_ctx* c, const kx_schema* s, const uint8_t* in, uin
   KxProgram* dp = nullptr;
   if ((rc = prog_on_device(const_cast<kx_schema*>(s), c->device, &dp))) return rc;
   size_t ws = kx_decode_ws_bytes(s->prog, in_len, offsets, n);
-  if ((rc = ensure_ws(c, ws, st))) return rc;
+  uint64_t epoch = 0;
+  if ((rc = ensure_ws(c, ws, st, &epoch))) return rc;
   return kx_launch_decode(dp, s->prog, in, in_len, offsets, n, lc, record_status, status, c->ws, c->ws_size,
-                          st, false);
+                          epoch, st, false);
 }
 
 int kx_thrift_skip_batch(kx_ctx* c, const uint8_t* in, uint64_t in_len, uint64_t n, uint64_t* offsets_out,
@@ -182,8 +218,9 @@ int kx_thrift_skip_batch(kx_ctx* c, const uint8_t* in, uint64_t in_len, uint64_t
     KX_HIP_CHECK(hipMemsetAsync(offsets_out, 0, 8, st));
     return KX_OK;
   }
-  if ((rc = ensure_ws(c, kx_skip_ws_bytes(in_len), st))) return rc;
-  return kx_launch_skip(in, in_len, n, offsets_out, status, c->ws, c->ws_size, st);
+  uint64_t epoch = 0;
+  if ((rc = ensure_ws(c, kx_skip_ws_bytes(in_len), st, &epoch))) return rc;
+  return kx_launch_skip(in, in_len, n, offsets_out, status, c->ws, c->ws_size, epoch, st);
 }
 
 int kx_thrift_encoded_size_batch(kx_ctx* c, const kx_schema* s, const kx_columns* in, uint64_t n,
@@ -197,8 +234,8 @@ int kx_thrift_encoded_size_batch(kx_ctx* c, const kx_schema* s, const kx_columns
   if (n == 0) return KX_OK;
   KxProgram* dp = nullptr;
   if ((rc = prog_on_device(const_cast<kx_schema*>(s), c->device, &dp))) return rc;
-  if ((rc = ensure_ws(c, kx_encode_ws_bytes(n), st))) return rc;
-  return kx_launch_encode(dp, s->prog, lc, n, nullptr, 0, sizes_out, nullptr, nullptr, c->ws, c->ws_size, st,
+  if ((rc = ensure_ews(c, kx_encode_ws_bytes(n), st))) return rc;
+  return kx_launch_encode(dp, s->prog, lc, n, nullptr, 0, sizes_out, nullptr, nullptr, c->ews, c->ews_size, st,
                           true);
 }
 
@@ -217,8 +254,8 @@ int kx_thrift_encode_batch(kx_ctx* c, const kx_schema* s, const kx_columns* in, 
   }
   KxProgram* dp = nullptr;
   if ((rc = prog_on_device(const_cast<kx_schema*>(s), c->device, &dp))) return rc;
-  if ((rc = ensure_ws(c, kx_encode_ws_bytes(n), st))) return rc;
-  return kx_launch_encode(dp, s->prog, lc, n, out, out_cap, nullptr, offsets_out, status, c->ws, c->ws_size,
+  if ((rc = ensure_ews(c, kx_encode_ws_bytes(n), st))) return rc;
+  return kx_launch_encode(dp, s->prog, lc, n, out, out_cap, nullptr, offsets_out, status, c->ews, c->ews_size,
                           st, false);
 }
 
@@ -242,9 +279,10 @@ int kx_pb_decode_batch(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_
   KxProgram* dp = nullptr;
   if ((rc = prog_on_device(const_cast<kx_schema*>(s), c->device, &dp))) return rc;
   size_t ws = kx_decode_ws_bytes(s->prog, in_len, offsets, n);
-  if ((rc = ensure_ws(c, ws, st))) return rc;
+  uint64_t epoch = 0;
+  if ((rc = ensure_ws(c, ws, st, &epoch))) return rc;
   return kx_launch_decode(dp, s->prog, in, in_len, offsets, n, lc, record_status, status, c->ws, c->ws_size,
-                          st, true);
+                          epoch, st, true);
 }
 
 int kx_host_decode_batch(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len,

@@ -23,9 +23,14 @@ struct kx_schema {
 struct kx_ctx {
   int device = 0;
   hipStream_t own_stream = nullptr;
-  // grow-only device workspace (tile descriptors + flags + counters)
+  // grow-only decode workspace: tile counter, error key, overflow flag, epoch-tagged tile
+  // descriptors. Zeroed once at allocation; every call leaves it re-armed (finalize kernel).
   void* ws = nullptr;
   size_t ws_size = 0;
+  uint64_t epoch = 0;                  // call epoch tagging descriptor words (1..65535)
+  // grow-only encode scratch (per-block sizes)
+  void* ews = nullptr;
+  size_t ews_size = 0;
   // pinned staging for kx_host_*
   void* pin = nullptr;
   size_t pin_size = 0;
@@ -45,11 +50,11 @@ struct KxLaunchCols {
 int kx_launch_decode(const KxProgram* dprog, const KxProgram& hprog, const uint8_t* in,
                      uint64_t in_len, const uint64_t* offsets, uint64_t n,
                      const KxLaunchCols& cols, uint8_t* record_status, kx_status* status,
-                     void* ws, size_t ws_size, hipStream_t stream, bool pb);
+                     void* ws, size_t ws_size, uint64_t epoch, hipStream_t stream, bool pb);
 size_t kx_decode_ws_bytes(const KxProgram& hprog, uint64_t in_len, const uint64_t* offsets, uint64_t n);
 
 int kx_launch_skip(const uint8_t* in, uint64_t in_len, uint64_t n, uint64_t* offsets_out,
-                   kx_status* status, void* ws, size_t ws_size, hipStream_t stream);
+                   kx_status* status, void* ws, size_t ws_size, uint64_t epoch, hipStream_t stream);
 size_t kx_skip_ws_bytes(uint64_t in_len);
 
 int kx_launch_encode(const KxProgram* dprog, const KxProgram& hprog, const KxLaunchCols& cols,

@@ -37,9 +37,11 @@ for mode in ("concat", "offsets"):
     torch.cuda.synchronize()
     L.kx_debug_phase_cycles(buf, 10)
     s = read_status(st)
-    tiles = (wire.numel() + 32767) // 32768 if o is None else (n + 255) // 256
-    names = ["load", "scan+walk1", "relax+scans", "lookback", "repair+INCL", "pre-walk2", "walk2"]
-    tot = sum(buf[:7])
+    # one wave per tile: 8 KiB (concatenated) or krec records (offsets mode)
+    krec = max(1, min(64, 8192 // max(1, -(-wire.numel() // n))))
+    tiles = (wire.numel() + 8191) // 8192 if o is None else (n + krec - 1) // krec
+    names = ["claim+window", "scan+walk1", "scans+AGG", "lookback", "repair+INCL", "walk2"]
+    tot = sum(buf[:6])
     print(f"{cfg} {mode}: code={s.code} tiles={tiles}")
     for i, nm in enumerate(names):
         print(f"  {nm:12s} {buf[i] / reps / tiles:10.0f} cycles/tile  {100 * buf[i] / max(1, tot):5.1f}%")
