@@ -149,7 +149,7 @@ __device__ __forceinline__ Fetch fetch12(const Src& w, uint64_t p) {
     f.w2 = __builtin_amdgcn_alignbyte(x3, x2, sh);
   } else if (p + 16 <= w.len) {
     uint64_t a = (uint64_t)w.in + p;
-    v4u v = *(const GLB v4u*)(a & ~3ull);
+    v4u v = *(const GLB v4u_a4*)(a & ~3ull);  // dword alignment suffices
     uint32_t sh = (uint32_t)(a & 3);
     f.w0 = __builtin_amdgcn_alignbyte(v.y, v.x, sh);
     f.w1 = __builtin_amdgcn_alignbyte(v.z, v.y, sh);
@@ -324,21 +324,21 @@ __device__ __forceinline__ void store_col(void* base, uint32_t width, uint64_t r
 
 // program tables are read from global memory (a few KiB, L1/L2-resident)
 __device__ __forceinline__ KxpField ld_field(const KxProgram* P, int i) {
-  v4u v = *(const GLB v4u*)&P->f[i];
+  v4u v = *(const GLB v4u_a4*)&P->f[i];
   KxpField F;
   __builtin_memcpy(&F, &v, sizeof F);
   return F;
 }
 __device__ __forceinline__ KxpInst ld_inst(const KxProgram* P, int i) {
   v4u v[2];
-  v[0] = ((const GLB v4u*)&P->inst[i])[0];
-  v[1] = ((const GLB v4u*)&P->inst[i])[1];
+  v[0] = ((const GLB v4u_a4*)&P->inst[i])[0];
+  v[1] = ((const GLB v4u_a4*)&P->inst[i])[1];
   KxpInst I;
   __builtin_memcpy(&I, v, sizeof I);
   return I;
 }
 __device__ __forceinline__ KxpCol ld_col(const KxProgram* P, int i) {
-  v4u v = *(const GLB v4u*)&P->col[i];
+  v4u v = *(const GLB v4u_a4*)&P->col[i];
   KxpCol K;
   __builtin_memcpy(&K, &v, sizeof K);
   return K;
@@ -354,8 +354,6 @@ __device__ __forceinline__ bool canon_record(const Src& w, const KxLaunchCols& c
   const KxpStep* __restrict__ steps = w.steps;
   uint32_t k = 0;
   while (k < w.nsteps) {
-    // every active lane is at the same step: make that explicit so the plan stays in SGPRs
-    k = __builtin_amdgcn_readfirstlane(k);
     const KxpStep st = steps[k];
     const uint64_t rem = limit - pos;
     if (st.kind == KXP_S_FIXED) {
@@ -562,7 +560,7 @@ __device__ __forceinline__ Q16 ld16(const Src& w, uint64_t p, bool inwin) {
     sh = q & 3;
   } else {
     const uint64_t a = (uint64_t)w.in + p;
-    const v4u v = *(const GLB v4u*)(a & ~3ull);
+    const v4u v = *(const GLB v4u_a4*)(a & ~3ull);
     x4 = *(const GLB uint32_t*)((a & ~3ull) + 16);
     x0 = v.x; x1 = v.y; x2 = v.z; x3 = v.w;
     sh = (uint32_t)(a & 3);

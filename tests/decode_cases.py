@@ -1,0 +1,223 @@
+"""Decode parity cases shared by the GPU suite (tests/test_gpu_thrift.py, the HIP library through
+the C-ABI) and the CPU emulation suite (tests/test_emu_decode.py, the same kernel source under the
+SIMT emulator). Every case compares against the CPU oracle on the same input, bit-exact: decoded
+columns field-for-field, error code / failing record / byte offset identical."""
+import numpy as np
+
+from kitex_amd import _abi as A
+from kitex_amd import schema as S
+from kitex_amd import synth
+from tests.helpers import assert_columns_equal, to_np
+
+
+def check_decode(dec, oracle, sch, wire, n, offsets=None):
+    rc, exp, est, ers = oracle.decode(sch, wire, n, offsets=offsets)
+    cols, st, rs = dec.decode(sch, wire, n, offsets)
+    assert st.code == est.code, (st.code, est.code)
+    if est.code:
+        assert (st.record, st.offset) == (est.record, est.offset)
+    nrec = est.n_records
+    assert st.n_records == nrec
+    if offsets is None:
+        assert st.consumed == est.consumed
+    else:
+        assert np.array_equal(to_np(rs)[:n], ers[:n])
+    _, infos, _ = oracle.flatten(sch)
+    ok_rows = nrec if offsets is None else n
+    assert_columns_equal(cols, exp, infos, ok_rows)
+    for k in range(min(8, sum(ci.kind != A.COL_FIXED for ci in infos))):
+        assert st.var_total[k] == est.var_total[k]
+    return cols, st
+
+
+def case_concat(dec, oracle, name, n):
+    sch = S.SCHEMAS[name]()
+    cs = synth.GENERATORS[name](n)
+    rc, wire, offs = oracle.encode(sch, cs)
+    assert rc == 0
+    cols, st = check_decode(dec, oracle, sch, wire, n)
+    assert st.code == 0 and st.consumed == wire.size
+
+
+def case_offsets(dec, oracle, name, n):
+    sch = S.SCHEMAS[name]()
+    cs = synth.GENERATORS[name](n, start=777)
+    rc, wire, offs = oracle.encode(sch, cs)
+    check_decode(dec, oracle, sch, wire, n, offsets=offs)
+
+
+def case_roundtrip(dec, oracle):
+    sch = S.schema_r2()
+    cs = synth.gen_r2(4096)
+    rc, wire, _ = oracle.encode(sch, cs)
+    cols, st, _ = dec.decode(sch, wire, cs.n, None)
+    assert st.code == 0
+    _, infos, _ = oracle.flatten(sch)
+    assert_columns_equal(cols, cs, infos, cs.n)
+
+
+# ---- hand-built records: non-canonical order, unknown fields, duplicates, ragged strings ----
+def rec_bytes(oracle, fields):
+    """fields: list of (ttype, id, payload bytes) in wire order; appends STOP."""
+    out = b""
+    for t, fid, payload in fields:
+        out += oracle.prim("kxo_write_field_begin", t, fid) + payload
+    return out + b"\x00"
+
+
+def i64(oracle, v):
+    return oracle.prim("kxo_write_i64", v)
+
+
+def sbytes(oracle, s: bytes):
+    return oracle.prim("kxo_write_string", s, len(s))
+
+
+def r2_record(oracle, rng, order=None, strlens=(32, 32), extra=None, dup=False):
+    fields = [(A.T_I64, f, i64(oracle, int(rng.integers(-2**63, 2**63 - 1)))) for f in range(1, 9)]
+    for j, f in enumerate((9, 10)):
+        s = bytes(rng.integers(97, 123, size=strlens[j], dtype=np.uint8))
+        fields.append((A.T_STRING, f, sbytes(oracle, s)))
+    if order is not None:
+        fields = [fields[k] for k in order]
+    if extra:
+        fields = fields[:3] + extra + fields[3:]
+    if dup:
+        fields.append((A.T_I64, 2, i64(oracle, 12345)))
+        fields.append((A.T_STRING, 9, sbytes(oracle, b"dup")))
+    return rec_bytes(oracle, fields)
+
+
+def concat(records):
+    wire = np.frombuffer(b"".join(records), dtype=np.uint8).copy()
+    offs = np.zeros(len(records) + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum([len(r) for r in records])
+    return wire, offs
+
+
+def case_noncanonical(dec, oracle, mode):
+    """reordered fields, unknown fields (skipped), mistyped known ids (skipped), duplicates
+    (last wins) — mixed with canonical ones so some tiles validate and some fall back."""
+    sch = S.schema_r2()
+    rng = np.random.default_rng(1)
+    unknown = [(A.T_STRUCT, 77, rec_bytes(oracle, [(A.T_LIST, 1, oracle.prim("kxo_write_list_begin", A.T_STRING, 2)
+                                                    + sbytes(oracle, b"a") + sbytes(oracle, b"bc"))])),
+               (A.T_I32, 3, oracle.prim("kxo_write_i32", 5)),          # field 3 with the wrong type
+               (A.T_MAP, 300, oracle.prim("kxo_write_map_begin", A.T_I64, A.T_DOUBLE, 2) + bytes(32))]
+    recs = []
+    for i in range(3000):
+        k = i % 10
+        if k == 3:
+            recs.append(r2_record(oracle, rng, order=list(rng.permutation(10))))
+        elif k == 5:
+            recs.append(r2_record(oracle, rng, extra=unknown))
+        elif k == 7:
+            recs.append(r2_record(oracle, rng, dup=True))
+        else:
+            recs.append(r2_record(oracle, rng))
+    wire, offs = concat(recs)
+    check_decode(dec, oracle, sch, wire, len(recs), offsets=offs if mode == "offsets" else None)
+
+
+def case_ragged(dec, oracle, mode):
+    """empty strings, strings crossing tile/halo boundaries, one string larger than a tile."""
+    sch = S.schema_r2()
+    rng = np.random.default_rng(2)
+    recs = []
+    lens = [0, 1, 3, 4, 5, 31, 32, 33, 127, 128, 129, 511, 513, 4097, 40000, 70000, 0, 2]
+    for i in range(600):
+        a = lens[i % len(lens)] if i % 3 == 0 else int(rng.integers(0, 64))
+        b = lens[(i * 7) % len(lens)] if i % 5 == 0 else int(rng.integers(0, 40))
+        recs.append(r2_record(oracle, rng, strlens=(a, b)))
+    wire, offs = concat(recs)
+    check_decode(dec, oracle, sch, wire, len(recs), offsets=offs if mode == "offsets" else None)
+
+
+def case_empty(dec, oracle):
+    """records with no fields at all (just STOP) decode to defaults; 1-byte records pack a tile."""
+    sch = S.Schema(S.Struct("D", [S.Field(1, A.T_I64, default=42), S.Field(2, A.T_I32, default=-7),
+                                  S.Field(3, A.T_BOOL), S.Field(4, A.T_STRING)]))
+    recs = []
+    for i in range(70000):
+        if i % 4 == 0:
+            recs.append(rec_bytes(oracle, [(A.T_I64, 1, i64(oracle, i)), (A.T_BOOL, 3, bytes([i % 3]))]))
+        else:
+            recs.append(b"\x00")
+    wire, offs = concat(recs)
+    check_decode(dec, oracle, sch, wire, len(recs))
+    check_decode(dec, oracle, sch, wire, len(recs), offsets=offs)
+
+
+def case_nested(dec, oracle):
+    inner = S.Struct("In", [S.Field(1, A.T_I64, req=A.REQ_REQUIRED), S.Field(2, A.T_STRING, req=A.REQ_OPTIONAL),
+                            S.Field(3, A.T_I16, default=9)])
+    sch = S.Schema(S.Struct("Out", [S.Field(1, A.T_I32), S.Field(2, A.T_STRUCT, child=inner),
+                                    S.Field(3, A.T_LIST, elem=A.T_I16), S.Field(4, A.T_DOUBLE, req=A.REQ_OPTIONAL)]))
+    P = oracle.prim
+    good_inner = rec_bytes(oracle, [(A.T_I64, 1, i64(oracle, 5)), (A.T_STRING, 2, sbytes(oracle, b"xy")),
+                                    (A.T_I16, 3, P("kxo_write_i16", 3))])
+    inner2 = rec_bytes(oracle, [(A.T_I64, 1, i64(oracle, 6))])                 # second occurrence resets
+    recs = []
+    for i in range(2000):
+        f = [(A.T_I32, 1, P("kxo_write_i32", i)), (A.T_STRUCT, 2, good_inner),
+             (A.T_LIST, 3, P("kxo_write_list_begin", A.T_I16, 3) + P("kxo_write_i16", 1) * 3)]
+        if i % 3 == 0:
+            f.append((A.T_STRUCT, 2, inner2))
+        if i % 4 == 0:
+            f.append((A.T_DOUBLE, 4, P("kxo_write_double", 1.5)))
+        if i % 11 == 0:
+            f.append((A.T_LIST, 3, P("kxo_write_list_begin", A.T_STRING, 1) + P("kxo_write_i16", 7)))  # elem type ignored
+        recs.append(rec_bytes(oracle, f))
+    wire, offs = concat(recs)
+    check_decode(dec, oracle, sch, wire, len(recs), offsets=offs)
+    check_decode(dec, oracle, sch, wire, len(recs))
+    # a record whose nested struct misses its required field fails with INVALID_DATA
+    bad = rec_bytes(oracle, [(A.T_I32, 1, P("kxo_write_i32", 1)),
+                             (A.T_STRUCT, 2, rec_bytes(oracle, [(A.T_I16, 3, P("kxo_write_i16", 3))]))])
+    wire2, offs2 = concat(recs[:500] + [bad] + recs[500:900])
+    cols, st = check_decode(dec, oracle, sch, wire2, 901)
+    assert st.code == A.ERR_INVALID_DATA and st.record == 500
+    cols, st = check_decode(dec, oracle, sch, wire2, 901, offsets=offs2)
+    assert st.code == A.ERR_INVALID_DATA and st.record == 500
+
+
+ERROR_CASES = ["truncated", "negative", "unknown_type", "depth", "short_input"]
+
+
+def case_error(dec, oracle, case):
+    sch = S.schema_r2()
+    rng = np.random.default_rng(4)
+    recs = [r2_record(oracle, rng) for _ in range(900)]
+    n = len(recs)
+    if case == "truncated":
+        wire, offs = concat(recs)
+        wire = wire[:-7]
+    elif case == "negative":
+        recs[400] = rec_bytes(oracle, [(A.T_STRING, 9, bytes.fromhex("fffffff0"))])
+        wire, offs = concat(recs)
+    elif case == "unknown_type":
+        recs[123] = rec_bytes(oracle, [(A.T_I64, 1, i64(oracle, 1)), (99, 50, b"")])
+        wire, offs = concat(recs)
+    elif case == "depth":
+        deep = rec_bytes(oracle, [(A.T_STRING, 1, sbytes(oracle, b"x"))])
+        for _ in range(63):
+            deep = rec_bytes(oracle, [(A.T_STRUCT, 1, deep)])
+        recs[77] = rec_bytes(oracle, [(A.T_STRUCT, 99, deep)])
+        wire, offs = concat(recs)
+    else:
+        wire, offs = concat(recs)
+        n = n + 5                                     # ask for more records than the input holds
+    check_decode(dec, oracle, sch, wire, n)
+    if case != "short_input":
+        o = offs.copy()
+        if case == "truncated":
+            o[-1] = wire.size
+        check_decode(dec, oracle, sch, wire, len(recs), offsets=o)
+
+
+def case_skip(skipper, oracle):
+    sch = S.schema_r3()
+    cs = synth.gen_r3(3000)
+    rc, wire, offs = oracle.encode(sch, cs)
+    got = skipper(wire, cs.n)
+    assert np.array_equal(to_np(got).astype(np.uint64), offs)

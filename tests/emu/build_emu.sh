@@ -1,0 +1,22 @@
+#!/bin/bash
+# Test infrastructure only: build the CPU SIMT emulation of the decode kernel (tests/emu/_build).
+# The kernel source is compiled as host C++ against tests/emu/hip/hip_runtime.h; the two
+# device-only spellings it uses (address-space qualifiers, the vmcnt wait) are rewritten on the
+# way in. Nothing here is linked into libkxcodec.so.
+set -e
+cd "$(dirname "$0")"
+ROOT=../..
+mkdir -p _build
+sed -e 's/^#define LDS __attribute__((address_space(3)))/#define LDS/' \
+    -e 's/^#define GLB __attribute__((address_space(1)))/#define GLB/' \
+    -e 's/__attribute__((amdgpu_waves_per_eu([0-9]*))) //' \
+    -e 's/asm volatile("s_waitcnt vmcnt(0)" ::: "memory");/emu_wait_vmcnt0();/' \
+    $ROOT/kitex_amd/csrc/kx_decode.hip > _build/kx_decode_emu.cpp
+CXX=${CXX:-/opt/rocm/lib/llvm/bin/clang++}
+FLAGS="-std=c++17 -O1 -g -fPIC -Wno-unknown-attributes -Wno-unused-function -I. -I$ROOT/kitex_amd/csrc"
+$CXX $FLAGS -c _build/kx_decode_emu.cpp -o _build/kx_decode_emu.o
+$CXX $FLAGS -c $ROOT/kitex_amd/csrc/kx_schema.cpp -o _build/kx_schema.o
+$CXX $FLAGS -c emu_rt.cpp -o _build/emu_rt.o
+$CXX $FLAGS -c emu_driver.cpp -o _build/emu_driver.o
+$CXX -shared -o _build/libkxemu.so _build/*.o -lpthread
+echo _build/libkxemu.so

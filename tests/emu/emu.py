@@ -1,0 +1,54 @@
+"""Test infrastructure only: ctypes binding of the CPU SIMT emulation of the decode kernel."""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+from kitex_amd import _abi as A
+from kitex_amd.columns import alloc_host, to_kx_columns
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "_build", "libkxemu.so")
+_lib = None
+
+
+def build():
+    subprocess.run([os.path.join(HERE, "build_emu.sh")], check=True, stdout=subprocess.DEVNULL)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        src = os.path.join(HERE, "..", "..", "kitex_amd", "csrc", "kx_decode.hip")
+        if not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(src):
+            build()
+        _lib = C.CDLL(LIB)
+        _lib.emu_decode.restype = C.c_int
+        _lib.emu_decode.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64,
+                                    C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]
+    return _lib
+
+
+def decode(schema, infos, npres, data: np.ndarray, n: int, offsets=None, var_caps=None, threads: int = 8):
+    os.environ["KX_EMU_THREADS"] = str(threads)
+    if var_caps is None:
+        var_caps = [0 if ci.kind == A.COL_FIXED else max(1, data.size) for ci in infos]
+    out = alloc_host(infos, n, var_caps, npres)
+    kc = to_kx_columns(out, infos, var_caps)
+    st = A.Status()
+    rs = np.zeros(max(1, n), dtype=np.uint8)
+    tab, ns = schema.struct_table()
+    rc = lib().emu_decode(C.cast(tab, C.c_void_p), ns, data.ctypes.data, data.size,
+                          offsets.ctypes.data if offsets is not None else None, n, C.addressof(kc),
+                          rs.ctypes.data, C.addressof(st), 0, None)
+    return rc, out, st, rs[:n]
+
+
+def skip(data: np.ndarray, n: int, threads: int = 8):
+    os.environ["KX_EMU_THREADS"] = str(threads)
+    offs = np.zeros(n + 1, dtype=np.uint64)
+    st = A.Status()
+    rc = lib().emu_decode(None, 0, data.ctypes.data, data.size, None, n, None, None, C.addressof(st), 1,
+                          offs.ctypes.data)
+    return rc, offs, st

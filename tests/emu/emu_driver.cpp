@@ -1,0 +1,32 @@
+// Test infrastructure only: C entry point that runs the decode kernel source under the SIMT
+// emulator with host buffers (see tests/test_emu_decode.py).
+#include "hip/hip_runtime.h"
+#include "kx_internal.h"
+
+extern "C" int emu_decode(const kx_struct_desc* structs, uint32_t nstructs, const uint8_t* in, uint64_t in_len,
+                          const uint64_t* offsets, uint64_t n, const kx_columns* out, uint8_t* record_status,
+                          kx_status* status, int skip, uint64_t* skip_out) {
+  static kx_schema s;  // the emulator is single-call-at-a-time
+  int rc = skip ? KX_OK : kx_build_program(structs, nstructs, &s);
+  if (rc) return rc;
+  KxLaunchCols lc;
+  memset(&lc, 0, sizeof lc);
+  if (!skip) {
+    for (uint32_t c = 0; c < s.ncols; c++) {
+      lc.data[c] = out->cols[c].data;
+      lc.offs[c] = out->cols[c].offsets;
+      lc.cap[c] = out->cols[c].capacity;
+    }
+    lc.presence = out->presence;
+  }
+  size_t ws_size = skip ? kx_skip_ws_bytes(in_len) : kx_decode_ws_bytes(s.prog, in_len, offsets, n);
+  char* ws = (char*)calloc(1, ws_size);
+  memset(ws + 8, 0xff, 8);
+  if (skip)
+    rc = kx_launch_skip(in, in_len, n, skip_out, status, ws, ws_size, 1, nullptr);
+  else
+    rc = kx_launch_decode(&s.prog, s.prog, in, in_len, offsets, n, lc, record_status, status, ws, ws_size, 1,
+                          nullptr, false);
+  free(ws);
+  return rc;
+}

@@ -1,0 +1,75 @@
+"""CPU runs of the decode KERNEL SOURCE (kitex_amd/csrc/kx_decode.hip) under the SIMT emulator
+(tests/emu): same parity cases as the GPU suite, oracle-checked. This covers the kernel's
+cross-tile logic (speculative entries, repair rounds, decoupled look-back, error paths) on every
+CPU test run; the emulator is test infrastructure and is never linked into the product."""
+import numpy as np
+import pytest
+
+from tests import decode_cases as DC
+from tests.emu import emu
+
+
+class EmuDecoder:
+    def __init__(self, oracle, threads=8):
+        self.oracle = oracle
+        self.threads = threads
+
+    def decode(self, sch, wire, n, offsets=None):
+        _, infos, npres = self.oracle.flatten(sch)
+        rc, out, st, rs = emu.decode(sch, infos, npres, wire, n, offsets=offsets, threads=self.threads)
+        assert rc == 0, rc
+        return out, st, rs
+
+
+@pytest.fixture(scope="module")
+def edec(oracle):
+    emu.lib()
+    return EmuDecoder(oracle)
+
+
+@pytest.mark.parametrize("name", ["r1", "r2", "r3"])
+@pytest.mark.parametrize("n", [1, 7, 1000, 25000])
+def test_emu_concat(edec, oracle, name, n):
+    DC.case_concat(edec, oracle, name, n)
+
+
+@pytest.mark.parametrize("name", ["r1", "r2", "r3"])
+@pytest.mark.parametrize("n", [1, 300, 5000])
+def test_emu_offsets(edec, oracle, name, n):
+    DC.case_offsets(edec, oracle, name, n)
+
+
+def test_emu_roundtrip(edec, oracle):
+    DC.case_roundtrip(edec, oracle)
+
+
+@pytest.mark.parametrize("mode", ["concat", "offsets"])
+def test_emu_noncanonical(edec, oracle, mode):
+    DC.case_noncanonical(edec, oracle, mode)
+
+
+@pytest.mark.parametrize("mode", ["concat", "offsets"])
+def test_emu_ragged(edec, oracle, mode):
+    DC.case_ragged(edec, oracle, mode)
+
+
+def test_emu_empty_records(edec, oracle):
+    DC.case_empty(edec, oracle)
+
+
+def test_emu_nested(edec, oracle):
+    DC.case_nested(edec, oracle)
+
+
+@pytest.mark.parametrize("case", DC.ERROR_CASES)
+def test_emu_errors(edec, oracle, case):
+    DC.case_error(edec, oracle, case)
+
+
+def test_emu_skip(edec, oracle):
+    DC.case_skip(lambda wire, n: emu.skip(wire, n)[1], oracle)
+
+
+def test_emu_deep_lookback(oracle):
+    """many workgroups in flight: 64 concurrent workgroups over ~1500 tiles"""
+    DC.case_concat(EmuDecoder(oracle, threads=64), oracle, "r2", 75000)
