@@ -820,9 +820,11 @@ __device__ __forceinline__ void publish_words(const DecParams& dp, uint64_t t, i
 // ---------------------------------------------------------------------------------------------
 // the kernel: 4 independent waves per workgroup, one tile per wave
 // ---------------------------------------------------------------------------------------------
+// (the lane builtins return int: keep both halves unsigned so bit 31 never sign-extends)
 __device__ __forceinline__ uint64_t rfl64(uint64_t v) {
-  return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
-         __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return ((uint64_t)hi << 32) | lo;
 }
 
 // first canonical signature (3 bytes) in a lane's 128-byte segment, read from the LDS window:

@@ -92,13 +92,14 @@ inline T __shfl_xor(T v, int m, int width = 64) {
   emu_wave_xchg(emu_bits(v), all);
   return emu_from<T>(all[(emu_lane() ^ m) & 63]);
 }
-inline uint32_t __builtin_amdgcn_readlane(uint32_t v, int l) {
+// like the real builtins these return int (a sign-extension trap the emulator must reproduce)
+inline int __builtin_amdgcn_readlane(int v, int l) {
   uint64_t all[64];
-  emu_wave_xchg(v, all);
-  return (uint32_t)all[l & 63];
+  emu_wave_xchg((uint32_t)v, all);
+  return (int)(uint32_t)all[l & 63];
 }
 // only used where every active lane holds the same value
-inline uint32_t __builtin_amdgcn_readfirstlane(uint32_t v) { return v; }
+inline int __builtin_amdgcn_readfirstlane(int v) { return v; }
 
 inline uint32_t __builtin_amdgcn_alignbyte(uint32_t hi, uint32_t lo, uint32_t s) {
   return (uint32_t)((((uint64_t)hi << 32) | lo) >> ((s & 3) * 8));
