@@ -44,14 +44,15 @@ constexpr int HALO = 512;                // the record straddling the tile end i
 constexpr int WINB = TILE + HALO + 16;   // LDS window bytes (+16 for the aligned-down start)
 constexpr int WINW = WINB / 4 + 4;       // window dwords (+ pad for the last aligned read pair)
 constexpr int WIN_LOADS = (WINB / 16 + 63) / 64;
-constexpr int DSTRIDE = 24;              // u64 words per tile descriptor
+constexpr int DFIELDS = 21;              // look-back word arrays (structure of arrays over tiles)
 
 constexpr uint64_t V48 = (1ull << 48) - 1;
 constexpr uint64_t X_ERR = V48;          // chain terminated by a decode error
 constexpr uint64_t X_DONE = V48 - 1;     // chain reached n records
 constexpr uint64_t X_NONE = V48 - 2;     // no candidate in this tile / lane
 
-// descriptor words (each = epoch << 48 | value)
+// descriptor words (each = epoch << 48 | value); word f of tile t lives at desc[f * ntiles + t], so a
+// wave reading 64 consecutive tiles' word f touches a few contiguous cache lines
 constexpr int D_AGG_CNT = 0, D_AGG_ENT = 1, D_AGG_EXIT = 2, D_AGG_VAR = 3;  // 3 + 8
 constexpr int D_INC_CNT = 11, D_INC_EXIT = 12, D_INC_VAR = 13;              // 2 + 8
 
@@ -673,7 +674,8 @@ __device__ __forceinline__ LB lookback(const DecParams& dp, uint64_t t, bool cha
   int64_t wend = (int64_t)t;
   while (ok && !done) {
     const int64_t j = wend - 1 - lane;
-    const uint64_t* d = dp.desc + (uint64_t)(j < 0 ? 0 : j) * DSTRIDE;
+    const uint64_t* d = dp.desc + (uint64_t)(j < 0 ? 0 : j);
+    const uint64_t nt = dp.ntiles;
     int state = j < 0 ? 2 : 0;  // 0 not ready, 1 AGG, 2 INCL
     uint64_t c = 0, en = X_NONE, ex = 0;
     uint64_t vv[KXP_NV_MAX];
@@ -683,8 +685,8 @@ __device__ __forceinline__ LB lookback(const DecParams& dp, uint64_t t, bool cha
     for (;;) {
       // heads: lanes still unknown poll the INCL and AGG count words
       if (state == 0) {
-        const uint64_t ic = aload64(d + D_INC_CNT);
-        const uint64_t ac = aload64(d + D_AGG_CNT);
+        const uint64_t ic = aload64(d + D_INC_CNT * nt);
+        const uint64_t ac = aload64(d + D_AGG_CNT * nt);
         if ((ic >> 48) == ep) { state = 2; c = ic & V48; }
         else if ((ac >> 48) == ep) { state = 1; c = ac & V48; }
       }
@@ -695,23 +697,23 @@ __device__ __forceinline__ LB lookback(const DecParams& dp, uint64_t t, bool cha
         bool bad = false;
         if (j >= 0 && lane <= p) {
           if (state == 2) {
-            const uint64_t ix = aload64(d + D_INC_EXIT);
+            const uint64_t ix = aload64(d + D_INC_EXIT * nt);
             bad |= (ix >> 48) != ep;
             ex = ix & V48;
 #pragma unroll
             for (int v = 0; v < NV; v++) {
-              const uint64_t iv = aload64(d + D_INC_VAR + v);
+              const uint64_t iv = aload64(d + (D_INC_VAR + v) * nt);
               bad |= (iv >> 48) != ep;
               vv[v] = iv & V48;
             }
           } else {
-            const uint64_t ae = aload64(d + D_AGG_ENT), ax = aload64(d + D_AGG_EXIT);
+            const uint64_t ae = aload64(d + D_AGG_ENT * nt), ax = aload64(d + D_AGG_EXIT * nt);
             bad |= (ae >> 48) != ep || (ax >> 48) != ep;
             en = ae & V48;
             ex = ax & V48;
 #pragma unroll
             for (int v = 0; v < NV; v++) {
-              const uint64_t av = aload64(d + D_AGG_VAR + v);
+              const uint64_t av = aload64(d + (D_AGG_VAR + v) * nt);
               bad |= (av >> 48) != ep;
               vv[v] = av & V48;
             }
@@ -774,16 +776,17 @@ __device__ __forceinline__ LB lookback(const DecParams& dp, uint64_t t, bool cha
   if (!ok) {
     if (lane == 0) atomicAdd((unsigned long long*)&dp.status->diag[1], 1ull);
     // wait for the immediate predecessor's inclusive prefix
-    const uint64_t* d = dp.desc + (t - 1) * DSTRIDE;
+    const uint64_t* d = dp.desc + (t - 1);
+    const uint64_t nt = dp.ntiles;
     bool got = false;
     int backoff = 1;
     for (;;) {
-      const uint64_t ic = aload64(d + D_INC_CNT), ix = aload64(d + D_INC_EXIT);
+      const uint64_t ic = aload64(d + D_INC_CNT * nt), ix = aload64(d + D_INC_EXIT * nt);
       uint64_t iv[KXP_NV_MAX];
       bool incl = (ic >> 48) == ep && (ix >> 48) == ep;
 #pragma unroll
       for (int v = 0; v < NV; v++) {
-        iv[v] = aload64(d + D_INC_VAR + v);
+        iv[v] = aload64(d + (D_INC_VAR + v) * nt);
         incl &= (iv[v] >> 48) == ep;
       }
       if (incl) {
@@ -812,9 +815,9 @@ __device__ __forceinline__ LB lookback(const DecParams& dp, uint64_t t, bool cha
 // one lane publishes a set of self-tagged words
 __device__ __forceinline__ void publish_words(const DecParams& dp, uint64_t t, int first, const uint64_t* vals,
                                               int nwords) {
-  uint64_t* d = dp.desc + t * DSTRIDE + first;
+  uint64_t* d = dp.desc + t + (uint64_t)first * dp.ntiles;
   const uint64_t ep = dp.epoch << 48;
-  for (int i = 0; i < nwords; i++) astore64(d + i, ep | (vals[i] & V48));
+  for (int i = 0; i < nwords; i++) astore64(d + (uint64_t)i * dp.ntiles, ep | (vals[i] & V48));
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1230,7 +1233,7 @@ __global__ void finalize_kernel(kx_status* st, unsigned long long* errkey, uint3
 // workspace: [0] tile counter u32, [8] errkey u64, [16] overflow u32, [256...) tile descriptors
 constexpr size_t WS_DESC = 256;
 
-size_t ws_total(uint64_t ntiles) { return WS_DESC + ntiles * DSTRIDE * 8; }
+size_t ws_total(uint64_t ntiles) { return WS_DESC + ntiles * DFIELDS * 8; }
 
 // offsets mode: records per tile so that a tile's bytes fit the LDS window on average
 uint32_t krec_for(uint64_t in_len, uint64_t n) {

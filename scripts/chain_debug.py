@@ -47,7 +47,7 @@ for r in range(reps):
     hip = C.CDLL("libamdhip64.so")
     rc = hip.hipMemcpy(C.c_void_p(host.ctypes.data), p, C.c_size_t(sz.value), 2)  # device -> host
     assert rc == 0, rc
-    words = host[32:32 + ntiles * DSTRIDE].reshape(ntiles, DSTRIDE)
+    words = host[32:32 + 21 * ntiles].reshape(21, ntiles).T  # structure of arrays: word f of tile t at f*ntiles+t
     tag = (words >> np.uint64(48)).astype(np.int64)
     val = (words & np.uint64(V48)).astype(np.int64)
     inc_ok = tag[:, 11] == ep.value
