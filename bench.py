@@ -162,8 +162,7 @@ def main():
                    "parallelism": f"shard{world}"},
         "gib_s": gib_s,
         "verified": ok,
-        "decode_diag": {"serial_rewalk_tiles": st.diag[0], "lookback_waits": st.diag[1],
-                        "inconsistent_tiles": st.diag[2]},
+        "decode_diag": {"tile_rewalks": st.diag[0], "group_rescans": st.diag[1]},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(cfg, args.mode),
                      "read_only_frac": per_rec_in * n / avg_launch_s / 1e9 / HBM_PEAK_GBS,

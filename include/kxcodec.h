@@ -134,8 +134,8 @@ typedef struct kx_status {
   uint64_t n_records;   /* records decoded */
   uint64_t consumed;    /* input bytes consumed (concatenated mode) */
   uint64_t var_total[8];  /* required arena size (arena units) of the first 8 var columns */
-  uint64_t diag[3];       /* decode diagnostics: [0] tiles re-walked serially, [1] look-backs that
-                             waited for the predecessor, [2] tiles whose speculation was inconsistent */
+  uint64_t diag[3];       /* decode diagnostics: [0] tiles re-walked from their true entry,
+                             [1] groups of 64 tiles re-scanned by the chain pass, [2] reserved */
 } kx_status;
 
 typedef struct kx_ctx kx_ctx; /* opaque; one per host thread / stream */

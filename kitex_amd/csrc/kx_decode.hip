@@ -5,23 +5,22 @@
 // message (pkg/remote/codec/thrift/codec_fast.go:60-82) or as the element loop of a list<Struct>;
 // unknown / mistyped fields go through the skip decoder (codec_apache.go:191-293).
 //
-// Design — ONE pass over HBM, one WAVE per tile, no workgroup barriers:
-//   * concatenated mode: a tile is 8 KiB of input. The wave pulls the tile (+ a 512-byte halo for
-//     the record straddling its end) into its own LDS window with LDS-DMA (global_load_lds_dwordx4:
-//     HBM -> LDS without registers, 9 loads in flight per lane). Lane l owns the 128-byte segment
-//     l: it finds the first canonical record signature in its segment and walks records
-//     (schema-aware FastRead lengths) until it leaves the segment ("walk 1").
-//   * lanes repair each other's entries with wave shuffles until the chain is consistent; record
-//     counts and arena bytes are prefix-summed across the wave;
-//   * the tile aggregate is published as self-tagged 64-bit words (16-bit call epoch + 48-bit value:
-//     no flag, no fence, no per-call memset) and a decoupled look-back over predecessor tiles yields
-//     the true entry, record base and arena bases; a wrong speculation is repaired from the true
-//     entry (more shuffle rounds) before the inclusive prefix is published;
-//   * "walk 2" re-parses from LDS and scatters: fixed-width columns are stored as parsed (lanes =
-//     consecutive records), strings / lists are copied from LDS with 16-byte stores.
-//   * known-offsets mode (fastUnmarshal with dataLen): a tile is up to 64 records, one per lane.
-// Walk 1, the repair rounds and walk 2 run through ONE instance of the record parser (a small
-// state machine around it), which keeps the kernel's code inside the instruction cache.
+// Design: three stream-ordered kernels, no wave ever waits for another tile's work.
+//   1. index pass — one WAVE per 8 KiB tile. The tile (+ a 512-byte halo for the record straddling
+//      its end) is pulled into the wave's LDS window by LDS-DMA (global_load_lds_dwordx4). Lane l owns
+//      the 128-byte segment l: it finds the first canonical record signature in it and walks records
+//      (schema-aware FastRead lengths) until it leaves the segment; lanes repair each other with wave
+//      shuffles until the chain is consistent. The tile writes its record starts (u16 list) and an
+//      aggregate (speculative entry, exit, count, arena bytes, first error) as epoch-tagged words.
+//      The last wave to finish a group of 64 tiles validates the chain between them (re-walking a
+//      tile from its true entry where the speculation was wrong) and scans the group.
+//   2. chain pass — one workgroup resolves the chain over the groups from offset 0 and writes every
+//      group's record / arena base and the number of records to emit (errors, EOF, n).
+//   3. emit pass — one wave per tile again (the tile is re-read, mostly from the Infinity Cache when
+//      it fits), lane = record: fixed-width fields are stored as parsed (lanes = consecutive records,
+//      coalesced), strings / lists are copied from LDS with 16-byte stores at scanned arena offsets.
+//   Known-offsets mode (fastUnmarshal with dataLen): a tile is up to 64 records, lane = record; the
+//   index pass only measures arena bytes (skipped entirely when the schema has no var columns).
 // Canonical records (the encoder's layout) take a straight-line step plan compiled from the schema;
 // anything else takes the generic field loop. Records or strings reaching past the LDS window are
 // read from global memory (same code, other source).
@@ -33,6 +32,7 @@
 
 #define LDS __attribute__((address_space(3)))
 #define GLB __attribute__((address_space(1)))
+#define KAS __attribute__((address_space(4)))  // kernarg segment (read in place, never copied to scratch)
 
 namespace {
 
@@ -44,22 +44,24 @@ constexpr int HALO = 512;                // the record straddling the tile end i
 constexpr int WINB = TILE + HALO + 16;   // LDS window bytes (+16 for the aligned-down start)
 constexpr int WINW = WINB / 4 + 4;       // window dwords (+ pad for the last aligned read pair)
 constexpr int WIN_LOADS = (WINB / 16 + 63) / 64;
-constexpr int DFIELDS = 21;              // look-back word arrays (structure of arrays over tiles)
+constexpr int GT = 64;                   // tiles per group (one group-scan lane per tile)
+constexpr int CT = 256, CW = CT / 64;    // chain pass: one workgroup, lane = group
 
 constexpr uint64_t V48 = (1ull << 48) - 1;
 constexpr uint64_t X_ERR = V48;          // chain terminated by a decode error
-constexpr uint64_t X_DONE = V48 - 1;     // chain reached n records
+constexpr uint64_t X_DONE = V48 - 1;     // chain already ended (no records to emit)
 constexpr uint64_t X_NONE = V48 - 2;     // no candidate in this tile / lane
+constexpr uint64_t X_BAD = V48 - 3;      // group whose speculative tile chain disagrees (chain pass repairs)
 
-// descriptor words (each = epoch << 48 | value); word f of tile t lives at desc[f * ntiles + t], so a
-// wave reading 64 consecutive tiles' word f touches a few contiguous cache lines
-constexpr int D_AGG_CNT = 0, D_AGG_ENT = 1, D_AGG_EXIT = 2, D_AGG_VAR = 3;  // 3 + 8
-constexpr int D_INC_CNT = 11, D_INC_EXIT = 12, D_INC_VAR = 13;              // 2 + 8
+// tile words (structure of arrays over tiles, epoch-tagged): aggregate of the index pass, then the
+// exclusive prefix inside the group written by the group scan
+enum { T_ENT = 0, T_EXIT, T_CNT, T_ERRC, T_ERRP, T_VAR, T_PCNT = T_VAR + KXP_NV_MAX, T_PVAR,
+       T_NF = T_PVAR + KXP_NV_MAX };
+// group words: group aggregate, then the global exclusive base written by the chain pass
+enum { G_ENT = 0, G_EXIT, G_CNT, G_ERRC, G_ERRP, G_VAR, G_BCNT = G_VAR + KXP_NV_MAX, G_BVAR,
+       G_NF = G_BVAR + KXP_NV_MAX };
 
 enum Mode { M_THRIFT = 0, M_SKIP = 1 };
-
-// opt-in phase timing (KX_PHASE_TIMING=1): shader cycles per phase summed over tiles (lane 0)
-__device__ unsigned long long g_phase[10];
 
 struct DecParams {
   const uint8_t* in;
@@ -71,16 +73,24 @@ struct DecParams {
   uint8_t* rstat;
   kx_status* status;
   uint64_t* skip_out;        // M_SKIP: record start offsets
-  uint32_t* counter;         // dynamic tile counter (reset by finalize)
-  uint64_t* desc;            // per-tile look-back words
+  uint64_t* tdesc;           // tile words
+  uint64_t* gdesc;           // group words
+  uint32_t* gcount;          // per-group arrival counters (cleared at launch)
+  uint16_t* starts;          // concatenated mode: record starts per tile (slotcap slots each)
   unsigned long long* errkey;  // offsets mode: min((record << 8) | code)
   uint32_t* overflow;        // an arena capacity was exceeded
-  uint64_t ntiles;
+  uint64_t* nstop;           // records to emit (chain pass)
+  uint64_t ntiles, ngroups, slotcap;
   uint64_t epoch;            // 16-bit call epoch (never 0)
   uint32_t krec;             // offsets mode: records per tile (<= 64)
-  int timing;
+  int direct;                // offsets mode without var columns: emit pass only
   int nolds;                 // diagnostics (KX_NOLDS=1): read every byte from global memory
 };
+
+// Kernels read their parameter block in place from the kernarg segment: indexing a by-value
+// parameter (cols.data[c]) would otherwise make the compiler copy the whole block to scratch per lane.
+typedef const KAS DecParams KParams;
+#define KX_PARAMS() (*(KParams*)__builtin_amdgcn_kernarg_segment_ptr())
 
 // ---------------------------------------------------------------------------------------------
 // byte access: the wave's LDS window, or global memory outside it
@@ -349,7 +359,7 @@ __device__ __forceinline__ KxpCol ld_col(const KxProgram* P, int i) {
 // encoder order, STOP bytes). The step index is wave-uniform (scalar loads); a lane whose record
 // deviates returns false and the record is re-parsed by the generic loop.
 template <int NV>
-__device__ __forceinline__ bool canon_record(const Src& w, const KxLaunchCols& cols, uint64_t start, uint64_t limit,
+__device__ __forceinline__ bool canon_record(const Src& w, const KAS KxLaunchCols& cols, uint64_t start, uint64_t limit,
                                              uint64_t rec, bool emit, uint64_t* endp, VarState<NV>& vs) {
   uint64_t pos = start;
   const KxpStep* __restrict__ steps = w.steps;
@@ -418,7 +428,7 @@ __device__ __forceinline__ bool canon_record(const Src& w, const KxLaunchCols& c
 // Generic FastRead field loop: any field order, unknown / mistyped fields skipped, repeated ids
 // (last wins; a repeated struct field is a fresh NewX()), required fields checked.
 template <int NV>
-__device__ __forceinline__ int generic_record(const Src& w, const KxProgram* P, const KxLaunchCols& cols,
+__device__ __forceinline__ int generic_record(const Src& w, const KxProgram* P, const KAS KxLaunchCols& cols,
                                               uint64_t start, uint64_t limit, uint64_t rec, bool emit,
                                               uint64_t* endp, VarState<NV>& vs, uint64_t& pres_out) {
 #pragma unroll
@@ -510,7 +520,7 @@ __device__ __forceinline__ int generic_record(const Src& w, const KxProgram* P, 
   return KX_OK;
 }
 
-__device__ __forceinline__ void emit_defaults(const KxProgram* P, const KxLaunchCols& cols, uint64_t rec) {
+__device__ __forceinline__ void emit_defaults(const KxProgram* P, const KAS KxLaunchCols& cols, uint64_t rec) {
   for (uint32_t c = 0; c < P->ncols; c++) {
     const KxpCol K = ld_col(P, c);
     if (K.kind == KXP_K_FIXED) store_col(cols.data[c], K.width, rec, (uint64_t)K.defv);
@@ -628,11 +638,18 @@ __device__ __forceinline__ uint64_t wave_incl_scan(uint64_t v, int lane) {
   return v;
 }
 
+__device__ __forceinline__ uint64_t wave_sum(uint64_t v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+  return v;
+}
+
 __device__ __forceinline__ uint64_t rl64(uint64_t v, int l) {
   uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, l);
   uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), l);
   return ((uint64_t)hi << 32) | lo;
 }
+
 
 __device__ __forceinline__ uint64_t aload64(const uint64_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -643,191 +660,38 @@ __device__ __forceinline__ void astore64(uint64_t* p, uint64_t v) {
 
 __device__ __forceinline__ uint64_t now_ns() { return __builtin_amdgcn_s_memrealtime() * 10; }  // 100 MHz
 
-struct LB {
-  uint64_t e, cnt;
-  uint64_t var[KXP_NV_MAX];
-};
+// ---------------------------------------------------------------------------------------------
+// self-tagged descriptor words (16-bit call epoch << 48 | 48-bit value), structure of arrays:
+// word f of item i lives at base[f * nitems + i]. A word is valid iff its tag is this call's, so no
+// per-call clearing and no fences: a reader polls the words it needs until their tags match.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ void put_word(uint64_t* base, uint64_t nitems, int f, uint64_t i, uint64_t ep,
+                                         uint64_t v) {
+  astore64(base + (uint64_t)f * nitems + i, (ep << 48) | (v & V48));
+}
 
-// Decoupled look-back by one wave (64 predecessors per window, newest in lane 0). Every word is
-// self-tagged with the call epoch, so no flag / fence protocol is needed: a word is valid iff its
-// tag is this call's. Polling touches only the two head words of each predecessor (INCL count,
-// AGG count) with exponential back-off; the remaining words of the tiles that matter are read once
-// they are ready (re-polled in the rare case one of them is not visible yet).
-// The speculative chain is verified on the way back: for consecutive candidate-bearing tiles
-// a < b, exit(a) == entry(b); the inclusive tile's exit equals the entry of the oldest candidate
-// tile after it. Any mismatch: wait for tile t-1's inclusive prefix.
-template <int NV>
-__device__ __forceinline__ LB lookback(const DecParams& dp, uint64_t t, bool chain, int lane) {
-  LB out;
-  out.e = 0; out.cnt = 0;
-#pragma unroll
-  for (int v = 0; v < KXP_NV_MAX; v++) out.var[v] = 0;
-  if (t == 0) return out;
-  const uint64_t ep = dp.epoch;
+// Polls `nw` words of item i (fields f0.. of `fields`), lanes with !act skip. Returns false on timeout.
+template <int NW>
+__device__ __forceinline__ bool get_words(const uint64_t* base, uint64_t nitems, const int* fields, int nw, uint64_t i,
+                                          uint64_t ep, bool act, uint64_t* out) {
   const uint64_t t0 = now_ns();
-  bool ok = true, done = false;
-  bool have_pending = false, have_newest = false;
-  uint64_t pending_ent = 0, newest_ex = 0, E = 0, cnt = 0;
-  uint64_t var[KXP_NV_MAX];
+  int backoff = 1;
+  for (;;) {
+    bool ok = true;
+    if (act) {
 #pragma unroll
-  for (int v = 0; v < KXP_NV_MAX; v++) var[v] = 0;
-  int64_t wend = (int64_t)t;
-  while (ok && !done) {
-    const int64_t j = wend - 1 - lane;
-    const uint64_t* d = dp.desc + (uint64_t)(j < 0 ? 0 : j);
-    const uint64_t nt = dp.ntiles;
-    int state = j < 0 ? 2 : 0;  // 0 not ready, 1 AGG, 2 INCL
-    uint64_t c = 0, en = X_NONE, ex = 0;
-    uint64_t vv[KXP_NV_MAX];
-#pragma unroll
-    for (int v = 0; v < KXP_NV_MAX; v++) vv[v] = 0;
-    int backoff = 1;
-    for (;;) {
-      // heads: lanes still unknown poll the INCL and AGG count words
-      if (state == 0) {
-        const uint64_t ic = aload64(d + D_INC_CNT * nt);
-        const uint64_t ac = aload64(d + D_AGG_CNT * nt);
-        if ((ic >> 48) == ep) { state = 2; c = ic & V48; }
-        else if ((ac >> 48) == ep) { state = 1; c = ac & V48; }
-      }
-      uint64_t inclm = __ballot(state == 2);
-      int p = inclm ? __ffsll((long long)inclm) - 1 : 64;
-      if (!__ballot(state == 0 && lane <= p)) {
-        // bodies of the tiles that matter (lanes <= p), one round trip
-        bool bad = false;
-        if (j >= 0 && lane <= p) {
-          if (state == 2) {
-            const uint64_t ix = aload64(d + D_INC_EXIT * nt);
-            bad |= (ix >> 48) != ep;
-            ex = ix & V48;
-#pragma unroll
-            for (int v = 0; v < NV; v++) {
-              const uint64_t iv = aload64(d + (D_INC_VAR + v) * nt);
-              bad |= (iv >> 48) != ep;
-              vv[v] = iv & V48;
-            }
-          } else {
-            const uint64_t ae = aload64(d + D_AGG_ENT * nt), ax = aload64(d + D_AGG_EXIT * nt);
-            bad |= (ae >> 48) != ep || (ax >> 48) != ep;
-            en = ae & V48;
-            ex = ax & V48;
-#pragma unroll
-            for (int v = 0; v < NV; v++) {
-              const uint64_t av = aload64(d + (D_AGG_VAR + v) * nt);
-              bad |= (av >> 48) != ep;
-              vv[v] = av & V48;
-            }
-          }
-        }
-        if (!__ballot(bad)) break;
-        if (bad) state = 0;  // a word not visible yet: poll again
-      }
-      if (now_ns() - t0 > 4000000000ull) { ok = false; break; }
-      __builtin_amdgcn_s_sleep(1);
-      for (int k = 1; k < backoff; k++) __builtin_amdgcn_s_sleep(1);
-      backoff = backoff < 32 ? backoff * 2 : 32;
-    }
-    if (!ok) break;
-    const uint64_t inclm = __ballot(state == 2);
-    const int p = inclm ? __ffsll((long long)inclm) - 1 : 64;
-    uint64_t sc = lane <= p ? c : 0;
-#pragma unroll
-    for (int dd = 32; dd >= 1; dd >>= 1) sc += __shfl_xor(sc, dd, 64);
-    cnt += sc;
-#pragma unroll
-    for (int v = 0; v < NV; v++) {
-      uint64_t sv = lane <= p ? vv[v] : 0;
-#pragma unroll
-      for (int dd = 32; dd >= 1; dd >>= 1) sv += __shfl_xor(sv, dd, 64);
-      var[v] += sv;
-    }
-    if (chain) {
-      const bool cand = lane < p && state == 1 && en != X_NONE;
-      const uint64_t cm = __ballot(cand);
-      const uint64_t older_mask = lane < 63 ? cm & ~((2ull << lane) - 1) : 0ull;
-      const int older = older_mask ? __ffsll((long long)older_mask) - 1 : -1;
-      const uint64_t older_ex = __shfl(ex, older < 0 ? lane : older, 64);
-      if (__ballot(cand && older >= 0 && older_ex != en)) ok = false;
-      if (cm) {
-        const int newest = __ffsll((long long)cm) - 1;
-        const int oldest = 63 - __clzll((long long)cm);
-        const uint64_t newest_exv = rl64(ex, newest);
-        if (have_pending && newest_exv != pending_ent) ok = false;
-        if (!have_newest) { newest_ex = newest_exv; have_newest = true; }
-        pending_ent = rl64(en, oldest);
-        have_pending = true;
+      for (int k = 0; k < NW; k++) {
+        if (k >= nw) break;
+        const uint64_t x = aload64(base + (uint64_t)fields[k] * nitems + i);
+        ok &= (x >> 48) == ep;
+        out[k] = x & V48;
       }
     }
-    if (p < 64) {
-      const uint64_t xp = rl64(ex, p);
-      if (xp == X_ERR || xp == X_DONE) {
-        E = xp;
-      } else if (chain) {
-        if (have_pending && xp != pending_ent) ok = false;
-        E = have_newest ? newest_ex : xp;
-      } else {
-        E = xp;
-      }
-      done = true;
-    } else {
-      wend -= 64;
-    }
+    if (!__ballot(!ok)) return true;
+    if (now_ns() - t0 > 2000000000ull) return false;
+    for (int k = 0; k < backoff; k++) __builtin_amdgcn_s_sleep(1);
+    backoff = backoff < 16 ? backoff * 2 : 16;
   }
-  if (!ok) {
-    if (lane == 0) atomicAdd((unsigned long long*)&dp.status->diag[1], 1ull);
-    // wait for the immediate predecessor's inclusive prefix
-    const uint64_t* d = dp.desc + (t - 1);
-    const uint64_t nt = dp.ntiles;
-    bool got = false;
-    int backoff = 1;
-    for (;;) {
-      const uint64_t ic = aload64(d + D_INC_CNT * nt), ix = aload64(d + D_INC_EXIT * nt);
-      uint64_t iv[KXP_NV_MAX];
-      bool incl = (ic >> 48) == ep && (ix >> 48) == ep;
-#pragma unroll
-      for (int v = 0; v < NV; v++) {
-        iv[v] = aload64(d + (D_INC_VAR + v) * nt);
-        incl &= (iv[v] >> 48) == ep;
-      }
-      if (incl) {
-        E = ix & V48; cnt = ic & V48;
-#pragma unroll
-        for (int v = 0; v < NV; v++) var[v] = iv[v] & V48;
-        got = true;
-        break;
-      }
-      if (now_ns() - t0 > 4000000000ull) break;
-      for (int k = 0; k < backoff; k++) __builtin_amdgcn_s_sleep(1);
-      backoff = backoff < 32 ? backoff * 2 : 32;
-    }
-    if (!got) {
-      E = X_ERR;  // give up: reported as an internal error
-      if (lane == 0) atomicCAS((int*)&dp.status->code, 0, KX_ERR_INTERNAL);
-    }
-  }
-  out.e = E;
-  out.cnt = cnt;
-#pragma unroll
-  for (int v = 0; v < NV; v++) out.var[v] = var[v];
-  return out;
-}
-
-// one lane publishes a set of self-tagged words
-__device__ __forceinline__ void publish_words(const DecParams& dp, uint64_t t, int first, const uint64_t* vals,
-                                              int nwords) {
-  uint64_t* d = dp.desc + t + (uint64_t)first * dp.ntiles;
-  const uint64_t ep = dp.epoch << 48;
-  for (int i = 0; i < nwords; i++) astore64(d + (uint64_t)i * dp.ntiles, ep | (vals[i] & V48));
-}
-
-// ---------------------------------------------------------------------------------------------
-// the kernel: 4 independent waves per workgroup, one tile per wave
-// ---------------------------------------------------------------------------------------------
-// (the lane builtins return int: keep both halves unsigned so bit 31 never sign-extends)
-__device__ __forceinline__ uint64_t rfl64(uint64_t v) {
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
-  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-  return ((uint64_t)hi << 32) | lo;
 }
 
 // first canonical signature (3 bytes) in a lane's 128-byte segment, read from the LDS window:
@@ -858,363 +722,641 @@ __device__ __forceinline__ uint64_t scan_segment(const Src& w, int32_t q0, uint6
   return found;
 }
 
-template <int NV, int MODE>
-__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) decode_kernel(DecParams dp) {
-  __shared__ __attribute__((aligned(16))) uint32_t WIN[WAVES][WINW];
-  const int lane = threadIdx.x & 63;
-  const int wv = threadIdx.x >> 6;
-  const bool known = dp.offsets != nullptr;
-  const KxProgram* P = dp.prog;
-  const uint32_t nvar = MODE == M_THRIFT ? P->nvar : 0u;
-
-  // ---- tile ids in claim order (forward progress of the look-back): one claim per workgroup ----
-  __shared__ uint32_t wg_claim;
-  if (threadIdx.x == 0) wg_claim = atomicAdd(dp.counter, 1u);
-  __syncthreads();
-  const uint64_t t = (uint64_t)wg_claim * WAVES + wv;
-  if (t >= dp.ntiles) return;
-  uint64_t tp_last = dp.timing ? __builtin_amdgcn_s_memtime() : 0;
-  auto phase = [&](int k) {
-    if (dp.timing && lane == 0) {
-      const uint64_t now = __builtin_amdgcn_s_memtime();
-      atomicAdd(&g_phase[k], (unsigned long long)(now - tp_last));
-      tp_last = now;
-    }
-  };
-
-  // ---- this tile's range ----
-  uint64_t tlo, thi = 0, r0 = 0, r1 = 0;
-  if (known) {
-    r0 = t * dp.krec;
-    r1 = min(r0 + dp.krec, dp.n);
-    tlo = dp.offsets[r0];
-  } else {
-    tlo = t * (uint64_t)TILE;
-    thi = min(tlo + TILE, dp.in_len);
-  }
-
-  // ---- LDS window: HBM -> LDS by DMA, all chunks in flight together ----
-  LDS uint32_t* win = (LDS uint32_t*)WIN[wv];
+// ---------------------------------------------------------------------------------------------
+// the decode pipeline
+// ---------------------------------------------------------------------------------------------
+// HBM -> LDS window for input position `lo` (all DMA chunks in flight together)
+__device__ __forceinline__ Src load_window(KParams& dp, LDS uint32_t* win, uint64_t lo, int lane, bool thrift,
+                                           bool wait = true) {
   const uint64_t abs_in = (uint64_t)dp.in;
-  const uint64_t wbase = (abs_in + min(tlo, dp.in_len)) & ~15ull;
+  const uint64_t wbase = (abs_in + min(lo, dp.in_len)) & ~15ull;
   const int32_t wlen = dp.nolds ? 0 : (int32_t)min((uint64_t)WINB, abs_in + dp.in_len - wbase);
-  {
-    const int nch = (wlen + 15) >> 4;
-    const GLB uint8_t* g = (const GLB uint8_t*)wbase;
+  const int nch = (wlen + 15) >> 4;
+  const GLB uint8_t* g = (const GLB uint8_t*)wbase;
 #pragma unroll
-    for (int k = 0; k < WIN_LOADS; k++) {
-      const int c = k * 64 + lane;
-      if (c < nch)
-        __builtin_amdgcn_global_load_lds((const GLB void*)(g + (size_t)c * 16), (LDS void*)(win + k * 256), 16, 0, 0);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  for (int k = 0; k < WIN_LOADS; k++) {
+    const int c = k * 64 + lane;
+    if (c < nch)
+      __builtin_amdgcn_global_load_lds((const GLB void*)(g + (size_t)c * 16), (LDS void*)(win + k * 256), 16, 0, 0);
   }
-  const Src w{dp.in, dp.in_len, wbase - abs_in, wlen, win,
-              MODE == M_THRIFT ? P->steps : nullptr, MODE == M_THRIFT ? P->nsteps : 0u,
-              MODE == M_THRIFT ? P->canon_pres : 0ull};
-  phase(0);
+  if (wait) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const KxProgram* P = dp.prog;
+  return Src{dp.in, dp.in_len, wbase - abs_in, wlen, win, thrift ? P->steps : nullptr, thrift ? P->nsteps : 0u,
+             thrift ? P->canon_pres : 0ull};
+}
 
-  // ---- per-lane segment (concatenated) or record (offsets) ----
-  uint64_t seg_lo = 0, seg_hi = 0, lim = dp.in_len, rrec = 0;
-  bool mine = false;
-  int kerr = 0;
+// One record: FastRead (emit) or its length / var extents only (measure).
+template <int NV, int MODE>
+__device__ __forceinline__ int parse_record(KParams& dp, const Src& w, uint64_t pos, uint64_t lim, uint64_t r,
+                                            bool emit, uint64_t* end, VarState<NV>& vs, uint64_t& pres) {
+#pragma unroll
+  for (int v = 0; v < NV; v++) { vs.len[v] = 0; vs.pos[v] = 0; }
+  pres = 0;
+  if (MODE == M_THRIFT) {
+    if (w.nsteps && canon_record<NV>(w, dp.cols, pos, lim, r, emit, end, vs)) {
+      pres = w.canon_pres;
+      return KX_OK;
+    }
+    return generic_record<NV>(w, dp.prog, dp.cols, pos, lim, r, emit, end, vs, pres);
+  }
+  uint64_t p2 = pos;
+  const int rc = dskip_body(w, p2, lim, KX_T_STRUCT, 64);
+  *end = p2;
+  return rc;
+}
+
+struct Agg {
+  uint64_t ent, ex, cnt, errc, errp;
+  uint64_t var[KXP_NV_MAX];
+};
+
+// Concatenated mode, one wave, one tile [tlo, thi) in the LDS window. Lane l owns the 128-byte
+// segment l: it starts at the first canonical record signature in its segment (or where the chain
+// of the lane below enters it) and walks records until it leaves the segment. Lanes re-walk until
+// the chain is consistent (`seed` = the tile's true entry when known, else the lowest lane's
+// candidate is trusted). The record starts of the tile are written to `starts` (u16, relative to
+// tlo). Returns the tile aggregate (uniform).
+template <int NV, int MODE>
+__device__ Agg walk_tile(KParams& dp, const Src& w, uint64_t tlo, uint64_t thi, uint64_t seed, int lane,
+                         uint16_t* starts) {
+  const KxProgram* P = dp.prog;
+  const uint64_t seg_lo = tlo + (uint64_t)lane * SEG;
+  const uint64_t seg_hi = min(seg_lo + SEG, thi);
   uint64_t ent = X_NONE;
-  if (known) {
-    rrec = r0 + lane;
-    mine = rrec < r1;
-    if (mine) {
-      const uint64_t a = dp.offsets[rrec], b = dp.offsets[rrec + 1];
-      ent = a;
-      lim = b;
-      if (a > b || b > dp.in_len) kerr = KX_ERR_INVALID_ARG;
-    }
-  } else {
-    seg_lo = tlo + (uint64_t)lane * SEG;
-    seg_hi = min(seg_lo + SEG, thi);
-    if (seg_lo < thi) {
-      const uint32_t sig = MODE == M_THRIFT ? P->sig : (uint32_t)KX_T_STOP;
-      const uint32_t slen = (MODE == M_THRIFT && P->sig_len == 3) ? 3u : 1u;
-      const uint64_t plim = min(seg_hi, dp.in_len >= slen ? dp.in_len - slen + 1 : 0ull);
-      const int32_t q0 = wofs(w, seg_lo, SEG + 12);
-      if (slen == 3 && seg_hi - seg_lo == SEG && q0 >= 0) {
-        ent = scan_segment(w, q0, seg_lo, plim, sig);
-      } else {
-        const uint32_t smask = slen == 3 ? 0xffffffu : 0xffu;
-        for (uint64_t p = seg_lo; p < plim; p++)
-          if ((ld4(w, p) & smask) == sig) { ent = p; break; }
-      }
+  if (seg_lo < thi) {
+    const uint32_t sig = MODE == M_THRIFT ? P->sig : (uint32_t)KX_T_STOP;
+    const uint32_t slen = (MODE == M_THRIFT && P->sig_len == 3) ? 3u : 1u;
+    const uint64_t plim = min(seg_hi, dp.in_len >= slen ? dp.in_len - slen + 1 : 0ull);
+    const int32_t q0 = wofs(w, seg_lo, SEG + 12);
+    if (slen == 3 && seg_hi - seg_lo == SEG && q0 >= 0) {
+      ent = scan_segment(w, q0, seg_lo, plim, sig);
+    } else {
+      const uint32_t smask = slen == 3 ? 0xffffffu : 0xffu;
+      for (uint64_t p = seg_lo; p < plim; p++)
+        if ((ld4(w, p) & smask) == sig) { ent = p; break; }
     }
   }
-
-  // ---- walks: ONE instance of the record loop serves walk 1 (measure), the repair rounds and
-  //      walk 2 (emit); the state machine around it decides who walks next ----
-  uint64_t ex = X_NONE, cnt = 0;
+  uint64_t ex = X_NONE, cnt = 0, errp = 0;
+  int errc = 0;
   uint64_t vsum[NV > 0 ? NV : 1];
 #pragma unroll
   for (int v = 0; v < (NV > 0 ? NV : 1); v++) vsum[v] = 0;
-  bool need = known ? mine : ent != X_NONE;
-  int stage = 0;            // 0 speculative walk 1, 1 repair from the true entry, 2 emit
+  uint64_t st0 = 0, st1 = 0, st2 = 0, st3 = 0;  // the lane's first record starts
+  bool need = ent != X_NONE;
   int rounds = 0;
-  uint64_t seed = X_NONE;
-  bool ok = true;
-  int fel = 64;
-  uint64_t cpre = 0, tile_cnt = 0;
-  uint64_t vpre[NV > 0 ? NV : 1], tile_var[NV > 0 ? NV : 1];
-  uint64_t spec_ent = X_NONE, tile_exit = X_NONE;
-  LB lb;
-  lb.e = 0; lb.cnt = 0;
-  uint64_t rec = 0;
-  uint64_t run[NV > 0 ? NV : 1];
-  bool terminal = false;
-
-  auto write_final = [&](uint64_t nrec, uint64_t consumed) {
-    kx_status* st = dp.status;
-    st->n_records = nrec;
-    st->consumed = consumed;
-#pragma unroll
-    for (int v = 0; v < NV; v++) {
-      if (v >= (int)nvar) break;
-      st->var_total[v] = run[v];
-      dp.cols.offs[P->var_col[v]][nrec] = (uint32_t)run[v];
-    }
-  };
-
+  bool enumerate = false;   // second pass: lanes with > 4 records write the rest of their starts
+  uint64_t sbase = 0;
+  Agg a;
   for (;;) {
     if (need) {
-      const bool emit = stage == 2;
       uint64_t pos = ent, c = 0;
+      int e = 0;
       uint64_t acc[NV > 0 ? NV : 1];
 #pragma unroll
       for (int v = 0; v < (NV > 0 ? NV : 1); v++) acc[v] = 0;
-      int e = 0;
-      for (;;) {
-        if (!known && !(pos < seg_hi && pos < dp.in_len)) break;
-        if (emit && !known && rec >= dp.n) break;
-        const uint64_t r = known ? rrec : rec;
+      while (pos < seg_hi && pos < dp.in_len) {
         VarState<NV> vs;
-#pragma unroll
-        for (int v = 0; v < NV; v++) { vs.len[v] = 0; vs.pos[v] = 0; }
-        uint64_t pres = 0, end = pos;
-        int rc = kerr;
-        if (!rc) {
-          if (MODE == M_THRIFT) {
-            const bool canon = w.nsteps && canon_record<NV>(w, dp.cols, pos, lim, r, emit, &end, vs);
-            if (canon) pres = w.canon_pres;
-            else rc = generic_record<NV>(w, P, dp.cols, pos, lim, r, emit, &end, vs, pres);
-          } else {
-            uint64_t p2 = pos;
-            rc = dskip_body(w, p2, lim, KX_T_STRUCT, 64);
-            end = p2;
-            if (emit && !rc) dp.skip_out[r] = pos;
-          }
-        }
-        if (rc) {
-          e = rc;
-          if (!known) break;
-          // offsets mode: the failed record reads as all defaults, empty payloads
-#pragma unroll
-          for (int v = 0; v < NV; v++) vs.len[v] = 0;
-          pres = 0;
-          if (emit && MODE == M_THRIFT) emit_defaults(P, dp.cols, r);
-        }
-        if (emit && MODE == M_THRIFT) {
-#pragma unroll
-          for (int v = 0; v < NV; v++) {
-            if (v >= (int)nvar) break;
-            const uint32_t cc = P->var_col[v];
-            dp.cols.offs[cc][r] = (uint32_t)run[v];
-            const uint32_t nn = vs.len[v];
-            if (run[v] + nn <= dp.cols.cap[cc]) {
-              if (nn) {
-                const KxpCol K = ld_col(P, cc);
-                copy_var(w, K, vs.pos[v], nn, (uint8_t*)dp.cols.data[cc] + run[v] * K.width);
-              }
-            } else {
-              atomicOr(dp.overflow, 1u);
-            }
-            run[v] += nn;
-          }
-          if (dp.cols.presence) dp.cols.presence[r] = pres;
+        uint64_t end = pos, pres;
+        const int rc = parse_record<NV, MODE>(dp, w, pos, dp.in_len, 0, false, &end, vs, pres);
+        if (rc) { e = rc; break; }
+        if (!enumerate) {
+          st0 = c == 0 ? pos : st0; st1 = c == 1 ? pos : st1;
+          st2 = c == 2 ? pos : st2; st3 = c == 3 ? pos : st3;
+        } else if (c >= 4) {
+          starts[sbase + c] = (uint16_t)(pos - tlo);
         }
         c++;
 #pragma unroll
         for (int v = 0; v < NV; v++) acc[v] += vs.len[v];
         pos = end;
-        if (emit && !known) {
-          rec++;
-          if (rec == dp.n) {
-            write_final(dp.n, pos);
-            if (MODE == M_SKIP) dp.skip_out[dp.n] = pos;
-          }
-        }
-        if (known) break;
-      }
-      if (emit) {
-        if (known) {
-          if (e) atomicMin(dp.errkey, (unsigned long long)((rrec << 8) | (uint64_t)(e & 0xff)));
-          if (dp.rstat) dp.rstat[rrec] = (uint8_t)e;
-          if (rrec == dp.n - 1) write_final(dp.n, dp.offsets[dp.n]);
-        } else if (e) {
-          // the validated chain stops here (single writer: the only error on the chain)
-          kx_status* st = dp.status;
-          st->code = e; st->record = rec; st->offset = pos;
-          write_final(rec, pos);
-          if (MODE == M_SKIP) dp.skip_out[rec] = pos;
-        }
       }
       ex = e ? X_ERR : pos;
       cnt = c;
+      errc = e;
+      errp = pos;
 #pragma unroll
       for (int v = 0; v < NV; v++) vsum[v] = acc[v];
     }
     need = false;
-    if (stage == 2) break;
+    if (enumerate) break;
 
-    if (!known) {
-      // ---- one repair round: every lane must start at the first true record start in its
-      //      segment, i.e. where the previous walking lane's chain (or `seed`) leaves off ----
-      const uint64_t hm = __ballot(ent != X_NONE);
+    // ---- one repair round: every lane must start at the first true record start in its segment,
+    //      i.e. where the chain of the nearest lower walking lane (or `seed`) enters it ----
+    const uint64_t hm = __ballot(ent != X_NONE);
+    const uint64_t below = hm & ((1ull << lane) - 1);
+    const int pc = below ? 63 - __clzll((long long)below) : -1;
+    const uint64_t pex = __shfl(ex, pc < 0 ? 0 : pc, 64);
+    const uint64_t pe = pc >= 0 ? pex : seed;
+    uint64_t want = ent;
+    if (pe != X_NONE) {
+      if (pe == X_ERR || seg_lo >= thi || pe >= seg_hi) want = X_NONE;
+      else if (pe >= seg_lo) want = pe;
+    }
+    const bool ch = want != ent;
+    if (__ballot(ch)) {
+      if (++rounds <= 70) {  // from a fixed lowest entry the chain settles in <= 65 rounds
+        if (ch) {
+          ent = want;
+          need = ent != X_NONE;
+          ex = X_NONE; cnt = 0; errc = 0;
+#pragma unroll
+          for (int v = 0; v < NV; v++) vsum[v] = 0;
+        }
+        continue;
+      }
+      if (lane == 0) atomicCAS((int*)&dp.status->code, 0, KX_ERR_INTERNAL);
+    }
+
+    // ---- converged: the tile aggregate ----
+    const uint64_t em = __ballot(ent != X_NONE && ex == X_ERR);
+    const int fel = em ? __ffsll((long long)em) - 1 : 64;
+    const bool live = ent != X_NONE && lane <= fel;
+    const uint64_t c0 = live ? cnt : 0;
+    const uint64_t inc = wave_incl_scan(c0, lane);
+    const uint64_t cpre = inc - c0;
+    a.cnt = rl64(inc, 63);
+#pragma unroll
+    for (int v = 0; v < NV; v++) a.var[v] = wave_sum(live ? vsum[v] : 0);
+    a.ent = hm ? rl64(ent, __ffsll((long long)hm) - 1) : X_NONE;
+    a.ex = fel < 64 ? X_ERR : hm ? rl64(ex, 63 - __clzll((long long)hm)) : seed;
+    a.errc = fel < 64 ? (uint64_t)__builtin_amdgcn_readlane(errc, fel) : 0;
+    a.errp = fel < 64 ? rl64(errp, fel) : 0;
+    if (live) {
+      const uint64_t b = cpre;
+      if (cnt > 0) starts[b + 0] = (uint16_t)(st0 - tlo);
+      if (cnt > 1) starts[b + 1] = (uint16_t)(st1 - tlo);
+      if (cnt > 2) starts[b + 2] = (uint16_t)(st2 - tlo);
+      if (cnt > 3) starts[b + 3] = (uint16_t)(st3 - tlo);
+    }
+    if (__ballot(live && cnt > 4)) {
+      enumerate = true;
+      need = live && cnt > 4;
+      sbase = cpre;
+      continue;
+    }
+    break;
+  }
+  return a;
+}
+
+// Known-offsets mode: lane = record. Measures the var extents (failed records count as empty).
+template <int NV, int MODE>
+__device__ __forceinline__ Agg measure_records(KParams& dp, const Src& w, uint64_t r0, uint64_t r1, int lane) {
+  const uint64_t r = r0 + lane;
+  VarState<NV> vs;
+#pragma unroll
+  for (int v = 0; v < NV; v++) vs.len[v] = 0;
+  if (r < r1) {
+    const uint64_t a = dp.offsets[r], b = dp.offsets[r + 1];
+    uint64_t end, pres;
+    int rc = (a > b || b > dp.in_len) ? KX_ERR_INVALID_ARG : parse_record<NV, MODE>(dp, w, a, b, r, false, &end, vs, pres);
+    if (rc) {
+#pragma unroll
+      for (int v = 0; v < NV; v++) vs.len[v] = 0;
+    }
+  }
+  Agg g;
+  g.ent = X_NONE; g.ex = X_NONE; g.errc = 0; g.errp = 0;
+  g.cnt = r1 - r0;
+#pragma unroll
+  for (int v = 0; v < NV; v++) g.var[v] = wave_sum(vs.len[v]);
+  return g;
+}
+
+// tile geometry
+__device__ __forceinline__ void tile_range(KParams& dp, uint64_t t, uint64_t& lo, uint64_t& hi) {
+  if (dp.offsets) {
+    const uint64_t r0 = t * dp.krec, r1 = min(r0 + dp.krec, dp.n);
+    lo = r0; hi = r1;  // records
+  } else {
+    lo = t * (uint64_t)TILE;
+    hi = min(lo + TILE, dp.in_len);
+  }
+}
+
+// (re)walk tile t of a concatenated batch with the wave's LDS window
+template <int NV, int MODE>
+__device__ Agg tile_agg(KParams& dp, LDS uint32_t* win, uint64_t t, uint64_t seed, int lane) {
+  uint64_t lo, hi;
+  tile_range(dp, t, lo, hi);
+  if (dp.offsets) {
+    const Src w = load_window(dp, win, dp.offsets[lo], lane, MODE == M_THRIFT);
+    return measure_records<NV, MODE>(dp, w, lo, hi, lane);
+  }
+  const Src w = load_window(dp, win, lo, lane, MODE == M_THRIFT);
+  return walk_tile<NV, MODE>(dp, w, lo, hi, seed, lane, dp.starts + t * dp.slotcap);
+}
+
+__device__ __forceinline__ void put_tile(KParams& dp, uint64_t t, const Agg& a, int nv) {
+  const uint64_t ep = dp.epoch, nt = dp.ntiles;
+  put_word(dp.tdesc, nt, T_ENT, t, ep, a.ent);
+  put_word(dp.tdesc, nt, T_EXIT, t, ep, a.ex);
+  put_word(dp.tdesc, nt, T_CNT, t, ep, a.cnt);
+  put_word(dp.tdesc, nt, T_ERRC, t, ep, a.errc);
+  put_word(dp.tdesc, nt, T_ERRP, t, ep, a.errp);
+  for (int v = 0; v < nv; v++) put_word(dp.tdesc, nt, T_VAR + v, t, ep, a.var[v]);
+}
+
+// Does a chain arriving at `E` agree with an item whose speculative entry is `ent`? (An item with no
+// record start is a pass-through: the chain must jump over it.)
+__device__ __forceinline__ bool chain_ok(uint64_t E, uint64_t ent, uint64_t hi) {
+  if (E == X_ERR || E == X_DONE) return true;  // the chain already ended
+  if (ent == X_BAD) return false;
+  return ent == X_NONE ? E >= hi : ent == E;
+}
+
+// Group scan, one wave, lane = tile of group g. Validates the speculative chain between the tiles
+// (`entry` = the group's true entry when known, else X_NONE = trust the first tile that has a record
+// start), then writes each tile's exclusive prefix inside the group and the group aggregate.
+// REPAIR: a tile that disagrees is re-walked from its true entry; otherwise the group is marked
+// X_BAD and left to the chain pass (keeps the re-walk out of the index pass's registers).
+template <int NV, int MODE, bool REPAIR>
+__device__ void group_scan(KParams& dp, LDS uint32_t* win, uint64_t g, uint64_t entry, int lane) {
+  const uint64_t t0 = g * GT;
+  const uint64_t ntg = min((uint64_t)GT, dp.ntiles - t0);
+  const bool act = (uint64_t)lane < ntg;
+  const uint64_t t = t0 + lane;
+  const uint64_t ep = dp.epoch;
+  constexpr int NW = 5 + NV;
+  int fields[NW];
+#pragma unroll
+  for (int k = 0; k < NW; k++) fields[k] = k < 5 ? k : T_VAR + (k - 5);
+  uint64_t x[NW];
+  if (!get_words<NW>(dp.tdesc, dp.ntiles, fields, NW, act ? t : 0, ep, act, x)) {
+    if (lane == 0) atomicCAS((int*)&dp.status->code, 0, KX_ERR_INTERNAL);
+    return;
+  }
+  uint64_t ent = act ? x[0] : X_NONE, ex = act ? x[1] : X_NONE, cnt = act ? x[2] : 0;
+  uint64_t errc = act ? x[3] : 0, errp = act ? x[4] : 0;
+  uint64_t var[NV > 0 ? NV : 1];
+#pragma unroll
+  for (int v = 0; v < NV; v++) var[v] = act ? x[5 + v] : 0;
+  uint64_t lo, hi;
+  tile_range(dp, act ? t : t0, lo, hi);
+  if (!dp.offsets) {
+    // effective exit of every tile: its own, or (pass-through) the one it inherits
+    for (int guard = 0; guard < 4 * GT + 8; guard++) {
+      const uint64_t hm = __ballot(act && ent != X_NONE);
+      // expected entry of each tile = exit of the nearest lower tile with a record start, else `entry`
       const uint64_t below = hm & ((1ull << lane) - 1);
       const int pc = below ? 63 - __clzll((long long)below) : -1;
       const uint64_t pex = __shfl(ex, pc < 0 ? 0 : pc, 64);
-      const uint64_t pe = pc >= 0 ? pex : seed;
-      uint64_t want = ent;
-      if (pe != X_NONE) {
-        if (pe == X_ERR || pe == X_DONE || seg_lo >= thi || pe >= seg_hi) want = X_NONE;
-        else if (pe >= seg_lo) want = pe;
-      }
-      const bool ch = want != ent;
-      if (__ballot(ch)) {
-        if (++rounds <= (stage == 0 ? 8 : 70)) {
-          if (ch) {
-            ent = want;
-            need = ent != X_NONE;
-            ex = X_NONE;
-            cnt = 0;
-#pragma unroll
-            for (int v = 0; v < NV; v++) vsum[v] = 0;
-          }
-          continue;
+      const uint64_t E = pc >= 0 ? pex : entry;
+      const bool bad = act && E != X_NONE && !chain_ok(E, ent, hi);
+      const uint64_t bm = __ballot(bad);
+      if (!bm) break;
+      if (!REPAIR) {
+        if (lane == 0) {
+          const uint64_t ng = dp.ngroups;
+          put_word(dp.gdesc, ng, G_EXIT, g, ep, X_NONE);
+          put_word(dp.gdesc, ng, G_CNT, g, ep, 0);
+          put_word(dp.gdesc, ng, G_ERRC, g, ep, 0);
+          put_word(dp.gdesc, ng, G_ERRP, g, ep, 0);
+          for (int v = 0; v < NV; v++) put_word(dp.gdesc, ng, G_VAR + v, g, ep, 0);
+          put_word(dp.gdesc, ng, G_ENT, g, ep, X_BAD);
         }
-        if (stage == 1) {  // cannot happen: from the true entry the chain settles in <= 65 rounds
-          if (lane == 0) atomicCAS((int*)&dp.status->code, 0, KX_ERR_INTERNAL);
-          ent = X_NONE;
-        }
-        ok = false;
+        return;
       }
-      if (stage == 0 && rounds && lane == 0) atomicAdd((unsigned long long*)&dp.status->diag[2], 1ull);
-    }
-    if (stage == 0) phase(1);
-
-    // ---- wave prefix sums of record counts and arena bytes ----
-    {
-      const uint64_t em = known ? 0ull : __ballot(ent != X_NONE && ex == X_ERR);
-      fel = em ? __ffsll((long long)em) - 1 : 64;
-      const bool live = known ? mine : (ent != X_NONE && lane <= fel);
-      const uint64_t c0 = live ? cnt : 0;
-      const uint64_t inc = wave_incl_scan(c0, lane);
-      cpre = inc - c0;
-      tile_cnt = rl64(inc, 63);
+      // re-walk the first disagreeing tile from its true entry
+      const int b = __ffsll((long long)bm) - 1;
+      const uint64_t Eb = rl64(E, b);
+      if (lane == 0) atomicAdd((unsigned long long*)&dp.status->diag[0], 1ull);
+      const Agg a = tile_agg<NV, MODE>(dp, win, t0 + b, Eb, lane);
+      put_tile(dp, t0 + b, a, NV);
+      if (lane == b) {
+        ent = a.ent; ex = a.ex; cnt = a.cnt; errc = a.errc; errp = a.errp;
 #pragma unroll
-      for (int v = 0; v < NV; v++) {
-        const uint64_t x = live ? vsum[v] : 0;
-        const uint64_t vi = wave_incl_scan(x, lane);
-        vpre[v] = vi - x;
-        tile_var[v] = rl64(vi, 63);
-      }
-      if (!known) {
-        const uint64_t hm = __ballot(ent != X_NONE);
-        spec_ent = hm ? rl64(ent, __ffsll((long long)hm) - 1) : X_NONE;
-        tile_exit = fel < 64 ? X_ERR : hm ? rl64(ex, 63 - __clzll((long long)hm)) : (stage == 0 ? X_NONE : seed);
+        for (int v = 0; v < NV; v++) var[v] = a.var[v];
       }
     }
-
-    if (stage == 0) {
-      // ---- publish the aggregate, then look back ----
-      if (lane == 0 && (known || ok)) {
-        uint64_t words[3 + KXP_NV_MAX];
-        words[0] = tile_cnt;
-        words[1] = known ? X_NONE : spec_ent;
-        words[2] = known ? 0 : tile_exit;
-#pragma unroll
-        for (int v = 0; v < NV; v++) words[3 + v] = tile_var[v];
-        publish_words(dp, t, D_AGG_CNT, words, 3 + NV);
-      }
-      phase(2);
-      lb = lookback<NV>(dp, t, !known, lane);
-      lb.e = rfl64(lb.e);
-      lb.cnt = rfl64(lb.cnt);
-#pragma unroll
-      for (int v = 0; v < NV; v++) lb.var[v] = rfl64(lb.var[v]);
-      phase(3);
-      terminal = lb.e == X_ERR || lb.e == X_DONE || (!known && lb.cnt >= dp.n);
-      if (!known && !terminal) {
-        const bool valid = ok && (spec_ent == X_NONE ? lb.e >= thi : lb.e == spec_ent);
-        if (!valid) {
-          if (lane == 0) atomicAdd((unsigned long long*)&dp.status->diag[0], 1ull);
-          stage = 1;
-          seed = lb.e;
-          rounds = 0;
-          ok = true;
-          continue;
-        }
-        if (spec_ent == X_NONE) tile_exit = lb.e;  // pass-through tile
-      }
-    }
-
-    // ---- publish the inclusive prefix ----
-    if (lane == 0) {
-      uint64_t words[2 + KXP_NV_MAX];
-      uint64_t xo;
-      const uint64_t base = lb.cnt;
-      if (known) {
-        xo = 0;
-        words[0] = base + tile_cnt;
-      } else if (terminal) {
-        xo = lb.e == X_DONE || base >= dp.n ? X_DONE : X_ERR;
-        words[0] = base;
-      } else {
-        const uint64_t tot = base + tile_cnt;
-        xo = tile_exit;
-        if (tot >= dp.n) {
-          xo = X_DONE;
-        } else if (xo == dp.in_len) {
-          // the input ends before n records: EOF at record `tot`
-          xo = X_ERR;
-          kx_status* st = dp.status;
-          st->code = KX_ERR_EOF; st->record = tot; st->offset = dp.in_len;
-          st->n_records = tot; st->consumed = dp.in_len;
-#pragma unroll
-          for (int v = 0; v < NV; v++) {
-            if (v >= (int)nvar) break;
-            const uint64_t vt = lb.var[v] + tile_var[v];
-            st->var_total[v] = vt;
-            dp.cols.offs[P->var_col[v]][tot] = (uint32_t)vt;
-          }
-          if (MODE == M_SKIP) dp.skip_out[tot] = dp.in_len;
-        }
-        words[0] = tot;
-      }
-      words[1] = xo;
-#pragma unroll
-      for (int v = 0; v < NV; v++) words[2 + v] = lb.var[v] + tile_var[v];
-      publish_words(dp, t, D_INC_CNT, words, 2 + NV);
-    }
-    phase(4);
-    if (!known && terminal) break;
-
-    // ---- walk 2 ----
-    need = known ? mine : (ent != X_NONE && lane <= fel);
-    rec = lb.cnt + cpre;
-#pragma unroll
-    for (int v = 0; v < NV; v++) run[v] = lb.var[v] + vpre[v];
-    stage = 2;
   }
-  phase(5);
+  // the chain stops at the first erroring tile
+  const uint64_t em = __ballot(act && ex == X_ERR);
+  const int fe = em ? __ffsll((long long)em) - 1 : 64;
+  const bool live = act && lane <= fe;
+  const uint64_t c0 = live ? cnt : 0;
+  const uint64_t ci = wave_incl_scan(c0, lane);
+  uint64_t vpre[NV > 0 ? NV : 1], vtot[NV > 0 ? NV : 1];
+#pragma unroll
+  for (int v = 0; v < NV; v++) {
+    const uint64_t x0 = live ? var[v] : 0;
+    const uint64_t vi = wave_incl_scan(x0, lane);
+    vpre[v] = vi - x0;
+    vtot[v] = rl64(vi, 63);
+  }
+  if (act) {
+    put_word(dp.tdesc, dp.ntiles, T_PCNT, t, ep, ci - c0);
+#pragma unroll
+    for (int v = 0; v < NV; v++) put_word(dp.tdesc, dp.ntiles, T_PVAR + v, t, ep, vpre[v]);
+  }
+  const uint64_t hm = __ballot(act && ent != X_NONE);
+  const uint64_t gent = hm ? rl64(ent, __ffsll((long long)hm) - 1) : X_NONE;
+  const uint64_t gex = fe < 64 ? X_ERR : hm ? rl64(ex, 63 - __clzll((long long)hm)) : entry;
+  const uint64_t gcnt = rl64(ci, 63);
+  const uint64_t gerrc = fe < 64 ? rl64(errc, fe) : 0;
+  const uint64_t gerrp = fe < 64 ? rl64(errp, fe) : 0;
+  if (lane == 0) {
+    const uint64_t ng = dp.ngroups;
+    put_word(dp.gdesc, ng, G_ENT, g, ep, gent);
+    put_word(dp.gdesc, ng, G_EXIT, g, ep, gex);
+    put_word(dp.gdesc, ng, G_CNT, g, ep, gcnt);
+    put_word(dp.gdesc, ng, G_ERRC, g, ep, gerrc);
+    put_word(dp.gdesc, ng, G_ERRP, g, ep, gerrp);
+#pragma unroll
+    for (int v = 0; v < NV; v++) put_word(dp.gdesc, ng, G_VAR + v, g, ep, vtot[v]);
+  }
 }
 
-// Completes a call and re-arms the workspace for the next one (tile counter, error key, overflow).
-__global__ void finalize_kernel(kx_status* st, unsigned long long* errkey, uint32_t* overflow, uint32_t* counter,
+// ---- kernel 1: index pass (one wave per tile; the last wave of each group of 64 tiles scans it) ----
+template <int NV, int MODE>
+__global__ void __launch_bounds__(NT) index_kernel(DecParams dp_) {
+  KParams& dp = KX_PARAMS();
+  (void)dp_;
+  __shared__ __attribute__((aligned(16))) uint32_t WIN[WAVES][WINW];
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const uint64_t t = (uint64_t)blockIdx.x * WAVES + wv;
+  if (t >= dp.ntiles) return;
+  LDS uint32_t* win = (LDS uint32_t*)WIN[wv];
+  const Agg a = tile_agg<NV, MODE>(dp, win, t, t == 0 ? 0ull : X_NONE, lane);
+  if (lane == 0) put_tile(dp, t, a, NV);
+  const uint64_t g = t / GT;
+  // arrival count of the group (the counters are cleared at launch)
+  uint32_t old = 0;
+  if (lane == 0) old = atomicAdd(dp.gcount + g, 1u);
+  old = __shfl(old, 0, 64);
+  const uint64_t ntg = min((uint64_t)GT, dp.ntiles - g * GT);
+  if ((uint64_t)old == ntg - 1) group_scan<NV, MODE, false>(dp, win, g, g == 0 && !dp.offsets ? 0ull : X_NONE, lane);
+}
+
+// ---- kernel 2: chain + scan over the groups (one workgroup of 4 waves, lane = group) ----
+// Resolves the group chain from offset 0 (re-scanning a group from its true entry where the
+// speculation disagreed), writes every group's exclusive record / arena base, the number of records
+// to emit, and the final status when the chain ends early (decode error, input exhausted).
+template <int NV, int MODE>
+__global__ void __launch_bounds__(CT) chain_kernel(DecParams dp_) {
+  KParams& dp = KX_PARAMS();
+  (void)dp_;
+  __shared__ __attribute__((aligned(16))) uint32_t WIN0[WINW];
+  __shared__ uint64_t s_wcnt[CW], s_wvar[CW][KXP_NV_MAX], s_wlast[CW];
+  __shared__ int s_werr[CW];
+  __shared__ uint64_t s_E, s_cnt, s_var[KXP_NV_MAX], s_nstop, s_badE;
+  __shared__ int s_bad, s_err, s_done;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const uint64_t ep = dp.epoch, ng = dp.ngroups;
+  const bool chain = !dp.offsets;
+  if (tid == 0) {
+    s_E = 0;  // the chain enters group 0 at offset 0
+    s_cnt = 0;
+    for (int v = 0; v < KXP_NV_MAX; v++) s_var[v] = 0;
+    s_nstop = dp.n;
+    s_err = 0;
+    s_done = 0;
+  }
+  __syncthreads();
+  for (uint64_t b0 = 0; b0 < ng; b0 += CT) {
+    if (s_err || s_done) {  // the chain already ended: later groups emit nothing
+      const uint64_t g = b0 + tid;
+      if (g < ng) put_word(dp.gdesc, ng, G_BCNT, g, ep, X_DONE);
+      continue;
+    }
+    const uint64_t g = b0 + tid;
+    const bool act = g < ng;
+    uint64_t gent, gex, cnt, errc, errp, var[NV > 0 ? NV : 1];
+    uint64_t base, vbase[NV > 0 ? NV : 1], c0, vx[NV > 0 ? NV : 1];
+    bool live, dead;
+    int fe;
+    for (;;) {
+      constexpr int NW = 5 + NV;
+      int fields[NW];
+#pragma unroll
+      for (int k = 0; k < NW; k++) fields[k] = k < 5 ? k : G_VAR + (k - 5);
+      uint64_t x[NW];
+      if (!get_words<NW>(dp.gdesc, ng, fields, NW, act ? g : 0, ep, act, x) && lane == 0)
+        atomicCAS((int*)&dp.status->code, 0, KX_ERR_INTERNAL);
+      gent = act ? x[0] : X_NONE; gex = act ? x[1] : X_NONE; cnt = act ? x[2] : 0;
+      errc = act ? x[3] : 0; errp = act ? x[4] : 0;
+#pragma unroll
+      for (int v = 0; v < NV; v++) var[v] = act ? x[5 + v] : 0;
+      // the chain stops at the first erroring group
+      const uint64_t em = __ballot(act && chain && gex == X_ERR);
+      fe = em ? __ffsll((long long)em) - 1 : 64;
+      live = act && lane <= fe;
+      c0 = live ? cnt : 0;
+      const uint64_t ci = wave_incl_scan(c0, lane);
+#pragma unroll
+      for (int v = 0; v < NV; v++) {
+        const uint64_t x0 = live ? var[v] : 0;
+        const uint64_t vi = wave_incl_scan(x0, lane);
+        vx[v] = vi - x0;
+        if (lane == 63) s_wvar[wv][v] = vi;
+      }
+      const uint64_t hm = __ballot(act && gent != X_NONE && gent != X_BAD);
+      if (lane == 63) s_wcnt[wv] = ci;
+      const uint64_t wlast = hm ? rl64(gex, 63 - __clzll((long long)hm)) : X_NONE;
+      if (lane == 0) {
+        s_wlast[wv] = wlast;
+        s_werr[wv] = em != 0;
+      }
+      if (tid == 0) s_bad = 1 << 30;
+      __syncthreads();
+      base = s_cnt + ci - c0;
+      dead = false;
+#pragma unroll
+      for (int v = 0; v < NV; v++) vbase[v] = s_var[v] + vx[v];
+      uint64_t Ein = s_E;
+      for (int k = 0; k < wv; k++) {
+        base += s_wcnt[k];
+#pragma unroll
+        for (int v = 0; v < NV; v++) vbase[v] += s_wvar[k][v];
+        dead |= s_werr[k] != 0;
+        if (s_wlast[k] != X_NONE) Ein = s_wlast[k];
+      }
+      if (!chain) break;
+      // expected entry = effective exit of the nearest lower group with a record start
+      const uint64_t below = hm & ((1ull << lane) - 1);
+      const int pc = below ? 63 - __clzll((long long)below) : -1;
+      const uint64_t pex = __shfl(gex, pc < 0 ? 0 : pc, 64);
+      const uint64_t E = pc >= 0 ? pex : Ein;
+      const uint64_t hi = min((g + 1) * (uint64_t)GT * TILE, dp.in_len);
+      const bool bad = live && !dead && base < dp.n && !chain_ok(E, gent, hi);
+      if (bad) atomicMin(&s_bad, tid);
+      __syncthreads();
+      const int b = s_bad;
+      if (b == (1 << 30)) break;
+      if (tid == b) s_badE = E;
+      __syncthreads();
+      if (wv == 0) {  // re-scan the first disagreeing group from its true entry, then re-check
+        if (lane == 0) atomicAdd((unsigned long long*)&dp.status->diag[1], 1ull);
+        group_scan<NV, MODE, true>(dp, (LDS uint32_t*)WIN0, b0 + b, s_badE, lane);
+      }
+      __syncthreads();
+    }
+    if (act) {
+      put_word(dp.gdesc, ng, G_BCNT, g, ep, (dead || !live) ? X_DONE : base);
+#pragma unroll
+      for (int v = 0; v < NV; v++) put_word(dp.gdesc, ng, G_BVAR + v, g, ep, vbase[v]);
+    }
+    // a decode error ends the chain (reported only when it falls before record n)
+    if (chain && !dead && fe < 64 && lane == fe) {
+      const uint64_t rec = base + cnt;  // records decoded before the failing one
+      if (rec < dp.n) {
+        kx_status* st = dp.status;
+        st->code = (int32_t)errc; st->record = rec; st->offset = errp;
+        st->n_records = rec; st->consumed = errp;
+#pragma unroll
+        for (int v = 0; v < NV; v++) {
+          if (v >= (int)dp.prog->nvar) break;
+          const uint64_t vt = vbase[v] + var[v];
+          st->var_total[v] = vt;
+          dp.cols.offs[dp.prog->var_col[v]][rec] = (uint32_t)vt;
+        }
+        if (MODE == M_SKIP) dp.skip_out[rec] = errp;
+        s_nstop = rec;
+      }
+      s_err = 1;
+    }
+    __syncthreads();
+    if (tid == 0) {  // carry into the next batch
+      bool stop = false;
+      for (int k = 0; k < CW && !stop; k++) {
+        s_cnt += s_wcnt[k];
+        for (int v = 0; v < NV; v++) s_var[v] += s_wvar[k][v];
+        if (s_wlast[k] != X_NONE) s_E = s_wlast[k];
+        stop = s_werr[k] != 0;
+      }
+      if (s_cnt >= dp.n) s_done = 1;
+    }
+    __syncthreads();
+  }
+  // the chain ran out of input before n records: EOF at the record after the last one
+  if (tid == 0) {
+    const uint64_t tot = s_cnt;
+    if (chain && !s_err && tot < dp.n) {
+      kx_status* st = dp.status;
+      st->code = KX_ERR_EOF; st->record = tot; st->offset = dp.in_len;
+      st->n_records = tot; st->consumed = dp.in_len;
+      for (int v = 0; v < NV; v++) {
+        if (v >= (int)dp.prog->nvar) break;
+        st->var_total[v] = s_var[v];
+        dp.cols.offs[dp.prog->var_col[v]][tot] = (uint32_t)s_var[v];
+      }
+      if (MODE == M_SKIP) dp.skip_out[tot] = dp.in_len;
+      s_nstop = tot;
+    }
+    *dp.nstop = s_nstop;
+  }
+}
+
+// ---- kernel 3: emit pass (one wave per tile, lane = record) ----
+template <int NV, int MODE>
+__global__ void __launch_bounds__(NT) emit_kernel(DecParams dp_) {
+  KParams& dp = KX_PARAMS();
+  (void)dp_;
+  __shared__ __attribute__((aligned(16))) uint32_t WIN[WAVES][WINW];
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const uint64_t t = (uint64_t)blockIdx.x * WAVES + wv;
+  if (t >= dp.ntiles) return;
+  const KxProgram* P = dp.prog;
+  const bool known = dp.offsets != nullptr;
+  const uint64_t ep = dp.epoch;
+  const uint64_t nstop = known ? dp.n : *(volatile uint64_t*)dp.nstop;
+  uint64_t lo, hi;
+  tile_range(dp, t, lo, hi);
+  // the window DMA is issued first; the tile's bases are read while it is in flight
+  LDS uint32_t* win = (LDS uint32_t*)WIN[wv];
+  const uint16_t* starts = dp.starts + t * dp.slotcap;
+  const Src w = load_window(dp, win, known ? dp.offsets[lo] : lo, lane, MODE == M_THRIFT, false);
+  uint64_t base = 0, cnt = 0, run[NV > 0 ? NV : 1];
+#pragma unroll
+  for (int v = 0; v < (NV > 0 ? NV : 1); v++) run[v] = 0;
+  if (dp.direct) {  // offsets mode without var columns: no index pass
+    base = lo;
+    cnt = hi - lo;
+  } else {
+    const uint64_t g = t / GT;
+    // written by earlier kernels of this call: plain (cached) loads suffice
+    const uint64_t* gd = dp.gdesc;
+    const uint64_t* td = dp.tdesc;
+    const uint64_t gb = gd[(uint64_t)G_BCNT * dp.ngroups + g] & V48;
+    base = gb + (td[(uint64_t)T_PCNT * dp.ntiles + t] & V48);
+    cnt = gb == X_DONE ? 0 : td[(uint64_t)T_CNT * dp.ntiles + t] & V48;
+#pragma unroll
+    for (int v = 0; v < NV; v++)
+      run[v] = (gd[(uint64_t)(G_BVAR + v) * dp.ngroups + g] & V48) + (td[(uint64_t)(T_PVAR + v) * dp.ntiles + t] & V48);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (cnt == 0 || base >= nstop) return;
+  cnt = min(cnt, nstop - base);
+  for (uint64_t j0 = 0; j0 < cnt; j0 += 64) {
+    const uint64_t j = j0 + lane;
+    const bool act = j < cnt;
+    const uint64_t r = base + j;
+    VarState<NV> vs;
+#pragma unroll
+    for (int v = 0; v < NV; v++) { vs.len[v] = 0; vs.pos[v] = 0; }
+    uint64_t pos = 0, lim = dp.in_len, end = 0, pres = 0;
+    int rc = 0;
+    if (act) {
+      if (known) {
+        pos = dp.offsets[r];
+        lim = dp.offsets[r + 1];
+        if (pos > lim || lim > dp.in_len) rc = KX_ERR_INVALID_ARG;
+      } else {
+        pos = lo + starts[j];
+      }
+      if (!rc) rc = parse_record<NV, MODE>(dp, w, pos, lim, r, MODE == M_THRIFT, &end, vs, pres);
+      if (rc) {  // offsets mode: the failed record reads as all defaults, empty payloads
+#pragma unroll
+        for (int v = 0; v < NV; v++) vs.len[v] = 0;
+        pres = 0;
+        if (MODE == M_THRIFT) emit_defaults(P, dp.cols, r);
+      }
+      if (MODE == M_SKIP) dp.skip_out[r] = pos;
+      if (MODE == M_THRIFT && dp.cols.presence) dp.cols.presence[r] = pres;
+      if (known) {
+        if (rc) atomicMin(dp.errkey, (unsigned long long)((r << 8) | (uint64_t)(rc & 0xff)));
+        if (dp.rstat) dp.rstat[r] = (uint8_t)rc;
+      }
+    }
+    // arena positions: wave exclusive scan of the var lengths
+#pragma unroll
+    for (int v = 0; v < NV; v++) {
+      if (v >= (int)P->nvar) break;
+      const uint64_t x0 = act ? vs.len[v] : 0;
+      const uint64_t xi = wave_incl_scan(x0, lane);
+      const uint64_t at = run[v] + xi - x0;
+      const uint32_t cc = P->var_col[v];
+      if (act) {
+        dp.cols.offs[cc][r] = (uint32_t)at;
+        const uint32_t nn = vs.len[v];
+        if (at + nn <= dp.cols.cap[cc]) {
+          if (nn) {
+            const KxpCol K = ld_col(P, cc);
+            copy_var(w, K, vs.pos[v], nn, (uint8_t*)dp.cols.data[cc] + at * K.width);
+          }
+        } else {
+          atomicOr(dp.overflow, 1u);
+        }
+      }
+      if (act && r == nstop - 1 && nstop == dp.n) {
+        dp.status->var_total[v] = at + vs.len[v];
+        dp.cols.offs[cc][dp.n] = (uint32_t)(at + vs.len[v]);
+      }
+      run[v] += rl64(xi, 63);
+    }
+    if (act && r == nstop - 1 && nstop == dp.n) {
+      kx_status* st = dp.status;
+      st->n_records = dp.n;
+      st->consumed = known ? dp.offsets[dp.n] : end;
+      if (MODE == M_SKIP) dp.skip_out[dp.n] = end;
+    }
+  }
+}
+
+// Completes a call and re-arms the workspace for the next one (error key, overflow, nstop).
+__global__ void finalize_kernel(kx_status* st, unsigned long long* errkey, uint32_t* overflow, uint64_t* nstop,
                                 const uint64_t* offsets, uint64_t n) {
   if (threadIdx.x != 0) return;
   unsigned long long k = *errkey;
@@ -1227,15 +1369,18 @@ __global__ void finalize_kernel(kx_status* st, unsigned long long* errkey, uint3
   if (offsets) st->n_records = n;
   *errkey = ~0ull;
   *overflow = 0;
-  *counter = 0;
+  *nstop = ~0ull;
 }
 
-// workspace: [0] tile counter u32, [8] errkey u64, [16] overflow u32, [256...) tile descriptors
-constexpr size_t WS_DESC = 256;
+// ---- workspace: [8] errkey u64, [16] overflow u32, [24] nstop u64, then tile words, group words,
+//      group arrival counters, record-start slots ----
+constexpr size_t WS_HDR = 256;
 
-size_t ws_total(uint64_t ntiles) { return WS_DESC + ntiles * DFIELDS * 8; }
+struct WsLayout {
+  uint64_t ntiles, ngroups, slotcap;
+  size_t tdesc, gdesc, gcount, starts, total;
+};
 
-// offsets mode: records per tile so that a tile's bytes fit the LDS window on average
 uint32_t krec_for(uint64_t in_len, uint64_t n) {
   if (n == 0) return 64;
   const uint64_t avg = (in_len + n - 1) / n;
@@ -1243,53 +1388,78 @@ uint32_t krec_for(uint64_t in_len, uint64_t n) {
   return (uint32_t)(k < 1 ? 1 : k > 64 ? 64 : k);
 }
 
-uint64_t tiles_for(uint64_t in_len, const uint64_t* offsets, uint64_t n) {
-  const uint64_t nt = offsets ? (n + krec_for(in_len, n) - 1) / krec_for(in_len, n) : (in_len + TILE - 1) / TILE;
-  return nt ? nt : 1;
+WsLayout ws_layout(uint64_t min_rec, uint64_t in_len, const uint64_t* offsets, uint64_t n) {
+  WsLayout L{};
+  if (offsets) {
+    const uint64_t k = krec_for(in_len, n);
+    L.ntiles = (n + k - 1) / k;
+    L.slotcap = 0;
+  } else {
+    L.ntiles = (in_len + TILE - 1) / TILE;
+    // a record can be a single STOP byte whatever the schema's encoded minimum: every byte of
+    // the tile may start one
+    (void)min_rec;
+    L.slotcap = (uint64_t)TILE + 1;
+  }
+  if (!L.ntiles) L.ntiles = 1;
+  L.slotcap = (L.slotcap + 3) & ~3ull;
+  L.ngroups = (L.ntiles + GT - 1) / GT;
+  size_t o = WS_HDR;
+  L.tdesc = o; o += (size_t)L.ntiles * T_NF * 8;
+  L.gdesc = o; o += (size_t)L.ngroups * G_NF * 8;
+  L.gcount = o; o += ((size_t)L.ngroups * 4 + 255) & ~(size_t)255;
+  L.starts = o; o += ((size_t)L.ntiles * L.slotcap * 2 + 255) & ~(size_t)255;
+  L.total = o;
+  return L;
 }
 
 template <int NV, int MODE>
-int launch_t(const DecParams& dp0, void* ws, hipStream_t stream) {
+int launch_t(const DecParams& dp0, const WsLayout& L, void* ws, hipStream_t stream) {
   DecParams dp = dp0;
   char* base = (char*)ws;
-  dp.counter = (uint32_t*)base;
   dp.errkey = (unsigned long long*)(base + 8);
   dp.overflow = (uint32_t*)(base + 16);
-  dp.desc = (uint64_t*)(base + WS_DESC);
+  dp.nstop = (uint64_t*)(base + 24);
+  dp.tdesc = (uint64_t*)(base + L.tdesc);
+  dp.gdesc = (uint64_t*)(base + L.gdesc);
+  dp.gcount = (uint32_t*)(base + L.gcount);
+  dp.starts = (uint16_t*)(base + L.starts);
+  dp.ntiles = L.ntiles;
+  dp.ngroups = L.ngroups;
+  dp.slotcap = L.slotcap;
+  dp.direct = dp.offsets && NV == 0;
   KX_HIP_CHECK(hipMemsetAsync(dp.status, 0, sizeof(kx_status), stream));
   const unsigned grid = (unsigned)((dp.ntiles + WAVES - 1) / WAVES);
-  hipLaunchKernelGGL((decode_kernel<NV, MODE>), dim3(grid), dim3(NT), 0, stream, dp);
+  if (!dp.direct) {
+    // a plain arrival counter per group, cleared here: a CAS-tagged counter costs retries when the
+    // 64 waves of a group finish together
+    KX_HIP_CHECK(hipMemsetAsync(dp.gcount, 0, (size_t)dp.ngroups * 4, stream));
+    hipLaunchKernelGGL((index_kernel<NV, MODE>), dim3(grid), dim3(NT), 0, stream, dp);
+    KX_HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL((chain_kernel<NV, MODE>), dim3(1), dim3(CT), 0, stream, dp);
+    KX_HIP_CHECK(hipGetLastError());
+  }
+  hipLaunchKernelGGL((emit_kernel<NV, MODE>), dim3(grid), dim3(NT), 0, stream, dp);
   KX_HIP_CHECK(hipGetLastError());
-  hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(64), 0, stream, dp.status, dp.errkey, dp.overflow,
-                     dp.counter, dp.offsets, dp.n);
+  hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(64), 0, stream, dp.status, dp.errkey, dp.overflow, dp.nstop,
+                     dp.offsets, dp.n);
   KX_HIP_CHECK(hipGetLastError());
   return KX_OK;
 }
 
 void fill_diag_flags(DecParams& dp) {
-  static int timing = -1, nolds = -1;
-  if (timing < 0) { const char* e = getenv("KX_PHASE_TIMING"); timing = e && e[0] == '1'; }
+  static int nolds = -1;
   if (nolds < 0) { const char* e = getenv("KX_NOLDS"); nolds = e && e[0] == '1'; }
-  dp.timing = timing;
   dp.nolds = nolds;
 }
 
 }  // namespace
 
-size_t kx_decode_ws_bytes(const KxProgram&, uint64_t in_len, const uint64_t* offsets, uint64_t n) {
-  return ws_total(tiles_for(in_len, offsets, n));
+size_t kx_decode_ws_bytes(const KxProgram& hprog, uint64_t in_len, const uint64_t* offsets, uint64_t n) {
+  return ws_layout(hprog.fixed_min, in_len, offsets, n).total;
 }
 
-size_t kx_skip_ws_bytes(uint64_t in_len) { return ws_total(tiles_for(in_len, nullptr, 0)); }
-
-// diagnostics (not part of the public ABI): read and reset the phase-timing accumulators
-extern "C" int kx_debug_phase_cycles(unsigned long long* out, int n) {
-  if (n > 10) n = 10;
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase), sizeof(unsigned long long) * n) != hipSuccess) return KX_ERR_HIP;
-  unsigned long long z[10] = {0};
-  if (hipMemcpyToSymbol(HIP_SYMBOL(g_phase), z, sizeof z) != hipSuccess) return KX_ERR_HIP;
-  return KX_OK;
-}
+size_t kx_skip_ws_bytes(uint64_t in_len) { return ws_layout(1, in_len, nullptr, 0).total; }
 
 int kx_launch_decode(const KxProgram* dprog, const KxProgram& hprog, const uint8_t* in, uint64_t in_len,
                      const uint64_t* offsets, uint64_t n, const KxLaunchCols& cols, uint8_t* record_status,
@@ -1300,14 +1470,14 @@ int kx_launch_decode(const KxProgram* dprog, const KxProgram& hprog, const uint8
   dp.in = in; dp.in_len = in_len; dp.offsets = offsets; dp.n = n; dp.prog = dprog;
   dp.cols = cols; dp.rstat = record_status; dp.status = status; dp.epoch = epoch;
   dp.krec = krec_for(in_len, n);
-  dp.ntiles = tiles_for(in_len, offsets, n);
-  if (ws_size < ws_total(dp.ntiles)) return KX_ERR_INVALID_ARG;
+  const WsLayout L = ws_layout(hprog.fixed_min, in_len, offsets, n);
+  if (ws_size < L.total) return KX_ERR_INVALID_ARG;
   switch (hprog.nvar) {
-    case 0: return launch_t<0, M_THRIFT>(dp, ws, stream);
-    case 1: return launch_t<1, M_THRIFT>(dp, ws, stream);
-    case 2: return launch_t<2, M_THRIFT>(dp, ws, stream);
-    case 3: case 4: return launch_t<4, M_THRIFT>(dp, ws, stream);
-    default: return launch_t<8, M_THRIFT>(dp, ws, stream);
+    case 0: return launch_t<0, M_THRIFT>(dp, L, ws, stream);
+    case 1: return launch_t<1, M_THRIFT>(dp, L, ws, stream);
+    case 2: return launch_t<2, M_THRIFT>(dp, L, ws, stream);
+    case 3: case 4: return launch_t<4, M_THRIFT>(dp, L, ws, stream);
+    default: return launch_t<8, M_THRIFT>(dp, L, ws, stream);
   }
 }
 
@@ -1318,7 +1488,7 @@ int kx_launch_skip(const uint8_t* in, uint64_t in_len, uint64_t n, uint64_t* off
   dp.in = in; dp.in_len = in_len; dp.offsets = nullptr; dp.n = n; dp.prog = nullptr;
   dp.status = status; dp.skip_out = offsets_out; dp.epoch = epoch;
   dp.krec = 64;
-  dp.ntiles = tiles_for(in_len, nullptr, n);
-  if (ws_size < ws_total(dp.ntiles)) return KX_ERR_INVALID_ARG;
-  return launch_t<0, M_SKIP>(dp, ws, stream);
+  const WsLayout L = ws_layout(1, in_len, nullptr, n);
+  if (ws_size < L.total) return KX_ERR_INVALID_ARG;
+  return launch_t<0, M_SKIP>(dp, L, ws, stream);
 }

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Test infrastructure only: build the CPU SIMT emulation of the decode kernel (tests/emu/_build).
 # The kernel source is compiled as host C++ against tests/emu/hip/hip_runtime.h; the two
-# device-only spellings it uses (address-space qualifiers, the vmcnt wait) are rewritten on the
+# device-only spellings it uses (address-space qualifiers, the in-place kernarg read, the vmcnt wait) are rewritten on the
 # way in. Nothing here is linked into libkxcodec.so.
 set -e
 cd "$(dirname "$0")"
@@ -9,6 +9,8 @@ ROOT=../..
 mkdir -p _build
 sed -e 's/^#define LDS __attribute__((address_space(3)))/#define LDS/' \
     -e 's/^#define GLB __attribute__((address_space(1)))/#define GLB/' \
+    -e 's/^#define KAS __attribute__((address_space(4))).*/#define KAS/' \
+    -e 's/^#define KX_PARAMS() .*/#define KX_PARAMS() (dp_)/' \
     -e 's/__attribute__((amdgpu_waves_per_eu([0-9]*))) //' \
     -e 's/asm volatile("s_waitcnt vmcnt(0)" ::: "memory");/emu_wait_vmcnt0();/' \
     $ROOT/kitex_amd/csrc/kx_decode.hip > _build/kx_decode_emu.cpp

@@ -20,13 +20,26 @@ extern "C" int emu_decode(const kx_struct_desc* structs, uint32_t nstructs, cons
     lc.presence = out->presence;
   }
   size_t ws_size = skip ? kx_skip_ws_bytes(in_len) : kx_decode_ws_bytes(s.prog, in_len, offsets, n);
-  char* ws = (char*)calloc(1, ws_size);
-  memset(ws + 8, 0xff, 8);
+  // one workspace reused across calls with a fresh epoch each time, exactly like a kx_ctx
+  // (kx_capi.cpp ensure_ws): stale words / counters of earlier calls must never leak into a call
+  static char* ws = nullptr;
+  static size_t ws_cap = 0;
+  static uint64_t epoch = 0xffff;
+  if (ws_cap < ws_size) {
+    free(ws);
+    ws_cap = ws_size + ws_size / 4;
+    ws = (char*)malloc(ws_cap);
+    epoch = 0xffff;
+  }
+  if (++epoch > 0xffff) {
+    memset(ws, 0, ws_cap);
+    memset(ws + 8, 0xff, 8);
+    epoch = 1;
+  }
   if (skip)
-    rc = kx_launch_skip(in, in_len, n, skip_out, status, ws, ws_size, 1, nullptr);
+    rc = kx_launch_skip(in, in_len, n, skip_out, status, ws, ws_cap, epoch, nullptr);
   else
-    rc = kx_launch_decode(&s.prog, s.prog, in, in_len, offsets, n, lc, record_status, status, ws, ws_size, 1,
+    rc = kx_launch_decode(&s.prog, s.prog, in, in_len, offsets, n, lc, record_status, status, ws, ws_cap, epoch,
                           nullptr, false);
-  free(ws);
   return rc;
 }
