@@ -85,6 +85,8 @@ struct DecParams {
   uint32_t krec;             // offsets mode: records per tile (<= 64)
   int direct;                // offsets mode without var columns: emit pass only
   int nolds;                 // diagnostics (KX_NOLDS=1): read every byte from global memory
+  int diag;                  // diagnostics (KX_DIAG bits, timing experiments only; output is wrong):
+                             // 1 no walk, 2 no group arrival, 4 no tile words, 256 index pass only
 };
 
 // Kernels read their parameter block in place from the kernarg segment: indexing a by-value
@@ -1078,8 +1080,18 @@ __global__ void __launch_bounds__(NT) index_kernel(DecParams dp_) {
   const uint64_t t = (uint64_t)blockIdx.x * WAVES + wv;
   if (t >= dp.ntiles) return;
   LDS uint32_t* win = (LDS uint32_t*)WIN[wv];
-  const Agg a = tile_agg<NV, MODE>(dp, win, t, t == 0 ? 0ull : X_NONE, lane);
-  if (lane == 0) put_tile(dp, t, a, NV);
+  Agg a;
+  if (dp.diag & 1) {
+    uint64_t lo, hi;
+    tile_range(dp, t, lo, hi);
+    const Src w = load_window(dp, win, dp.offsets ? dp.offsets[lo] : lo, lane, MODE == M_THRIFT);
+    a.ent = lo + (w.win[lane] & 1); a.ex = hi; a.cnt = 0; a.errc = 0; a.errp = 0;
+    for (int v = 0; v < NV; v++) a.var[v] = 0;
+  } else {
+    a = tile_agg<NV, MODE>(dp, win, t, t == 0 ? 0ull : X_NONE, lane);
+  }
+  if (lane == 0 && !(dp.diag & 4)) put_tile(dp, t, a, NV);
+  if (dp.diag & 2) return;
   const uint64_t g = t / GT;
   // arrival count of the group (the counters are cleared at launch)
   uint32_t old = 0;
@@ -1430,6 +1442,11 @@ int launch_t(const DecParams& dp0, const WsLayout& L, void* ws, hipStream_t stre
   dp.direct = dp.offsets && NV == 0;
   KX_HIP_CHECK(hipMemsetAsync(dp.status, 0, sizeof(kx_status), stream));
   const unsigned grid = (unsigned)((dp.ntiles + WAVES - 1) / WAVES);
+  if (dp.diag & 256) {
+    KX_HIP_CHECK(hipMemsetAsync(dp.gcount, 0, (size_t)dp.ngroups * 4, stream));
+    hipLaunchKernelGGL((index_kernel<NV, MODE>), dim3(grid), dim3(NT), 0, stream, dp);
+    return KX_OK;
+  }
   if (!dp.direct) {
     // a plain arrival counter per group, cleared here: a CAS-tagged counter costs retries when the
     // 64 waves of a group finish together
@@ -1448,9 +1465,11 @@ int launch_t(const DecParams& dp0, const WsLayout& L, void* ws, hipStream_t stre
 }
 
 void fill_diag_flags(DecParams& dp) {
-  static int nolds = -1;
+  static int nolds = -1, diag = -1;
   if (nolds < 0) { const char* e = getenv("KX_NOLDS"); nolds = e && e[0] == '1'; }
+  if (diag < 0) { const char* e = getenv("KX_DIAG"); diag = e ? atoi(e) : 0; }
   dp.nolds = nolds;
+  dp.diag = diag;
 }
 
 }  // namespace

@@ -1,11 +1,11 @@
-"""Diagnostic: decode kernel time under KX_ABLATE variants (each in its own process)."""
+"""Diagnostic: decode-call time under KX_DIAG variants (each in its own process; output not checked)."""
 import os
 import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CHILD = r'''
-import os, sys, time
+import os, sys
 sys.path.insert(0, %r)
 import torch
 from kitex_amd import _abi as A, schema as S, synth
@@ -34,10 +34,11 @@ print("%%.3f" %% (e0.elapsed_time(e1) / 5))
 ''' % ROOT
 cfg = sys.argv[1] if len(sys.argv) > 1 else "r2"
 n = sys.argv[2] if len(sys.argv) > 2 else str(16 << 20)
+variants = sys.argv[3].split(",") if len(sys.argv) > 3 else ["0", "256", "257", "258", "262", "263"]
 for mode in ("concat",):
-    for ab in ["0", "1", "2", "4", "6", "7"]:
-        env = dict(os.environ, KX_ABLATE=ab)
+    for ab in variants:
+        env = dict(os.environ, KX_DIAG=ab)
         r = subprocess.run([sys.executable, "-c", CHILD, cfg, n, mode], env=env, capture_output=True, text=True,
                            timeout=240)
-        print(f"{cfg} {mode} ablate={ab}: {r.stdout.strip()} ms {r.stderr.strip()[-200:] if r.returncode else ''}",
+        print(f"{cfg} {mode} KX_DIAG={ab}: {r.stdout.strip()} ms {r.stderr.strip()[-300:] if r.returncode else ''}",
               flush=True)
