@@ -131,6 +131,9 @@ def read_status(t) -> A.Status:
 class ThriftCodec:
     """Batch Thrift-binary payload codec on one MI355X (remote.PayloadCodec mirror)."""
 
+    _DECODE = "kx_thrift_decode_batch"
+    _WHAT = "thrift unmarshal"
+
     def __init__(self, schema: Schema, codec_type: CodecType = CodecType.FastReadWrite, device: int = 0):
         import torch
         self.codec_type = codec_type
@@ -155,14 +158,14 @@ class ThriftCodec:
         kc = to_kx_columns(out, ds.infos, var_caps)
         st = status if status is not None else status_tensor(self.device)
         rs = torch.empty(max(1, n), dtype=torch.uint8, device=self.device) if record_status else None
-        rc = lib().kx_thrift_decode_batch(self.ctx.handle, ds.handle, _ptr(buf), buf.numel(), _ptr(offsets), n,
+        rc = getattr(lib(), self._DECODE)(self.ctx.handle, ds.handle, _ptr(buf), buf.numel(), _ptr(offsets), n,
                                           C.byref(kc), _ptr(rs), _ptr(st), _stream_ptr(stream))
-        check(rc, "kx_thrift_decode_batch")
+        check(rc, self._DECODE)
         res = DecodeResult(out, st, rs)
         if raise_on_error:
             s = res.read_status()
             if s.code:
-                raise ProtocolError(s.code, "thrift unmarshal", s.record, s.offset)
+                raise ProtocolError(s.code, self._WHAT, s.record, s.offset)
         return res
 
     def Marshal(self, cols: ColumnSet, with_offsets: bool = True, stream=None, out=None):
@@ -212,6 +215,28 @@ class ThriftCodec:
 
     # lower-case aliases
     name, unmarshal, marshal, blength, skip = Name, Unmarshal, Marshal, BLength, Skip
+
+
+class ProtobufCodec(ThriftCodec):
+    """Batch Kitex-Protobuf payload codec (pkg/remote/codec/protobuf/protobuf.go:49-61).
+
+    Unmarshal = proto.Unmarshal of each record body (protobuf.go:135-170 -> service.go:358-365):
+    with offsets, n bare proto3 bodies with known extents; without, the body of
+    `message Batch { repeated Rec recs = 1; }` (record boundaries found on the GPU)."""
+
+    _DECODE = "kx_pb_decode_batch"
+    _WHAT = "protobuf unmarshal"
+
+    def __init__(self, schema: Schema, device: int = 0):
+        super().__init__(schema, CodecType.Basic, device)
+
+    def Name(self) -> str:
+        return "protobuf"
+
+    def Skip(self, buf, n: int, stream=None):
+        raise KxError(A.ERR_NOT_IMPLEMENTED, "protobuf has no skip decoder")
+
+    name, skip = Name, Skip
 
 
 def write_message_begin(name: str, msg_type: int, seqid: int) -> bytes:

@@ -61,21 +61,23 @@ enum { T_ENT = 0, T_EXIT, T_CNT, T_ERRC, T_ERRP, T_VAR, T_PCNT = T_VAR + KXP_NV_
 enum { G_ENT = 0, G_EXIT, G_CNT, G_ERRC, G_ERRP, G_VAR, G_BCNT = G_VAR + KXP_NV_MAX, G_BVAR,
        G_NF = G_BVAR + KXP_NV_MAX };
 
-enum Mode { M_THRIFT = 0, M_SKIP = 1 };
+enum Mode { M_THRIFT = 0, M_SKIP = 1, M_PB = 2 };
+
+// diagnostics (KX_DIAG & 64): shader-clock cycles per index-pass phase, summed over tiles (lane 0)
+__device__ unsigned long long g_phase[8];
 
 struct DecParams {
   const uint8_t* in;
   uint64_t in_len;
   const uint64_t* offsets;   // known-offsets mode when non-null
   uint64_t n;
-  const KxProgram* prog;
+  const KAS KxProgram* prog;  // compiled schema (constant address space: scalar loads when uniform)
   KxLaunchCols cols;
   uint8_t* rstat;
   kx_status* status;
   uint64_t* skip_out;        // M_SKIP: record start offsets
   uint64_t* tdesc;           // tile words
   uint64_t* gdesc;           // group words
-  uint32_t* gcount;          // per-group arrival counters (cleared at launch)
   uint16_t* starts;          // concatenated mode: record starts per tile (slotcap slots each)
   unsigned long long* errkey;  // offsets mode: min((record << 8) | code)
   uint32_t* overflow;        // an arena capacity was exceeded
@@ -106,7 +108,7 @@ struct Src {
   uint64_t wpos;             // input position of window byte 0 (mod 2^64: may precede 0)
   int32_t wlen;              // valid bytes in the window
   const LDS uint32_t* win;
-  const KxpStep* steps;      // canonical plan (uniform index -> scalar loads)
+  const KAS KxpStep* steps;  // canonical plan (uniform index -> scalar loads)
   uint32_t nsteps;
   uint64_t canon_pres;
 };
@@ -335,27 +337,21 @@ __device__ __forceinline__ void store_col(void* base, uint32_t width, uint64_t r
   }
 }
 
-// program tables are read from global memory (a few KiB, L1/L2-resident)
-__device__ __forceinline__ KxpField ld_field(const KxProgram* P, int i) {
-  v4u v = *(const GLB v4u_a4*)&P->f[i];
-  KxpField F;
-  __builtin_memcpy(&F, &v, sizeof F);
-  return F;
+// program tables live in the constant address space: a uniform index becomes a scalar load
+template <typename T>
+__device__ __forceinline__ T ldk(const KAS T* p) {
+  static_assert(sizeof(T) % 4 == 0, "dword-sized tables");
+  uint32_t w[sizeof(T) / 4];
+  const KAS uint32_t* q = (const KAS uint32_t*)p;
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(T) / 4); i++) w[i] = q[i];
+  T v;
+  __builtin_memcpy(&v, w, sizeof(T));
+  return v;
 }
-__device__ __forceinline__ KxpInst ld_inst(const KxProgram* P, int i) {
-  v4u v[2];
-  v[0] = ((const GLB v4u_a4*)&P->inst[i])[0];
-  v[1] = ((const GLB v4u_a4*)&P->inst[i])[1];
-  KxpInst I;
-  __builtin_memcpy(&I, v, sizeof I);
-  return I;
-}
-__device__ __forceinline__ KxpCol ld_col(const KxProgram* P, int i) {
-  v4u v = *(const GLB v4u_a4*)&P->col[i];
-  KxpCol K;
-  __builtin_memcpy(&K, &v, sizeof K);
-  return K;
-}
+__device__ __forceinline__ KxpField ld_field(const KAS KxProgram* P, int i) { return ldk(&P->f[i]); }
+__device__ __forceinline__ KxpInst ld_inst(const KAS KxProgram* P, int i) { return ldk(&P->inst[i]); }
+__device__ __forceinline__ KxpCol ld_col(const KAS KxProgram* P, int i) { return ldk(&P->col[i]); }
 
 // Canonical fast path: the record is checked against the schema's canonical plan (header bytes in
 // encoder order, STOP bytes). The step index is wave-uniform (scalar loads); a lane whose record
@@ -364,17 +360,20 @@ template <int NV>
 __device__ __forceinline__ bool canon_record(const Src& w, const KAS KxLaunchCols& cols, uint64_t start, uint64_t limit,
                                              uint64_t rec, bool emit, uint64_t* endp, VarState<NV>& vs) {
   uint64_t pos = start;
-  const KxpStep* __restrict__ steps = w.steps;
+  const KAS KxpStep* __restrict__ steps = w.steps;
   uint32_t k = 0;
   while (k < w.nsteps) {
-    const KxpStep st = steps[k];
+    // every lane still on the plan is at the same step: make that explicit so the plan is read
+    // with scalar loads (a per-lane index would turn each step into a vector memory round trip)
+    k = __builtin_amdgcn_readfirstlane(k);
+    const KxpStep st = ldk(&steps[k]);
     const uint64_t rem = limit - pos;
     if (st.kind == KXP_S_FIXED) {
       // up to 4 consecutive fixed-width fields: their positions do not depend on data
       const uint32_t m = min(st.hdr >> 24, 4u);
-      const KxpStep s1 = steps[k + (m > 1 ? 1 : 0)];
-      const KxpStep s2 = steps[k + (m > 2 ? 2 : 0)];
-      const KxpStep s3 = steps[k + (m > 3 ? 3 : 0)];
+      const KxpStep s1 = ldk(&steps[k + (m > 1 ? 1 : 0)]);
+      const KxpStep s2 = ldk(&steps[k + (m > 2 ? 2 : 0)]);
+      const KxpStep s3 = ldk(&steps[k + (m > 3 ? 3 : 0)]);
       const uint32_t o1 = 3 + st.width, o2 = o1 + 3 + s1.width, o3 = o2 + 3 + s2.width;
       const uint32_t len = m == 1 ? o1 : m == 2 ? o2 : m == 3 ? o3 : o3 + 3 + s3.width;
       if (rem < len) return false;
@@ -430,7 +429,7 @@ __device__ __forceinline__ bool canon_record(const Src& w, const KAS KxLaunchCol
 // Generic FastRead field loop: any field order, unknown / mistyped fields skipped, repeated ids
 // (last wins; a repeated struct field is a fresh NewX()), required fields checked.
 template <int NV>
-__device__ __forceinline__ int generic_record(const Src& w, const KxProgram* P, const KAS KxLaunchCols& cols,
+__device__ __forceinline__ int generic_record(const Src& w, const KAS KxProgram* P, const KAS KxLaunchCols& cols,
                                               uint64_t start, uint64_t limit, uint64_t rec, bool emit,
                                               uint64_t* endp, VarState<NV>& vs, uint64_t& pres_out) {
 #pragma unroll
@@ -522,11 +521,167 @@ __device__ __forceinline__ int generic_record(const Src& w, const KxProgram* P, 
   return KX_OK;
 }
 
-__device__ __forceinline__ void emit_defaults(const KxProgram* P, const KAS KxLaunchCols& cols, uint64_t rec) {
+__device__ __forceinline__ void emit_defaults(const KAS KxProgram* P, const KAS KxLaunchCols& cols, uint64_t rec) {
   for (uint32_t c = 0; c < P->ncols; c++) {
     const KxpCol K = ld_col(P, c);
     if (K.kind == KXP_K_FIXED) store_col(cols.data[c], K.width, rec, (uint64_t)K.defv);
   }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Kitex-Protobuf body: proto.Unmarshal of a flat proto3 message
+// (protobuf.go:135-170; protowire rules as restated in oracle/kx_oracle.c pb_reader): fields in any
+// order, unknown numbers and mismatched wire types skipped, the last occurrence wins, `string`
+// fields UTF-8 validated, groups (wire types 3/4) rejected.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t fbyte(const Fetch& f, int i) {
+  const uint32_t x = i < 4 ? f.w0 : i < 8 ? f.w1 : f.w2;
+  return (x >> (8 * (i & 3))) & 0xffu;
+}
+
+// protowire.ConsumeVarint at p: at most 10 bytes, the 10th <= 1; `rem` bytes are available
+__device__ __forceinline__ int pb_varint(const Src& w, uint64_t p, uint64_t rem, uint64_t& v, uint32_t& used) {
+  const Fetch f = fetch12(w, p);
+  uint64_t x = 0;
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    if ((uint64_t)i >= rem) return KX_ERR_EOF;
+    const uint32_t c = fbyte(f, i);
+    if (i == 9 && c > 1) return KX_ERR_INVALID_DATA;
+    x |= (uint64_t)(c & 0x7f) << (7 * i);
+    if (c < 0x80) {
+      v = x;
+      used = (uint32_t)i + 1;
+      return KX_OK;
+    }
+  }
+  return KX_ERR_INVALID_DATA;
+}
+
+// utf8.Valid (what protobuf-go enforces on proto3 `string` fields), byte by byte
+__device__ __noinline__ bool pb_utf8_slow(const Src w, uint64_t p, uint64_t n) {
+  uint64_t i = 0;
+  while (i < n) {
+    const uint32_t c = ld1(w, p + i);
+    if (c < 0x80) { i++; continue; }
+    uint32_t k, cp;
+    if ((c & 0xe0) == 0xc0) { k = 1; cp = c & 0x1f; }
+    else if ((c & 0xf0) == 0xe0) { k = 2; cp = c & 0x0f; }
+    else if ((c & 0xf8) == 0xf0) { k = 3; cp = c & 0x07; }
+    else return false;
+    if (i + k >= n) return false;  // truncated sequence
+    for (uint32_t j = 1; j <= k; j++) {
+      const uint32_t d = ld1(w, p + i + j);
+      if ((d & 0xc0) != 0x80) return false;
+      cp = (cp << 6) | (d & 0x3f);
+    }
+    if ((k == 1 && cp < 0x80) || (k == 2 && cp < 0x800) || (k == 3 && cp < 0x10000)) return false;
+    if (cp > 0x10ffff || (cp >= 0xd800 && cp <= 0xdfff)) return false;
+    i += k + 1;
+  }
+  return true;
+}
+
+// ASCII fast path from the LDS window (OR of the covering dwords), else the full check
+__device__ __forceinline__ bool pb_utf8_ok(const Src& w, uint64_t p, uint64_t n) {
+  if (n == 0) return true;
+  const int32_t q = n <= 4096 ? wofs(w, p, (uint32_t)n) : -1;
+  if (q >= 0) {
+    const LDS uint32_t* s = w.win + (q >> 2);
+    const int sh = q & 3;
+    const int nd = (sh + (int)n + 3) >> 2;
+    const int tail = (sh + (int)n) & 3;
+    uint32_t acc = 0;
+    for (int i = 0; i < nd; i++) {
+      uint32_t m = 0xffffffffu;
+      if (i == 0) m &= 0xffffffffu << (8 * sh);
+      if (i == nd - 1 && tail) m &= 0xffffffffu >> (8 * (4 - tail));
+      acc |= s[i] & m;
+    }
+    if (!(acc & 0x80808080u)) return true;
+  }
+  return pb_utf8_slow(w, p, n);
+}
+
+template <int NV>
+__device__ __forceinline__ int pb_body(const Src& w, const KAS KxProgram* P, const KAS KxLaunchCols& cols,
+                                       uint64_t start, uint64_t limit, uint64_t rec, bool emit,
+                                       VarState<NV>& vs, uint64_t& pres_out) {
+  uint64_t pos = start, seen = 0, pres = 0;
+  const int nf = (int)P->nfields;
+  int pred = 0;  // fields usually arrive in field-number order: try the one after the last match first
+  while (pos < limit) {
+    uint64_t tag;
+    uint32_t u;
+    int rc = pb_varint(w, pos, limit - pos, tag, u);
+    if (rc) return rc;
+    pos += u;
+    const uint64_t num = tag >> 3;
+    const uint32_t wt = (uint32_t)tag & 7u;
+    if (num == 0 || num > 536870911ull) return KX_ERR_INVALID_DATA;
+    const int id = num <= 32767 ? (int)num : -1;
+    int fi = -1;
+    KxpField F = ld_field(P, pred);
+    if (id >= 0 && pred < nf && F.id == id) {
+      fi = pred;
+    } else if (id >= 0) {
+      for (int k = 0; k < nf; k++)
+        if (P->f[k].id == id) { fi = k; break; }
+      if (fi >= 0) F = ld_field(P, fi);
+    }
+    const uint64_t rem = limit - pos;
+    if (fi < 0 || F.pb_wt != wt) {  // unknown number / other wire type: skipped (ConsumeFieldValue)
+      if (wt == 0) {
+        uint64_t v;
+        if ((rc = pb_varint(w, pos, rem, v, u))) return rc;
+        pos += u;
+      } else if (wt == 1 || wt == 5) {
+        const uint32_t k = wt == 1 ? 8u : 4u;
+        if (rem < k) return KX_ERR_EOF;
+        pos += k;
+      } else if (wt == 2) {
+        uint64_t l;
+        if ((rc = pb_varint(w, pos, rem, l, u))) return rc;
+        if (l > rem - u) return KX_ERR_EOF;
+        pos += u + l;
+      } else {
+        return KX_ERR_INVALID_DATA;  // groups and reserved wire types
+      }
+      continue;
+    }
+    pred = fi + 1 < nf ? fi + 1 : 0;
+    if (wt == 0) {
+      uint64_t v;
+      if ((rc = pb_varint(w, pos, rem, v, u))) return rc;
+      pos += u;
+      if (F.ttype == KX_T_BOOL) v = v != 0;
+      if (emit) store_col(cols.data[F.col], F.width, rec, v);  // int32: low 32 bits
+    } else if (wt == 1) {
+      if (rem < 8) return KX_ERR_EOF;
+      const Fetch f = fetch12(w, pos);
+      if (emit) store_col(cols.data[F.col], F.width, rec, (uint64_t)f.w0 | ((uint64_t)f.w1 << 32));
+      pos += 8;
+    } else {
+      uint64_t l;
+      if ((rc = pb_varint(w, pos, rem, l, u))) return rc;
+      pos += u;
+      if (l > rem - u) return KX_ERR_EOF;
+      if (!(F.flags & 1) && !pb_utf8_ok(w, pos, l)) return KX_ERR_INVALID_DATA;
+      vset<NV>(vs, F.vslot, pos, (uint32_t)l);
+      pos += l;
+    }
+    seen |= 1ull << fi;
+    if (F.pbit >= 0) pres |= 1ull << F.pbit;
+  }
+  if (emit) {
+    // fields never seen keep their (proto3 zero / schema) default
+    for (uint32_t c = 0; c < P->ncols; c++) {
+      const KxpCol K = ld_col(P, c);
+      if (K.kind == KXP_K_FIXED && !((seen >> K.field) & 1)) store_col(cols.data[c], K.width, rec, (uint64_t)K.defv);
+    }
+  }
+  pres_out = pres;
+  return KX_OK;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -696,32 +851,84 @@ __device__ __forceinline__ bool get_words(const uint64_t* base, uint64_t nitems,
   }
 }
 
-// first canonical signature (3 bytes) in a lane's 128-byte segment, read from the LDS window:
-// 35 dwords in registers, SWAR test for the first signature byte, exact 3-byte check on hits
+// first canonical signature (3 bytes) in a lane's 128-byte segment, read from the LDS window with
+// a SWAR test for the first signature byte and an exact 3-byte check on hits. Segments are 128 B
+// apart, so lanes reading dword i of their segment together would all hit one LDS bank; each lane
+// instead starts at dword (lane mod 33) and rotates through its 33 dwords (conflict-free), keeping
+// the lowest hit.
 __device__ __forceinline__ uint64_t scan_segment(const Src& w, int32_t q0, uint64_t seg_lo, uint64_t plim,
-                                                 uint32_t sig) {
+                                                 uint32_t sig, int lane) {
   const LDS uint32_t* s = w.win + (q0 >> 2);
   const int sh0 = q0 & 3;
-  uint32_t d[35];
-#pragma unroll
-  for (int i = 0; i < 35; i++) d[i] = s[i];
   const uint32_t b0 = (sig & 0xff) * 0x01010101u;
-  uint64_t found = X_NONE;
-#pragma unroll
-  for (int i = 0; i < 34; i++) {
-    const uint32_t t = d[i] ^ b0;
+  int idx = lane % 33;
+  int best = 1 << 30;
+#pragma unroll 4
+  for (int i = 0; i < 33; i++) {
+    const uint32_t x0 = s[idx], x1 = s[idx + 1];
+    const uint32_t t = x0 ^ b0;
     const uint32_t z = (t - 0x01010101u) & ~t & 0x80808080u;   // bytes equal to the first sig byte
-    if (found == X_NONE && z) {
+    if (z) {
 #pragma unroll
       for (int j = 0; j < 4; j++) {
-        const int rel = 4 * i + j - sh0;
-        if (found == X_NONE && rel >= 0 && rel < SEG && seg_lo + rel < plim &&
-            (__builtin_amdgcn_alignbyte(d[i + 1], d[i], j) & 0xffffffu) == sig)
-          found = seg_lo + rel;
+        const int rel = 4 * idx + j - sh0;
+        if (((z >> (8 * j + 7)) & 1) && rel >= 0 && rel < best &&
+            (__builtin_amdgcn_alignbyte(x1, x0, j) & 0xffffffu) == sig)
+          best = rel;
       }
     }
+    idx = idx == 32 ? 0 : idx + 1;
   }
-  return found;
+  return (best < SEG && seg_lo + (uint64_t)best < plim) ? seg_lo + (uint64_t)best : X_NONE;
+}
+
+// Kitex-Protobuf record candidate at p: a Batch frame header (0x0A, uvarint length) whose body fits
+// the input, starts with a plausible tag, and is followed by the next frame's 0x0A (or the end).
+__device__ __forceinline__ int pb_varint(const Src& w, uint64_t p, uint64_t rem, uint64_t& v, uint32_t& used);
+__device__ __forceinline__ bool pb_frame_ok(const Src& w, uint64_t p, uint64_t len) {
+  uint64_t l;
+  uint32_t u;
+  if (p + 1 >= len || pb_varint(w, p + 1, len - p - 1, l, u) || u > 5 || l > len - p - 1 - u) return false;
+  const uint64_t b = p + 1 + u, e = b + l;
+  if (l) {
+    const uint32_t t = ld1(w, b), wt = t & 7;
+    if (t < 8 || wt == 3 || wt == 4 || wt > 5) return false;
+  }
+  return e == len || ld1(w, e) == 0x0Au;
+}
+
+// first Kitex-Protobuf candidate in a lane's segment [seg_lo, seg_hi) (rotated like scan_segment)
+__device__ __forceinline__ uint64_t pb_scan_segment(const Src& w, uint64_t seg_lo, uint64_t seg_hi, uint64_t len,
+                                                    int lane) {
+  const int32_t q0 = wofs(w, seg_lo, SEG + 8);
+  const int n = (int)(seg_hi - seg_lo);
+  int best = 1 << 30;
+  if (q0 >= 0 && n == SEG) {
+    const LDS uint32_t* s = w.win + (q0 >> 2);
+    const int sh0 = q0 & 3;
+    int idx = lane % 33;
+    for (int i = 0; i < 33; i++) {
+      const uint32_t x0 = s[idx];
+      const uint32_t t = x0 ^ 0x0A0A0A0Au;
+      uint32_t z = (t - 0x01010101u) & ~t & 0x80808080u;
+      while (z) {
+        const int j = __builtin_ctz(z) >> 3;
+        z &= z - 1;
+        const int rel = 4 * idx + j - sh0;
+        if (rel >= 0 && rel < best && rel < SEG && ((x0 >> (8 * j)) & 0xffu) == 0x0Au &&
+            pb_frame_ok(w, seg_lo + (uint64_t)rel, len))
+          best = rel;
+      }
+      idx = idx == 32 ? 0 : idx + 1;
+    }
+  } else {
+    for (int rel = 0; rel < n; rel++)
+      if (ld1(w, seg_lo + (uint64_t)rel) == 0x0Au && pb_frame_ok(w, seg_lo + (uint64_t)rel, len)) {
+        best = rel;
+        break;
+      }
+  }
+  return best < SEG ? seg_lo + (uint64_t)best : X_NONE;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -742,7 +949,7 @@ __device__ __forceinline__ Src load_window(KParams& dp, LDS uint32_t* win, uint6
       __builtin_amdgcn_global_load_lds((const GLB void*)(g + (size_t)c * 16), (LDS void*)(win + k * 256), 16, 0, 0);
   }
   if (wait) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  const KxProgram* P = dp.prog;
+  const KAS KxProgram* P = dp.prog;
   return Src{dp.in, dp.in_len, wbase - abs_in, wlen, win, thrift ? P->steps : nullptr, thrift ? P->nsteps : 0u,
              thrift ? P->canon_pres : 0ull};
 }
@@ -760,6 +967,22 @@ __device__ __forceinline__ int parse_record(KParams& dp, const Src& w, uint64_t 
       return KX_OK;
     }
     return generic_record<NV>(w, dp.prog, dp.cols, pos, lim, r, emit, end, vs, pres);
+  }
+  if (MODE == M_PB) {
+    uint64_t b = pos, e = lim;
+    if (!dp.offsets) {  // Batch framing: 0x0A, uvarint(len), body
+      if (pos >= lim) return KX_ERR_EOF;
+      if (ld1(w, pos) != 0x0Au) return KX_ERR_INVALID_DATA;
+      uint64_t l;
+      uint32_t u;
+      const int rc = pb_varint(w, pos + 1, lim - pos - 1, l, u);
+      if (rc) return rc;
+      if (l > lim - pos - 1 - u) return KX_ERR_EOF;
+      b = pos + 1 + u;
+      e = b + l;
+    }
+    *end = e;
+    return pb_body<NV>(w, dp.prog, dp.cols, b, e, r, emit, vs, pres);
   }
   uint64_t p2 = pos;
   const int rc = dskip_body(w, p2, lim, KX_T_STRUCT, 64);
@@ -781,23 +1004,34 @@ struct Agg {
 template <int NV, int MODE>
 __device__ Agg walk_tile(KParams& dp, const Src& w, uint64_t tlo, uint64_t thi, uint64_t seed, int lane,
                          uint16_t* starts) {
-  const KxProgram* P = dp.prog;
+  const KAS KxProgram* P = dp.prog;
   const uint64_t seg_lo = tlo + (uint64_t)lane * SEG;
   const uint64_t seg_hi = min(seg_lo + SEG, thi);
   uint64_t ent = X_NONE;
-  if (seg_lo < thi) {
+  if (seg_lo < thi && MODE == M_PB) {
+    ent = pb_scan_segment(w, seg_lo, seg_hi, dp.in_len, lane);
+  } else if (seg_lo < thi) {
     const uint32_t sig = MODE == M_THRIFT ? P->sig : (uint32_t)KX_T_STOP;
     const uint32_t slen = (MODE == M_THRIFT && P->sig_len == 3) ? 3u : 1u;
     const uint64_t plim = min(seg_hi, dp.in_len >= slen ? dp.in_len - slen + 1 : 0ull);
     const int32_t q0 = wofs(w, seg_lo, SEG + 12);
     if (slen == 3 && seg_hi - seg_lo == SEG && q0 >= 0) {
-      ent = scan_segment(w, q0, seg_lo, plim, sig);
+      ent = scan_segment(w, q0, seg_lo, plim, sig, lane);
     } else {
       const uint32_t smask = slen == 3 ? 0xffffffu : 0xffu;
       for (uint64_t p = seg_lo; p < plim; p++)
         if ((ld4(w, p) & smask) == sig) { ent = p; break; }
     }
   }
+  uint64_t tp = (dp.diag & 64) ? __builtin_amdgcn_s_memtime() : 0;
+  auto phase = [&](int k) {
+    if (dp.diag & 64) {
+      const uint64_t now = __builtin_amdgcn_s_memtime();
+      if (lane == 0) atomicAdd(&g_phase[k], (unsigned long long)(now - tp));
+      tp = now;
+    }
+  };
+  phase(1);
   uint64_t ex = X_NONE, cnt = 0, errp = 0;
   int errc = 0;
   uint64_t vsum[NV > 0 ? NV : 1];
@@ -841,6 +1075,7 @@ __device__ Agg walk_tile(KParams& dp, const Src& w, uint64_t tlo, uint64_t thi, 
     }
     need = false;
     if (enumerate) break;
+    phase(2);
 
     // ---- one repair round: every lane must start at the first true record start in its segment,
     //      i.e. where the chain of the nearest lower walking lane (or `seed`) enters it ----
@@ -883,6 +1118,7 @@ __device__ Agg walk_tile(KParams& dp, const Src& w, uint64_t tlo, uint64_t thi, 
     a.ex = fel < 64 ? X_ERR : hm ? rl64(ex, 63 - __clzll((long long)hm)) : seed;
     a.errc = fel < 64 ? (uint64_t)__builtin_amdgcn_readlane(errc, fel) : 0;
     a.errp = fel < 64 ? rl64(errp, fel) : 0;
+    phase(3);
     if (live) {
       const uint64_t b = cpre;
       if (cnt > 0) starts[b + 0] = (uint16_t)(st0 - tlo);
@@ -898,6 +1134,7 @@ __device__ Agg walk_tile(KParams& dp, const Src& w, uint64_t tlo, uint64_t thi, 
     }
     break;
   }
+  phase(4);
   return a;
 }
 
@@ -945,7 +1182,9 @@ __device__ Agg tile_agg(KParams& dp, LDS uint32_t* win, uint64_t t, uint64_t see
     const Src w = load_window(dp, win, dp.offsets[lo], lane, MODE == M_THRIFT);
     return measure_records<NV, MODE>(dp, w, lo, hi, lane);
   }
+  const uint64_t t0 = (dp.diag & 64) ? __builtin_amdgcn_s_memtime() : 0;
   const Src w = load_window(dp, win, lo, lane, MODE == M_THRIFT);
+  if ((dp.diag & 64) && lane == 0) atomicAdd(&g_phase[0], (unsigned long long)(__builtin_amdgcn_s_memtime() - t0));
   return walk_tile<NV, MODE>(dp, w, lo, hi, seed, lane, dp.starts + t * dp.slotcap);
 }
 
@@ -1069,7 +1308,7 @@ __device__ void group_scan(KParams& dp, LDS uint32_t* win, uint64_t g, uint64_t 
   }
 }
 
-// ---- kernel 1: index pass (one wave per tile; the last wave of each group of 64 tiles scans it) ----
+// ---- kernel 1: index pass (one wave per tile) ----
 template <int NV, int MODE>
 __global__ void __launch_bounds__(NT) index_kernel(DecParams dp_) {
   KParams& dp = KX_PARAMS();
@@ -1080,6 +1319,7 @@ __global__ void __launch_bounds__(NT) index_kernel(DecParams dp_) {
   const uint64_t t = (uint64_t)blockIdx.x * WAVES + wv;
   if (t >= dp.ntiles) return;
   LDS uint32_t* win = (LDS uint32_t*)WIN[wv];
+  const uint64_t t_start = (dp.diag & 64) ? __builtin_amdgcn_s_memtime() : 0;
   Agg a;
   if (dp.diag & 1) {
     uint64_t lo, hi;
@@ -1091,14 +1331,21 @@ __global__ void __launch_bounds__(NT) index_kernel(DecParams dp_) {
     a = tile_agg<NV, MODE>(dp, win, t, t == 0 ? 0ull : X_NONE, lane);
   }
   if (lane == 0 && !(dp.diag & 4)) put_tile(dp, t, a, NV);
-  if (dp.diag & 2) return;
+  if ((dp.diag & 64) && lane == 0) atomicAdd(&g_phase[5], (unsigned long long)(__builtin_amdgcn_s_memtime() - t_start));
   const uint64_t g = t / GT;
-  // arrival count of the group (the counters are cleared at launch)
-  uint32_t old = 0;
-  if (lane == 0) old = atomicAdd(dp.gcount + g, 1u);
-  old = __shfl(old, 0, 64);
-  const uint64_t ntg = min((uint64_t)GT, dp.ntiles - g * GT);
-  if ((uint64_t)old == ntg - 1) group_scan<NV, MODE, false>(dp, win, g, g == 0 && !dp.offsets ? 0ull : X_NONE, lane);
+}
+
+// ---- kernel 1b: group scan (one wave per group of 64 tiles) ----
+template <int NV, int MODE>
+__global__ void __launch_bounds__(NT) group_kernel(DecParams dp_) {
+  KParams& dp = KX_PARAMS();
+  (void)dp_;
+  __shared__ __attribute__((aligned(16))) uint32_t WIN[WAVES][WINW];
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const uint64_t g = (uint64_t)blockIdx.x * WAVES + wv;
+  if (g >= dp.ngroups) return;
+  group_scan<NV, MODE, false>(dp, (LDS uint32_t*)WIN[wv], g, g == 0 && !dp.offsets ? 0ull : X_NONE, lane);
 }
 
 // ---- kernel 2: chain + scan over the groups (one workgroup of 4 waves, lane = group) ----
@@ -1270,9 +1517,8 @@ __global__ void __launch_bounds__(NT) emit_kernel(DecParams dp_) {
   const int wv = threadIdx.x >> 6;
   const uint64_t t = (uint64_t)blockIdx.x * WAVES + wv;
   if (t >= dp.ntiles) return;
-  const KxProgram* P = dp.prog;
+  const KAS KxProgram* P = dp.prog;
   const bool known = dp.offsets != nullptr;
-  const uint64_t ep = dp.epoch;
   const uint64_t nstop = known ? dp.n : *(volatile uint64_t*)dp.nstop;
   uint64_t lo, hi;
   tile_range(dp, t, lo, hi);
@@ -1318,15 +1564,15 @@ __global__ void __launch_bounds__(NT) emit_kernel(DecParams dp_) {
       } else {
         pos = lo + starts[j];
       }
-      if (!rc) rc = parse_record<NV, MODE>(dp, w, pos, lim, r, MODE == M_THRIFT, &end, vs, pres);
+      if (!rc) rc = parse_record<NV, MODE>(dp, w, pos, lim, r, MODE != M_SKIP, &end, vs, pres);
       if (rc) {  // offsets mode: the failed record reads as all defaults, empty payloads
 #pragma unroll
         for (int v = 0; v < NV; v++) vs.len[v] = 0;
         pres = 0;
-        if (MODE == M_THRIFT) emit_defaults(P, dp.cols, r);
+        if (MODE != M_SKIP) emit_defaults(P, dp.cols, r);
       }
       if (MODE == M_SKIP) dp.skip_out[r] = pos;
-      if (MODE == M_THRIFT && dp.cols.presence) dp.cols.presence[r] = pres;
+      if (MODE != M_SKIP && dp.cols.presence) dp.cols.presence[r] = pres;
       if (known) {
         if (rc) atomicMin(dp.errkey, (unsigned long long)((r << 8) | (uint64_t)(rc & 0xff)));
         if (dp.rstat) dp.rstat[r] = (uint8_t)rc;
@@ -1385,12 +1631,12 @@ __global__ void finalize_kernel(kx_status* st, unsigned long long* errkey, uint3
 }
 
 // ---- workspace: [8] errkey u64, [16] overflow u32, [24] nstop u64, then tile words, group words,
-//      group arrival counters, record-start slots ----
+//      record-start slots ----
 constexpr size_t WS_HDR = 256;
 
 struct WsLayout {
   uint64_t ntiles, ngroups, slotcap;
-  size_t tdesc, gdesc, gcount, starts, total;
+  size_t tdesc, gdesc, starts, total;
 };
 
 uint32_t krec_for(uint64_t in_len, uint64_t n) {
@@ -1419,7 +1665,6 @@ WsLayout ws_layout(uint64_t min_rec, uint64_t in_len, const uint64_t* offsets, u
   size_t o = WS_HDR;
   L.tdesc = o; o += (size_t)L.ntiles * T_NF * 8;
   L.gdesc = o; o += (size_t)L.ngroups * G_NF * 8;
-  L.gcount = o; o += ((size_t)L.ngroups * 4 + 255) & ~(size_t)255;
   L.starts = o; o += ((size_t)L.ntiles * L.slotcap * 2 + 255) & ~(size_t)255;
   L.total = o;
   return L;
@@ -1434,7 +1679,6 @@ int launch_t(const DecParams& dp0, const WsLayout& L, void* ws, hipStream_t stre
   dp.nstop = (uint64_t*)(base + 24);
   dp.tdesc = (uint64_t*)(base + L.tdesc);
   dp.gdesc = (uint64_t*)(base + L.gdesc);
-  dp.gcount = (uint32_t*)(base + L.gcount);
   dp.starts = (uint16_t*)(base + L.starts);
   dp.ntiles = L.ntiles;
   dp.ngroups = L.ngroups;
@@ -1442,16 +1686,15 @@ int launch_t(const DecParams& dp0, const WsLayout& L, void* ws, hipStream_t stre
   dp.direct = dp.offsets && NV == 0;
   KX_HIP_CHECK(hipMemsetAsync(dp.status, 0, sizeof(kx_status), stream));
   const unsigned grid = (unsigned)((dp.ntiles + WAVES - 1) / WAVES);
+  const unsigned ggrid = (unsigned)((dp.ngroups + WAVES - 1) / WAVES);
   if (dp.diag & 256) {
-    KX_HIP_CHECK(hipMemsetAsync(dp.gcount, 0, (size_t)dp.ngroups * 4, stream));
     hipLaunchKernelGGL((index_kernel<NV, MODE>), dim3(grid), dim3(NT), 0, stream, dp);
     return KX_OK;
   }
   if (!dp.direct) {
-    // a plain arrival counter per group, cleared here: a CAS-tagged counter costs retries when the
-    // 64 waves of a group finish together
-    KX_HIP_CHECK(hipMemsetAsync(dp.gcount, 0, (size_t)dp.ngroups * 4, stream));
     hipLaunchKernelGGL((index_kernel<NV, MODE>), dim3(grid), dim3(NT), 0, stream, dp);
+    KX_HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL((group_kernel<NV, MODE>), dim3(ggrid), dim3(NT), 0, stream, dp);
     KX_HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL((chain_kernel<NV, MODE>), dim3(1), dim3(CT), 0, stream, dp);
     KX_HIP_CHECK(hipGetLastError());
@@ -1462,6 +1705,17 @@ int launch_t(const DecParams& dp0, const WsLayout& L, void* ws, hipStream_t stre
                      dp.offsets, dp.n);
   KX_HIP_CHECK(hipGetLastError());
   return KX_OK;
+}
+
+template <int MODE>
+int launch_nv(const DecParams& dp, const WsLayout& L, void* ws, hipStream_t stream, uint32_t nvar) {
+  switch (nvar) {
+    case 0: return launch_t<0, MODE>(dp, L, ws, stream);
+    case 1: return launch_t<1, MODE>(dp, L, ws, stream);
+    case 2: return launch_t<2, MODE>(dp, L, ws, stream);
+    case 3: case 4: return launch_t<4, MODE>(dp, L, ws, stream);
+    default: return launch_t<8, MODE>(dp, L, ws, stream);
+  }
 }
 
 void fill_diag_flags(DecParams& dp) {
@@ -1478,26 +1732,28 @@ size_t kx_decode_ws_bytes(const KxProgram& hprog, uint64_t in_len, const uint64_
   return ws_layout(hprog.fixed_min, in_len, offsets, n).total;
 }
 
+// diagnostics (not part of the public ABI): read and reset the phase-timing accumulators
+extern "C" int kx_debug_phase_cycles(unsigned long long* out, int n) {
+  if (n > 8) n = 8;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase), sizeof(unsigned long long) * n) != hipSuccess) return KX_ERR_HIP;
+  unsigned long long z[8] = {0};
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_phase), z, sizeof z) != hipSuccess) return KX_ERR_HIP;
+  return KX_OK;
+}
+
 size_t kx_skip_ws_bytes(uint64_t in_len) { return ws_layout(1, in_len, nullptr, 0).total; }
 
 int kx_launch_decode(const KxProgram* dprog, const KxProgram& hprog, const uint8_t* in, uint64_t in_len,
                      const uint64_t* offsets, uint64_t n, const KxLaunchCols& cols, uint8_t* record_status,
                      kx_status* status, void* ws, size_t ws_size, uint64_t epoch, hipStream_t stream, bool pb) {
-  if (pb) return KX_ERR_NOT_IMPLEMENTED;
   DecParams dp{};
   fill_diag_flags(dp);
-  dp.in = in; dp.in_len = in_len; dp.offsets = offsets; dp.n = n; dp.prog = dprog;
+  dp.in = in; dp.in_len = in_len; dp.offsets = offsets; dp.n = n; dp.prog = (const KAS KxProgram*)dprog;
   dp.cols = cols; dp.rstat = record_status; dp.status = status; dp.epoch = epoch;
   dp.krec = krec_for(in_len, n);
   const WsLayout L = ws_layout(hprog.fixed_min, in_len, offsets, n);
   if (ws_size < L.total) return KX_ERR_INVALID_ARG;
-  switch (hprog.nvar) {
-    case 0: return launch_t<0, M_THRIFT>(dp, L, ws, stream);
-    case 1: return launch_t<1, M_THRIFT>(dp, L, ws, stream);
-    case 2: return launch_t<2, M_THRIFT>(dp, L, ws, stream);
-    case 3: case 4: return launch_t<4, M_THRIFT>(dp, L, ws, stream);
-    default: return launch_t<8, M_THRIFT>(dp, L, ws, stream);
-  }
+  return pb ? launch_nv<M_PB>(dp, L, ws, stream, hprog.nvar) : launch_nv<M_THRIFT>(dp, L, ws, stream, hprog.nvar);
 }
 
 int kx_launch_skip(const uint8_t* in, uint64_t in_len, uint64_t n, uint64_t* offsets_out, kx_status* status,

@@ -30,7 +30,8 @@ def lib():
     return _lib
 
 
-def decode(schema, infos, npres, data: np.ndarray, n: int, offsets=None, var_caps=None, threads: int = 8):
+def decode(schema, infos, npres, data: np.ndarray, n: int, offsets=None, var_caps=None, threads: int = 8,
+           pb: bool = False):
     os.environ["KX_EMU_THREADS"] = str(threads)
     if var_caps is None:
         var_caps = [0 if ci.kind == A.COL_FIXED else max(1, data.size) for ci in infos]
@@ -41,7 +42,7 @@ def decode(schema, infos, npres, data: np.ndarray, n: int, offsets=None, var_cap
     tab, ns = schema.struct_table()
     rc = lib().emu_decode(C.cast(tab, C.c_void_p), ns, data.ctypes.data, data.size,
                           offsets.ctypes.data if offsets is not None else None, n, C.addressof(kc),
-                          rs.ctypes.data, C.addressof(st), 0, None)
+                          rs.ctypes.data, C.addressof(st), 2 if pb else 0, None)
     return rc, out, st, rs[:n]
 
 

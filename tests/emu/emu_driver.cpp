@@ -3,10 +3,12 @@
 #include "hip/hip_runtime.h"
 #include "kx_internal.h"
 
+// mode: 0 = Thrift decode, 1 = skip decoder, 2 = Kitex-Protobuf decode
 extern "C" int emu_decode(const kx_struct_desc* structs, uint32_t nstructs, const uint8_t* in, uint64_t in_len,
                           const uint64_t* offsets, uint64_t n, const kx_columns* out, uint8_t* record_status,
-                          kx_status* status, int skip, uint64_t* skip_out) {
+                          kx_status* status, int mode, uint64_t* skip_out) {
   static kx_schema s;  // the emulator is single-call-at-a-time
+  const bool skip = mode == 1;
   int rc = skip ? KX_OK : kx_build_program(structs, nstructs, &s);
   if (rc) return rc;
   KxLaunchCols lc;
@@ -40,6 +42,6 @@ extern "C" int emu_decode(const kx_struct_desc* structs, uint32_t nstructs, cons
     rc = kx_launch_skip(in, in_len, n, skip_out, status, ws, ws_cap, epoch, nullptr);
   else
     rc = kx_launch_decode(&s.prog, s.prog, in, in_len, offsets, n, lc, record_status, status, ws, ws_cap, epoch,
-                          nullptr, false);
+                          nullptr, mode == 2);
   return rc;
 }

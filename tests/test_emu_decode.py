@@ -6,6 +6,7 @@ import numpy as np
 import pytest
 
 from tests import decode_cases as DC
+from tests import pb_cases as PC
 from tests.emu import emu
 
 
@@ -14,9 +15,9 @@ class EmuDecoder:
         self.oracle = oracle
         self.threads = threads
 
-    def decode(self, sch, wire, n, offsets=None):
+    def decode(self, sch, wire, n, offsets=None, pb=False):
         _, infos, npres = self.oracle.flatten(sch)
-        rc, out, st, rs = emu.decode(sch, infos, npres, wire, n, offsets=offsets, threads=self.threads)
+        rc, out, st, rs = emu.decode(sch, infos, npres, wire, n, offsets=offsets, threads=self.threads, pb=pb)
         assert rc == 0, rc
         return out, st, rs
 
@@ -73,3 +74,25 @@ def test_emu_skip(edec, oracle):
 def test_emu_deep_lookback(oracle):
     """many workgroups in flight: 64 concurrent workgroups over ~1500 tiles"""
     DC.case_concat(EmuDecoder(oracle, threads=64), oracle, "r2", 75000)
+
+
+# ---- Kitex-Protobuf (same kernels, M_PB walker) ----
+@pytest.mark.parametrize("n", [1, 7, 1000, 20000])
+def test_emu_pb_concat(edec, oracle, n):
+    PC.case_pb_concat(edec, oracle, n)
+
+
+@pytest.mark.parametrize("n", [1, 300, 5000])
+def test_emu_pb_offsets(edec, oracle, n):
+    PC.case_pb_offsets(edec, oracle, n)
+
+
+@pytest.mark.parametrize("mode", ["concat", "offsets"])
+def test_emu_pb_noncanonical(edec, oracle, mode):
+    PC.case_pb_noncanonical(edec, oracle, mode)
+
+
+@pytest.mark.parametrize("mode", ["concat", "offsets"])
+@pytest.mark.parametrize("case", PC.PB_ERRORS)
+def test_emu_pb_errors(edec, oracle, case, mode):
+    PC.case_pb_error(edec, oracle, case, mode)
