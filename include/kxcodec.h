@@ -22,6 +22,9 @@
  *                                 field reorder pkg tool/.../thriftgo/patcher.go:503-522)
  *   kx_pb_decode_batch .......... proto.Unmarshal of the Kitex-Protobuf body
  *                                 (pkg/remote/codec/protobuf/protobuf.go:209-216 -> service.go:358-365)
+ *   kx_pb_encoded_size_batch .... proto.Size of each record + its Batch frame header
+ *   kx_pb_encode_batch .......... proto.Marshal of the Kitex-Protobuf body (protobuf.go:64-134,
+ *                                 deterministic field-number order) as a `repeated Rec recs = 1` stream
  *   kx_host_decode_batch ........ fastUnmarshal end to end from host (netpoll) memory: pinned H2D ->
  *                                 decode -> D2H (codec_fast.go:60-82 with the Next(dataLen) slice)
  *   kx_strerror ................. error text; codes mirror pkg/remote/codec/perrors/protocol_error.go:28-36
@@ -188,6 +191,14 @@ int kx_thrift_encode_batch(kx_ctx* c, const kx_schema* s, const kx_columns* in, 
 int kx_pb_decode_batch(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len,
                        const uint64_t* offsets, uint64_t n, const kx_columns* out,
                        uint8_t* record_status, kx_status* status, void* stream);
+/* Framed size of each record (0x0A + uvarint(body) + body), device sizes_out[n]. */
+int kx_pb_encoded_size_batch(kx_ctx* c, const kx_schema* s, const kx_columns* in, uint64_t n,
+                             uint64_t* sizes_out, void* stream);
+/* Writes the n records as the body of `message Batch { repeated Rec recs = 1; }`; offsets_out
+ * (n+1, device, optional) receives each record's frame start; status->consumed the total size. */
+int kx_pb_encode_batch(kx_ctx* c, const kx_schema* s, const kx_columns* in, uint64_t n,
+                       uint8_t* out, uint64_t out_cap, uint64_t* offsets_out,
+                       kx_status* status, void* stream);
 
 /* ---- host-memory entry point (the netpoll buffer side) ----
  * in / out columns / status are HOST memory (pinned or pageable). Synchronous. */

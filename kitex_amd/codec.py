@@ -25,7 +25,7 @@ from typing import List, Optional, Sequence
 
 from . import _abi as A
 from ._lib import KxError, check, lib
-from .columns import alloc_device, to_kx_columns
+from .columns import alloc_device, alloc_host, to_kx_columns
 from .schema import Schema
 from .synth import ColumnSet
 
@@ -132,6 +132,8 @@ class ThriftCodec:
     """Batch Thrift-binary payload codec on one MI355X (remote.PayloadCodec mirror)."""
 
     _DECODE = "kx_thrift_decode_batch"
+    _ENCODE = "kx_thrift_encode_batch"
+    _SIZE = "kx_thrift_encoded_size_batch"
     _WHAT = "thrift unmarshal"
 
     def __init__(self, schema: Schema, codec_type: CodecType = CodecType.FastReadWrite, device: int = 0):
@@ -168,6 +170,29 @@ class ThriftCodec:
                 raise ProtocolError(s.code, self._WHAT, s.record, s.offset)
         return res
 
+    def UnmarshalHost(self, wire, n: int, offsets=None, var_caps: Sequence[int] = None,
+                      raise_on_error: bool = True):
+        """fastUnmarshal from host memory (netpoll buffers): numpy uint8 wire (+ uint64 offsets[n+1])
+        -> host ColumnSet + status, via kx_host_decode_batch (H2D, device decode, D2H)."""
+        import numpy as np
+        ds = self.dschema
+        if var_caps is None:
+            var_caps = [0 if ci.kind == A.COL_FIXED else max(1, wire.size) for ci in ds.infos]
+        out = alloc_host(ds.infos, n, var_caps, ds.npresence)
+        kc = to_kx_columns(out, ds.infos, var_caps)
+        st = A.Status()
+        wire = np.ascontiguousarray(wire, dtype=np.uint8)
+        offp = None
+        if offsets is not None:
+            offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+            offp = offsets.ctypes.data
+        rc = lib().kx_host_decode_batch(self.ctx.handle, ds.handle, wire.ctypes.data if wire.size else None,
+                                        wire.size, offp, n, C.byref(kc), C.byref(st))
+        check(rc, "kx_host_decode_batch")
+        if raise_on_error and st.code:
+            raise ProtocolError(st.code, self._WHAT, st.record, st.offset)
+        return out, st
+
     def Marshal(self, cols: ColumnSet, with_offsets: bool = True, stream=None, out=None):
         """Encode the columns; returns (wire uint8 tensor, record offsets int64[n+1] or None)."""
         import torch
@@ -182,12 +207,12 @@ class ThriftCodec:
             total = out.numel()
         offs = torch.empty(n + 1, dtype=torch.int64, device=self.device) if with_offsets else None
         st = status_tensor(self.device)
-        rc = lib().kx_thrift_encode_batch(self.ctx.handle, ds.handle, C.byref(kc), n, _ptr(out), out.numel(),
+        rc = getattr(lib(), self._ENCODE)(self.ctx.handle, ds.handle, C.byref(kc), n, _ptr(out), out.numel(),
                                           _ptr(offs), _ptr(st), _stream_ptr(stream))
-        check(rc, "kx_thrift_encode_batch")
+        check(rc, self._ENCODE)
         s = read_status(st)
         if s.code:
-            raise ProtocolError(s.code, "thrift marshal")
+            raise ProtocolError(s.code, self._ENCODE)
         return out[:s.consumed], offs
 
     def BLength(self, cols: ColumnSet, stream=None):
@@ -195,9 +220,9 @@ class ThriftCodec:
         ds = self.dschema
         kc = to_kx_columns(cols, ds.infos)
         sizes = torch.empty(max(1, cols.n), dtype=torch.int64, device=self.device)
-        rc = lib().kx_thrift_encoded_size_batch(self.ctx.handle, ds.handle, C.byref(kc), cols.n, _ptr(sizes),
-                                                _stream_ptr(stream))
-        check(rc, "kx_thrift_encoded_size_batch")
+        rc = getattr(lib(), self._SIZE)(self.ctx.handle, ds.handle, C.byref(kc), cols.n, _ptr(sizes),
+                                        _stream_ptr(stream))
+        check(rc, self._SIZE)
         return sizes[:cols.n]
 
     def Skip(self, buf, n: int, stream=None):
@@ -225,6 +250,8 @@ class ProtobufCodec(ThriftCodec):
     `message Batch { repeated Rec recs = 1; }` (record boundaries found on the GPU)."""
 
     _DECODE = "kx_pb_decode_batch"
+    _ENCODE = "kx_pb_encode_batch"
+    _SIZE = "kx_pb_encoded_size_batch"
     _WHAT = "protobuf unmarshal"
 
     def __init__(self, schema: Schema, device: int = 0):
@@ -235,6 +262,9 @@ class ProtobufCodec(ThriftCodec):
 
     def Skip(self, buf, n: int, stream=None):
         raise KxError(A.ERR_NOT_IMPLEMENTED, "protobuf has no skip decoder")
+
+    def UnmarshalHost(self, *a, **k):
+        raise KxError(A.ERR_NOT_IMPLEMENTED, "kx_host_decode_batch is the Thrift fastUnmarshal path")
 
     name, skip = Name, Skip
 

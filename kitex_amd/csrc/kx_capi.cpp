@@ -180,6 +180,8 @@ void kx_ctx_destroy(kx_ctx* c) {
   if (c->ws) (void)hipFree(c->ws);
   if (c->ews) (void)hipFree(c->ews);
   if (c->pin) (void)hipHostFree(c->pin);
+  if (c->dstage) (void)hipFree(c->dstage);
+  if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   delete c;
 }
 
@@ -259,6 +261,12 @@ int kx_thrift_encode_batch(kx_ctx* c, const kx_schema* s, const kx_columns* in, 
                           st, false);
 }
 
+static int pb_schema_ok(const kx_schema* s) {
+  for (uint32_t f = 0; f < s->prog.nfields; f++)
+    if (s->prog.f[f].pb_wt == 7 || s->prog.ninst != 1) return KX_ERR_NOT_IMPLEMENTED;
+  return KX_OK;
+}
+
 int kx_pb_decode_batch(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len,
                        const uint64_t* offsets, uint64_t n, const kx_columns* out, uint8_t* record_status,
                        kx_status* status, void* stream) {
@@ -268,8 +276,7 @@ int kx_pb_decode_batch(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_
   hipStream_t st = (hipStream_t)stream;
   KxLaunchCols lc;
   if ((rc = to_launch_cols(s, out, &lc))) return rc;
-  for (uint32_t f = 0; f < s->prog.nfields; f++)
-    if (s->prog.f[f].pb_wt == 7 || s->prog.ninst != 1) return KX_ERR_NOT_IMPLEMENTED;
+  if ((rc = pb_schema_ok(s))) return rc;
   if (n == 0) {
     KX_HIP_CHECK(hipMemsetAsync(status, 0, sizeof(kx_status), st));
     for (uint32_t k = 0; k < s->ncols; k++)
@@ -285,10 +292,116 @@ int kx_pb_decode_batch(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_
                           epoch, st, true);
 }
 
+int kx_pb_encoded_size_batch(kx_ctx* c, const kx_schema* s, const kx_columns* in, uint64_t n,
+                             uint64_t* sizes_out, void* stream) {
+  if (!c || !s || !sizes_out) return KX_ERR_INVALID_ARG;
+  int rc = set_device(c);
+  if (rc) return rc;
+  if ((rc = pb_schema_ok(s))) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  KxLaunchCols lc;
+  if ((rc = to_launch_cols(s, in, &lc))) return rc;
+  if (n == 0) return KX_OK;
+  KxProgram* dp = nullptr;
+  if ((rc = prog_on_device(const_cast<kx_schema*>(s), c->device, &dp))) return rc;
+  if ((rc = ensure_ews(c, kx_encode_ws_bytes(n), st))) return rc;
+  return kx_launch_encode(dp, s->prog, lc, n, nullptr, 0, sizes_out, nullptr, nullptr, c->ews, c->ews_size, st,
+                          true, true);
+}
+
+int kx_pb_encode_batch(kx_ctx* c, const kx_schema* s, const kx_columns* in, uint64_t n, uint8_t* out,
+                       uint64_t out_cap, uint64_t* offsets_out, kx_status* status, void* stream) {
+  if (!c || !s || !status || (!out && out_cap)) return KX_ERR_INVALID_ARG;
+  int rc = set_device(c);
+  if (rc) return rc;
+  if ((rc = pb_schema_ok(s))) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  KxLaunchCols lc;
+  if ((rc = to_launch_cols(s, in, &lc))) return rc;
+  if (n == 0) {
+    KX_HIP_CHECK(hipMemsetAsync(status, 0, sizeof(kx_status), st));
+    if (offsets_out) KX_HIP_CHECK(hipMemsetAsync(offsets_out, 0, 8, st));
+    return KX_OK;
+  }
+  KxProgram* dp = nullptr;
+  if ((rc = prog_on_device(const_cast<kx_schema*>(s), c->device, &dp))) return rc;
+  if ((rc = ensure_ews(c, kx_encode_ws_bytes(n), st))) return rc;
+  return kx_launch_encode(dp, s->prog, lc, n, out, out_cap, nullptr, offsets_out, status, c->ews, c->ews_size,
+                          st, false, true);
+}
+
+// fastUnmarshal from host (netpoll) memory: H2D of the wire bytes (+ offsets) into a grow-only
+// device staging area, the device decode, then D2H of exactly the decoded bytes (fixed columns,
+// var offsets, var payloads up to their totals, presence) and the status. One stream, synchronous.
 int kx_host_decode_batch(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len,
                          const uint64_t* offsets, uint64_t n, const kx_columns* out, kx_status* status) {
-  (void)c; (void)s; (void)in; (void)in_len; (void)offsets; (void)n; (void)out; (void)status;
-  return KX_ERR_NOT_IMPLEMENTED;
+  if (!c || !s || !status || !out || (!in && in_len)) return KX_ERR_INVALID_ARG;
+  if (out->ncols != s->ncols) return KX_ERR_INVALID_ARG;
+  int rc = set_device(c);
+  if (rc) return rc;
+  if (!c->own_stream) KX_HIP_CHECK(hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking));
+  hipStream_t st = c->own_stream;
+  auto al = [](uint64_t x) { return (x + 255) & ~255ull; };
+  // staging layout: status | input | offsets | columns (fixed data, var offsets + arenas) | presence
+  uint64_t need = al(sizeof(kx_status)) + al(in_len) + (offsets ? al((n + 1) * 8) : 0);
+  for (uint32_t k = 0; k < s->ncols; k++) {
+    const kx_column_info& ci = s->info[k];
+    if (ci.kind == KX_COL_FIXED) need += al(n * ci.width);
+    else need += al((n + 1) * 4) + al(out->cols[k].capacity * (ci.kind == KX_COL_LIST ? ci.width : 1));
+  }
+  if (s->npres) need += al(n * 8);
+  if (c->dstage_size < need) {
+    if (c->dstage) KX_HIP_CHECK(hipFree(c->dstage));
+    c->dstage = nullptr;
+    c->dstage_size = 0;
+    KX_HIP_CHECK(hipMalloc(&c->dstage, need));
+    c->dstage_size = need;
+  }
+  char* p = (char*)c->dstage;
+  kx_status* d_st = (kx_status*)p; p += al(sizeof(kx_status));
+  uint8_t* d_in = (uint8_t*)p; p += al(in_len);
+  uint64_t* d_off = nullptr;
+  if (offsets) { d_off = (uint64_t*)p; p += al((n + 1) * 8); }
+  kx_columns dc;
+  memset(&dc, 0, sizeof dc);
+  dc.ncols = s->ncols;
+  for (uint32_t k = 0; k < s->ncols; k++) {
+    const kx_column_info& ci = s->info[k];
+    if (ci.kind == KX_COL_FIXED) {
+      dc.cols[k].data = p; p += al(n * ci.width);
+    } else {
+      dc.cols[k].offsets = (uint32_t*)p; p += al((n + 1) * 4);
+      dc.cols[k].data = p; p += al(out->cols[k].capacity * (ci.kind == KX_COL_LIST ? ci.width : 1));
+      dc.cols[k].capacity = out->cols[k].capacity;
+    }
+  }
+  if (s->npres) { dc.presence = (uint64_t*)p; p += al(n * 8); }
+  if (in_len) KX_HIP_CHECK(hipMemcpyAsync(d_in, in, in_len, hipMemcpyHostToDevice, st));
+  if (offsets) KX_HIP_CHECK(hipMemcpyAsync(d_off, offsets, (n + 1) * 8, hipMemcpyHostToDevice, st));
+  rc = kx_thrift_decode_batch(c, s, d_in, in_len, d_off, n, &dc, nullptr, d_st, st);
+  if (rc) return rc;
+  KX_HIP_CHECK(hipMemcpyAsync(status, d_st, sizeof(kx_status), hipMemcpyDeviceToHost, st));
+  // fixed columns and var offsets are needed whatever the payload totals are
+  for (uint32_t k = 0; k < s->ncols; k++) {
+    const kx_column_info& ci = s->info[k];
+    if (ci.kind == KX_COL_FIXED) {
+      if (n) KX_HIP_CHECK(hipMemcpyAsync(out->cols[k].data, dc.cols[k].data, n * ci.width, hipMemcpyDeviceToHost, st));
+    } else {
+      KX_HIP_CHECK(hipMemcpyAsync(out->cols[k].offsets, dc.cols[k].offsets, (n + 1) * 4, hipMemcpyDeviceToHost, st));
+    }
+  }
+  if (s->npres && n) KX_HIP_CHECK(hipMemcpyAsync(out->presence, dc.presence, n * 8, hipMemcpyDeviceToHost, st));
+  KX_HIP_CHECK(hipStreamSynchronize(st));
+  // var payloads: only the decoded bytes (status->var_total per var slot)
+  for (uint32_t v = 0; v < s->prog.nvar && v < KXP_NV_MAX; v++) {
+    const uint32_t k = s->prog.var_col[v];
+    const kx_column_info& ci = s->info[k];
+    const uint64_t units = status->var_total[v] < out->cols[k].capacity ? status->var_total[v] : out->cols[k].capacity;
+    const uint64_t bytes = units * (ci.kind == KX_COL_LIST ? ci.width : 1);
+    if (bytes) KX_HIP_CHECK(hipMemcpyAsync(out->cols[k].data, dc.cols[k].data, bytes, hipMemcpyDeviceToHost, st));
+  }
+  KX_HIP_CHECK(hipStreamSynchronize(st));
+  return KX_OK;
 }
 
 uint64_t kx_thrift_message_begin_length(uint32_t name_len) { return 12ull + name_len; }

@@ -377,10 +377,14 @@ __device__ __forceinline__ bool canon_record(const Src& w, const KAS KxLaunchCol
       const uint32_t o1 = 3 + st.width, o2 = o1 + 3 + s1.width, o3 = o2 + 3 + s2.width;
       const uint32_t len = m == 1 ? o1 : m == 2 ? o2 : m == 3 ? o3 : o3 + 3 + s3.width;
       if (rem < len) return false;
-      const Fetch f0 = fetch12(w, pos);
-      const Fetch f1 = fetch12(w, pos + o1);
-      const Fetch f2 = fetch12(w, pos + o2);
-      const Fetch f3 = fetch12(w, pos + o3);
+      // the walk (measure) pass only checks the headers: 2 dwords per field instead of 4
+      Fetch f0, f1, f2, f3;
+      if (emit) {
+        f0 = fetch12(w, pos); f1 = fetch12(w, pos + o1); f2 = fetch12(w, pos + o2); f3 = fetch12(w, pos + o3);
+      } else {
+        f0.w0 = ld4(w, pos); f1.w0 = ld4(w, pos + o1); f2.w0 = ld4(w, pos + o2); f3.w0 = ld4(w, pos + o3);
+        f0.w1 = f0.w2 = f1.w1 = f1.w2 = f2.w1 = f2.w2 = f3.w1 = f3.w2 = 0;
+      }
       bool ok = (f0.w0 & 0xffffffu) == (st.hdr & 0xffffffu);
       if (m > 1) ok &= (f1.w0 & 0xffffffu) == (s1.hdr & 0xffffffu);
       if (m > 2) ok &= (f2.w0 & 0xffffffu) == (s2.hdr & 0xffffffu);

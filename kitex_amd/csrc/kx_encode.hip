@@ -34,6 +34,7 @@ struct EncParams {
   kx_status* status;
   uint64_t* block_tot;   // workspace: per-block total size, then (after scan) block base
   uint64_t nblocks;
+  bool pb;               // Kitex-Protobuf records (Batch framing) instead of Thrift binary
 };
 
 __device__ __forceinline__ uint64_t var_len(const KxLaunchCols& C, int col, uint64_t r) {
@@ -121,6 +122,21 @@ __device__ __forceinline__ uint64_t load_fixed(const void* base, uint32_t w, uin
   }
 }
 
+// raw bytes into the sink, 4 at a time
+__device__ __forceinline__ void put_bytes(Sink& s, const uint8_t* src, uint32_t len) {
+  const uint64_t sa = (uint64_t)src, se = sa + len;
+  uint32_t i = 0;
+  for (; i + 4 <= len; i += 4) {
+    // unaligned 4-byte read of the source string: aligned dwords that hold string bytes only
+    uint64_t A = (sa + i) & ~3ull;
+    uint32_t sh = (uint32_t)((sa + i) & 3);
+    uint32_t x0 = *(const uint32_t*)A;
+    uint32_t x1 = (sh && A + 4 < se) ? *(const uint32_t*)(A + 4) : 0u;
+    s.put(sh ? __builtin_amdgcn_alignbyte(x1, x0, sh) : x0, 4);
+  }
+  for (; i < len; i++) s.put(src[i], 1);
+}
+
 // FastWriteNocopy for one record into the sink
 __device__ void write_record(const KxProgram& P, const KxLaunchCols& C, uint64_t r, Sink& s) {
   uint64_t pres = C.presence ? C.presence[r] : 0;
@@ -147,18 +163,7 @@ __device__ void write_record(const KxProgram& P, const KxLaunchCols& C, uint64_t
       uint64_t o = C.offs[F.col][r];
       uint32_t len = (uint32_t)var_len(C, F.col, r);
       put_be(s, len, 4);
-      const uint8_t* src = (const uint8_t*)C.data[F.col] + o;
-      const uint64_t sa = (uint64_t)src, se = sa + len;
-      uint32_t i = 0;
-      for (; i + 4 <= len; i += 4) {
-        // unaligned 4-byte read of the source string: aligned dwords that hold string bytes only
-        uint64_t A = (sa + i) & ~3ull;
-        uint32_t sh = (uint32_t)((sa + i) & 3);
-        uint32_t x0 = *(const uint32_t*)A;
-        uint32_t x1 = (sh && A + 4 < se) ? *(const uint32_t*)(A + 4) : 0u;
-        s.put(sh ? __builtin_amdgcn_alignbyte(x1, x0, sh) : x0, 4);
-      }
-      for (; i < len; i++) s.put(src[i], 1);
+      put_bytes(s, (const uint8_t*)C.data[F.col] + o, len);
     } else if (F.kind == KXP_K_LIST) {
       uint64_t o = C.offs[F.col][r];
       uint32_t cnt = (uint32_t)var_len(C, F.col, r);
@@ -177,6 +182,98 @@ __device__ void write_record(const KxProgram& P, const KxLaunchCols& C, uint64_t
     f = F.enc_next;
   }
   s.flush();
+}
+
+// ---- Kitex-Protobuf records: `0x0A uvarint(len) body` per record (the Batch message's repeated
+//      field 1), body = proto.Marshal of a flat proto3 message: fields in field-number order, zero
+//      values of implicit-presence fields omitted, optional fields when set (protobuf.go:64-134) ----
+__device__ __forceinline__ uint32_t uvarint_len(uint64_t v) {
+  const int bits = v ? 64 - __clzll((long long)v) : 1;
+  return (uint32_t)((bits + 6) / 7);
+}
+
+__device__ __forceinline__ void put_uvarint(Sink& s, uint64_t v) {
+  while (v >= 0x80) {
+    s.put((uint32_t)(v & 0x7f) | 0x80u, 1);
+    v >>= 7;
+  }
+  s.put((uint32_t)v, 1);
+}
+
+// scalar as the proto wire value: int32/int16/int8 sign-extend to 64 bits, bool -> 0/1
+__device__ __forceinline__ uint64_t pb_value(const KxpField& F, const KxLaunchCols& C, uint64_t r) {
+  uint64_t v = load_fixed(C.data[F.col], F.width, r);
+  if (F.pb_wt == 0) {
+    if (F.width == 4) v = (uint64_t)(int64_t)(int32_t)(uint32_t)v;
+    else if (F.width == 2) v = (uint64_t)(int64_t)(int16_t)(uint16_t)v;
+    else if (F.width == 1) v = F.ttype == KX_T_BOOL ? ((v & 0xff) ? 1 : 0) : (uint64_t)(int64_t)(int8_t)(uint8_t)v;
+  }
+  return v;
+}
+
+__device__ uint64_t pb_body_size(const KxProgram& P, const KxLaunchCols& C, uint64_t r) {
+  const uint64_t pres = C.presence ? C.presence[r] : 0;
+  uint64_t sz = 0;
+  for (int f = P.pb_first; f >= 0; f = P.f[f].pb_next) {
+    const KxpField F = P.f[f];
+    const bool expl = F.req == KX_REQ_OPTIONAL;
+    if (expl && !((pres >> F.pbit) & 1)) continue;
+    const uint32_t tl = uvarint_len(((uint64_t)(uint16_t)F.id << 3) | F.pb_wt);
+    if (F.pb_wt == 2) {
+      const uint64_t n = var_len(C, F.col, r);
+      if (n == 0 && !expl) continue;
+      sz += tl + uvarint_len(n) + n;
+    } else {
+      const uint64_t v = pb_value(F, C, r);
+      if (v == 0 && !expl) continue;
+      sz += tl + (F.pb_wt == 0 ? uvarint_len(v) : 8u);
+    }
+  }
+  return sz;
+}
+
+__device__ __forceinline__ uint64_t pb_record_size(const KxProgram& P, const KxLaunchCols& C, uint64_t r) {
+  const uint64_t b = pb_body_size(P, C, r);
+  return 1 + uvarint_len(b) + b;
+}
+
+__device__ void pb_write_record(const KxProgram& P, const KxLaunchCols& C, uint64_t r, Sink& s) {
+  s.put(0x0Au, 1);
+  put_uvarint(s, pb_body_size(P, C, r));
+  const uint64_t pres = C.presence ? C.presence[r] : 0;
+  for (int f = P.pb_first; f >= 0; f = P.f[f].pb_next) {
+    const KxpField F = P.f[f];
+    const bool expl = F.req == KX_REQ_OPTIONAL;
+    if (expl && !((pres >> F.pbit) & 1)) continue;
+    const uint64_t tag = ((uint64_t)(uint16_t)F.id << 3) | F.pb_wt;
+    if (F.pb_wt == 2) {
+      const uint64_t n = var_len(C, F.col, r);
+      if (n == 0 && !expl) continue;
+      put_uvarint(s, tag);
+      put_uvarint(s, n);
+      put_bytes(s, (const uint8_t*)C.data[F.col] + C.offs[F.col][r], (uint32_t)n);
+    } else {
+      const uint64_t v = pb_value(F, C, r);
+      if (v == 0 && !expl) continue;
+      put_uvarint(s, tag);
+      if (F.pb_wt == 0) {
+        put_uvarint(s, v);
+      } else {  // fixed64, little-endian
+        s.put((uint32_t)v, 4);
+        s.put((uint32_t)(v >> 32), 4);
+      }
+    }
+  }
+  s.flush();
+}
+
+__device__ __forceinline__ uint64_t any_size(const EncParams& ep, const KxProgram& P, uint64_t r) {
+  return ep.pb ? pb_record_size(P, ep.cols, r) : record_size(P, ep.cols, r);
+}
+
+__device__ __forceinline__ void any_write(const EncParams& ep, const KxProgram& P, uint64_t r, Sink& s) {
+  if (ep.pb) pb_write_record(P, ep.cols, r, s);
+  else write_record(P, ep.cols, r, s);
 }
 
 __device__ __forceinline__ uint64_t wave_incl_scan(uint64_t v, int lane) {
@@ -216,7 +313,7 @@ __global__ void __launch_bounds__(NT) size_kernel(EncParams ep) {
     uint64_t r = b * RB + k * NT + threadIdx.x;
     uint64_t sz = 0;
     if (r < ep.n) {
-      sz = record_size(P, ep.cols, r);
+      sz = any_size(ep, P, r);
       if (ep.sizes_out) ep.sizes_out[r] = sz;
     }
     acc += sz;
@@ -265,7 +362,7 @@ __global__ void __launch_bounds__(NT) write_kernel(EncParams ep) {
   uint64_t gpos = ep.block_tot[b];
   while (r < rend) {
     uint64_t my = r + threadIdx.x;
-    uint64_t sz = my < rend ? record_size(P, ep.cols, my) : 0;
+    uint64_t sz = my < rend ? any_size(ep, P, my) : 0;
     uint64_t tot;
     uint64_t pre = block_excl_scan(sz, &tot, scratch);
     const uint32_t skew = (uint32_t)(((uint64_t)ep.out + gpos) & 15);
@@ -283,7 +380,7 @@ __global__ void __launch_bounds__(NT) write_kernel(EncParams ep) {
       // a single record larger than the image: thread 0 writes it straight to HBM
       if (threadIdx.x == 0) {
         Sink s{ep.out, gpos, 0, 0};
-        write_record(P, ep.cols, r, s);
+        any_write(ep, P, r, s);
         if (ep.offsets_out) ep.offsets_out[r] = gpos;
         s_round_bytes = sz;
       }
@@ -295,7 +392,7 @@ __global__ void __launch_bounds__(NT) write_kernel(EncParams ep) {
     }
     if (threadIdx.x < take) {
       Sink s{img, skew + pre, 0, 0};
-      write_record(P, ep.cols, my, s);
+      any_write(ep, P, my, s);
       if (ep.offsets_out) ep.offsets_out[my] = gpos + pre;
     }
     __syncthreads();
@@ -328,9 +425,11 @@ size_t kx_encode_ws_bytes(uint64_t n) { return ((n + RB - 1) / RB) * 8 + 256; }
 
 int kx_launch_encode(const KxProgram* dprog, const KxProgram& hprog, const KxLaunchCols& cols, uint64_t n,
                      uint8_t* out, uint64_t out_cap, uint64_t* sizes_out, uint64_t* offsets_out,
-                     kx_status* status, void* ws, size_t ws_size, hipStream_t stream, bool sizes_only) {
+                     kx_status* status, void* ws, size_t ws_size, hipStream_t stream, bool sizes_only,
+                     bool pb) {
   (void)hprog;
   EncParams ep{};
+  ep.pb = pb;
   ep.prog = dprog; ep.cols = cols; ep.n = n; ep.out = out; ep.out_cap = out_cap;
   ep.sizes_out = sizes_out; ep.offsets_out = offsets_out; ep.status = status;
   ep.nblocks = (n + RB - 1) / RB;

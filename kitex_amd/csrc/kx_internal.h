@@ -34,6 +34,9 @@ struct kx_ctx {
   // pinned staging for kx_host_*
   void* pin = nullptr;
   size_t pin_size = 0;
+  // grow-only device staging for kx_host_decode_batch (input, offsets, columns, status)
+  void* dstage = nullptr;
+  size_t dstage_size = 0;
 };
 
 // kx_schema.cpp
@@ -60,7 +63,7 @@ size_t kx_skip_ws_bytes(uint64_t in_len);
 int kx_launch_encode(const KxProgram* dprog, const KxProgram& hprog, const KxLaunchCols& cols,
                      uint64_t n, uint8_t* out, uint64_t out_cap, uint64_t* sizes_out,
                      uint64_t* offsets_out, kx_status* status, void* ws, size_t ws_size,
-                     hipStream_t stream, bool sizes_only);
+                     hipStream_t stream, bool sizes_only, bool pb = false);
 size_t kx_encode_ws_bytes(uint64_t n);
 
 #define KX_HIP_CHECK(x)                       \

@@ -36,7 +36,7 @@ struct KxpField {      // 16 B
   uint8_t req;         // KX_REQ_*
   uint8_t flags;       // bit0: protobuf bytes (no UTF-8 check)
   uint8_t pb_wt;       // protobuf wire type for this field
-  uint8_t pad;
+  int8_t pb_next;      // next root field in field-number order (protobuf encode), -1 at the end
 };
 
 struct KxpInst {       // 32 B
@@ -90,7 +90,7 @@ struct KxProgram {
   uint8_t var_col[KXP_NV_MAX];  // var slot -> column
   uint64_t fixed_min;    // minimum encoded record size (optional unset, var empty)
   uint32_t nsteps;       // canonical plan length, 0 = no canonical fast path
-  uint32_t pad0;
+  int32_t pb_first;      // first root field in field-number order (protobuf encode), -1 if none
   uint64_t canon_pres;   // presence word of a canonical record
   uint64_t pad[1];
   KxpStep steps[KXP_MAX_STEPS];

@@ -5,6 +5,8 @@
 // (reorderStructFields, tool/internal_pkg/pluginmode/thriftgo/patcher.go:503-522).
 #include <string.h>
 
+#include <algorithm>
+
 #include "kx_internal.h"
 
 namespace {
@@ -231,6 +233,16 @@ int kx_build_program(const kx_struct_desc* structs, uint32_t nstructs, kx_schema
     I.ret_pred = P.f[I.self_field].enc_next;
   }
   P.inst[0].ret_pred = -1;
+
+  // protobuf encode order: root fields by field number (stable), proto.Marshal's deterministic order
+  {
+    const KxpInst& R0 = P.inst[0];
+    std::vector<int> ord;
+    for (int k = 0; k < R0.nfields; k++) ord.push_back(R0.first + k);
+    std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return P.f[a].id < P.f[b].id; });
+    P.pb_first = ord.empty() ? -1 : ord[0];
+    for (size_t o = 0; o < ord.size(); o++) P.f[ord[o]].pb_next = o + 1 < ord.size() ? (int8_t)ord[o + 1] : (int8_t)-1;
+  }
 
   // canonical first bytes of a record (speculative boundary signature)
   const KxpInst& R = P.inst[0];

@@ -1,0 +1,66 @@
+"""Summarise a scripts/profile_gpu.sh run into profiles/: per-kernel average duration (kernel trace)
+and HBM bytes per decode call from the PMC passes (MI355X_MICROARCH.md HBM section: FETCH_SIZE and
+WRITE_SIZE are in KiB; gfx950 FETCH_SIZE counts half of a wide streaming read -> x2).
+
+  python scripts/pmc_summary.py <gpurun_out/prof_TAG> <cfg> <mode>  -> profiles/pmc_<cfg>_<mode>.json
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+DECODE = ("index_kernel", "group_kernel", "chain_kernel", "emit_kernel", "finalize_kernel")
+
+
+def short(name):
+    for k in DECODE:
+        if k in name:
+            return k
+    return None
+
+
+def counter_sums(path, counter):
+    per = defaultdict(list)
+    for f in glob.glob(os.path.join(path, "**", "*counter_collection.csv"), recursive=True):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                k = short(row["Kernel_Name"])
+                if k and row["Counter_Name"] == counter:
+                    per[k].append(float(row["Counter_Value"]))
+    return per
+
+
+def main():
+    d, cfg, mode = sys.argv[1], sys.argv[2], sys.argv[3]
+    fetch = counter_sums(os.path.join(d, "fetch"), "FETCH_SIZE")
+    write = counter_sums(os.path.join(d, "write"), "WRITE_SIZE")
+    calls = len(fetch.get("emit_kernel", [])) or 1
+    kib = 1024.0
+    fetch_b = sum(sum(v) for v in fetch.values()) * kib * 2 / calls
+    write_b = sum(sum(v) for v in write.values()) * kib / calls
+    per_kernel = {k: {"fetch_bytes": sum(fetch.get(k, [])) * kib * 2 / calls,
+                      "write_bytes": sum(write.get(k, [])) * kib / calls} for k in DECODE}
+    dur = defaultdict(list)
+    for f in glob.glob(os.path.join(d, "stats", "**", "*kernel_trace.csv"), recursive=True):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                k = short(row["Kernel_Name"])
+                if k:
+                    dur[k].append((int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) / 1e6)
+    res = {"workload": f"{cfg}_decode_{mode}", "calls": calls,
+           "hbm_bytes_per_launch": fetch_b + write_b, "fetch_bytes_per_call": fetch_b,
+           "write_bytes_per_call": write_b, "per_kernel": per_kernel,
+           "avg_ms": {k: sum(v) / len(v) for k, v in dur.items() if v},
+           "note": "FETCH_SIZE x2 (gfx950 wide-read correction) + WRITE_SIZE, KiB -> bytes, summed over the "
+                   "decode kernels of one call; Infinity-Cache hits are counted by these counters"}
+    out = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles",
+                       f"pmc_{cfg}_{mode}.json")
+    with open(out, "w") as fh:
+        json.dump(res, fh, indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -189,3 +189,31 @@ def test_decode_beyond_2gib(torch, dev):
         del out
     del wire, src
     torch.cuda.empty_cache()
+
+
+# ---------------------------------------------------------------------------------------------
+# host-memory entry point (kx_host_decode_batch: H2D -> decode -> D2H)
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("mode", ["concat", "offsets"])
+@pytest.mark.parametrize("name", ["r2", "r3"])
+def test_host_decode_matches_oracle(torch, oracle, name, mode):
+    sch, cdc = codec(name)
+    cs = synth.GENERATORS[name](20000, start=5)
+    rc, wire, offs = oracle.encode(sch, cs)
+    o = offs if mode == "offsets" else None
+    out, st = cdc.UnmarshalHost(wire, cs.n, offsets=o)
+    rc2, exp, est, _ = oracle.decode(sch, wire, cs.n, offsets=o)
+    assert st.code == est.code == 0 and st.n_records == cs.n
+    _, infos, _ = oracle.flatten(sch)
+    from tests.helpers import assert_columns_equal
+    assert_columns_equal(out, exp, infos, cs.n)
+
+
+def test_host_decode_error_status(torch, oracle):
+    sch, cdc = codec("r2")
+    cs = synth.gen_r2(3000)
+    rc, wire, offs = oracle.encode(sch, cs)
+    wire = wire[:-5]
+    out, st = cdc.UnmarshalHost(wire, cs.n, raise_on_error=False)
+    _, _, est, _ = oracle.decode(sch, wire, cs.n)
+    assert (st.code, st.record, st.offset) == (est.code, est.record, est.offset) and st.code == A.ERR_EOF
