@@ -40,6 +40,7 @@ def parse():
     ap.add_argument("--mode", default="concat", choices=["concat", "offsets"])
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-host", action="store_true")
+    ap.add_argument("--no-concat", action="store_true", help="N>1: skip the RCCL concatenation into rank 0")
     ap.add_argument("--cpu-records", type=int, default=4 * 1024 * 1024)
     return ap.parse_args()
 
@@ -130,6 +131,24 @@ def main():
         dist.all_reduce(okt, op=dist.ReduceOp.MIN)
         ok = bool(okt.item())
 
+    # ---- N > 1: concatenation of the decoded shards into rank 0 over RCCL (reported separately) ----
+    concat = None
+    if world > 1 and not args.no_concat:
+        from kitex_amd.shard import concat_to_root
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        full = concat_to_root(out, n, infos)
+        torch.cuda.synchronize()
+        dist.barrier()
+        tc = time.perf_counter() - t0
+        shard_bytes = sum((c[0][:n + 1].numel() * 4 + int(src.cols[i][0][-1].item()) * c[1].element_size())
+                          if isinstance(c, tuple) else n * c.element_size() for i, c in enumerate(out.cols))
+        concat = {"ms": tc * 1e3, "bytes_to_root": shard_bytes * (world - 1),
+                  "gb_s": shard_bytes * (world - 1) / tc / 1e9, "ok": full is None or full.n == n * world,
+                  "note": "decoded shards -> rank 0, batched isend/irecv over RCCL (xGMI); not in value"}
+        del full
+
     steps = args.steps
     total_records = n * world * steps
     value = total_records / t_rank
@@ -170,6 +189,8 @@ def main():
                      "kernel": "decode_kernel", "avg_launch_ms": avg_launch_s * 1e3},
         "cpu_baseline": None,
     }
+    if concat is not None:
+        result["concat"] = concat
 
     if rank == 0 and world == 1 and not args.no_host and cfg != "pf":
         result["host_inclusive"] = host_inclusive(cdc, wire, n, offsets, var_caps, infos, dev)

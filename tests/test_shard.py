@@ -1,0 +1,99 @@
+"""Multi-rank path on CPU (gloo, world_size 2 and 3): record-range shards and the concatenation of
+decoded shards into rank 0 (kitex_amd/shard.py). The same code runs over RCCL/xGMI on GPUs."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from kitex_amd import schema as S
+from kitex_amd import synth
+from kitex_amd.shard import shard_range
+
+
+def test_shard_range_covers_all():
+    for n in (0, 1, 7, 1000, 16 << 20):
+        for world in (1, 2, 3, 8):
+            got = [shard_range(n, world, r) for r in range(world)]
+            assert sum(c for _, c in got) == n
+            pos = 0
+            for s, c in got:
+                assert s == pos
+                pos += c
+            assert max(c for _, c in got) - min(c for _, c in got) <= 1
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _to_torch(cs):
+    import torch
+    cols = []
+    for c in cs.cols:
+        if isinstance(c, tuple):
+            cols.append((torch.from_numpy(c[0].view(np.int32).copy()), torch.from_numpy(c[1].copy())))
+        else:
+            cols.append(torch.from_numpy(c.copy()))
+    pres = torch.from_numpy(cs.presence.view(np.int64).copy()) if cs.presence is not None else None
+    return synth.ColumnSet(cols, pres, cs.n)
+
+
+def _shift_arena(cs, shift):
+    """a decoded shard whose arenas do not start at 0 (offsets[0] = shift), as a sliced decode gives"""
+    cols = []
+    for c in cs.cols:
+        if isinstance(c, tuple):
+            off = c[0].astype(np.uint64) + shift
+            data = np.concatenate([np.zeros(shift * (c[1].itemsize and 1), dtype=c[1].dtype), c[1]])
+            cols.append((off.astype(np.uint32), data))
+        else:
+            cols.append(c)
+    return synth.ColumnSet(cols, cs.presence, cs.n)
+
+
+def _worker(rank, world, port, name, n, q):
+    import torch.distributed as dist
+
+    from kitex_amd.shard import concat_to_root
+    from oracle import oracle
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        sch = S.SCHEMAS[name]()
+        _, infos, _ = oracle.flatten(sch)
+        s0, cnt = shard_range(n, world, rank)
+        local = synth.GENERATORS[name](cnt, start=s0)
+        if rank == 1:
+            local = _shift_arena(local, 5)
+        out = concat_to_root(_to_torch(local), cnt, infos)
+        if rank == 0:
+            from tests.helpers import assert_columns_equal
+            full = synth.GENERATORS[name](n)
+            assert out.n == n
+            assert_columns_equal(out, full, infos, n)
+            for c, ci in enumerate(infos):
+                if isinstance(full.cols[c], tuple):
+                    assert int(out.cols[c][0][n]) == int(full.cols[c][0][n])
+        q.put((rank, "ok"))
+    except Exception as e:  # report to the parent
+        q.put((rank, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,name,n", [(2, "r2", 5001), (3, "r3", 2000), (2, "r1", 1)])
+def test_concat_to_root_gloo(world, name, n):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, name, n, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in ps:
+        p.join(timeout=60)
+    assert all(v == "ok" for v in res.values()), res
