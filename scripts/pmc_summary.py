@@ -16,7 +16,7 @@ DECODE = ("index_kernel", "group_kernel", "chain_kernel", "emit_kernel", "finali
 
 def short(name):
     for k in DECODE:
-        if k in name:
+        if "namespace)::" + k in name:
             return k
     return None
 
