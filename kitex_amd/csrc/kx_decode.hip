@@ -538,28 +538,43 @@ __device__ __forceinline__ void emit_defaults(const KAS KxProgram* P, const KAS 
 // order, unknown numbers and mismatched wire types skipped, the last occurrence wins, `string`
 // fields UTF-8 validated, groups (wire types 3/4) rejected.
 // ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t fbyte(const Fetch& f, int i) {
-  const uint32_t x = i < 4 ? f.w0 : i < 8 ? f.w1 : f.w2;
-  return (x >> (8 * (i & 3))) & 0xffu;
+// protowire.ConsumeVarint of the varint starting at byte 0 of f: at most 10 bytes, the 10th <= 1;
+// `rem` bytes are available. Branch-free SWAR: the terminator is the first byte with bit 7 clear,
+// the 7-bit groups of the first 8 bytes are compacted in three shift/mask steps.
+__device__ __forceinline__ int pb_varint_f(const Fetch& f, uint64_t rem, uint64_t& v, uint32_t& used) {
+  const uint64_t lo = (uint64_t)f.w0 | ((uint64_t)f.w1 << 32);
+  const uint64_t stop = ~lo & 0x8080808080808080ull;
+  const uint32_t b8 = f.w2 & 0xffu, b9 = (f.w2 >> 8) & 0xffu;
+  const uint32_t k = stop ? (uint32_t)__builtin_ctzll(stop) >> 3 : b8 < 0x80 ? 8u : b9 < 0x80 ? 9u : 10u;
+  if (k >= 9) {  // the 10th byte decides: it must exist, and be <= 1
+    if (rem <= 9) return KX_ERR_EOF;
+    if (b9 > 1) return KX_ERR_INVALID_DATA;
+  } else if ((uint64_t)k >= rem) {
+    return KX_ERR_EOF;
+  }
+  const uint64_t keep = k >= 7 ? ~0ull : (2ull << (8 * k + 7)) - 1;  // bytes 0..k
+  uint64_t x = lo & keep & 0x7f7f7f7f7f7f7f7full;
+  x = (x & 0x007f007f007f007full) | ((x & 0x7f007f007f007f00ull) >> 1);
+  x = (x & 0x00003fff00003fffull) | ((x & 0x3fff00003fff0000ull) >> 2);
+  x = (x & 0x000000000fffffffull) | ((x & 0x0fffffff00000000ull) >> 4);
+  if (k >= 8) x |= (uint64_t)(b8 & 0x7f) << 56;
+  if (k >= 9) x |= (uint64_t)(b9 & 0x01) << 63;
+  v = x;
+  used = k + 1;
+  return KX_OK;
 }
 
-// protowire.ConsumeVarint at p: at most 10 bytes, the 10th <= 1; `rem` bytes are available
 __device__ __forceinline__ int pb_varint(const Src& w, uint64_t p, uint64_t rem, uint64_t& v, uint32_t& used) {
-  const Fetch f = fetch12(w, p);
-  uint64_t x = 0;
-#pragma unroll
-  for (int i = 0; i < 10; i++) {
-    if ((uint64_t)i >= rem) return KX_ERR_EOF;
-    const uint32_t c = fbyte(f, i);
-    if (i == 9 && c > 1) return KX_ERR_INVALID_DATA;
-    x |= (uint64_t)(c & 0x7f) << (7 * i);
-    if (c < 0x80) {
-      v = x;
-      used = (uint32_t)i + 1;
-      return KX_OK;
-    }
-  }
-  return KX_ERR_INVALID_DATA;
+  return pb_varint_f(fetch12(w, p), rem, v, used);
+}
+
+// the 12-byte fetch advanced by u (<= 2) bytes: the value after a 1- or 2-byte tag
+__device__ __forceinline__ Fetch fetch_skip(const Fetch& f, uint32_t u) {
+  Fetch g;
+  g.w0 = __builtin_amdgcn_alignbyte(f.w1, f.w0, u);
+  g.w1 = __builtin_amdgcn_alignbyte(f.w2, f.w1, u);
+  g.w2 = __builtin_amdgcn_alignbyte(0u, f.w2, u);
+  return g;
 }
 
 // utf8.Valid (what protobuf-go enforces on proto3 `string` fields), byte by byte
@@ -617,9 +632,13 @@ __device__ __forceinline__ int pb_body(const Src& w, const KAS KxProgram* P, con
   while (pos < limit) {
     uint64_t tag;
     uint32_t u;
-    int rc = pb_varint(w, pos, limit - pos, tag, u);
+    const Fetch ft = fetch12(w, pos);
+    int rc = pb_varint_f(ft, limit - pos, tag, u);
     if (rc) return rc;
     pos += u;
+    // value bytes: from the same fetch when the tag is short (value varints need <= 10 of the
+    // remaining 12 - u bytes)
+    const Fetch fv = u <= 2 ? fetch_skip(ft, u) : fetch12(w, pos);
     const uint64_t num = tag >> 3;
     const uint32_t wt = (uint32_t)tag & 7u;
     if (num == 0 || num > 536870911ull) return KX_ERR_INVALID_DATA;
@@ -637,7 +656,7 @@ __device__ __forceinline__ int pb_body(const Src& w, const KAS KxProgram* P, con
     if (fi < 0 || F.pb_wt != wt) {  // unknown number / other wire type: skipped (ConsumeFieldValue)
       if (wt == 0) {
         uint64_t v;
-        if ((rc = pb_varint(w, pos, rem, v, u))) return rc;
+        if ((rc = pb_varint_f(fv, rem, v, u))) return rc;
         pos += u;
       } else if (wt == 1 || wt == 5) {
         const uint32_t k = wt == 1 ? 8u : 4u;
@@ -645,7 +664,7 @@ __device__ __forceinline__ int pb_body(const Src& w, const KAS KxProgram* P, con
         pos += k;
       } else if (wt == 2) {
         uint64_t l;
-        if ((rc = pb_varint(w, pos, rem, l, u))) return rc;
+        if ((rc = pb_varint_f(fv, rem, l, u))) return rc;
         if (l > rem - u) return KX_ERR_EOF;
         pos += u + l;
       } else {
@@ -656,18 +675,17 @@ __device__ __forceinline__ int pb_body(const Src& w, const KAS KxProgram* P, con
     pred = fi + 1 < nf ? fi + 1 : 0;
     if (wt == 0) {
       uint64_t v;
-      if ((rc = pb_varint(w, pos, rem, v, u))) return rc;
+      if ((rc = pb_varint_f(fv, rem, v, u))) return rc;
       pos += u;
       if (F.ttype == KX_T_BOOL) v = v != 0;
       if (emit) store_col(cols.data[F.col], F.width, rec, v);  // int32: low 32 bits
     } else if (wt == 1) {
       if (rem < 8) return KX_ERR_EOF;
-      const Fetch f = fetch12(w, pos);
-      if (emit) store_col(cols.data[F.col], F.width, rec, (uint64_t)f.w0 | ((uint64_t)f.w1 << 32));
+      if (emit) store_col(cols.data[F.col], F.width, rec, (uint64_t)fv.w0 | ((uint64_t)fv.w1 << 32));
       pos += 8;
     } else {
       uint64_t l;
-      if ((rc = pb_varint(w, pos, rem, l, u))) return rc;
+      if ((rc = pb_varint_f(fv, rem, l, u))) return rc;
       pos += u;
       if (l > rem - u) return KX_ERR_EOF;
       if (!(F.flags & 1) && !pb_utf8_ok(w, pos, l)) return KX_ERR_INVALID_DATA;
@@ -855,32 +873,36 @@ __device__ __forceinline__ bool get_words(const uint64_t* base, uint64_t nitems,
   }
 }
 
-// first canonical signature (3 bytes) in a lane's 128-byte segment, read from the LDS window with
-// a SWAR test for the first signature byte and an exact 3-byte check on hits. Segments are 128 B
-// apart, so lanes reading dword i of their segment together would all hit one LDS bank; each lane
-// instead starts at dword (lane mod 33) and rotates through its 33 dwords (conflict-free), keeping
-// the lowest hit.
+// 0x80 in every byte of v that is 0x00, nothing elsewhere (exact, no borrow false positives)
+__device__ __forceinline__ uint32_t zero_bytes(uint32_t v) {
+  return ~(((v & 0x7f7f7f7fu) + 0x7f7f7f7fu) | v | 0x7f7f7f7fu);
+}
+
+// first canonical signature (3 bytes) in a lane's 128-byte segment, read from the LDS window. All
+// four alignments of a dword are tested at once (byte j matches iff bytes j, j+1, j+2 equal the
+// signature: OR of the three XORs is zero), so the loop is branch-free whatever the data (the first
+// signature byte alone, e.g. 0x0A = T_I64, occurs every few bytes). Segments are 128 B apart, so
+// lanes reading dword i of their segment together would all hit one LDS bank; each lane instead
+// starts at dword (lane mod 33) and rotates through its 33 dwords (conflict-free), keeping the
+// lowest hit.
 __device__ __forceinline__ uint64_t scan_segment(const Src& w, int32_t q0, uint64_t seg_lo, uint64_t plim,
                                                  uint32_t sig, int lane) {
   const LDS uint32_t* s = w.win + (q0 >> 2);
   const int sh0 = q0 & 3;
-  const uint32_t b0 = (sig & 0xff) * 0x01010101u;
+  const uint32_t b0 = (sig & 0xff) * 0x01010101u, b1 = ((sig >> 8) & 0xff) * 0x01010101u;
+  const uint32_t b2 = ((sig >> 16) & 0xff) * 0x01010101u;
+  const uint32_t first_mask = 0xffffffffu << (8 * sh0);                 // dword 0: from the segment start
+  const uint32_t last_mask = sh0 ? 0xffffffffu >> (8 * (4 - sh0)) : 0u;  // dword 32: up to the segment end
   int idx = lane % 33;
-  int best = 1 << 30;
-#pragma unroll 4
+  int best = SEG;
+#pragma unroll 3
   for (int i = 0; i < 33; i++) {
     const uint32_t x0 = s[idx], x1 = s[idx + 1];
-    const uint32_t t = x0 ^ b0;
-    const uint32_t z = (t - 0x01010101u) & ~t & 0x80808080u;   // bytes equal to the first sig byte
-    if (z) {
-#pragma unroll
-      for (int j = 0; j < 4; j++) {
-        const int rel = 4 * idx + j - sh0;
-        if (((z >> (8 * j + 7)) & 1) && rel >= 0 && rel < best &&
-            (__builtin_amdgcn_alignbyte(x1, x0, j) & 0xffffffu) == sig)
-          best = rel;
-      }
-    }
+    uint32_t m = zero_bytes((x0 ^ b0) | (__builtin_amdgcn_alignbyte(x1, x0, 1) ^ b1) |
+                            (__builtin_amdgcn_alignbyte(x1, x0, 2) ^ b2));
+    m &= idx == 0 ? first_mask : idx == 32 ? last_mask : 0xffffffffu;
+    const int rel = m ? 4 * idx + (int)(__builtin_ctz(m) >> 3) - sh0 : SEG;
+    best = min(best, rel);
     idx = idx == 32 ? 0 : idx + 1;
   }
   return (best < SEG && seg_lo + (uint64_t)best < plim) ? seg_lo + (uint64_t)best : X_NONE;
