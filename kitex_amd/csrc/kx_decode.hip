@@ -542,6 +542,12 @@ __device__ __forceinline__ void emit_defaults(const KAS KxProgram* P, const KAS 
 // `rem` bytes are available. Branch-free SWAR: the terminator is the first byte with bit 7 clear,
 // the 7-bit groups of the first 8 bytes are compacted in three shift/mask steps.
 __device__ __forceinline__ int pb_varint_f(const Fetch& f, uint64_t rem, uint64_t& v, uint32_t& used) {
+  if (!(f.w0 & 0x80u)) {  // one byte: tags, lengths < 128, small values (usually wave-uniform)
+    if (rem < 1) return KX_ERR_EOF;
+    v = f.w0 & 0x7fu;
+    used = 1;
+    return KX_OK;
+  }
   const uint64_t lo = (uint64_t)f.w0 | ((uint64_t)f.w1 << 32);
   const uint64_t stop = ~lo & 0x8080808080808080ull;
   const uint32_t b8 = f.w2 & 0xffu, b9 = (f.w2 >> 8) & 0xffu;
