@@ -884,34 +884,39 @@ __device__ __forceinline__ uint32_t zero_bytes(uint32_t v) {
   return ~(((v & 0x7f7f7f7fu) + 0x7f7f7f7fu) | v | 0x7f7f7f7fu);
 }
 
+// bytes j of the stream x0|x1 (little-endian dwords) where bytes j, j+1, j+2 equal the signature
+__device__ __forceinline__ uint32_t sig_hits(uint32_t x0, uint32_t x1, uint32_t b0, uint32_t b1, uint32_t b2) {
+  return zero_bytes((x0 ^ b0) | (__builtin_amdgcn_alignbyte(x1, x0, 1) ^ b1) |
+                    (__builtin_amdgcn_alignbyte(x1, x0, 2) ^ b2));
+}
+
+// byte index of the lowest hit, or >= 0x1fffffff when there is none (v_ffbl returns -1 for 0)
+__device__ __forceinline__ uint32_t first_hit(uint32_t m) { return (uint32_t)(__builtin_ffs((int)m) - 1) >> 3; }
+
 // first canonical signature (3 bytes) in a lane's 128-byte segment, read from the LDS window. All
 // four alignments of a dword are tested at once (byte j matches iff bytes j, j+1, j+2 equal the
-// signature: OR of the three XORs is zero), so the loop is branch-free whatever the data (the first
-// signature byte alone, e.g. 0x0A = T_I64, occurs every few bytes). Segments are 128 B apart, so
-// lanes reading dword i of their segment together would all hit one LDS bank; each lane instead
-// starts at dword (lane mod 33) and rotates through its 33 dwords (conflict-free), keeping the
-// lowest hit.
+// signature: OR of the three XORs is zero), so the loop is branch- and select-free whatever the data
+// (the first signature byte alone, e.g. 0x0A = T_I64, occurs every few bytes). Segments are 128 B
+// apart, so lanes reading dword i of their segment together would all hit one LDS bank; each lane
+// starts at dword (lane mod 33) and rotates through its 33 dwords (conflict-free), keeping the lowest
+// hit. Hits before the segment start wrap to huge unsigned offsets and lose every min; a hit of the
+// first dword that sits above such a one is missed, which only costs a repair round (the candidate
+// is speculation: the chain from the lane / tile below decides).
 __device__ __forceinline__ uint64_t scan_segment(const Src& w, int32_t q0, uint64_t seg_lo, uint64_t plim,
                                                  uint32_t sig, int lane) {
   const LDS uint32_t* s = w.win + (q0 >> 2);
-  const int sh0 = q0 & 3;
+  const uint32_t sh0 = q0 & 3;
   const uint32_t b0 = (sig & 0xff) * 0x01010101u, b1 = ((sig >> 8) & 0xff) * 0x01010101u;
   const uint32_t b2 = ((sig >> 16) & 0xff) * 0x01010101u;
-  const uint32_t first_mask = 0xffffffffu << (8 * sh0);                 // dword 0: from the segment start
-  const uint32_t last_mask = sh0 ? 0xffffffffu >> (8 * (4 - sh0)) : 0u;  // dword 32: up to the segment end
+  uint32_t best = SEG;
   int idx = lane % 33;
-  int best = SEG;
 #pragma unroll 3
   for (int i = 0; i < 33; i++) {
-    const uint32_t x0 = s[idx], x1 = s[idx + 1];
-    uint32_t m = zero_bytes((x0 ^ b0) | (__builtin_amdgcn_alignbyte(x1, x0, 1) ^ b1) |
-                            (__builtin_amdgcn_alignbyte(x1, x0, 2) ^ b2));
-    m &= idx == 0 ? first_mask : idx == 32 ? last_mask : 0xffffffffu;
-    const int rel = m ? 4 * idx + (int)(__builtin_ctz(m) >> 3) - sh0 : SEG;
-    best = min(best, rel);
+    const uint32_t m = sig_hits(s[idx], s[idx + 1], b0, b1, b2);
+    best = min(best, (uint32_t)(4 * idx) - sh0 + first_hit(m));
     idx = idx == 32 ? 0 : idx + 1;
   }
-  return (best < SEG && seg_lo + (uint64_t)best < plim) ? seg_lo + (uint64_t)best : X_NONE;
+  return (best < (uint32_t)SEG && seg_lo + best < plim) ? seg_lo + best : X_NONE;
 }
 
 // Kitex-Protobuf record candidate at p: a Batch frame header (0x0A, uvarint length) whose body fits
