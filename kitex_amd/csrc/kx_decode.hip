@@ -879,14 +879,18 @@ __device__ __forceinline__ bool get_words(const uint64_t* base, uint64_t nitems,
   }
 }
 
+// 0x80 in the lowest byte of v that is 0x00 (bytes above it may be flagged spuriously)
+__device__ __forceinline__ uint32_t low_zero_byte(uint32_t v) { return (v - 0x01010101u) & ~v & 0x80808080u; }
+
 // 0x80 in every byte of v that is 0x00, nothing elsewhere (exact, no borrow false positives)
 __device__ __forceinline__ uint32_t zero_bytes(uint32_t v) {
   return ~(((v & 0x7f7f7f7fu) + 0x7f7f7f7fu) | v | 0x7f7f7f7fu);
 }
 
 // bytes j of the stream x0|x1 (little-endian dwords) where bytes j, j+1, j+2 equal the signature
+// (the lowest flagged byte of the borrow-based zero test is exact, and only the lowest is used)
 __device__ __forceinline__ uint32_t sig_hits(uint32_t x0, uint32_t x1, uint32_t b0, uint32_t b1, uint32_t b2) {
-  return zero_bytes((x0 ^ b0) | (__builtin_amdgcn_alignbyte(x1, x0, 1) ^ b1) |
+  return low_zero_byte((x0 ^ b0) | (__builtin_amdgcn_alignbyte(x1, x0, 1) ^ b1) |
                     (__builtin_amdgcn_alignbyte(x1, x0, 2) ^ b2));
 }
 
@@ -1059,6 +1063,12 @@ __device__ Agg walk_tile(KParams& dp, const Src& w, uint64_t tlo, uint64_t thi, 
       for (uint64_t p = seg_lo; p < plim; p++)
         if ((ld4(w, p) & smask) == sig) { ent = p; break; }
     }
+  }
+  if (dp.diag & 512) {  // diagnostics: DMA + candidate scan only
+    Agg a;
+    a.ent = __ballot(ent != X_NONE) ? ent : X_NONE; a.ex = thi; a.cnt = 0; a.errc = 0; a.errp = 0;
+    for (int v = 0; v < NV; v++) a.var[v] = 0;
+    return a;
   }
   uint64_t tp = (dp.diag & 64) ? __builtin_amdgcn_s_memtime() : 0;
   auto phase = [&](int k) {
