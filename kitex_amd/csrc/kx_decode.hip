@@ -938,38 +938,42 @@ __device__ __forceinline__ bool pb_frame_ok(const Src& w, uint64_t p, uint64_t l
   return e == len || ld1(w, e) == 0x0Au;
 }
 
-// first Kitex-Protobuf candidate in a lane's segment [seg_lo, seg_hi) (rotated like scan_segment)
+// Kitex-Protobuf candidate in a lane's segment [seg_lo, seg_hi): the rotated, conflict-free scan
+// (as scan_segment) keeps the two lowest 0x0A bytes, then only those two are validated as frame
+// headers. Frame validation is a varint decode plus two probes, far too costly to run for every
+// 0x0A byte inside the scan loop (a divergent branch taken by the whole wave). If neither validates
+// the lane has no candidate and takes its entry from the chain below (speculation only).
 __device__ __forceinline__ uint64_t pb_scan_segment(const Src& w, uint64_t seg_lo, uint64_t seg_hi, uint64_t len,
                                                     int lane) {
   const int32_t q0 = wofs(w, seg_lo, SEG + 8);
-  const int n = (int)(seg_hi - seg_lo);
-  int best = 1 << 30;
+  const uint32_t n = (uint32_t)(seg_hi - seg_lo);
+  uint32_t c1 = ~0u, c2 = ~0u;  // the two lowest 0x0A offsets in the segment
   if (q0 >= 0 && n == SEG) {
     const LDS uint32_t* s = w.win + (q0 >> 2);
-    const int sh0 = q0 & 3;
+    const uint32_t sh0 = q0 & 3;
     int idx = lane % 33;
+#pragma unroll 3
     for (int i = 0; i < 33; i++) {
-      const uint32_t x0 = s[idx];
-      const uint32_t t = x0 ^ 0x0A0A0A0Au;
-      uint32_t z = (t - 0x01010101u) & ~t & 0x80808080u;
-      while (z) {
-        const int j = __builtin_ctz(z) >> 3;
-        z &= z - 1;
-        const int rel = 4 * idx + j - sh0;
-        if (rel >= 0 && rel < best && rel < SEG && ((x0 >> (8 * j)) & 0xffu) == 0x0Au &&
-            pb_frame_ok(w, seg_lo + (uint64_t)rel, len))
-          best = rel;
-      }
+      uint32_t m = zero_bytes(s[idx] ^ 0x0A0A0A0Au);
+      const uint32_t base = (uint32_t)(4 * idx) - sh0;  // bytes before the segment wrap to huge offsets
+      const uint32_t h1 = base + first_hit(m);
+      m &= m - 1;
+      const uint32_t h2 = base + first_hit(m);
+      const uint32_t lo = min(c1, h1);
+      c2 = min(min(c2, h2), max(c1, h1));
+      c1 = lo;
       idx = idx == 32 ? 0 : idx + 1;
     }
   } else {
-    for (int rel = 0; rel < n; rel++)
-      if (ld1(w, seg_lo + (uint64_t)rel) == 0x0Au && pb_frame_ok(w, seg_lo + (uint64_t)rel, len)) {
-        best = rel;
-        break;
+    for (uint32_t rel = 0; rel < n; rel++)
+      if (ld1(w, seg_lo + rel) == 0x0Au) {
+        if (c1 == ~0u) c1 = rel;
+        else { c2 = rel; break; }
       }
   }
-  return best < SEG ? seg_lo + (uint64_t)best : X_NONE;
+  if (c1 < n && pb_frame_ok(w, seg_lo + c1, len)) return seg_lo + c1;
+  if (c2 < n && pb_frame_ok(w, seg_lo + c2, len)) return seg_lo + c2;
+  return X_NONE;
 }
 
 // ---------------------------------------------------------------------------------------------
