@@ -631,7 +631,7 @@ __device__ __forceinline__ bool pb_utf8_ok(const Src& w, uint64_t p, uint64_t n)
 template <int NV>
 __device__ __forceinline__ int pb_body(const Src& w, const KAS KxProgram* P, const KAS KxLaunchCols& cols,
                                        uint64_t start, uint64_t limit, uint64_t rec, bool emit,
-                                       VarState<NV>& vs, uint64_t& pres_out) {
+                                       VarState<NV>& vs, uint64_t& pres_out, bool utf8 = true) {
   uint64_t pos = start, seen = 0, pres = 0;
   const int nf = (int)P->nfields;
   int pred = 0;  // fields usually arrive in field-number order: try the one after the last match first
@@ -694,7 +694,7 @@ __device__ __forceinline__ int pb_body(const Src& w, const KAS KxProgram* P, con
       if ((rc = pb_varint_f(fv, rem, l, u))) return rc;
       pos += u;
       if (l > rem - u) return KX_ERR_EOF;
-      if (!(F.flags & 1) && !pb_utf8_ok(w, pos, l)) return KX_ERR_INVALID_DATA;
+      if (utf8 && !(F.flags & 1) && !pb_utf8_ok(w, pos, l)) return KX_ERR_INVALID_DATA;
       vset<NV>(vs, F.vslot, pos, (uint32_t)l);
       pos += l;
     }
@@ -1027,7 +1027,9 @@ __device__ __forceinline__ int parse_record(KParams& dp, const Src& w, uint64_t 
       e = b + l;
     }
     *end = e;
-    return pb_body<NV>(w, dp.prog, dp.cols, b, e, r, emit, vs, pres);
+    // concatenated mode: the index pass already validated every record the chain reaches, so the
+    // emit pass skips the UTF-8 check; with known extents the emit pass is the validator
+    return pb_body<NV>(w, dp.prog, dp.cols, b, e, r, emit, vs, pres, !emit || dp.offsets != nullptr);
   }
   uint64_t p2 = pos;
   const int rc = dskip_body(w, p2, lim, KX_T_STRUCT, 64);
