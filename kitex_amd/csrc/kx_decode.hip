@@ -923,6 +923,32 @@ __device__ __forceinline__ uint64_t scan_segment(const Src& w, int32_t q0, uint6
   return (best < (uint32_t)SEG && seg_lo + best < plim) ? seg_lo + best : X_NONE;
 }
 
+// the two lowest signature offsets of the segment (same scan; >= SEG when absent), for schemas
+// whose signature also starts a nested struct
+__device__ __forceinline__ void scan_segment2(const Src& w, int32_t q0, uint32_t sig, int lane, uint32_t& c1,
+                                              uint32_t& c2) {
+  const LDS uint32_t* s = w.win + (q0 >> 2);
+  const uint32_t sh0 = q0 & 3;
+  const uint32_t b0 = (sig & 0xff) * 0x01010101u, b1 = ((sig >> 8) & 0xff) * 0x01010101u;
+  const uint32_t b2 = ((sig >> 16) & 0xff) * 0x01010101u;
+  c1 = ~0u;
+  c2 = ~0u;
+  int idx = lane % 33;
+  for (int i = 0; i < 33; i++) {
+    const uint32_t x0 = s[idx], x1 = s[idx + 1];
+    uint32_t m = zero_bytes((x0 ^ b0) | (__builtin_amdgcn_alignbyte(x1, x0, 1) ^ b1) |
+                            (__builtin_amdgcn_alignbyte(x1, x0, 2) ^ b2));
+    const uint32_t base = (uint32_t)(4 * idx) - sh0;
+    const uint32_t h1 = base + first_hit(m);
+    m &= m - 1;
+    const uint32_t h2 = base + first_hit(m);
+    const uint32_t lo = min(c1, h1);
+    c2 = min(min(c2, h2), max(c1, h1));
+    c1 = lo;
+    idx = idx == 32 ? 0 : idx + 1;
+  }
+}
+
 // Kitex-Protobuf record candidate at p: a Batch frame header (0x0A, uvarint length) whose body fits
 // the input, starts with a plausible tag, and is followed by the next frame's 0x0A (or the end).
 __device__ __forceinline__ int pb_varint(const Src& w, uint64_t p, uint64_t rem, uint64_t& v, uint32_t& used);
@@ -1062,7 +1088,20 @@ __device__ Agg walk_tile(KParams& dp, const Src& w, uint64_t tlo, uint64_t thi, 
     const uint32_t slen = (MODE == M_THRIFT && P->sig_len == 3) ? 3u : 1u;
     const uint64_t plim = min(seg_hi, dp.in_len >= slen ? dp.in_len - slen + 1 : 0ull);
     const int32_t q0 = wofs(w, seg_lo, SEG + 12);
-    if (slen == 3 && seg_hi - seg_lo == SEG && q0 >= 0) {
+    if (slen == 3 && seg_hi - seg_lo == SEG && q0 >= 0 && MODE == M_THRIFT && P->sig_ambig && w.nsteps) {
+      // the signature also starts a nested struct: keep the lowest of the two lowest hits that parses
+      // as a canonical record (a nested-struct start does not), else no candidate (speculation only)
+      uint32_t c1, c2;
+      scan_segment2(w, q0, sig, lane, c1, c2);
+      VarState<NV> vs0;
+      uint64_t e0;
+      if (c1 < (uint32_t)SEG && seg_lo + c1 < plim &&
+          canon_record<NV>(w, dp.cols, seg_lo + c1, dp.in_len, 0, false, &e0, vs0))
+        ent = seg_lo + c1;
+      else if (c2 < (uint32_t)SEG && seg_lo + c2 < plim &&
+               canon_record<NV>(w, dp.cols, seg_lo + c2, dp.in_len, 0, false, &e0, vs0))
+        ent = seg_lo + c2;
+    } else if (slen == 3 && seg_hi - seg_lo == SEG && q0 >= 0) {
       ent = scan_segment(w, q0, seg_lo, plim, sig, lane);
     } else {
       const uint32_t smask = slen == 3 ? 0xffffffu : 0xffu;

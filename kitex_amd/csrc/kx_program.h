@@ -92,7 +92,8 @@ struct KxProgram {
   uint32_t nsteps;       // canonical plan length, 0 = no canonical fast path
   int32_t pb_first;      // first root field in field-number order (protobuf encode), -1 if none
   uint64_t canon_pres;   // presence word of a canonical record
-  uint64_t pad[1];
+  uint32_t sig_ambig;    // the signature is also the first header of a nested struct: validate candidates
+  uint32_t pad1;
   KxpStep steps[KXP_MAX_STEPS];
 };
 

@@ -250,6 +250,16 @@ int kx_build_program(const kx_struct_desc* structs, uint32_t nstructs, kx_schema
     const KxpField& F = P.f[R.enc_first];
     P.sig = (uint32_t)F.ttype | ((uint32_t)((uint16_t)F.id >> 8) << 8) | ((uint32_t)(F.id & 0xff) << 16);
     P.sig_len = 3;
+    // a nested struct whose encoder-first field has the same header makes every occurrence of that
+    // struct a false record candidate (R3: Inner.x and R3.id are both `i64, id 1`)
+    P.sig_ambig = 0;
+    for (uint32_t i = 1; i < P.ninst; i++) {
+      const int ef = P.inst[i].enc_first;
+      if (ef < 0) continue;
+      const KxpField& G = P.f[ef];
+      const uint32_t h = (uint32_t)G.ttype | ((uint32_t)((uint16_t)G.id >> 8) << 8) | ((uint32_t)(G.id & 0xff) << 16);
+      if (h == P.sig) P.sig_ambig = 1;
+    }
   } else {
     P.sig = 0;
     P.sig_len = 1;
