@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define KX_ABI_VERSION 1
+#define KX_ABI_VERSION 2
 
 /* ---- Thrift TType ids (gopkg protocol/thrift; pinned by pkg/protocol/bthrift/binary_test.go) ---- */
 enum {
@@ -94,16 +94,19 @@ typedef struct kx_schema kx_schema; /* opaque */
 
 /* Column kinds produced by flattening (depth-first over the IDL, struct fields inlined). */
 enum {
-  KX_COL_FIXED = 1,   /* one value per record, width 1/2/4/8 bytes, host (little-endian) order */
-  KX_COL_BYTES = 2,   /* string/binary: u32 offsets[n+1] (bytes) + data arena */
-  KX_COL_LIST = 3     /* list/set of fixed scalars: u32 offsets[n+1] (elements) + element arena */
+  KX_COL_FIXED = 1,      /* one value per record, width 1/2/4/8 bytes, host (little-endian) order */
+  KX_COL_BYTES = 2,      /* string/binary: offsets[n+1] (bytes) + data arena */
+  KX_COL_LIST = 3,       /* list/set of fixed scalars (or one side of a map of them):
+                            offsets[n+1] (elements) + element arena */
+  KX_COL_LIST_BYTES = 4  /* list/set of strings (or the string side of a map): offsets[n+1]
+                            (elements), elem_offsets[elements+1] (bytes) + byte arena */
 };
 
 typedef struct kx_column_info {
   uint32_t kind;        /* KX_COL_* */
-  uint32_t width;       /* FIXED: value width; LIST: element width; BYTES: 1 */
-  uint8_t ttype;        /* wire type of the field (LIST/SET for lists) */
-  uint8_t elem_ttype;   /* LIST: element wire type */
+  uint32_t width;       /* FIXED: value width; LIST: element width; BYTES / LIST_BYTES: 1 */
+  uint8_t ttype;        /* wire type of the field (LIST/SET/MAP for containers) */
+  uint8_t elem_ttype;   /* LIST / LIST_BYTES: element wire type */
   int16_t field_id;     /* id of the leaf field */
   int32_t presence_bit; /* bit in the presence word for this field, or -1 */
   uint32_t depth;       /* nesting depth (0 = root field) */
@@ -111,11 +114,18 @@ typedef struct kx_column_info {
 } kx_column_info;
 
 /* A batch of decoded records in struct-of-arrays form. All pointers are DEVICE memory for the
- * *_batch calls and HOST memory for kx_host_* calls. */
+ * *_batch calls and HOST memory for kx_host_* calls.
+ * Offsets are unsigned, `offset_bytes` wide (4 = uint32_t, the default when 0; 8 = uint64_t). With
+ * 4-byte offsets a column whose arena position would pass UINT32_MAX fails with KX_ERR_SIZE_LIMIT
+ * (it never wraps); use 8-byte offsets for arenas of 4 GiB units and more. */
 typedef struct kx_column {
-  void* data;           /* FIXED: n*width bytes; BYTES/LIST: arena */
-  uint32_t* offsets;    /* BYTES/LIST: n+1 entries (arena units: bytes or elements); FIXED: NULL */
-  uint64_t capacity;    /* BYTES/LIST: arena capacity in arena units; FIXED: ignored */
+  void* data;             /* FIXED: n*width bytes; BYTES/LIST/LIST_BYTES: arena */
+  void* offsets;          /* BYTES/LIST/LIST_BYTES: n+1 entries (bytes / elements); FIXED: NULL */
+  uint64_t capacity;      /* arena capacity in arena units (bytes; LIST: elements); FIXED: ignored */
+  void* elem_offsets;     /* LIST_BYTES: byte offset of every element (elem_capacity+1 entries) */
+  uint64_t elem_capacity; /* LIST_BYTES: element capacity */
+  uint32_t offset_bytes;  /* 4 (or 0) / 8: width of offsets and elem_offsets entries */
+  uint32_t reserved0;
 } kx_column;
 
 #define KX_MAX_COLUMNS 32

@@ -6,7 +6,7 @@ layout is checked by tests/test_abi.py against the compiled library.
 """
 import ctypes as C
 
-KX_ABI_VERSION = 1
+KX_ABI_VERSION = 2
 
 # Thrift TType ids (gopkg protocol/thrift; pinned by pkg/protocol/bthrift/binary_test.go)
 T_STOP, T_VOID, T_BOOL, T_BYTE, T_DOUBLE = 0, 1, 2, 3, 4
@@ -31,7 +31,7 @@ ERR_INTERNAL = 103
 REQ_DEFAULT, REQ_REQUIRED, REQ_OPTIONAL = 0, 1, 2
 FIELD_BINARY = 1  # kx_field_desc.reserved0 flag: protobuf `bytes` (no UTF-8 validation)
 
-COL_FIXED, COL_BYTES, COL_LIST = 1, 2, 3
+COL_FIXED, COL_BYTES, COL_LIST, COL_LIST_BYTES = 1, 2, 3, 4
 MAX_COLUMNS = 32
 MAX_STRUCTS = 16
 
@@ -68,7 +68,9 @@ class ColumnInfo(C.Structure):
 
 
 class Column(C.Structure):
-    _fields_ = [("data", C.c_void_p), ("offsets", C.c_void_p), ("capacity", C.c_uint64)]
+    _fields_ = [("data", C.c_void_p), ("offsets", C.c_void_p), ("capacity", C.c_uint64),
+                ("elem_offsets", C.c_void_p), ("elem_capacity", C.c_uint64),
+                ("offset_bytes", C.c_uint32), ("reserved0", C.c_uint32)]
 
 
 class Columns(C.Structure):
@@ -95,7 +97,8 @@ class Status(C.Structure):
 
 assert C.sizeof(FieldDesc) == 16
 assert C.sizeof(Status) == 128
-assert C.sizeof(Columns) == MAX_COLUMNS * 24 + 16
+assert C.sizeof(Column) == 48
+assert C.sizeof(Columns) == MAX_COLUMNS * 48 + 16
 
 ERROR_NAMES = {
     OK: "ok",

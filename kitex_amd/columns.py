@@ -25,8 +25,17 @@ def _ptr(x) -> int:
     return x.data_ptr()
 
 
+def _numel(x) -> int:
+    return x.numel() if hasattr(x, "numel") else x.size
+
+
+def _itemsize(x) -> int:
+    return x.element_size() if hasattr(x, "element_size") else x.itemsize
+
+
 def to_kx_columns(cs: ColumnSet, infos: Sequence[A.ColumnInfo], caps: Sequence[int] = None) -> A.Columns:
-    """Describe a ColumnSet to the C-ABI. `caps[c]` overrides a var column's arena capacity."""
+    """Describe a ColumnSet to the C-ABI. `caps[c]` lowers a var column's arena capacity (never
+    above the arena actually allocated). Offsets may be 4- or 8-byte integers (kx_column.offset_bytes)."""
     out = A.Columns()
     out.ncols = len(infos)
     for c, ci in enumerate(infos):
@@ -34,41 +43,62 @@ def to_kx_columns(cs: ColumnSet, infos: Sequence[A.ColumnInfo], caps: Sequence[i
             out.cols[c].data = _ptr(cs.cols[c])
             out.cols[c].offsets = 0
             out.cols[c].capacity = 0
-        else:
-            offs, data = cs.cols[c]
-            out.cols[c].data = _ptr(data)
-            out.cols[c].offsets = _ptr(offs)
-            cap = caps[c] if caps is not None and caps[c] is not None else (
-                data.numel() if hasattr(data, "numel") else data.size)
-            out.cols[c].capacity = int(cap)
+            continue
+        parts = cs.cols[c]
+        offs, data = parts[0], parts[-1]
+        out.cols[c].data = _ptr(data)
+        out.cols[c].offsets = _ptr(offs)
+        out.cols[c].offset_bytes = _itemsize(offs)
+        have = _numel(data)
+        cap = caps[c] if caps is not None and caps[c] is not None else have
+        out.cols[c].capacity = int(min(int(cap), have))
+        if ci.kind == A.COL_LIST_BYTES:  # (record offsets, element byte offsets, bytes)
+            eoffs = parts[1]
+            assert _itemsize(eoffs) == _itemsize(offs)
+            out.cols[c].elem_offsets = _ptr(eoffs)
+            out.cols[c].elem_capacity = max(0, _numel(eoffs) - 1)
     out.presence = _ptr(cs.presence)
     return out
 
 
-def alloc_host(infos: Sequence[A.ColumnInfo], n: int, var_caps: Sequence[int], npresence: int) -> ColumnSet:
+def alloc_host(infos: Sequence[A.ColumnInfo], n: int, var_caps: Sequence[int], npresence: int,
+               wide: bool = False, elem_caps: Sequence[int] = None) -> ColumnSet:
+    """Host columns. wide: 8-byte offsets. elem_caps[c]: element capacity of LIST_BYTES columns."""
+    odt = np.uint64 if wide else np.uint32
     cols: List[object] = []
     for c, ci in enumerate(infos):
         if ci.kind == A.COL_FIXED:
             cols.append(np.zeros(n, dtype=_NP_FIXED[ci.width]))
+        elif ci.kind == A.COL_LIST_BYTES:
+            ec = elem_caps[c] if elem_caps is not None else max(1, var_caps[c])
+            cols.append((np.zeros(n + 1, dtype=odt), np.zeros(ec + 1, dtype=odt),
+                         np.zeros(max(1, var_caps[c]), dtype=np.uint8)))
         else:
             dt = np.uint8 if ci.kind == A.COL_BYTES else _NP_FIXED[ci.width]
-            cols.append((np.zeros(n + 1, dtype=np.uint32), np.zeros(max(1, var_caps[c]), dtype=dt)))
+            cols.append((np.zeros(n + 1, dtype=odt), np.zeros(max(1, var_caps[c]), dtype=dt)))
     pres = np.zeros(n, dtype=np.uint64) if npresence else None
     return ColumnSet(cols, pres, n)
 
 
 def alloc_device(infos: Sequence[A.ColumnInfo], n: int, var_caps: Sequence[int], npresence: int,
-                 device, fill: int = None) -> ColumnSet:
+                 device, fill: int = None, wide: bool = False, elem_caps: Sequence[int] = None) -> ColumnSet:
+    """Device columns (torch). wide: 8-byte offsets (int64) instead of 4-byte (int32 storage of
+    the unsigned offsets)."""
     import torch
     tdt = {1: torch.uint8, 2: torch.int16, 4: torch.int32, 8: torch.int64}
+    odt = torch.int64 if wide else torch.int32
     mk = torch.empty if fill is None else (lambda *a, **k: torch.full(*a[:1], fill, **k))
     cols: List[object] = []
     for c, ci in enumerate(infos):
         if ci.kind == A.COL_FIXED:
             cols.append(mk((n,), dtype=tdt[ci.width], device=device))
+        elif ci.kind == A.COL_LIST_BYTES:
+            ec = elem_caps[c] if elem_caps is not None else max(1, var_caps[c])
+            cols.append((mk((n + 1,), dtype=odt, device=device), mk((ec + 1,), dtype=odt, device=device),
+                         mk((max(1, var_caps[c]),), dtype=torch.uint8, device=device)))
         else:
             dt = torch.uint8 if ci.kind == A.COL_BYTES else tdt[ci.width]
-            cols.append((mk((n + 1,), dtype=torch.int32, device=device),
+            cols.append((mk((n + 1,), dtype=odt, device=device),
                          mk((max(1, var_caps[c]),), dtype=dt, device=device)))
     pres = mk((n,), dtype=torch.int64, device=device) if npresence else None
     return ColumnSet(cols, pres, n)
@@ -81,5 +111,5 @@ def var_caps_of(cs: ColumnSet, infos: Sequence[A.ColumnInfo]) -> List[int]:
             caps.append(0)
         else:
             offs = cs.cols[c][0]
-            caps.append(int(offs[-1]) & 0xFFFFFFFF)
+            caps.append(int(offs[-1]) & (0xFFFFFFFF if _itemsize(offs) == 4 else (1 << 64) - 1))
     return caps

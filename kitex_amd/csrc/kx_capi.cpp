@@ -66,6 +66,10 @@ int ensure_ews(kx_ctx* c, size_t bytes, hipStream_t stream) {
   return KX_OK;
 }
 
+int offset_width(const kx_column& k) {
+  return k.offset_bytes == 0 || k.offset_bytes == 4 ? 4 : k.offset_bytes == 8 ? 8 : 0;
+}
+
 int to_launch_cols(const kx_schema* s, const kx_columns* out, KxLaunchCols* lc) {
   if (!out) return KX_ERR_INVALID_ARG;
   if (out->ncols != s->ncols) return KX_ERR_INVALID_ARG;
@@ -73,15 +77,21 @@ int to_launch_cols(const kx_schema* s, const kx_columns* out, KxLaunchCols* lc) 
   memset(lc, 0, sizeof *lc);
   for (uint32_t c = 0; c < s->ncols; c++) {
     const kx_column& k = out->cols[c];
-    if (s->info[c].kind == KX_COL_FIXED) {
+    const uint32_t kind = s->info[c].kind;
+    if (kind == KX_COL_FIXED) {
       if (!k.data) return KX_ERR_INVALID_ARG;
     } else {
-      if (!k.offsets) return KX_ERR_INVALID_ARG;
+      const int ow = offset_width(k);
+      if (!ow || !k.offsets) return KX_ERR_INVALID_ARG;
       if (!k.data && k.capacity) return KX_ERR_INVALID_ARG;
+      if (kind == KX_COL_LIST_BYTES && (!k.elem_offsets || (!k.data && k.capacity))) return KX_ERR_INVALID_ARG;
+      if (ow == 8) lc->owide |= 1u << c;
     }
     lc->data[c] = k.data;
     lc->offs[c] = k.offsets;
     lc->cap[c] = k.capacity;
+    lc->eoffs[c] = k.elem_offsets;
+    lc->ecap[c] = k.elem_capacity;
   }
   lc->presence = out->presence;
   return KX_OK;
@@ -197,7 +207,7 @@ int kx_thrift_decode_batch(kx_ctx* c, const kx_schema* s, const uint8_t* in, uin
   if (n == 0) {
     KX_HIP_CHECK(hipMemsetAsync(status, 0, sizeof(kx_status), st));
     for (uint32_t k = 0; k < s->ncols; k++)
-      if (lc.offs[k]) KX_HIP_CHECK(hipMemsetAsync(lc.offs[k], 0, 4, st));
+      if (lc.offs[k]) KX_HIP_CHECK(hipMemsetAsync(lc.offs[k], 0, ((lc.owide >> k) & 1) ? 8 : 4, st));
     return KX_OK;
   }
   KxProgram* dp = nullptr;
@@ -280,7 +290,7 @@ int kx_pb_decode_batch(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_
   if (n == 0) {
     KX_HIP_CHECK(hipMemsetAsync(status, 0, sizeof(kx_status), st));
     for (uint32_t k = 0; k < s->ncols; k++)
-      if (lc.offs[k]) KX_HIP_CHECK(hipMemsetAsync(lc.offs[k], 0, 4, st));
+      if (lc.offs[k]) KX_HIP_CHECK(hipMemsetAsync(lc.offs[k], 0, ((lc.owide >> k) & 1) ? 8 : 4, st));
     return KX_OK;
   }
   KxProgram* dp = nullptr;
@@ -347,7 +357,8 @@ int kx_host_decode_batch(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint6
   for (uint32_t k = 0; k < s->ncols; k++) {
     const kx_column_info& ci = s->info[k];
     if (ci.kind == KX_COL_FIXED) need += al(n * ci.width);
-    else need += al((n + 1) * 4) + al(out->cols[k].capacity * (ci.kind == KX_COL_LIST ? ci.width : 1));
+    else need += al((n + 1) * offset_width(out->cols[k])) +
+                 al(out->cols[k].capacity * (ci.kind == KX_COL_LIST ? ci.width : 1));
   }
   if (s->npres) need += al(n * 8);
   if (c->dstage_size < need) {
@@ -370,7 +381,8 @@ int kx_host_decode_batch(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint6
     if (ci.kind == KX_COL_FIXED) {
       dc.cols[k].data = p; p += al(n * ci.width);
     } else {
-      dc.cols[k].offsets = (uint32_t*)p; p += al((n + 1) * 4);
+      dc.cols[k].offset_bytes = (uint32_t)offset_width(out->cols[k]);
+      dc.cols[k].offsets = p; p += al((n + 1) * dc.cols[k].offset_bytes);
       dc.cols[k].data = p; p += al(out->cols[k].capacity * (ci.kind == KX_COL_LIST ? ci.width : 1));
       dc.cols[k].capacity = out->cols[k].capacity;
     }
@@ -387,7 +399,8 @@ int kx_host_decode_batch(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint6
     if (ci.kind == KX_COL_FIXED) {
       if (n) KX_HIP_CHECK(hipMemcpyAsync(out->cols[k].data, dc.cols[k].data, n * ci.width, hipMemcpyDeviceToHost, st));
     } else {
-      KX_HIP_CHECK(hipMemcpyAsync(out->cols[k].offsets, dc.cols[k].offsets, (n + 1) * 4, hipMemcpyDeviceToHost, st));
+      KX_HIP_CHECK(hipMemcpyAsync(out->cols[k].offsets, dc.cols[k].offsets, (n + 1) * dc.cols[k].offset_bytes,
+                                  hipMemcpyDeviceToHost, st));
     }
   }
   if (s->npres && n) KX_HIP_CHECK(hipMemcpyAsync(out->presence, dc.presence, n * 8, hipMemcpyDeviceToHost, st));

@@ -37,8 +37,13 @@ struct EncParams {
   bool pb;               // Kitex-Protobuf records (Batch framing) instead of Thrift binary
 };
 
+// record offsets are 4 or 8 bytes wide (kx_column.offset_bytes)
+__device__ __forceinline__ uint64_t off_at(const KxLaunchCols& C, int col, uint64_t r) {
+  return ((C.owide >> col) & 1) ? ((const uint64_t*)C.offs[col])[r] : (uint64_t)((const uint32_t*)C.offs[col])[r];
+}
+
 __device__ __forceinline__ uint64_t var_len(const KxLaunchCols& C, int col, uint64_t r) {
-  return (uint64_t)C.offs[col][r + 1] - (uint64_t)C.offs[col][r];
+  return off_at(C, col, r + 1) - off_at(C, col, r);
 }
 
 // BLength (struct_tpl.go:266-391)
@@ -160,12 +165,12 @@ __device__ void write_record(const KxProgram& P, const KxLaunchCols& C, uint64_t
       if (F.ttype == KX_T_BOOL) v = (v & 0xff) ? 1 : 0;
       put_be(s, v, F.width);
     } else if (F.kind == KXP_K_BYTES) {
-      uint64_t o = C.offs[F.col][r];
+      uint64_t o = off_at(C, F.col, r);
       uint32_t len = (uint32_t)var_len(C, F.col, r);
       put_be(s, len, 4);
       put_bytes(s, (const uint8_t*)C.data[F.col] + o, len);
     } else if (F.kind == KXP_K_LIST) {
-      uint64_t o = C.offs[F.col][r];
+      uint64_t o = off_at(C, F.col, r);
       uint32_t cnt = (uint32_t)var_len(C, F.col, r);
       s.put(F.elem, 1);
       put_be(s, cnt, 4);
@@ -251,7 +256,7 @@ __device__ void pb_write_record(const KxProgram& P, const KxLaunchCols& C, uint6
       if (n == 0 && !expl) continue;
       put_uvarint(s, tag);
       put_uvarint(s, n);
-      put_bytes(s, (const uint8_t*)C.data[F.col] + C.offs[F.col][r], (uint32_t)n);
+      put_bytes(s, (const uint8_t*)C.data[F.col] + off_at(C, F.col, r), (uint32_t)n);
     } else {
       const uint64_t v = pb_value(F, C, r);
       if (v == 0 && !expl) continue;

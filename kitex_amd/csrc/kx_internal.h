@@ -45,9 +45,15 @@ int kx_build_program(const kx_struct_desc* structs, uint32_t nstructs, kx_schema
 // device launchers (kx_decode.hip / kx_encode.hip)
 struct KxLaunchCols {
   void* data[KX_MAX_COLUMNS];
-  uint32_t* offs[KX_MAX_COLUMNS];
+  void* offs[KX_MAX_COLUMNS];    // record offsets (u32 or u64, see owide)
   uint64_t cap[KX_MAX_COLUMNS];
+  void* eoffs[KX_MAX_COLUMNS];   // LIST_BYTES: element byte offsets
+  uint64_t ecap[KX_MAX_COLUMNS];
+  uint32_t owide;                // bit c: column c has 8-byte offsets
+  uint32_t pad;
   uint64_t* presence;
+  uint64_t nrec;                 // records of the call (device-side guard of every column store)
+  unsigned long long* guard;     // where a refused out-of-range access is reported (kx_status.diag[2])
 };
 
 int kx_launch_decode(const KxProgram* dprog, const KxProgram& hprog, const uint8_t* in,

@@ -23,6 +23,19 @@ static inline void put32(uint8_t* p, uint32_t v) {
 }
 static inline void put64(uint8_t* p, uint64_t v) { put32(p, (uint32_t)(v >> 32)); put32(p + 4, (uint32_t)v); }
 
+/* kx_column offsets are 4 (default) or 8 bytes wide; a 4-byte column never wraps (SIZE_LIMIT) */
+static int off_w(const kx_column* c) { return c->offset_bytes == 8 ? 8 : 4; }
+static uint64_t off_get(const kx_column* c, uint64_t i) {
+  return off_w(c) == 8 ? ((const uint64_t*)c->offsets)[i] : ((const uint32_t*)c->offsets)[i];
+}
+static void off_set(const kx_column* c, uint64_t i, uint64_t v) {
+  if (off_w(c) == 8) ((uint64_t*)c->offsets)[i] = v;
+  else ((uint32_t*)c->offsets)[i] = (uint32_t)v;
+}
+static uint64_t arena_lim(const kx_column* c) {
+  return off_w(c) == 8 || c->capacity < 0xffffffffull ? c->capacity : 0xffffffffull;
+}
+
 /* typeToSize (codec_apache.go:182-189) */
 static int type_size(uint8_t t) {
   switch (t) {
@@ -401,8 +414,9 @@ static int emit_record_tail(dec_t* d, uint64_t* cursor, int* overflow) {
     if (vs < 0) continue;
     const kx_column* col = &d->out->cols[c];
     uint64_t n = d->vlen[c];
-    if (d->emit) col->offsets[d->rec] = (uint32_t)cursor[vs];
-    if (d->emit && cursor[vs] + n <= col->capacity) {
+    const uint64_t lim = arena_lim(col);
+    if (d->emit && cursor[vs] + n <= lim) {
+      off_set(col, d->rec, cursor[vs]);
       if (p->cols[c].kind == KX_COL_BYTES) {
         if (n) memcpy((uint8_t*)col->data + cursor[vs], d->vptr[c], n);
       } else {
@@ -414,7 +428,7 @@ static int emit_record_tail(dec_t* d, uint64_t* cursor, int* overflow) {
           memcpy(dst + i * w, &x, w);
         }
       }
-    } else if (cursor[vs] + n > col->capacity) {
+    } else if (cursor[vs] + n > lim) {
       *overflow = 1;
     }
     cursor[vs] += n;
@@ -486,7 +500,10 @@ static void finish_status(const plan_t* p, const kx_columns* out, kx_status* st,
   for (uint32_t c = 0; c < p->ncols; c++) {
     int vs = p->varidx[c];
     if (vs < 0) continue;
-    if (out->cols[c].offsets) out->cols[c].offsets[n_rec] = (uint32_t)cursor[vs];
+    if (out->cols[c].offsets) {
+      if (cursor[vs] <= arena_lim(&out->cols[c])) off_set(&out->cols[c], n_rec, cursor[vs]);
+      else overflow = 1;
+    }
     if (k < 8) st->var_total[k++] = cursor[vs];
   }
   if (overflow && st->code == 0) st->code = KX_ERR_SIZE_LIMIT;
@@ -595,7 +612,7 @@ typedef struct { const plan_t* p; const kx_columns* in; uint64_t rec; uint8_t* o
 
 static uint64_t col_len(const enc_t* e, int col) {
   const kx_column* c = &e->in->cols[col];
-  return (uint64_t)c->offsets[e->rec + 1] - (uint64_t)c->offsets[e->rec];
+  return off_get(c, e->rec + 1) - off_get(c, e->rec);
 }
 
 static uint64_t fixed_val(const enc_t* e, int col) {
@@ -642,7 +659,7 @@ static uint64_t write_struct(enc_t* e, int inst, uint64_t pres, uint8_t* b) {
           uint64_t n = col_len(e, m->col);
           if (b) {
             const kx_column* c = &e->in->cols[m->col];
-            kxo_write_string(b + off, (const uint8_t*)c->data + c->offsets[e->rec], (uint32_t)n);
+            kxo_write_string(b + off, (const uint8_t*)c->data + off_get(c, e->rec), (uint32_t)n);
           }
           off += 4 + n;
           break;
@@ -653,7 +670,7 @@ static uint64_t write_struct(enc_t* e, int inst, uint64_t pres, uint8_t* b) {
           if (b) {
             const kx_column* c = &e->in->cols[m->col];
             kxo_write_list_begin(b + off, f->elem_ttype, (int32_t)n);
-            const uint8_t* s = (const uint8_t*)c->data + (uint64_t)c->offsets[e->rec] * w;
+            const uint8_t* s = (const uint8_t*)c->data + off_get(c, e->rec) * w;
             uint8_t* d = b + off + 5;
             for (uint64_t k = 0; k < n; k++) {
               uint64_t v = 0;
@@ -995,7 +1012,7 @@ static uint64_t pb_write_record(const plan_t* p, const kx_columns* in, uint64_t 
     uint64_t tag = ((uint64_t)(uint16_t)f->id << 3) | (uint64_t)wt;
     if (wt == 2) {
       const kx_column* c = &in->cols[m->col];
-      uint64_t n = (uint64_t)c->offsets[rec + 1] - c->offsets[rec];
+      uint64_t n = off_get(c, rec + 1) - off_get(c, rec);
       if (n == 0 && !explicit_presence) continue;
       size_t u = kxo_put_uvarint(tmp, tag);
       if (b) memcpy(b + off, tmp, u);
@@ -1003,7 +1020,7 @@ static uint64_t pb_write_record(const plan_t* p, const kx_columns* in, uint64_t 
       u = kxo_put_uvarint(tmp, n);
       if (b) memcpy(b + off, tmp, u);
       off += u;
-      if (b && n) memcpy(b + off, (const uint8_t*)c->data + c->offsets[rec], n);
+      if (b && n) memcpy(b + off, (const uint8_t*)c->data + off_get(c, rec), n);
       off += n;
       continue;
     }

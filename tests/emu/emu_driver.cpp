@@ -18,6 +18,9 @@ extern "C" int emu_decode(const kx_struct_desc* structs, uint32_t nstructs, cons
       lc.data[c] = out->cols[c].data;
       lc.offs[c] = out->cols[c].offsets;
       lc.cap[c] = out->cols[c].capacity;
+      lc.eoffs[c] = out->cols[c].elem_offsets;
+      lc.ecap[c] = out->cols[c].elem_capacity;
+      if (out->cols[c].offset_bytes == 8) lc.owide |= 1u << c;
     }
     lc.presence = out->presence;
   }
@@ -38,6 +41,7 @@ extern "C" int emu_decode(const kx_struct_desc* structs, uint32_t nstructs, cons
     memset(ws + 8, 0xff, 8);
     epoch = 1;
   }
+  status->diag[0] = status->diag[1] = 0;
   if (skip)
     rc = kx_launch_skip(in, in_len, n, skip_out, status, ws, ws_cap, epoch, nullptr);
   else

@@ -26,6 +26,7 @@ struct Wave {
   int gen = 0, arrived = 0, live = 0;
   uint64_t slot[64], snap[64];
 };
+static_assert(sizeof(uint64_t) == 8, "");
 
 struct WG {
   std::vector<Fiber> f;
@@ -33,7 +34,7 @@ struct WG {
   ucontext_t sched;
   Wave wave[16];
   int bar_gen = 0, bar_arrived = 0, bar_live = 0;
-  unsigned block = 0;
+  unsigned block = 0, grid = 0;
   void (*tramp)(void*) = nullptr;
   void* arg = nullptr;
 };
@@ -48,10 +49,11 @@ void fiber_main(int idx) {
   wg->bar_live--;
 }
 
-void run_wg(unsigned b, unsigned block, void (*tramp)(void*), void* arg) {
+void run_wg(unsigned b, unsigned grid, unsigned block, void (*tramp)(void*), void* arg) {
   WG wg;
   wg.nthreads = (int)block;
   wg.block = b;
+  wg.grid = grid;
   wg.tramp = tramp;
   wg.arg = arg;
   wg.f.resize(block);
@@ -85,6 +87,12 @@ void run_wg(unsigned b, unsigned block, void (*tramp)(void*), void* arg) {
 
 EmuTid emu_thread_idx() { return EmuTid{(unsigned)g_wg->cur, 0, 0}; }
 EmuTid emu_block_idx() { return EmuTid{g_wg->block, 0, 0}; }
+EmuTid emu_grid_dim() { return EmuTid{g_wg->grid, 1, 1}; }
+int emu_threads() {
+  const char* e = getenv("KX_EMU_THREADS");
+  int nt = e ? atoi(e) : 8;
+  return nt < 1 ? 1 : nt;
+}
 int emu_lane() { return g_wg->cur & 63; }
 
 void emu_yield() {
@@ -127,9 +135,7 @@ uint64_t emu_clock_ns() {
 }
 
 void emu_launch(unsigned grid, unsigned block, void (*tramp)(void*), void* arg) {
-  const char* e = getenv("KX_EMU_THREADS");
-  int nt = e ? atoi(e) : 8;
-  if (nt < 1) nt = 1;
+  const int nt = emu_threads();
   std::atomic<unsigned> next{0};
   std::vector<std::thread> th;
   for (int i = 0; i < nt; i++)
@@ -137,7 +143,7 @@ void emu_launch(unsigned grid, unsigned block, void (*tramp)(void*), void* arg) 
       for (;;) {
         unsigned b = next.fetch_add(1);
         if (b >= grid) break;
-        run_wg(b, block, tramp, arg);
+        run_wg(b, grid, block, tramp, arg);
       }
     });
   for (auto& t : th) t.join();

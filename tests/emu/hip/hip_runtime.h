@@ -42,6 +42,8 @@ struct EmuTid {
 };
 EmuTid emu_thread_idx();
 EmuTid emu_block_idx();
+EmuTid emu_grid_dim();
+int emu_threads();
 int emu_lane();
 void emu_yield();
 void emu_sync_wg();
@@ -51,6 +53,7 @@ uint64_t emu_clock_ns();
 
 #define threadIdx (emu_thread_idx())
 #define blockIdx (emu_block_idx())
+#define gridDim (emu_grid_dim())
 #define blockDim (EmuTid{256, 1, 1})
 inline void __syncthreads() { emu_sync_wg(); }
 
@@ -168,6 +171,13 @@ inline hipError_t hipMemsetAsync(void* p, int v, size_t n, hipStream_t) {
   return hipSuccess;
 }
 #define HIP_SYMBOL(x) (&(x))
+// the persistent decode grid is sized from these: one workgroup per emulator thread, all co-resident
+enum hipDeviceAttribute_t { hipDeviceAttributeMultiprocessorCount = 0 };
+// (one "device" per emulator thread count: the kernel caches its grid size per device)
+inline hipError_t hipGetDevice(int* d) { *d = emu_threads() & 63; return hipSuccess; }
+inline hipError_t hipDeviceGetAttribute(int* v, hipDeviceAttribute_t, int) { *v = emu_threads(); return hipSuccess; }
+template <typename F>
+inline hipError_t hipOccupancyMaxActiveBlocksPerMultiprocessor(int* n, F, int, size_t) { *n = 1; return hipSuccess; }
 inline hipError_t hipMemcpyFromSymbol(void* dst, const void* sym, size_t n) {
   memcpy(dst, sym, n);
   return hipSuccess;

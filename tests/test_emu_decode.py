@@ -71,9 +71,22 @@ def test_emu_skip(edec, oracle):
     DC.case_skip(lambda wire, n: emu.skip(wire, n)[1], oracle)
 
 
-def test_emu_deep_lookback(oracle):
-    """many workgroups in flight: 64 concurrent workgroups over ~1500 tiles"""
-    DC.case_concat(EmuDecoder(oracle, threads=64), oracle, "r2", 75000)
+@pytest.mark.parametrize("name,n", [("r2", 75000), ("r3", 20000), ("r1", 60000)])
+def test_emu_deep_lookback(oracle, name, n):
+    """64 co-resident workgroups, one super-tile each: look-back windows that reach past their
+    first 16 predecessors before finding an inclusive prefix"""
+    DC.case_concat(EmuDecoder(oracle, threads=64), oracle, name, n)
+
+
+def test_emu_deep_lookback_pb(oracle):
+    PC.case_pb_concat(EmuDecoder(oracle, threads=64), oracle, 25000)
+
+
+@pytest.mark.parametrize("name,n", [("r2", 120000), ("r3", 30000)])
+def test_emu_persistent_loop(oracle, name, n):
+    """3 workgroups, each looping over many super-tiles (the persistent grid of the GPU)"""
+    DC.case_concat(EmuDecoder(oracle, threads=3), oracle, name, n)
+    DC.case_offsets(EmuDecoder(oracle, threads=3), oracle, name, n // 4)
 
 
 # ---- Kitex-Protobuf (same kernels, M_PB walker) ----

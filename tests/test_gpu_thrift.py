@@ -191,6 +191,46 @@ def test_decode_beyond_2gib(torch, dev):
     torch.cuda.empty_cache()
 
 
+def test_decode_arena_beyond_4gib(torch, dev):
+    """one string arena past 2^32 bytes: 2M records with a 2100-byte string (4.4 GB arena), encoded
+    on the GPU from 8-byte-offset columns and decoded in both modes. 8-byte offsets give the source
+    columns back; 4-byte offsets fail with SIZE_LIMIT instead of wrapping."""
+    from kitex_amd.codec import ThriftCodec, read_status, status_tensor
+    from kitex_amd.columns import alloc_device
+    sch = S.Schema(S.Struct("Big", [S.Field(1, A.T_I64), S.Field(2, A.T_STRING), S.Field(3, A.T_STRING)]))
+    cdc = ThriftCodec(sch)
+    n, L = 1 << 21, 2100
+    ids = torch.arange(n, dtype=torch.int64, device=dev) * 7 - 5
+    big_off = torch.arange(n + 1, dtype=torch.int64, device=dev) * L
+    big = (torch.arange(n * L, dtype=torch.int64, device=dev) % 251).to(torch.uint8)
+    sm_len = (torch.arange(n, device=dev) % 5).to(torch.int64)
+    sm_off = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    sm_off[1:] = torch.cumsum(sm_len, 0)
+    small = (torch.arange(int(sm_off[-1]), device=dev) % 26 + 97).to(torch.uint8)
+    src = synth.ColumnSet([ids, (big_off, big), (sm_off, small)], None, n)
+    wire, offs = cdc.Marshal(src)
+    assert big.numel() > (1 << 32) and wire.numel() > (1 << 32)
+    infos = cdc.dschema.infos
+    caps = [0, n * L, int(sm_off[-1])]
+    for o in (None, offs):
+        out = alloc_device(infos, n, caps, 0, dev, wide=True)
+        st = status_tensor(dev)
+        cdc.Unmarshal(wire, n, offsets=o, out=out, var_caps=caps, raise_on_error=False, status=st)
+        s = read_status(st)
+        assert s.code == 0 and s.n_records == n and s.var_total[0] == n * L
+        assert torch.equal(out.cols[0], ids)
+        assert torch.equal(out.cols[1][0], big_off) and torch.equal(out.cols[2][0], sm_off)
+        assert torch.equal(out.cols[1][1], big) and torch.equal(out.cols[2][1][:small.numel()], small)
+        del out
+        narrow = alloc_device(infos, n, caps, 0, dev)
+        st = status_tensor(dev)
+        cdc.Unmarshal(wire, n, offsets=o, out=narrow, var_caps=caps, raise_on_error=False, status=st)
+        assert read_status(st).code == A.ERR_SIZE_LIMIT
+        del narrow
+    del wire, offs, src, big
+    torch.cuda.empty_cache()
+
+
 # ---------------------------------------------------------------------------------------------
 # host-memory entry point (kx_host_decode_batch: H2D -> decode -> D2H)
 # ---------------------------------------------------------------------------------------------
