@@ -11,7 +11,8 @@ import os
 from . import _abi as A
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libkxcodec.so")
+# KXCODEC_LIB: an alternative in-tree build of the same library (kernel-tuning experiments)
+LIB_PATH = os.environ.get("KXCODEC_LIB") or os.path.join(HERE, "lib", "libkxcodec.so")
 
 _lib = None
 

@@ -8,6 +8,7 @@ import glob
 import os
 import subprocess
 import sys
+from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
@@ -29,26 +30,58 @@ def _stale() -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force: bool = False, verbose: bool = False, extra=()) -> str:
-    if not force and not _stale():
-        return LIB
-    os.makedirs(LIBDIR, exist_ok=True)
-    objs = []
+DECODE_PARTS = 6   # kx_decode.hip is compiled once per part (-DKX_DEC_PART=k): its kernels in parallel
+
+
+def _units(libdir=LIBDIR):
+    """(source, object, extra flags) per translation unit."""
+    out = []
     for src in sources():
-        obj = os.path.join(LIBDIR, os.path.basename(src) + ".o")
+        base = os.path.join(libdir, os.path.basename(src))
+        if os.path.basename(src) == "kx_decode.hip":
+            out += [(src, f"{base}.{k}.o", [f"-DKX_DEC_PART={k}"]) for k in range(DECODE_PARTS)]
+        else:
+            out.append((src, base + ".o", []))
+    return out
+
+
+def build(force: bool = False, verbose: bool = False, extra=(), variant: str = "") -> str:
+    """variant: build into lib/<variant>/ (with `extra` flags) for kernel-tuning experiments."""
+    libdir = os.path.join(LIBDIR, variant) if variant else LIBDIR
+    lib = os.path.join(libdir, "libkxcodec.so")
+    if not force and not variant and not _stale():
+        return LIB
+    os.makedirs(libdir, exist_ok=True)
+    hdrs = glob.glob(os.path.join(CSRC, "*.h")) + [os.path.join(HERE, "..", "include", "kxcodec.h")]
+    newest_hdr = max(os.path.getmtime(h) for h in hdrs)
+    jobs = []
+    for src, obj, flags in _units(libdir):
+        fresh = (not force and not extra and not variant and os.path.exists(obj)
+                 and os.path.getmtime(obj) > max(os.path.getmtime(src), newest_hdr))
+        if fresh:
+            continue
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-Wall",
-               "-Wno-unused-function", "-munsafe-fp-atomics", "-c", src, "-o", obj, *extra]
+               "-Wno-unused-function", "-munsafe-fp-atomics", *flags, "-c", src, "-o", obj, *extra]
+        jobs.append(cmd)
+
+    def run(cmd):
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
-        subprocess.run(cmd, check=True)
-        objs.append(obj)
-    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB + ".tmp", *objs]
+        return subprocess.run(cmd).returncode
+
+    workers = max(1, min(len(jobs), len(os.sched_getaffinity(0)), 8))
+    with ThreadPoolExecutor(max_workers=workers) as ex:
+        rcs = list(ex.map(run, jobs))
+    if any(rcs):
+        raise RuntimeError("hipcc failed")
+    objs = [obj for _, obj, _ in _units(libdir)]
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib + ".tmp", *objs]
     subprocess.run(cmd, check=True)
-    os.replace(LIB + ".tmp", LIB)
-    for o in objs:
-        os.remove(o)
-    return LIB
+    os.replace(lib + ".tmp", lib)
+    return lib
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True))
+    args = [a for a in sys.argv[1:] if a != "--force"]
+    # python -m kitex_amd.build [--force] [VARIANT -DFLAG ...]
+    print(build(force="--force" in sys.argv, verbose=True, variant=args[0] if args else "", extra=tuple(args[1:])))

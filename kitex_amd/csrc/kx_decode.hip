@@ -5,25 +5,26 @@
 // message (pkg/remote/codec/thrift/codec_fast.go:60-82) or as the element loop of a list<Struct>;
 // unknown / mistyped fields go through the skip decoder (codec_apache.go:191-293).
 //
-// Design: ONE persistent kernel; every input byte is read from HBM once.
-//   A workgroup of 8 waves owns a super-tile (ST) of 8 tiles x 8 KiB at a time (persistent grid,
-//   super-tiles dealt round-robin). Each wave pulls its tile (+ a 512-byte halo for the record
-//   straddling its end) into LDS by LDS-DMA (global_load_lds_dwordx4) and walks it speculatively:
-//   lane l owns the 128-byte segment l, starts at the first canonical record signature in it and
-//   walks records (schema-aware FastRead lengths) until it leaves the segment; lanes repair each
-//   other with wave shuffles until the chain is consistent. The 8 tile aggregates are chained in
-//   LDS into the ST aggregate (entry, exit, records, arena bytes, first error), which is published
-//   as epoch-tagged words; a decoupled look-back over the preceding STs (with a chain-consistency
-//   check at every boundary: a tile's speculative entry must be where the chain below exits) gives
-//   the ST's true entry and its record / arena bases. A tile whose speculation was wrong is re-walked
-//   from its true entry out of LDS. Then every wave emits its tile from LDS (lane = segment):
-//   fixed-width fields are stored as parsed, strings / lists are copied with 16-byte stores.
+// Design: three stream-ordered kernels, no wave ever waits for another tile's work.
+//   1. index pass — one WAVE per 8 KiB tile. The tile (+ a 512-byte halo for the record straddling
+//      its end) is pulled into the wave's LDS window by LDS-DMA (global_load_lds_dwordx4). Lane l owns
+//      the 128-byte segment l: it finds the first canonical record signature in it and walks records
+//      (schema-aware FastRead lengths) until it leaves the segment; lanes repair each other with wave
+//      shuffles until the chain is consistent. The tile writes its record starts (u16 list) and an
+//      aggregate (speculative entry, exit, count, arena bytes, first error) as epoch-tagged words.
+//      The last wave to finish a group of 64 tiles validates the chain between them (re-walking a
+//      tile from its true entry where the speculation was wrong) and scans the group.
+//   2. chain pass — one workgroup resolves the chain over the groups from offset 0 and writes every
+//      group's record / arena base and the number of records to emit (errors, EOF, n).
+//   3. emit pass — one wave per tile again (the tile is re-read, mostly from the Infinity Cache when
+//      it fits), lane = record: fixed-width fields are stored as parsed (lanes = consecutive records,
+//      coalesced), strings / lists are copied from LDS with 16-byte stores at scanned arena offsets.
 //   Known-offsets mode (fastUnmarshal with dataLen): a tile is up to 64 records, lane = record; the
-//   look-back carries only arena bytes (none at all when the schema has no var columns).
+//   index pass only measures arena bytes (skipped entirely when the schema has no var columns).
 // Canonical records (the encoder's layout) take a straight-line step plan compiled from the schema;
 // anything else takes the generic field loop. Records or strings reaching past the LDS window are
 // read from global memory (same code, other source).
-// No MFMA anywhere: this is byte movement, bounded by HBM bandwidth.
+// No MFMA anywhere: this is byte movement, bounded by HBM bandwidth and memory latency.
 #include <hip/hip_runtime.h>
 #include <stdlib.h>
 
@@ -35,25 +36,35 @@
 
 namespace {
 
-constexpr int WGW = 8;                   // waves per workgroup = tiles per super-tile
-constexpr int NT = WGW * 64;
+constexpr int NT = 256;                  // threads per workgroup (4 independent waves)
+constexpr int WAVES = NT / 64;
 constexpr int SEG = 128;                 // bytes per lane segment
 constexpr int TILE = 64 * SEG;           // 8 KiB of input per wave
-constexpr int HALO = 256;                // the record straddling the tile end is read from LDS up to here
+constexpr int HALO = 512;                // the record straddling the tile end is read from LDS up to here
 constexpr int WINB = TILE + HALO + 16;   // LDS window bytes (+16 for the aligned-down start)
 constexpr int WINW = WINB / 4 + 4;       // window dwords (+ pad for the last aligned read pair)
 constexpr int WIN_LOADS = (WINB / 16 + 63) / 64;
+constexpr int GT = 64;                   // tiles per group (one group-scan lane per tile)
+constexpr int CT = 256, CW = CT / 64;    // chain pass: one workgroup, lane = group
 
 constexpr uint64_t V48 = (1ull << 48) - 1;
 constexpr uint64_t X_ERR = V48;          // chain terminated by a decode error
-constexpr uint64_t X_NONE = V48 - 2;     // no record start (candidate / entry / exit unknown)
+constexpr uint64_t X_DONE = V48 - 1;     // chain already ended (no records to emit)
+constexpr uint64_t X_NONE = V48 - 2;     // no candidate in this tile / lane
+constexpr uint64_t X_BAD = V48 - 3;      // group whose speculative tile chain disagrees (chain pass repairs)
 
-// super-tile descriptor words (structure of arrays over STs, epoch-tagged):
-//   A = the ST's speculative aggregate, P = the inclusive prefix through the ST
-enum { A_S = 0, A_X, A_C, A_EC, A_EP, A_V, P_X = A_V + KXP_NV_MAX, P_C, P_EC, P_EP, P_V,
-       S_NF = P_V + KXP_NV_MAX };
+// tile words (structure of arrays over tiles, epoch-tagged): aggregate of the index pass, then the
+// exclusive prefix inside the group written by the group scan
+enum { T_ENT = 0, T_EXIT, T_CNT, T_ERRC, T_ERRP, T_VAR, T_PCNT = T_VAR + KXP_NV_MAX, T_PVAR,
+       T_NF = T_PVAR + KXP_NV_MAX };
+// group words: group aggregate, then the global exclusive base written by the chain pass
+enum { G_ENT = 0, G_EXIT, G_CNT, G_ERRC, G_ERRP, G_VAR, G_BCNT = G_VAR + KXP_NV_MAX, G_BVAR,
+       G_NF = G_BVAR + KXP_NV_MAX };
 
 enum Mode { M_THRIFT = 0, M_SKIP = 1, M_PB = 2 };
+
+// diagnostics (KX_DIAG & 64): shader-clock cycles per index-pass phase, summed over tiles (lane 0)
+__device__ unsigned long long g_phase[8];
 
 struct DecParams {
   const uint8_t* in;
@@ -65,18 +76,19 @@ struct DecParams {
   uint8_t* rstat;
   kx_status* status;
   uint64_t* skip_out;        // M_SKIP: record start offsets
-  uint64_t* sdesc;           // super-tile words
+  uint64_t* tdesc;           // tile words
+  uint64_t* gdesc;           // group words
+  uint16_t* starts;          // concatenated mode: record starts per tile (slotcap slots each)
   unsigned long long* errkey;  // offsets mode: min((record << 8) | code)
-  uint32_t* overflow;        // an arena capacity (or the 4-byte offset range) was exceeded
-  uint32_t* abort;           // a look-back wait timed out: every other wait gives up at once
-  unsigned long long* ticket;  // super-tiles handed out so far (claimed in order: deadlock-free look-back)
-  unsigned long long* progress;  // inclusive prefixes published so far (the look-back watchdog's clock)
-  uint64_t ntiles, nst;
+  uint32_t* overflow;        // an arena capacity was exceeded
+  uint64_t* nstop;           // records to emit (chain pass)
+  uint64_t ntiles, ngroups, slotcap;
   uint64_t epoch;            // 16-bit call epoch (never 0)
   uint32_t krec;             // offsets mode: records per tile (<= 64)
-  int direct;                // offsets mode without var columns: no look-back
+  int direct;                // offsets mode without var columns: emit pass only
   int nolds;                 // diagnostics (KX_NOLDS=1): read every byte from global memory
-  int diag;
+  int diag;                  // diagnostics (KX_DIAG bits, timing experiments only; output is wrong):
+                             // 1 no walk, 2 no group arrival, 4 no tile words, 256 index pass only
 };
 
 // Kernels read their parameter block in place from the kernarg segment: indexing a by-value
@@ -316,22 +328,24 @@ __device__ __forceinline__ void vset(VarState<NV>& v, uint32_t slot, uint64_t p,
     if ((uint32_t)i == slot) { v.pos[i] = p; v.len[i] = l; }
 }
 
-// refused out-of-range device accesses (never expected; a bit per site lands in kx_status.diag[2])
-enum { G_ROUNDS = 1, G_LB_WAIT = 2, G_LB_SLOW = 4, G_NFIX = 8, G_COMBINE = 16, G_COLUMN = 32, G_OFFSET = 64,
-       G_ROWS = 128, G_WORD = 256 };
-
-__device__ __forceinline__ void store_col_(void* base, uint32_t width, uint64_t rec, uint64_t v);
-// store value v of record rec into fixed column col
-__device__ __forceinline__ void store_col(const KAS KxLaunchCols& cols, int col, uint32_t width, uint64_t rec,
+// record offsets: 4 or 8 bytes per entry (kx_column.offset_bytes). A 4-byte column never wraps: an
+// arena position past 2^32 - 1 counts as an overflow (KX_ERR_SIZE_LIMIT), like one past the capacity.
+__device__ __forceinline__ void put_off(const KAS KxLaunchCols& cols, uint32_t c, uint64_t r, uint64_t v) {
+  if ((cols.owide >> c) & 1) ((GLB uint64_t*)cols.offs[c])[r] = v;
+  else ((GLB uint32_t*)cols.offs[c])[r] = (uint32_t)v;
+}
+// the arena limit of column c in arena units: its capacity, and the 4-byte offset range
+__device__ __forceinline__ uint64_t arena_lim(const KAS KxLaunchCols& cols, uint32_t c) {
+  return ((cols.owide >> c) & 1) ? cols.cap[c] : kmin64(cols.cap[c], 0xffffffffull);
+}
+// offsets[i] = v for the record that ends the decoded prefix (n, or the failing record)
+__device__ __forceinline__ void put_total(const KAS KxLaunchCols& cols, uint32_t* overflow, uint32_t c, uint64_t i,
                                           uint64_t v) {
-  if (rec >= cols.nrec || col < 0 || col >= KX_MAX_COLUMNS) {
-    atomicOr(cols.guard, (unsigned long long)G_COLUMN);
-    return;
-  }
-  store_col_(cols.data[col], width, rec, v);
+  if (v <= arena_lim(cols, c)) put_off(cols, c, i, v);
+  else atomicOr(overflow, 1u);
 }
 
-__device__ __forceinline__ void store_col_(void* base, uint32_t width, uint64_t rec, uint64_t v) {
+__device__ __forceinline__ void store_col(void* base, uint32_t width, uint64_t rec, uint64_t v) {
   switch (width) {
     case 1: ((GLB uint8_t*)base)[rec] = (uint8_t)v; break;
     case 2: ((GLB uint16_t*)base)[rec] = (uint16_t)v; break;
@@ -394,10 +408,10 @@ __device__ __forceinline__ bool canon_record(const Src& w, const KAS KxLaunchCol
       if (m > 3) ok &= (f3.w0 & 0xffffffu) == (s3.hdr & 0xffffffu);
       if (!ok) return false;
       if (emit) {
-        store_col(cols, st.col, st.width, rec, fixed_after_header(f0, st.hdr & 0xff));
-        if (m > 1) store_col(cols, s1.col, s1.width, rec, fixed_after_header(f1, s1.hdr & 0xff));
-        if (m > 2) store_col(cols, s2.col, s2.width, rec, fixed_after_header(f2, s2.hdr & 0xff));
-        if (m > 3) store_col(cols, s3.col, s3.width, rec, fixed_after_header(f3, s3.hdr & 0xff));
+        store_col(cols.data[st.col], st.width, rec, fixed_after_header(f0, st.hdr & 0xff));
+        if (m > 1) store_col(cols.data[s1.col], s1.width, rec, fixed_after_header(f1, s1.hdr & 0xff));
+        if (m > 2) store_col(cols.data[s2.col], s2.width, rec, fixed_after_header(f2, s2.hdr & 0xff));
+        if (m > 3) store_col(cols.data[s3.col], s3.width, rec, fixed_after_header(f3, s3.hdr & 0xff));
       }
       pos += len;
       k += m;
@@ -482,7 +496,7 @@ __device__ __forceinline__ int generic_record(const Src& w, const KAS KxProgram*
     if (F.kind == KXP_K_FIXED) {
       const uint32_t wd = F.width;
       if (limit - vp < wd) return KX_ERR_EOF;
-      if (emit) store_col(cols, F.col, wd, rec, fixed_after_header(fx, t));
+      if (emit) store_col(cols.data[F.col], wd, rec, fixed_after_header(fx, t));
       pos = vp + wd;
     } else if (F.kind == KXP_K_BYTES) {                      // ReadString (copies)
       if (limit - vp < 4) return KX_ERR_EOF;
@@ -520,7 +534,7 @@ __device__ __forceinline__ int generic_record(const Src& w, const KAS KxProgram*
     // fields never seen (or reset by a repeated struct field) take their default
     for (uint32_t c = 0; c < P->ncols; c++) {
       const KxpCol K = ld_col(P, c);
-      if (K.kind == KXP_K_FIXED && !((seen >> K.field) & 1)) store_col(cols, (int)c, K.width, rec, (uint64_t)K.defv);
+      if (K.kind == KXP_K_FIXED && !((seen >> K.field) & 1)) store_col(cols.data[c], K.width, rec, (uint64_t)K.defv);
     }
   }
   pres_out = pres;
@@ -531,7 +545,7 @@ __device__ __forceinline__ int generic_record(const Src& w, const KAS KxProgram*
 __device__ __forceinline__ void emit_defaults(const KAS KxProgram* P, const KAS KxLaunchCols& cols, uint64_t rec) {
   for (uint32_t c = 0; c < P->ncols; c++) {
     const KxpCol K = ld_col(P, c);
-    if (K.kind == KXP_K_FIXED) store_col(cols, (int)c, K.width, rec, (uint64_t)K.defv);
+    if (K.kind == KXP_K_FIXED) store_col(cols.data[c], K.width, rec, (uint64_t)K.defv);
   }
 }
 
@@ -587,7 +601,7 @@ __device__ __forceinline__ Fetch fetch_skip(const Fetch& f, uint32_t u) {
 }
 
 // utf8.Valid (what protobuf-go enforces on proto3 `string` fields), byte by byte
-__device__ __forceinline__ bool pb_utf8_slow(const Src w, uint64_t p, uint64_t n) {
+__device__ __noinline__ bool pb_utf8_slow(const Src w, uint64_t p, uint64_t n) {
   uint64_t i = 0;
   while (i < n) {
     const uint32_t c = ld1(w, p + i);
@@ -687,10 +701,10 @@ __device__ __forceinline__ int pb_body(const Src& w, const KAS KxProgram* P, con
       if ((rc = pb_varint_f(fv, rem, v, u))) return rc;
       pos += u;
       if (F.ttype == KX_T_BOOL) v = v != 0;
-      if (emit) store_col(cols, F.col, F.width, rec, v);  // int32: low 32 bits
+      if (emit) store_col(cols.data[F.col], F.width, rec, v);  // int32: low 32 bits
     } else if (wt == 1) {
       if (rem < 8) return KX_ERR_EOF;
-      if (emit) store_col(cols, F.col, F.width, rec, (uint64_t)fv.w0 | ((uint64_t)fv.w1 << 32));
+      if (emit) store_col(cols.data[F.col], F.width, rec, (uint64_t)fv.w0 | ((uint64_t)fv.w1 << 32));
       pos += 8;
     } else {
       uint64_t l;
@@ -708,7 +722,7 @@ __device__ __forceinline__ int pb_body(const Src& w, const KAS KxProgram* P, con
     // fields never seen keep their (proto3 zero / schema) default
     for (uint32_t c = 0; c < P->ncols; c++) {
       const KxpCol K = ld_col(P, c);
-      if (K.kind == KXP_K_FIXED && !((seen >> K.field) & 1)) store_col(cols, (int)c, K.width, rec, (uint64_t)K.defv);
+      if (K.kind == KXP_K_FIXED && !((seen >> K.field) & 1)) store_col(cols.data[c], K.width, rec, (uint64_t)K.defv);
     }
   }
   pres_out = pres;
@@ -718,7 +732,7 @@ __device__ __forceinline__ int pb_body(const Src& w, const KAS KxProgram* P, con
 // ---------------------------------------------------------------------------------------------
 // variable-length payload copy (strings: raw bytes; lists: big-endian elements -> host order)
 // ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ void copy_var_slow(const Src w, KxpCol K, uint64_t src, uint32_t n, uint8_t* dst_) {
+__device__ __noinline__ void copy_var_slow(const Src w, KxpCol K, uint64_t src, uint32_t n, uint8_t* dst_) {
   GLB uint8_t* dst = (GLB uint8_t*)dst_;
   if (K.kind == KXP_K_BYTES) {
     for (uint32_t i = 0; i < n; i++) dst[i] = (uint8_t)ld1(w, src + i);
@@ -858,6 +872,30 @@ __device__ __forceinline__ void put_word(uint64_t* base, uint64_t nitems, int f,
   astore64(base + (uint64_t)f * nitems + i, (ep << 48) | (v & V48));
 }
 
+// Polls `nw` words of item i (fields f0.. of `fields`), lanes with !act skip. Returns false on timeout.
+template <int NW>
+__device__ __forceinline__ bool get_words(const uint64_t* base, uint64_t nitems, const int* fields, int nw, uint64_t i,
+                                          uint64_t ep, bool act, uint64_t* out) {
+  const uint64_t t0 = now_ns();
+  int backoff = 1;
+  for (;;) {
+    bool ok = true;
+    if (act) {
+#pragma unroll
+      for (int k = 0; k < NW; k++) {
+        if (k >= nw) break;
+        const uint64_t x = aload64(base + (uint64_t)fields[k] * nitems + i);
+        ok &= (x >> 48) == ep;
+        out[k] = x & V48;
+      }
+    }
+    if (!__ballot(!ok)) return true;
+    if (now_ns() - t0 > 2000000000ull) return false;
+    for (int k = 0; k < backoff; k++) __builtin_amdgcn_s_sleep(1);
+    backoff = backoff < 16 ? backoff * 2 : 16;
+  }
+}
+
 // 0x80 in the lowest byte of v that is 0x00 (bytes above it may be flagged spuriously)
 __device__ __forceinline__ uint32_t low_zero_byte(uint32_t v) { return (v - 0x01010101u) & ~v & 0x80808080u; }
 
@@ -984,39 +1022,29 @@ __device__ __forceinline__ uint64_t pb_scan_segment(const Src& w, uint64_t seg_l
 // ---------------------------------------------------------------------------------------------
 // the decode pipeline
 // ---------------------------------------------------------------------------------------------
-// HBM -> LDS window for input position `lo` (all DMA chunks in flight together)
-// the window descriptor for input position `lo` (what load_window DMA'd there; cheap to recompute)
-// (whole 16-byte chunks inside the input only: the last < 16 bytes of the input are read from HBM)
-__device__ __forceinline__ int32_t window_len(KParams& dp, uint64_t wbase) {
-  const uint64_t end = (uint64_t)dp.in + dp.in_len;
-  return dp.nolds || end < wbase + 16 ? 0 : (int32_t)min((uint64_t)WINB, (end - wbase) & ~15ull);
-}
-
-__device__ __forceinline__ Src window_src(KParams& dp, LDS uint32_t* win, uint64_t lo, bool thrift) {
+// HBM -> LDS window for input position `lo`: buffer LDS-DMA, every chunk in flight together. Only
+// whole 16-byte chunks inside the input are loaded (the input buffer may end right there); the last
+// < 16 bytes of the input are read from global memory. The descriptor is built from wave-uniform
+// values (SGPRs); a chunk past num_records still writes its LDS slot (zeros), so the issue loop masks
+// the lanes past the window's end.
+__device__ __forceinline__ Src load_window(KParams& dp, LDS uint32_t* win, uint64_t lo, int lane, bool thrift,
+                                           bool wait = true) {
   const uint64_t abs_in = (uint64_t)dp.in;
-  const uint64_t wbase = (abs_in + min(lo, dp.in_len)) & ~15ull;
-  const int32_t wlen = window_len(dp, wbase);
+  const uint64_t wbase = (abs_in + kmin64(lo, dp.in_len)) & ~15ull;
+  const uint64_t end = abs_in + dp.in_len;
+  const int32_t wlen = dp.nolds || end < wbase + 16 ? 0 : (int32_t)kmin64((uint64_t)WINB, (end - wbase) & ~15ull);
+  const uint32_t blo = __builtin_amdgcn_readfirstlane((uint32_t)wbase);
+  const uint32_t bhi = __builtin_amdgcn_readfirstlane((uint32_t)(wbase >> 32));
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(((uint64_t)bhi << 32) | blo), (short)0, __builtin_amdgcn_readfirstlane(wlen), 0x00020000);
+#pragma unroll
+  for (int k = 0; k < WIN_LOADS; k++)
+    if ((k + 1) * 64 <= WINB / 16 || k * 64 + lane < WINB / 16)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (LDS void*)(win + k * 256), 16, lane * 16, k * 1024, 0, 0);
+  if (wait) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const KAS KxProgram* P = dp.prog;
   return Src{dp.in, dp.in_len, wbase - abs_in, wlen, win, thrift ? P->steps : nullptr, thrift ? P->nsteps : 0u,
              thrift ? P->canon_pres : 0ull};
-}
-
-// HBM -> LDS window for input position `lo` (all DMA chunks in flight together)
-__device__ __forceinline__ void load_window(KParams& dp, LDS uint32_t* win, uint64_t lo, int lane) {
-  const uint64_t abs_in = (uint64_t)dp.in;
-  const uint64_t wbase = (abs_in + min(lo, dp.in_len)) & ~15ull;
-  const int32_t wlen = window_len(dp, wbase);
-  const int nch = wlen >> 4;
-  const GLB uint8_t* g = (const GLB uint8_t*)wbase;
-  // the window is reused tile after tile: the wave's reads of the previous tile complete first
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-  for (int k = 0; k < WIN_LOADS; k++) {
-    const int c = k * 64 + lane;
-    if (c < nch)
-      __builtin_amdgcn_global_load_lds((const GLB void*)(g + (size_t)c * 16), (LDS void*)(win + k * 256), 16, 0, 0);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // One record: FastRead (emit) or its length / var extents only (measure).
@@ -1057,215 +1085,115 @@ __device__ __forceinline__ int parse_record(KParams& dp, const Src& w, uint64_t 
   return rc;
 }
 
-// ---------------------------------------------------------------------------------------------
-// output offsets: 4 or 8 bytes per entry (kx_column.offset_bytes); a 4-byte column never wraps
-// ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ void put_off(KParams& dp, uint32_t c, uint64_t r, uint64_t v) {
-  if (r > dp.n || c >= KX_MAX_COLUMNS) { atomicOr(dp.cols.guard, (unsigned long long)G_OFFSET); return; }
-  if ((dp.cols.owide >> c) & 1) ((GLB uint64_t*)dp.cols.offs[c])[r] = v;
-  else ((GLB uint32_t*)dp.cols.offs[c])[r] = (uint32_t)v;
-}
-// arena limit of column c in arena units: its capacity, and the 4-byte offset range
-__device__ __forceinline__ uint64_t arena_lim(KParams& dp, uint32_t c) {
-  const uint64_t cap = dp.cols.cap[c];
-  return ((dp.cols.owide >> c) & 1) ? cap : min(cap, 0xffffffffull);
-}
-// offsets[i] = v for a record that ends the decoded prefix (n, or the failing record)
-__device__ __forceinline__ void put_total(KParams& dp, uint32_t c, uint64_t i, uint64_t v) {
-  if (v <= arena_lim(dp, c)) put_off(dp, c, i, v);
-  else atomicOr(dp.overflow, 1u);
-}
-
-// ---------------------------------------------------------------------------------------------
-// aggregates: lane / tile / super-tile
-// ---------------------------------------------------------------------------------------------
-constexpr uint32_t NOREL = 0xffffu;  // no tile-relative position
-
-// A lane's walk, kept in LDS between the walk and the emit (so nothing of it stays live in
-// registers across the super-tile's chaining and look-back). Positions are tile-relative, counts
-// per lane / tile fit 16 bits; arena prefixes are kept modulo 2^32 (exact unless the tile's own
-// records carry >= 4 GiB of payload, which the tile flags and the emit then recomputes).
-template <int NV>
-struct LaneS {
-  uint16_t cand;            // first record signature in the lane's segment, or NOREL
-  uint16_t ent;             // where the lane's records start, or NOREL
-  uint16_t cnt;             // records the lane emits (0 unless live)
-  uint16_t cpre;            // records of the live lanes below it
-  uint32_t vpre[NV > 0 ? NV : 1];  // arena units of the live lanes below it (mod 2^32), per var slot
-};
-
-struct TAgg {               // a tile's chain: entry, exit (X_ERR: ends in an error), records, arena units
+struct Agg {
   uint64_t ent, ex, cnt, errc, errp;
   uint64_t var[KXP_NV_MAX];
-  uint32_t wide;            // a var slot's total reaches 2^32: the emit recomputes the lane prefixes
-  uint32_t pad;
 };
 
-// A composite of consecutive super-tiles, or an inclusive prefix (kind 2, S unused).
-// kind 0: nothing; 1: no record start anywhere (the chain must pass over it: entry >= maxhi);
-// 2: records from entry S to exit X (X_ERR: the chain ends in error ec at byte ep, after C records).
-template <int NV>
-struct Comp {
-  uint32_t kind, ec;
-  uint64_t S, X, C, ep, maxhi;
-  uint64_t V[NV > 0 ? NV : 1];
-};
-
-// L then H (H covers the input right after L). False when the speculative entries disagree.
-template <int NV>
-__device__ __forceinline__ bool combine(const Comp<NV> L, const Comp<NV> H, Comp<NV>& out) {  // by value: out may alias
-  if (L.kind == 0) { out = H; return true; }
-  if (H.kind == 0 || (L.kind == 2 && L.X == X_ERR)) { out = L; return true; }
-  if (H.kind == 1) {
-    if (L.kind == 1) { out = L; out.maxhi = max(L.maxhi, H.maxhi); return true; }
-    if (L.X >= H.maxhi) { out = L; return true; }
-    return false;
-  }
-  if (L.kind == 1) { out = H; return true; }  // H.S lies past everything L covers
-  if (L.X != H.S) return false;
-  out = L;
-  out.X = H.X;
-  out.C = L.C + H.C;
-  out.ec = H.ec;
-  out.ep = H.ep;
-#pragma unroll
-  for (int v = 0; v < NV; v++) out.V[v] = L.V[v] + H.V[v];
-  return true;
-}
-
-// ---------------------------------------------------------------------------------------------
-// concatenated mode: candidates, lane walks, the tile walk with in-wave repair
-// ---------------------------------------------------------------------------------------------
-// The record signature is the first 3 bytes of a record. The schema's canonical one (the encoder's
-// first field header) is used when the batch's first record starts with it; otherwise (an
-// IDL-order producer, an unset optional first field, the schema-less skip decoder) the first
-// record's own first 3 bytes are: records of one batch normally start alike.
-__device__ __forceinline__ uint32_t data_sig(KParams& dp) {
-  if (dp.in_len < 3) return 0;
-  const GLB uint8_t* p = (const GLB uint8_t*)dp.in;
-  return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16);
-}
-
-#define P_SIG(P, MODE) ((MODE) == M_THRIFT ? (P)->sig : ~0u)
-
-// does the record at c parse, and is it followed by the signature again (or the end of the input)?
+// Concatenated mode, one wave, one tile [tlo, thi) in the LDS window. Lane l owns the 128-byte
+// segment l: it starts at the first canonical record signature in its segment (or where the chain
+// of the lane below enters it) and walks records until it leaves the segment. Lanes re-walk until
+// the chain is consistent (`seed` = the tile's true entry when known, else the lowest lane's
+// candidate is trusted). The record starts of the tile are written to `starts` (u16, relative to
+// tlo). Returns the tile aggregate (uniform).
 template <int NV, int MODE>
-__device__ __forceinline__ bool succ_ok(KParams& dp, const Src& w, uint64_t c, uint32_t sig) {
-  VarState<NV> vs;
-  uint64_t e = c, pres;
-  if (parse_record<NV, MODE>(dp, w, c, dp.in_len, 0, false, &e, vs, pres)) return false;
-  return e == dp.in_len || (dp.in_len - e >= 3 && (ld4(w, e) & 0xffffffu) == sig);
-}
-
-// first plausible record start in the lane's segment [seg_lo, seg_hi) (speculation only)
-template <int NV, int MODE>
-__device__ __forceinline__ uint64_t lane_candidate(KParams& dp, const Src& w, uint64_t seg_lo, uint64_t seg_hi,
-                                                   uint32_t dsig, int lane) {
-  if (seg_lo >= seg_hi) return X_NONE;
-  if (MODE == M_PB) return pb_scan_segment(w, seg_lo, seg_hi, dp.in_len, lane);
+__device__ Agg walk_tile(KParams& dp, const Src& w, uint64_t tlo, uint64_t thi, uint64_t seed, int lane,
+                         uint16_t* starts) {
   const KAS KxProgram* P = dp.prog;
-  const bool dok = dsig != 0 && canon_t(dsig & 0xff) != 1;  // the first record starts with a field header
-  uint32_t sig, slen;
-  bool ambig = false;
-  if (MODE == M_THRIFT && P->sig_len == 3 && (!dok || dsig == P->sig)) {
-    sig = P->sig; slen = 3; ambig = P->sig_ambig && w.nsteps;
-  } else if (dok) {
-    sig = dsig; slen = 3;
-  } else if (MODE == M_THRIFT) {
-    sig = P->sig; slen = P->sig_len;
-  } else {
-    sig = KX_T_STOP; slen = 1;
-  }
-  const uint64_t plim = min(seg_hi, dp.in_len >= slen ? dp.in_len - slen + 1 : 0ull);
-  const int32_t q0 = wofs(w, seg_lo, SEG + 12);
-  uint64_t ent = X_NONE;
-  if (slen == 3 && seg_hi - seg_lo == SEG && q0 >= 0 && MODE == M_THRIFT && ambig) {
-    // the signature also starts a nested struct: keep the lowest of the two lowest hits that parses
-    // as a canonical record (a nested-struct start does not), else no candidate
-    uint32_t c1, c2;
-    scan_segment2(w, q0, sig, lane, c1, c2);
-    VarState<NV> vs0;
-    uint64_t e0;
-    if (c1 < (uint32_t)SEG && seg_lo + c1 < plim &&
-        canon_record<NV>(w, dp.cols, seg_lo + c1, dp.in_len, 0, false, &e0, vs0))
-      ent = seg_lo + c1;
-    else if (c2 < (uint32_t)SEG && seg_lo + c2 < plim &&
-             canon_record<NV>(w, dp.cols, seg_lo + c2, dp.in_len, 0, false, &e0, vs0))
-      ent = seg_lo + c2;
-  } else if (slen == 3 && seg_hi - seg_lo == SEG && q0 >= 0 && sig != P_SIG(P, MODE)) {
-    // a signature taken from the data may also start nested structs: keep the lowest of the two
-    // lowest hits whose record is followed by the signature again (or ends the input)
-    uint32_t c1, c2;
-    scan_segment2(w, q0, sig, lane, c1, c2);
-    if (c1 < (uint32_t)SEG && seg_lo + c1 < plim && succ_ok<NV, MODE>(dp, w, seg_lo + c1, sig)) ent = seg_lo + c1;
-    else if (c2 < (uint32_t)SEG && seg_lo + c2 < plim && succ_ok<NV, MODE>(dp, w, seg_lo + c2, sig)) ent = seg_lo + c2;
-  } else if (slen == 3 && seg_hi - seg_lo == SEG && q0 >= 0) {
-    ent = scan_segment(w, q0, seg_lo, plim, sig, lane);
-  } else {
-    const uint32_t smask = slen == 3 ? 0xffffffu : 0xffu;
-    for (uint64_t p = seg_lo; p < plim; p++)
-      if ((ld4(w, p) & smask) == sig) { ent = p; break; }
-  }
-  return ent;
-}
-
-// walk records from `ent` until the lane's segment is left (measure only); on a decode error ex =
-// X_ERR and errp = the failing record's start
-template <int NV, int MODE>
-__device__ __forceinline__ void walk_lane(KParams& dp, const Src& w, uint64_t ent, uint64_t seg_hi, uint64_t& ex,
-                                          uint64_t& cnt, uint32_t& errc, uint64_t& errp, uint64_t* vsum) {
-  uint64_t pos = ent, c = 0;
-  int e = 0;
-#pragma unroll
-  for (int v = 0; v < NV; v++) vsum[v] = 0;
-  while (pos < seg_hi && pos < dp.in_len) {
-    VarState<NV> vs;
-    uint64_t end = pos, pres;
-    const int rc = parse_record<NV, MODE>(dp, w, pos, dp.in_len, 0, false, &end, vs, pres);
-    if (rc) { e = rc; break; }
-    c++;
-#pragma unroll
-    for (int v = 0; v < NV; v++) vsum[v] += vs.len[v];
-    pos = end;
-  }
-  ex = e ? X_ERR : pos;
-  cnt = c;
-  errc = (uint32_t)e;
-  errp = pos;
-}
-
-// One wave, tile [tlo, thi) in the LDS window. Every lane starts at its candidate (ls[lane].cand) or
-// where the chain of the nearest lower walking lane (or `seed`, the tile's true entry when known)
-// enters its segment, and walks until it leaves it; lanes re-walk until the chain is consistent.
-// While speculating (seed unknown) a candidate whose own walk fails is dropped, so a false signature
-// hit does not end the tile's chain. Returns the tile aggregate (uniform) and leaves every lane's
-// emit state (entry, records, prefixes among the live lanes) in ls[lane].
-template <int NV, int MODE>
-__device__ __forceinline__ TAgg walk_tile(KParams& dp, const Src& w, uint64_t tlo, uint64_t thi, uint64_t seed,
-                                          int lane, LDS LaneS<NV>* ls) {
   const uint64_t seg_lo = tlo + (uint64_t)lane * SEG;
-  const uint64_t seg_hi = min(seg_lo + SEG, thi);
-  const uint32_t c0 = ls[lane].cand;  // (NOREL: none)
-  uint64_t ent = c0 == NOREL ? X_NONE : tlo + c0;
+  const uint64_t seg_hi = kmin64(seg_lo + SEG, thi);
+  uint64_t ent = X_NONE;
+  if (seg_lo < thi && MODE == M_PB) {
+    ent = pb_scan_segment(w, seg_lo, seg_hi, dp.in_len, lane);
+  } else if (seg_lo < thi) {
+    const uint32_t sig = MODE == M_THRIFT ? P->sig : (uint32_t)KX_T_STOP;
+    const uint32_t slen = (MODE == M_THRIFT && P->sig_len == 3) ? 3u : 1u;
+    const uint64_t plim = kmin64(seg_hi, dp.in_len >= slen ? dp.in_len - slen + 1 : 0ull);
+    const int32_t q0 = wofs(w, seg_lo, SEG + 12);
+    if (slen == 3 && seg_hi - seg_lo == SEG && q0 >= 0 && MODE == M_THRIFT && P->sig_ambig && w.nsteps) {
+      // the signature also starts a nested struct: keep the lowest of the two lowest hits that parses
+      // as a canonical record (a nested-struct start does not), else no candidate (speculation only)
+      uint32_t c1, c2;
+      scan_segment2(w, q0, sig, lane, c1, c2);
+      VarState<NV> vs0;
+      uint64_t e0;
+      if (c1 < (uint32_t)SEG && seg_lo + c1 < plim &&
+          canon_record<NV>(w, dp.cols, seg_lo + c1, dp.in_len, 0, false, &e0, vs0))
+        ent = seg_lo + c1;
+      else if (c2 < (uint32_t)SEG && seg_lo + c2 < plim &&
+               canon_record<NV>(w, dp.cols, seg_lo + c2, dp.in_len, 0, false, &e0, vs0))
+        ent = seg_lo + c2;
+    } else if (slen == 3 && seg_hi - seg_lo == SEG && q0 >= 0) {
+      ent = scan_segment(w, q0, seg_lo, plim, sig, lane);
+    } else {
+      const uint32_t smask = slen == 3 ? 0xffffffu : 0xffu;
+      for (uint64_t p = seg_lo; p < plim; p++)
+        if ((ld4(w, p) & smask) == sig) { ent = p; break; }
+    }
+  }
+  if (dp.diag & 512) {  // diagnostics: DMA + candidate scan only
+    Agg a;
+    a.ent = __ballot(ent != X_NONE) ? ent : X_NONE; a.ex = thi; a.cnt = 0; a.errc = 0; a.errp = 0;
+    for (int v = 0; v < NV; v++) a.var[v] = 0;
+    return a;
+  }
+  uint64_t tp = (dp.diag & 64) ? __builtin_amdgcn_s_memtime() : 0;
+  auto phase = [&](int k) {
+    if (dp.diag & 64) {
+      const uint64_t now = __builtin_amdgcn_s_memtime();
+      if (lane == 0) atomicAdd(&g_phase[k], (unsigned long long)(now - tp));
+      tp = now;
+    }
+  };
+  phase(1);
   uint64_t ex = X_NONE, cnt = 0, errp = 0;
-  uint32_t errc = 0;
+  int errc = 0;
   uint64_t vsum[NV > 0 ? NV : 1];
 #pragma unroll
   for (int v = 0; v < (NV > 0 ? NV : 1); v++) vsum[v] = 0;
+  uint64_t st0 = 0, st1 = 0, st2 = 0, st3 = 0;  // the lane's first record starts
   bool need = ent != X_NONE;
   int rounds = 0;
-  bool first = true;
-  uint64_t hm;
+  bool enumerate = false;   // second pass: lanes with > 4 records write the rest of their starts
+  uint64_t sbase = 0;
+  Agg a;
   for (;;) {
-    if (need) walk_lane<NV, MODE>(dp, w, ent, seg_hi, ex, cnt, errc, errp, vsum);
-    need = false;
-    if (first && seed == X_NONE && ent != X_NONE && ex == X_ERR) {
-      ent = X_NONE; ex = X_NONE; cnt = 0; errc = 0;
+    if (need) {
+      uint64_t pos = ent, c = 0;
+      int e = 0;
+      uint64_t acc[NV > 0 ? NV : 1];
 #pragma unroll
-      for (int v = 0; v < NV; v++) vsum[v] = 0;
+      for (int v = 0; v < (NV > 0 ? NV : 1); v++) acc[v] = 0;
+      while (pos < seg_hi && pos < dp.in_len) {
+        VarState<NV> vs;
+        uint64_t end = pos, pres;
+        const int rc = parse_record<NV, MODE>(dp, w, pos, dp.in_len, 0, false, &end, vs, pres);
+        if (rc) { e = rc; break; }
+        if (!enumerate) {
+          st0 = c == 0 ? pos : st0; st1 = c == 1 ? pos : st1;
+          st2 = c == 2 ? pos : st2; st3 = c == 3 ? pos : st3;
+        } else if (c >= 4) {
+          starts[sbase + c] = (uint16_t)(pos - tlo);
+        }
+        c++;
+#pragma unroll
+        for (int v = 0; v < NV; v++) acc[v] += vs.len[v];
+        pos = end;
+      }
+      ex = e ? X_ERR : pos;
+      cnt = c;
+      errc = e;
+      errp = pos;
+#pragma unroll
+      for (int v = 0; v < NV; v++) vsum[v] = acc[v];
     }
-    first = false;
-    hm = __ballot(ent != X_NONE);
+    need = false;
+    if (enumerate) break;
+    phase(2);
+
+    // ---- one repair round: every lane must start at the first true record start in its segment,
+    //      i.e. where the chain of the nearest lower walking lane (or `seed`) enters it ----
+    const uint64_t hm = __ballot(ent != X_NONE);
     const uint64_t below = hm & ((1ull << lane) - 1);
     const int pc = below ? 63 - __clzll((long long)below) : -1;
     const uint64_t pex = __shfl(ex, pc < 0 ? 0 : pc, 64);
@@ -1276,51 +1204,57 @@ __device__ __forceinline__ TAgg walk_tile(KParams& dp, const Src& w, uint64_t tl
       else if (pe >= seg_lo) want = pe;
     }
     const bool ch = want != ent;
-    if (!__ballot(ch)) break;
-    if (++rounds > 70) {  // from a fixed lowest entry the chain settles in <= 65 rounds
-      if (lane == 0) {
-        atomicCAS((int*)&dp.status->code, 0, KX_ERR_INTERNAL);
-        atomicOr((unsigned long long*)&dp.status->diag[2], (unsigned long long)G_ROUNDS);
+    if (__ballot(ch)) {
+      if (++rounds <= 70) {  // from a fixed lowest entry the chain settles in <= 65 rounds
+        if (ch) {
+          ent = want;
+          need = ent != X_NONE;
+          ex = X_NONE; cnt = 0; errc = 0;
+#pragma unroll
+          for (int v = 0; v < NV; v++) vsum[v] = 0;
+        }
+        continue;
       }
-      break;
+      if (lane == 0) atomicCAS((int*)&dp.status->code, 0, KX_ERR_INTERNAL);
     }
-    if (ch) {
-      ent = want;
-      need = want != X_NONE;
-      ex = X_NONE; cnt = 0; errc = 0;
+
+    // ---- converged: the tile aggregate ----
+    const uint64_t em = __ballot(ent != X_NONE && ex == X_ERR);
+    const int fel = em ? __ffsll((long long)em) - 1 : 64;
+    const bool live = ent != X_NONE && lane <= fel;
+    const uint64_t c0 = live ? cnt : 0;
+    const uint64_t inc = wave_incl_scan(c0, lane);
+    const uint64_t cpre = inc - c0;
+    a.cnt = rl64(inc, 63);
 #pragma unroll
-      for (int v = 0; v < NV; v++) vsum[v] = 0;
+    for (int v = 0; v < NV; v++) a.var[v] = wave_sum(live ? vsum[v] : 0);
+    a.ent = hm ? rl64(ent, __ffsll((long long)hm) - 1) : X_NONE;
+    a.ex = fel < 64 ? X_ERR : hm ? rl64(ex, 63 - __clzll((long long)hm)) : seed;
+    a.errc = fel < 64 ? (uint64_t)__builtin_amdgcn_readlane(errc, fel) : 0;
+    a.errp = fel < 64 ? rl64(errp, fel) : 0;
+    phase(3);
+    if (live) {
+      const uint64_t b = cpre;
+      if (cnt > 0) starts[b + 0] = (uint16_t)(st0 - tlo);
+      if (cnt > 1) starts[b + 1] = (uint16_t)(st1 - tlo);
+      if (cnt > 2) starts[b + 2] = (uint16_t)(st2 - tlo);
+      if (cnt > 3) starts[b + 3] = (uint16_t)(st3 - tlo);
     }
+    if (__ballot(live && cnt > 4)) {
+      enumerate = true;
+      need = live && cnt > 4;
+      sbase = cpre;
+      continue;
+    }
+    break;
   }
-  const uint64_t em = __ballot(ent != X_NONE && ex == X_ERR);
-  const int fel = em ? __ffsll((long long)em) - 1 : 64;
-  const bool live = ent != X_NONE && lane <= fel;
-  TAgg a;
-  a.wide = 0;
-  const uint64_t lc = live ? cnt : 0;
-  const uint64_t ci = wave_incl_scan(lc, lane);
-  a.cnt = rl64(ci, 63);
-  ls[lane].ent = live ? (uint16_t)(ent - tlo) : (uint16_t)NOREL;
-  ls[lane].cnt = (uint16_t)lc;
-  ls[lane].cpre = (uint16_t)(ci - lc);
-#pragma unroll
-  for (int v = 0; v < NV; v++) {
-    const uint64_t x0 = live ? vsum[v] : 0;
-    const uint64_t xi = wave_incl_scan(x0, lane);
-    ls[lane].vpre[v] = (uint32_t)(xi - x0);
-    a.var[v] = rl64(xi, 63);
-    a.wide |= a.var[v] >> 32 ? 1u : 0u;
-  }
-  a.ent = hm ? rl64(ent, __ffsll((long long)hm) - 1) : X_NONE;
-  a.ex = fel < 64 ? X_ERR : hm ? rl64(ex, 63 - __clzll((long long)hm)) : seed;
-  a.errc = fel < 64 ? (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)errc, fel) : 0;
-  a.errp = fel < 64 ? rl64(errp, fel) : 0;
+  phase(4);
   return a;
 }
 
 // Known-offsets mode: lane = record. Measures the var extents (failed records count as empty).
 template <int NV, int MODE>
-__device__ __forceinline__ TAgg measure_records(KParams& dp, const Src& w, uint64_t r0, uint64_t r1, int lane) {
+__device__ __forceinline__ Agg measure_records(KParams& dp, const Src& w, uint64_t r0, uint64_t r1, int lane) {
   const uint64_t r = r0 + lane;
   VarState<NV> vs;
 #pragma unroll
@@ -1334,566 +1268,468 @@ __device__ __forceinline__ TAgg measure_records(KParams& dp, const Src& w, uint6
       for (int v = 0; v < NV; v++) vs.len[v] = 0;
     }
   }
-  TAgg g;
-  g.ent = 0; g.ex = 0; g.errc = 0; g.errp = 0; g.wide = 0;
+  Agg g;
+  g.ent = X_NONE; g.ex = X_NONE; g.errc = 0; g.errp = 0;
   g.cnt = r1 - r0;
 #pragma unroll
   for (int v = 0; v < NV; v++) g.var[v] = wave_sum(vs.len[v]);
   return g;
 }
 
-// tile geometry: bytes (concatenated) or records (known offsets)
+// tile geometry
 __device__ __forceinline__ void tile_range(KParams& dp, uint64_t t, uint64_t& lo, uint64_t& hi) {
   if (dp.offsets) {
-    lo = t * dp.krec;
-    hi = min(lo + dp.krec, dp.n);
+    const uint64_t r0 = t * dp.krec, r1 = kmin64(r0 + dp.krec, dp.n);
+    lo = r0; hi = r1;  // records
   } else {
     lo = t * (uint64_t)TILE;
-    hi = min(lo + TILE, dp.in_len);
-  }
-}
-__device__ __forceinline__ uint64_t st_hi(KParams& dp, uint64_t s) {
-  return min((s + 1) * (uint64_t)WGW * TILE, dp.in_len);
-}
-// the input position of a tile's window
-__device__ __forceinline__ uint64_t tile_pos(KParams& dp, uint64_t lo) { return dp.offsets ? dp.offsets[lo] : lo; }
-
-// ---------------------------------------------------------------------------------------------
-// super-tile: chaining the tiles of one workgroup (LDS), publishing, decoupled look-back
-// ---------------------------------------------------------------------------------------------
-// super-tile state machine (decode_kernel, st_step)
-enum { ST_SPEC = 0, ST_LB = 1, ST_TRUE = 2, ST_DONE = 3 };
-
-template <int NV>
-struct StShared {
-  TAgg ta[WGW];               // tile aggregates
-  uint64_t tbc[WGW];          // records of the ST's chain before tile k
-  uint64_t tbv[WGW][KXP_NV_MAX];
-  int on[WGW];                // tile k is on the chain
-  int fix;                    // tile to re-walk (-1: none)
-  int state;                  // ST_* (decode_kernel)
-  int nfix;                   // re-walks of this super-tile so far
-  uint64_t fixE;              // ... from this entry
-  uint64_t tk, tkn[2];        // first ticket; the next one (prefetched; by iteration parity)
-  Comp<NV> agg, fin, pre;     // speculative / true ST aggregate, prefix before the ST
-};
-
-// Chains the tile aggregates of super-tile s from entry Ein (X_NONE = speculative: the first tile
-// with a record start is trusted). Returns the first tile that disagrees with the chain (to be
-// re-walked from *fixE), or -1 with the ST aggregate in `out` and each tile's base / membership.
-template <int NV>
-__device__ __forceinline__ int st_fold(KParams& dp, StShared<NV>* sh, uint64_t s, uint64_t Ein, Comp<NV>& out,
-                                       uint64_t* fixE) {
-  Comp<NV> cur;
-  cur.kind = Ein == X_NONE ? 0u : 2u;
-  cur.S = Ein; cur.X = Ein; cur.C = 0; cur.ec = 0; cur.ep = 0; cur.maxhi = 0;
-#pragma unroll
-  for (int v = 0; v < (NV > 0 ? NV : 1); v++) cur.V[v] = 0;
-  const bool known = dp.offsets != nullptr;
-  for (int k = 0; k < WGW; k++) {
-    const uint64_t t = s * WGW + k;
-    sh->tbc[k] = cur.C;
-#pragma unroll
-    for (int v = 0; v < NV; v++) sh->tbv[k][v] = cur.V[v];
-    sh->on[k] = 0;
-    if (t >= dp.ntiles) continue;
-    const TAgg& a = sh->ta[k];
-    if (!known) {
-      uint64_t lo, hi;
-      tile_range(dp, t, lo, hi);
-      if (cur.kind == 2 && cur.X == X_ERR) continue;
-      if (cur.kind != 2) {
-        if (a.ent == X_NONE) continue;
-        cur.kind = 2;
-        cur.S = a.ent;
-      } else {
-        if (cur.X >= hi) continue;  // the chain passes over this tile
-        if (a.ent != cur.X) { *fixE = cur.X; return k; }
-      }
-      cur.X = a.ex;
-      if (a.ex == X_ERR) { cur.ec = (uint32_t)a.errc; cur.ep = a.errp; }
-    }
-    sh->on[k] = 1;
-    cur.C += a.cnt;
-#pragma unroll
-    for (int v = 0; v < NV; v++) cur.V[v] += a.var[v];
-  }
-  if (cur.kind != 2) {
-    cur.kind = 1;
-    cur.S = cur.X = X_NONE;
-    cur.maxhi = st_hi(dp, s);
-  }
-  out = cur;
-  return -1;
-}
-
-__device__ __forceinline__ uint64_t sword(KParams& dp, int f, uint64_t j) {
-  if (j >= dp.nst) { atomicOr(dp.cols.guard, (unsigned long long)G_WORD); return 0; }
-  return aload64(dp.sdesc + (uint64_t)f * dp.nst + j);
-}
-
-template <int NV>
-__device__ __forceinline__ void publish(KParams& dp, uint64_t s, const Comp<NV>& c, bool inclusive) {
-  const uint64_t ep = dp.epoch, ns = dp.nst;
-  if (s >= ns) { atomicOr(dp.cols.guard, (unsigned long long)G_WORD); return; }
-  if (inclusive) {
-    put_word(dp.sdesc, ns, P_C, s, ep, c.C);
-    put_word(dp.sdesc, ns, P_EC, s, ep, c.ec);
-    put_word(dp.sdesc, ns, P_EP, s, ep, c.ep);
-#pragma unroll
-    for (int v = 0; v < NV; v++) put_word(dp.sdesc, ns, P_V + v, s, ep, c.V[v]);
-    put_word(dp.sdesc, ns, P_X, s, ep, c.X);
-  } else {
-    const bool pass = c.kind != 2;
-    put_word(dp.sdesc, ns, A_X, s, ep, pass ? X_NONE : c.X);
-    put_word(dp.sdesc, ns, A_C, s, ep, c.C);
-    put_word(dp.sdesc, ns, A_EC, s, ep, c.ec);
-    put_word(dp.sdesc, ns, A_EP, s, ep, c.ep);
-#pragma unroll
-    for (int v = 0; v < NV; v++) put_word(dp.sdesc, ns, A_V + v, s, ep, c.V[v]);
-    put_word(dp.sdesc, ns, A_S, s, ep, pass ? X_NONE : c.S);
+    hi = kmin64(lo + TILE, dp.in_len);
   }
 }
 
-// the A (speculative) or P (inclusive) words of super-tile j; false unless all carry this epoch
-template <int NV>
-__device__ __forceinline__ bool load_st(KParams& dp, uint64_t j, bool inclusive, Comp<NV>& c) {
+// (re)walk tile t of a concatenated batch with the wave's LDS window
+template <int NV, int MODE>
+__device__ Agg tile_agg(KParams& dp, LDS uint32_t* win, uint64_t t, uint64_t seed, int lane) {
+  uint64_t lo, hi;
+  tile_range(dp, t, lo, hi);
+  if (dp.offsets) {
+    const Src w = load_window(dp, win, dp.offsets[lo], lane, MODE == M_THRIFT);
+    return measure_records<NV, MODE>(dp, w, lo, hi, lane);
+  }
+  const uint64_t t0 = (dp.diag & 64) ? __builtin_amdgcn_s_memtime() : 0;
+  const Src w = load_window(dp, win, lo, lane, MODE == M_THRIFT);
+  if ((dp.diag & 64) && lane == 0) atomicAdd(&g_phase[0], (unsigned long long)(__builtin_amdgcn_s_memtime() - t0));
+  return walk_tile<NV, MODE>(dp, w, lo, hi, seed, lane, dp.starts + t * dp.slotcap);
+}
+
+__device__ __forceinline__ void put_tile(KParams& dp, uint64_t t, const Agg& a, int nv) {
+  const uint64_t ep = dp.epoch, nt = dp.ntiles;
+  put_word(dp.tdesc, nt, T_ENT, t, ep, a.ent);
+  put_word(dp.tdesc, nt, T_EXIT, t, ep, a.ex);
+  put_word(dp.tdesc, nt, T_CNT, t, ep, a.cnt);
+  put_word(dp.tdesc, nt, T_ERRC, t, ep, a.errc);
+  put_word(dp.tdesc, nt, T_ERRP, t, ep, a.errp);
+  for (int v = 0; v < nv; v++) put_word(dp.tdesc, nt, T_VAR + v, t, ep, a.var[v]);
+}
+
+// Does a chain arriving at `E` agree with an item whose speculative entry is `ent`? (An item with no
+// record start is a pass-through: the chain must jump over it.)
+__device__ __forceinline__ bool chain_ok(uint64_t E, uint64_t ent, uint64_t hi) {
+  if (E == X_ERR || E == X_DONE) return true;  // the chain already ended
+  if (ent == X_BAD) return false;
+  return ent == X_NONE ? E >= hi : ent == E;
+}
+
+// Group scan, one wave, lane = tile of group g. Validates the speculative chain between the tiles
+// (`entry` = the group's true entry when known, else X_NONE = trust the first tile that has a record
+// start), then writes each tile's exclusive prefix inside the group and the group aggregate.
+// REPAIR: a tile that disagrees is re-walked from its true entry; otherwise the group is marked
+// X_BAD and left to the chain pass (keeps the re-walk out of the index pass's registers).
+template <int NV, int MODE, bool REPAIR>
+__device__ void group_scan(KParams& dp, LDS uint32_t* win, uint64_t g, uint64_t entry, int lane) {
+  const uint64_t t0 = g * GT;
+  const uint64_t ntg = kmin64((uint64_t)GT, dp.ntiles - t0);
+  const bool act = (uint64_t)lane < ntg;
+  const uint64_t t = t0 + lane;
   const uint64_t ep = dp.epoch;
-  bool ok = true;
-  uint64_t x;
-  if (inclusive) {
-    x = sword(dp, P_X, j); ok &= (x >> 48) == ep; c.X = x & V48;
-    x = sword(dp, P_C, j); ok &= (x >> 48) == ep; c.C = x & V48;
-    x = sword(dp, P_EC, j); ok &= (x >> 48) == ep; c.ec = (uint32_t)(x & V48);
-    x = sword(dp, P_EP, j); ok &= (x >> 48) == ep; c.ep = x & V48;
+  constexpr int NW = 5 + NV;
+  int fields[NW];
 #pragma unroll
-    for (int v = 0; v < NV; v++) { x = sword(dp, P_V + v, j); ok &= (x >> 48) == ep; c.V[v] = x & V48; }
-    c.kind = 2;
-    c.S = 0;
-  } else {
-    x = sword(dp, A_S, j); ok &= (x >> 48) == ep; c.S = x & V48;
-    x = sword(dp, A_X, j); ok &= (x >> 48) == ep; c.X = x & V48;
-    x = sword(dp, A_C, j); ok &= (x >> 48) == ep; c.C = x & V48;
-    x = sword(dp, A_EC, j); ok &= (x >> 48) == ep; c.ec = (uint32_t)(x & V48);
-    x = sword(dp, A_EP, j); ok &= (x >> 48) == ep; c.ep = x & V48;
-#pragma unroll
-    for (int v = 0; v < NV; v++) { x = sword(dp, A_V + v, j); ok &= (x >> 48) == ep; c.V[v] = x & V48; }
-    c.kind = c.S == X_NONE ? 1u : 2u;
-  }
-  c.maxhi = dp.offsets ? 0 : st_hi(dp, j);
-  return ok;
-}
-
-// Watchdog of the look-back waits: a wait gives up (the call fails with KX_ERR_INTERNAL, the returned
-// prefix ends the chain) only when no super-tile anywhere has published its prefix for 2 s (a long
-// but moving serial chain is not a hang), or when another wait already gave up.
-__device__ __forceinline__ bool wait_expired(KParams& dp, uint64_t& t0, uint64_t& prog) {
-  if (__hip_atomic_load(dp.abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return true;
-  const uint64_t p = aload64((const uint64_t*)dp.progress);
-  const uint64_t now = now_ns();
-  if (p != prog) { prog = p; t0 = now; return false; }
-  if (now - t0 <= 2000000000ull) return false;
-  __hip_atomic_store(dp.abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return true;
-}
-
-template <int NV>
-__device__ __forceinline__ Comp<NV> bcast(const Comp<NV>& c, int l) {
-  Comp<NV> r;
-  r.kind = (uint32_t)__builtin_amdgcn_readlane((int)c.kind, l);
-  r.ec = (uint32_t)__builtin_amdgcn_readlane((int)c.ec, l);
-  r.S = rl64(c.S, l); r.X = rl64(c.X, l); r.C = rl64(c.C, l); r.ep = rl64(c.ep, l); r.maxhi = rl64(c.maxhi, l);
-#pragma unroll
-  for (int v = 0; v < NV; v++) r.V[v] = rl64(c.V[v], l);
-  return r;
-}
-
-template <int NV>
-__device__ __forceinline__ Comp<NV> failed_prefix(KParams& dp, int lane, uint64_t why) {
-  if (lane == 0) {
-    atomicCAS((int*)&dp.status->code, 0, KX_ERR_INTERNAL);
-    atomicOr((unsigned long long*)&dp.status->diag[2], why);
-  }
-  Comp<NV> e;
-  e.kind = 2; e.ec = KX_ERR_INTERNAL; e.S = 0; e.X = X_ERR; e.C = 0; e.ep = 0; e.maxhi = 0;
-#pragma unroll
-  for (int v = 0; v < (NV > 0 ? NV : 1); v++) e.V[v] = 0;
-  return e;
-}
-
-// Decoupled look-back (one wave): the inclusive prefix of the chain before super-tile s. Lane l
-// reads super-tile jhi - l (its inclusive prefix P when published, else its speculative aggregate A);
-// the window's A are combined up to the nearest P, every boundary checked for chain consistency. If
-// the speculation disagrees anywhere, the predecessor's own P is awaited (it re-walks itself from
-// its true entry).
-template <int NV>
-__device__ __forceinline__ Comp<NV> lookback(KParams& dp, uint64_t s, int lane) {
-  Comp<NV> base0;
-  base0.kind = 2; base0.ec = 0; base0.S = 0; base0.X = 0; base0.C = 0; base0.ep = 0; base0.maxhi = 0;
-#pragma unroll
-  for (int v = 0; v < (NV > 0 ? NV : 1); v++) base0.V[v] = 0;
-  if (s == 0) return base0;
-  Comp<NV> acc;
-  acc.kind = 0;
-  uint64_t jhi = s - 1;
-  int wsz = 16;
-  uint64_t t0 = now_ns(), prog = ~0ull;
-  int backoff = 1;
-  bool ok = true;
-  for (;;) {
-    const bool inwin = lane < wsz;
-    const bool v = inwin && jhi >= (uint64_t)lane;
-    Comp<NV> c;
-    bool hp = false, ha = false;
-    if (v) {
-      hp = load_st<NV>(dp, jhi - lane, true, c);
-      if (!hp) ha = load_st<NV>(dp, jhi - lane, false, c);
-    }
-    const uint64_t pm = __ballot(hp || (inwin && !v));
-    const int p = pm ? __ffsll((long long)pm) - 1 : wsz;
-    const uint64_t need = p >= 64 ? ~0ull : ((1ull << p) - 1);
-    if ((__ballot(ha) & need) != need) {
-      if (__ballot(wait_expired(dp, t0, prog))) return failed_prefix<NV>(dp, lane, G_LB_WAIT);
-      for (int k = 0; k < backoff; k++) __builtin_amdgcn_s_sleep(1);
-      backoff = backoff < 32 ? backoff * 2 : 32;
-      continue;
-    }
-    Comp<NV> wc;
-    wc.kind = 0;
-    for (int k = p - 1; k >= 0 && ok; k--) ok = combine(wc, bcast(c, k), wc);
-    if (ok) ok = combine(wc, acc, acc);
-    if (!ok) break;
-    if (p < wsz || jhi < (uint64_t)wsz) {  // a published prefix, or the window reached super-tile 0
-      const Comp<NV> base = p < wsz && jhi >= (uint64_t)p ? bcast(c, p) : base0;
-      Comp<NV> r;
-      if (combine(base, acc, r) && r.kind == 2) return r;
-      break;
-    }
-    jhi -= (uint64_t)wsz;
-    wsz = 64;
-  }
-  if (lane == 0) atomicAdd((unsigned long long*)&dp.status->diag[1], 1ull);
-  // the speculation disagrees below s: the predecessor resolves itself; take its inclusive prefix
-  backoff = 1;
-  for (;;) {
-    Comp<NV> P;
-    const bool hp = load_st<NV>(dp, s - 1, true, P);
-    if (__ballot(hp) & 1ull) return bcast(P, 0);
-    if (__ballot(wait_expired(dp, t0, prog))) return failed_prefix<NV>(dp, lane, G_LB_SLOW);
-    for (int k = 0; k < backoff; k++) __builtin_amdgcn_s_sleep(1);
-    backoff = backoff < 32 ? backoff * 2 : 32;
-  }
-}
-
-// ---------------------------------------------------------------------------------------------
-// emit
-// ---------------------------------------------------------------------------------------------
-// the var payloads of record r at the running arena positions
-template <int NV>
-__device__ __forceinline__ void emit_vars(KParams& dp, const Src& w, const VarState<NV>& vs, uint64_t r, uint64_t* run) {
-  const KAS KxProgram* P = dp.prog;
-#pragma unroll
-  for (int v = 0; v < NV; v++) {
-    if (v >= (int)P->nvar) break;
-    const uint32_t c = P->var_col[v];
-    const uint32_t nn = vs.len[v];
-    const uint64_t at = run[v];
-    if (at + nn <= arena_lim(dp, c)) {
-      put_off(dp, c, r, at);
-      if (nn) {
-        const KxpCol K = ld_col(P, c);
-        copy_var(w, K, vs.pos[v], nn, (uint8_t*)dp.cols.data[c] + at * K.width);
-      }
-    } else {
-      atomicOr(dp.overflow, 1u);
-    }
-    run[v] = at + nn;
-  }
-}
-
-// record n-1 was decoded: the call's final status
-template <int NV, int MODE>
-__device__ __forceinline__ void finish_ok(KParams& dp, uint64_t consumed, const uint64_t* run) {
-  const KAS KxProgram* P = dp.prog;
-  kx_status* st = dp.status;
-  st->n_records = dp.n;
-  st->consumed = consumed;
-  if (MODE == M_SKIP) dp.skip_out[dp.n] = consumed;
-#pragma unroll
-  for (int v = 0; v < NV; v++) {
-    if (v >= (int)P->nvar) break;
-    st->var_total[v] = run[v];
-    put_total(dp, P->var_col[v], dp.n, run[v]);
-  }
-}
-
-// concatenated mode, lane = segment: every live lane re-walks its records from its entry, emitting
-template <int NV, int MODE>
-__device__ __forceinline__ void emit_concat(KParams& dp, const Src& w, uint64_t tlo, uint64_t thi,
-                                            const LDS LaneS<NV>* ls, bool wide, uint64_t rbase,
-                                            const uint64_t* vbase, int lane) {
-  const uint32_t e0 = ls[lane].ent, cnt = ls[lane].cnt;
-  uint64_t run[NV > 0 ? NV : 1];
-  if (wide) {  // >= 4 GiB of payload in this tile: re-measure the lanes for exact 64-bit prefixes
-    uint64_t ex, c, ep, vsum[NV > 0 ? NV : 1];
-    uint32_t ec;
-#pragma unroll
-    for (int v = 0; v < (NV > 0 ? NV : 1); v++) vsum[v] = 0;
-    const uint64_t seg_hi = min(tlo + (uint64_t)lane * SEG + SEG, thi);
-    if (e0 != NOREL && cnt) walk_lane<NV, MODE>(dp, w, tlo + e0, seg_hi, ex, c, ec, ep, vsum);
-#pragma unroll
-    for (int v = 0; v < NV; v++) {
-      const uint64_t x0 = (e0 != NOREL && cnt) ? vsum[v] : 0;
-      run[v] = vbase[v] + wave_incl_scan(x0, lane) - x0;
-    }
-  } else {
-#pragma unroll
-    for (int v = 0; v < NV; v++) run[v] = vbase[v] + ls[lane].vpre[v];
-  }
-  if (e0 == NOREL || cnt == 0) return;
-  uint64_t r = rbase + ls[lane].cpre;
-  uint64_t pos = tlo + e0;
-  for (uint32_t j = 0; j < cnt && r < dp.n; j++, r++) {
-    VarState<NV> vs;
-    uint64_t end = pos, pres = 0;
-    (void)parse_record<NV, MODE>(dp, w, pos, dp.in_len, r, MODE != M_SKIP, &end, vs, pres);
-    if (r >= dp.n) { atomicOr(dp.cols.guard, (unsigned long long)G_ROWS); break; }
-    if (MODE == M_SKIP) dp.skip_out[r] = pos;
-    else if (dp.cols.presence) dp.cols.presence[r] = pres;
-    emit_vars<NV>(dp, w, vs, r, run);
-    if (r == dp.n - 1) finish_ok<NV, MODE>(dp, end, run);
-    pos = end;
-  }
-}
-
-// known-offsets mode, lane = record (<= 64 per tile)
-template <int NV, int MODE>
-__device__ __forceinline__ void emit_offsets(KParams& dp, const Src& w, uint64_t r0, uint64_t r1, const uint64_t* vbase,
-                                             int lane) {
-  const uint64_t r = r0 + lane;
-  const bool act = r < r1;
-  VarState<NV> vs;
-#pragma unroll
-  for (int v = 0; v < NV; v++) { vs.len[v] = 0; vs.pos[v] = 0; }
-  if (act) {
-    const uint64_t pos = dp.offsets[r], lim = dp.offsets[r + 1];
-    uint64_t end = 0, pres = 0;
-    int rc = (pos > lim || lim > dp.in_len) ? KX_ERR_INVALID_ARG : KX_OK;
-    if (!rc) rc = parse_record<NV, MODE>(dp, w, pos, lim, r, MODE != M_SKIP, &end, vs, pres);
-    if (rc) {  // the failed record reads as all defaults, empty payloads
-#pragma unroll
-      for (int v = 0; v < NV; v++) vs.len[v] = 0;
-      pres = 0;
-      if (MODE != M_SKIP) emit_defaults(dp.prog, dp.cols, r);
-      atomicMin(dp.errkey, (unsigned long long)((r << 8) | (uint64_t)(rc & 0xff)));
-    }
-    if (dp.rstat) dp.rstat[r] = (uint8_t)rc;
-    if (MODE == M_SKIP) dp.skip_out[r] = pos;
-    else if (dp.cols.presence) dp.cols.presence[r] = pres;
-  }
-  uint64_t run[NV > 0 ? NV : 1];
-#pragma unroll
-  for (int v = 0; v < NV; v++) {
-    const uint64_t x0 = act ? vs.len[v] : 0;
-    run[v] = vbase[v] + wave_incl_scan(x0, lane) - x0;
-  }
-  if (act) {
-    emit_vars<NV>(dp, w, vs, r, run);
-    if (r == dp.n - 1) finish_ok<NV, MODE>(dp, dp.offsets[dp.n], run);
-  }
-}
-
-// the chain ended in super-tile s before record n (decode error or input exhausted): final status
-template <int NV, int MODE>
-__device__ __forceinline__ void finish_short(KParams& dp, const Comp<NV>& fin, int code, uint64_t offset) {
-  const KAS KxProgram* P = dp.prog;
-  kx_status* st = dp.status;
-  st->code = code;
-  st->record = fin.C;
-  st->offset = offset;
-  st->n_records = fin.C;
-  st->consumed = offset;
-  if (fin.C > dp.n) { atomicOr(dp.cols.guard, (unsigned long long)G_ROWS); return; }
-  if (MODE == M_SKIP) dp.skip_out[fin.C] = offset;
-#pragma unroll
-  for (int v = 0; v < NV; v++) {
-    if (v >= (int)P->nvar) break;
-    st->var_total[v] = fin.V[v];
-    put_total(dp, P->var_col[v], fin.C, fin.V[v]);
-  }
-}
-
-// One step of the super-tile state machine (thread 0; see decode_kernel). Sets sh->fix to the tile
-// to re-walk from sh->fixE (or -1), advances sh->state.
-template <int NV, int MODE>
-__device__ __forceinline__ void st_step(KParams& dp, StShared<NV>* sh, uint64_t s) {
-  const bool known = dp.offsets != nullptr;
-  uint64_t fe = 0;
-  int k;
-  if (sh->fix >= 0 && ++sh->nfix > 4 * WGW) {  // each fold fixes one tile for good: cannot happen
-    atomicCAS((int*)&dp.status->code, 0, KX_ERR_INTERNAL);
-    atomicOr((unsigned long long*)&dp.status->diag[2], (unsigned long long)G_NFIX);
-    sh->fix = -1;
-    sh->state = ST_DONE;
-    Comp<NV> e = sh->agg;
-    e.kind = 2; e.X = X_ERR; e.ec = KX_ERR_INTERNAL;
-    publish<NV>(dp, s, e, true);
-    atomicAdd(dp.progress, 1ull);
-    sh->pre = e;  // nothing is emitted
+  for (int k = 0; k < NW; k++) fields[k] = k < 5 ? k : T_VAR + (k - 5);
+  uint64_t x[NW];
+  if (!get_words<NW>(dp.tdesc, dp.ntiles, fields, NW, act ? t : 0, ep, act, x)) {
+    if (lane == 0) atomicCAS((int*)&dp.status->code, 0, KX_ERR_INTERNAL);
     return;
   }
-  switch (sh->state) {
-    case ST_SPEC:
-      k = st_fold<NV>(dp, sh, s, (s == 0 || known) ? 0ull : X_NONE, sh->agg, &fe);
-      sh->fix = k;
-      sh->fixE = fe;
-      if (k < 0) {
-        publish<NV>(dp, s, sh->agg, false);
-        sh->state = ST_LB;  // wave 0 looks back before the next step
+  uint64_t ent = act ? x[0] : X_NONE, ex = act ? x[1] : X_NONE, cnt = act ? x[2] : 0;
+  uint64_t errc = act ? x[3] : 0, errp = act ? x[4] : 0;
+  uint64_t var[NV > 0 ? NV : 1];
+#pragma unroll
+  for (int v = 0; v < NV; v++) var[v] = act ? x[5 + v] : 0;
+  uint64_t lo, hi;
+  tile_range(dp, act ? t : t0, lo, hi);
+  if (!dp.offsets) {
+    // effective exit of every tile: its own, or (pass-through) the one it inherits
+    for (int guard = 0; guard < 4 * GT + 8; guard++) {
+      const uint64_t hm = __ballot(act && ent != X_NONE);
+      // expected entry of each tile = exit of the nearest lower tile with a record start, else `entry`
+      const uint64_t below = hm & ((1ull << lane) - 1);
+      const int pc = below ? 63 - __clzll((long long)below) : -1;
+      const uint64_t pex = __shfl(ex, pc < 0 ? 0 : pc, 64);
+      const uint64_t E = pc >= 0 ? pex : entry;
+      const bool bad = act && E != X_NONE && !chain_ok(E, ent, hi);
+      const uint64_t bm = __ballot(bad);
+      if (!bm) break;
+      if (!REPAIR) {
+        if (lane == 0) {
+          const uint64_t ng = dp.ngroups;
+          put_word(dp.gdesc, ng, G_EXIT, g, ep, X_NONE);
+          put_word(dp.gdesc, ng, G_CNT, g, ep, 0);
+          put_word(dp.gdesc, ng, G_ERRC, g, ep, 0);
+          put_word(dp.gdesc, ng, G_ERRP, g, ep, 0);
+          for (int v = 0; v < NV; v++) put_word(dp.gdesc, ng, G_VAR + v, g, ep, 0);
+          put_word(dp.gdesc, ng, G_ENT, g, ep, X_BAD);
+        }
+        return;
       }
-      return;
-    case ST_LB: {
-      const Comp<NV>& pre = sh->pre;
-      // the speculative chain stands when it starts at the true entry (always, known offsets)
-      if (known || s == 0 || pre.X == X_ERR || (sh->agg.kind == 2 && sh->agg.S == pre.X)) {
-        sh->fin = sh->agg;
-        break;
+      // re-walk the first disagreeing tile from its true entry
+      const int b = __ffsll((long long)bm) - 1;
+      const uint64_t Eb = rl64(E, b);
+      if (lane == 0) atomicAdd((unsigned long long*)&dp.status->diag[0], 1ull);
+      const Agg a = tile_agg<NV, MODE>(dp, win, t0 + b, Eb, lane);
+      put_tile(dp, t0 + b, a, NV);
+      if (lane == b) {
+        ent = a.ent; ex = a.ex; cnt = a.cnt; errc = a.errc; errp = a.errp;
+#pragma unroll
+        for (int v = 0; v < NV; v++) var[v] = a.var[v];
       }
-      sh->state = ST_TRUE;
     }
-    // fallthrough
-    case ST_TRUE:
-      k = st_fold<NV>(dp, sh, s, sh->pre.X, sh->fin, &fe);
-      sh->fix = k;
-      sh->fixE = fe;
-      if (k >= 0) return;
-      break;
-    default:
-      return;
   }
-  // the ST's true chain is known: publish the inclusive prefix, settle the call's status
-  sh->fix = -1;
-  sh->state = ST_DONE;
-  const Comp<NV> pre = sh->pre;
-  Comp<NV> fin;
-  if (!combine(pre, sh->fin, fin)) {  // cannot happen: sh->fin starts at pre.X
-    atomicCAS((int*)&dp.status->code, 0, KX_ERR_INTERNAL);
-    atomicOr((unsigned long long*)&dp.status->diag[2], (unsigned long long)G_COMBINE);
-    fin = pre;
-    fin.X = X_ERR;
-    fin.ec = KX_ERR_INTERNAL;
+  // the chain stops at the first erroring tile
+  const uint64_t em = __ballot(act && ex == X_ERR);
+  const int fe = em ? __ffsll((long long)em) - 1 : 64;
+  const bool live = act && lane <= fe;
+  const uint64_t c0 = live ? cnt : 0;
+  const uint64_t ci = wave_incl_scan(c0, lane);
+  uint64_t vpre[NV > 0 ? NV : 1], vtot[NV > 0 ? NV : 1];
+#pragma unroll
+  for (int v = 0; v < NV; v++) {
+    const uint64_t x0 = live ? var[v] : 0;
+    const uint64_t vi = wave_incl_scan(x0, lane);
+    vpre[v] = vi - x0;
+    vtot[v] = rl64(vi, 63);
   }
-  publish<NV>(dp, s, fin, true);
-  atomicAdd(dp.progress, 1ull);
-  if (!known && pre.X != X_ERR && pre.C < dp.n) {
-    if (fin.X == X_ERR && fin.C < dp.n) finish_short<NV, MODE>(dp, fin, (int)fin.ec, fin.ep);
-    else if (s == dp.nst - 1 && fin.X != X_ERR && fin.C < dp.n) finish_short<NV, MODE>(dp, fin, KX_ERR_EOF, dp.in_len);
+  if (act) {
+    put_word(dp.tdesc, dp.ntiles, T_PCNT, t, ep, ci - c0);
+#pragma unroll
+    for (int v = 0; v < NV; v++) put_word(dp.tdesc, dp.ntiles, T_PVAR + v, t, ep, vpre[v]);
+  }
+  const uint64_t hm = __ballot(act && ent != X_NONE);
+  const uint64_t gent = hm ? rl64(ent, __ffsll((long long)hm) - 1) : X_NONE;
+  const uint64_t gex = fe < 64 ? X_ERR : hm ? rl64(ex, 63 - __clzll((long long)hm)) : entry;
+  const uint64_t gcnt = rl64(ci, 63);
+  const uint64_t gerrc = fe < 64 ? rl64(errc, fe) : 0;
+  const uint64_t gerrp = fe < 64 ? rl64(errp, fe) : 0;
+  if (lane == 0) {
+    const uint64_t ng = dp.ngroups;
+    put_word(dp.gdesc, ng, G_ENT, g, ep, gent);
+    put_word(dp.gdesc, ng, G_EXIT, g, ep, gex);
+    put_word(dp.gdesc, ng, G_CNT, g, ep, gcnt);
+    put_word(dp.gdesc, ng, G_ERRC, g, ep, gerrc);
+    put_word(dp.gdesc, ng, G_ERRP, g, ep, gerrp);
+#pragma unroll
+    for (int v = 0; v < NV; v++) put_word(dp.gdesc, ng, G_VAR + v, g, ep, vtot[v]);
   }
 }
 
-// ---- the persistent decode kernel ----
-// Super-tiles are claimed in order from one counter (the next claim is issued a whole super-tile
-// ahead of its use), so a look-back only ever waits on super-tiles that running workgroups hold.
-// Per super-tile, a small state machine run by thread 0 between workgroup barriers decides who
-// walks next (every walk of a tile goes through one call site):
-//   SPEC: chain the tiles speculatively, re-walking tiles that disagree inside the ST; publish A
-//   LB:   wave 0 looks back for the true prefix; TRUE: re-chain from the true entry (re-walks out of
-//   LDS where the speculation was wrong); publish P and the final status; then every wave emits.
-// Without var columns in offsets mode nothing is chained: tiles are dealt round-robin, emit only.
-// Everything is inlined: out-of-line calls from divergent code (lane 0 / a subset of lanes) lose
-// inactive lanes' registers on this toolchain.
+// ---- kernel 1: index pass (one wave per tile) ----
 template <int NV, int MODE>
-__global__ void __launch_bounds__(NT, 4) decode_kernel(DecParams dp_) {
+__global__ void __launch_bounds__(NT) index_kernel(DecParams dp_) {
   KParams& dp = KX_PARAMS();
   (void)dp_;
-  __shared__ __attribute__((aligned(16))) uint32_t WIN[WGW][WINW];
-  __shared__ LaneS<NV> LSA[WGW][64];
-  __shared__ StShared<NV> SH;
-  StShared<NV>* sh = &SH;
+  __shared__ __attribute__((aligned(16))) uint32_t WIN[WAVES][WINW];
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
+  const uint64_t t = (uint64_t)blockIdx.x * WAVES + wv;
+  if (t >= dp.ntiles) return;
   LDS uint32_t* win = (LDS uint32_t*)WIN[wv];
-  LDS LaneS<NV>* ls = (LDS LaneS<NV>*)LSA[wv];
-  const bool known = dp.offsets != nullptr;
-  const bool thrift = MODE == M_THRIFT;
-  const uint32_t dsig = known ? 0u : data_sig(dp);
-  if (threadIdx.x == 0) sh->tk = dp.direct ? blockIdx.x : atomicAdd(dp.ticket, 1ull);
+  const uint64_t t_start = (dp.diag & 64) ? __builtin_amdgcn_s_memtime() : 0;
+  Agg a;
+  if (dp.diag & 1) {
+    uint64_t lo, hi;
+    tile_range(dp, t, lo, hi);
+    const Src w = load_window(dp, win, dp.offsets ? dp.offsets[lo] : lo, lane, MODE == M_THRIFT);
+    a.ent = lo + (w.win[lane] & 1); a.ex = hi; a.cnt = 0; a.errc = 0; a.errp = 0;
+    for (int v = 0; v < NV; v++) a.var[v] = 0;
+  } else {
+    a = tile_agg<NV, MODE>(dp, win, t, t == 0 ? 0ull : X_NONE, lane);
+  }
+  if (lane == 0 && !(dp.diag & 4)) put_tile(dp, t, a, NV);
+  if ((dp.diag & 64) && lane == 0) atomicAdd(&g_phase[5], (unsigned long long)(__builtin_amdgcn_s_memtime() - t_start));
+  const uint64_t g = t / GT;
+}
+
+// ---- kernel 1b: group scan (one wave per group of 64 tiles) ----
+template <int NV, int MODE>
+__global__ void __launch_bounds__(NT) group_kernel(DecParams dp_) {
+  KParams& dp = KX_PARAMS();
+  (void)dp_;
+  __shared__ __attribute__((aligned(16))) uint32_t WIN[WAVES][WINW];
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const uint64_t g = (uint64_t)blockIdx.x * WAVES + wv;
+  if (g >= dp.ngroups) return;
+  group_scan<NV, MODE, false>(dp, (LDS uint32_t*)WIN[wv], g, g == 0 && !dp.offsets ? 0ull : X_NONE, lane);
+}
+
+// ---- kernel 2: chain + scan over the groups (one workgroup of 4 waves, lane = group) ----
+// Resolves the group chain from offset 0 (re-scanning a group from its true entry where the
+// speculation disagreed), writes every group's exclusive record / arena base, the number of records
+// to emit, and the final status when the chain ends early (decode error, input exhausted).
+template <int NV, int MODE>
+__global__ void __launch_bounds__(CT) chain_kernel(DecParams dp_) {
+  KParams& dp = KX_PARAMS();
+  (void)dp_;
+  __shared__ __attribute__((aligned(16))) uint32_t WIN0[WINW];
+  __shared__ uint64_t s_wcnt[CW], s_wvar[CW][KXP_NV_MAX], s_wlast[CW];
+  __shared__ int s_werr[CW];
+  __shared__ uint64_t s_E, s_cnt, s_var[KXP_NV_MAX], s_nstop, s_badE;
+  __shared__ int s_bad, s_err, s_done;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const uint64_t ep = dp.epoch, ng = dp.ngroups;
+  const bool chain = !dp.offsets;
+  if (tid == 0) {
+    s_E = 0;  // the chain enters group 0 at offset 0
+    s_cnt = 0;
+    for (int v = 0; v < KXP_NV_MAX; v++) s_var[v] = 0;
+    s_nstop = dp.n;
+    s_err = 0;
+    s_done = 0;
+  }
   __syncthreads();
-  uint32_t it = 0;
-  for (uint64_t s = sh->tk; s < dp.nst; it ^= 1) {
-    if (threadIdx.x == 0 && !dp.direct) sh->tkn[it] = atomicAdd(dp.ticket, 1ull);
-    const uint64_t t = s * WGW + wv;
-    const bool has = t < dp.ntiles;
-    uint64_t lo = 0, hi = 0;
-    if (has) {
-      tile_range(dp, t, lo, hi);
-      load_window(dp, win, tile_pos(dp, lo), lane);
-      if (dp.direct) {
-        uint64_t zero[NV > 0 ? NV : 1];
-#pragma unroll
-        for (int v = 0; v < (NV > 0 ? NV : 1); v++) zero[v] = 0;
-        emit_offsets<NV, MODE>(dp, window_src(dp, win, tile_pos(dp, lo), thrift), lo, hi, zero, lane);
-      } else if (!known) {
-        const uint64_t seg_lo = lo + (uint64_t)lane * SEG;
-        const uint64_t c = lane_candidate<NV, MODE>(dp, window_src(dp, win, lo, thrift), seg_lo,
-                                                    min(seg_lo + SEG, hi), dsig, lane);
-        ls[lane].cand = c == X_NONE ? (uint16_t)NOREL : (uint16_t)(c - lo);
-      }
-    }
-    if (dp.direct) {
-      s += gridDim.x;
+  for (uint64_t b0 = 0; b0 < ng; b0 += CT) {
+    if (s_err || s_done) {  // the chain already ended: later groups emit nothing
+      const uint64_t g = b0 + tid;
+      if (g < ng) put_word(dp.gdesc, ng, G_BCNT, g, ep, X_DONE);
       continue;
     }
-    if (threadIdx.x == 0) { sh->state = ST_SPEC; sh->fix = -1; sh->nfix = 0; }
-    bool walk = has;
-    uint64_t seed = (t == 0 && !known) ? 0ull : X_NONE;
+    const uint64_t g = b0 + tid;
+    const bool act = g < ng;
+    uint64_t gent, gex, cnt, errc, errp, var[NV > 0 ? NV : 1];
+    uint64_t base, vbase[NV > 0 ? NV : 1], c0, vx[NV > 0 ? NV : 1];
+    bool live, dead;
+    int fe;
     for (;;) {
-      if (walk) {
-        const Src w = window_src(dp, win, tile_pos(dp, lo), thrift);
-        const TAgg a = known ? measure_records<NV, MODE>(dp, w, lo, hi, lane)
-                             : walk_tile<NV, MODE>(dp, w, lo, hi, seed, lane, ls);
-        if (lane == 0) sh->ta[wv] = a;
-      } else if (!has && lane == 0) {
-        TAgg a;
-        a.ent = X_NONE; a.ex = X_NONE; a.cnt = 0; a.errc = 0; a.errp = 0; a.wide = 0;
+      constexpr int NW = 5 + NV;
+      int fields[NW];
 #pragma unroll
-        for (int v = 0; v < KXP_NV_MAX; v++) a.var[v] = 0;
-        sh->ta[wv] = a;
+      for (int k = 0; k < NW; k++) fields[k] = k < 5 ? k : G_VAR + (k - 5);
+      uint64_t x[NW];
+      if (!get_words<NW>(dp.gdesc, ng, fields, NW, act ? g : 0, ep, act, x) && lane == 0)
+        atomicCAS((int*)&dp.status->code, 0, KX_ERR_INTERNAL);
+      gent = act ? x[0] : X_NONE; gex = act ? x[1] : X_NONE; cnt = act ? x[2] : 0;
+      errc = act ? x[3] : 0; errp = act ? x[4] : 0;
+#pragma unroll
+      for (int v = 0; v < NV; v++) var[v] = act ? x[5 + v] : 0;
+      // the chain stops at the first erroring group
+      const uint64_t em = __ballot(act && chain && gex == X_ERR);
+      fe = em ? __ffsll((long long)em) - 1 : 64;
+      live = act && lane <= fe;
+      c0 = live ? cnt : 0;
+      const uint64_t ci = wave_incl_scan(c0, lane);
+#pragma unroll
+      for (int v = 0; v < NV; v++) {
+        const uint64_t x0 = live ? var[v] : 0;
+        const uint64_t vi = wave_incl_scan(x0, lane);
+        vx[v] = vi - x0;
+        if (lane == 63) s_wvar[wv][v] = vi;
+      }
+      const uint64_t hm = __ballot(act && gent != X_NONE && gent != X_BAD);
+      if (lane == 63) s_wcnt[wv] = ci;
+      const uint64_t wlast = hm ? rl64(gex, 63 - __clzll((long long)hm)) : X_NONE;
+      if (lane == 0) {
+        s_wlast[wv] = wlast;
+        s_werr[wv] = em != 0;
+      }
+      if (tid == 0) s_bad = 1 << 30;
+      __syncthreads();
+      base = s_cnt + ci - c0;
+      dead = false;
+#pragma unroll
+      for (int v = 0; v < NV; v++) vbase[v] = s_var[v] + vx[v];
+      uint64_t Ein = s_E;
+      for (int k = 0; k < wv; k++) {
+        base += s_wcnt[k];
+#pragma unroll
+        for (int v = 0; v < NV; v++) vbase[v] += s_wvar[k][v];
+        dead |= s_werr[k] != 0;
+        if (s_wlast[k] != X_NONE) Ein = s_wlast[k];
+      }
+      if (!chain) break;
+      // expected entry = effective exit of the nearest lower group with a record start
+      const uint64_t below = hm & ((1ull << lane) - 1);
+      const int pc = below ? 63 - __clzll((long long)below) : -1;
+      const uint64_t pex = __shfl(gex, pc < 0 ? 0 : pc, 64);
+      const uint64_t E = pc >= 0 ? pex : Ein;
+      const uint64_t hi = kmin64((g + 1) * (uint64_t)GT * TILE, dp.in_len);
+      const bool bad = live && !dead && base < dp.n && !chain_ok(E, gent, hi);
+      if (bad) atomicMin(&s_bad, tid);
+      __syncthreads();
+      const int b = s_bad;
+      if (b == (1 << 30)) break;
+      if (tid == b) s_badE = E;
+      __syncthreads();
+      if (wv == 0) {  // re-scan the first disagreeing group from its true entry, then re-check
+        if (lane == 0) atomicAdd((unsigned long long*)&dp.status->diag[1], 1ull);
+        group_scan<NV, MODE, true>(dp, (LDS uint32_t*)WIN0, b0 + b, s_badE, lane);
       }
       __syncthreads();
-      if (wv == 0 && __shfl(sh->state, 0, 64) == ST_LB) {  // lane 0's read: it runs st_step next
-        const Comp<NV> pre = lookback<NV>(dp, s, lane);
-        if (lane == 0) sh->pre = pre;
-      }
-      if (threadIdx.x == 0) st_step<NV, MODE>(dp, sh, s);
-      __syncthreads();
-      const int k = sh->fix;
-      if (sh->state == ST_DONE) break;
-      walk = k == wv;
-      if (walk) {
-        seed = sh->fixE;
-        if (lane == 0) atomicAdd((unsigned long long*)&dp.status->diag[0], 1ull);
-      }
     }
-    // emit this wave's tile
-    if (has && sh->on[wv] && sh->pre.X != X_ERR) {
-      const uint64_t rbase = sh->pre.C + sh->tbc[wv];
-      uint64_t vbase[NV > 0 ? NV : 1];
+    if (act) {
+      put_word(dp.gdesc, ng, G_BCNT, g, ep, (dead || !live) ? X_DONE : base);
 #pragma unroll
-      for (int v = 0; v < NV; v++) vbase[v] = sh->pre.V[v] + sh->tbv[wv][v];
-      const Src w = window_src(dp, win, tile_pos(dp, lo), thrift);
-      if (known) emit_offsets<NV, MODE>(dp, w, lo, hi, vbase, lane);
-      else if (rbase < dp.n) emit_concat<NV, MODE>(dp, w, lo, hi, ls, sh->ta[wv].wide != 0, rbase, vbase, lane);
+      for (int v = 0; v < NV; v++) put_word(dp.gdesc, ng, G_BVAR + v, g, ep, vbase[v]);
+    }
+    // a decode error ends the chain (reported only when it falls before record n)
+    if (chain && !dead && fe < 64 && lane == fe) {
+      const uint64_t rec = base + cnt;  // records decoded before the failing one
+      if (rec < dp.n) {
+        kx_status* st = dp.status;
+        st->code = (int32_t)errc; st->record = rec; st->offset = errp;
+        st->n_records = rec; st->consumed = errp;
+#pragma unroll
+        for (int v = 0; v < NV; v++) {
+          if (v >= (int)dp.prog->nvar) break;
+          const uint64_t vt = vbase[v] + var[v];
+          st->var_total[v] = vt;
+          put_total(dp.cols, dp.overflow, dp.prog->var_col[v], rec, vt);
+        }
+        if (MODE == M_SKIP) dp.skip_out[rec] = errp;
+        s_nstop = rec;
+      }
+      s_err = 1;
     }
     __syncthreads();
-    s = sh->tkn[it];
+    if (tid == 0) {  // carry into the next batch
+      bool stop = false;
+      for (int k = 0; k < CW && !stop; k++) {
+        s_cnt += s_wcnt[k];
+        for (int v = 0; v < NV; v++) s_var[v] += s_wvar[k][v];
+        if (s_wlast[k] != X_NONE) s_E = s_wlast[k];
+        stop = s_werr[k] != 0;
+      }
+      if (s_cnt >= dp.n) s_done = 1;
+    }
+    __syncthreads();
+  }
+  // the chain ran out of input before n records: EOF at the record after the last one
+  if (tid == 0) {
+    const uint64_t tot = s_cnt;
+    if (chain && !s_err && tot < dp.n) {
+      kx_status* st = dp.status;
+      st->code = KX_ERR_EOF; st->record = tot; st->offset = dp.in_len;
+      st->n_records = tot; st->consumed = dp.in_len;
+      for (int v = 0; v < NV; v++) {
+        if (v >= (int)dp.prog->nvar) break;
+        st->var_total[v] = s_var[v];
+        put_total(dp.cols, dp.overflow, dp.prog->var_col[v], tot, s_var[v]);
+      }
+      if (MODE == M_SKIP) dp.skip_out[tot] = dp.in_len;
+      s_nstop = tot;
+    }
+    *dp.nstop = s_nstop;
   }
 }
 
-// Completes a call and re-arms the workspace for the next one (error key, overflow).
-__global__ void finalize_kernel(kx_status* st, unsigned long long* errkey, uint32_t* overflow, uint32_t* abort,
-                                unsigned long long* ticket, const uint64_t* offsets, uint64_t n) {
-  unsigned long long* progress = ticket + 1;
+// ---- kernel 3: emit pass (one wave per tile, lane = record) ----
+template <int NV, int MODE>
+__global__ void __launch_bounds__(NT) emit_kernel(DecParams dp_) {
+  KParams& dp = KX_PARAMS();
+  (void)dp_;
+  __shared__ __attribute__((aligned(16))) uint32_t WIN[WAVES][WINW];
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const uint64_t t = (uint64_t)blockIdx.x * WAVES + wv;
+  if (t >= dp.ntiles) return;
+  const KAS KxProgram* P = dp.prog;
+  const bool known = dp.offsets != nullptr;
+  const uint64_t nstop = known ? dp.n : *(volatile uint64_t*)dp.nstop;
+  uint64_t lo, hi;
+  tile_range(dp, t, lo, hi);
+  // the window DMA is issued first; the tile's bases are read while it is in flight
+  LDS uint32_t* win = (LDS uint32_t*)WIN[wv];
+  const uint16_t* starts = dp.starts + t * dp.slotcap;
+  const Src w = load_window(dp, win, known ? dp.offsets[lo] : lo, lane, MODE == M_THRIFT, false);
+  uint64_t base = 0, cnt = 0, run[NV > 0 ? NV : 1];
+#pragma unroll
+  for (int v = 0; v < (NV > 0 ? NV : 1); v++) run[v] = 0;
+  if (dp.direct) {  // offsets mode without var columns: no index pass
+    base = lo;
+    cnt = hi - lo;
+  } else {
+    const uint64_t g = t / GT;
+    // written by earlier kernels of this call: plain (cached) loads suffice
+    const uint64_t* gd = dp.gdesc;
+    const uint64_t* td = dp.tdesc;
+    const uint64_t gb = gd[(uint64_t)G_BCNT * dp.ngroups + g] & V48;
+    base = gb + (td[(uint64_t)T_PCNT * dp.ntiles + t] & V48);
+    cnt = gb == X_DONE ? 0 : td[(uint64_t)T_CNT * dp.ntiles + t] & V48;
+#pragma unroll
+    for (int v = 0; v < NV; v++)
+      run[v] = (gd[(uint64_t)(G_BVAR + v) * dp.ngroups + g] & V48) + (td[(uint64_t)(T_PVAR + v) * dp.ntiles + t] & V48);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (cnt == 0 || base >= nstop) return;
+  cnt = kmin64(cnt, nstop - base);
+  for (uint64_t j0 = 0; j0 < cnt; j0 += 64) {
+    const uint64_t j = j0 + lane;
+    const bool act = j < cnt;
+    const uint64_t r = base + j;
+    VarState<NV> vs;
+#pragma unroll
+    for (int v = 0; v < NV; v++) { vs.len[v] = 0; vs.pos[v] = 0; }
+    uint64_t pos = 0, lim = dp.in_len, end = 0, pres = 0;
+    int rc = 0;
+    if (act) {
+      if (known) {
+        pos = dp.offsets[r];
+        lim = dp.offsets[r + 1];
+        if (pos > lim || lim > dp.in_len) rc = KX_ERR_INVALID_ARG;
+      } else {
+        pos = lo + starts[j];
+      }
+      if (!rc) rc = parse_record<NV, MODE>(dp, w, pos, lim, r, MODE != M_SKIP, &end, vs, pres);
+      if (rc) {  // offsets mode: the failed record reads as all defaults, empty payloads
+#pragma unroll
+        for (int v = 0; v < NV; v++) vs.len[v] = 0;
+        pres = 0;
+        if (MODE != M_SKIP) emit_defaults(P, dp.cols, r);
+      }
+      if (MODE == M_SKIP) dp.skip_out[r] = pos;
+      if (MODE != M_SKIP && dp.cols.presence) dp.cols.presence[r] = pres;
+      if (known) {
+        if (rc) atomicMin(dp.errkey, (unsigned long long)((r << 8) | (uint64_t)(rc & 0xff)));
+        if (dp.rstat) dp.rstat[r] = (uint8_t)rc;
+      }
+    }
+    // arena positions: wave exclusive scan of the var lengths
+#pragma unroll
+    for (int v = 0; v < NV; v++) {
+      if (v >= (int)P->nvar) break;
+      const uint64_t x0 = act ? vs.len[v] : 0;
+      const uint64_t xi = wave_incl_scan(x0, lane);
+      const uint64_t at = run[v] + xi - x0;
+      const uint32_t cc = P->var_col[v];
+      if (act) {
+        const uint32_t nn = vs.len[v];
+        if (at + nn <= arena_lim(dp.cols, cc)) {
+          put_off(dp.cols, cc, r, at);
+          if (nn) {
+            const KxpCol K = ld_col(P, cc);
+            copy_var(w, K, vs.pos[v], nn, (uint8_t*)dp.cols.data[cc] + at * K.width);
+          }
+        } else {
+          atomicOr(dp.overflow, 1u);
+        }
+      }
+      if (act && r == nstop - 1 && nstop == dp.n) {
+        dp.status->var_total[v] = at + vs.len[v];
+        put_total(dp.cols, dp.overflow, cc, dp.n, at + vs.len[v]);
+      }
+      run[v] += rl64(xi, 63);
+    }
+    if (act && r == nstop - 1 && nstop == dp.n) {
+      kx_status* st = dp.status;
+      st->n_records = dp.n;
+      st->consumed = known ? dp.offsets[dp.n] : end;
+      if (MODE == M_SKIP) dp.skip_out[dp.n] = end;
+    }
+  }
+}
+
+// Completes a call and re-arms the workspace for the next one (error key, overflow, nstop).
+__global__ void finalize_kernel(kx_status* st, unsigned long long* errkey, uint32_t* overflow, uint64_t* nstop,
+                                const uint64_t* offsets, uint64_t n) {
   if (threadIdx.x != 0) return;
   unsigned long long k = *errkey;
   if (k != ~0ull && st->code == 0) {
@@ -1905,18 +1741,16 @@ __global__ void finalize_kernel(kx_status* st, unsigned long long* errkey, uint3
   if (offsets) st->n_records = n;
   *errkey = ~0ull;
   *overflow = 0;
-  *abort = 0;
-  *ticket = 0;
-  *progress = 0;
+  *nstop = ~0ull;
 }
 
-// ---- workspace: [8] errkey u64, [16] overflow u32, [32] abort u32, [40] ticket u64, [48] progress
-//      u64, then the super-tile words ----
+// ---- workspace: [8] errkey u64, [16] overflow u32, [24] nstop u64, then tile words, group words,
+//      record-start slots ----
 constexpr size_t WS_HDR = 256;
 
 struct WsLayout {
-  uint64_t ntiles, nst;
-  size_t sdesc, total;
+  uint64_t ntiles, ngroups, slotcap;
+  size_t tdesc, gdesc, starts, total;
 };
 
 uint32_t krec_for(uint64_t in_len, uint64_t n) {
@@ -1926,37 +1760,28 @@ uint32_t krec_for(uint64_t in_len, uint64_t n) {
   return (uint32_t)(k < 1 ? 1 : k > 64 ? 64 : k);
 }
 
-WsLayout ws_layout(uint64_t in_len, const uint64_t* offsets, uint64_t n) {
+WsLayout ws_layout(uint64_t min_rec, uint64_t in_len, const uint64_t* offsets, uint64_t n) {
   WsLayout L{};
   if (offsets) {
     const uint64_t k = krec_for(in_len, n);
     L.ntiles = (n + k - 1) / k;
+    L.slotcap = 0;
   } else {
     L.ntiles = (in_len + TILE - 1) / TILE;
+    // a record can be a single STOP byte whatever the schema's encoded minimum: every byte of
+    // the tile may start one
+    (void)min_rec;
+    L.slotcap = (uint64_t)TILE + 1;
   }
   if (!L.ntiles) L.ntiles = 1;
-  L.nst = (L.ntiles + WGW - 1) / WGW;
-  L.sdesc = WS_HDR;
-  L.total = WS_HDR + (size_t)L.nst * S_NF * 8;
+  L.slotcap = (L.slotcap + 3) & ~3ull;
+  L.ngroups = (L.ntiles + GT - 1) / GT;
+  size_t o = WS_HDR;
+  L.tdesc = o; o += (size_t)L.ntiles * T_NF * 8;
+  L.gdesc = o; o += (size_t)L.ngroups * G_NF * 8;
+  L.starts = o; o += ((size_t)L.ntiles * L.slotcap * 2 + 255) & ~(size_t)255;
+  L.total = o;
   return L;
-}
-
-// workgroups of this kernel that are resident at once on device `dev` (the persistent grid: every
-// workgroup of it must be co-resident, since a super-tile's look-back waits on earlier ones)
-template <int NV, int MODE>
-unsigned resident_grid() {
-  static int cache[64] = {0};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
-  if (!cache[dev]) {
-    int per_cu = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, decode_kernel<NV, MODE>, NT, 0) != hipSuccess ||
-        per_cu < 1)
-      per_cu = 1;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 1;
-    cache[dev] = per_cu * cus;
-  }
-  return (unsigned)cache[dev];
 }
 
 template <int NV, int MODE>
@@ -1965,52 +1790,118 @@ int launch_t(const DecParams& dp0, const WsLayout& L, void* ws, hipStream_t stre
   char* base = (char*)ws;
   dp.errkey = (unsigned long long*)(base + 8);
   dp.overflow = (uint32_t*)(base + 16);
-  dp.abort = (uint32_t*)(base + 32);
-  dp.ticket = (unsigned long long*)(base + 40);
-  dp.progress = (unsigned long long*)(base + 48);
-  dp.sdesc = (uint64_t*)(base + L.sdesc);
+  dp.nstop = (uint64_t*)(base + 24);
+  dp.tdesc = (uint64_t*)(base + L.tdesc);
+  dp.gdesc = (uint64_t*)(base + L.gdesc);
+  dp.starts = (uint16_t*)(base + L.starts);
   dp.ntiles = L.ntiles;
-  dp.nst = L.nst;
+  dp.ngroups = L.ngroups;
+  dp.slotcap = L.slotcap;
   dp.direct = dp.offsets && NV == 0;
   KX_HIP_CHECK(hipMemsetAsync(dp.status, 0, sizeof(kx_status), stream));
-  static int grid_cap = -1;  // diagnostics: KX_GRID caps the persistent grid
-  if (grid_cap < 0) { const char* e = getenv("KX_GRID"); grid_cap = e ? atoi(e) : 0; }
-  uint64_t g = min((uint64_t)resident_grid<NV, MODE>(), dp.nst);
-  if (grid_cap > 0) g = min(g, (uint64_t)grid_cap);
-  hipLaunchKernelGGL((decode_kernel<NV, MODE>), dim3((unsigned)g), dim3(NT), 0, stream, dp);
+  const unsigned grid = (unsigned)((dp.ntiles + WAVES - 1) / WAVES);
+  const unsigned ggrid = (unsigned)((dp.ngroups + WAVES - 1) / WAVES);
+  if (dp.diag & 256) {
+    hipLaunchKernelGGL((index_kernel<NV, MODE>), dim3(grid), dim3(NT), 0, stream, dp);
+    return KX_OK;
+  }
+  if (!dp.direct) {
+    hipLaunchKernelGGL((index_kernel<NV, MODE>), dim3(grid), dim3(NT), 0, stream, dp);
+    KX_HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL((group_kernel<NV, MODE>), dim3(ggrid), dim3(NT), 0, stream, dp);
+    KX_HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL((chain_kernel<NV, MODE>), dim3(1), dim3(CT), 0, stream, dp);
+    KX_HIP_CHECK(hipGetLastError());
+  }
+  hipLaunchKernelGGL((emit_kernel<NV, MODE>), dim3(grid), dim3(NT), 0, stream, dp);
   KX_HIP_CHECK(hipGetLastError());
-  hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(64), 0, stream, dp.status, dp.errkey, dp.overflow, dp.abort,
-                     dp.ticket, dp.offsets, dp.n);
+  hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(64), 0, stream, dp.status, dp.errkey, dp.overflow, dp.nstop,
+                     dp.offsets, dp.n);
   KX_HIP_CHECK(hipGetLastError());
   return KX_OK;
 }
 
-template <int MODE>
-int launch_nv(const DecParams& dp, const WsLayout& L, void* ws, hipStream_t stream, uint32_t nvar) {
-  switch (nvar) {
-    case 0: return launch_t<0, MODE>(dp, L, ws, stream);
-    case 1: return launch_t<1, MODE>(dp, L, ws, stream);
-    case 2: return launch_t<2, MODE>(dp, L, ws, stream);
-    case 3: case 4: return launch_t<4, MODE>(dp, L, ws, stream);
-    default: return launch_t<8, MODE>(dp, L, ws, stream);
-  }
-}
-
 void fill_diag_flags(DecParams& dp) {
-  static int nolds = -1;
+  static int nolds = -1, diag = -1;
   if (nolds < 0) { const char* e = getenv("KX_NOLDS"); nolds = e && e[0] == '1'; }
+  if (diag < 0) { const char* e = getenv("KX_DIAG"); diag = e ? atoi(e) : 0; }
   dp.nolds = nolds;
-  dp.diag = 0;
+  dp.diag = diag;
 }
 
 }  // namespace
 
-size_t kx_decode_ws_bytes(const KxProgram& hprog, uint64_t in_len, const uint64_t* offsets, uint64_t n) {
-  (void)hprog;
-  return ws_layout(in_len, offsets, n).total;
+// Split compilation: build.py compiles this file once per part (-DKX_DEC_PART=k, k = 0..5); each
+// part instantiates its share of the decode kernels, part 0 also holds the host entry points.
+// Without KX_DEC_PART (one translation unit: the emulator build) everything is instantiated here.
+#ifndef KX_DEC_PART
+#define KX_DEC_PART -1
+#endif
+#define KX_OWNS(p) (KX_DEC_PART < 0 || KX_DEC_PART == (p))
+
+template <int NV, int MODE>
+int kx_dec_launch(const void* dp, const void* L, void* ws, hipStream_t stream) {
+  return launch_t<NV, MODE>(*(const DecParams*)dp, *(const WsLayout*)L, ws, stream);
+}
+#define KX_DEF(NV, MODE) template int kx_dec_launch<NV, MODE>(const void*, const void*, void*, hipStream_t);
+#define KX_EXT(NV, MODE) extern template int kx_dec_launch<NV, MODE>(const void*, const void*, void*, hipStream_t);
+#if KX_OWNS(0)
+KX_DEF(0, M_THRIFT) KX_DEF(1, M_THRIFT)
+#else
+KX_EXT(0, M_THRIFT) KX_EXT(1, M_THRIFT)
+#endif
+#if KX_OWNS(1)
+KX_DEF(2, M_THRIFT) KX_DEF(0, M_SKIP)
+#else
+KX_EXT(2, M_THRIFT) KX_EXT(0, M_SKIP)
+#endif
+#if KX_OWNS(2)
+KX_DEF(4, M_THRIFT)
+#else
+KX_EXT(4, M_THRIFT)
+#endif
+#if KX_OWNS(3)
+KX_DEF(8, M_THRIFT)
+#else
+KX_EXT(8, M_THRIFT)
+#endif
+#if KX_OWNS(4)
+KX_DEF(0, M_PB) KX_DEF(1, M_PB) KX_DEF(2, M_PB)
+#else
+KX_EXT(0, M_PB) KX_EXT(1, M_PB) KX_EXT(2, M_PB)
+#endif
+#if KX_OWNS(5)
+KX_DEF(4, M_PB) KX_DEF(8, M_PB)
+#else
+KX_EXT(4, M_PB) KX_EXT(8, M_PB)
+#endif
+
+#if KX_DEC_PART <= 0
+template <int MODE>
+static int launch_nv(const DecParams& dp, const WsLayout& L, void* ws, hipStream_t stream, uint32_t nvar) {
+  switch (nvar) {
+    case 0: return kx_dec_launch<0, MODE>(&dp, &L, ws, stream);
+    case 1: return kx_dec_launch<1, MODE>(&dp, &L, ws, stream);
+    case 2: return kx_dec_launch<2, MODE>(&dp, &L, ws, stream);
+    case 3: case 4: return kx_dec_launch<4, MODE>(&dp, &L, ws, stream);
+    default: return kx_dec_launch<8, MODE>(&dp, &L, ws, stream);
+  }
 }
 
-size_t kx_skip_ws_bytes(uint64_t in_len) { return ws_layout(in_len, nullptr, 0).total; }
+size_t kx_decode_ws_bytes(const KxProgram& hprog, uint64_t in_len, const uint64_t* offsets, uint64_t n) {
+  return ws_layout(hprog.fixed_min, in_len, offsets, n).total;
+}
+
+// diagnostics (not part of the public ABI): read and reset the phase-timing accumulators
+extern "C" int kx_debug_phase_cycles(unsigned long long* out, int n) {
+  if (n > 8) n = 8;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase), sizeof(unsigned long long) * n) != hipSuccess) return KX_ERR_HIP;
+  unsigned long long z[8] = {0};
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_phase), z, sizeof z) != hipSuccess) return KX_ERR_HIP;
+  return KX_OK;
+}
+
+size_t kx_skip_ws_bytes(uint64_t in_len) { return ws_layout(1, in_len, nullptr, 0).total; }
 
 int kx_launch_decode(const KxProgram* dprog, const KxProgram& hprog, const uint8_t* in, uint64_t in_len,
                      const uint64_t* offsets, uint64_t n, const KxLaunchCols& cols, uint8_t* record_status,
@@ -2019,10 +1910,8 @@ int kx_launch_decode(const KxProgram* dprog, const KxProgram& hprog, const uint8
   fill_diag_flags(dp);
   dp.in = in; dp.in_len = in_len; dp.offsets = offsets; dp.n = n; dp.prog = (const KAS KxProgram*)dprog;
   dp.cols = cols; dp.rstat = record_status; dp.status = status; dp.epoch = epoch;
-  dp.cols.nrec = n;
-  dp.cols.guard = (unsigned long long*)&status->diag[2];
   dp.krec = krec_for(in_len, n);
-  const WsLayout L = ws_layout(in_len, offsets, n);
+  const WsLayout L = ws_layout(hprog.fixed_min, in_len, offsets, n);
   if (ws_size < L.total) return KX_ERR_INVALID_ARG;
   return pb ? launch_nv<M_PB>(dp, L, ws, stream, hprog.nvar) : launch_nv<M_THRIFT>(dp, L, ws, stream, hprog.nvar);
 }
@@ -2033,10 +1922,9 @@ int kx_launch_skip(const uint8_t* in, uint64_t in_len, uint64_t n, uint64_t* off
   fill_diag_flags(dp);
   dp.in = in; dp.in_len = in_len; dp.offsets = nullptr; dp.n = n; dp.prog = nullptr;
   dp.status = status; dp.skip_out = offsets_out; dp.epoch = epoch;
-  dp.cols.nrec = n;
-  dp.cols.guard = (unsigned long long*)&status->diag[2];
   dp.krec = 64;
-  const WsLayout L = ws_layout(in_len, nullptr, n);
+  const WsLayout L = ws_layout(1, in_len, nullptr, n);
   if (ws_size < L.total) return KX_ERR_INVALID_ARG;
-  return launch_t<0, M_SKIP>(dp, L, ws, stream);
+  return kx_dec_launch<0, M_SKIP>(&dp, &L, ws, stream);
 }
+#endif  // KX_DEC_PART <= 0

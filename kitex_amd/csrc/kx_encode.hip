@@ -332,7 +332,7 @@ __global__ void __launch_bounds__(1024) scan_kernel(EncParams ep) {
   __shared__ uint64_t scratch[16];
   uint64_t nb = ep.nblocks;
   uint64_t per = (nb + 1023) / 1024;
-  uint64_t lo = threadIdx.x * per, hi = min(lo + per, nb);
+  uint64_t lo = threadIdx.x * per, hi = kmin64(lo + per, nb);
   uint64_t s = 0;
   for (uint64_t i = lo; i < hi; i++) s += ep.block_tot[i];
   uint64_t tot;
@@ -363,7 +363,7 @@ __global__ void __launch_bounds__(NT) write_kernel(EncParams ep) {
   const KxProgram& P = *reinterpret_cast<const KxProgram*>(progw);
   const uint64_t b = blockIdx.x;
   uint64_t r = b * RB;
-  const uint64_t rend = min(r + RB, ep.n);
+  const uint64_t rend = kmin64(r + RB, ep.n);
   uint64_t gpos = ep.block_tot[b];
   while (r < rend) {
     uint64_t my = r + threadIdx.x;

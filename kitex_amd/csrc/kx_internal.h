@@ -8,6 +8,10 @@
 #include "../../include/kxcodec.h"
 #include "kx_program.h"
 
+// 64-bit min/max (HIP's min()/max() on mixed unsigned long / unsigned long long picks a double overload)
+__host__ __device__ __forceinline__ uint64_t kmin64(uint64_t a, uint64_t b) { return a < b ? a : b; }
+__host__ __device__ __forceinline__ uint64_t kmax64(uint64_t a, uint64_t b) { return a > b ? a : b; }
+
 struct kx_schema {
   KxProgram prog;                      // host copy of the compiled schema
   kx_column_info info[KX_MAX_COLUMNS];

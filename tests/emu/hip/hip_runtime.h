@@ -129,6 +129,19 @@ inline void emu_wait_vmcnt0() {  // the DMA of every lane of the wave has landed
 inline void __builtin_amdgcn_global_load_lds(const void* src, void* dst, unsigned size, int, int) {
   memcpy((char*)dst + (size_t)emu_lane() * size, src, size);
 }
+struct emu_rsrc {
+  const char* base;
+  int32_t n;
+};
+typedef emu_rsrc __amdgpu_buffer_rsrc_t;
+inline emu_rsrc __builtin_amdgcn_make_buffer_rsrc(void* p, short, int32_t n, int32_t) { return emu_rsrc{(const char*)p, n}; }
+inline void __builtin_amdgcn_raw_ptr_buffer_load_lds(emu_rsrc r, void* dst, unsigned size, int voff, int soff, int off,
+                                                     int) {
+  // the range check turns a chunk past num_records into zeros: the LDS slot is still written
+  const int64_t o = (int64_t)voff + soff + off;
+  if (o + (int64_t)size <= r.n) memcpy((char*)dst + (size_t)emu_lane() * size, r.base + o, size);
+  else memset((char*)dst + (size_t)emu_lane() * size, 0, size);
+}
 inline int __ffsll(long long x) { return __builtin_ffsll(x); }
 inline int __clzll(long long x) { return x ? __builtin_clzll((unsigned long long)x) : 64; }
 
@@ -166,6 +179,12 @@ struct EmuThunk {
     emu_launch(dim3(grid).x, dim3(block).x, &EmuThunk<decltype(emu_fn_)>::run, &emu_th_); \
   } while (0)
 inline hipError_t hipGetLastError() { return hipSuccess; }
+enum hipMemcpyKind { hipMemcpyHostToDevice = 1, hipMemcpyDeviceToHost = 2, hipMemcpyDeviceToDevice = 3 };
+inline hipError_t hipMemcpyAsync(void* d, const void* s, size_t n, hipMemcpyKind, hipStream_t) {
+  memcpy(d, s, n);
+  return hipSuccess;
+}
+inline hipError_t hipStreamSynchronize(hipStream_t) { return hipSuccess; }
 inline hipError_t hipMemsetAsync(void* p, int v, size_t n, hipStream_t) {
   memset(p, v, n);
   return hipSuccess;
