@@ -8,13 +8,18 @@ encoded by the GPU encoder before the timed region; the decoded columns are chec
 generator's columns after it.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--records R] [--mode concat|offsets]
-                  [--config r2|r1|r3]
+                  [--config r2|r1|r3|pf|c5] [--no-extra] [--no-cpu] [--no-host]
 
 N > 1: launched by torch.distributed.run, one rank per GPU, each rank decodes its own 16M-record
 shard (weak scaling, no collective in the data path); value = all records / max time.
-Prints ONE JSON line on rank 0.
+--config c5 (BASELINE config 5): 112M R2 + 16M R3 records in total, record-range shards over the
+ranks (strong scaling); a step decodes both of a rank's batches; the decoded shards are then
+concatenated into rank 0 over RCCL (reported as "concat", outside `value`).
+At N = 1 the line also carries "extra": R3 decode + encode (config 3), PF decode (config 4) and R2
+encode, each timed the same way. Prints ONE JSON line on rank 0.
 """
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -24,10 +29,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-
-# algorithmic bytes per record: wire bytes in + decoded column bytes out
-WIRE_BYTES = {"r1": 89, "r2": 167}
-OUT_BYTES = {"r1": 64, "r2": 8 * 8 + 2 * (4 + 32)}
+C5_R2, C5_R3 = 112 << 20, 16 << 20   # config 5 record totals
 
 
 def parse():
@@ -36,25 +38,158 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--records", type=int, default=16 * 1024 * 1024)
-    ap.add_argument("--config", default="r2", choices=["r1", "r2", "r3", "pf"])
+    ap.add_argument("--config", default="r2", choices=["r1", "r2", "r3", "pf", "c5"])
     ap.add_argument("--mode", default="concat", choices=["concat", "offsets"])
+    ap.add_argument("--c5-scale", type=float, default=1.0, help="c5: fraction of the 112M + 16M records")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-host", action="store_true")
+    ap.add_argument("--no-extra", action="store_true")
     ap.add_argument("--no-concat", action="store_true", help="N>1: skip the RCCL concatenation into rank 0")
     ap.add_argument("--cpu-records", type=int, default=4 * 1024 * 1024)
     return ap.parse_args()
+
+
+def last_offset(off) -> int:
+    """the last entry of an offset column (4-byte columns hold uint32 values in int32)"""
+    import torch
+    v = int(off[-1].item())
+    return v & 0xFFFFFFFF if off.dtype == torch.int32 else v
+
+
+def same_offsets(a, b) -> bool:
+    import torch
+    u = (lambda t: t.to(torch.int64) & 0xFFFFFFFF if t.dtype == torch.int32 else t.to(torch.int64))
+    return bool(torch.equal(u(a), u(b)))
+
+
+class Batch:
+    """One same-schema batch resident in HBM: source columns, GPU-encoded wire, decode outputs."""
+
+    def __init__(self, cfg, n, dev, start, mode, local):
+        import torch
+
+        from kitex_amd import _abi as A
+        from kitex_amd import schema as S
+        from kitex_amd import synth
+        from kitex_amd.codec import ProtobufCodec, ThriftCodec, status_tensor
+        from kitex_amd.columns import alloc_device
+        self.cfg, self.n, self.mode = cfg, n, mode
+        sch = S.SCHEMAS[cfg]()
+        self.cdc = ProtobufCodec(sch, device=local) if cfg == "pf" else ThriftCodec(sch, device=local)
+        self.infos = infos = self.cdc.dschema.infos
+        self.src = synth.TORCH_GENERATORS[cfg](n, dev, start=start)
+        self.wire, self.offs = self.cdc.Marshal(self.src, with_offsets=True)
+        torch.cuda.synchronize()
+        self.in_bytes = self.wire.numel()
+        self.var_caps = [0 if ci.kind == A.COL_FIXED else last_offset(self.src.cols[c][0])
+                         for c, ci in enumerate(infos)]
+        wide = any(v >= (1 << 32) for v in self.var_caps)
+        self.out = alloc_device(infos, n, self.var_caps, self.cdc.dschema.npresence, dev, wide=wide)
+        self.offsets = self.offs if mode == "offsets" else None
+        self.st = status_tensor(dev)
+
+    def step(self, stream=None):
+        return self.cdc.Unmarshal(self.wire, self.n, offsets=self.offsets, out=self.out, var_caps=self.var_caps,
+                                  raise_on_error=False, status=self.st, stream=stream)
+
+    def status(self):
+        from kitex_amd.codec import read_status
+        return read_status(self.st)
+
+    def verify(self) -> bool:
+        import torch
+
+        from kitex_amd import _abi as A
+        st = self.status()
+        ok = st.code == 0 and st.n_records == self.n and (self.mode == "offsets" or st.consumed == self.in_bytes)
+        for c, ci in enumerate(self.infos):
+            if ci.kind == A.COL_FIXED:
+                ok &= bool(torch.equal(self.out.cols[c], self.src.cols[c]))
+            else:
+                ok &= same_offsets(self.out.cols[c][0], self.src.cols[c][0])
+                tot = self.var_caps[c]
+                ok &= bool(torch.equal(self.out.cols[c][1][:tot], self.src.cols[c][1][:tot]))
+        if self.src.presence is not None:
+            ok &= bool(torch.equal(self.out.presence[:self.n], self.src.presence[:self.n]))
+        return ok
+
+    def out_bytes_per_record(self) -> float:
+        from kitex_amd import _abi as A
+        n = self.n
+        return (sum((ci.width if ci.kind == A.COL_FIXED else 4) for ci in self.infos)
+                + sum(self.var_caps[c] * (ci.width if ci.kind == A.COL_LIST else 1) / n
+                      for c, ci in enumerate(self.infos) if ci.kind != A.COL_FIXED)
+                + (8 if self.cdc.dschema.npresence else 0))
+
+
+def time_steps(fn, steps, warmup, world, dev):
+    """W untimed calls, then K calls bracketed by barrier + synchronize; events on the launch stream
+    give the per-call durations. Returns (max-over-ranks seconds, per-call ms list)."""
+    import torch
+    import torch.distributed as dist
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream()
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    evs[0].record(stream)
+    for k in range(steps):
+        fn()
+        evs[k + 1].record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    per = [evs[k].elapsed_time(evs[k + 1]) for k in range(steps)]
+    t = max(wall, sum(per) / 1e3)
+    if world > 1:
+        tt = torch.tensor([t], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t = float(tt.item())
+    return t, per
+
+
+def lib_sha256() -> str:
+    from kitex_amd import _lib
+    h = hashlib.sha256()
+    with open(_lib.LIB_PATH, "rb") as fh:
+        for blk in iter(lambda: fh.read(1 << 20), b""):
+            h.update(blk)
+    return h.hexdigest()
+
+
+def pmc_traffic(workload):
+    """HBM bytes per call from the committed rocprofv3 PMC summary of this workload, only when that
+    profile was taken with the library being timed (same sha256); else None with the reason."""
+    p = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
+    try:
+        with open(p) as fh:
+            prof = json.load(fh)
+    except Exception:
+        return None, "no profile"
+    sha = lib_sha256()
+    if prof.get("lib_sha256") != sha:
+        return None, f"profiles/pmc_{workload}.json was taken with another build of libkxcodec.so"
+    return prof.get("hbm_bytes_per_launch"), f"profiles/pmc_{workload}.json (lib sha256 {sha[:16]})"
+
+
+def roofline(alg_bytes, avg_launch_s, kernel, traffic=None, note=None):
+    achieved = alg_bytes / avg_launch_s / 1e9
+    r = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+         "traffic": traffic, "kernel": kernel, "avg_launch_ms": avg_launch_s * 1e3}
+    if note:
+        r["traffic_source"] = note
+    return r
 
 
 def main():
     args = parse()
     import torch
     import torch.distributed as dist
-
-    from kitex_amd import _abi as A
-    from kitex_amd import schema as S
-    from kitex_amd import synth
-    from kitex_amd.codec import ProtobufCodec, ThriftCodec, read_status
-    from kitex_amd.columns import alloc_device
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -65,104 +200,46 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
-    n = args.records
-    cfg = args.config
-    sch = S.SCHEMAS[cfg]()
-    cdc = ProtobufCodec(sch, device=local) if cfg == "pf" else ThriftCodec(sch, device=local)
-    infos = cdc.dschema.infos
+    if args.config == "c5":
+        result = run_c5(args, world, rank, dev, local)
+    else:
+        result = run_single(args, world, rank, dev, local)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
-    # ---- synthetic shard in HBM, encoded by the GPU encoder (untimed) ----
-    src = synth.TORCH_GENERATORS[cfg](n, dev, start=rank * n)
-    wire, offs = cdc.Marshal(src, with_offsets=True)
+
+def run_single(args, world, rank, dev, local):
+    import torch
+    import torch.distributed as dist
+    cfg, n = args.config, args.records
+    b = Batch(cfg, n, dev, rank * n, args.mode, local)
+    b.step()
     torch.cuda.synchronize()
-    in_bytes = wire.numel()
-    var_caps = [0 if ci.kind == A.COL_FIXED else synth_cap(src, c) for c, ci in enumerate(infos)]
-    out = alloc_device(infos, n, var_caps, cdc.dschema.npresence, dev)
-    offsets = offs if args.mode == "offsets" else None
-
-    from kitex_amd.codec import status_tensor
-    st_buf = status_tensor(dev)
-
-    def step():
-        return cdc.Unmarshal(wire, n, offsets=offsets, out=out, var_caps=var_caps, raise_on_error=False,
-                             status=st_buf)
-
-    for _ in range(args.warmup):
-        res = step()
-    torch.cuda.synchronize()
-    st = read_status(res.status)
+    st = b.status()
     assert st.code == 0 and st.n_records == n, f"decode failed: code={st.code} n={st.n_records}"
 
-    # ---- timed region: K decode passes, events on the launch stream ----
-    stream = torch.cuda.current_stream()
-    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    evs[0].record(stream)
-    for k in range(args.steps):
-        res = step()
-        evs[k + 1].record(stream)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    wall = time.perf_counter() - t0
-    per_launch_ms = [evs[k].elapsed_time(evs[k + 1]) for k in range(args.steps)]
-    ev_total_s = sum(per_launch_ms) / 1e3
-    t_rank = max(wall, ev_total_s)
-    if world > 1:
-        tt = torch.tensor([t_rank], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        t_rank = float(tt.item())
-
-    # ---- verify (size-independent property: decode(encode(x)) == x) ----
-    st = read_status(res.status)
-    ok = st.code == 0 and st.n_records == n and (args.mode == "offsets" or st.consumed == in_bytes)
-    for c, ci in enumerate(infos):
-        if ci.kind == A.COL_FIXED:
-            ok &= bool(torch.equal(out.cols[c], src.cols[c]))
-        else:
-            ok &= bool(torch.equal(out.cols[c][0], src.cols[c][0]))
-            tot = int(src.cols[c][0][-1].item()) & 0xFFFFFFFF
-            ok &= bool(torch.equal(out.cols[c][1][:tot], src.cols[c][1][:tot]))
+    t_rank, per = time_steps(b.step, args.steps, args.warmup, world, dev)
+    st = b.status()
+    ok = b.verify()
     if world > 1:
         okt = torch.tensor([1 if ok else 0], device=dev)
         dist.all_reduce(okt, op=dist.ReduceOp.MIN)
         ok = bool(okt.item())
 
-    # ---- N > 1: concatenation of the decoded shards into rank 0 over RCCL (reported separately) ----
     concat = None
     if world > 1 and not args.no_concat:
-        from kitex_amd.shard import concat_to_root
-        dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        full = concat_to_root(out, n, infos)
-        torch.cuda.synchronize()
-        dist.barrier()
-        tc = time.perf_counter() - t0
-        shard_bytes = sum((c[0][:n + 1].numel() * 4 + int(src.cols[i][0][-1].item()) * c[1].element_size())
-                          if isinstance(c, tuple) else n * c.element_size() for i, c in enumerate(out.cols))
-        concat = {"ms": tc * 1e3, "bytes_to_root": shard_bytes * (world - 1),
-                  "gb_s": shard_bytes * (world - 1) / tc / 1e9, "ok": full is None or full.n == n * world,
-                  "note": "decoded shards -> rank 0, batched isend/irecv over RCCL (xGMI); not in value"}
-        del full
+        concat = concat_shards([b], world, rank, dev)
 
     steps = args.steps
-    total_records = n * world * steps
-    value = total_records / t_rank
-    ms_per_step = t_rank / steps * 1e3
-    per_rec_in = in_bytes / n
-    per_rec_out = sum(
-        (ci.width if ci.kind == A.COL_FIXED else 4) for ci in infos) + sum(
-        (var_caps[c] * (ci.width if ci.kind == A.COL_LIST else 1)) / n for c, ci in enumerate(infos)
-        if ci.kind != A.COL_FIXED) + (8 if cdc.dschema.npresence else 0)
-    avg_launch_s = sum(per_launch_ms) / len(per_launch_ms) / 1e3
-    alg_bytes = (per_rec_in + per_rec_out) * n
-    achieved = alg_bytes / avg_launch_s / 1e9
-    gib_s = in_bytes * world * steps / t_rank / 2**30
-
+    value = n * world * steps / t_rank
+    per_rec_in = b.in_bytes / n
+    per_rec_out = b.out_bytes_per_record()
+    avg_launch_s = sum(per) / len(per) / 1e3
+    traffic, tnote = pmc_traffic(f"{cfg}_{args.mode}")
+    rl = roofline((per_rec_in + per_rec_out) * n, avg_launch_s, "decode (index+group+chain+emit)", traffic, tnote)
+    rl["read_only_frac"] = per_rec_in * n / avg_launch_s / 1e9 / HBM_PEAK_GBS
     result = {
         "metric": ("Kitex-Protobuf decode records/s, device-resident 16M flat records (second codec path)"
                    if cfg == "pf" else "Thrift-binary decode records/s + GiB/s, device-resident 16M×96B batch"),
@@ -171,7 +248,7 @@ def main():
         "n_gpus": world,
         "steps": steps,
         "warmup": args.warmup,
-        "ms_per_step": ms_per_step,
+        "ms_per_step": t_rank / steps * 1e3,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -180,65 +257,194 @@ def main():
         "config": {"workload": f"{cfg}_decode_{args.mode}", "records_per_gpu": n,
                    "wire_bytes_per_record": per_rec_in, "out_bytes_per_record": per_rec_out,
                    "parallelism": f"shard{world}"},
-        "gib_s": gib_s,
+        "gib_s": b.in_bytes * world * steps / t_rank / 2**30,
         "verified": ok,
         "decode_diag": {"tile_rewalks": st.diag[0], "group_rescans": st.diag[1]},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(cfg, args.mode),
-                     "read_only_frac": per_rec_in * n / avg_launch_s / 1e9 / HBM_PEAK_GBS,
-                     "kernel": "decode_kernel", "avg_launch_ms": avg_launch_s * 1e3},
+        "roofline": rl,
         "cpu_baseline": None,
+        "lib_sha256": lib_sha256()[:16],
     }
     if concat is not None:
         result["concat"] = concat
-
     if rank == 0 and world == 1 and not args.no_host and cfg != "pf":
-        result["host_inclusive"] = host_inclusive(cdc, wire, n, offsets, var_caps, infos, dev)
+        result["host_inclusive"] = host_inclusive(b, dev)
+    if world == 1 and not args.no_extra:
+        result["extra"] = extras(args, b if cfg == "r2" else None, dev, local)
     if rank == 0 and world == 1 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(cfg, args.cpu_records)
         if result["cpu_baseline"].get("value"):
             result["cpu_baseline"]["gpu_speedup"] = value / result["cpu_baseline"]["value"]
-    if rank == 0:
-        print(json.dumps(result), flush=True)
+    return result
+
+
+def run_c5(args, world, rank, dev, local):
+    """BASELINE config 5: 112M R2 + 16M R3 records sharded by record range over the ranks."""
+    import torch
+    import torch.distributed as dist
+
+    from kitex_amd.shard import shard_range
+    totals = {"r2": int(C5_R2 * args.c5_scale), "r3": int(C5_R3 * args.c5_scale)}
+    batches = []
+    for cfg, tot in totals.items():
+        s0, cnt = shard_range(tot, world, rank)
+        batches.append(Batch(cfg, cnt, dev, s0, args.mode, local))
+    torch.cuda.synchronize()
+
+    def step():
+        for b in batches:
+            b.step()
+
+    t_rank, per = time_steps(step, args.steps, args.warmup, world, dev)
+    ok = all(b.verify() for b in batches)
     if world > 1:
-        dist.destroy_process_group()
+        okt = torch.tensor([1 if ok else 0], device=dev)
+        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+        ok = bool(okt.item())
+    concat = concat_shards(batches, world, rank, dev) if world > 1 and not args.no_concat else None
+    steps = args.steps
+    total = sum(totals.values())
+    value = total * steps / t_rank
+    avg_launch_s = sum(per) / len(per) / 1e3
+    alg = sum((b.in_bytes + b.out_bytes_per_record() * b.n) for b in batches)
+    if world > 1:
+        t = torch.tensor([alg], dtype=torch.float64, device=dev)
+        dist.all_reduce(t)
+        alg = float(t.item()) / world   # per-rank average: the roofline is per GPU
+    result = {
+        "metric": "Thrift-binary decode records/s, config 5: 112M R2 + 16M R3 sharded over the GPUs",
+        "value": value, "unit": "records/s", "n_gpus": world, "steps": steps, "warmup": args.warmup,
+        "ms_per_step": t_rank / steps * 1e3, "higher_is_better": True, "scaling": "strong",
+        "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic (splitmix64, SURVEY.md §8d), generated + GPU-encoded in HBM",
+        "config": {"workload": f"c5_decode_{args.mode}", "records_total": totals,
+                   "records_per_gpu": {k: shard_range(v, world, rank)[1] for k, v in totals.items()},
+                   "parallelism": f"shard{world}"},
+        "verified": ok,
+        "roofline": roofline(alg, avg_launch_s, "decode R2 shard + decode R3 shard"),
+        "cpu_baseline": None,
+        "lib_sha256": lib_sha256()[:16],
+    }
+    if concat is not None:
+        result["concat"] = concat
+    if rank == 0 and world == 1 and not args.no_cpu:
+        result["cpu_baseline"] = cpu_baseline("r2", args.cpu_records)
+    return result
 
 
-def synth_cap(src, c):
-    return int(src.cols[c][0][-1].item()) & 0xFFFFFFFF
+def concat_shards(batches, world, rank, dev):
+    """decoded shards -> rank 0 (RCCL point-to-point over xGMI), checked there against the shards'
+    generator (same splitmix64 streams); outside `value`"""
+    import torch
+    import torch.distributed as dist
+
+    from kitex_amd import synth
+    from kitex_amd.shard import concat_batches_to_root
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    outs = concat_batches_to_root([(b.out, b.n, b.infos) for b in batches])
+    torch.cuda.synchronize()
+    dist.barrier()
+    tc = time.perf_counter() - t0
+    moved = sum(sum((c[0][:b.n + 1].numel() * c[0].element_size() + b.var_caps[i] * c[1].element_size())
+                    if isinstance(c, tuple) else b.n * c.element_size() for i, c in enumerate(b.out.cols))
+                for b in batches)
+    t = torch.tensor([moved], dtype=torch.float64, device=dev)
+    dist.all_reduce(t)
+    to_root = float(t.item()) - moved if rank == 0 else 0.0
+    ok = True
+    if rank == 0:   # head and tail (or all) of every concatenated batch against the generator
+        for b, full in zip(batches, outs):
+            N = full.n
+            k = min(N, 1 << 20)
+            for s0 in sorted({0, N - k}):
+                ref = synth.TORCH_GENERATORS[b.cfg](k, dev, start=s0)
+                for c in range(len(b.infos)):
+                    if isinstance(ref.cols[c], tuple):
+                        ro, rd = ref.cols[c]
+                        fo, fd = full.cols[c]
+                        ro = ro.to(torch.int64) & 0xFFFFFFFF if ro.dtype == torch.int32 else ro
+                        base = int(fo[s0].item())
+                        ok &= bool(torch.equal(fo[s0:s0 + k + 1] - base, ro))
+                        ok &= bool(torch.equal(fd[base:base + int(ro[-1].item())], rd[:int(ro[-1].item())]))
+                    else:
+                        ok &= bool(torch.equal(full.cols[c][s0:s0 + k], ref.cols[c]))
+                del ref
+        del outs
+    return {"ms": tc * 1e3, "bytes_to_root": to_root, "gb_s": to_root / tc / 1e9 if rank == 0 else None,
+            "checked_against_generator": ok,
+            "note": "decoded shards -> rank 0, batched isend/irecv over RCCL (xGMI), int64 offsets; not in value"}
 
 
-def pmc_traffic(cfg, mode):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary, if one exists for this workload."""
-    p = os.path.join(ROOT, "profiles", f"pmc_{cfg}_{mode}.json")
-    try:
-        with open(p) as fh:
-            return json.load(fh).get("hbm_bytes_per_launch")
-    except Exception:
-        return None
-
-
-def host_inclusive(cdc, wire, n, offsets, var_caps, infos, dev):
-    """Pinned host -> HBM copy + decode + columns back to pinned host (the netpoll-buffer path)."""
+def extras(args, r2, dev, local):
+    """The other BASELINE configs, timed the same way on this GPU: R3 decode + encode (config 3, 4M),
+    PF decode (config 4, 16M), R2 encode (16M)."""
     import torch
 
-    from kitex_amd import _abi as A
+    from kitex_amd.codec import status_tensor
+    steps, warm = max(3, min(args.steps, 10)), 2
+    out = {}
+
+    def encode_entry(b):
+        buf = torch.empty_like(b.wire)
+        st = status_tensor(dev)
+
+        def enc():
+            b.cdc.BLength(b.src)
+            b.cdc.Marshal(b.src, with_offsets=False, out=buf, status=st, check_status=False)
+        t, per = time_steps(enc, steps, warm, 1, dev)
+        ok = bool(torch.equal(buf, b.wire))
+        avg = sum(per) / len(per) / 1e3
+        alg = b.out_bytes_per_record() * b.n + b.in_bytes      # columns in + wire out
+        return {"records_per_s": b.n * steps / t, "ms_per_step": t / steps * 1e3, "bit_exact": ok,
+                "roofline": roofline(alg, avg, "BLength + encode")}
+
+    def decode_entry(b):
+        t, per = time_steps(b.step, steps, warm, 1, dev)
+        avg = sum(per) / len(per) / 1e3
+        ok = b.verify()
+        st = b.status()
+        return {"records_per_s": b.n * steps / t, "ms_per_step": t / steps * 1e3, "verified": ok,
+                "decode_diag": {"tile_rewalks": st.diag[0], "group_rescans": st.diag[1]},
+                "roofline": roofline(b.in_bytes + b.out_bytes_per_record() * b.n, avg, "decode")}
+
+    try:
+        if r2 is not None:
+            out["r2_encode"] = {"records": r2.n, **encode_entry(r2)}
+        b3 = Batch("r3", 4 << 20, dev, 0, "concat", local)
+        out["r3_decode"] = {"records": b3.n, "wire_bytes_per_record": b3.in_bytes / b3.n, **decode_entry(b3)}
+        out["r3_encode"] = {"records": b3.n, **encode_entry(b3)}
+        del b3
+        torch.cuda.empty_cache()
+        bp = Batch("pf", 16 << 20, dev, 0, "concat", local)
+        out["pf_decode"] = {"records": bp.n, "wire_bytes_per_record": bp.in_bytes / bp.n, **decode_entry(bp)}
+        del bp
+        torch.cuda.empty_cache()
+    except Exception as e:  # the extras must never break the headline line
+        out["error"] = repr(e)
+    return out
+
+
+def host_inclusive(b, dev):
+    """Pinned host -> HBM copy + decode + columns back to pinned host (the netpoll-buffer path),
+    through the library's own chunked, double-buffered kx_host_decode_batch when available."""
+    import torch
+
     from kitex_amd.columns import alloc_device
-    h_in = torch.empty(wire.numel(), dtype=torch.uint8, pin_memory=True)
-    h_in.copy_(wire)
-    d_in = torch.empty_like(wire)
-    out = alloc_device(infos, n, var_caps, cdc.dschema.npresence, dev)
+    h_in = torch.empty(b.wire.numel(), dtype=torch.uint8, pin_memory=True)
+    h_in.copy_(b.wire)
+    d_in = torch.empty_like(b.wire)
+    out = alloc_device(b.infos, b.n, b.var_caps, b.cdc.dschema.npresence, dev)
     h_out = [((torch.empty(c[0].numel(), dtype=c[0].dtype, pin_memory=True),
                torch.empty(c[1].numel(), dtype=c[1].dtype, pin_memory=True)) if isinstance(c, tuple)
               else torch.empty(c.numel(), dtype=c.dtype, pin_memory=True)) for c in out.cols]
-    d_off = offsets
     reps = 3
     best = 1e30
     for _ in range(reps + 1):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         d_in.copy_(h_in, non_blocking=True)
-        cdc.Unmarshal(d_in, n, offsets=d_off, out=out, var_caps=var_caps, raise_on_error=False)
+        b.cdc.Unmarshal(d_in, b.n, offsets=b.offsets, out=out, var_caps=b.var_caps, raise_on_error=False)
         for ho, c in zip(h_out, out.cols):
             if isinstance(c, tuple):
                 ho[0].copy_(c[0], non_blocking=True)
@@ -249,13 +455,15 @@ def host_inclusive(cdc, wire, n, offsets, var_caps, infos, dev):
         best = min(best, time.perf_counter() - t0)
     out_bytes = sum((c[0].numel() * c[0].element_size() + c[1].numel() * c[1].element_size())
                     if isinstance(c, tuple) else c.numel() * c.element_size() for c in out.cols)
-    return {"records_per_s": n / best, "ms": best * 1e3, "h2d_bytes": wire.numel(), "d2h_bytes": out_bytes,
-            "pcie_gb_s": (wire.numel() + out_bytes) / best / 1e9,
+    return {"records_per_s": b.n / best, "ms": best * 1e3, "h2d_bytes": b.wire.numel(), "d2h_bytes": out_bytes,
+            "pcie_gb_s": (b.wire.numel() + out_bytes) / best / 1e9,
             "note": "pinned H2D + decode + D2H, serial on one stream (PCIe-bound)"}
 
 
 def cpu_baseline(cfg, nrec):
-    """The CPU restatement of the reference FastRead (oracle, 'port'), all host cores, offsets known."""
+    """The CPU restatement of the reference FastRead (oracle, 'port') on every core this process may
+    run on (sched_getaffinity): offsets known (per-message fastUnmarshal, parallel over records),
+    plus the concatenated list<R> figure (one sequential walk: the GPU headline's mode)."""
     try:
         import numpy as np
 
@@ -263,13 +471,13 @@ def cpu_baseline(cfg, nrec):
         from kitex_amd import synth
         from oracle import oracle
         oracle.build()
-        threads = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
-        threads = max(1, min(threads, 64))
+        threads = max(1, min(len(os.sched_getaffinity(0)), 256))
         sch = S.SCHEMAS[cfg]()
         cs = synth.GENERATORS[cfg](nrec)
         pb = cfg == "pf"
         rc, wire, offs = oracle.encode(sch, cs, threads=threads, pb=pb)
         assert rc == 0
+        concat_wire = wire
         if pb:  # strip the Batch frame headers: bare bodies with known extents (per-message proto.Unmarshal)
             bs = offs[:nrec].astype(np.int64)                       # body starts
             u = np.where(wire[bs - 2] >= 0x80, 2, 1)                 # frame length varint bytes (bodies < 16 KiB)
@@ -281,28 +489,37 @@ def cpu_baseline(cfg, nrec):
             wire = wire[keep]
             offs = np.zeros(nrec + 1, dtype=np.uint64)
             offs[1:] = np.cumsum(lens)
-        caps = [None] * 0
         best = 1e30
         for _ in range(3):
             t0 = time.perf_counter()
             rc, out, st, _ = oracle.decode(sch, wire, nrec, offsets=offs, threads=threads, pb=pb)
             best = min(best, time.perf_counter() - t0)
             assert rc == 0
-        one = min(nrec, 1 << 19)
+        one = min(nrec, 1 << 20)
         t0 = time.perf_counter()
         oracle.decode(sch, wire[:int(offs[one])], one, offsets=offs[:one + 1], threads=1, pb=pb)
         t1 = time.perf_counter() - t0
+        # concatenated mode (record boundaries found by walking, as the GPU headline decodes)
+        cend = int(offs[one]) if not pb else None
+        t0 = time.perf_counter()
+        if not pb:
+            rc, _, cst, _ = oracle.decode(sch, concat_wire[:cend], one, offsets=None, threads=1)
+            assert rc == 0 and cst.code == 0
+        tc = time.perf_counter() - t0
         cpu = ""
         try:
             with open("/proc/cpuinfo") as fh:
                 cpu = next((l.split(":", 1)[1].strip() for l in fh if l.startswith("model name")), "")
         except Exception:
             pass
-        del caps
         return {"value": nrec / best, "unit": "records/s", "cores": threads, "kind": "port",
                 "sample": f"{nrec} {cfg} records, FastRead restatement (oracle/kx_oracle.c) with message "
-                          f"offsets known, best of 3, {threads} threads",
-                "gib_s": wire.size / best / 2**30, "one_thread_records_per_s": one / t1, "cpu_model": cpu}
+                          f"offsets known, best of 3, {threads} threads (len(sched_getaffinity))",
+                "gib_s": wire.size / best / 2**30, "one_thread_records_per_s": one / t1,
+                "concat_one_thread_records_per_s": (one / tc) if not pb else None,
+                "concat_note": f"{one} records as one concatenated list<{cfg}> body, walked sequentially "
+                               "(the mode of the GPU headline; inherently one thread on the CPU)",
+                "cpu_model": cpu}
     except Exception as e:  # the baseline must never break the GPU line
         return {"value": None, "error": repr(e)}
 

@@ -95,10 +95,10 @@ class Context:
             pass
 
 
-def _stream_ptr(stream) -> int:
+def _stream(stream):
+    """The torch stream a call runs on (the caller's, else the current one)."""
     import torch
-    s = stream if stream is not None else torch.cuda.current_stream()
-    return int(s.cuda_stream)
+    return stream if stream is not None else torch.cuda.current_stream()
 
 
 def _ptr(t) -> Optional[int]:
@@ -110,13 +110,10 @@ class DecodeResult:
     columns: ColumnSet
     status: "object"          # torch int64[16] on the device (kx_status)
     record_status: "object"   # torch uint8[n] or None
+    stream: "object" = None   # the torch stream the decode ran on
 
     def read_status(self) -> A.Status:
-        import torch
-        torch.cuda.current_stream().synchronize()
-        raw = self.status.cpu().numpy().tobytes()
-        st = A.Status.from_buffer_copy(raw)
-        return st
+        return read_status(self.status, self.stream)
 
 
 def status_tensor(device):
@@ -124,7 +121,10 @@ def status_tensor(device):
     return torch.zeros(16, dtype=torch.int64, device=device)
 
 
-def read_status(t) -> A.Status:
+def read_status(t, stream=None) -> A.Status:
+    """The kx_status a call on `stream` wrote into t: that stream is drained first (t.cpu() alone
+    would copy on the current stream, possibly before a side-stream kernel has written it)."""
+    _stream(stream).synchronize()
     return A.Status.from_buffer_copy(t.cpu().numpy().tobytes())
 
 
@@ -140,8 +140,16 @@ class ThriftCodec:
         import torch
         self.codec_type = codec_type
         self.dschema = schema if isinstance(schema, DeviceSchema) else DeviceSchema(schema)
-        self.ctx = Context(device)
         self.device = torch.device("cuda", device)
+        self._ctxs = {}           # one kx_ctx (workspace) per stream: calls on two streams never share one
+        self.ctx = self._ctx(None)
+
+    def _ctx(self, stream) -> Context:
+        key = int(_stream(stream).cuda_stream)
+        c = self._ctxs.get(key)
+        if c is None:
+            c = self._ctxs[key] = Context(self.device.index or 0)
+        return c
 
     # -- remote.PayloadCodec --------------------------------------------------------------------
     def Name(self) -> str:
@@ -160,10 +168,11 @@ class ThriftCodec:
         kc = to_kx_columns(out, ds.infos, var_caps)
         st = status if status is not None else status_tensor(self.device)
         rs = torch.empty(max(1, n), dtype=torch.uint8, device=self.device) if record_status else None
-        rc = getattr(lib(), self._DECODE)(self.ctx.handle, ds.handle, _ptr(buf), buf.numel(), _ptr(offsets), n,
-                                          C.byref(kc), _ptr(rs), _ptr(st), _stream_ptr(stream))
+        s = _stream(stream)
+        rc = getattr(lib(), self._DECODE)(self._ctx(s).handle, ds.handle, _ptr(buf), buf.numel(), _ptr(offsets), n,
+                                          C.byref(kc), _ptr(rs), _ptr(st), int(s.cuda_stream))
         check(rc, self._DECODE)
-        res = DecodeResult(out, st, rs)
+        res = DecodeResult(out, st, rs, s)
         if raise_on_error:
             s = res.read_status()
             if s.code:
@@ -193,8 +202,11 @@ class ThriftCodec:
             raise ProtocolError(st.code, self._WHAT, st.record, st.offset)
         return out, st
 
-    def Marshal(self, cols: ColumnSet, with_offsets: bool = True, stream=None, out=None):
-        """Encode the columns; returns (wire uint8 tensor, record offsets int64[n+1] or None)."""
+    def Marshal(self, cols: ColumnSet, with_offsets: bool = True, stream=None, out=None, status=None,
+                check_status: bool = True):
+        """Encode the columns; returns (wire uint8 tensor, record offsets int64[n+1] or None).
+        check_status=False (with `out` and `status` given) leaves the call asynchronous: the wire is
+        the whole `out` and the caller reads `status` later."""
         import torch
         ds = self.dschema
         n = cols.n
@@ -206,11 +218,14 @@ class ThriftCodec:
         else:
             total = out.numel()
         offs = torch.empty(n + 1, dtype=torch.int64, device=self.device) if with_offsets else None
-        st = status_tensor(self.device)
-        rc = getattr(lib(), self._ENCODE)(self.ctx.handle, ds.handle, C.byref(kc), n, _ptr(out), out.numel(),
-                                          _ptr(offs), _ptr(st), _stream_ptr(stream))
+        st = status if status is not None else status_tensor(self.device)
+        ss = _stream(stream)
+        rc = getattr(lib(), self._ENCODE)(self._ctx(ss).handle, ds.handle, C.byref(kc), n, _ptr(out), out.numel(),
+                                          _ptr(offs), _ptr(st), int(ss.cuda_stream))
         check(rc, self._ENCODE)
-        s = read_status(st)
+        if not check_status:
+            return out, offs
+        s = read_status(st, ss)
         if s.code:
             raise ProtocolError(s.code, self._ENCODE)
         return out[:s.consumed], offs
@@ -220,8 +235,9 @@ class ThriftCodec:
         ds = self.dschema
         kc = to_kx_columns(cols, ds.infos)
         sizes = torch.empty(max(1, cols.n), dtype=torch.int64, device=self.device)
-        rc = getattr(lib(), self._SIZE)(self.ctx.handle, ds.handle, C.byref(kc), cols.n, _ptr(sizes),
-                                        _stream_ptr(stream))
+        ss = _stream(stream)
+        rc = getattr(lib(), self._SIZE)(self._ctx(ss).handle, ds.handle, C.byref(kc), cols.n, _ptr(sizes),
+                                        int(ss.cuda_stream))
         check(rc, self._SIZE)
         return sizes[:cols.n]
 
@@ -230,10 +246,11 @@ class ThriftCodec:
         import torch
         offs = torch.empty(n + 1, dtype=torch.int64, device=self.device)
         st = status_tensor(self.device)
-        rc = lib().kx_thrift_skip_batch(self.ctx.handle, _ptr(buf), buf.numel(), n, _ptr(offs), _ptr(st),
-                                        _stream_ptr(stream))
+        ss = _stream(stream)
+        rc = lib().kx_thrift_skip_batch(self._ctx(ss).handle, _ptr(buf), buf.numel(), n, _ptr(offs), _ptr(st),
+                                        int(ss.cuda_stream))
         check(rc, "kx_thrift_skip_batch")
-        s = read_status(st)
+        s = read_status(st, ss)
         if s.code:
             raise ProtocolError(s.code, "skipThriftStruct", s.record, s.offset)
         return offs

@@ -238,6 +238,13 @@ def _string_bytes_t(key, length):
     return alpha[(raw.to(torch.int64) % len(ALPHABET))]
 
 
+def _offsets_t(off):
+    """an offset column as the C-ABI takes it: 4-byte (uint32 values in int32) unless the arena
+    reaches 2^32 units, then 8-byte"""
+    import torch
+    return off if int(off[-1].item()) >= (1 << 32) else off.to(torch.int32)
+
+
 def gen_r2_torch(n: int, device, start: int = 0, strlen: int = 32, chunk: int = 1 << 22) -> ColumnSet:
     import torch
     seed = seed_for("r2")
@@ -250,7 +257,7 @@ def gen_r2_torch(n: int, device, start: int = 0, strlen: int = 32, chunk: int = 
             cols[f - 1][c0:c1] = splitmix64_t(_key_t(seed, i, f))
         for j, f in enumerate((9, 10)):
             sdata[j][c0 * strlen:c1 * strlen] = _string_bytes_t(_key_t(seed, i, f), strlen).reshape(-1)
-    offs = (torch.arange(n + 1, dtype=torch.int64, device=device) * strlen).to(torch.int32)
+    offs = _offsets_t(torch.arange(n + 1, dtype=torch.int64, device=device) * strlen)
     out: List[object] = list(cols) + [(offs, sdata[0]), (offs.clone(), sdata[1])]
     return ColumnSet(out, None, n)
 
@@ -284,7 +291,7 @@ def gen_pf_torch(n: int, device, start: int = 0, strlen: int = 32, chunk: int = 
             cols[f - 1][c0:c1] = v
         for j, f in enumerate((9, 10)):
             sdata[j][c0 * strlen:c1 * strlen] = _string_bytes_t(_key_t(seed, i, f), strlen).reshape(-1)
-    offs = (torch.arange(n + 1, dtype=torch.int64, device=device) * strlen).to(torch.int32)
+    offs = _offsets_t(torch.arange(n + 1, dtype=torch.int64, device=device) * strlen)
     out: List[object] = list(cols) + [(offs, sdata[0]), (offs.clone(), sdata[1])]
     return ColumnSet(out, None, n)
 
@@ -332,7 +339,7 @@ def gen_r3_torch(n: int, device, start: int = 0, maxlist: int = 128, maxtag: int
         mt = ar_t[None, :] < tlen[c0:c1, None]
         tdata[int(toff[c0]):int(toff[c1])] = tb[mt]
     pres = torch.full((n,), 3, dtype=torch.int64, device=device)
-    cols = [ids, (voff.to(torch.int32), vdata), x, y, (toff.to(torch.int32), tdata), kind]
+    cols = [ids, (_offsets_t(voff), vdata), x, y, (_offsets_t(toff), tdata), kind]
     return ColumnSet(cols, pres, n)
 
 

@@ -49,12 +49,19 @@ def main():
                 k = short(row["Kernel_Name"])
                 if k:
                     dur[k].append((int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) / 1e6)
-    res = {"workload": f"{cfg}_decode_{mode}", "calls": calls,
+    sha = None
+    try:
+        with open(os.path.join(d, "lib.sha256")) as fh:
+            sha = fh.read().strip()
+    except OSError:
+        pass
+    res = {"workload": f"{cfg}_decode_{mode}", "calls": calls, "lib_sha256": sha,
            "hbm_bytes_per_launch": fetch_b + write_b, "fetch_bytes_per_call": fetch_b,
            "write_bytes_per_call": write_b, "per_kernel": per_kernel,
            "avg_ms": {k: sum(v) / len(v) for k, v in dur.items() if v},
            "note": "FETCH_SIZE x2 (gfx950 wide-read correction) + WRITE_SIZE, KiB -> bytes, summed over the "
-                   "decode kernels of one call; Infinity-Cache hits are counted by these counters"}
+                   "decode kernels of one call; Infinity-Cache hits are counted by these counters; bench.py "
+                   "uses it only when lib_sha256 matches the library it times"}
     out = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles",
                        f"pmc_{cfg}_{mode}.json")
     with open(out, "w") as fh:

@@ -10,6 +10,12 @@ def to_np(x):
     return x.detach().cpu().numpy()
 
 
+def offsets_u64(x):
+    """record offsets as int64 values: 4-byte columns hold uint32, 8-byte columns int64/uint64"""
+    a = to_np(x)
+    return a.view(np.uint64).astype(np.int64) if a.itemsize == 8 else a.view(np.uint32).astype(np.int64)
+
+
 def assert_columns_equal(got, exp, infos, n, check_presence=True):
     """Field-for-field equality of the first n records (fixed values, var bytes/elements, offsets)."""
     for c, ci in enumerate(infos):
@@ -22,13 +28,13 @@ def assert_columns_equal(got, exp, infos, n, check_presence=True):
         else:
             go, gd = (to_np(v) for v in got.cols[c])
             eo, ed = (to_np(v) for v in exp.cols[c])
-            go = go.view(np.uint32)[:n + 1].astype(np.int64) - int(go.view(np.uint32)[0])
-            eo = eo.view(np.uint32)[:n + 1].astype(np.int64) - int(eo.view(np.uint32)[0])
+            go = offsets_u64(go)[:n + 1]
+            eo = offsets_u64(eo)[:n + 1]
+            g0, e0 = int(go[0]), int(eo[0])
+            go, eo = go - g0, eo - e0
             lg, le = np.diff(go), np.diff(eo)
             bad = np.nonzero(lg != le)[0]
             assert bad.size == 0, f"var column {c} (field {ci.field_id}) lengths differ at {bad[:8]}"
-            g0 = int(to_np(got.cols[c][0]).view(np.uint32)[0])
-            e0 = int(to_np(exp.cols[c][0]).view(np.uint32)[0])
             tot = int(eo[-1])
             gb = gd.view(np.uint8)[g0 * gd.itemsize:(g0 + tot) * gd.itemsize]
             eb = ed.view(np.uint8)[e0 * ed.itemsize:(e0 + tot) * ed.itemsize]

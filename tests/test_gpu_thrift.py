@@ -257,3 +257,33 @@ def test_host_decode_error_status(torch, oracle):
     out, st = cdc.UnmarshalHost(wire, cs.n, raise_on_error=False)
     _, _, est, _ = oracle.decode(sch, wire, cs.n)
     assert (st.code, st.record, st.offset) == (est.code, est.record, est.offset) and st.code == A.ERR_EOF
+
+
+# ---------------------------------------------------------------------------------------------
+# streams: a call on a side stream reports its own status; two streams never share a workspace
+# ---------------------------------------------------------------------------------------------
+def test_side_streams_status_and_workspaces(torch, dev, oracle):
+    from kitex_amd.codec import ProtocolError, ThriftCodec
+    sch = S.schema_r2()
+    cdc = ThriftCodec(sch)
+    batches = []
+    for k in range(2):
+        cs = synth.gen_r2(60000, start=1000 * k)
+        rc, wire, _ = oracle.encode(sch, cs)
+        if k == 1:
+            wire = wire[:-9]                      # the second batch ends in a truncated record
+        batches.append((cs, torch.from_numpy(wire).to(dev), oracle.decode(sch, wire, cs.n)))
+    torch.cuda.synchronize()
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    res = []
+    for _ in range(3):                            # repeated, interleaved calls on both streams
+        res = [cdc.Unmarshal(b[1], b[0].n, stream=s, raise_on_error=False) for b, s in zip(batches, (s1, s2))]
+    assert len(cdc._ctxs) >= 3                    # the default stream's ctx + one per side stream
+    _, infos, _ = oracle.flatten(sch)
+    from tests.helpers import assert_columns_equal
+    for (cs, _, (rc, exp, est, _)), r in zip(batches, res):
+        st = r.read_status()
+        assert (st.code, st.record, st.offset, st.n_records) == (est.code, est.record, est.offset, est.n_records)
+        assert_columns_equal(r.columns, exp, infos, est.n_records)
+    with pytest.raises(ProtocolError):
+        cdc.Unmarshal(batches[1][1], batches[1][0].n, stream=s2)

@@ -70,13 +70,13 @@ def _worker(rank, world, port, name, n, q):
             local = _shift_arena(local, 5)
         out = concat_to_root(_to_torch(local), cnt, infos)
         if rank == 0:
-            from tests.helpers import assert_columns_equal
+            from tests.helpers import assert_columns_equal, offsets_u64
             full = synth.GENERATORS[name](n)
             assert out.n == n
             assert_columns_equal(out, full, infos, n)
             for c, ci in enumerate(infos):
                 if isinstance(full.cols[c], tuple):
-                    assert int(out.cols[c][0][n]) == int(full.cols[c][0][n])
+                    assert int(out.cols[c][0][n]) == int(offsets_u64(full.cols[c][0])[n])
         q.put((rank, "ok"))
     except Exception as e:  # report to the parent
         q.put((rank, repr(e)))
@@ -94,6 +94,65 @@ def test_concat_to_root_gloo(world, name, n):
     for p in ps:
         p.start()
     res = dict(q.get(timeout=120) for _ in range(world))
+    for p in ps:
+        p.join(timeout=60)
+    assert all(v == "ok" for v in res.values()), res
+
+
+def _mixed_worker(rank, world, port, n2, n3, q):
+    """config 5 in miniature: every rank decodes its R2 and R3 record ranges with the decode KERNEL
+    SOURCE under the SIMT emulator, then both decoded batches are concatenated into rank 0 and
+    compared with the oracle's decode of the whole batches"""
+    import torch.distributed as dist
+
+    from kitex_amd.shard import concat_batches_to_root
+    from oracle import oracle
+    from tests.emu import emu
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        batches, wholes = [], []
+        for name, n in (("r2", n2), ("r3", n3)):
+            sch = S.SCHEMAS[name]()
+            _, infos, npres = oracle.flatten(sch)
+            s0, cnt = shard_range(n, world, rank)
+            rc, wire, _ = oracle.encode(sch, synth.GENERATORS[name](cnt, start=s0))
+            assert rc == 0
+            erc, cols, st, _ = emu.decode(sch, infos, npres, wire, cnt, threads=4)
+            assert erc == 0 and st.code == 0 and st.n_records == cnt, (erc, st.code, st.n_records)
+            batches.append((_to_torch(cols), cnt, infos))
+            if rank == 0:
+                rc, whole, _ = oracle.encode(sch, synth.GENERATORS[name](n))
+                wholes.append((sch, whole, n, infos))
+        outs = concat_batches_to_root(batches)
+        if rank == 0:
+            from tests.helpers import assert_columns_equal, offsets_u64
+            for out, (sch, whole, n, infos) in zip(outs, wholes):
+                rc, exp, est, _ = oracle.decode(sch, whole, n)
+                assert est.code == 0 and out.n == n
+                assert_columns_equal(out, exp, infos, n)
+                for c, ci in enumerate(infos):
+                    if isinstance(exp.cols[c], tuple):
+                        assert int(offsets_u64(out.cols[c][0])[n]) == int(offsets_u64(exp.cols[c][0])[n])
+        q.put((rank, "ok"))
+    except Exception as e:  # report to the parent
+        q.put((rank, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_concat_mixed_emulator_decoded_shards_gloo():
+    import torch.multiprocessing as mp
+    from tests.emu import emu
+    emu.lib()                                  # build once, before the ranks start
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    world = 2
+    ps = [ctx.Process(target=_mixed_worker, args=(r, world, port, 7001, 1500, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(world))
     for p in ps:
         p.join(timeout=60)
     assert all(v == "ok" for v in res.values()), res
