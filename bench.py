@@ -503,7 +503,7 @@ def cpu_baseline(cfg, nrec):
         cend = int(offs[one]) if not pb else None
         t0 = time.perf_counter()
         if not pb:
-            rc, _, cst, _ = oracle.decode(sch, concat_wire[:cend], one, offsets=None, threads=1)
+            rc, _, cst, _ = oracle.decode(sch, concat_wire[:cend], one, offsets=None)
             assert rc == 0 and cst.code == 0
         tc = time.perf_counter() - t0
         cpu = ""

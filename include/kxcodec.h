@@ -64,6 +64,8 @@ enum {
   KX_ERR_NOT_IMPLEMENTED = 5,  /* schema shape not supported by this build */
   KX_ERR_DEPTH_LIMIT = 6,      /* skip recursion depth (64, codec_apache.go:167) exceeded */
   KX_ERR_EOF = 8,              /* record runs past the end of its buffer */
+  KX_ERR_APPLICATION_EXCEPTION = 9, /* message of type EXCEPTION: a TApplicationException, not a
+                                       record (thrift.go:192-195; decoded by the host shim) */
   KX_ERR_INVALID_ARG = 100,
   KX_ERR_HIP = 101,            /* a HIP runtime call failed */
   KX_ERR_NO_DEVICE = 102,
@@ -215,6 +217,34 @@ int kx_pb_encode_batch(kx_ctx* c, const kx_schema* s, const kx_columns* in, uint
 int kx_host_decode_batch(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len,
                          const uint64_t* offsets, uint64_t n, const kx_columns* out,
                          kx_status* status);
+
+/* ---- message level: N framed RPC messages (framing already removed by the transport) ----
+ * message i = in[offsets[i] .. offsets[i+1]) (u64, n+1 entries, device).
+ * Thrift: MessageBegin (strict binary: i32 0x8001_00TT, string name, i32 seqid) + the method's
+ *   argument / result struct; its field `body_field` (1 = Args{1: req}, 0 = Result{0: success}) of
+ *   type STRUCT is the record decoded into `out` (schema `s` = that struct); every other field is
+ *   skipped (skip decoder, depth 64). An absent record field decodes as an empty struct.
+ *   (thriftCodec.Unmarshal, thrift.go:180-225; Args.FastRead, k-mock.go:422-517)
+ * Protobuf: Kitex-PB meta header (u32 0x9001_0000 + type, u32-length method name, u32 seqid), the
+ *   rest of the message is the proto body (protobufCodec.Unmarshal, protobuf.go:136-165).
+ * msg_cols (optional, 3 entries): [0] method name (KX_COL_BYTES: offsets + arena), [1] message type
+ *   (int32), [2] seqid (int32). Per-message codes in record_status (header errors, an EXCEPTION
+ *   message = KX_ERR_APPLICATION_EXCEPTION, else the record's decode code); status as offsets mode
+ *   (the first failing message; offset = its start). */
+int kx_thrift_decode_messages(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len,
+                              const uint64_t* offsets, uint64_t n, int32_t body_field,
+                              const kx_column* msg_cols, const kx_columns* out, uint8_t* record_status,
+                              kx_status* status, void* stream);
+int kx_pb_decode_messages(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len,
+                          const uint64_t* offsets, uint64_t n, const kx_column* msg_cols,
+                          const kx_columns* out, uint8_t* record_status, kx_status* status, void* stream);
+
+/* Kitex-Protobuf meta header (host memory; protobuf.go:77-90 / 136-165). */
+uint64_t kx_pb_meta_length(uint32_t name_len);
+int kx_pb_write_meta(uint8_t* buf, uint64_t cap, const char* name, uint32_t name_len, int32_t msg_type,
+                     int32_t seqid, uint64_t* written);
+int kx_pb_read_meta(const uint8_t* buf, uint64_t len, const char** name, uint32_t* name_len,
+                    int32_t* msg_type, int32_t* seqid, uint64_t* consumed);
 
 /* ---- Thrift MessageBegin (WriteMessageBegin / ReadMessageBegin, binary_test.go:387-457) ---- */
 uint64_t kx_thrift_message_begin_length(uint32_t name_len);

@@ -23,6 +23,7 @@ ERR_BAD_VERSION = 4
 ERR_NOT_IMPLEMENTED = 5
 ERR_DEPTH_LIMIT = 6
 ERR_EOF = 8
+ERR_APPLICATION_EXCEPTION = 9
 ERR_INVALID_ARG = 100
 ERR_HIP = 101
 ERR_NO_DEVICE = 102
@@ -109,6 +110,7 @@ ERROR_NAMES = {
     ERR_NOT_IMPLEMENTED: "not implemented",
     ERR_DEPTH_LIMIT: "depth limit exceeded",
     ERR_EOF: "unexpected EOF",
+    ERR_APPLICATION_EXCEPTION: "application exception message",
     ERR_INVALID_ARG: "invalid argument",
     ERR_HIP: "HIP runtime error",
     ERR_NO_DEVICE: "no device",

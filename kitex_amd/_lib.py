@@ -23,6 +23,8 @@ EXPORTS = [
     "kx_thrift_encode_batch", "kx_pb_decode_batch", "kx_pb_encoded_size_batch",
     "kx_pb_encode_batch", "kx_host_decode_batch",
     "kx_thrift_message_begin_length", "kx_thrift_write_message_begin", "kx_thrift_read_message_begin",
+    "kx_thrift_decode_messages", "kx_pb_decode_messages", "kx_pb_meta_length", "kx_pb_write_meta",
+    "kx_pb_read_meta",
 ]
 
 
@@ -80,6 +82,14 @@ def lib():
     L.kx_thrift_write_message_begin.argtypes = [vp, u64, C.c_char_p, u32, i32, i32, C.POINTER(u64)]
     L.kx_thrift_read_message_begin.argtypes = [vp, u64, C.POINTER(C.c_char_p), C.POINTER(u32),
                                                C.POINTER(i32), C.POINTER(i32), C.POINTER(u64)]
+    L.kx_thrift_decode_messages.argtypes = [vp, vp, vp, u64, vp, u64, i32, C.POINTER(A.Column),
+                                            C.POINTER(A.Columns), vp, vp, vp]
+    L.kx_pb_decode_messages.argtypes = [vp, vp, vp, u64, vp, u64, C.POINTER(A.Column), C.POINTER(A.Columns),
+                                        vp, vp, vp]
+    L.kx_pb_meta_length.argtypes = [u32]
+    L.kx_pb_meta_length.restype = u64
+    L.kx_pb_write_meta.argtypes = L.kx_thrift_write_message_begin.argtypes
+    L.kx_pb_read_meta.argtypes = L.kx_thrift_read_message_begin.argtypes
     if L.kx_abi_version() != A.KX_ABI_VERSION:
         raise ImportError(f"libkxcodec ABI {L.kx_abi_version()} != {A.KX_ABI_VERSION}")
     _lib = L

@@ -116,6 +116,18 @@ class DecodeResult:
         return read_status(self.status, self.stream)
 
 
+@dataclass
+class MessageBatch(DecodeResult):
+    names: "object" = None     # (int64 offsets[n+1], uint8 arena) method names
+    msg_type: "object" = None  # int32[n]
+    seqid: "object" = None     # int32[n]
+
+    def name(self, i: int) -> str:
+        o = self.names[0]
+        a, b = int(o[i].item()), int(o[i + 1].item())
+        return bytes(self.names[1][a:b].cpu().numpy()).decode()
+
+
 def status_tensor(device):
     import torch
     return torch.zeros(16, dtype=torch.int64, device=device)
@@ -202,6 +214,46 @@ class ThriftCodec:
             raise ProtocolError(st.code, self._WHAT, st.record, st.offset)
         return out, st
 
+    _MESSAGES = "kx_thrift_decode_messages"
+
+    def UnmarshalMessages(self, buf, n: int, offsets, body_field: int = 1, out: ColumnSet = None,
+                          var_caps: Sequence[int] = None, name_cap: int = None, stream=None,
+                          raise_on_error: bool = True) -> "MessageBatch":
+        """thriftCodec.Unmarshal over n framed messages: buf[offsets[i]:offsets[i+1]] = MessageBegin +
+        the method's Args (body_field 1) / Result (body_field 0) struct holding one record.
+        Returns the record columns plus method name / message type / seqid columns."""
+        import torch
+        ds = self.dschema
+        if out is None:
+            if var_caps is None:
+                var_caps = [0 if ci.kind == A.COL_FIXED else max(1, buf.numel()) for ci in ds.infos]
+            out = alloc_device(ds.infos, n, var_caps, ds.npresence, self.device)
+        kc = to_kx_columns(out, ds.infos, var_caps)
+        name_cap = max(1, buf.numel() if name_cap is None else name_cap)
+        names = (torch.zeros(n + 1, dtype=torch.int64, device=self.device),
+                 torch.empty(name_cap, dtype=torch.uint8, device=self.device))
+        mtype = torch.zeros(max(1, n), dtype=torch.int32, device=self.device)
+        seqid = torch.zeros(max(1, n), dtype=torch.int32, device=self.device)
+        mc = (A.Column * 3)()
+        mc[0].data, mc[0].offsets, mc[0].capacity, mc[0].offset_bytes = names[1].data_ptr(), names[0].data_ptr(), \
+            name_cap, 8
+        mc[1].data = mtype.data_ptr()
+        mc[2].data = seqid.data_ptr()
+        st = status_tensor(self.device)
+        rs = torch.empty(max(1, n), dtype=torch.uint8, device=self.device)
+        s = _stream(stream)
+        args = [self._ctx(s).handle, ds.handle, _ptr(buf), buf.numel(), _ptr(offsets), n]
+        if self._MESSAGES == "kx_thrift_decode_messages":
+            args.append(body_field)
+        rc = getattr(lib(), self._MESSAGES)(*args, mc, C.byref(kc), _ptr(rs), _ptr(st), int(s.cuda_stream))
+        check(rc, self._MESSAGES)
+        res = MessageBatch(out, st, rs, s, names, mtype[:n], seqid[:n])
+        if raise_on_error:
+            stt = res.read_status()
+            if stt.code:
+                raise ProtocolError(stt.code, self._WHAT, stt.record, stt.offset)
+        return res
+
     def Marshal(self, cols: ColumnSet, with_offsets: bool = True, stream=None, out=None, status=None,
                 check_status: bool = True):
         """Encode the columns; returns (wire uint8 tensor, record offsets int64[n+1] or None).
@@ -267,6 +319,7 @@ class ProtobufCodec(ThriftCodec):
     `message Batch { repeated Rec recs = 1; }` (record boundaries found on the GPU)."""
 
     _DECODE = "kx_pb_decode_batch"
+    _MESSAGES = "kx_pb_decode_messages"
     _ENCODE = "kx_pb_encode_batch"
     _SIZE = "kx_pb_encoded_size_batch"
     _WHAT = "protobuf unmarshal"
@@ -304,5 +357,24 @@ def read_message_begin(data: bytes):
                                         C.byref(u))
     if rc:
         raise ProtocolError(rc, "ReadMessageBegin")
+    off = C.cast(name, C.c_void_p).value - C.addressof(arr)
+    return bytes(data[off:off + nl.value]).decode(), t.value, s.value, u.value
+
+
+def write_pb_meta(name: str, msg_type: int, seqid: int) -> bytes:
+    """Kitex-Protobuf meta header (protobuf.go:77-90) via the C-ABI."""
+    nb = name.encode()
+    buf = (C.c_uint8 * (12 + len(nb)))()
+    w = C.c_uint64()
+    check(lib().kx_pb_write_meta(buf, len(buf), nb, len(nb), msg_type, seqid, C.byref(w)), "pb write meta")
+    return bytes(buf[:w.value])
+
+
+def read_pb_meta(data: bytes):
+    arr = (C.c_uint8 * max(1, len(data))).from_buffer_copy(data or b"\0")
+    name, nl, t, s, u = C.c_char_p(), C.c_uint32(), C.c_int32(), C.c_int32(), C.c_uint64()
+    rc = lib().kx_pb_read_meta(arr, len(data), C.byref(name), C.byref(nl), C.byref(t), C.byref(s), C.byref(u))
+    if rc:
+        raise ProtocolError(rc, "pb read meta")
     off = C.cast(name, C.c_void_p).value - C.addressof(arr)
     return bytes(data[off:off + nl.value]).decode(), t.value, s.value, u.value

@@ -66,6 +66,22 @@ int ensure_ews(kx_ctx* c, size_t bytes, hipStream_t stream) {
   return KX_OK;
 }
 
+int ensure_mws(kx_ctx* c, size_t bytes, hipStream_t stream) {
+  if (c->mws_size >= bytes) return KX_OK;
+  if (c->mws) {
+    KX_HIP_CHECK(hipStreamSynchronize(stream));
+    KX_HIP_CHECK(hipFree(c->mws));
+    c->mws = nullptr;
+    c->mws_size = 0;
+  }
+  size_t sz = bytes < (1u << 20) ? (1u << 20) : bytes + bytes / 4;
+  KX_HIP_CHECK(hipMalloc(&c->mws, sz));
+  c->mws_size = sz;
+  KX_HIP_CHECK(hipMemsetAsync(c->mws, 0, 256, stream));
+  KX_HIP_CHECK(hipMemsetAsync(c->mws, 0xff, 8, stream));  // error key: none
+  return KX_OK;
+}
+
 int offset_width(const kx_column& k) {
   return k.offset_bytes == 0 || k.offset_bytes == 4 ? 4 : k.offset_bytes == 8 ? 8 : 0;
 }
@@ -118,6 +134,7 @@ const char* kx_strerror(int code) {
     case KX_ERR_NOT_IMPLEMENTED: return "not implemented";
     case KX_ERR_DEPTH_LIMIT: return "depth limit exceeded";
     case KX_ERR_EOF: return "unexpected EOF";
+    case KX_ERR_APPLICATION_EXCEPTION: return "application exception message";
     case KX_ERR_INVALID_ARG: return "invalid argument";
     case KX_ERR_HIP: return "HIP runtime error";
     case KX_ERR_NO_DEVICE: return "no device";
@@ -189,6 +206,7 @@ void kx_ctx_destroy(kx_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->ws) (void)hipFree(c->ws);
   if (c->ews) (void)hipFree(c->ews);
+  if (c->mws) (void)hipFree(c->mws);
   if (c->pin) (void)hipHostFree(c->pin);
   if (c->dstage) (void)hipFree(c->dstage);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
@@ -300,6 +318,68 @@ int kx_pb_decode_batch(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_
   if ((rc = ensure_ws(c, ws, st, &epoch))) return rc;
   return kx_launch_decode(dp, s->prog, in, in_len, offsets, n, lc, record_status, status, c->ws, c->ws_size,
                           epoch, st, true);
+}
+
+// N framed messages: headers on the device (kx_message.hip), then the record bodies through the
+// known-offsets decode with explicit ends, then the per-message codes merged (header code first)
+static int decode_messages(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len,
+                           const uint64_t* offsets, uint64_t n, int32_t body_field, bool pb,
+                           const kx_column* msg_cols, const kx_columns* out, uint8_t* record_status,
+                           kx_status* status, void* stream) {
+  if (!c || !s || !status || !offsets || (!in && in_len)) return KX_ERR_INVALID_ARG;
+  int rc = set_device(c);
+  if (rc) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  KxLaunchCols lc;
+  if ((rc = to_launch_cols(s, out, &lc))) return rc;
+  if (pb && (rc = pb_schema_ok(s))) return rc;
+  KxMsgOut mo{};
+  if (msg_cols) {
+    const kx_column& nm = msg_cols[0];
+    const int w = offset_width(nm);
+    if (!w) return KX_ERR_INVALID_ARG;
+    mo.name_offs = nm.offsets;
+    mo.name_data = (uint8_t*)nm.data;
+    mo.name_cap = nm.data ? nm.capacity : 0;
+    mo.name_owide = w == 8;
+    mo.msg_type = (int32_t*)msg_cols[1].data;
+    mo.seqid = (int32_t*)msg_cols[2].data;
+  }
+  if (n == 0) {
+    KX_HIP_CHECK(hipMemsetAsync(status, 0, sizeof(kx_status), st));
+    for (uint32_t k = 0; k < s->ncols; k++)
+      if (lc.offs[k]) KX_HIP_CHECK(hipMemsetAsync(lc.offs[k], 0, ((lc.owide >> k) & 1) ? 8 : 4, st));
+    if (mo.name_offs) KX_HIP_CHECK(hipMemsetAsync(mo.name_offs, 0, mo.name_owide ? 8 : 4, st));
+    return KX_OK;
+  }
+  if ((rc = ensure_mws(c, kx_message_ws_bytes(n), st))) return rc;
+  uint64_t *rs = nullptr, *re = nullptr;
+  uint8_t *hrc = nullptr, *brc = nullptr;
+  if ((rc = kx_launch_message_headers(in, in_len, offsets, n, body_field, pb, mo, c->mws, &rs, &re, &hrc, &brc,
+                                      st)))
+    return rc;
+  KxProgram* dp = nullptr;
+  if ((rc = prog_on_device(const_cast<kx_schema*>(s), c->device, &dp))) return rc;
+  uint64_t epoch = 0;
+  if ((rc = ensure_ws(c, kx_decode_ws_bytes(s->prog, in_len, rs, n), st, &epoch))) return rc;
+  if ((rc = kx_launch_decode(dp, s->prog, in, in_len, rs, n, lc, brc, status, c->ws, c->ws_size, epoch, st, pb,
+                             re)))
+    return rc;
+  return kx_launch_message_merge(offsets, n, hrc, brc, record_status, status, c->mws, st);
+}
+
+int kx_thrift_decode_messages(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len,
+                              const uint64_t* offsets, uint64_t n, int32_t body_field,
+                              const kx_column* msg_cols, const kx_columns* out, uint8_t* record_status,
+                              kx_status* status, void* stream) {
+  return decode_messages(c, s, in, in_len, offsets, n, body_field, false, msg_cols, out, record_status, status,
+                         stream);
+}
+
+int kx_pb_decode_messages(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len,
+                          const uint64_t* offsets, uint64_t n, const kx_column* msg_cols,
+                          const kx_columns* out, uint8_t* record_status, kx_status* status, void* stream) {
+  return decode_messages(c, s, in, in_len, offsets, n, 0, true, msg_cols, out, record_status, status, stream);
 }
 
 int kx_pb_encoded_size_batch(kx_ctx* c, const kx_schema* s, const kx_columns* in, uint64_t n,
@@ -452,6 +532,46 @@ int kx_thrift_read_message_begin(const uint8_t* buf, uint64_t len, const char** 
   *name = (const char*)buf + 8;
   *name_len = (uint32_t)n;
   *msg_type = (int32_t)(v & 0xffu);
+  *seqid = (int32_t)be(buf + 8 + n);
+  *consumed = 12ull + (uint64_t)n;
+  return KX_OK;
+}
+
+uint64_t kx_pb_meta_length(uint32_t name_len) { return 12ull + name_len; }
+
+// codec.WriteUint32(ProtobufV1Magic + msgType), codec.WriteString(method), codec.WriteUint32(seqID)
+// (protobuf.go:77-90)
+int kx_pb_write_meta(uint8_t* buf, uint64_t cap, const char* name, uint32_t name_len, int32_t msg_type,
+                     int32_t seqid, uint64_t* written) {
+  if (!buf || (!name && name_len) || !written) return KX_ERR_INVALID_ARG;
+  const uint64_t need = 12ull + name_len;
+  if (cap < need) return KX_ERR_SIZE_LIMIT;
+  auto put = [](uint8_t* p, uint32_t v) { p[0] = v >> 24; p[1] = v >> 16; p[2] = v >> 8; p[3] = (uint8_t)v; };
+  put(buf, 0x90010000u + ((uint32_t)msg_type & 0xffffu));
+  put(buf + 4, name_len);
+  if (name_len) memcpy(buf + 8, name, name_len);
+  put(buf + 8 + name_len, (uint32_t)seqid);
+  *written = need;
+  return KX_OK;
+}
+
+// protobufCodec.Unmarshal's meta read (protobuf.go:136-160): magic check, type, method, seqID
+int kx_pb_read_meta(const uint8_t* buf, uint64_t len, const char** name, uint32_t* name_len, int32_t* msg_type,
+                    int32_t* seqid, uint64_t* consumed) {
+  if (!buf || !name || !name_len || !msg_type || !seqid || !consumed) return KX_ERR_INVALID_ARG;
+  auto be = [](const uint8_t* p) {
+    return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+  };
+  if (len < 4) return KX_ERR_EOF;
+  const uint32_t v = be(buf);
+  if ((v & 0xffff0000u) != 0x90010000u) return KX_ERR_BAD_VERSION;
+  if (len < 8) return KX_ERR_EOF;
+  const int32_t n = (int32_t)be(buf + 4);
+  if (n < 0) return KX_ERR_NEGATIVE_SIZE;
+  if (len < 12ull + (uint64_t)n) return KX_ERR_EOF;
+  *name = (const char*)buf + 8;
+  *name_len = (uint32_t)n;
+  *msg_type = (int32_t)(v & 0xffffu);
   *seqid = (int32_t)be(buf + 8 + n);
   *consumed = 12ull + (uint64_t)n;
   return KX_OK;

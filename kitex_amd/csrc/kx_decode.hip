@@ -70,6 +70,7 @@ struct DecParams {
   const uint8_t* in;
   uint64_t in_len;
   const uint64_t* offsets;   // known-offsets mode when non-null
+  const uint64_t* ends;      // known-offsets mode: record r ends at ends[r] (else offsets[r + 1])
   uint64_t n;
   const KAS KxProgram* prog;  // compiled schema (constant address space: scalar loads when uniform)
   KxLaunchCols cols;
@@ -95,6 +96,11 @@ struct DecParams {
 // parameter (cols.data[c]) would otherwise make the compiler copy the whole block to scratch per lane.
 typedef const KAS DecParams KParams;
 #define KX_PARAMS() (*(KParams*)__builtin_amdgcn_kernarg_segment_ptr())
+
+// known-offsets mode: where record r ends (message bodies: an explicit end per record)
+__device__ __forceinline__ uint64_t rec_end(KParams& dp, uint64_t r) {
+  return dp.ends ? dp.ends[r] : dp.offsets[r + 1];
+}
 
 // ---------------------------------------------------------------------------------------------
 // byte access: the wave's LDS window, or global memory outside it
@@ -1260,7 +1266,7 @@ __device__ __forceinline__ Agg measure_records(KParams& dp, const Src& w, uint64
 #pragma unroll
   for (int v = 0; v < NV; v++) vs.len[v] = 0;
   if (r < r1) {
-    const uint64_t a = dp.offsets[r], b = dp.offsets[r + 1];
+    const uint64_t a = dp.offsets[r], b = rec_end(dp, r);
     uint64_t end, pres;
     int rc = (a > b || b > dp.in_len) ? KX_ERR_INVALID_ARG : parse_record<NV, MODE>(dp, w, a, b, r, false, &end, vs, pres);
     if (rc) {
@@ -1673,7 +1679,7 @@ __global__ void __launch_bounds__(NT) emit_kernel(DecParams dp_) {
     if (act) {
       if (known) {
         pos = dp.offsets[r];
-        lim = dp.offsets[r + 1];
+        lim = rec_end(dp, r);
         if (pos > lim || lim > dp.in_len) rc = KX_ERR_INVALID_ARG;
       } else {
         pos = lo + starts[j];
@@ -1721,7 +1727,7 @@ __global__ void __launch_bounds__(NT) emit_kernel(DecParams dp_) {
     if (act && r == nstop - 1 && nstop == dp.n) {
       kx_status* st = dp.status;
       st->n_records = dp.n;
-      st->consumed = known ? dp.offsets[dp.n] : end;
+      st->consumed = known ? rec_end(dp, dp.n - 1) : end;
       if (MODE == M_SKIP) dp.skip_out[dp.n] = end;
     }
   }
@@ -1905,10 +1911,12 @@ size_t kx_skip_ws_bytes(uint64_t in_len) { return ws_layout(1, in_len, nullptr, 
 
 int kx_launch_decode(const KxProgram* dprog, const KxProgram& hprog, const uint8_t* in, uint64_t in_len,
                      const uint64_t* offsets, uint64_t n, const KxLaunchCols& cols, uint8_t* record_status,
-                     kx_status* status, void* ws, size_t ws_size, uint64_t epoch, hipStream_t stream, bool pb) {
+                     kx_status* status, void* ws, size_t ws_size, uint64_t epoch, hipStream_t stream, bool pb,
+                     const uint64_t* ends) {
   DecParams dp{};
   fill_diag_flags(dp);
-  dp.in = in; dp.in_len = in_len; dp.offsets = offsets; dp.n = n; dp.prog = (const KAS KxProgram*)dprog;
+  dp.in = in; dp.in_len = in_len; dp.offsets = offsets; dp.ends = offsets ? ends : nullptr; dp.n = n;
+  dp.prog = (const KAS KxProgram*)dprog;
   dp.cols = cols; dp.rstat = record_status; dp.status = status; dp.epoch = epoch;
   dp.krec = krec_for(in_len, n);
   const WsLayout L = ws_layout(hprog.fixed_min, in_len, offsets, n);

@@ -32,6 +32,9 @@ struct kx_ctx {
   void* ws = nullptr;
   size_t ws_size = 0;
   uint64_t epoch = 0;                  // call epoch tagging descriptor words (1..65535)
+  // grow-only message-header workspace (kx_*_decode_messages)
+  void* mws = nullptr;
+  size_t mws_size = 0;
   // grow-only encode scratch (per-block sizes)
   void* ews = nullptr;
   size_t ews_size = 0;
@@ -63,7 +66,8 @@ struct KxLaunchCols {
 int kx_launch_decode(const KxProgram* dprog, const KxProgram& hprog, const uint8_t* in,
                      uint64_t in_len, const uint64_t* offsets, uint64_t n,
                      const KxLaunchCols& cols, uint8_t* record_status, kx_status* status,
-                     void* ws, size_t ws_size, uint64_t epoch, hipStream_t stream, bool pb);
+                     void* ws, size_t ws_size, uint64_t epoch, hipStream_t stream, bool pb,
+                     const uint64_t* ends = nullptr);
 size_t kx_decode_ws_bytes(const KxProgram& hprog, uint64_t in_len, const uint64_t* offsets, uint64_t n);
 
 int kx_launch_skip(const uint8_t* in, uint64_t in_len, uint64_t n, uint64_t* offsets_out,
@@ -75,6 +79,23 @@ int kx_launch_encode(const KxProgram* dprog, const KxProgram& hprog, const KxLau
                      uint64_t* offsets_out, kx_status* status, void* ws, size_t ws_size,
                      hipStream_t stream, bool sizes_only, bool pb = false);
 size_t kx_encode_ws_bytes(uint64_t n);
+
+// kx_message.hip: MessageBegin + Args{1: Req} headers of n framed messages (lane = message)
+struct KxMsgOut {
+  int32_t* msg_type;            // per message (may be null)
+  int32_t* seqid;               // per message (may be null)
+  void* name_offs;              // method names: offsets (4 or 8 bytes, name_owide) + arena
+  uint8_t* name_data;
+  uint64_t name_cap;
+  uint32_t name_owide;
+};
+size_t kx_message_ws_bytes(uint64_t n);
+int kx_launch_message_headers(const uint8_t* in, uint64_t in_len, const uint64_t* offsets, uint64_t n,
+                              int32_t body_field, bool pb, const KxMsgOut& mo, void* mws,
+                              uint64_t** req_start, uint64_t** req_end,
+                              uint8_t** hdr_rc, uint8_t** body_rc, hipStream_t stream);
+int kx_launch_message_merge(const uint64_t* offsets, uint64_t n, const uint8_t* hdr_rc, const uint8_t* body_rc,
+                            uint8_t* record_status, kx_status* status, void* mws, hipStream_t stream);
 
 #define KX_HIP_CHECK(x)                       \
   do {                                        \

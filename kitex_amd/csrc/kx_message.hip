@@ -1,0 +1,351 @@
+// kx_message.hip — message level of an RPC batch on CDNA4 / gfx950: N framed messages, each
+// MessageBegin + the method's argument (or result) struct, whose one field holds the record; or each
+// a Kitex-Protobuf meta header + the proto body (protobuf.go:77-90,136-165: u32 0x9001_0000 + type,
+// u32-length method name, u32 seqid).
+//
+// Reference semantics: thriftCodec.Unmarshal (pkg/remote/codec/thrift/thrift.go:180-225):
+// ReadMessageBegin (strict binary: i32 0x8001_00TT, string name, i32 seqid; binary_test.go:387-457),
+// an EXCEPTION message carries a TApplicationException instead of the arguments (thrift.go:192-195),
+// then the generated Args/Result FastRead (internal/mocks/thrift/k-mock.go:422-517): fields until
+// STOP, field `body` (1 = Args.Req, 0 = Result.Success) of type STRUCT is the record, every other
+// field goes through the skip decoder (codec_apache.go:191-293, depth 64).
+//
+// Pipeline (all stream-ordered, lane = message):
+//   header_kernel  MessageBegin + Args walk -> type / seqid columns, name extents, the record's
+//                  extent [req_start, req_end) (an absent record field -> the Args STOP byte, i.e.
+//                  an empty struct), a per-message header code
+//   scan_kernel    exclusive scan of the name lengths (one workgroup, contiguous runs per thread)
+//   name_kernel    method names copied into the name arena
+//   (the record bodies: kx_launch_decode in known-offsets mode with explicit ends)
+//   merge_kernel   per-message code = header code, else body code; first failing message -> status
+// Header walks read global memory byte-wise: headers are tens of bytes, the bodies are the work.
+#include <hip/hip_runtime.h>
+
+#include "kx_internal.h"
+
+namespace {
+
+constexpr int MT = 256;       // threads per workgroup (lane = message)
+constexpr int ST = 1024;      // scan kernel: one workgroup
+constexpr int MAXDEPTH = 64;  // skip recursion depth (codec_apache.go:167)
+
+__device__ __forceinline__ uint32_t be32(const uint8_t* p) {
+  return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+}
+
+__device__ __forceinline__ int fixed_size(uint32_t t) {
+  switch (t) {
+    case KX_T_BOOL: case KX_T_BYTE: return 1;
+    case KX_T_I16: return 2;
+    case KX_T_I32: return 4;
+    case KX_T_I64: case KX_T_DOUBLE: return 8;
+    default: return 0;
+  }
+}
+
+// skipType (codec_apache.go:191-293) of one value of type t at pos, bounded by end; an explicit
+// stack of struct / list / map frames instead of recursion (depth limit as the reference)
+struct Frame {
+  uint8_t kind, t1, t2, phase;  // kind 0 struct, 1 list/set, 2 map (phase 0 key, 1 value)
+  uint32_t left;
+};
+
+__device__ __forceinline__ int skip_value(const uint8_t* in, uint64_t& pos, uint64_t end, uint32_t t) {
+  Frame st[MAXDEPTH];
+  int sp = 0;
+  uint32_t cur = t;
+  for (;;) {
+    const int w = fixed_size(cur);
+    if (w) {
+      if (end - pos < (uint64_t)w) return KX_ERR_EOF;
+      pos += w;
+    } else if (cur == KX_T_STRING) {
+      if (end - pos < 4) return KX_ERR_EOF;
+      const int32_t l = (int32_t)be32(in + pos);
+      if (l < 0) return KX_ERR_NEGATIVE_SIZE;
+      if (end - pos - 4 < (uint64_t)l) return KX_ERR_EOF;
+      pos += 4 + (uint64_t)l;
+    } else if (cur == KX_T_STRUCT) {
+      if (sp == MAXDEPTH) return KX_ERR_DEPTH_LIMIT;
+      st[sp++] = Frame{0, 0, 0, 0, 0};
+    } else if (cur == KX_T_LIST || cur == KX_T_SET) {
+      if (end - pos < 5) return KX_ERR_EOF;
+      const uint32_t et = in[pos];
+      const int32_t sz = (int32_t)be32(in + pos + 1);
+      pos += 5;
+      if (sz < 0) return KX_ERR_NEGATIVE_SIZE;
+      const int ew = fixed_size(et);
+      if (ew) {
+        if ((end - pos) / (uint64_t)ew < (uint64_t)sz) return KX_ERR_EOF;
+        pos += (uint64_t)sz * ew;
+      } else if (sz) {
+        if (sp == MAXDEPTH) return KX_ERR_DEPTH_LIMIT;
+        st[sp++] = Frame{1, (uint8_t)et, 0, 0, (uint32_t)sz};
+      }
+    } else if (cur == KX_T_MAP) {
+      if (end - pos < 6) return KX_ERR_EOF;
+      const uint32_t kt = in[pos], vt = in[pos + 1];
+      const int32_t sz = (int32_t)be32(in + pos + 2);
+      pos += 6;
+      if (sz < 0) return KX_ERR_NEGATIVE_SIZE;
+      const int kw = fixed_size(kt), vw = fixed_size(vt);
+      if (kw && vw) {
+        if ((end - pos) / (uint64_t)(kw + vw) < (uint64_t)sz) return KX_ERR_EOF;
+        pos += (uint64_t)sz * (kw + vw);
+      } else if (sz) {
+        if (sp == MAXDEPTH) return KX_ERR_DEPTH_LIMIT;
+        st[sp++] = Frame{2, (uint8_t)kt, (uint8_t)vt, 0, (uint32_t)sz};
+      }
+    } else {
+      return KX_ERR_INVALID_DATA;  // unknown data type
+    }
+    // the next value to skip, from the innermost open frame
+    for (;;) {
+      if (sp == 0) return KX_OK;
+      Frame& f = st[sp - 1];
+      if (f.kind == 0) {
+        if (pos >= end) return KX_ERR_EOF;
+        const uint32_t ft = in[pos];
+        if (ft == KX_T_STOP) { pos++; sp--; continue; }
+        if (end - pos < 3) return KX_ERR_EOF;
+        pos += 3;
+        cur = ft;
+        break;
+      }
+      if (f.left == 0) { sp--; continue; }
+      if (f.kind == 1) {
+        f.left--;
+        cur = f.t1;
+      } else if (f.phase == 0) {
+        f.phase = 1;
+        cur = f.t1;
+      } else {
+        f.phase = 0;
+        f.left--;
+        cur = f.t2;
+      }
+      break;
+    }
+  }
+}
+
+struct MsgParams {
+  const uint8_t* in;
+  uint64_t in_len;
+  const uint64_t* offsets;   // n + 1 message boundaries
+  uint64_t n;
+  int32_t body_field;        // 1: Args{1: req}, 0: Result{0: success}
+  int pb;                    // Kitex-Protobuf meta header (magic 0x9001, 16-bit type), body = the rest
+  KxMsgOut mo;
+  uint64_t* req_start;       // n + 1 (req_start[n] = in_len)
+  uint64_t* req_end;
+  uint64_t* name_pos;
+  uint64_t* name_len;        // n + 1, scanned in place into the name offsets
+  uint8_t* hdr_rc;
+  unsigned long long* errkey;
+  uint32_t* overflow;
+};
+
+__global__ void __launch_bounds__(MT) header_kernel(MsgParams mp) {
+  const uint64_t i = (uint64_t)blockIdx.x * MT + threadIdx.x;
+  if (i >= mp.n) {
+    if (i == mp.n) { mp.req_start[i] = mp.in_len; mp.name_len[i] = 0; }
+    return;
+  }
+  const uint8_t* in = mp.in;
+  const uint64_t p = mp.offsets[i], e = mp.offsets[i + 1];
+  int rc = KX_OK;
+  uint32_t type = 0;
+  int32_t seqid = 0, nl = 0;
+  uint64_t rs = p, re = p;
+  if (p > e || e > mp.in_len) {
+    rc = KX_ERR_INVALID_ARG;
+  } else if (e - p < 4) {
+    rc = KX_ERR_EOF;
+  } else {
+    const uint32_t v = be32(in + p);
+    if ((v & 0xffff0000u) != (mp.pb ? 0x90010000u : 0x80010000u)) {
+      rc = KX_ERR_BAD_VERSION;
+    } else if (e - p < 8) {
+      rc = KX_ERR_EOF;
+    } else {
+      nl = (int32_t)be32(in + p + 4);
+      if (nl < 0) rc = KX_ERR_NEGATIVE_SIZE;
+      else if (e - p < 12ull + (uint64_t)nl) rc = KX_ERR_EOF;
+      else {
+        type = v & (mp.pb ? 0xffffu : 0xffu);
+        seqid = (int32_t)be32(in + p + 8 + nl);
+      }
+    }
+  }
+  if (!rc && type == KX_MSG_EXCEPTION) rc = KX_ERR_APPLICATION_EXCEPTION;
+  if (!rc && mp.pb) {  // protobuf.go:136-165: the body is the rest of the payload
+    rs = p + 12 + (uint64_t)nl;
+    re = e;
+  } else if (!rc) {  // the Args / Result struct: fields until STOP, the record field kept, the rest skipped
+    uint64_t pos = p + 12 + (uint64_t)nl;
+    bool have = false;
+    for (;;) {
+      if (pos >= e) { rc = KX_ERR_EOF; break; }
+      const uint32_t t = in[pos];
+      if (t == KX_T_STOP) {
+        if (!have) { rs = pos; re = pos + 1; }  // no record field: an empty struct (the STOP byte)
+        break;
+      }
+      if (e - pos < 3) { rc = KX_ERR_EOF; break; }
+      const int32_t id = (int16_t)(((uint32_t)in[pos + 1] << 8) | in[pos + 2]);
+      pos += 3;
+      const uint64_t s0 = pos;
+      rc = skip_value(in, pos, e, t);
+      if (rc) break;
+      if (id == mp.body_field && t == KX_T_STRUCT) { rs = s0; re = pos; have = true; }
+    }
+  }
+  if (rc) { rs = re = p; nl = 0; type = 0; seqid = 0; }
+  mp.req_start[i] = rs;
+  mp.req_end[i] = re;
+  mp.name_pos[i] = p + 8;
+  mp.name_len[i] = (uint64_t)nl;
+  mp.hdr_rc[i] = (uint8_t)rc;
+  if (mp.mo.msg_type) mp.mo.msg_type[i] = (int32_t)type;
+  if (mp.mo.seqid) mp.mo.seqid[i] = seqid;
+}
+
+// exclusive scan of name_len[0..n] in place (one workgroup; each thread a contiguous run)
+__global__ void __launch_bounds__(ST) scan_kernel(uint64_t* v, uint64_t n1) {
+  __shared__ uint64_t part[ST];
+  const uint64_t per = (n1 + ST - 1) / ST;
+  const uint64_t lo = kmin64((uint64_t)threadIdx.x * per, n1), hi = kmin64(lo + per, n1);
+  uint64_t s = 0;
+  for (uint64_t k = lo; k < hi; k++) s += v[k];
+  part[threadIdx.x] = s;
+  __syncthreads();
+  for (int d = 1; d < ST; d <<= 1) {
+    const uint64_t x = threadIdx.x >= (unsigned)d ? part[threadIdx.x - d] : 0;
+    __syncthreads();
+    part[threadIdx.x] += x;
+    __syncthreads();
+  }
+  uint64_t run = part[threadIdx.x] - s;
+  for (uint64_t k = lo; k < hi; k++) {
+    const uint64_t x = v[k];
+    v[k] = run;
+    run += x;
+  }
+}
+
+__global__ void __launch_bounds__(MT) name_kernel(MsgParams mp) {
+  const uint64_t i = (uint64_t)blockIdx.x * MT + threadIdx.x;
+  if (i > mp.n) return;
+  const uint64_t at = mp.name_len[i];  // exclusive prefix after the scan
+  const bool wide = mp.mo.name_owide != 0;
+  const uint64_t lim = wide ? mp.mo.name_cap : kmin64(mp.mo.name_cap, 0xffffffffull);
+  if (mp.mo.name_offs) {
+    if (at <= lim) {
+      if (wide) ((uint64_t*)mp.mo.name_offs)[i] = at;
+      else ((uint32_t*)mp.mo.name_offs)[i] = (uint32_t)at;
+    } else if (i == mp.n) {
+      atomicOr(mp.overflow, 1u);
+    }
+  }
+  if (i == mp.n || !mp.mo.name_data) return;
+  const uint64_t len = mp.name_len[i + 1] - at;
+  if (at + len > lim) return;
+  const uint8_t* src = mp.in + mp.name_pos[i];
+  for (uint64_t k = 0; k < len; k++) mp.mo.name_data[at + k] = src[k];
+}
+
+__global__ void __launch_bounds__(MT) merge_kernel(const uint8_t* hdr_rc, const uint8_t* body_rc,
+                                                   uint8_t* record_status, uint64_t n, unsigned long long* errkey) {
+  const uint64_t i = (uint64_t)blockIdx.x * MT + threadIdx.x;
+  if (i >= n) return;
+  const int rc = hdr_rc[i] ? hdr_rc[i] : body_rc[i];
+  if (record_status) record_status[i] = (uint8_t)rc;
+  if (rc) atomicMin(errkey, (unsigned long long)((i << 8) | (uint64_t)(rc & 0xff)));
+}
+
+// the call's status: the first failing message (header or body) wins; else the body decode's own
+// code (an arena overflow), else a name-arena overflow
+__global__ void final_kernel(kx_status* st, const uint64_t* offsets, uint64_t n, unsigned long long* errkey,
+                             uint32_t* overflow) {
+  if (threadIdx.x != 0) return;
+  const unsigned long long k = *errkey;
+  if (k != ~0ull) {
+    st->code = (int32_t)(k & 0xff);
+    st->record = k >> 8;
+    st->offset = offsets[k >> 8];
+  } else if (st->code != KX_ERR_SIZE_LIMIT && st->code != KX_ERR_INTERNAL) {
+    st->code = 0;
+    st->record = 0;
+    st->offset = 0;
+  }
+  if (*overflow && st->code == 0) st->code = KX_ERR_SIZE_LIMIT;
+  st->n_records = n;
+  st->consumed = offsets[n];
+  *errkey = ~0ull;
+  *overflow = 0;
+}
+
+// message workspace: [0] errkey, [8] overflow, then req_start, req_end, name_pos, name_len, hdr_rc, body_rc
+struct MsgWs {
+  size_t req_start, req_end, name_pos, name_len, hdr_rc, body_rc, total;
+};
+
+MsgWs msg_ws(uint64_t n) {
+  MsgWs L{};
+  size_t o = 256;
+  auto take = [&](size_t bytes) { const size_t at = o; o += (bytes + 255) & ~(size_t)255; return at; };
+  L.req_start = take((n + 1) * 8);
+  L.req_end = take((n + 1) * 8);
+  L.name_pos = take((n + 1) * 8);
+  L.name_len = take((n + 1) * 8);
+  L.hdr_rc = take(n + 1);
+  L.body_rc = take(n + 1);
+  L.total = o;
+  return L;
+}
+
+}  // namespace
+
+size_t kx_message_ws_bytes(uint64_t n) { return msg_ws(n).total; }
+
+int kx_launch_message_headers(const uint8_t* in, uint64_t in_len, const uint64_t* offsets, uint64_t n,
+                              int32_t body_field, bool pb, const KxMsgOut& mo, void* mws, uint64_t** req_start,
+                              uint64_t** req_end, uint8_t** hdr_rc, uint8_t** body_rc, hipStream_t stream) {
+  const MsgWs L = msg_ws(n);
+  char* b = (char*)mws;
+  MsgParams mp{};
+  mp.in = in; mp.in_len = in_len; mp.offsets = offsets; mp.n = n; mp.body_field = body_field; mp.mo = mo;
+  mp.pb = pb;
+  mp.req_start = (uint64_t*)(b + L.req_start);
+  mp.req_end = (uint64_t*)(b + L.req_end);
+  mp.name_pos = (uint64_t*)(b + L.name_pos);
+  mp.name_len = (uint64_t*)(b + L.name_len);
+  mp.hdr_rc = (uint8_t*)(b + L.hdr_rc);
+  mp.errkey = (unsigned long long*)b;
+  mp.overflow = (uint32_t*)(b + 8);
+  const unsigned grid = (unsigned)((n + 1 + MT - 1) / MT);
+  hipLaunchKernelGGL(header_kernel, dim3(grid), dim3(MT), 0, stream, mp);
+  KX_HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(ST), 0, stream, mp.name_len, n + 1);
+  KX_HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(name_kernel, dim3(grid), dim3(MT), 0, stream, mp);
+  KX_HIP_CHECK(hipGetLastError());
+  *req_start = mp.req_start;
+  *req_end = mp.req_end;
+  *hdr_rc = mp.hdr_rc;
+  *body_rc = (uint8_t*)(b + L.body_rc);
+  return KX_OK;
+}
+
+int kx_launch_message_merge(const uint64_t* offsets, uint64_t n, const uint8_t* hdr_rc, const uint8_t* body_rc,
+                            uint8_t* record_status, kx_status* status, void* mws, hipStream_t stream) {
+  unsigned long long* errkey = (unsigned long long*)mws;
+  uint32_t* overflow = (uint32_t*)((char*)mws + 8);
+  const unsigned grid = (unsigned)((n + MT - 1) / MT);
+  hipLaunchKernelGGL(merge_kernel, dim3(grid), dim3(MT), 0, stream, hdr_rc, body_rc, record_status, n, errkey);
+  KX_HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(final_kernel, dim3(1), dim3(64), 0, stream, status, offsets, n, errkey, overflow);
+  KX_HIP_CHECK(hipGetLastError());
+  return KX_OK;
+}

@@ -83,6 +83,22 @@ def test_message_begin_matches_kat(kxlib, mtype):
     assert kxlib.kx_thrift_message_begin_length(5) == 17
 
 
+def test_pb_meta_matches_oracle(kxlib, oracle):
+    """Kitex-Protobuf meta header in the product ABI == the oracle's (protobuf.go:77-90,136-165)"""
+    from kitex_amd.codec import ProtocolError, read_pb_meta, write_pb_meta
+    for name, t, seq in (("mock", 1, 7), ("", 2, -1), ("EchoMethod", 3, 1 << 30)):
+        b = write_pb_meta(name, t, seq)
+        assert b == oracle.prim("kxo_pb_write_meta", name.encode(), len(name), t, seq)
+        assert read_pb_meta(b) == (name, t, seq, 12 + len(name))
+    assert kxlib.kx_pb_meta_length(4) == 16
+    with pytest.raises(ProtocolError) as e:
+        read_pb_meta(bytes.fromhex("80010001000000046d6f636b00000007"))   # a thrift header: bad magic
+    assert e.value.code == A.ERR_BAD_VERSION
+    with pytest.raises(ProtocolError) as e:
+        read_pb_meta(bytes.fromhex("9001000100000004"))                   # truncated
+    assert e.value.code == A.ERR_EOF
+
+
 def test_ctx_without_gpu(kxlib):
     import torch
     if torch.cuda.is_available():
