@@ -735,6 +735,61 @@ __device__ __forceinline__ int pb_body(const Src& w, const KAS KxProgram* P, con
   return KX_OK;
 }
 
+// Protobuf canonical plan (the PB counterpart of canon_record): the steps are the root fields in
+// field-number order, the order proto.Marshal writes (protobuf.go:209-216 -> proto.Marshal); every
+// lane runs the same step at once, so each step's descriptor is a scalar load, and a lane whose next
+// tag is not the step's tag has that field absent (proto3 omits zero values) and keeps its default.
+// False when the record has anything else left at the end (unknown or out-of-order fields, a
+// repeated field, a malformed value): the generic field loop then decodes it from the start and
+// reports the error.
+template <int NV>
+__device__ __forceinline__ bool pb_canon(const Src& w, const KAS KxProgram* P, const KAS KxLaunchCols& cols,
+                                         uint64_t start, uint64_t limit, uint64_t rec, bool emit, bool utf8,
+                                         VarState<NV>& vs, uint64_t& pres_out) {
+  uint64_t pos = start, pres = 0;
+  const uint32_t ns = P->npbsteps;
+  for (uint32_t k = 0; k < ns; k++) {
+    const KxpStep S = ldk(&P->pbsteps[k]);
+    const uint32_t tl = (S.hdr >> 16) & 3u;
+    const KxpCol K = ld_col(P, S.col);
+    bool present = false;
+    if (pos < limit) {
+      const Fetch f = fetch12(w, pos);
+      present = (f.w0 & (tl == 1 ? 0xffu : 0xffffu)) == (S.hdr & 0xffffu) && limit - pos > tl;
+      if (present) {
+        const uint64_t rem = limit - pos - tl;
+        const Fetch fv = fetch_skip(f, tl);
+        uint64_t v;
+        uint32_t u;
+        if (S.kind == KXP_S_PB_VARINT) {
+          if (pb_varint_f(fv, rem, v, u)) return false;
+          if ((S.hdr >> 24) & 1u) v = v != 0;
+          if (emit) store_col(cols.data[S.col], S.width, rec, v);  // int32: low 32 bits
+          pos += tl + u;
+        } else if (S.kind == KXP_S_PB_FIXED64) {
+          if (rem < 8) return false;
+          if (emit) store_col(cols.data[S.col], S.width, rec, (uint64_t)fv.w0 | ((uint64_t)fv.w1 << 32));
+          pos += tl + 8;
+        } else {
+          if (pb_varint_f(fv, rem, v, u) || v > rem - u) return false;
+          const uint64_t b = pos + tl + u;
+          if (utf8 && !((S.hdr >> 25) & 1u) && !pb_utf8_ok(w, b, v)) return false;
+          vset<NV>(vs, S.vslot, b, (uint32_t)v);
+          pos = b + v;
+        }
+        if (K.field >= 0) {
+          const int8_t pb = ld_field(P, K.field).pbit;
+          if (pb >= 0) pres |= 1ull << pb;
+        }
+      }
+    }
+    if (!present && emit && S.kind != KXP_S_PB_LEN) store_col(cols.data[S.col], S.width, rec, (uint64_t)K.defv);
+  }
+  if (pos != limit) return false;
+  pres_out = pres;
+  return true;
+}
+
 // ---------------------------------------------------------------------------------------------
 // variable-length payload copy (strings: raw bytes; lists: big-endian elements -> host order)
 // ---------------------------------------------------------------------------------------------
@@ -1056,7 +1111,8 @@ __device__ __forceinline__ Src load_window(KParams& dp, LDS uint32_t* win, uint6
 // One record: FastRead (emit) or its length / var extents only (measure).
 template <int NV, int MODE>
 __device__ __forceinline__ int parse_record(KParams& dp, const Src& w, uint64_t pos, uint64_t lim, uint64_t r,
-                                            bool emit, uint64_t* end, VarState<NV>& vs, uint64_t& pres) {
+                                            bool emit, uint64_t* end, VarState<NV>& vs, uint64_t& pres,
+                                            bool canon_only = false) {
 #pragma unroll
   for (int v = 0; v < NV; v++) { vs.len[v] = 0; vs.pos[v] = 0; }
   pres = 0;
@@ -1065,6 +1121,7 @@ __device__ __forceinline__ int parse_record(KParams& dp, const Src& w, uint64_t 
       pres = w.canon_pres;
       return KX_OK;
     }
+    if (canon_only) return KX_ERR_INVALID_DATA;
     return generic_record<NV>(w, dp.prog, dp.cols, pos, lim, r, emit, end, vs, pres);
   }
   if (MODE == M_PB) {
@@ -1083,7 +1140,9 @@ __device__ __forceinline__ int parse_record(KParams& dp, const Src& w, uint64_t 
     *end = e;
     // concatenated mode: the index pass already validated every record the chain reaches, so the
     // emit pass skips the UTF-8 check; with known extents the emit pass is the validator
-    return pb_body<NV>(w, dp.prog, dp.cols, b, e, r, emit, vs, pres, !emit || dp.offsets != nullptr);
+    const bool utf8 = !emit || dp.offsets != nullptr;
+    if (dp.prog->npbsteps && pb_canon<NV>(w, dp.prog, dp.cols, b, e, r, emit, utf8, vs, pres)) return KX_OK;
+    return pb_body<NV>(w, dp.prog, dp.cols, b, e, r, emit, vs, pres, utf8);
   }
   uint64_t p2 = pos;
   const int rc = dskip_body(w, p2, lim, KX_T_STRUCT, 64);
@@ -1095,6 +1154,96 @@ struct Agg {
   uint64_t ent, ex, cnt, errc, errp;
   uint64_t var[KXP_NV_MAX];
 };
+
+// Record signature taken from the data: the first record's first 3 bytes. The schema's canonical
+// signature (encoder-first field header) is used when the batch's first record starts with it;
+// otherwise (an IDL-order producer, an unset optional first field, the schema-less skip decoder) the
+// first record's own header is: records of one batch normally start alike.
+__device__ __forceinline__ uint32_t data_sig(KParams& dp) {
+  if (dp.in_len < 3 || dp.offsets) return 0;
+  const GLB uint8_t* p = (const GLB uint8_t*)dp.in;
+  return __builtin_amdgcn_readfirstlane((uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16));
+}
+
+// The lane's speculation: its segment's boundary signature, and the first signature hit. A hit is
+// a guess; a guess whose own walk fails is replaced by the next hit (walk_tile), so payload bytes
+// that contain the signature (binary strings saturated with it, strings holding serialized records)
+// cost extra walks of the lanes they fall in, never the serial chain repair.
+struct Cand {
+  uint64_t ent;     // first hit (X_NONE: none)
+  uint64_t plim;    // hits are < plim
+  uint32_t sig, smask;
+  uint32_t s2o, s2; // canonical second-header pre-check for later hits (s2o = 0: none)
+  bool strict;      // several hits in the segment: a guess must parse as a canonical record
+};
+
+template <int NV, int MODE>
+__device__ __forceinline__ Cand lane_candidate(KParams& dp, const Src& w, uint64_t seg_lo, uint64_t seg_hi, int lane) {
+  Cand cd;
+  cd.ent = X_NONE; cd.plim = seg_lo; cd.sig = 0; cd.smask = 0xffu; cd.s2o = 0; cd.s2 = 0; cd.strict = false;
+  if (seg_lo >= seg_hi) return cd;
+  if (MODE == M_PB) {
+    cd.ent = pb_scan_segment(w, seg_lo, seg_hi, dp.in_len, lane);
+    return cd;
+  }
+  const KAS KxProgram* P = dp.prog;
+  const uint32_t dsig = data_sig(dp);
+  const bool dok = dsig != 0 && canon_t(dsig & 0xff) != 1;  // the first record starts with a field header
+  uint32_t sig, slen;
+  bool own = false;
+  if (MODE == M_THRIFT && P->sig_len == 3 && (!dok || dsig == P->sig)) {
+    sig = P->sig; slen = 3; own = true;
+  } else if (dok) {
+    sig = dsig; slen = 3;
+  } else if (MODE == M_THRIFT) {
+    sig = P->sig; slen = P->sig_len;
+  } else {
+    sig = KX_T_STOP; slen = 1;
+  }
+  const uint64_t plim = kmin64(seg_hi, dp.in_len >= slen ? dp.in_len - slen + 1 : 0ull);
+  cd.plim = plim; cd.sig = sig; cd.smask = slen == 3 ? 0xffffffu : 0xffu;
+  if (own && w.nsteps) { cd.s2o = P->sig2_off; cd.s2 = P->sig2; }
+  const int32_t q0 = wofs(w, seg_lo, SEG + 12);
+  if (slen == 3 && seg_hi - seg_lo == SEG && q0 >= 0 && own && P->sig_ambig && w.nsteps) {
+    // the signature also starts a nested struct (whose walk would succeed): keep the lowest of the
+    // two lowest hits that parses as a canonical record, else no candidate
+    uint32_t c1, c2;
+    scan_segment2(w, q0, sig, lane, c1, c2);
+    VarState<NV> vs0;
+    uint64_t e0;
+    if (c1 < (uint32_t)SEG && seg_lo + c1 < plim &&
+        canon_record<NV>(w, dp.cols, seg_lo + c1, dp.in_len, 0, false, &e0, vs0))
+      cd.ent = seg_lo + c1;
+    else if (c2 < (uint32_t)SEG && seg_lo + c2 < plim &&
+             canon_record<NV>(w, dp.cols, seg_lo + c2, dp.in_len, 0, false, &e0, vs0))
+      cd.ent = seg_lo + c2;
+    cd.plim = seg_lo;  // no further hits are tried
+  } else if (slen == 3 && seg_hi - seg_lo == SEG && q0 >= 0 && own && w.nsteps) {
+    // a second hit means the signature also occurs inside payload bytes: a guess must then parse as a
+    // canonical record (a run of fields that merely parses, e.g. a serialized record held in a
+    // string, would be followed and would merge into the true chain a record late)
+    uint32_t c1, c2;
+    scan_segment2(w, q0, sig, lane, c1, c2);
+    cd.ent = c1 < (uint32_t)SEG && seg_lo + c1 < plim ? seg_lo + c1 : X_NONE;
+    cd.strict = c2 < (uint32_t)SEG;
+  } else if (slen == 3 && seg_hi - seg_lo == SEG && q0 >= 0) {
+    cd.ent = scan_segment(w, q0, seg_lo, plim, sig, lane);
+  } else {
+    for (uint64_t p = seg_lo; p < plim; p++)
+      if ((ld4(w, p) & cd.smask) == sig) { cd.ent = p; break; }
+  }
+  return cd;
+}
+
+// the next signature hit after p (exclusive) in the lane's segment, or X_NONE
+__device__ __forceinline__ uint64_t next_hit(KParams& dp, const Src& w, const Cand& cd, uint64_t p) {
+  for (uint64_t q = p + 1; q < cd.plim; q++) {
+    if ((ld4(w, q) & cd.smask) != cd.sig) continue;
+    if (cd.s2o && (q + cd.s2o + 3 > dp.in_len || (ld4(w, q + cd.s2o) & 0xffffffu) != cd.s2)) continue;
+    return q;
+  }
+  return X_NONE;
+}
 
 // Concatenated mode, one wave, one tile [tlo, thi) in the LDS window. Lane l owns the 128-byte
 // segment l: it starts at the first canonical record signature in its segment (or where the chain
@@ -1108,35 +1257,8 @@ __device__ Agg walk_tile(KParams& dp, const Src& w, uint64_t tlo, uint64_t thi, 
   const KAS KxProgram* P = dp.prog;
   const uint64_t seg_lo = tlo + (uint64_t)lane * SEG;
   const uint64_t seg_hi = kmin64(seg_lo + SEG, thi);
-  uint64_t ent = X_NONE;
-  if (seg_lo < thi && MODE == M_PB) {
-    ent = pb_scan_segment(w, seg_lo, seg_hi, dp.in_len, lane);
-  } else if (seg_lo < thi) {
-    const uint32_t sig = MODE == M_THRIFT ? P->sig : (uint32_t)KX_T_STOP;
-    const uint32_t slen = (MODE == M_THRIFT && P->sig_len == 3) ? 3u : 1u;
-    const uint64_t plim = kmin64(seg_hi, dp.in_len >= slen ? dp.in_len - slen + 1 : 0ull);
-    const int32_t q0 = wofs(w, seg_lo, SEG + 12);
-    if (slen == 3 && seg_hi - seg_lo == SEG && q0 >= 0 && MODE == M_THRIFT && P->sig_ambig && w.nsteps) {
-      // the signature also starts a nested struct: keep the lowest of the two lowest hits that parses
-      // as a canonical record (a nested-struct start does not), else no candidate (speculation only)
-      uint32_t c1, c2;
-      scan_segment2(w, q0, sig, lane, c1, c2);
-      VarState<NV> vs0;
-      uint64_t e0;
-      if (c1 < (uint32_t)SEG && seg_lo + c1 < plim &&
-          canon_record<NV>(w, dp.cols, seg_lo + c1, dp.in_len, 0, false, &e0, vs0))
-        ent = seg_lo + c1;
-      else if (c2 < (uint32_t)SEG && seg_lo + c2 < plim &&
-               canon_record<NV>(w, dp.cols, seg_lo + c2, dp.in_len, 0, false, &e0, vs0))
-        ent = seg_lo + c2;
-    } else if (slen == 3 && seg_hi - seg_lo == SEG && q0 >= 0) {
-      ent = scan_segment(w, q0, seg_lo, plim, sig, lane);
-    } else {
-      const uint32_t smask = slen == 3 ? 0xffffffu : 0xffu;
-      for (uint64_t p = seg_lo; p < plim; p++)
-        if ((ld4(w, p) & smask) == sig) { ent = p; break; }
-    }
-  }
+  const Cand cd = lane_candidate<NV, MODE>(dp, w, seg_lo, seg_hi, lane);
+  uint64_t ent = cd.ent;
   if (dp.diag & 512) {  // diagnostics: DMA + candidate scan only
     Agg a;
     a.ent = __ballot(ent != X_NONE) ? ent : X_NONE; a.ex = thi; a.cnt = 0; a.errc = 0; a.errp = 0;
@@ -1173,7 +1295,8 @@ __device__ Agg walk_tile(KParams& dp, const Src& w, uint64_t tlo, uint64_t thi, 
       while (pos < seg_hi && pos < dp.in_len) {
         VarState<NV> vs;
         uint64_t end = pos, pres;
-        const int rc = parse_record<NV, MODE>(dp, w, pos, dp.in_len, 0, false, &end, vs, pres);
+        const bool strict = cd.strict && c == 0 && rounds == 0 && seed == X_NONE && !enumerate;
+        const int rc = parse_record<NV, MODE>(dp, w, pos, dp.in_len, 0, false, &end, vs, pres, strict);
         if (rc) { e = rc; break; }
         if (!enumerate) {
           st0 = c == 0 ? pos : st0; st1 = c == 1 ? pos : st1;
@@ -1195,6 +1318,16 @@ __device__ Agg walk_tile(KParams& dp, const Src& w, uint64_t tlo, uint64_t thi, 
     }
     need = false;
     if (enumerate) break;
+    if (rounds == 0 && seed == X_NONE && ent != X_NONE && ex == X_ERR) {
+      // speculating: a candidate whose own walk fails was a false signature hit, not the chain's end;
+      // the lane tries its next hit (or has no candidate)
+      ent = next_hit(dp, w, cd, ent);
+      need = ent != X_NONE;
+      ex = X_NONE; cnt = 0; errc = 0;
+#pragma unroll
+      for (int v = 0; v < NV; v++) vsum[v] = 0;
+    }
+    if (__ballot(need)) continue;  // uniform: lanes re-walk their next hit before the repair round
     phase(2);
 
     // ---- one repair round: every lane must start at the first true record start in its segment,
@@ -1430,7 +1563,7 @@ __device__ void group_scan(KParams& dp, LDS uint32_t* win, uint64_t g, uint64_t 
 
 // ---- kernel 1: index pass (one wave per tile) ----
 template <int NV, int MODE>
-__global__ void __launch_bounds__(NT) index_kernel(DecParams dp_) {
+__global__ void __launch_bounds__(NT, 4) index_kernel(DecParams dp_) {  // 4 waves per SIMD: <= 128 VGPRs
   KParams& dp = KX_PARAMS();
   (void)dp_;
   __shared__ __attribute__((aligned(16))) uint32_t WIN[WAVES][WINW];

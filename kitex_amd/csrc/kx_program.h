@@ -67,7 +67,8 @@ struct KxpCol {        // 16 B
 // Canonical plan: the byte layout every record written by the encoder has (encoder order, all
 // non-optional fields present, nil-free structs). Executed as a straight line of steps; a record
 // that deviates at any step is re-parsed by the generic field loop.
-enum : uint8_t { KXP_S_FIXED = 1, KXP_S_BYTES = 2, KXP_S_LIST = 3, KXP_S_STRUCT = 4, KXP_S_END = 5 };
+enum : uint8_t { KXP_S_FIXED = 1, KXP_S_BYTES = 2, KXP_S_LIST = 3, KXP_S_STRUCT = 4, KXP_S_END = 5,
+                 KXP_S_PB_VARINT = 6, KXP_S_PB_FIXED64 = 7, KXP_S_PB_LEN = 8 };
 #define KXP_MAX_STEPS 96
 
 struct KxpStep {       // 8 B
@@ -93,8 +94,13 @@ struct KxProgram {
   int32_t pb_first;      // first root field in field-number order (protobuf encode), -1 if none
   uint64_t canon_pres;   // presence word of a canonical record
   uint32_t sig_ambig;    // the signature is also the first header of a nested struct: validate candidates
-  uint32_t pad1;
+  uint32_t sig2_off;     // canonical record: offset of the second field header (0: not fixed)
+  uint32_t sig2;         // ... and its 3 bytes (a cheap pre-check before a full canonical parse)
+  uint32_t npbsteps;     // protobuf canonical plan length (root fields in number order), 0 = none
   KxpStep steps[KXP_MAX_STEPS];
+  // Protobuf canonical plan: one step per root field in field-number order (proto.Marshal's order);
+  // hdr = tag bytes (bits 0-15) | tag length (16-17) | bool (bit 24) | bytes, no UTF-8 check (25)
+  KxpStep pbsteps[KXP_MAX_FIELDS];
 };
 
 static_assert(sizeof(KxpField) == 16, "KxpField layout");

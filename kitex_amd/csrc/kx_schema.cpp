@@ -242,6 +242,27 @@ int kx_build_program(const kx_struct_desc* structs, uint32_t nstructs, kx_schema
     std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return P.f[a].id < P.f[b].id; });
     P.pb_first = ord.empty() ? -1 : ord[0];
     for (size_t o = 0; o < ord.size(); o++) P.f[ord[o]].pb_next = o + 1 < ord.size() ? (int8_t)ord[o + 1] : (int8_t)-1;
+    // canonical plan: every root field in number order, each a scalar or string with a tag of <= 2
+    // bytes (field numbers < 2048); any other shape decodes through the generic field loop only
+    P.npbsteps = 0;
+    bool ok = P.ninst == 1 && !ord.empty();
+    for (size_t o = 0; ok && o < ord.size(); o++) {
+      const KxpField& F = P.f[ord[o]];
+      if (F.pb_wt == 7 || F.id <= 0 || F.id >= 2048 || (F.kind != KXP_K_FIXED && F.kind != KXP_K_BYTES)) {
+        ok = false;
+        break;
+      }
+      const uint32_t tag = ((uint32_t)F.id << 3) | F.pb_wt;
+      KxpStep& T = P.pbsteps[o];
+      const uint32_t tb = tag < 0x80 ? tag : ((tag & 0x7f) | 0x80) | ((tag >> 7) << 8);
+      T.hdr = tb | ((tag < 0x80 ? 1u : 2u) << 16) | ((F.ttype == KX_T_BOOL ? 1u : 0u) << 24) |
+              ((F.flags & 1u) << 25);
+      T.kind = F.pb_wt == 0 ? KXP_S_PB_VARINT : F.pb_wt == 1 ? KXP_S_PB_FIXED64 : KXP_S_PB_LEN;
+      T.width = F.width;
+      T.col = F.col;
+      T.vslot = F.vslot;
+    }
+    if (ok) P.npbsteps = (uint32_t)ord.size();
   }
 
   // canonical first bytes of a record (speculative boundary signature)
@@ -259,6 +280,16 @@ int kx_build_program(const kx_struct_desc* structs, uint32_t nstructs, kx_schema
       const KxpField& G = P.f[ef];
       const uint32_t h = (uint32_t)G.ttype | ((uint32_t)((uint16_t)G.id >> 8) << 8) | ((uint32_t)(G.id & 0xff) << 16);
       if (h == P.sig) P.sig_ambig = 1;
+    }
+    // a fixed-width, always-written first field puts the second field's header at a fixed offset
+    P.sig2_off = 0;
+    P.sig2 = 0;
+    if (F.kind == KXP_K_FIXED && F.req != KX_REQ_OPTIONAL && F.enc_next >= 0) {
+      const KxpField& G = P.f[F.enc_next];
+      if (G.req != KX_REQ_OPTIONAL) {
+        P.sig2_off = 3u + F.width;
+        P.sig2 = (uint32_t)G.ttype | ((uint32_t)((uint16_t)G.id >> 8) << 8) | ((uint32_t)(G.id & 0xff) << 16);
+      }
     }
   } else {
     P.sig = 0;

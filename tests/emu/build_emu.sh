@@ -16,7 +16,7 @@ sed -e 's/^#define LDS __attribute__((address_space(3)))/#define LDS/' \
     -e 's/asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");/emu_wait_vmcnt0();/' \
     $ROOT/kitex_amd/csrc/kx_decode.hip > _build/kx_decode_emu.cpp
 CXX=${CXX:-/opt/rocm/lib/llvm/bin/clang++}
-FLAGS="-std=c++17 -O1 -g -fPIC -Wno-unknown-attributes -Wno-unused-function -I. -I$ROOT/kitex_amd/csrc"
+FLAGS="-std=c++17 -O1 -g -fPIC -Wno-unknown-attributes -Wno-unused-function -I. -I$ROOT/kitex_amd/csrc ${EMU_EXTRA:-}"
 $CXX $FLAGS -c _build/kx_decode_emu.cpp -o _build/kx_decode_emu.o
 $CXX $FLAGS -c $ROOT/kitex_amd/csrc/kx_schema.cpp -o _build/kx_schema.o
 $CXX $FLAGS -c emu_rt.cpp -o _build/emu_rt.o

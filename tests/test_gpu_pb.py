@@ -114,3 +114,20 @@ def test_pb_marshal_unmarshal_roundtrip_device(torch):
             assert torch.equal(got[0][:n + 1], col[0][:n + 1]) and torch.equal(got[1][:col[1].numel()], col[1])
         else:
             assert torch.equal(got[:n], col)
+
+
+def test_pb_golden_fixture_on_gpu(torch, oracle):
+    """tests/golden/pf_batch_64.bin (google.protobuf serialization, pinned by the oracle) decoded by
+    kx_pb_decode_batch: the generator's 64 records field-for-field"""
+    import os
+
+    from kitex_amd.codec import ProtobufCodec
+    golden = np.fromfile(os.path.join(os.path.dirname(__file__), "golden", "pf_batch_64.bin"), dtype=np.uint8)
+    sch = S.schema_pf()
+    cdc = ProtobufCodec(sch)
+    dev = torch.device("cuda", 0)
+    res = cdc.Unmarshal(torch.from_numpy(golden).to(dev), 64)
+    st = res.read_status()
+    assert st.code == 0 and st.n_records == 64 and st.consumed == golden.size
+    _, infos, _ = oracle.flatten(sch)
+    assert_columns_equal(res.columns, synth.gen_pf(64), infos, 64)

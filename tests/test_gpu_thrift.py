@@ -287,3 +287,37 @@ def test_side_streams_status_and_workspaces(torch, dev, oracle):
         assert_columns_equal(r.columns, exp, infos, est.n_records)
     with pytest.raises(ProtocolError):
         cdc.Unmarshal(batches[1][1], batches[1][0].n, stream=s2)
+
+
+# ---------------------------------------------------------------------------------------------
+# the reference's own skip-decoder vectors through kx_thrift_skip_batch (codec_apache_test.go)
+# ---------------------------------------------------------------------------------------------
+def test_skip_batch_reference_fixture(torch, dev, oracle):
+    """genTestSkipDecoderBytes (codec_apache_test.go:115-184: map<i64,double>, map<string,i64>,
+    map<i64,struct>, list<struct>, nested struct) repeated 3000x, skipped on the GPU"""
+    from kitex_amd.codec import ThriftCodec
+    from tests.test_oracle_kat import gen_test_skip_decoder_bytes
+    one = gen_test_skip_decoder_bytes(oracle)
+    assert oracle.skip(one, A.T_STRUCT) == (0, len(one))
+    n = 3000
+    wire = np.frombuffer(one * n, dtype=np.uint8).copy()
+    cdc = ThriftCodec(S.schema_r1())
+    offs = to_np(cdc.Skip(torch.from_numpy(wire).to(dev), n))
+    assert np.array_equal(offs, np.arange(n + 1, dtype=np.int64) * len(one))
+
+
+def test_skip_batch_truncated_vector(torch, dev, oracle):
+    """codec_apache_test.go:38-54: a struct cut after its first field header fails with EOF, at the
+    same record and offset as the oracle"""
+    from kitex_amd.codec import ProtocolError, ThriftCodec
+    P = oracle.prim
+    good = P("kxo_write_field_begin", A.T_BOOL, 1) + P("kxo_write_bool", 1) + P("kxo_write_field_stop")
+    cut = P("kxo_write_field_begin", A.T_BOOL, 1)
+    n = 5000
+    wire = np.frombuffer(good * (n - 1) + cut, dtype=np.uint8).copy()
+    exp_rc, exp_offs, done = oracle.skip_batch(wire, n)
+    assert exp_rc == A.ERR_EOF and done == n - 1
+    cdc = ThriftCodec(S.schema_r1())
+    with pytest.raises(ProtocolError) as e:
+        cdc.Skip(torch.from_numpy(wire).to(dev), n)
+    assert (e.value.code, e.value.record, e.value.offset) == (A.ERR_EOF, n - 1, len(good) * (n - 1))
