@@ -426,25 +426,61 @@ def extras(args, r2, dev, local):
 
 
 def host_inclusive(b, dev):
-    """Pinned host -> HBM copy + decode + columns back to pinned host (the netpoll-buffer path),
-    through the library's own chunked, double-buffered kx_host_decode_batch when available."""
+    """The netpoll-buffer path: records start and end in host memory. Measured through the library's
+    kx_host_decode_batch from pinned buffers with message offsets known (the RPC case: framing gives
+    every message's length), which pipelines 8 record-range chunks so H2D, decode and D2H overlap;
+    plus the serial H2D -> decode -> D2H of the concatenated batch for comparison."""
+    import numpy as np
     import torch
 
+    from kitex_amd import _abi as A
     from kitex_amd.columns import alloc_device
-    h_in = torch.empty(b.wire.numel(), dtype=torch.uint8, pin_memory=True)
+
+    def pinned(n, dtype):
+        return torch.empty(max(1, n), dtype=dtype, pin_memory=True)
+
+    h_in = pinned(b.wire.numel(), torch.uint8)
     h_in.copy_(b.wire)
+    h_off = pinned(b.n + 1, torch.int64)
+    h_off.copy_(b.offs)
+    infos, n = b.infos, b.n
+    cols = []
+    for c, ci in enumerate(infos):
+        if ci.kind == A.COL_FIXED:
+            cols.append(pinned(n * ci.width, torch.uint8).numpy().view(np.dtype(f"<u{ci.width}")
+                                                                         if ci.width > 1 else np.uint8))
+        else:
+            w = 1 if ci.kind == A.COL_BYTES else ci.width
+            cols.append((pinned(n + 1, torch.int32).numpy().view(np.uint32),
+                         pinned(b.var_caps[c] * w, torch.uint8).numpy()))
+    from kitex_amd.synth import ColumnSet
+    pres = pinned(n, torch.int64).numpy().view(np.uint64) if b.cdc.dschema.npresence else None
+    hout = ColumnSet(cols, pres, n)
+    wire_np, off_np = h_in.numpy(), h_off.numpy().view(np.uint64)
+    best = 1e30
+    for _ in range(4):
+        t0 = time.perf_counter()
+        _, st = b.cdc.UnmarshalHost(wire_np, n, offsets=off_np, var_caps=b.var_caps, out=hout, raise_on_error=False)
+        best = min(best, time.perf_counter() - t0)
+    ok = st.code == 0 and st.n_records == n
+    ok &= bool(np.array_equal(cols[0][:n].view(np.int64), b.src.cols[0][:n].cpu().numpy()))
+    out_bytes = sum((c[0].nbytes + c[1].nbytes) if isinstance(c, tuple) else c.nbytes for c in cols)
+    res = {"records_per_s": n / best, "ms": best * 1e3, "h2d_bytes": b.wire.numel() + (n + 1) * 8,
+           "d2h_bytes": out_bytes, "pcie_gb_s": (b.wire.numel() + out_bytes) / best / 1e9, "verified": ok,
+           "note": "kx_host_decode_batch from pinned host buffers, message offsets known: 16-chunk pipeline, "
+                   "H2D / decode / D2H of different chunks overlap"}
+    # serial reference: the concatenated batch, H2D -> decode -> D2H on one stream
     d_in = torch.empty_like(b.wire)
-    out = alloc_device(b.infos, b.n, b.var_caps, b.cdc.dschema.npresence, dev)
+    out = alloc_device(infos, n, b.var_caps, b.cdc.dschema.npresence, dev)
     h_out = [((torch.empty(c[0].numel(), dtype=c[0].dtype, pin_memory=True),
                torch.empty(c[1].numel(), dtype=c[1].dtype, pin_memory=True)) if isinstance(c, tuple)
               else torch.empty(c.numel(), dtype=c.dtype, pin_memory=True)) for c in out.cols]
-    reps = 3
-    best = 1e30
-    for _ in range(reps + 1):
+    sbest = 1e30
+    for _ in range(3):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        d_in.copy_(h_in, non_blocking=True)
-        b.cdc.Unmarshal(d_in, b.n, offsets=b.offsets, out=out, var_caps=b.var_caps, raise_on_error=False)
+        d_in.copy_(h_in[:b.wire.numel()], non_blocking=True)
+        b.cdc.Unmarshal(d_in, n, out=out, var_caps=b.var_caps, raise_on_error=False)
         for ho, c in zip(h_out, out.cols):
             if isinstance(c, tuple):
                 ho[0].copy_(c[0], non_blocking=True)
@@ -452,12 +488,10 @@ def host_inclusive(b, dev):
             else:
                 ho.copy_(c, non_blocking=True)
         torch.cuda.synchronize()
-        best = min(best, time.perf_counter() - t0)
-    out_bytes = sum((c[0].numel() * c[0].element_size() + c[1].numel() * c[1].element_size())
-                    if isinstance(c, tuple) else c.numel() * c.element_size() for c in out.cols)
-    return {"records_per_s": b.n / best, "ms": best * 1e3, "h2d_bytes": b.wire.numel(), "d2h_bytes": out_bytes,
-            "pcie_gb_s": (b.wire.numel() + out_bytes) / best / 1e9,
-            "note": "pinned H2D + decode + D2H, serial on one stream (PCIe-bound)"}
+        sbest = min(sbest, time.perf_counter() - t0)
+    res["serial_concat"] = {"records_per_s": n / sbest, "ms": sbest * 1e3,
+                            "note": "concatenated batch (no offsets): pinned H2D, decode, D2H serial on one stream"}
+    return res
 
 
 def cpu_baseline(cfg, nrec):

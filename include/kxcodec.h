@@ -26,7 +26,11 @@
  *   kx_pb_encode_batch .......... proto.Marshal of the Kitex-Protobuf body (protobuf.go:64-134,
  *                                 deterministic field-number order) as a `repeated Rec recs = 1` stream
  *   kx_host_decode_batch ........ fastUnmarshal end to end from host (netpoll) memory: pinned H2D ->
- *                                 decode -> D2H (codec_fast.go:60-82 with the Next(dataLen) slice)
+ *                                 decode -> D2H (codec_fast.go:60-82 with the Next(dataLen) slice);
+ *                                 kx_host_pb_decode_batch the same for protobufCodec.Unmarshal bodies
+ *   kx_thrift_decode_messages ... thriftCodec.Unmarshal over N framed messages (thrift.go:180-225):
+ *                                 MessageBegin + Args{1: req} (k-mock.go:422-517) on the device
+ *   kx_pb_decode_messages ....... protobufCodec.Unmarshal over N framed messages (protobuf.go:136-216)
  *   kx_strerror ................. error text; codes mirror pkg/remote/codec/perrors/protocol_error.go:28-36
  */
 #ifndef KXCODEC_H_
@@ -213,10 +217,17 @@ int kx_pb_encode_batch(kx_ctx* c, const kx_schema* s, const kx_columns* in, uint
                        kx_status* status, void* stream);
 
 /* ---- host-memory entry point (the netpoll buffer side) ----
- * in / out columns / status are HOST memory (pinned or pageable). Synchronous. */
+ * in / out columns / status are HOST memory (pinned for full PCIe rate, or pageable). Synchronous.
+ * With offsets (each message's length known from its framing) the batch is a pipeline of 16
+ * record-range chunks over three streams of the ctx: H2D, decode and D2H of different chunks
+ * overlap. Without offsets: H2D, decode, D2H in sequence. */
 int kx_host_decode_batch(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len,
                          const uint64_t* offsets, uint64_t n, const kx_columns* out,
                          kx_status* status);
+/* The same for Kitex-Protobuf bodies (offsets semantics as kx_pb_decode_batch). */
+int kx_host_pb_decode_batch(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len,
+                            const uint64_t* offsets, uint64_t n, const kx_columns* out,
+                            kx_status* status);
 
 /* ---- message level: N framed RPC messages (framing already removed by the transport) ----
  * message i = in[offsets[i] .. offsets[i+1]) (u64, n+1 entries, device).

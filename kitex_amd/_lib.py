@@ -21,7 +21,7 @@ EXPORTS = [
     "kx_schema_column_info", "kx_schema_presence_bits", "kx_schema_min_record_size", "kx_ctx_create",
     "kx_ctx_destroy", "kx_thrift_decode_batch", "kx_thrift_skip_batch", "kx_thrift_encoded_size_batch",
     "kx_thrift_encode_batch", "kx_pb_decode_batch", "kx_pb_encoded_size_batch",
-    "kx_pb_encode_batch", "kx_host_decode_batch",
+    "kx_pb_encode_batch", "kx_host_decode_batch", "kx_host_pb_decode_batch",
     "kx_thrift_message_begin_length", "kx_thrift_write_message_begin", "kx_thrift_read_message_begin",
     "kx_thrift_decode_messages", "kx_pb_decode_messages", "kx_pb_meta_length", "kx_pb_write_meta",
     "kx_pb_read_meta",
@@ -77,6 +77,7 @@ def lib():
     L.kx_pb_encoded_size_batch.argtypes = L.kx_thrift_encoded_size_batch.argtypes
     L.kx_pb_encode_batch.argtypes = L.kx_thrift_encode_batch.argtypes
     L.kx_host_decode_batch.argtypes = [vp, vp, vp, u64, vp, u64, C.POINTER(A.Columns), C.POINTER(A.Status)]
+    L.kx_host_pb_decode_batch.argtypes = L.kx_host_decode_batch.argtypes
     L.kx_thrift_message_begin_length.argtypes = [u32]
     L.kx_thrift_message_begin_length.restype = u64
     L.kx_thrift_write_message_begin.argtypes = [vp, u64, C.c_char_p, u32, i32, i32, C.POINTER(u64)]

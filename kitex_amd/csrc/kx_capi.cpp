@@ -210,6 +210,8 @@ void kx_ctx_destroy(kx_ctx* c) {
   if (c->pin) (void)hipHostFree(c->pin);
   if (c->dstage) (void)hipFree(c->dstage);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+  if (c->h2d_stream) (void)hipStreamDestroy(c->h2d_stream);
+  if (c->d2h_stream) (void)hipStreamDestroy(c->d2h_stream);
   delete c;
 }
 
@@ -423,17 +425,43 @@ int kx_pb_encode_batch(kx_ctx* c, const kx_schema* s, const kx_columns* in, uint
 // fastUnmarshal from host (netpoll) memory: H2D of the wire bytes (+ offsets) into a grow-only
 // device staging area, the device decode, then D2H of exactly the decoded bytes (fixed columns,
 // var offsets, var payloads up to their totals, presence) and the status. One stream, synchronous.
-int kx_host_decode_batch(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len,
-                         const uint64_t* offsets, uint64_t n, const kx_columns* out, kx_status* status) {
+// device decode of one batch (thrift or protobuf body), arena positions starting at var_base
+static int decode_device(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len, const uint64_t* offsets,
+                         uint64_t n, const kx_columns* out, kx_status* status, hipStream_t st, bool pb,
+                         const uint64_t* var_base) {
+  KxLaunchCols lc;
+  int rc = to_launch_cols(s, out, &lc);
+  if (rc) return rc;
+  if (pb && (rc = pb_schema_ok(s))) return rc;
+  KxProgram* dp = nullptr;
+  if ((rc = prog_on_device(const_cast<kx_schema*>(s), c->device, &dp))) return rc;
+  uint64_t epoch = 0;
+  if ((rc = ensure_ws(c, kx_decode_ws_bytes(s->prog, in_len, offsets, n), st, &epoch))) return rc;
+  return kx_launch_decode(dp, s->prog, in, in_len, offsets, n, lc, nullptr, status, c->ws, c->ws_size, epoch, st, pb,
+                          nullptr, var_base);
+}
+
+// fastUnmarshal end to end from host (netpoll) memory. With message offsets (the RPC case: framing
+// gives every message's length) the batch runs as a pipeline of record-range chunks over three
+// streams: H2D of chunk k+1, decode of chunk k and D2H of chunk k-1 overlap (PCIe is full duplex).
+// The input lands at its own offsets in one device buffer, so a chunk decodes with the caller's
+// offsets as they are; each chunk's arena continues where the previous one ended (var_base), which
+// the host learns from the previous chunk's status before launching the next decode. Without
+// offsets the record boundaries are only known after the decode: H2D, decode, D2H in sequence.
+static int host_decode(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len, const uint64_t* offsets,
+                       uint64_t n, const kx_columns* out, kx_status* status, bool pb) {
   if (!c || !s || !status || !out || (!in && in_len)) return KX_ERR_INVALID_ARG;
   if (out->ncols != s->ncols) return KX_ERR_INVALID_ARG;
   int rc = set_device(c);
   if (rc) return rc;
   if (!c->own_stream) KX_HIP_CHECK(hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking));
-  hipStream_t st = c->own_stream;
+  if (!c->h2d_stream) KX_HIP_CHECK(hipStreamCreateWithFlags(&c->h2d_stream, hipStreamNonBlocking));
+  if (!c->d2h_stream) KX_HIP_CHECK(hipStreamCreateWithFlags(&c->d2h_stream, hipStreamNonBlocking));
+  hipStream_t st = c->own_stream, sh = c->h2d_stream, sd = c->d2h_stream;
+  const uint32_t K = offsets && n >= (1u << 16) ? 16u : 1u;  // chunks
   auto al = [](uint64_t x) { return (x + 255) & ~255ull; };
-  // staging layout: status | input | offsets | columns (fixed data, var offsets + arenas) | presence
-  uint64_t need = al(sizeof(kx_status)) + al(in_len) + (offsets ? al((n + 1) * 8) : 0);
+  // staging layout: K statuses | input | offsets | columns (fixed data, var offsets + arenas) | presence
+  uint64_t need = al(K * sizeof(kx_status)) + al(in_len) + (offsets ? al((n + 1) * 8) : 0);
   for (uint32_t k = 0; k < s->ncols; k++) {
     const kx_column_info& ci = s->info[k];
     if (ci.kind == KX_COL_FIXED) need += al(n * ci.width);
@@ -449,7 +477,7 @@ int kx_host_decode_batch(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint6
     c->dstage_size = need;
   }
   char* p = (char*)c->dstage;
-  kx_status* d_st = (kx_status*)p; p += al(sizeof(kx_status));
+  kx_status* d_st = (kx_status*)p; p += al(K * sizeof(kx_status));
   uint8_t* d_in = (uint8_t*)p; p += al(in_len);
   uint64_t* d_off = nullptr;
   if (offsets) { d_off = (uint64_t*)p; p += al((n + 1) * 8); }
@@ -468,33 +496,128 @@ int kx_host_decode_batch(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint6
     }
   }
   if (s->npres) { dc.presence = (uint64_t*)p; p += al(n * 8); }
-  if (in_len) KX_HIP_CHECK(hipMemcpyAsync(d_in, in, in_len, hipMemcpyHostToDevice, st));
-  if (offsets) KX_HIP_CHECK(hipMemcpyAsync(d_off, offsets, (n + 1) * 8, hipMemcpyHostToDevice, st));
-  rc = kx_thrift_decode_batch(c, s, d_in, in_len, d_off, n, &dc, nullptr, d_st, st);
-  if (rc) return rc;
-  KX_HIP_CHECK(hipMemcpyAsync(status, d_st, sizeof(kx_status), hipMemcpyDeviceToHost, st));
-  // fixed columns and var offsets are needed whatever the payload totals are
-  for (uint32_t k = 0; k < s->ncols; k++) {
-    const kx_column_info& ci = s->info[k];
-    if (ci.kind == KX_COL_FIXED) {
-      if (n) KX_HIP_CHECK(hipMemcpyAsync(out->cols[k].data, dc.cols[k].data, n * ci.width, hipMemcpyDeviceToHost, st));
-    } else {
-      KX_HIP_CHECK(hipMemcpyAsync(out->cols[k].offsets, dc.cols[k].offsets, (n + 1) * dc.cols[k].offset_bytes,
-                                  hipMemcpyDeviceToHost, st));
+  auto unit = [&](uint32_t k) -> uint64_t { return s->info[k].kind == KX_COL_LIST ? s->info[k].width : 1; };
+
+  if (K == 1) {  // serial: H2D, decode, D2H
+    if (in_len) KX_HIP_CHECK(hipMemcpyAsync(d_in, in, in_len, hipMemcpyHostToDevice, st));
+    if (offsets) KX_HIP_CHECK(hipMemcpyAsync(d_off, offsets, (n + 1) * 8, hipMemcpyHostToDevice, st));
+    if (n == 0) {
+      KX_HIP_CHECK(hipStreamSynchronize(st));
+      memset(status, 0, sizeof *status);
+      for (uint32_t k = 0; k < s->ncols; k++)
+        if (s->info[k].kind != KX_COL_FIXED) memset(out->cols[k].offsets, 0, (size_t)offset_width(out->cols[k]));
+      return KX_OK;
+    }
+    if ((rc = decode_device(c, s, d_in, in_len, d_off, n, &dc, d_st, st, pb, nullptr))) return rc;
+    KX_HIP_CHECK(hipMemcpyAsync(status, d_st, sizeof(kx_status), hipMemcpyDeviceToHost, st));
+    for (uint32_t k = 0; k < s->ncols; k++) {
+      const kx_column_info& ci = s->info[k];
+      if (ci.kind == KX_COL_FIXED)
+        KX_HIP_CHECK(hipMemcpyAsync(out->cols[k].data, dc.cols[k].data, n * ci.width, hipMemcpyDeviceToHost, st));
+      else
+        KX_HIP_CHECK(hipMemcpyAsync(out->cols[k].offsets, dc.cols[k].offsets, (n + 1) * dc.cols[k].offset_bytes,
+                                    hipMemcpyDeviceToHost, st));
+    }
+    if (s->npres) KX_HIP_CHECK(hipMemcpyAsync(out->presence, dc.presence, n * 8, hipMemcpyDeviceToHost, st));
+    KX_HIP_CHECK(hipStreamSynchronize(st));
+    // var payloads: only the decoded units (status->var_total per var slot)
+    for (uint32_t v = 0; v < s->prog.nvar && v < KXP_NV_MAX; v++) {
+      const uint32_t k = s->prog.var_col[v];
+      const uint64_t units = status->var_total[v] < out->cols[k].capacity ? status->var_total[v] : out->cols[k].capacity;
+      if (units)
+        KX_HIP_CHECK(hipMemcpyAsync(out->cols[k].data, dc.cols[k].data, units * unit(k), hipMemcpyDeviceToHost, st));
+    }
+    KX_HIP_CHECK(hipStreamSynchronize(st));
+    return KX_OK;
+  }
+
+  // ---- chunked pipeline (offsets known) ----
+  uint64_t r[17];
+  for (uint32_t k = 0; k <= K; k++) r[k] = n * k / K;
+  for (uint32_t k = 0; k < K; k++)
+    if (offsets[r[k + 1]] < offsets[r[k]] || offsets[r[k + 1]] > in_len) return KX_ERR_INVALID_ARG;
+  hipEvent_t ev_in[16], ev_dec[16];
+  for (uint32_t k = 0; k < K; k++) {
+    KX_HIP_CHECK(hipEventCreateWithFlags(&ev_in[k], hipEventDisableTiming));
+    KX_HIP_CHECK(hipEventCreateWithFlags(&ev_dec[k], hipEventDisableTiming));
+  }
+  // every chunk's input lands at its own offsets: the caller's offsets work unchanged on the device
+  KX_HIP_CHECK(hipMemcpyAsync(d_off, offsets, (n + 1) * 8, hipMemcpyHostToDevice, sh));
+  for (uint32_t k = 0; k < K; k++) {
+    const uint64_t a = offsets[r[k]], b = offsets[r[k + 1]];
+    if (b > a) KX_HIP_CHECK(hipMemcpyAsync(d_in + a, in + a, b - a, hipMemcpyHostToDevice, sh));
+    KX_HIP_CHECK(hipEventRecord(ev_in[k], sh));
+  }
+  uint64_t base[KXP_NV_MAX] = {0};
+  kx_status first{};
+  bool failed = false;
+  for (uint32_t k = 0; k < K; k++) {
+    const uint64_t r0 = r[k], nk = r[k + 1] - r[k];
+    kx_columns ck = dc;  // this chunk's window of the output columns
+    for (uint32_t j = 0; j < s->ncols; j++) {
+      const kx_column_info& ci = s->info[j];
+      if (ci.kind == KX_COL_FIXED) ck.cols[j].data = (char*)dc.cols[j].data + r0 * ci.width;
+      else ck.cols[j].offsets = (char*)dc.cols[j].offsets + r0 * dc.cols[j].offset_bytes;
+    }
+    if (dc.presence) ck.presence = dc.presence + r0;
+    KX_HIP_CHECK(hipStreamWaitEvent(st, ev_in[k], 0));
+    if ((rc = decode_device(c, s, d_in, in_len, d_off + r0, nk, &ck, d_st + k, st, pb, base))) return rc;
+    KX_HIP_CHECK(hipEventRecord(ev_dec[k], st));
+    kx_status sk;
+    KX_HIP_CHECK(hipMemcpyAsync(&sk, d_st + k, sizeof sk, hipMemcpyDeviceToHost, st));
+    KX_HIP_CHECK(hipStreamSynchronize(st));  // the next chunk's arena starts where this one ends
+    if (sk.code && !failed) {
+      failed = true;
+      first = sk;
+      first.record += r0;
+    }
+    // D2H of this chunk behind its decode, while the next chunk decodes
+    KX_HIP_CHECK(hipStreamWaitEvent(sd, ev_dec[k], 0));
+    for (uint32_t j = 0; j < s->ncols; j++) {
+      const kx_column_info& ci = s->info[j];
+      if (ci.kind == KX_COL_FIXED) {
+        KX_HIP_CHECK(hipMemcpyAsync((char*)out->cols[j].data + r0 * ci.width, (char*)dc.cols[j].data + r0 * ci.width,
+                                    nk * ci.width, hipMemcpyDeviceToHost, sd));
+      } else {
+        const uint32_t ob = dc.cols[j].offset_bytes;
+        KX_HIP_CHECK(hipMemcpyAsync((char*)out->cols[j].offsets + r0 * ob, (char*)dc.cols[j].offsets + r0 * ob,
+                                    (nk + (k == K - 1 ? 1 : 0)) * ob, hipMemcpyDeviceToHost, sd));
+      }
+    }
+    if (s->npres)
+      KX_HIP_CHECK(hipMemcpyAsync(out->presence + r0, dc.presence + r0, nk * 8, hipMemcpyDeviceToHost, sd));
+    for (uint32_t v = 0; v < s->prog.nvar && v < KXP_NV_MAX; v++) {
+      const uint32_t j = s->prog.var_col[v];
+      const uint64_t cap = out->cols[j].capacity;
+      const uint64_t hi = sk.var_total[v] < cap ? sk.var_total[v] : cap, lo = base[v] < hi ? base[v] : hi;
+      if (hi > lo)
+        KX_HIP_CHECK(hipMemcpyAsync((char*)out->cols[j].data + lo * unit(j), (char*)dc.cols[j].data + lo * unit(j),
+                                    (hi - lo) * unit(j), hipMemcpyDeviceToHost, sd));
+      base[v] = sk.var_total[v];
+    }
+    if (k == K - 1) {
+      *status = failed ? first : sk;
+      status->n_records = n;
+      status->consumed = offsets[n];
+      for (uint32_t v = 0; v < KXP_NV_MAX; v++) status->var_total[v] = sk.var_total[v];
     }
   }
-  if (s->npres && n) KX_HIP_CHECK(hipMemcpyAsync(out->presence, dc.presence, n * 8, hipMemcpyDeviceToHost, st));
-  KX_HIP_CHECK(hipStreamSynchronize(st));
-  // var payloads: only the decoded bytes (status->var_total per var slot)
-  for (uint32_t v = 0; v < s->prog.nvar && v < KXP_NV_MAX; v++) {
-    const uint32_t k = s->prog.var_col[v];
-    const kx_column_info& ci = s->info[k];
-    const uint64_t units = status->var_total[v] < out->cols[k].capacity ? status->var_total[v] : out->cols[k].capacity;
-    const uint64_t bytes = units * (ci.kind == KX_COL_LIST ? ci.width : 1);
-    if (bytes) KX_HIP_CHECK(hipMemcpyAsync(out->cols[k].data, dc.cols[k].data, bytes, hipMemcpyDeviceToHost, st));
+  KX_HIP_CHECK(hipStreamSynchronize(sd));
+  for (uint32_t k = 0; k < K; k++) {
+    (void)hipEventDestroy(ev_in[k]);
+    (void)hipEventDestroy(ev_dec[k]);
   }
-  KX_HIP_CHECK(hipStreamSynchronize(st));
   return KX_OK;
+}
+
+int kx_host_decode_batch(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len,
+                         const uint64_t* offsets, uint64_t n, const kx_columns* out, kx_status* status) {
+  return host_decode(c, s, in, in_len, offsets, n, out, status, false);
+}
+
+int kx_host_pb_decode_batch(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len,
+                            const uint64_t* offsets, uint64_t n, const kx_columns* out, kx_status* status) {
+  return host_decode(c, s, in, in_len, offsets, n, out, status, true);
 }
 
 uint64_t kx_thrift_message_begin_length(uint32_t name_len) { return 12ull + name_len; }

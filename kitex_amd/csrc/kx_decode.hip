@@ -83,6 +83,7 @@ struct DecParams {
   unsigned long long* errkey;  // offsets mode: min((record << 8) | code)
   uint32_t* overflow;        // an arena capacity was exceeded
   uint64_t* nstop;           // records to emit (chain pass)
+  uint64_t var_base[KXP_NV_MAX];  // arena positions start here (a chunk of a larger batch)
   uint64_t ntiles, ngroups, slotcap;
   uint64_t epoch;            // 16-bit call epoch (never 0)
   uint32_t krec;             // offsets mode: records per tile (<= 64)
@@ -1620,7 +1621,7 @@ __global__ void __launch_bounds__(CT) chain_kernel(DecParams dp_) {
   if (tid == 0) {
     s_E = 0;  // the chain enters group 0 at offset 0
     s_cnt = 0;
-    for (int v = 0; v < KXP_NV_MAX; v++) s_var[v] = 0;
+    for (int v = 0; v < KXP_NV_MAX; v++) s_var[v] = dp.var_base[v];  // arena units before this call
     s_nstop = dp.n;
     s_err = 0;
     s_done = 0;
@@ -2045,9 +2046,11 @@ size_t kx_skip_ws_bytes(uint64_t in_len) { return ws_layout(1, in_len, nullptr, 
 int kx_launch_decode(const KxProgram* dprog, const KxProgram& hprog, const uint8_t* in, uint64_t in_len,
                      const uint64_t* offsets, uint64_t n, const KxLaunchCols& cols, uint8_t* record_status,
                      kx_status* status, void* ws, size_t ws_size, uint64_t epoch, hipStream_t stream, bool pb,
-                     const uint64_t* ends) {
+                     const uint64_t* ends, const uint64_t* var_base) {
   DecParams dp{};
   fill_diag_flags(dp);
+  if (var_base)
+    for (int v = 0; v < KXP_NV_MAX; v++) dp.var_base[v] = var_base[v];
   dp.in = in; dp.in_len = in_len; dp.offsets = offsets; dp.ends = offsets ? ends : nullptr; dp.n = n;
   dp.prog = (const KAS KxProgram*)dprog;
   dp.cols = cols; dp.rstat = record_status; dp.status = status; dp.epoch = epoch;

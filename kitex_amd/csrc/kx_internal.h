@@ -27,6 +27,7 @@ struct kx_schema {
 struct kx_ctx {
   int device = 0;
   hipStream_t own_stream = nullptr;
+  hipStream_t h2d_stream = nullptr, d2h_stream = nullptr;  // kx_host_decode_batch copy engines
   // grow-only decode workspace: tile counter, error key, overflow flag, epoch-tagged tile
   // descriptors. Zeroed once at allocation; every call leaves it re-armed (finalize kernel).
   void* ws = nullptr;
@@ -67,7 +68,7 @@ int kx_launch_decode(const KxProgram* dprog, const KxProgram& hprog, const uint8
                      uint64_t in_len, const uint64_t* offsets, uint64_t n,
                      const KxLaunchCols& cols, uint8_t* record_status, kx_status* status,
                      void* ws, size_t ws_size, uint64_t epoch, hipStream_t stream, bool pb,
-                     const uint64_t* ends = nullptr);
+                     const uint64_t* ends = nullptr, const uint64_t* var_base = nullptr);
 size_t kx_decode_ws_bytes(const KxProgram& hprog, uint64_t in_len, const uint64_t* offsets, uint64_t n);
 
 int kx_launch_skip(const uint8_t* in, uint64_t in_len, uint64_t n, uint64_t* offsets_out,

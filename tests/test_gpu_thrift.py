@@ -321,3 +321,35 @@ def test_skip_batch_truncated_vector(torch, dev, oracle):
     with pytest.raises(ProtocolError) as e:
         cdc.Skip(torch.from_numpy(wire).to(dev), n)
     assert (e.value.code, e.value.record, e.value.offset) == (A.ERR_EOF, n - 1, len(good) * (n - 1))
+
+
+@pytest.mark.parametrize("name", ["r2", "r3", "pf"])
+def test_host_decode_chunked_pipeline(torch, oracle, name):
+    """kx_host_decode_batch / kx_host_pb_decode_batch with offsets and >= 65536 records: the 8-chunk
+    pipeline (arena continued across chunks), field-for-field against the oracle; a failing record
+    in the 5th chunk reports its global index"""
+    from kitex_amd.codec import ProtobufCodec, ThriftCodec
+    sch = S.SCHEMAS[name]()
+    pb = name == "pf"
+    cdc = ProtobufCodec(sch) if pb else ThriftCodec(sch)
+    n = 100_000
+    cs = synth.GENERATORS[name](n, start=17)
+    rc, wire, offs = oracle.encode(sch, cs, pb=pb)
+    if pb:  # bare bodies with known extents
+        from tests.test_gpu_messages import _frame, _records
+        bodies = _records(oracle, sch, cs, pb=True)
+        wire, offs = _frame(bodies)
+        offs = offs.astype(np.uint64)
+    out, st = cdc.UnmarshalHost(wire, n, offsets=offs)
+    rc2, exp, est, _ = oracle.decode(sch, wire, n, offsets=offs, pb=pb)
+    assert st.code == est.code == 0 and st.n_records == n
+    _, infos, _ = oracle.flatten(sch)
+    from tests.helpers import assert_columns_equal
+    assert_columns_equal(out, exp, infos, n)
+    if not pb:
+        bad = wire.copy()
+        k = 63_000
+        bad[int(offs[k])] = 99                    # an unknown field type in record k
+        out, st = cdc.UnmarshalHost(bad, n, offsets=offs, raise_on_error=False)
+        _, _, est, _ = oracle.decode(sch, bad, n, offsets=offs)
+        assert (st.code, st.record, st.offset) == (est.code, est.record, est.offset) and st.record == k
