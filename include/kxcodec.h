@@ -84,7 +84,8 @@ typedef struct kx_field_desc {
   int16_t id;            /* thrift field id */
   uint8_t ttype;         /* KX_T_* of the field */
   uint8_t req;           /* KX_REQ_* */
-  uint8_t elem_ttype;    /* LIST/SET: element KX_T_* (must be a scalar, or STRING) */
+  uint8_t elem_ttype;    /* LIST/SET: element KX_T_* (a scalar, or STRING);
+                            MAP: key KX_T_* | value KX_T_* << 4 (each a scalar or STRING) */
   uint8_t reserved0;
   int16_t child;         /* STRUCT: index of the child struct in the schema's struct table; else -1 */
   int64_t default_bits;  /* scalar default value (two's complement / IEEE bits); ignored otherwise */
@@ -107,6 +108,12 @@ enum {
   KX_COL_LIST_BYTES = 4  /* list/set of strings (or the string side of a map): offsets[n+1]
                             (elements), elem_offsets[elements+1] (bytes) + byte arena */
 };
+/* A MAP field flattens to two consecutive columns, keys then values (each LIST or LIST_BYTES,
+ * record offsets in entries); the value column's elem_ttype carries KX_ELEM_MAP_VALUE. Encoding
+ * writes entries in column order (Go iterates a map in random order: its bytes are only
+ * deterministic for maps of <= 1 entry, k-mock.go:225,259). list<struct> is not supported
+ * (KX_ERR_NOT_IMPLEMENTED at kx_schema_create). */
+#define KX_ELEM_MAP_VALUE 0x80
 
 typedef struct kx_column_info {
   uint32_t kind;        /* KX_COL_* */

@@ -23,6 +23,7 @@ ERR_BAD_VERSION = 4
 ERR_NOT_IMPLEMENTED = 5
 ERR_DEPTH_LIMIT = 6
 ERR_EOF = 8
+ELEM_MAP_VALUE = 0x80
 ERR_APPLICATION_EXCEPTION = 9
 ERR_INVALID_ARG = 100
 ERR_HIP = 101

@@ -352,6 +352,17 @@ __device__ __forceinline__ void put_total(const KAS KxLaunchCols& cols, uint32_t
   else atomicOr(overflow, 1u);
 }
 
+// LIST_BYTES: element byte offsets (the record offsets' width), the element limit
+__device__ __forceinline__ void put_eoff(const KAS KxLaunchCols& cols, uint32_t c, uint64_t i, uint64_t v) {
+  if ((cols.owide >> c) & 1) ((GLB uint64_t*)cols.eoffs[c])[i] = v;
+  else ((GLB uint32_t*)cols.eoffs[c])[i] = (uint32_t)v;
+}
+__device__ __forceinline__ uint64_t elem_lim(const KAS KxLaunchCols& cols, uint32_t c) {
+  const uint64_t cap = cols.ecap[c];
+  return ((cols.owide >> c) & 1) ? cap : kmin64(cap, 0xffffffffull);
+}
+
+
 __device__ __forceinline__ void store_col(void* base, uint32_t width, uint64_t rec, uint64_t v) {
   switch (width) {
     case 1: ((GLB uint8_t*)base)[rec] = (uint8_t)v; break;
@@ -376,6 +387,33 @@ __device__ __forceinline__ T ldk(const KAS T* p) {
 __device__ __forceinline__ KxpField ld_field(const KAS KxProgram* P, int i) { return ldk(&P->f[i]); }
 __device__ __forceinline__ KxpInst ld_inst(const KAS KxProgram* P, int i) { return ldk(&P->inst[i]); }
 __device__ __forceinline__ KxpCol ld_col(const KAS KxProgram* P, int i) { return ldk(&P->col[i]); }
+
+// The decoded prefix ends at record i with per-slot arena totals tot[]: offsets[i] of every var column
+// (in elements for a container column) and, for LIST_BYTES, elem_offsets[elements] = bytes.
+template <int NV>
+__device__ __forceinline__ void close_slots(const KAS KxProgram* P, const KAS KxLaunchCols& cols, uint32_t* overflow,
+                                            uint64_t i, const uint64_t* tot) {
+#pragma unroll
+  for (int v = 0; v < NV; v++) {
+    if (v >= (int)P->nvar) break;
+    const uint32_t c = P->var_col[v];
+    const KxpCol K = ld_col(P, c);
+    if (K.kind == KXP_K_LISTB) {
+      if ((uint32_t)v != K.vslot) continue;
+      uint64_t nb = 0;
+#pragma unroll
+      for (int u = 0; u < NV; u++) if ((uint32_t)u == K.vslot2) nb = tot[u];
+      if (tot[v] <= elem_lim(cols, c) && nb <= arena_lim(cols, c)) {
+        put_off(cols, c, i, tot[v]);
+        put_eoff(cols, c, tot[v], nb);
+      } else {
+        atomicOr(overflow, 1u);
+      }
+    } else {
+      put_total(cols, overflow, c, i, tot[v]);
+    }
+  }
+}
 
 // Canonical fast path: the record is checked against the schema's canonical plan (header bytes in
 // encoder order, STOP bytes). The step index is wave-uniform (scalar loads); a lane whose record
@@ -512,6 +550,59 @@ __device__ __forceinline__ int generic_record(const Src& w, const KAS KxProgram*
       if (limit - vp - 4 < (uint64_t)l) return KX_ERR_EOF;
       vset<NV>(vs, F.vslot, vp + 4, (uint32_t)l);
       pos = vp + 4 + (uint64_t)l;
+    } else if (F.kind == KXP_K_LISTB) {                      // list/set<string>: size x ReadString (:582-625)
+      if (limit - vp < 5) return KX_ERR_EOF;
+      const int32_t l = (int32_t)__builtin_bswap32(fx.w1);
+      if (l < 0) return KX_ERR_NEGATIVE_SIZE;
+      uint64_t q = vp + 5, nb = 0;
+      for (int32_t j = 0; j < l; j++) {
+        if (limit - q < 4) return KX_ERR_EOF;
+        const int32_t sl = (int32_t)__builtin_bswap32(ld4(w, q));
+        if (sl < 0) return KX_ERR_NEGATIVE_SIZE;
+        if (limit - q - 4 < (uint64_t)sl) return KX_ERR_EOF;
+        nb += (uint64_t)sl;
+        q += 4 + (uint64_t)sl;
+      }
+      const KxpCol K = ld_col(P, F.col);
+      vset<NV>(vs, K.vslot, vp + 5, (uint32_t)l);
+      vset<NV>(vs, K.vslot2, vp + 5, (uint32_t)nb);
+      pos = q;
+    } else if (F.kind == KXP_K_MAP) {                        // ReadMapBegin + size x (key, value) (:466-533)
+      if (limit - vp < 6) return KX_ERR_EOF;
+      const int32_t l = (int32_t)__builtin_bswap32(__builtin_amdgcn_alignbyte(fx.w2, fx.w1, 1));
+      if (l < 0) return KX_ERR_NEGATIVE_SIZE;
+      const uint32_t kt = F.elem & 15u, vt = F.elem >> 4;
+      const uint32_t kw = (uint32_t)tsize(kt), vw = (uint32_t)tsize(vt);
+      uint64_t q = vp + 6, nb[2] = {0, 0};
+      if (kw && vw) {
+        if ((limit - q) / (kw + vw) < (uint64_t)l) return KX_ERR_EOF;
+        q += (uint64_t)l * (kw + vw);
+      } else {
+        for (int32_t j = 0; j < l; j++) {
+#pragma unroll
+          for (int side = 0; side < 2; side++) {
+            const uint32_t sw = side ? vw : kw;
+            if (sw) {
+              if (limit - q < sw) return KX_ERR_EOF;
+              q += sw;
+            } else {
+              if (limit - q < 4) return KX_ERR_EOF;
+              const int32_t sl = (int32_t)__builtin_bswap32(ld4(w, q));
+              if (sl < 0) return KX_ERR_NEGATIVE_SIZE;
+              if (limit - q - 4 < (uint64_t)sl) return KX_ERR_EOF;
+              nb[side] += (uint64_t)sl;
+              q += 4 + (uint64_t)sl;
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int side = 0; side < 2; side++) {
+        const KxpCol K = ld_col(P, F.col + side);
+        vset<NV>(vs, K.vslot, vp + 6, (uint32_t)l);
+        if (K.vslot2 != 0xff) vset<NV>(vs, K.vslot2, vp + 6, (uint32_t)nb[side]);
+      }
+      pos = q;
     } else if (F.kind == KXP_K_LIST) {                       // ReadListBegin: elem type ignored (:587)
       if (limit - vp < 5) return KX_ERR_EOF;
       const int32_t l = (int32_t)__builtin_bswap32(fx.w1);
@@ -1717,13 +1808,13 @@ __global__ void __launch_bounds__(CT) chain_kernel(DecParams dp_) {
         kx_status* st = dp.status;
         st->code = (int32_t)errc; st->record = rec; st->offset = errp;
         st->n_records = rec; st->consumed = errp;
+        uint64_t tot[NV > 0 ? NV : 1];
 #pragma unroll
         for (int v = 0; v < NV; v++) {
-          if (v >= (int)dp.prog->nvar) break;
-          const uint64_t vt = vbase[v] + var[v];
-          st->var_total[v] = vt;
-          put_total(dp.cols, dp.overflow, dp.prog->var_col[v], rec, vt);
+          tot[v] = vbase[v] + var[v];
+          if (v < (int)dp.prog->nvar) st->var_total[v] = tot[v];
         }
+        close_slots<NV>(dp.prog, dp.cols, dp.overflow, rec, tot);
         if (MODE == M_SKIP) dp.skip_out[rec] = errp;
         s_nstop = rec;
       }
@@ -1749,15 +1840,74 @@ __global__ void __launch_bounds__(CT) chain_kernel(DecParams dp_) {
       kx_status* st = dp.status;
       st->code = KX_ERR_EOF; st->record = tot; st->offset = dp.in_len;
       st->n_records = tot; st->consumed = dp.in_len;
+      uint64_t vt[NV > 0 ? NV : 1];
       for (int v = 0; v < NV; v++) {
-        if (v >= (int)dp.prog->nvar) break;
-        st->var_total[v] = s_var[v];
-        put_total(dp.cols, dp.overflow, dp.prog->var_col[v], tot, s_var[v]);
+        vt[v] = s_var[v];
+        if (v < (int)dp.prog->nvar) st->var_total[v] = s_var[v];
       }
+      close_slots<NV>(dp.prog, dp.cols, dp.overflow, tot, vt);
       if (MODE == M_SKIP) dp.skip_out[tot] = dp.in_len;
       s_nstop = tot;
     }
     *dp.nstop = s_nstop;
+  }
+}
+
+// one element of wire type t at q: its payload position and length (strings) or width (scalars)
+__device__ __forceinline__ uint64_t elem_at(const Src& w, uint64_t q, uint32_t t, uint64_t& xp, uint32_t& xl) {
+  if (t == KX_T_STRING) {
+    xl = __builtin_bswap32(ld4(w, q));
+    xp = q + 4;
+    return q + 4 + xl;
+  }
+  xl = (uint32_t)tsize(t);
+  xp = q;
+  return q + xl;
+}
+
+// A list/set<string> column or one side of a map for record r: record offsets in elements at E,
+// element byte offsets from B (LIST_BYTES) or host-order scalars (a map's fixed side). The record's
+// walk already checked every length against its extent.
+__device__ __forceinline__ void emit_container(const Src& w, const KAS KxProgram* P, const KAS KxLaunchCols& cols,
+                                               uint32_t c, const KxpCol& K, uint64_t pos, uint32_t n, uint64_t E,
+                                               uint64_t B, uint64_t nb, uint64_t r, uint32_t* overflow) {
+  const bool lb = K.kind == KXP_K_LISTB;
+  const bool fits = lb ? (E + n <= elem_lim(cols, c) && B + nb <= arena_lim(cols, c)) : E + n <= arena_lim(cols, c);
+  if (!fits) { atomicOr(overflow, 1u); return; }
+  put_off(cols, c, r, E);
+  uint32_t kt = KX_T_STRING, vt = KX_T_STRING;
+  if (K.mside) {
+    const KxpField F = ld_field(P, K.field);
+    kt = F.elem & 15u;
+    vt = F.elem >> 4;
+  }
+  KxpCol KB = K;
+  KB.kind = KXP_K_BYTES;
+  KB.width = 1;
+  uint64_t q = pos, acc = 0;
+  for (uint32_t j = 0; j < n; j++) {
+    uint64_t xp, kp, vp;
+    uint32_t xl, kl, vl;
+    if (K.mside) {
+      q = elem_at(w, q, kt, kp, kl);
+      q = elem_at(w, q, vt, vp, vl);
+      xp = K.mside == 1 ? kp : vp;
+      xl = K.mside == 1 ? kl : vl;
+    } else {
+      q = elem_at(w, q, KX_T_STRING, xp, xl);
+    }
+    if (lb) {
+      put_eoff(cols, c, E + j, B + acc);
+      if (xl) copy_var(w, KB, xp, xl, (uint8_t*)cols.data[c] + B + acc);
+      acc += xl;
+    } else {
+      uint64_t v;
+      if (K.width == 1) v = K.elem == KX_T_BOOL ? (ld1(w, xp) == 1) : ld1(w, xp);
+      else if (K.width == 2) v = __builtin_bswap32(ld4(w, xp)) >> 16;
+      else if (K.width == 4) v = __builtin_bswap32(ld4(w, xp));
+      else v = be64(w, xp);
+      store_col(cols.data[c], K.width, E + j, v);
+    }
   }
 }
 
@@ -1832,31 +1982,48 @@ __global__ void __launch_bounds__(NT) emit_kernel(DecParams dp_) {
         if (dp.rstat) dp.rstat[r] = (uint8_t)rc;
       }
     }
-    // arena positions: wave exclusive scan of the var lengths
+    // arena positions: wave exclusive scan of the var lengths (per slot)
+    uint64_t atv[NV > 0 ? NV : 1];
 #pragma unroll
     for (int v = 0; v < NV; v++) {
       if (v >= (int)P->nvar) break;
       const uint64_t x0 = act ? vs.len[v] : 0;
       const uint64_t xi = wave_incl_scan(x0, lane);
-      const uint64_t at = run[v] + xi - x0;
+      atv[v] = run[v] + xi - x0;
+      run[v] += rl64(xi, 63);
+    }
+#pragma unroll
+    for (int v = 0; v < NV; v++) {
+      if (v >= (int)P->nvar) break;
+      const uint64_t at = atv[v];
       const uint32_t cc = P->var_col[v];
-      if (act) {
+      const KxpCol K = ld_col(P, cc);
+      if (K.kind == KXP_K_LISTB || K.mside) {   // containers: element by element, with both slots
+        if ((uint32_t)v == K.vslot && act) {
+          uint64_t B = 0, nb = 0;
+#pragma unroll
+          for (int u = 0; u < NV; u++)
+            if ((uint32_t)u == K.vslot2) { B = atv[u]; nb = vs.len[u]; }
+          emit_container(w, P, dp.cols, cc, K, vs.pos[v], vs.len[v], at, B, nb, r, dp.overflow);
+        }
+      } else if (act) {
         const uint32_t nn = vs.len[v];
         if (at + nn <= arena_lim(dp.cols, cc)) {
           put_off(dp.cols, cc, r, at);
-          if (nn) {
-            const KxpCol K = ld_col(P, cc);
-            copy_var(w, K, vs.pos[v], nn, (uint8_t*)dp.cols.data[cc] + at * K.width);
-          }
+          if (nn) copy_var(w, K, vs.pos[v], nn, (uint8_t*)dp.cols.data[cc] + at * K.width);
         } else {
           atomicOr(dp.overflow, 1u);
         }
       }
-      if (act && r == nstop - 1 && nstop == dp.n) {
-        dp.status->var_total[v] = at + vs.len[v];
-        put_total(dp.cols, dp.overflow, cc, dp.n, at + vs.len[v]);
+    }
+    if (act && r == nstop - 1 && nstop == dp.n) {
+      uint64_t tot[NV > 0 ? NV : 1];
+#pragma unroll
+      for (int v = 0; v < NV; v++) {
+        tot[v] = (v < (int)P->nvar) ? atv[v] + vs.len[v] : 0;
+        if (v < (int)P->nvar) dp.status->var_total[v] = tot[v];
       }
-      run[v] += rl64(xi, 63);
+      close_slots<NV>(P, dp.cols, dp.overflow, dp.n, tot);
     }
     if (act && r == nstop - 1 && nstop == dp.n) {
       kx_status* st = dp.status;

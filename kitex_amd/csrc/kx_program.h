@@ -19,7 +19,9 @@
 #define KXP_MAX_COLS 32
 #define KXP_NV_MAX 8  // var (BYTES / LIST) columns per schema handled by the device kernels
 
-enum : uint8_t { KXP_K_FIXED = 1, KXP_K_BYTES = 2, KXP_K_LIST = 3, KXP_K_STRUCT = 4 };
+enum : uint8_t { KXP_K_FIXED = 1, KXP_K_BYTES = 2, KXP_K_LIST = 3, KXP_K_STRUCT = 4,
+                 KXP_K_LISTB = 5,   // list/set<string>: column LIST_BYTES, slots vslot (elements) + vslot2 (bytes)
+                 KXP_K_MAP = 6 };   // map<K,V>: field kind only; columns col (keys), col + 1 (values)
 
 struct KxpField {      // 16 B
   int16_t id;
@@ -54,13 +56,14 @@ struct KxpInst {       // 32 B
 };
 
 struct KxpCol {        // 16 B
-  uint8_t kind;        // KXP_K_FIXED / BYTES / LIST
+  uint8_t kind;        // KXP_K_FIXED / BYTES / LIST / LISTB (a map side: LIST or LISTB)
   uint8_t width;
-  uint8_t elem;        // LIST element type (BOOL needs normalisation)
-  uint8_t vslot;       // 0xff for FIXED
+  uint8_t elem;        // LIST element type (BOOL needs normalisation); map side: this side's type
+  uint8_t vslot;       // 0xff for FIXED; LISTB: the elements slot
   int8_t field;        // flat field
   uint8_t ttype;
-  uint8_t pad[2];
+  uint8_t vslot2;      // LISTB: the bytes slot, else 0xff
+  uint8_t mside;       // 1: map keys, 2: map values, 0: not a map side
   int64_t defv;        // FIXED default (bits)
 };
 

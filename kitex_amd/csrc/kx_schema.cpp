@@ -88,7 +88,13 @@ struct Builder {
           ci.width = 1;
           break;
         case KX_T_LIST: case KX_T_SET:
-          if (type_size(f->elem_ttype) == 0) return KX_ERR_NOT_IMPLEMENTED;  // list<string|struct>
+          if (f->elem_ttype == KX_T_STRING) {  // list/set<string>: FieldFastReadList (struct_tpl.go:582-625)
+            ci.kind = KX_COL_LIST_BYTES;
+            ci.width = 1;
+            ci.elem_ttype = KX_T_STRING;
+            break;
+          }
+          if (type_size(f->elem_ttype) == 0) return KX_ERR_NOT_IMPLEMENTED;  // list<struct|container>
           ci.kind = KX_COL_LIST;
           ci.width = (uint32_t)type_size(f->elem_ttype);
           ci.elem_ttype = f->elem_ttype;
@@ -103,8 +109,23 @@ struct Builder {
           inst_fields[me][slot].child = child;
           continue;
         }
-        case KX_T_MAP:
-          return KX_ERR_NOT_IMPLEMENTED;
+        case KX_T_MAP: {  // FieldFastReadMap (struct_tpl.go:466-533): a keys column and a values column
+          const uint8_t kt = f->elem_ttype & 15, vt = (uint8_t)(f->elem_ttype >> 4);
+          if ((type_size(kt) == 0 && kt != KX_T_STRING) || (type_size(vt) == 0 && vt != KX_T_STRING))
+            return KX_ERR_NOT_IMPLEMENTED;  // map<.., struct|container>
+          if (s->ncols + 2 > KX_MAX_COLUMNS) return KX_ERR_NOT_IMPLEMENTED;
+          pf.col = (int)s->ncols;
+          for (int side = 0; side < 2; side++) {
+            const uint8_t t = side ? vt : kt;
+            kx_column_info cm = ci;
+            cm.kind = t == KX_T_STRING ? KX_COL_LIST_BYTES : KX_COL_LIST;
+            cm.width = t == KX_T_STRING ? 1u : (uint32_t)type_size(t);
+            cm.elem_ttype = (uint8_t)(t | (side ? KX_ELEM_MAP_VALUE : 0));
+            s->info[s->ncols++] = cm;
+          }
+          inst_fields[me].push_back(pf);
+          continue;
+        }
         default:
           return KX_ERR_INVALID_ARG;
       }
@@ -145,20 +166,27 @@ int kx_build_program(const kx_struct_desc* structs, uint32_t nstructs, kx_schema
   P.ncols = s->ncols;
   P.npres = s->npres;
 
-  // var slots in column order
+  // var slots in column order (LIST_BYTES: the elements slot, then the bytes slot)
   int nvar = 0;
   for (uint32_t c = 0; c < s->ncols; c++) {
     KxpCol& kc = P.col[c];
     const kx_column_info& ci = s->info[c];
-    kc.kind = ci.kind == KX_COL_FIXED ? KXP_K_FIXED : ci.kind == KX_COL_BYTES ? KXP_K_BYTES : KXP_K_LIST;
+    kc.kind = ci.kind == KX_COL_FIXED ? KXP_K_FIXED : ci.kind == KX_COL_BYTES ? KXP_K_BYTES
+            : ci.kind == KX_COL_LIST_BYTES ? KXP_K_LISTB : KXP_K_LIST;
     kc.width = (uint8_t)ci.width;
-    kc.elem = ci.elem_ttype;
+    kc.elem = (uint8_t)(ci.elem_ttype & 15);
     kc.ttype = ci.ttype;
     kc.vslot = 0xff;
+    kc.vslot2 = 0xff;
+    kc.mside = ci.ttype == KX_T_MAP ? ((ci.elem_ttype & KX_ELEM_MAP_VALUE) ? 2 : 1) : 0;
     if (ci.kind != KX_COL_FIXED) {
-      if (nvar >= KXP_NV_MAX) return KX_ERR_NOT_IMPLEMENTED;
+      if (nvar + (ci.kind == KX_COL_LIST_BYTES ? 2 : 1) > KXP_NV_MAX) return KX_ERR_NOT_IMPLEMENTED;
       kc.vslot = (uint8_t)nvar;
       P.var_col[nvar++] = (uint8_t)c;
+      if (ci.kind == KX_COL_LIST_BYTES) {
+        kc.vslot2 = (uint8_t)nvar;
+        P.var_col[nvar++] = (uint8_t)c;
+      }
     }
   }
   P.nvar = (uint32_t)nvar;
@@ -193,11 +221,12 @@ int kx_build_program(const kx_struct_desc* structs, uint32_t nstructs, kx_schema
       F.enc_next = -1;
       if (fl[k].col >= 0) {
         const KxpCol& kc = P.col[fl[k].col];
-        F.kind = kc.kind;
+        F.kind = d->ttype == KX_T_MAP ? KXP_K_MAP : kc.kind;
         F.width = kc.width;
         F.vslot = kc.vslot;
         P.col[fl[k].col].field = (int8_t)ff;
         P.col[fl[k].col].defv = d->default_bits;
+        if (d->ttype == KX_T_MAP) P.col[fl[k].col + 1].field = (int8_t)ff;
       } else {
         F.kind = KXP_K_STRUCT;
         F.width = 0;
@@ -217,7 +246,11 @@ int kx_build_program(const kx_struct_desc* structs, uint32_t nstructs, kx_schema
       const KxpField& F = P.f[I.first + k];
       m |= 1ull << (I.first + k);
       if (F.pbit >= 0) pm |= 1ull << F.pbit;
-      if (F.vslot != 0xff) vm |= (uint8_t)(1u << F.vslot);
+      if (F.col >= 0)  // every var slot of the field's columns (map: both sides; LISTB: both slots)
+        for (int cc = F.col; cc <= F.col + (F.kind == KXP_K_MAP ? 1 : 0); cc++) {
+          if (P.col[cc].vslot != 0xff) vm |= (uint8_t)(1u << P.col[cc].vslot);
+          if (P.col[cc].vslot2 != 0xff) vm |= (uint8_t)(1u << P.col[cc].vslot2);
+        }
       if (F.child >= 0) {
         m |= P.inst[F.child].subtree_mask;
         pm |= P.inst[F.child].pres_mask;
@@ -303,7 +336,8 @@ int kx_build_program(const kx_struct_desc* structs, uint32_t nstructs, kx_schema
     mn += 3;
     if (F.kind == KXP_K_FIXED) mn += F.width;
     else if (F.kind == KXP_K_BYTES) mn += 4;
-    else if (F.kind == KXP_K_LIST) mn += 5;
+    else if (F.kind == KXP_K_LIST || F.kind == KXP_K_LISTB) mn += 5;
+    else if (F.kind == KXP_K_MAP) mn += 6;
     else mn += 1;
   }
   P.fixed_min = mn;
@@ -323,7 +357,7 @@ int kx_build_program(const kx_struct_desc* structs, uint32_t nstructs, kx_schema
       const KxpInst& I = P.inst[i];
       for (int f = I.enc_first; f >= 0; f = P.f[f].enc_next) {
         const KxpField& F = P.f[f];
-        if (F.req == KX_REQ_OPTIONAL) { ok = false; return; }
+        if (F.req == KX_REQ_OPTIONAL || F.kind == KXP_K_LISTB || F.kind == KXP_K_MAP) { ok = false; return; }
         KxpStep st{};
         st.hdr = (uint32_t)F.ttype | ((uint32_t)((uint16_t)F.id >> 8) << 8) | ((uint32_t)(F.id & 0xff) << 16);
         st.col = F.col;

@@ -24,7 +24,8 @@ class Field:
     ttype: int
     name: str = ""
     req: int = A.REQ_DEFAULT
-    elem: int = 0                       # LIST/SET element type
+    elem: int = 0                       # LIST/SET element type; MAP key type
+    val: int = 0                        # MAP value type
     child: Optional["Struct"] = None    # STRUCT fields
     default: int = 0                    # scalar default (two's complement / IEEE bits)
     binary: bool = False                # protobuf `bytes` (no UTF-8 check); thrift: same wire as string
@@ -52,7 +53,7 @@ class Schema:
                 arr[j].id = f.id
                 arr[j].ttype = f.ttype
                 arr[j].req = f.req
-                arr[j].elem_ttype = f.elem
+                arr[j].elem_ttype = f.elem | (f.val << 4 if f.ttype == A.T_MAP else 0)
                 arr[j].reserved0 = A.FIELD_BINARY if f.binary else 0
                 arr[j].child = self._index[id(f.child)] if f.child is not None else -1
                 arr[j].default_bits = _signed64(f.default)
@@ -111,6 +112,29 @@ def schema_pf() -> Schema:
     fs = [Field(i, A.T_I64, f"a{i}") for i in range(1, 9)]
     fs += [Field(9, A.T_STRING, "s9"), Field(10, A.T_STRING, "s10")]
     return Schema(Struct("PF", fs))
+
+
+def schema_mockreq() -> Schema:
+    """MockReq (internal/mocks/thrift/k-mock.go:116-184): 1: string Msg, 2: map<string,string>
+    strMap, 3: list<string> strList."""
+    return Schema(Struct("MockReq", [Field(1, A.T_STRING, "Msg"),
+                                     Field(2, A.T_MAP, "strMap", elem=A.T_STRING, val=A.T_STRING),
+                                     Field(3, A.T_LIST, "strList", elem=A.T_STRING)]))
+
+
+def schema_cx1() -> Schema:
+    """Containers beyond list<scalar>, MockReq's shapes next to an i64: id, msg, map<string,string>,
+    list<string> (7 var slots: the device handles 8 per schema)."""
+    return Schema(Struct("CX1", [Field(1, A.T_I64, "id"), Field(2, A.T_STRING, "msg"),
+                                 Field(3, A.T_MAP, "strMap", elem=A.T_STRING, val=A.T_STRING),
+                                 Field(4, A.T_LIST, "strList", elem=A.T_STRING)]))
+
+
+def schema_cx2() -> Schema:
+    """set<string>, map<i64,double> and an optional map<i32,string> next to an i64."""
+    return Schema(Struct("CX2", [Field(1, A.T_I64, "id"), Field(5, A.T_SET, "tags", elem=A.T_STRING),
+                                 Field(6, A.T_MAP, "scores", elem=A.T_I64, val=A.T_DOUBLE),
+                                 Field(7, A.T_MAP, "names", elem=A.T_I32, val=A.T_STRING, req=A.REQ_OPTIONAL)]))
 
 
 SCHEMAS = {"r1": schema_r1, "r2": schema_r2, "r3": schema_r3, "pf": schema_pf}

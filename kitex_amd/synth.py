@@ -22,7 +22,7 @@ from . import _abi as A
 M64 = (1 << 64) - 1
 ALPHABET = b"abcdefghijklmnopqrstuvwxyz0123456789"
 SEED_BASE = 0x4B495445
-CONFIG_ID = {"r1": 1, "r2": 2, "r3": 3, "pf": 4}
+CONFIG_ID = {"cx": 7, "r1": 1, "r2": 2, "r3": 3, "pf": 4}
 
 
 def seed_for(config: str) -> int:
@@ -188,6 +188,60 @@ def gen_pf(n: int, start: int = 0, strlen: int = 32) -> ColumnSet:
     for f in (9, 10):
         cols.append(_fixed_strings_np(_key_np(seed, i, f), strlen))
     return ColumnSet(cols, None, n)
+
+
+_ALPHA_NP = np.frombuffer(ALPHABET, dtype=np.uint8)
+
+
+def _strings(rng, counts, lo, hi):
+    """LIST_BYTES column parts for per-record element counts: (record offsets, element byte
+    offsets, bytes) with element lengths in [lo, hi] from [a-z0-9]"""
+    ne = int(counts.sum())
+    lens = rng.integers(lo, hi + 1, size=ne)
+    eoff = np.zeros(ne + 1, dtype=np.uint32)
+    eoff[1:] = np.cumsum(lens)
+    roff = np.zeros(counts.size + 1, dtype=np.uint32)
+    roff[1:] = np.cumsum(counts)
+    data = _ALPHA_NP[rng.integers(0, len(ALPHABET), size=max(1, int(eoff[-1])))]
+    return roff, eoff, data
+
+
+def gen_cx1(n: int, start: int = 0) -> ColumnSet:
+    """records of schema.schema_cx1(): i64 id, string msg, map<string,string> (0..3 entries),
+    list<string> (0..4 elements)"""
+    rng = np.random.default_rng(seed_for("cx") + start)
+    ids = rng.integers(-2**63, 2**63 - 1, size=n, dtype=np.int64)
+    msg_len = rng.integers(0, 21, size=n)
+    moff = np.zeros(n + 1, dtype=np.uint32)
+    moff[1:] = np.cumsum(msg_len)
+    msg = _ALPHA_NP[rng.integers(0, len(ALPHABET), size=max(1, int(moff[-1])))]
+    c_map = rng.integers(0, 4, size=n)
+    km = _strings(rng, c_map, 1, 6)
+    vm = _strings(rng, c_map, 0, 8)
+    lst = _strings(rng, rng.integers(0, 5, size=n), 0, 10)
+    pres = np.full(n, 0b11, dtype=np.uint64)  # strMap 0, strList 1 (always written)
+    return ColumnSet([ids, (moff, msg), km, vm, lst], pres, n)
+
+
+def gen_cx2(n: int, start: int = 0) -> ColumnSet:
+    """records of schema.schema_cx2(): i64 id, set<string> (0..3), map<i64,double> (0..3), optional
+    map<i32,string> (present in half the records, 0..2 entries)"""
+    rng = np.random.default_rng(seed_for("cx") + 1000003 + start)
+    ids = rng.integers(-2**63, 2**63 - 1, size=n, dtype=np.int64)
+    tags = _strings(rng, rng.integers(0, 4, size=n), 1, 5)
+    c_sc = rng.integers(0, 4, size=n)
+    soff = np.zeros(n + 1, dtype=np.uint32)
+    soff[1:] = np.cumsum(c_sc)
+    sk = rng.integers(-2**40, 2**40, size=max(1, int(soff[-1])), dtype=np.int64)
+    sv = rng.standard_normal(size=max(1, int(soff[-1]))).view(np.int64)
+    has = rng.integers(0, 2, size=n).astype(bool)
+    c_nm = np.where(has, rng.integers(0, 3, size=n), 0)
+    noff = np.zeros(n + 1, dtype=np.uint32)
+    noff[1:] = np.cumsum(c_nm)
+    nk = rng.integers(-2**31, 2**31 - 1, size=max(1, int(noff[-1])), dtype=np.int64).astype(np.int32)
+    nv = _strings(rng, c_nm, 0, 7)
+    pres = (np.uint64(0b11) | (has.astype(np.uint64) << np.uint64(2))).astype(np.uint64)  # tags 0, scores 1, names 2
+    return ColumnSet([ids, tags, (soff, sk), (soff.copy(), sv), (noff, nk), nv], pres, n)
 
 
 GENERATORS = {"r1": gen_r1, "r2": gen_r2, "r3": gen_r3, "pf": gen_pf}

@@ -35,6 +35,17 @@ static void off_set(const kx_column* c, uint64_t i, uint64_t v) {
 static uint64_t arena_lim(const kx_column* c) {
   return off_w(c) == 8 || c->capacity < 0xffffffffull ? c->capacity : 0xffffffffull;
 }
+/* LIST_BYTES: element byte offsets (same width as the record offsets), element capacity */
+static void eoff_set(const kx_column* c, uint64_t i, uint64_t v) {
+  if (off_w(c) == 8) ((uint64_t*)c->elem_offsets)[i] = v;
+  else ((uint32_t*)c->elem_offsets)[i] = (uint32_t)v;
+}
+static uint64_t eoff_get(const kx_column* c, uint64_t i) {
+  return off_w(c) == 8 ? ((const uint64_t*)c->elem_offsets)[i] : ((const uint32_t*)c->elem_offsets)[i];
+}
+static uint64_t elem_lim(const kx_column* c) {
+  return off_w(c) == 8 || c->elem_capacity < 0xffffffffull ? c->elem_capacity : 0xffffffffull;
+}
 
 /* typeToSize (codec_apache.go:182-189) */
 static int type_size(uint8_t t) {
@@ -199,7 +210,10 @@ typedef struct {
   kx_column_info cols[KX_MAX_COLUMNS];
   uint32_t ncols, npres;
   int nvar;
-  int varidx[KX_MAX_COLUMNS]; /* column -> var slot, -1 for fixed */
+  int varidx[KX_MAX_COLUMNS]; /* column -> var slot (elements / bytes), -1 for fixed */
+  int varidx2[KX_MAX_COLUMNS]; /* LIST_BYTES column -> its bytes slot, else -1 */
+  uint8_t mside[KX_MAX_COLUMNS]; /* 1: map key column, 2: map value column, 0: neither */
+  uint8_t mkt[KX_MAX_COLUMNS], mvt[KX_MAX_COLUMNS]; /* map key / value types (map columns) */
   int is_pb;
 } plan_t;
 
@@ -235,8 +249,28 @@ static int flatten_rec(plan_t* p, int sidx, int depth, int16_t* path, int* stack
       case KX_T_STRING:
         ci.kind = KX_COL_BYTES; ci.width = 1; break;
       case KX_T_LIST: case KX_T_SET:
-        if (type_size(f->elem_ttype) == 0) return KX_ERR_NOT_IMPLEMENTED;
+        if (f->elem_ttype == KX_T_STRING) {                /* list/set<string>: FieldFastReadList (:582-625) */
+          ci.kind = KX_COL_LIST_BYTES; ci.width = 1; ci.elem_ttype = KX_T_STRING; break;
+        }
+        if (type_size(f->elem_ttype) == 0) return KX_ERR_NOT_IMPLEMENTED;  /* list<struct|container> */
         ci.kind = KX_COL_LIST; ci.width = (uint32_t)type_size(f->elem_ttype); ci.elem_ttype = f->elem_ttype; break;
+      case KX_T_MAP: {                                     /* FieldFastReadMap (:466-533): keys, values columns */
+        const uint8_t kt = f->elem_ttype & 15, vt = (uint8_t)(f->elem_ttype >> 4);
+        if ((type_size(kt) == 0 && kt != KX_T_STRING) || (type_size(vt) == 0 && vt != KX_T_STRING))
+          return KX_ERR_NOT_IMPLEMENTED;                   /* map<.., struct|container> */
+        if (p->ncols + 2 > KX_MAX_COLUMNS) return KX_ERR_NOT_IMPLEMENTED;
+        m->col = (int)p->ncols;
+        for (int side = 0; side < 2; side++) {
+          const uint8_t t = side ? vt : kt;
+          kx_column_info cm = ci;
+          cm.kind = t == KX_T_STRING ? KX_COL_LIST_BYTES : KX_COL_LIST;
+          cm.width = t == KX_T_STRING ? 1u : (uint32_t)type_size(t);
+          cm.elem_ttype = (uint8_t)(t | (side ? KX_ELEM_MAP_VALUE : 0));
+          p->mside[p->ncols] = (uint8_t)(1 + side); p->mkt[p->ncols] = kt; p->mvt[p->ncols] = vt;
+          p->cols[p->ncols++] = cm;
+        }
+        continue;
+      }
       case KX_T_STRUCT: {
         int child = -1;
         int rc = flatten_rec(p, f->child, depth + 1, path, stack, &child);
@@ -244,7 +278,6 @@ static int flatten_rec(plan_t* p, int sidx, int depth, int16_t* path, int* stack
         m->inst = child;
         continue;
       }
-      case KX_T_MAP: return KX_ERR_NOT_IMPLEMENTED;
       default: return KX_ERR_INVALID_ARG;
     }
     if (p->ncols >= KX_MAX_COLUMNS) return KX_ERR_NOT_IMPLEMENTED;
@@ -263,8 +296,10 @@ static int plan_build(plan_t* p, const kx_struct_desc* structs, uint32_t nstruct
   int rc = flatten_rec(p, 0, 0, path, stack, &root);
   if (rc) return rc;
   p->nvar = 0;
-  for (uint32_t c = 0; c < p->ncols; c++)
+  for (uint32_t c = 0; c < p->ncols; c++) {  /* var slots in column order; LIST_BYTES: elements, bytes */
     p->varidx[c] = p->cols[c].kind == KX_COL_FIXED ? -1 : p->nvar++;
+    p->varidx2[c] = p->cols[c].kind == KX_COL_LIST_BYTES ? p->nvar++ : -1;
+  }
   return KX_OK;
 }
 
@@ -293,7 +328,8 @@ typedef struct {
   int emit;
   uint64_t presence;
   const uint8_t* vptr[KX_MAX_COLUMNS];
-  uint64_t vlen[KX_MAX_COLUMNS];
+  uint64_t vlen[KX_MAX_COLUMNS];    /* bytes / elements */
+  uint64_t vbytes[KX_MAX_COLUMNS];  /* LIST_BYTES: payload bytes of the elements */
 } dec_t;
 
 static void store_fixed(const dec_t* d, int col, uint64_t v) {
@@ -316,7 +352,10 @@ static void set_defaults(dec_t* d, int inst) {
     if (m->pbit >= 0) d->presence &= ~(1ull << m->pbit);
     if (m->inst >= 0) { set_defaults(d, m->inst); continue; }
     if (d->p->cols[m->col].kind == KX_COL_FIXED) store_fixed(d, m->col, (uint64_t)sd->fields[i].default_bits);
-    else { d->vptr[m->col] = NULL; d->vlen[m->col] = 0; }
+    else {
+      const int nc = sd->fields[i].ttype == KX_T_MAP ? 2 : 1;
+      for (int k = 0; k < nc; k++) { d->vptr[m->col + k] = NULL; d->vlen[m->col + k] = 0; d->vbytes[m->col + k] = 0; }
+    }
   }
 }
 
@@ -382,10 +421,55 @@ static int read_struct(dec_t* d, int inst, const uint8_t* b, size_t len, size_t*
         if (rem < 5) return KX_ERR_EOF;
         int32_t n = (int32_t)be32(v + 1);
         if (n < 0) return KX_ERR_NEGATIVE_SIZE;
+        if (f->elem_ttype == KX_T_STRING) {                /* n x ReadString */
+          size_t q = 5;
+          uint64_t bytes = 0;
+          for (int32_t j = 0; j < n; j++) {
+            if (rem - q < 4) return KX_ERR_EOF;
+            int32_t l = (int32_t)be32(v + q);
+            if (l < 0) return KX_ERR_NEGATIVE_SIZE;
+            if ((uint64_t)(rem - q - 4) < (uint64_t)l) return KX_ERR_EOF;
+            bytes += (uint64_t)l;
+            q += 4 + (size_t)l;
+          }
+          d->vptr[m->col] = v + 5; d->vlen[m->col] = (uint64_t)n; d->vbytes[m->col] = bytes;
+          off += q;
+          break;
+        }
         uint64_t w = (uint64_t)type_size(f->elem_ttype);
         if ((uint64_t)rem < 5 + (uint64_t)n * w) return KX_ERR_EOF;
         d->vptr[m->col] = v + 5; d->vlen[m->col] = (uint64_t)n;
         off += 5 + (size_t)((uint64_t)n * w);
+        break;
+      }
+      case KX_T_MAP: {                                     /* ReadMapBegin; key/value types ignored */
+        if (rem < 6) return KX_ERR_EOF;
+        int32_t n = (int32_t)be32(v + 2);
+        if (n < 0) return KX_ERR_NEGATIVE_SIZE;
+        const uint8_t kt = f->elem_ttype & 15, vt = (uint8_t)(f->elem_ttype >> 4);
+        size_t q = 6;
+        uint64_t kb = 0, vb = 0;
+        for (int32_t j = 0; j < n; j++) {
+          for (int side = 0; side < 2; side++) {
+            const uint8_t t = side ? vt : kt;
+            if (t == KX_T_STRING) {
+              if (rem - q < 4) return KX_ERR_EOF;
+              int32_t l = (int32_t)be32(v + q);
+              if (l < 0) return KX_ERR_NEGATIVE_SIZE;
+              if ((uint64_t)(rem - q - 4) < (uint64_t)l) return KX_ERR_EOF;
+              if (side) vb += (uint64_t)l; else kb += (uint64_t)l;
+              q += 4 + (size_t)l;
+            } else {
+              const size_t w = (size_t)type_size(t);
+              if (rem - q < w) return KX_ERR_EOF;
+              q += w;
+            }
+          }
+        }
+        d->vptr[m->col] = d->vptr[m->col + 1] = v + 6;
+        d->vlen[m->col] = d->vlen[m->col + 1] = (uint64_t)n;
+        d->vbytes[m->col] = kb; d->vbytes[m->col + 1] = vb;
+        off += q;
         break;
       }
       case KX_T_STRUCT: {
@@ -406,6 +490,54 @@ static int read_struct(dec_t* d, int inst, const uint8_t* b, size_t len, size_t*
   return KX_OK;
 }
 
+/* One element of wire type t at q: its payload (a string's bytes, a scalar's wire bytes). */
+static const uint8_t* elem_at(const uint8_t* q, uint8_t t, const uint8_t** data, uint64_t* len) {
+  if (t == KX_T_STRING) { *len = be32(q); *data = q + 4; return q + 4 + *len; }
+  *len = (uint64_t)type_size(t); *data = q; return q + *len;
+}
+
+/* A list<string> / set<string> column or one side of a map: record offsets in elements, element
+ * byte offsets (LIST_BYTES) or host-order scalars (a map's fixed side), cursors per slot. */
+static void emit_container(dec_t* d, uint32_t c, uint64_t* cursor, int* overflow) {
+  const plan_t* p = d->p;
+  const kx_column* col = &d->out->cols[c];
+  const int vs = p->varidx[c], vs2 = p->varidx2[c];
+  const uint64_t n = d->vlen[c], nb = vs2 >= 0 ? d->vbytes[c] : 0;
+  const uint64_t E = cursor[vs], B = vs2 >= 0 ? cursor[vs2] : 0;
+  const int lb = p->cols[c].kind == KX_COL_LIST_BYTES;
+  const int fits = lb ? (E + n <= elem_lim(col) && B + nb <= arena_lim(col)) : E + n <= arena_lim(col);
+  if (d->emit && fits) {
+    off_set(col, d->rec, E);
+    const uint8_t* q = d->vptr[c];
+    uint64_t acc = 0;
+    for (uint64_t j = 0; j < n; j++) {
+      const uint8_t *kd, *vd, *x;
+      uint64_t kl, vl, xl;
+      if (p->mside[c]) {
+        q = elem_at(q, p->mkt[c], &kd, &kl);
+        q = elem_at(q, p->mvt[c], &vd, &vl);
+        x = p->mside[c] == 1 ? kd : vd;
+        xl = p->mside[c] == 1 ? kl : vl;
+      } else {
+        q = elem_at(q, KX_T_STRING, &x, &xl);
+      }
+      if (lb) {
+        eoff_set(col, E + j, B + acc);
+        if (xl) memcpy((uint8_t*)col->data + B + acc, x, xl);
+        acc += xl;
+      } else {
+        const uint32_t w = p->cols[c].width;
+        uint64_t v = read_scalar(p->cols[c].elem_ttype & 15, x);
+        memcpy((uint8_t*)col->data + (E + j) * w, &v, w);
+      }
+    }
+  } else if (!fits) {
+    *overflow = 1;
+  }
+  cursor[vs] += n;
+  if (vs2 >= 0) cursor[vs2] += nb;
+}
+
 /* Emit buffered var fields + presence for record d->rec. cursors: arena cursor per var slot. */
 static int emit_record_tail(dec_t* d, uint64_t* cursor, int* overflow) {
   const plan_t* p = d->p;
@@ -414,6 +546,10 @@ static int emit_record_tail(dec_t* d, uint64_t* cursor, int* overflow) {
     if (vs < 0) continue;
     const kx_column* col = &d->out->cols[c];
     uint64_t n = d->vlen[c];
+    if (p->cols[c].kind == KX_COL_LIST_BYTES || p->mside[c]) {  /* element by element */
+      emit_container(d, c, cursor, overflow);
+      continue;
+    }
     const uint64_t lim = arena_lim(col);
     if (d->emit && cursor[vs] + n <= lim) {
       off_set(col, d->rec, cursor[vs]);
@@ -443,6 +579,7 @@ static int check_out(const plan_t* p, const kx_columns* out) {
   for (uint32_t c = 0; c < p->ncols; c++) {
     if (!out->cols[c].data && p->cols[c].kind == KX_COL_FIXED) return KX_ERR_INVALID_ARG;
     if (p->cols[c].kind != KX_COL_FIXED && !out->cols[c].offsets) return KX_ERR_INVALID_ARG;
+    if (p->cols[c].kind == KX_COL_LIST_BYTES && !out->cols[c].elem_offsets) return KX_ERR_INVALID_ARG;
   }
   return KX_OK;
 }
@@ -498,13 +635,20 @@ static void finish_status(const plan_t* p, const kx_columns* out, kx_status* st,
                           uint64_t n_rec, int overflow) {
   int k = 0;
   for (uint32_t c = 0; c < p->ncols; c++) {
-    int vs = p->varidx[c];
+    int vs = p->varidx[c], vs2 = p->varidx2[c];
     if (vs < 0) continue;
-    if (out->cols[c].offsets) {
-      if (cursor[vs] <= arena_lim(&out->cols[c])) off_set(&out->cols[c], n_rec, cursor[vs]);
+    const kx_column* col = &out->cols[c];
+    if (col->offsets) {
+      const uint64_t lim = vs2 >= 0 ? elem_lim(col) : arena_lim(col);
+      if (cursor[vs] <= lim) off_set(col, n_rec, cursor[vs]);
+      else overflow = 1;
+    }
+    if (vs2 >= 0 && col->elem_offsets) {  /* elem_offsets[elements] closes the byte arena */
+      if (cursor[vs] <= elem_lim(col) && cursor[vs2] <= arena_lim(col)) eoff_set(col, cursor[vs], cursor[vs2]);
       else overflow = 1;
     }
     if (k < 8) st->var_total[k++] = cursor[vs];
+    if (vs2 >= 0 && k < 8) st->var_total[k++] = cursor[vs2];
   }
   if (overflow && st->code == 0) st->code = KX_ERR_SIZE_LIMIT;
 }
@@ -666,6 +810,18 @@ static uint64_t write_struct(enc_t* e, int inst, uint64_t pres, uint8_t* b) {
         }
         case KX_T_LIST: case KX_T_SET: {
           uint64_t n = col_len(e, m->col);
+          if (f->elem_ttype == KX_T_STRING) {                  /* FieldFastWriteList of strings */
+            const kx_column* c = &e->in->cols[m->col];
+            const uint64_t E = off_get(c, e->rec);
+            if (b) kxo_write_list_begin(b + off, KX_T_STRING, (int32_t)n);
+            off += 5;
+            for (uint64_t k = 0; k < n; k++) {
+              const uint64_t a0 = eoff_get(c, E + k), l = eoff_get(c, E + k + 1) - a0;
+              if (b) kxo_write_string(b + off, (const uint8_t*)c->data + a0, (uint32_t)l);
+              off += 4 + l;
+            }
+            break;
+          }
           uint32_t w = e->p->cols[m->col].width;
           if (b) {
             const kx_column* c = &e->in->cols[m->col];
@@ -683,6 +839,39 @@ static uint64_t write_struct(enc_t* e, int inst, uint64_t pres, uint8_t* b) {
             }
           }
           off += 5 + n * w;
+          break;
+        }
+        case KX_T_MAP: {  /* FieldFastWriteMap (:875-912) in stored order (Go's map order is random) */
+          const kx_column* kc = &e->in->cols[m->col];
+          const kx_column* vc = &e->in->cols[m->col + 1];
+          const uint8_t kt = f->elem_ttype & 15, vt = (uint8_t)(f->elem_ttype >> 4);
+          const uint64_t n = col_len(e, m->col), EK = off_get(kc, e->rec), EV = off_get(vc, e->rec);
+          if (b) kxo_write_map_begin(b + off, kt, vt, (int32_t)n);
+          off += 6;
+          for (uint64_t k = 0; k < n; k++) {
+            for (int side = 0; side < 2; side++) {
+              const kx_column* c = side ? vc : kc;
+              const uint8_t t = side ? vt : kt;
+              const uint64_t E = side ? EV : EK;
+              if (t == KX_T_STRING) {
+                const uint64_t a0 = eoff_get(c, E + k), l = eoff_get(c, E + k + 1) - a0;
+                if (b) kxo_write_string(b + off, (const uint8_t*)c->data + a0, (uint32_t)l);
+                off += 4 + l;
+              } else {
+                const int w = type_size(t);
+                uint64_t v = 0;
+                memcpy(&v, (const uint8_t*)c->data + (E + k) * (uint64_t)w, (size_t)w);
+                if (b) {
+                  if (t == KX_T_BOOL) b[off] = v ? 1 : 0;
+                  else if (w == 1) b[off] = (uint8_t)v;
+                  else if (w == 2) put16(b + off, (uint16_t)v);
+                  else if (w == 4) put32(b + off, (uint32_t)v);
+                  else put64(b + off, v);
+                }
+                off += (uint64_t)w;
+              }
+            }
+          }
           break;
         }
         case KX_T_STRUCT: {

@@ -221,3 +221,35 @@ def case_skip(skipper, oracle):
     rc, wire, offs = oracle.encode(sch, cs)
     got = skipper(wire, cs.n)
     assert np.array_equal(to_np(got).astype(np.uint64), offs)
+
+
+# ---- containers beyond list<scalar>: list<string>, set<string>, map<K,V> (FieldFastReadList/Map,
+#      struct_tpl.go:466-625) -------------------------------------------------------------------
+CONTAINER_SCHEMAS = {"cx1": (S.schema_cx1, synth.gen_cx1), "cx2": (S.schema_cx2, synth.gen_cx2)}
+
+
+def case_containers(dec, oracle, name, n, mode):
+    mk, gen = CONTAINER_SCHEMAS[name]
+    sch = mk()
+    cs = gen(n, start=5)
+    rc, wire, offs = oracle.encode(sch, cs)
+    assert rc == 0
+    cols, st = check_decode(dec, oracle, sch, wire, n, offsets=offs if mode == "offsets" else None)
+    assert st.code == 0
+    _, infos, _ = oracle.flatten(sch)
+    assert_columns_equal(cols, cs, infos, n)
+
+
+def case_mock_req_fault(dec, oracle):
+    """thrift_data_test.go:100-118: list<i16> bytes where MockReq declares list<string> -> EOF on the
+    device exactly as in the oracle (the reference asserts err != nil); the golden MockReq bytes
+    (thrift_data_test.go:35-40, empty map and list) decode"""
+    from tests.test_oracle_kat import FAULT_MOCK_REQ_THRIFT, MOCK_REQ_THRIFT
+    sch = S.schema_mockreq()
+    for raw, code in ((FAULT_MOCK_REQ_THRIFT, A.ERR_EOF), (MOCK_REQ_THRIFT, 0)):
+        data = np.frombuffer(raw * 3, dtype=np.uint8).copy()
+        offs = np.arange(4, dtype=np.uint64) * len(raw)
+        cols, st = check_decode(dec, oracle, sch, data, 3, offsets=offs)
+        assert st.code == code
+        cols, st = check_decode(dec, oracle, sch, data, 3)
+        assert st.code == code

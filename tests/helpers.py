@@ -16,6 +16,20 @@ def offsets_u64(x):
     return a.view(np.uint64).astype(np.int64) if a.itemsize == 8 else a.view(np.uint32).astype(np.int64)
 
 
+def _assert_list_bytes(got, exp, n, c, ci):
+    """LIST_BYTES: per-record element counts, per-element lengths, element bytes"""
+    go, ge, gd = (to_np(v) for v in got)
+    eo, ee, ed = (to_np(v) for v in exp)
+    go, eo = offsets_u64(go)[:n + 1], offsets_u64(eo)[:n + 1]
+    assert np.array_equal(np.diff(go), np.diff(eo)), f"list column {c} (field {ci.field_id}) counts differ"
+    ge = offsets_u64(ge)[int(go[0]):int(go[-1]) + 1]
+    ee = offsets_u64(ee)[int(eo[0]):int(eo[-1]) + 1]
+    assert np.array_equal(np.diff(ge), np.diff(ee)), f"list column {c} (field {ci.field_id}) element lengths differ"
+    gb = gd.view(np.uint8)[int(ge[0]):int(ge[-1])]
+    eb = ed.view(np.uint8)[int(ee[0]):int(ee[-1])]
+    assert np.array_equal(gb, eb), f"list column {c} (field {ci.field_id}) bytes differ"
+
+
 def assert_columns_equal(got, exp, infos, n, check_presence=True):
     """Field-for-field equality of the first n records (fixed values, var bytes/elements, offsets)."""
     for c, ci in enumerate(infos):
@@ -25,6 +39,8 @@ def assert_columns_equal(got, exp, infos, n, check_presence=True):
             if n:
                 bad = np.nonzero((g != e).any(axis=1))[0]
                 assert bad.size == 0, f"column {c} (field {ci.field_id}) differs at records {bad[:8]}"
+        elif ci.kind == A.COL_LIST_BYTES:
+            _assert_list_bytes(got.cols[c], exp.cols[c], n, c, ci)
         else:
             go, gd = (to_np(v) for v in got.cols[c])
             eo, ed = (to_np(v) for v in exp.cols[c])

@@ -109,3 +109,13 @@ def test_emu_pb_noncanonical(edec, oracle, mode):
 @pytest.mark.parametrize("case", PC.PB_ERRORS)
 def test_emu_pb_errors(edec, oracle, case, mode):
     PC.case_pb_error(edec, oracle, case, mode)
+
+
+@pytest.mark.parametrize("name", ["cx1", "cx2"])
+@pytest.mark.parametrize("mode", ["concat", "offsets"])
+def test_emu_containers(edec, oracle, name, mode):
+    DC.case_containers(edec, oracle, name, 3000, mode)
+
+
+def test_emu_mock_req_fault(edec, oracle):
+    DC.case_mock_req_fault(edec, oracle)

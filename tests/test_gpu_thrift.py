@@ -353,3 +353,14 @@ def test_host_decode_chunked_pipeline(torch, oracle, name):
         out, st = cdc.UnmarshalHost(bad, n, offsets=offs, raise_on_error=False)
         _, _, est, _ = oracle.decode(sch, bad, n, offsets=offs)
         assert (st.code, st.record, st.offset) == (est.code, est.record, est.offset) and st.record == k
+
+
+@pytest.mark.parametrize("name", ["cx1", "cx2"])
+@pytest.mark.parametrize("mode", ["concat", "offsets"])
+@pytest.mark.parametrize("n", [1, 20000])
+def test_decode_containers_match_oracle(gdec, oracle, name, mode, n):
+    DC.case_containers(gdec, oracle, name, n, mode)
+
+
+def test_mock_req_fault_vector_on_gpu(gdec, oracle):
+    DC.case_mock_req_fault(gdec, oracle)

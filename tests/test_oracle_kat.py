@@ -6,6 +6,9 @@ reproduce it before any GPU result is compared with the oracle.
 import struct
 
 import numpy as np
+
+from kitex_amd import schema as S
+from kitex_amd import synth
 import pytest
 
 from kitex_amd import _abi as A
@@ -134,15 +137,61 @@ def test_fault_vector_skip(oracle):
     assert oracle.skip(FAULT_MOCK_REQ_THRIFT, A.T_STRUCT) == (0, len(FAULT_MOCK_REQ_THRIFT))
 
 
-def test_fault_vector_typed_read(oracle):
-    """Declared list<string> read as strings runs past the end (EOF); as list<i16> it decodes."""
-    ok = Schema(Struct("M", [Field(1, A.T_STRING), Field(3, A.T_LIST, elem=A.T_I16)]))
+def test_fault_vector_fails_as_mock_req(oracle):
+    """thrift_data_test.go:100-118: the fault vector sends field 3 as list<i16> where MockReq declares
+    list<string>; FastRead reads the element as a string (i32 length from the i16 bytes) and runs
+    past the end -> the decode FAILS (EOF), exactly where the reference's test asserts err != nil."""
+    sch = S.schema_mockreq()
     data = np.frombuffer(FAULT_MOCK_REQ_THRIFT, dtype=np.uint8).copy()
-    offs = np.array([0, data.size], dtype=np.uint64)
-    rc, out, st, _ = oracle.decode(ok, data, 1, offsets=offs)
+    rc, out, st, rs = oracle.decode(sch, data, 1, offsets=np.array([0, data.size], dtype=np.uint64))
+    assert rc == A.ERR_EOF and st.code == A.ERR_EOF and st.record == 0 and rs[0] == A.ERR_EOF
+    # declared as list<i16> instead, the same bytes decode
+    ok = Schema(Struct("M", [Field(1, A.T_STRING), Field(3, A.T_LIST, elem=A.T_I16)]))
+    rc, out, st, _ = oracle.decode(ok, data, 1, offsets=np.array([0, data.size], dtype=np.uint64))
     assert rc == 0
     lo, le = out.cols[1]
     assert list(le[lo[0]:lo[1]]) == [1]
+
+
+def test_mock_req_encode_decode_golden(oracle):
+    """MockReq{Msg:"hello"} (empty strMap / strList still written, thrift_data_test.go:35-40): the
+    oracle's FastWriteNocopy gives the golden 30 bytes and FastRead gives the struct back"""
+    sch = S.schema_mockreq()
+    _, infos, npres = oracle.flatten(sch)
+    u32 = lambda *v: np.array(v, dtype=np.uint32)  # noqa: E731
+    cs = synth.ColumnSet([(u32(0, 5), np.frombuffer(b"hello", np.uint8).copy()),
+                          (u32(0, 0), u32(0), np.zeros(1, np.uint8)),
+                          (u32(0, 0), u32(0), np.zeros(1, np.uint8)),
+                          (u32(0, 0), u32(0), np.zeros(1, np.uint8))], np.zeros(1, np.uint64), 1)
+    rc, wire, offs = oracle.encode(sch, cs)
+    assert rc == 0 and bytes(wire) == MOCK_REQ_THRIFT
+    data = np.frombuffer(MOCK_REQ_THRIFT, dtype=np.uint8).copy()
+    rc, out, st, _ = oracle.decode(sch, data, 1)
+    assert rc == 0 and st.consumed == 30
+    o, b = out.cols[0]
+    assert bytes(b[o[0]:o[1]]) == b"hello"
+    for c in (1, 2, 3):
+        assert out.cols[c][0][1] - out.cols[c][0][0] == 0
+    # one entry each: map<string,string>{"k": "vv"}, list<string>["a", "", "bcd"]
+    P = oracle.prim
+    one = (P("kxo_write_field_begin", A.T_STRING, 1) + P("kxo_write_string", b"hi", 2)
+           + P("kxo_write_field_begin", A.T_MAP, 2) + P("kxo_write_map_begin", A.T_STRING, A.T_STRING, 1)
+           + P("kxo_write_string", b"k", 1) + P("kxo_write_string", b"vv", 2)
+           + P("kxo_write_field_begin", A.T_LIST, 3) + P("kxo_write_list_begin", A.T_STRING, 3)
+           + P("kxo_write_string", b"a", 1) + P("kxo_write_string", b"", 0) + P("kxo_write_string", b"bcd", 3)
+           + b"\x00")
+    data = np.frombuffer(one, dtype=np.uint8).copy()
+    rc, out, st, _ = oracle.decode(sch, data, 1)
+    assert rc == 0
+    ko, keo, kb = out.cols[1]
+    vo, veo, vb = out.cols[2]
+    lo, leo, lb = out.cols[3]
+    assert (ko[1] - ko[0], bytes(kb[keo[0]:keo[1]])) == (1, b"k")
+    assert (vo[1] - vo[0], bytes(vb[veo[0]:veo[1]])) == (1, b"vv")
+    assert [bytes(lb[leo[k]:leo[k + 1]]) for k in range(lo[0], lo[1])] == [b"a", b"", b"bcd"]
+    assert list(st.var_total[:7]) == [2, 1, 1, 1, 2, 3, 4]
+    rc, wire, _ = oracle.encode(sch, out)
+    assert rc == 0 and bytes(wire) == one
 
 
 # ---- pkg/remote/codec/thrift/codec_apache_test.go ----------------------------------------------
