@@ -208,8 +208,9 @@ int kx_thrift_encode_batch(kx_ctx* c, const kx_schema* s, const kx_columns* in, 
 
 /* ---- Kitex-Protobuf (proto3 body) ----
  * The schema's field ids are proto field numbers; ttype selects the proto scalar mapping
- * (I64 = int64 varint, I32 = int32 varint, BOOL, DOUBLE = fixed64, STRING = string/bytes,
- * LIST of a scalar = packed repeated). offsets semantics as kx_thrift_decode_batch; with
+ * (I64 = int64 varint, I32 = int32 varint, BOOL, DOUBLE = fixed64, STRING = string/bytes).
+ * Repeated / packed fields, maps and nested messages are not supported on this path
+ * (KX_ERR_NOT_IMPLEMENTED); unknown fields are skipped. offsets semantics as kx_thrift_decode_batch; with
  * offsets == NULL the input is the body of `message Batch { repeated Rec recs = 1; }`. */
 int kx_pb_decode_batch(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len,
                        const uint64_t* offsets, uint64_t n, const kx_columns* out,

@@ -255,18 +255,9 @@ int kx_thrift_skip_batch(kx_ctx* c, const uint8_t* in, uint64_t in_len, uint64_t
   return kx_launch_skip(in, in_len, n, offsets_out, status, c->ws, c->ws_size, epoch, st);
 }
 
-// the device encoder writes list<scalar> containers; list<string> / set<string> / map columns
-// decode on the device but encode through the host (oracle-equivalent) path only for now
-static int encode_supported(const kx_schema* s) {
-  for (uint32_t f = 0; f < s->prog.nfields; f++)
-    if (s->prog.f[f].kind == KXP_K_LISTB || s->prog.f[f].kind == KXP_K_MAP) return KX_ERR_NOT_IMPLEMENTED;
-  return KX_OK;
-}
-
 int kx_thrift_encoded_size_batch(kx_ctx* c, const kx_schema* s, const kx_columns* in, uint64_t n,
                                  uint64_t* sizes_out, void* stream) {
   if (!c || !s || !sizes_out) return KX_ERR_INVALID_ARG;
-  if (s && encode_supported(s)) return KX_ERR_NOT_IMPLEMENTED;
   int rc = set_device(c);
   if (rc) return rc;
   hipStream_t st = (hipStream_t)stream;
@@ -283,7 +274,6 @@ int kx_thrift_encoded_size_batch(kx_ctx* c, const kx_schema* s, const kx_columns
 int kx_thrift_encode_batch(kx_ctx* c, const kx_schema* s, const kx_columns* in, uint64_t n, uint8_t* out,
                            uint64_t out_cap, uint64_t* offsets_out, kx_status* status, void* stream) {
   if (!c || !s || !status || (!out && out_cap)) return KX_ERR_INVALID_ARG;
-  if (s && encode_supported(s)) return KX_ERR_NOT_IMPLEMENTED;
   int rc = set_device(c);
   if (rc) return rc;
   hipStream_t st = (hipStream_t)stream;

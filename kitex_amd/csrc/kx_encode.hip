@@ -46,6 +46,19 @@ __device__ __forceinline__ uint64_t var_len(const KxLaunchCols& C, int col, uint
   return off_at(C, col, r + 1) - off_at(C, col, r);
 }
 
+// LIST_BYTES columns: element byte offsets (same width as the record offsets)
+__device__ __forceinline__ uint64_t eoff_at(const KxLaunchCols& C, int col, uint64_t i) {
+  return ((C.owide >> col) & 1) ? ((const uint64_t*)C.eoffs[col])[i] : (uint64_t)((const uint32_t*)C.eoffs[col])[i];
+}
+
+// encoded bytes of elements [E, E + cnt) of a container column side: fixed width or strings
+__device__ __forceinline__ uint64_t side_bytes(const KxProgram& P, const KxLaunchCols& C, int col, uint64_t E,
+                                               uint64_t cnt) {
+  const KxpCol& K = P.col[col];
+  if (K.kind == KXP_K_LISTB) return 4 * cnt + eoff_at(C, col, E + cnt) - eoff_at(C, col, E);
+  return cnt * K.width;
+}
+
 // BLength (struct_tpl.go:266-391)
 __device__ uint64_t record_size(const KxProgram& P, const KxLaunchCols& C, uint64_t r) {
   uint64_t pres = C.presence ? C.presence[r] : 0;
@@ -66,7 +79,13 @@ __device__ uint64_t record_size(const KxProgram& P, const KxLaunchCols& C, uint6
     if (F.kind == KXP_K_FIXED) sz += F.width;
     else if (F.kind == KXP_K_BYTES) sz += 4 + var_len(C, F.col, r);
     else if (F.kind == KXP_K_LIST) sz += 5 + var_len(C, F.col, r) * F.width;
-    else {
+    else if (F.kind == KXP_K_LISTB)  // list/set<string> (FieldListLength, struct_tpl.go:1038-1061)
+      sz += 5 + side_bytes(P, C, F.col, off_at(C, F.col, r), var_len(C, F.col, r));
+    else if (F.kind == KXP_K_MAP) {  // map (FieldMapLength): both sides, the keys' entry count
+      const uint64_t cnt = var_len(C, F.col, r);
+      sz += 6 + side_bytes(P, C, F.col, off_at(C, F.col, r), cnt) +
+            side_bytes(P, C, F.col + 1, off_at(C, F.col + 1, r), cnt);
+    } else {
       if ((pres >> F.pbit) & 1) { inst = F.child; f = P.inst[inst].enc_first; continue; }
       sz += 1;                                   // nil *T -> STOP only (k-mock.go:190-199)
     }
@@ -180,6 +199,34 @@ __device__ void write_record(const KxProgram& P, const KxLaunchCols& C, uint64_t
         if (F.elem == KX_T_BOOL) v = (v & 0xff) ? 1 : 0;
         put_be(s, v, F.width);
       }
+    } else if (F.kind == KXP_K_LISTB || F.kind == KXP_K_MAP) {
+      // FieldFastWriteList of strings / FieldFastWriteMap (struct_tpl.go:875-912, 1011-1036); a map
+      // in column order (Go iterates its maps in random order)
+      const bool map = F.kind == KXP_K_MAP;
+      const uint64_t cnt = var_len(C, F.col, r);
+      if (map) {
+        s.put(F.elem & 15u, 1);
+        s.put(F.elem >> 4, 1);
+      } else {
+        s.put(KX_T_STRING, 1);
+      }
+      put_be(s, cnt, 4);
+      const int nside = map ? 2 : 1;
+      uint64_t E[2] = {off_at(C, F.col, r), map ? off_at(C, F.col + 1, r) : 0};
+      for (uint64_t j = 0; j < cnt; j++)
+        for (int side = 0; side < nside; side++) {
+          const int col = F.col + side;
+          const KxpCol& K = P.col[col];
+          if (K.kind == KXP_K_LISTB) {
+            const uint64_t a = eoff_at(C, col, E[side] + j), len = eoff_at(C, col, E[side] + j + 1) - a;
+            put_be(s, len, 4);
+            put_bytes(s, (const uint8_t*)C.data[col] + a, (uint32_t)len);
+          } else {
+            uint64_t v = load_fixed(C.data[col], K.width, E[side] + j);
+            if (K.elem == KX_T_BOOL) v = (v & 0xff) ? 1 : 0;
+            put_be(s, v, K.width);
+          }
+        }
     } else {
       if ((pres >> F.pbit) & 1) { inst = F.child; f = P.inst[inst].enc_first; continue; }
       s.put(KX_T_STOP, 1);
