@@ -180,6 +180,13 @@ uint64_t kx_schema_min_record_size(const kx_schema* s);
 
 int kx_ctx_create(int device, kx_ctx** out);
 void kx_ctx_destroy(kx_ctx* c);
+/* Decode pipelining of this ctx (a tuning knob; no reference counterpart). A batch of more than two
+ * chunks of `chunk_bytes` input (rounded to whole 512 KiB groups of tiles; 0 = never chunk) is
+ * decoded as a pipeline: the index pass of chunk k runs on a second stream of the ctx while chain +
+ * emit of chunk k - 1 run on the caller's stream, `ahead` chunks apart at most, so the emit pass
+ * re-reads input the index pass has just brought into the Infinity Cache. Results are identical
+ * for every setting. Default: KX_CHUNK_MB environment variable, else 64 MiB, ahead 1. */
+int kx_ctx_set_pipeline(kx_ctx* c, uint64_t chunk_bytes, int ahead);
 
 /* ---- Thrift binary: batched FastRead ----
  * offsets != NULL : record i is in[offsets[i] .. offsets[i+1]) (u64, n+1 entries, device). Each record

@@ -24,7 +24,7 @@ EXPORTS = [
     "kx_pb_encode_batch", "kx_host_decode_batch", "kx_host_pb_decode_batch",
     "kx_thrift_message_begin_length", "kx_thrift_write_message_begin", "kx_thrift_read_message_begin",
     "kx_thrift_decode_messages", "kx_pb_decode_messages", "kx_pb_meta_length", "kx_pb_write_meta",
-    "kx_pb_read_meta",
+    "kx_pb_read_meta", "kx_ctx_set_pipeline",
 ]
 
 
@@ -68,6 +68,7 @@ def lib():
     L.kx_ctx_create.argtypes = [C.c_int, C.POINTER(vp)]
     L.kx_ctx_destroy.argtypes = [vp]
     L.kx_ctx_destroy.restype = None
+    L.kx_ctx_set_pipeline.argtypes = [vp, u64, C.c_int]
     dec = [vp, vp, vp, u64, vp, u64, C.POINTER(A.Columns), vp, vp, vp]
     L.kx_thrift_decode_batch.argtypes = dec
     L.kx_pb_decode_batch.argtypes = dec

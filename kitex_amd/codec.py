@@ -155,6 +155,7 @@ class ThriftCodec:
         self.dschema = schema if isinstance(schema, DeviceSchema) else DeviceSchema(schema)
         self.device = torch.device("cuda", device)
         self._ctxs = {}           # one kx_ctx (workspace) per stream: calls on two streams never share one
+        self._pipeline = None     # (chunk_bytes, ahead) applied to every ctx, None = library default
         self.ctx = self._ctx(None)
 
     def _ctx(self, stream) -> Context:
@@ -162,7 +163,16 @@ class ThriftCodec:
         c = self._ctxs.get(key)
         if c is None:
             c = self._ctxs[key] = Context(self.device.index or 0)
+            if self._pipeline is not None:
+                check(lib().kx_ctx_set_pipeline(c.handle, *self._pipeline), "kx_ctx_set_pipeline")
         return c
+
+    def set_pipeline(self, chunk_bytes: int, ahead: int = 1):
+        """Decode pipelining (kx_ctx_set_pipeline): chunk size in input bytes (0 = one chunk) and how
+        many chunks the index pass may run ahead of emit. Results do not depend on it."""
+        self._pipeline = (int(chunk_bytes), int(ahead))
+        for c in self._ctxs.values():
+            check(lib().kx_ctx_set_pipeline(c.handle, *self._pipeline), "kx_ctx_set_pipeline")
 
     # -- remote.PayloadCodec --------------------------------------------------------------------
     def Name(self) -> str:

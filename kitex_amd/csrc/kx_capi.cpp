@@ -3,6 +3,7 @@
 // Thin, allocation-light host layer: argument checks, per-device upload of the compiled schema,
 // a grow-only workspace per context, and kernel launches on the caller's stream. No torch types,
 // no exceptions cross the boundary.
+#include <stdlib.h>
 #include <string.h>
 
 #include <new>
@@ -33,6 +34,7 @@ int ensure_ws(kx_ctx* c, size_t bytes, hipStream_t stream, uint64_t* epoch) {
   if (c->ws_size < bytes) {
     if (c->ws) {
       KX_HIP_CHECK(hipStreamSynchronize(stream));  // the old workspace may still be in use
+      if (c->pipe.aux) KX_HIP_CHECK(hipStreamSynchronize(c->pipe.aux));
       KX_HIP_CHECK(hipFree(c->ws));
       c->ws = nullptr;
       c->ws_size = 0;
@@ -49,6 +51,25 @@ int ensure_ws(kx_ctx* c, size_t bytes, hipStream_t stream, uint64_t* epoch) {
     c->epoch = 1;
   }
   *epoch = c->epoch;
+  return KX_OK;
+}
+
+// The chunked decode pipeline's second stream and events (KxPipe). Chunk size: KX_CHUNK_MB MiB of
+// 8 KiB tiles (0 = one chunk), KX_CHUNK_AHEAD chunks of index-pass lead.
+static int ensure_pipe(kx_ctx* c) {
+  KxPipe& p = c->pipe;
+  if (p.aux) return KX_OK;
+  const char* e = getenv("KX_CHUNK_MB");
+  const uint64_t mb = e ? strtoull(e, nullptr, 10) : KX_CHUNK_MB_DEFAULT;
+  const char* a = getenv("KX_CHUNK_AHEAD");
+  p.ahead = a ? atoi(a) : 1;
+  p.chunk_tiles = (mb * 128 + 63) & ~63ull;  // 128 tiles of 8 KiB per MiB, whole groups of 64 tiles
+  KX_HIP_CHECK(hipEventCreateWithFlags(&p.fork, hipEventDisableTiming));
+  for (int k = 0; k < KX_PIPE_EV; k++) {
+    KX_HIP_CHECK(hipEventCreateWithFlags(&p.ev_idx[k], hipEventDisableTiming));
+    KX_HIP_CHECK(hipEventCreateWithFlags(&p.ev_emit[k], hipEventDisableTiming));
+  }
+  KX_HIP_CHECK(hipStreamCreateWithFlags(&p.aux, hipStreamNonBlocking));
   return KX_OK;
 }
 
@@ -210,9 +231,29 @@ void kx_ctx_destroy(kx_ctx* c) {
   if (c->pin) (void)hipHostFree(c->pin);
   if (c->dstage) (void)hipFree(c->dstage);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+  if (c->pipe.aux) {
+    (void)hipStreamSynchronize(c->pipe.aux);
+    (void)hipStreamDestroy(c->pipe.aux);
+    (void)hipEventDestroy(c->pipe.fork);
+    for (int k = 0; k < KX_PIPE_EV; k++) {
+      (void)hipEventDestroy(c->pipe.ev_idx[k]);
+      (void)hipEventDestroy(c->pipe.ev_emit[k]);
+    }
+  }
   if (c->h2d_stream) (void)hipStreamDestroy(c->h2d_stream);
   if (c->d2h_stream) (void)hipStreamDestroy(c->d2h_stream);
   delete c;
+}
+
+int kx_ctx_set_pipeline(kx_ctx* c, uint64_t chunk_bytes, int ahead) {
+  if (!c || ahead < 0 || ahead > KX_PIPE_EV - 2) return KX_ERR_INVALID_ARG;
+  int rc = set_device(c);
+  if (rc) return rc;
+  if ((rc = ensure_pipe(c))) return rc;
+  const uint64_t tiles = (chunk_bytes + 8191) / 8192;
+  c->pipe.chunk_tiles = (tiles + 63) & ~63ull;
+  c->pipe.ahead = ahead;
+  return KX_OK;
 }
 
 int kx_thrift_decode_batch(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len,
@@ -235,8 +276,9 @@ int kx_thrift_decode_batch(kx_ctx* c, const kx_schema* s, const uint8_t* in, uin
   size_t ws = kx_decode_ws_bytes(s->prog, in_len, offsets, n);
   uint64_t epoch = 0;
   if ((rc = ensure_ws(c, ws, st, &epoch))) return rc;
+  if ((rc = ensure_pipe(c))) return rc;
   return kx_launch_decode(dp, s->prog, in, in_len, offsets, n, lc, record_status, status, c->ws, c->ws_size,
-                          epoch, st, false);
+                          epoch, st, false, nullptr, nullptr, &c->pipe);
 }
 
 int kx_thrift_skip_batch(kx_ctx* c, const uint8_t* in, uint64_t in_len, uint64_t n, uint64_t* offsets_out,
@@ -318,8 +360,9 @@ int kx_pb_decode_batch(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_
   size_t ws = kx_decode_ws_bytes(s->prog, in_len, offsets, n);
   uint64_t epoch = 0;
   if ((rc = ensure_ws(c, ws, st, &epoch))) return rc;
+  if ((rc = ensure_pipe(c))) return rc;
   return kx_launch_decode(dp, s->prog, in, in_len, offsets, n, lc, record_status, status, c->ws, c->ws_size,
-                          epoch, st, true);
+                          epoch, st, true, nullptr, nullptr, &c->pipe);
 }
 
 // N framed messages: headers on the device (kx_message.hip), then the record bodies through the
@@ -364,8 +407,9 @@ static int decode_messages(kx_ctx* c, const kx_schema* s, const uint8_t* in, uin
   if ((rc = prog_on_device(const_cast<kx_schema*>(s), c->device, &dp))) return rc;
   uint64_t epoch = 0;
   if ((rc = ensure_ws(c, kx_decode_ws_bytes(s->prog, in_len, rs, n), st, &epoch))) return rc;
+  if ((rc = ensure_pipe(c))) return rc;
   if ((rc = kx_launch_decode(dp, s->prog, in, in_len, rs, n, lc, brc, status, c->ws, c->ws_size, epoch, st, pb,
-                             re)))
+                             re, nullptr, &c->pipe)))
     return rc;
   return kx_launch_message_merge(offsets, n, hrc, brc, record_status, status, c->mws, st);
 }
@@ -437,8 +481,9 @@ static int decode_device(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint6
   if ((rc = prog_on_device(const_cast<kx_schema*>(s), c->device, &dp))) return rc;
   uint64_t epoch = 0;
   if ((rc = ensure_ws(c, kx_decode_ws_bytes(s->prog, in_len, offsets, n), st, &epoch))) return rc;
+  if ((rc = ensure_pipe(c))) return rc;
   return kx_launch_decode(dp, s->prog, in, in_len, offsets, n, lc, nullptr, status, c->ws, c->ws_size, epoch, st, pb,
-                          nullptr, var_base);
+                          nullptr, var_base, &c->pipe);
 }
 
 // fastUnmarshal end to end from host (netpoll) memory. With message offsets (the RPC case: framing

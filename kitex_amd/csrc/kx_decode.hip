@@ -85,6 +85,11 @@ struct DecParams {
   uint64_t* nstop;           // records to emit (chain pass)
   uint64_t var_base[KXP_NV_MAX];  // arena positions start here (a chunk of a larger batch)
   uint64_t ntiles, ngroups, slotcap;
+  // chunked pipeline (launch_t): this launch covers tiles [t_lo, t_hi) and groups [g_lo, g_hi); the
+  // chain pass carries its state between chunks in `carry`
+  uint64_t t_lo, t_hi, g_lo, g_hi;
+  uint64_t* carry;
+  int chunk_first, chunk_last;
   uint64_t epoch;            // 16-bit call epoch (never 0)
   uint32_t krec;             // offsets mode: records per tile (<= 64)
   int direct;                // offsets mode without var columns: emit pass only
@@ -1661,8 +1666,8 @@ __global__ void __launch_bounds__(NT, 4) index_kernel(DecParams dp_) {  // 4 wav
   __shared__ __attribute__((aligned(16))) uint32_t WIN[WAVES][WINW];
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
-  const uint64_t t = (uint64_t)blockIdx.x * WAVES + wv;
-  if (t >= dp.ntiles) return;
+  const uint64_t t = dp.t_lo + (uint64_t)blockIdx.x * WAVES + wv;
+  if (t >= dp.t_hi) return;
   LDS uint32_t* win = (LDS uint32_t*)WIN[wv];
   const uint64_t t_start = (dp.diag & 64) ? __builtin_amdgcn_s_memtime() : 0;
   Agg a;
@@ -1677,7 +1682,6 @@ __global__ void __launch_bounds__(NT, 4) index_kernel(DecParams dp_) {  // 4 wav
   }
   if (lane == 0 && !(dp.diag & 4)) put_tile(dp, t, a, NV);
   if ((dp.diag & 64) && lane == 0) atomicAdd(&g_phase[5], (unsigned long long)(__builtin_amdgcn_s_memtime() - t_start));
-  const uint64_t g = t / GT;
 }
 
 // ---- kernel 1b: group scan (one wave per group of 64 tiles) ----
@@ -1688,8 +1692,8 @@ __global__ void __launch_bounds__(NT) group_kernel(DecParams dp_) {
   __shared__ __attribute__((aligned(16))) uint32_t WIN[WAVES][WINW];
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
-  const uint64_t g = (uint64_t)blockIdx.x * WAVES + wv;
-  if (g >= dp.ngroups) return;
+  const uint64_t g = dp.g_lo + (uint64_t)blockIdx.x * WAVES + wv;
+  if (g >= dp.g_hi) return;
   group_scan<NV, MODE, false>(dp, (LDS uint32_t*)WIN[wv], g, g == 0 && !dp.offsets ? 0ull : X_NONE, lane);
 }
 
@@ -1709,23 +1713,34 @@ __global__ void __launch_bounds__(CT) chain_kernel(DecParams dp_) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const uint64_t ep = dp.epoch, ng = dp.ngroups;
   const bool chain = !dp.offsets;
+  uint64_t* const cy = dp.carry;  // chain state between chunks: E, cnt, var[8], nstop, err | done << 1
   if (tid == 0) {
-    s_E = 0;  // the chain enters group 0 at offset 0
-    s_cnt = 0;
-    for (int v = 0; v < KXP_NV_MAX; v++) s_var[v] = dp.var_base[v];  // arena units before this call
-    s_nstop = dp.n;
-    s_err = 0;
-    s_done = 0;
+    if (dp.chunk_first) {
+      s_E = 0;  // the chain enters group 0 at offset 0
+      s_cnt = 0;
+      for (int v = 0; v < KXP_NV_MAX; v++) s_var[v] = dp.var_base[v];  // arena units before this call
+      s_nstop = dp.n;
+      s_err = 0;
+      s_done = 0;
+    } else {
+      s_E = cy[0];
+      s_cnt = cy[1];
+      for (int v = 0; v < KXP_NV_MAX; v++) s_var[v] = cy[2 + v];
+      s_nstop = cy[10];
+      s_err = (int)(cy[11] & 1);
+      s_done = (int)(cy[11] >> 1);
+    }
   }
   __syncthreads();
-  for (uint64_t b0 = 0; b0 < ng; b0 += CT) {
+  const uint64_t gend = dp.g_hi;
+  for (uint64_t b0 = dp.g_lo; b0 < gend; b0 += CT) {
     if (s_err || s_done) {  // the chain already ended: later groups emit nothing
       const uint64_t g = b0 + tid;
-      if (g < ng) put_word(dp.gdesc, ng, G_BCNT, g, ep, X_DONE);
+      if (g < gend) put_word(dp.gdesc, ng, G_BCNT, g, ep, X_DONE);
       continue;
     }
     const uint64_t g = b0 + tid;
-    const bool act = g < ng;
+    const bool act = g < gend;
     uint64_t gent, gex, cnt, errc, errp, var[NV > 0 ? NV : 1];
     uint64_t base, vbase[NV > 0 ? NV : 1], c0, vx[NV > 0 ? NV : 1];
     bool live, dead;
@@ -1836,7 +1851,7 @@ __global__ void __launch_bounds__(CT) chain_kernel(DecParams dp_) {
   // the chain ran out of input before n records: EOF at the record after the last one
   if (tid == 0) {
     const uint64_t tot = s_cnt;
-    if (chain && !s_err && tot < dp.n) {
+    if (dp.chunk_last && chain && !s_err && tot < dp.n) {
       kx_status* st = dp.status;
       st->code = KX_ERR_EOF; st->record = tot; st->offset = dp.in_len;
       st->n_records = tot; st->consumed = dp.in_len;
@@ -1849,7 +1864,15 @@ __global__ void __launch_bounds__(CT) chain_kernel(DecParams dp_) {
       if (MODE == M_SKIP) dp.skip_out[tot] = dp.in_len;
       s_nstop = tot;
     }
-    *dp.nstop = s_nstop;
+    // emit of this chunk bounds itself by nstop: final once the chain has ended, else unbounded
+    *dp.nstop = (dp.chunk_last || s_err || s_done) ? s_nstop : ~0ull;
+    if (!dp.chunk_last) {
+      cy[0] = s_E;
+      cy[1] = s_cnt;
+      for (int v = 0; v < KXP_NV_MAX; v++) cy[2 + v] = s_var[v];
+      cy[10] = s_nstop;
+      cy[11] = (uint64_t)(s_err != 0) | (uint64_t)(s_done != 0) << 1;
+    }
   }
 }
 
@@ -1919,8 +1942,8 @@ __global__ void __launch_bounds__(NT) emit_kernel(DecParams dp_) {
   __shared__ __attribute__((aligned(16))) uint32_t WIN[WAVES][WINW];
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
-  const uint64_t t = (uint64_t)blockIdx.x * WAVES + wv;
-  if (t >= dp.ntiles) return;
+  const uint64_t t = dp.t_lo + (uint64_t)blockIdx.x * WAVES + wv;
+  if (t >= dp.t_hi) return;
   const KAS KxProgram* P = dp.prog;
   const bool known = dp.offsets != nullptr;
   const uint64_t nstop = known ? dp.n : *(volatile uint64_t*)dp.nstop;
@@ -2091,13 +2114,26 @@ WsLayout ws_layout(uint64_t min_rec, uint64_t in_len, const uint64_t* offsets, u
   return L;
 }
 
+// chunk k of a chunked call: tiles [k·cht, (k+1)·cht) and the groups they make up
+DecParams chunk_params(const DecParams& dp, uint64_t k, uint64_t nch, uint64_t cht) {
+  DecParams c = dp;
+  c.t_lo = k * cht;
+  c.t_hi = kmin64(dp.ntiles, c.t_lo + cht);
+  c.g_lo = c.t_lo / GT;
+  c.g_hi = (c.t_hi + GT - 1) / GT;
+  c.chunk_first = k == 0;
+  c.chunk_last = k + 1 == nch;
+  return c;
+}
+
 template <int NV, int MODE>
-int launch_t(const DecParams& dp0, const WsLayout& L, void* ws, hipStream_t stream) {
+int launch_t(const DecParams& dp0, const WsLayout& L, void* ws, hipStream_t stream, const KxPipe* pp) {
   DecParams dp = dp0;
   char* base = (char*)ws;
   dp.errkey = (unsigned long long*)(base + 8);
   dp.overflow = (uint32_t*)(base + 16);
   dp.nstop = (uint64_t*)(base + 24);
+  dp.carry = (uint64_t*)(base + 64);  // 12 words, inside WS_HDR
   dp.tdesc = (uint64_t*)(base + L.tdesc);
   dp.gdesc = (uint64_t*)(base + L.gdesc);
   dp.starts = (uint16_t*)(base + L.starts);
@@ -2105,11 +2141,51 @@ int launch_t(const DecParams& dp0, const WsLayout& L, void* ws, hipStream_t stre
   dp.ngroups = L.ngroups;
   dp.slotcap = L.slotcap;
   dp.direct = dp.offsets && NV == 0;
+  dp.t_lo = 0; dp.t_hi = dp.ntiles; dp.g_lo = 0; dp.g_hi = dp.ngroups;
+  dp.chunk_first = dp.chunk_last = 1;
   KX_HIP_CHECK(hipMemsetAsync(dp.status, 0, sizeof(kx_status), stream));
   const unsigned grid = (unsigned)((dp.ntiles + WAVES - 1) / WAVES);
   const unsigned ggrid = (unsigned)((dp.ngroups + WAVES - 1) / WAVES);
   if (dp.diag & 256) {
     hipLaunchKernelGGL((index_kernel<NV, MODE>), dim3(grid), dim3(NT), 0, stream, dp);
+    return KX_OK;
+  }
+  const uint64_t cht = pp && pp->aux ? pp->chunk_tiles : 0;
+  if (!dp.direct && cht && dp.ntiles >= 2 * cht) {
+    // chunked pipeline: aux stream index + group(k) | caller's stream chain + emit(k - ahead)
+    const uint64_t nch = (dp.ntiles + cht - 1) / cht;
+    const uint64_t D = (uint64_t)(pp->ahead < 0 ? 0 : pp->ahead > KX_PIPE_EV - 2 ? KX_PIPE_EV - 2 : pp->ahead);
+    KX_HIP_CHECK(hipEventRecord(pp->fork, stream));
+    KX_HIP_CHECK(hipStreamWaitEvent(pp->aux, pp->fork, 0));
+    for (uint64_t s = 0; s < nch + D; s++) {
+      if (s < nch) {
+        const uint64_t k = s;
+        // the index pass runs at most `ahead` chunks in front of emit (Infinity-Cache residency)
+        if (k >= D + 1) KX_HIP_CHECK(hipStreamWaitEvent(pp->aux, pp->ev_emit[(k - D - 1) % KX_PIPE_EV], 0));
+        const DecParams c = chunk_params(dp, k, nch, cht);
+        const unsigned cg = (unsigned)((c.t_hi - c.t_lo + WAVES - 1) / WAVES);
+        const unsigned gg = (unsigned)((c.g_hi - c.g_lo + WAVES - 1) / WAVES);
+        hipLaunchKernelGGL((index_kernel<NV, MODE>), dim3(cg), dim3(NT), 0, pp->aux, c);
+        KX_HIP_CHECK(hipGetLastError());
+        hipLaunchKernelGGL((group_kernel<NV, MODE>), dim3(gg), dim3(NT), 0, pp->aux, c);
+        KX_HIP_CHECK(hipGetLastError());
+        KX_HIP_CHECK(hipEventRecord(pp->ev_idx[k % KX_PIPE_EV], pp->aux));
+      }
+      if (s >= D) {
+        const uint64_t k = s - D;
+        const DecParams c = chunk_params(dp, k, nch, cht);
+        const unsigned cg = (unsigned)((c.t_hi - c.t_lo + WAVES - 1) / WAVES);
+        KX_HIP_CHECK(hipStreamWaitEvent(stream, pp->ev_idx[k % KX_PIPE_EV], 0));
+        hipLaunchKernelGGL((chain_kernel<NV, MODE>), dim3(1), dim3(CT), 0, stream, c);
+        KX_HIP_CHECK(hipGetLastError());
+        hipLaunchKernelGGL((emit_kernel<NV, MODE>), dim3(cg), dim3(NT), 0, stream, c);
+        KX_HIP_CHECK(hipGetLastError());
+        KX_HIP_CHECK(hipEventRecord(pp->ev_emit[k % KX_PIPE_EV], stream));
+      }
+    }
+    hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(64), 0, stream, dp.status, dp.errkey, dp.overflow, dp.nstop,
+                       dp.offsets, dp.n);
+    KX_HIP_CHECK(hipGetLastError());
     return KX_OK;
   }
   if (!dp.direct) {
@@ -2147,11 +2223,13 @@ void fill_diag_flags(DecParams& dp) {
 #define KX_OWNS(p) (KX_DEC_PART < 0 || KX_DEC_PART == (p))
 
 template <int NV, int MODE>
-int kx_dec_launch(const void* dp, const void* L, void* ws, hipStream_t stream) {
-  return launch_t<NV, MODE>(*(const DecParams*)dp, *(const WsLayout*)L, ws, stream);
+int kx_dec_launch(const void* dp, const void* L, void* ws, hipStream_t stream, const KxPipe* pp) {
+  return launch_t<NV, MODE>(*(const DecParams*)dp, *(const WsLayout*)L, ws, stream, pp);
 }
-#define KX_DEF(NV, MODE) template int kx_dec_launch<NV, MODE>(const void*, const void*, void*, hipStream_t);
-#define KX_EXT(NV, MODE) extern template int kx_dec_launch<NV, MODE>(const void*, const void*, void*, hipStream_t);
+#define KX_DEF(NV, MODE) \
+  template int kx_dec_launch<NV, MODE>(const void*, const void*, void*, hipStream_t, const KxPipe*);
+#define KX_EXT(NV, MODE) \
+  extern template int kx_dec_launch<NV, MODE>(const void*, const void*, void*, hipStream_t, const KxPipe*);
 #if KX_OWNS(0)
 KX_DEF(0, M_THRIFT) KX_DEF(1, M_THRIFT)
 #else
@@ -2185,13 +2263,14 @@ KX_EXT(4, M_PB) KX_EXT(8, M_PB)
 
 #if KX_DEC_PART <= 0
 template <int MODE>
-static int launch_nv(const DecParams& dp, const WsLayout& L, void* ws, hipStream_t stream, uint32_t nvar) {
+static int launch_nv(const DecParams& dp, const WsLayout& L, void* ws, hipStream_t stream, uint32_t nvar,
+                     const KxPipe* pp) {
   switch (nvar) {
-    case 0: return kx_dec_launch<0, MODE>(&dp, &L, ws, stream);
-    case 1: return kx_dec_launch<1, MODE>(&dp, &L, ws, stream);
-    case 2: return kx_dec_launch<2, MODE>(&dp, &L, ws, stream);
-    case 3: case 4: return kx_dec_launch<4, MODE>(&dp, &L, ws, stream);
-    default: return kx_dec_launch<8, MODE>(&dp, &L, ws, stream);
+    case 0: return kx_dec_launch<0, MODE>(&dp, &L, ws, stream, pp);
+    case 1: return kx_dec_launch<1, MODE>(&dp, &L, ws, stream, pp);
+    case 2: return kx_dec_launch<2, MODE>(&dp, &L, ws, stream, pp);
+    case 3: case 4: return kx_dec_launch<4, MODE>(&dp, &L, ws, stream, pp);
+    default: return kx_dec_launch<8, MODE>(&dp, &L, ws, stream, pp);
   }
 }
 
@@ -2213,7 +2292,7 @@ size_t kx_skip_ws_bytes(uint64_t in_len) { return ws_layout(1, in_len, nullptr, 
 int kx_launch_decode(const KxProgram* dprog, const KxProgram& hprog, const uint8_t* in, uint64_t in_len,
                      const uint64_t* offsets, uint64_t n, const KxLaunchCols& cols, uint8_t* record_status,
                      kx_status* status, void* ws, size_t ws_size, uint64_t epoch, hipStream_t stream, bool pb,
-                     const uint64_t* ends, const uint64_t* var_base) {
+                     const uint64_t* ends, const uint64_t* var_base, const KxPipe* pipe) {
   DecParams dp{};
   fill_diag_flags(dp);
   if (var_base)
@@ -2224,7 +2303,8 @@ int kx_launch_decode(const KxProgram* dprog, const KxProgram& hprog, const uint8
   dp.krec = krec_for(in_len, n);
   const WsLayout L = ws_layout(hprog.fixed_min, in_len, offsets, n);
   if (ws_size < L.total) return KX_ERR_INVALID_ARG;
-  return pb ? launch_nv<M_PB>(dp, L, ws, stream, hprog.nvar) : launch_nv<M_THRIFT>(dp, L, ws, stream, hprog.nvar);
+  return pb ? launch_nv<M_PB>(dp, L, ws, stream, hprog.nvar, pipe)
+            : launch_nv<M_THRIFT>(dp, L, ws, stream, hprog.nvar, pipe);
 }
 
 int kx_launch_skip(const uint8_t* in, uint64_t in_len, uint64_t n, uint64_t* offsets_out, kx_status* status,
@@ -2236,6 +2316,6 @@ int kx_launch_skip(const uint8_t* in, uint64_t in_len, uint64_t n, uint64_t* off
   dp.krec = 64;
   const WsLayout L = ws_layout(1, in_len, nullptr, n);
   if (ws_size < L.total) return KX_ERR_INVALID_ARG;
-  return kx_dec_launch<0, M_SKIP>(&dp, &L, ws, stream);
+  return kx_dec_launch<0, M_SKIP>(&dp, &L, ws, stream, nullptr);
 }
 #endif  // KX_DEC_PART <= 0

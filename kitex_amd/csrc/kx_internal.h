@@ -24,8 +24,23 @@ struct kx_schema {
   void* dev_prog[64] = {nullptr};
 };
 
+// Chunked decode pipeline (kx_decode.hip launch_t): index + group of chunk k run on `aux` while chain +
+// emit of chunk k - 1 run on the caller's stream, so emit re-reads a chunk the index pass has just
+// pulled through the Infinity Cache. Events order the two streams (rings of KX_PIPE_EV).
+#define KX_PIPE_EV 8
+#define KX_CHUNK_MB_DEFAULT 64
+struct KxPipe {
+  hipStream_t aux = nullptr;
+  hipEvent_t fork = nullptr;
+  hipEvent_t ev_idx[KX_PIPE_EV] = {};   // chunk k indexed (aux) -> chain(k) may start
+  hipEvent_t ev_emit[KX_PIPE_EV] = {};  // chunk k emitted (caller's stream) -> throttles aux
+  uint64_t chunk_tiles = 0;             // tiles per chunk (a multiple of 64), 0 = one chunk
+  int ahead = 1;                        // chunks the index pass may run ahead of emit
+};
+
 struct kx_ctx {
   int device = 0;
+  KxPipe pipe;                         // created lazily (ensure_pipe)
   hipStream_t own_stream = nullptr;
   hipStream_t h2d_stream = nullptr, d2h_stream = nullptr;  // kx_host_decode_batch copy engines
   // grow-only decode workspace: tile counter, error key, overflow flag, epoch-tagged tile
@@ -68,7 +83,8 @@ int kx_launch_decode(const KxProgram* dprog, const KxProgram& hprog, const uint8
                      uint64_t in_len, const uint64_t* offsets, uint64_t n,
                      const KxLaunchCols& cols, uint8_t* record_status, kx_status* status,
                      void* ws, size_t ws_size, uint64_t epoch, hipStream_t stream, bool pb,
-                     const uint64_t* ends = nullptr, const uint64_t* var_base = nullptr);
+                     const uint64_t* ends = nullptr, const uint64_t* var_base = nullptr,
+                     const KxPipe* pipe = nullptr);
 size_t kx_decode_ws_bytes(const KxProgram& hprog, uint64_t in_len, const uint64_t* offsets, uint64_t n);
 
 int kx_launch_skip(const uint8_t* in, uint64_t in_len, uint64_t n, uint64_t* offsets_out,

@@ -253,3 +253,56 @@ def case_mock_req_fault(dec, oracle):
         assert st.code == code
         cols, st = check_decode(dec, oracle, sch, data, 3)
         assert st.code == code
+
+
+# ---- chunked pipeline (launch_t): the batch is cut into whole groups of tiles; index + group of
+#      chunk k overlap chain + emit of chunk k - ahead, the chain state is carried between chunks ----
+CHUNK_CASES = ["r2", "r3", "r2_offsets", "error", "error_offsets", "truncated", "short_input", "fewer",
+               "noncanonical", "pb", "pb_offsets", "containers"]
+
+
+def case_chunked(dec, oracle, case):
+    """each batch spans >= 4 chunks of 64 tiles (512 KiB); errors / the end of the chain fall in a
+    middle chunk"""
+    n = 15000
+    if case in ("r2", "r3", "r2_offsets"):
+        name = case.split("_")[0]
+        n = 5000 if name == "r3" else n
+        sch = S.SCHEMAS[name]()
+        rc, wire, offs = oracle.encode(sch, synth.GENERATORS[name](n, start=3))
+        check_decode(dec, oracle, sch, wire, n, offsets=offs if case.endswith("offsets") else None)
+        return
+    if case in ("pb", "pb_offsets"):
+        from tests import pb_cases as PC
+        PC.case_pb_concat(dec, oracle, 20000) if case == "pb" else PC.case_pb_offsets(dec, oracle, 20000)
+        return
+    if case == "containers":
+        case_containers(dec, oracle, "cx1", 6000, "concat")
+        return
+    sch = S.schema_r2()
+    rng = np.random.default_rng(9)
+    if case == "noncanonical":
+        recs = []
+        for i in range(n):
+            k = i % 97
+            recs.append(r2_record(oracle, rng, order=list(rng.permutation(10))) if k == 3 else
+                        r2_record(oracle, rng, dup=True) if k == 50 else r2_record(oracle, rng))
+        wire, offs = concat(recs)
+        check_decode(dec, oracle, sch, wire, n)
+        check_decode(dec, oracle, sch, wire, n, offsets=offs)
+        return
+    cs = synth.gen_r2(n, start=11)
+    rc, wire, offs = oracle.encode(sch, cs)
+    if case in ("error", "error_offsets"):
+        # record 9001 gets an unknown wire type in place of field 1's header
+        p = int(offs[9001])
+        wire = wire.copy()
+        wire[p] = 99
+        check_decode(dec, oracle, sch, wire, n, offsets=offs if case == "error_offsets" else None)
+    elif case == "truncated":
+        check_decode(dec, oracle, sch, wire[:int(offs[11000]) + 40].copy(), n)
+    elif case == "short_input":
+        check_decode(dec, oracle, sch, wire, n + 3)
+    elif case == "fewer":
+        cols, st = check_decode(dec, oracle, sch, wire, 6000)   # the chain ends in chunk 1 of 5
+        assert st.consumed == int(offs[6000])

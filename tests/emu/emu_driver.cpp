@@ -45,7 +45,16 @@ extern "C" int emu_decode(const kx_struct_desc* structs, uint32_t nstructs, cons
   if (skip)
     rc = kx_launch_skip(in, in_len, n, skip_out, status, ws, ws_cap, epoch, nullptr);
   else
+  {
+    // KX_EMU_CHUNK = tiles per chunk (a multiple of 64): the chunked two-stream pipeline of launch_t
+    static KxPipe pipe;
+    const char* e = getenv("KX_EMU_CHUNK");
+    pipe.chunk_tiles = e ? strtoull(e, nullptr, 10) : 0;
+    const char* a = getenv("KX_EMU_AHEAD");
+    pipe.ahead = a ? atoi(a) : 1;
+    pipe.aux = (hipStream_t)&pipe;  // any non-null handle
     rc = kx_launch_decode(&s.prog, s.prog, in, in_len, offsets, n, lc, record_status, status, ws, ws_cap, epoch,
-                          nullptr, mode == 2);
+                          nullptr, mode == 2, nullptr, nullptr, &pipe);
+  }
   return rc;
 }

@@ -185,6 +185,11 @@ inline hipError_t hipMemcpyAsync(void* d, const void* s, size_t n, hipMemcpyKind
   return hipSuccess;
 }
 inline hipError_t hipStreamSynchronize(hipStream_t) { return hipSuccess; }
+// streams and events: the emulator runs every launch at enqueue time, in enqueue order (a valid
+// serialisation of any multi-stream schedule the event waits allow)
+typedef void* hipEvent_t;
+inline hipError_t hipEventRecord(hipEvent_t, hipStream_t) { return hipSuccess; }
+inline hipError_t hipStreamWaitEvent(hipStream_t, hipEvent_t, unsigned) { return hipSuccess; }
 inline hipError_t hipMemsetAsync(void* p, int v, size_t n, hipStream_t) {
   memset(p, v, n);
   return hipSuccess;

@@ -119,3 +119,12 @@ def test_emu_containers(edec, oracle, name, mode):
 
 def test_emu_mock_req_fault(edec, oracle):
     DC.case_mock_req_fault(edec, oracle)
+
+
+@pytest.mark.parametrize("ahead", [0, 1, 3])
+@pytest.mark.parametrize("case", DC.CHUNK_CASES)
+def test_emu_chunked(edec, oracle, case, ahead, monkeypatch):
+    """the chunked two-stream pipeline (64-tile chunks, index pass 0/1/3 chunks ahead of emit)"""
+    monkeypatch.setenv("KX_EMU_CHUNK", "64")
+    monkeypatch.setenv("KX_EMU_AHEAD", str(ahead))
+    DC.case_chunked(edec, oracle, case)
