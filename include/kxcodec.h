@@ -70,6 +70,9 @@ enum {
   KX_ERR_EOF = 8,              /* record runs past the end of its buffer */
   KX_ERR_APPLICATION_EXCEPTION = 9, /* message of type EXCEPTION: a TApplicationException, not a
                                        record (thrift.go:192-195; decoded by the host shim) */
+  KX_ERR_UNKNOWN_PROTOCOL = 10, /* framing sniff: no TTHeader / Mesh / Framed / PurePayload / Kitex-PB
+                                  magic where one is required, or a malformed TTHeader / Mesh header
+                                  (perrors UnknownProtocolError, type 0, default_codec.go:411-416) */
   KX_ERR_INVALID_ARG = 100,
   KX_ERR_HIP = 101,            /* a HIP runtime call failed */
   KX_ERR_NO_DEVICE = 102,
@@ -264,6 +267,36 @@ int kx_thrift_decode_messages(kx_ctx* c, const kx_schema* s, const uint8_t* in, 
 int kx_pb_decode_messages(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len,
                           const uint64_t* offsets, uint64_t n, const kx_column* msg_cols,
                           const kx_columns* out, uint8_t* record_status, kx_status* status, void* stream);
+
+/* ---- socket buffer level: framing sniff (defaultCodec.DecodeMeta + checkPayload,
+ *      default_codec.go:189-221, 328-427; Mesh header header_codec.go:192-212; TTHeader meta and
+ *      info blocks per gopkg protocol/ttheader) ----
+ * in = n frames back to back (device). Per frame: frame_offsets[i] (n + 1 entries; frame i =
+ * [frame_offsets[i], frame_offsets[i+1])), the payload the payload codec reads = [payload_start[i],
+ * payload_end[i]) (MessageBegin / Kitex-PB meta first; the Framed length and all headers removed),
+ * kinds[i] (optional) = transport.Protocol (KX_TRANS_*) | KX_FRAME_PB | KX_FRAME_MESH.
+ * PurePayload frames (no length prefix) are delimited by their MessageBegin + struct.
+ * max_payload > 0: a longer payload is INVALID_DATA (checkPayloadSize, :429-434).
+ * Status as concatenated decode: the first frame that cannot be delimited (UNKNOWN_PROTOCOL, EOF,
+ * ...), status->n_records = frames delimited; boundaries are found in parallel on the device. */
+enum {
+  KX_TRANS_PURE = 0, KX_TRANS_TTHEADER = 2, KX_TRANS_FRAMED = 4, KX_TRANS_TTHEADER_FRAMED = 6,
+  KX_FRAME_PB = 0x10, KX_FRAME_MESH = 0x20
+};
+int kx_frame_scan(kx_ctx* c, const uint8_t* in, uint64_t in_len, uint64_t n, uint64_t max_payload,
+                  uint64_t* frame_offsets, uint64_t* payload_start, uint64_t* payload_end, uint8_t* kinds,
+                  kx_status* status, void* stream);
+/* A socket buffer of n frames straight to columns: kx_frame_scan, then kx_*_decode_messages on the
+ * payloads. frame_offsets (n + 1) and kinds are optional outputs. A frame that cannot be delimited
+ * ends the batch: it and every later message get its code in record_status, and the call's status
+ * is the scan's (record = that frame, offset = its start). */
+int kx_thrift_decode_frames(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len, uint64_t n,
+                            int32_t body_field, uint64_t max_payload, uint64_t* frame_offsets, uint8_t* kinds,
+                            const kx_column* msg_cols, const kx_columns* out, uint8_t* record_status,
+                            kx_status* status, void* stream);
+int kx_pb_decode_frames(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len, uint64_t n,
+                        uint64_t max_payload, uint64_t* frame_offsets, uint8_t* kinds, const kx_column* msg_cols,
+                        const kx_columns* out, uint8_t* record_status, kx_status* status, void* stream);
 
 /* Kitex-Protobuf meta header (host memory; protobuf.go:77-90 / 136-165). */
 uint64_t kx_pb_meta_length(uint32_t name_len);

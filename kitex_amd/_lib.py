@@ -24,7 +24,8 @@ EXPORTS = [
     "kx_pb_encode_batch", "kx_host_decode_batch", "kx_host_pb_decode_batch",
     "kx_thrift_message_begin_length", "kx_thrift_write_message_begin", "kx_thrift_read_message_begin",
     "kx_thrift_decode_messages", "kx_pb_decode_messages", "kx_pb_meta_length", "kx_pb_write_meta",
-    "kx_pb_read_meta", "kx_ctx_set_pipeline",
+    "kx_pb_read_meta", "kx_ctx_set_pipeline", "kx_frame_scan", "kx_thrift_decode_frames",
+    "kx_pb_decode_frames",
 ]
 
 
@@ -88,6 +89,11 @@ def lib():
                                             C.POINTER(A.Columns), vp, vp, vp]
     L.kx_pb_decode_messages.argtypes = [vp, vp, vp, u64, vp, u64, C.POINTER(A.Column), C.POINTER(A.Columns),
                                         vp, vp, vp]
+    L.kx_frame_scan.argtypes = [vp, vp, u64, u64, u64, vp, vp, vp, vp, vp, vp]
+    L.kx_thrift_decode_frames.argtypes = [vp, vp, vp, u64, u64, i32, u64, vp, vp, C.POINTER(A.Column),
+                                          C.POINTER(A.Columns), vp, vp, vp]
+    L.kx_pb_decode_frames.argtypes = [vp, vp, vp, u64, u64, u64, vp, vp, C.POINTER(A.Column),
+                                      C.POINTER(A.Columns), vp, vp, vp]
     L.kx_pb_meta_length.argtypes = [u32]
     L.kx_pb_meta_length.restype = u64
     L.kx_pb_write_meta.argtypes = L.kx_thrift_write_message_begin.argtypes

@@ -121,6 +121,8 @@ class MessageBatch(DecodeResult):
     names: "object" = None     # (int64 offsets[n+1], uint8 arena) method names
     msg_type: "object" = None  # int32[n]
     seqid: "object" = None     # int32[n]
+    frame_offsets: "object" = None  # UnmarshalFrames: int64[n + 1]
+    kinds: "object" = None          # UnmarshalFrames: uint8[n]
 
     def name(self, i: int) -> str:
         o = self.names[0]
@@ -228,6 +230,7 @@ class ThriftCodec:
         return out, st
 
     _MESSAGES = "kx_thrift_decode_messages"
+    _FRAMES = "kx_thrift_decode_frames"
 
     def UnmarshalMessages(self, buf, n: int, offsets, body_field: int = 1, out: ColumnSet = None,
                           var_caps: Sequence[int] = None, name_cap: int = None, stream=None,
@@ -235,6 +238,32 @@ class ThriftCodec:
         """thriftCodec.Unmarshal over n framed messages: buf[offsets[i]:offsets[i+1]] = MessageBegin +
         the method's Args (body_field 1) / Result (body_field 0) struct holding one record.
         Returns the record columns plus method name / message type / seqid columns."""
+        s = _stream(stream)
+        args = [self._ctx(s).handle, self.dschema.handle, _ptr(buf), buf.numel(), _ptr(offsets), n]
+        if self._MESSAGES == "kx_thrift_decode_messages":
+            args.append(body_field)
+        return self._messages(self._MESSAGES, args, buf, n, out, var_caps, name_cap, s, raise_on_error)
+
+    def UnmarshalFrames(self, buf, n: int, body_field: int = 1, max_payload: int = 0, out: ColumnSet = None,
+                        var_caps: Sequence[int] = None, name_cap: int = None, stream=None,
+                        raise_on_error: bool = True) -> "MessageBatch":
+        """A socket buffer of n frames (TTHeader / Mesh / Framed / PurePayload, default_codec.go:189-221)
+        straight to columns: framing sniff on the device, then UnmarshalMessages on the payloads.
+        The batch also carries frame_offsets (int64[n+1]) and kinds (uint8[n], transport.Protocol |
+        FRAME_PB | FRAME_MESH)."""
+        import torch
+        s = _stream(stream)
+        fo = torch.zeros(n + 1, dtype=torch.int64, device=self.device)
+        kinds = torch.zeros(max(1, n), dtype=torch.uint8, device=self.device)
+        args = [self._ctx(s).handle, self.dschema.handle, _ptr(buf), buf.numel(), n]
+        if self._FRAMES == "kx_thrift_decode_frames":
+            args.append(body_field)
+        args += [max_payload, _ptr(fo), _ptr(kinds)]
+        res = self._messages(self._FRAMES, args, buf, n, out, var_caps, name_cap, s, raise_on_error)
+        res.frame_offsets, res.kinds = fo, kinds[:n]
+        return res
+
+    def _messages(self, fn, args, buf, n, out, var_caps, name_cap, s, raise_on_error):
         import torch
         ds = self.dschema
         if out is None:
@@ -254,12 +283,8 @@ class ThriftCodec:
         mc[2].data = seqid.data_ptr()
         st = status_tensor(self.device)
         rs = torch.empty(max(1, n), dtype=torch.uint8, device=self.device)
-        s = _stream(stream)
-        args = [self._ctx(s).handle, ds.handle, _ptr(buf), buf.numel(), _ptr(offsets), n]
-        if self._MESSAGES == "kx_thrift_decode_messages":
-            args.append(body_field)
-        rc = getattr(lib(), self._MESSAGES)(*args, mc, C.byref(kc), _ptr(rs), _ptr(st), int(s.cuda_stream))
-        check(rc, self._MESSAGES)
+        rc = getattr(lib(), fn)(*args, mc, C.byref(kc), _ptr(rs), _ptr(st), int(s.cuda_stream))
+        check(rc, fn)
         res = MessageBatch(out, st, rs, s, names, mtype[:n], seqid[:n])
         if raise_on_error:
             stt = res.read_status()
@@ -334,6 +359,7 @@ class ProtobufCodec(ThriftCodec):
     _DECODE = "kx_pb_decode_batch"
     _HOST = "kx_host_pb_decode_batch"
     _MESSAGES = "kx_pb_decode_messages"
+    _FRAMES = "kx_pb_decode_frames"
     _ENCODE = "kx_pb_encode_batch"
     _SIZE = "kx_pb_encoded_size_batch"
     _WHAT = "protobuf unmarshal"
@@ -389,3 +415,26 @@ def read_pb_meta(data: bytes):
         raise ProtocolError(rc, "pb read meta")
     off = C.cast(name, C.c_void_p).value - C.addressof(arr)
     return bytes(data[off:off + nl.value]).decode(), t.value, s.value, u.value
+
+
+def frame_scan(buf, n: int, max_payload: int = 0, device: int = 0, stream=None):
+    """kx_frame_scan: the framing sniff alone over a device buffer of n frames. Returns (frame offsets
+    int64[n+1], payload starts int64[n], payload ends int64[n], kinds uint8[n], status tensor)."""
+    import torch
+    dev = torch.device("cuda", device)
+    s = _stream(stream)
+    key = (device, int(s.cuda_stream))
+    ctx = _SCAN_CTX.get(key)
+    if ctx is None:
+        ctx = _SCAN_CTX[key] = Context(device)
+    fo = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    ps = torch.zeros(max(1, n), dtype=torch.int64, device=dev)
+    pe = torch.zeros(max(1, n), dtype=torch.int64, device=dev)
+    kinds = torch.zeros(max(1, n), dtype=torch.uint8, device=dev)
+    st = status_tensor(dev)
+    check(lib().kx_frame_scan(ctx.handle, _ptr(buf), buf.numel(), n, max_payload, _ptr(fo), _ptr(ps), _ptr(pe),
+                              _ptr(kinds), _ptr(st), int(s.cuda_stream)), "kx_frame_scan")
+    return fo, ps[:n], pe[:n], kinds[:n], st
+
+
+_SCAN_CTX = {}

@@ -156,6 +156,7 @@ const char* kx_strerror(int code) {
     case KX_ERR_DEPTH_LIMIT: return "depth limit exceeded";
     case KX_ERR_EOF: return "unexpected EOF";
     case KX_ERR_APPLICATION_EXCEPTION: return "application exception message";
+    case KX_ERR_UNKNOWN_PROTOCOL: return "unknown protocol (framing sniff)";
     case KX_ERR_INVALID_ARG: return "invalid argument";
     case KX_ERR_HIP: return "HIP runtime error";
     case KX_ERR_NO_DEVICE: return "no device";
@@ -228,6 +229,7 @@ void kx_ctx_destroy(kx_ctx* c) {
   if (c->ws) (void)hipFree(c->ws);
   if (c->ews) (void)hipFree(c->ews);
   if (c->mws) (void)hipFree(c->mws);
+  if (c->fws) (void)hipFree(c->fws);
   if (c->pin) (void)hipHostFree(c->pin);
   if (c->dstage) (void)hipFree(c->dstage);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
@@ -367,10 +369,13 @@ int kx_pb_decode_batch(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_
 
 // N framed messages: headers on the device (kx_message.hip), then the record bodies through the
 // known-offsets decode with explicit ends, then the per-message codes merged (header code first)
+// (framed payloads: message i = in[offsets[i] .. ends[i]), rep = the n + 1 frame offsets reported in
+// the status, pre = the framing scan's status)
 static int decode_messages(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len,
                            const uint64_t* offsets, uint64_t n, int32_t body_field, bool pb,
                            const kx_column* msg_cols, const kx_columns* out, uint8_t* record_status,
-                           kx_status* status, void* stream) {
+                           kx_status* status, void* stream, const uint64_t* ends = nullptr,
+                           const uint64_t* rep = nullptr, const kx_status* pre = nullptr) {
   if (!c || !s || !status || !offsets || (!in && in_len)) return KX_ERR_INVALID_ARG;
   int rc = set_device(c);
   if (rc) return rc;
@@ -401,7 +406,7 @@ static int decode_messages(kx_ctx* c, const kx_schema* s, const uint8_t* in, uin
   uint64_t *rs = nullptr, *re = nullptr;
   uint8_t *hrc = nullptr, *brc = nullptr;
   if ((rc = kx_launch_message_headers(in, in_len, offsets, n, body_field, pb, mo, c->mws, &rs, &re, &hrc, &brc,
-                                      st)))
+                                      st, ends, pre)))
     return rc;
   KxProgram* dp = nullptr;
   if ((rc = prog_on_device(const_cast<kx_schema*>(s), c->device, &dp))) return rc;
@@ -411,7 +416,82 @@ static int decode_messages(kx_ctx* c, const kx_schema* s, const uint8_t* in, uin
   if ((rc = kx_launch_decode(dp, s->prog, in, in_len, rs, n, lc, brc, status, c->ws, c->ws_size, epoch, st, pb,
                              re, nullptr, &c->pipe)))
     return rc;
-  return kx_launch_message_merge(offsets, n, hrc, brc, record_status, status, c->mws, st);
+  return kx_launch_message_merge(rep ? rep : offsets, n, hrc, brc, record_status, status, c->mws, st, pre);
+}
+
+static int ensure_fws(kx_ctx* c, size_t bytes, hipStream_t stream) {
+  if (c->fws_size >= bytes) return KX_OK;
+  if (c->fws) {
+    KX_HIP_CHECK(hipStreamSynchronize(stream));
+    KX_HIP_CHECK(hipFree(c->fws));
+    c->fws = nullptr;
+    c->fws_size = 0;
+  }
+  size_t sz = bytes < (1u << 20) ? (1u << 20) : bytes + bytes / 4;
+  KX_HIP_CHECK(hipMalloc(&c->fws, sz));
+  c->fws_size = sz;
+  return KX_OK;
+}
+
+int kx_frame_scan(kx_ctx* c, const uint8_t* in, uint64_t in_len, uint64_t n, uint64_t max_payload,
+                  uint64_t* frame_offsets, uint64_t* payload_start, uint64_t* payload_end, uint8_t* kinds,
+                  kx_status* status, void* stream) {
+  if (!c || !status || !frame_offsets || (n && (!payload_start || !payload_end)) || (!in && in_len))
+    return KX_ERR_INVALID_ARG;
+  int rc = set_device(c);
+  if (rc) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  if (n == 0) {
+    KX_HIP_CHECK(hipMemsetAsync(status, 0, sizeof(kx_status), st));
+    KX_HIP_CHECK(hipMemsetAsync(frame_offsets, 0, 8, st));
+    return KX_OK;
+  }
+  uint64_t epoch = 0;
+  if ((rc = ensure_ws(c, kx_skip_ws_bytes(in_len), st, &epoch))) return rc;
+  return kx_launch_frames(in, in_len, n, max_payload, frame_offsets, payload_start, payload_end, kinds, status, c->ws,
+                          c->ws_size, epoch, st);
+}
+
+// a socket buffer of n frames -> frame scan -> message headers -> record bodies
+static int decode_frames(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len, uint64_t n,
+                         int32_t body_field, bool pb, uint64_t max_payload, uint64_t* frame_offsets, uint8_t* kinds,
+                         const kx_column* msg_cols, const kx_columns* out, uint8_t* record_status, kx_status* status,
+                         void* stream) {
+  if (!c || !s || !status || (!in && in_len)) return KX_ERR_INVALID_ARG;
+  int rc = set_device(c);
+  if (rc) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  if (n == 0) {
+    if (frame_offsets) KX_HIP_CHECK(hipMemsetAsync(frame_offsets, 0, 8, st));
+    uint64_t z = 0;
+    return decode_messages(c, s, in, in_len, &z, 0, body_field, pb, msg_cols, out, record_status, status, stream);
+  }
+  // scratch: [scan status 256 B][frame offsets n + 1][payload starts n + 1][payload ends n]
+  const size_t fo_at = 256, ps_at = fo_at + (n + 1) * 8, pe_at = ps_at + (n + 1) * 8;
+  if ((rc = ensure_fws(c, pe_at + n * 8, st))) return rc;
+  char* f = (char*)c->fws;
+  kx_status* pre = (kx_status*)f;
+  uint64_t* fo = frame_offsets ? frame_offsets : (uint64_t*)(f + fo_at);
+  uint64_t* ps = (uint64_t*)(f + ps_at);
+  uint64_t* pe = (uint64_t*)(f + pe_at);
+  if ((rc = kx_frame_scan(c, in, in_len, n, max_payload, fo, ps, pe, kinds, pre, stream))) return rc;
+  return decode_messages(c, s, in, in_len, ps, n, body_field, pb, msg_cols, out, record_status, status, stream, pe,
+                         fo, pre);
+}
+
+int kx_thrift_decode_frames(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len, uint64_t n,
+                            int32_t body_field, uint64_t max_payload, uint64_t* frame_offsets, uint8_t* kinds,
+                            const kx_column* msg_cols, const kx_columns* out, uint8_t* record_status,
+                            kx_status* status, void* stream) {
+  return decode_frames(c, s, in, in_len, n, body_field, false, max_payload, frame_offsets, kinds, msg_cols, out,
+                       record_status, status, stream);
+}
+
+int kx_pb_decode_frames(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len, uint64_t n,
+                        uint64_t max_payload, uint64_t* frame_offsets, uint8_t* kinds, const kx_column* msg_cols,
+                        const kx_columns* out, uint8_t* record_status, kx_status* status, void* stream) {
+  return decode_frames(c, s, in, in_len, n, 1, true, max_payload, frame_offsets, kinds, msg_cols, out,
+                       record_status, status, stream);
 }
 
 int kx_thrift_decode_messages(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len,

@@ -61,7 +61,7 @@ enum { T_ENT = 0, T_EXIT, T_CNT, T_ERRC, T_ERRP, T_VAR, T_PCNT = T_VAR + KXP_NV_
 enum { G_ENT = 0, G_EXIT, G_CNT, G_ERRC, G_ERRP, G_VAR, G_BCNT = G_VAR + KXP_NV_MAX, G_BVAR,
        G_NF = G_BVAR + KXP_NV_MAX };
 
-enum Mode { M_THRIFT = 0, M_SKIP = 1, M_PB = 2 };
+enum Mode { M_THRIFT = 0, M_SKIP = 1, M_PB = 2, M_FRAME = 3 };  // M_FRAME: framing sniff
 
 // diagnostics (KX_DIAG & 64): shader-clock cycles per index-pass phase, summed over tiles (lane 0)
 __device__ unsigned long long g_phase[8];
@@ -76,7 +76,11 @@ struct DecParams {
   KxLaunchCols cols;
   uint8_t* rstat;
   kx_status* status;
-  uint64_t* skip_out;        // M_SKIP: record start offsets
+  uint64_t* skip_out;        // M_SKIP / M_FRAME: record (frame) start offsets
+  uint64_t* fr_ps;           // M_FRAME: payload start / end per frame, kind per frame
+  uint64_t* fr_pe;
+  uint8_t* fr_kind;
+  uint64_t fr_max;           // M_FRAME: payload size limit (0: none)
   uint64_t* tdesc;           // tile words
   uint64_t* gdesc;           // group words
   uint16_t* starts;          // concatenated mode: record starts per tile (slotcap slots each)
@@ -1205,6 +1209,132 @@ __device__ __forceinline__ Src load_window(KParams& dp, LDS uint32_t* win, uint6
              thrift ? P->canon_pres : 0ull};
 }
 
+// ---------------------------------------------------------------------------------------------
+// Framing sniff (M_FRAME): one socket-buffer frame at pos. defaultCodec.DecodeMeta + checkPayload
+// (default_codec.go:189-221, 328-427), Mesh header (header_codec.go:192-212), TTHeader meta + info
+// blocks (gopkg protocol/ttheader, un-vendored; same restatement as oracle kxo_frame_one).
+// kind = transport.Protocol (0 PurePayload, 2 TTHeader, 4 Framed, 6 TTHeaderFramed) | 0x10 Kitex-PB
+// | 0x20 Mesh. Lane-serial per frame: headers are short and rarely repeated within a wave.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t be16s(const Src& w, uint64_t p) { return __builtin_bswap32(ld4(w, p)) >> 16; }
+
+// readStrKVInfo (header_codec.go:115-138) over [b, b + len); *i advanced
+__device__ __forceinline__ int fr_kv_strings(const Src& w, uint64_t b, uint64_t len, uint64_t& i) {
+  if (i + 2 > len) return KX_ERR_UNKNOWN_PROTOCOL;
+  const uint32_t k = be16s(w, b + i);
+  i += 2;
+  for (uint32_t j = 0; j < 2 * k; j++) {
+    if (i + 2 > len) return KX_ERR_UNKNOWN_PROTOCOL;
+    const uint64_t l = be16s(w, b + i);
+    if (i + 2 + l > len) return KX_ERR_UNKNOWN_PROTOCOL;
+    i += 2 + l;
+  }
+  return KX_OK;
+}
+
+__device__ __forceinline__ int fr_tth_info(const Src& w, uint64_t b, uint64_t len) {
+  const uint32_t proto = ld1(w, b);
+  if (proto != 0 && proto != 3 && proto != 4) return KX_ERR_UNKNOWN_PROTOCOL;  // checkProtocolID
+  const uint64_t nt = ld1(w, b + 1);
+  if (len - 2 < nt) return KX_ERR_UNKNOWN_PROTOCOL;
+  uint64_t i = 2 + nt;
+  while (i < len) {
+    const uint32_t id = ld1(w, b + i++);
+    if (id == 0x00) continue;  // padding
+    int rc = KX_OK;
+    if (id == 0x01) {
+      rc = fr_kv_strings(w, b, len, i);
+    } else if (id == 0x10) {  // int KVs: u16 count, (u16 key, u16-length string)
+      if (i + 2 > len) return KX_ERR_UNKNOWN_PROTOCOL;
+      const uint32_t k = be16s(w, b + i);
+      i += 2;
+      for (uint32_t j = 0; j < k; j++) {
+        if (i + 4 > len) return KX_ERR_UNKNOWN_PROTOCOL;
+        const uint64_t l = be16s(w, b + i + 2);
+        if (i + 4 + l > len) return KX_ERR_UNKNOWN_PROTOCOL;
+        i += 4 + l;
+      }
+    } else if (id == 0x11) {  // ACL token
+      if (i + 2 > len) return KX_ERR_UNKNOWN_PROTOCOL;
+      const uint64_t l = be16s(w, b + i);
+      if (i + 2 + l > len) return KX_ERR_UNKNOWN_PROTOCOL;
+      i += 2 + l;
+    } else {
+      rc = KX_ERR_UNKNOWN_PROTOCOL;
+    }
+    if (rc) return rc;
+  }
+  return KX_OK;
+}
+
+__device__ __forceinline__ int frame_one(const Src& w, uint64_t pos, uint64_t lim, uint64_t maxp, uint64_t* end,
+                                         uint64_t& ps, uint64_t& pe, uint32_t& kind) {
+  if (pos > lim || lim - pos < 8) return KX_ERR_EOF;
+  const uint64_t len = lim - pos;
+  const uint32_t a = be32(w, pos), c = be32(w, pos + 4);
+  uint64_t p = 0, fend = 0, plen = 0;
+  bool tth = false, mesh = false;
+  if ((c & 0xffff0000u) == 0x10000000u) {  // IsTTHeader
+    tth = true;
+    if (len < 14) return KX_ERR_EOF;
+    const uint64_t hs = (uint64_t)be16s(w, pos + 12) * 4;
+    if (hs > 65536 || hs < 2) return KX_ERR_UNKNOWN_PROTOCOL;
+    if (14 + hs > len) return KX_ERR_EOF;
+    const int rc = fr_tth_info(w, pos + 14, hs);
+    if (rc) return rc;
+    fend = 4 + (uint64_t)a;
+    if (fend < 14 + hs) return KX_ERR_UNKNOWN_PROTOCOL;
+    p = 14 + hs;
+    plen = fend - p;
+  } else if ((a & 0xffff0000u) == 0xFFAF0000u) {  // isMeshHeader
+    mesh = true;
+    const uint64_t hl = a & 0xffffu;
+    if (4 + hl > len) return KX_ERR_EOF;
+    uint64_t i = 0;
+    const int rc = fr_kv_strings(w, pos + 4, hl, i);
+    if (rc) return rc;
+    p = 4 + hl;
+  }
+  const uint64_t avail = tth ? fend : len;
+  if (tth && fend > len) return KX_ERR_EOF;
+  if (p + 8 > avail) return KX_ERR_EOF;
+  const uint32_t x = be32(w, pos + p), y = be32(w, pos + p + 4);
+  uint32_t k;
+  if ((x & 0xffff0000u) == 0x80010000u) {  // isThriftBinary: TTHeader / PurePayload
+    k = tth ? 2u : 0u;
+    if (tth) {
+      ps = p; pe = fend;
+    } else {  // the message delimits itself: strict MessageBegin + the struct after it
+      const int32_t nl = (int32_t)be32(w, pos + p + 4);
+      if (nl < 0) return KX_ERR_NEGATIVE_SIZE;
+      if (len - p < 12 + (uint64_t)nl) return KX_ERR_EOF;
+      uint64_t q = pos + p + 12 + (uint64_t)nl;
+      const int rc = dskip_body(w, q, lim, KX_T_STRUCT, 64);
+      if (rc) return rc;
+      ps = p; pe = q - pos;
+      fend = pe;
+      plen = 0;  // unknown when checkPayloadSize runs
+    }
+  } else if ((y & 0xffff0000u) == 0x80010000u || (y & 0xffff0000u) == 0x90010000u) {  // Framed
+    k = (tth ? 6u : 4u) | ((y & 0xffff0000u) == 0x90010000u ? 0x10u : 0u);
+    plen = x;
+    if (tth) {
+      if (p + 4 + plen > fend) return KX_ERR_EOF;
+    } else {
+      fend = p + 4 + plen;
+      if (fend > len) return KX_ERR_EOF;
+    }
+    ps = p + 4; pe = p + 4 + plen;
+  } else {
+    return KX_ERR_UNKNOWN_PROTOCOL;  // invalid payload (default_codec.go:411-416)
+  }
+  if (maxp && plen > maxp) return KX_ERR_INVALID_DATA;  // checkPayloadSize
+  *end = pos + fend;
+  ps += pos; pe += pos;
+  kind = k | (mesh ? 0x20u : 0u);
+  return KX_OK;
+}
+
 // One record: FastRead (emit) or its length / var extents only (measure).
 template <int NV, int MODE>
 __device__ __forceinline__ int parse_record(KParams& dp, const Src& w, uint64_t pos, uint64_t lim, uint64_t r,
@@ -1241,6 +1371,17 @@ __device__ __forceinline__ int parse_record(KParams& dp, const Src& w, uint64_t 
     if (dp.prog->npbsteps && pb_canon<NV>(w, dp.prog, dp.cols, b, e, r, emit, utf8, vs, pres)) return KX_OK;
     return pb_body<NV>(w, dp.prog, dp.cols, b, e, r, emit, vs, pres, utf8);
   }
+  if (MODE == M_FRAME) {
+    uint64_t ps, pe;
+    uint32_t kind;
+    const int rc = frame_one(w, pos, lim, dp.fr_max, end, ps, pe, kind);
+    if (emit && !rc) {
+      dp.fr_ps[r] = ps;
+      dp.fr_pe[r] = pe;
+      if (dp.fr_kind) dp.fr_kind[r] = (uint8_t)kind;
+    }
+    return rc;
+  }
   uint64_t p2 = pos;
   const int rc = dskip_body(w, p2, lim, KX_T_STRUCT, 64);
   *end = p2;
@@ -1274,6 +1415,32 @@ struct Cand {
   bool strict;      // several hits in the segment: a guess must parse as a canonical record
 };
 
+// M_FRAME candidates: positions that start a frame of the batch's first frame's class (batches from
+// one connection are homogeneous; frames of another class are still reached by the chain walk)
+__device__ __forceinline__ uint64_t frame_scan_segment(KParams& dp, const Src& w, uint64_t lo, uint64_t hi) {
+  if (dp.in_len < 8) return lo < hi && lo == 0 ? 0 : X_NONE;
+  const GLB uint8_t* g = (const GLB uint8_t*)dp.in;
+  const uint32_t a0 = __builtin_amdgcn_readfirstlane(((uint32_t)g[0] << 24) | ((uint32_t)g[1] << 16) |
+                                                     ((uint32_t)g[2] << 8) | g[3]);
+  const uint32_t c0 = __builtin_amdgcn_readfirstlane(((uint32_t)g[4] << 24) | ((uint32_t)g[5] << 16) |
+                                                     ((uint32_t)g[6] << 8) | g[7]);
+  // class: 0 length-prefixed (TTHeader / Framed: magic in bytes 4-5), 1 Mesh, 2 PurePayload
+  const uint32_t cls = (c0 >> 16) == 0x1000u ? 0u : (a0 >> 16) == 0xFFAFu ? 1u : (a0 >> 16) == 0x8001u ? 2u : 0u;
+  const uint32_t m0 = cls == 0 ? (c0 >> 16) : (a0 >> 16);
+  const uint64_t plim = kmin64(hi, dp.in_len - 7);
+  for (uint64_t p = lo; p < plim; p++) {
+    const uint32_t a = be32(w, p);
+    if (cls == 0) {
+      const uint32_t c = be32(w, p + 4);
+      if ((c >> 16) != m0 || (uint64_t)a + 4 > dp.in_len - p) continue;
+    } else if ((a >> 16) != m0) {
+      continue;
+    }
+    return p;
+  }
+  return X_NONE;
+}
+
 template <int NV, int MODE>
 __device__ __forceinline__ Cand lane_candidate(KParams& dp, const Src& w, uint64_t seg_lo, uint64_t seg_hi, int lane) {
   Cand cd;
@@ -1281,6 +1448,10 @@ __device__ __forceinline__ Cand lane_candidate(KParams& dp, const Src& w, uint64
   if (seg_lo >= seg_hi) return cd;
   if (MODE == M_PB) {
     cd.ent = pb_scan_segment(w, seg_lo, seg_hi, dp.in_len, lane);
+    return cd;
+  }
+  if (MODE == M_FRAME) {
+    cd.ent = frame_scan_segment(dp, w, seg_lo, seg_hi);
     return cd;
   }
   const KAS KxProgram* P = dp.prog;
@@ -1830,7 +2001,7 @@ __global__ void __launch_bounds__(CT) chain_kernel(DecParams dp_) {
           if (v < (int)dp.prog->nvar) st->var_total[v] = tot[v];
         }
         close_slots<NV>(dp.prog, dp.cols, dp.overflow, rec, tot);
-        if (MODE == M_SKIP) dp.skip_out[rec] = errp;
+        if (MODE == M_SKIP || MODE == M_FRAME) dp.skip_out[rec] = errp;
         s_nstop = rec;
       }
       s_err = 1;
@@ -1861,7 +2032,7 @@ __global__ void __launch_bounds__(CT) chain_kernel(DecParams dp_) {
         if (v < (int)dp.prog->nvar) st->var_total[v] = s_var[v];
       }
       close_slots<NV>(dp.prog, dp.cols, dp.overflow, tot, vt);
-      if (MODE == M_SKIP) dp.skip_out[tot] = dp.in_len;
+      if (MODE == M_SKIP || MODE == M_FRAME) dp.skip_out[tot] = dp.in_len;
       s_nstop = tot;
     }
     // emit of this chunk bounds itself by nstop: final once the chain has ended, else unbounded
@@ -1996,10 +2167,10 @@ __global__ void __launch_bounds__(NT) emit_kernel(DecParams dp_) {
 #pragma unroll
         for (int v = 0; v < NV; v++) vs.len[v] = 0;
         pres = 0;
-        if (MODE != M_SKIP) emit_defaults(P, dp.cols, r);
+        if (MODE != M_SKIP && MODE != M_FRAME) emit_defaults(P, dp.cols, r);
       }
-      if (MODE == M_SKIP) dp.skip_out[r] = pos;
-      if (MODE != M_SKIP && dp.cols.presence) dp.cols.presence[r] = pres;
+      if (MODE == M_SKIP || MODE == M_FRAME) dp.skip_out[r] = pos;
+      if (MODE != M_SKIP && MODE != M_FRAME && dp.cols.presence) dp.cols.presence[r] = pres;
       if (known) {
         if (rc) atomicMin(dp.errkey, (unsigned long long)((r << 8) | (uint64_t)(rc & 0xff)));
         if (dp.rstat) dp.rstat[r] = (uint8_t)rc;
@@ -2052,7 +2223,7 @@ __global__ void __launch_bounds__(NT) emit_kernel(DecParams dp_) {
       kx_status* st = dp.status;
       st->n_records = dp.n;
       st->consumed = known ? rec_end(dp, dp.n - 1) : end;
-      if (MODE == M_SKIP) dp.skip_out[dp.n] = end;
+      if (MODE == M_SKIP || MODE == M_FRAME) dp.skip_out[dp.n] = end;
     }
   }
 }
@@ -2236,9 +2407,9 @@ KX_DEF(0, M_THRIFT) KX_DEF(1, M_THRIFT)
 KX_EXT(0, M_THRIFT) KX_EXT(1, M_THRIFT)
 #endif
 #if KX_OWNS(1)
-KX_DEF(2, M_THRIFT) KX_DEF(0, M_SKIP)
+KX_DEF(2, M_THRIFT) KX_DEF(0, M_SKIP) KX_DEF(0, M_FRAME)
 #else
-KX_EXT(2, M_THRIFT) KX_EXT(0, M_SKIP)
+KX_EXT(2, M_THRIFT) KX_EXT(0, M_SKIP) KX_EXT(0, M_FRAME)
 #endif
 #if KX_OWNS(2)
 KX_DEF(4, M_THRIFT)
@@ -2317,5 +2488,19 @@ int kx_launch_skip(const uint8_t* in, uint64_t in_len, uint64_t n, uint64_t* off
   const WsLayout L = ws_layout(1, in_len, nullptr, n);
   if (ws_size < L.total) return KX_ERR_INVALID_ARG;
   return kx_dec_launch<0, M_SKIP>(&dp, &L, ws, stream, nullptr);
+}
+
+int kx_launch_frames(const uint8_t* in, uint64_t in_len, uint64_t n, uint64_t max_payload, uint64_t* frame_offsets,
+                     uint64_t* pay_start, uint64_t* pay_end, uint8_t* kinds, kx_status* status, void* ws,
+                     size_t ws_size, uint64_t epoch, hipStream_t stream) {
+  DecParams dp{};
+  fill_diag_flags(dp);
+  dp.in = in; dp.in_len = in_len; dp.offsets = nullptr; dp.n = n; dp.prog = nullptr;
+  dp.status = status; dp.skip_out = frame_offsets; dp.epoch = epoch;
+  dp.fr_ps = pay_start; dp.fr_pe = pay_end; dp.fr_kind = kinds; dp.fr_max = max_payload;
+  dp.krec = 64;
+  const WsLayout L = ws_layout(1, in_len, nullptr, n);
+  if (ws_size < L.total) return KX_ERR_INVALID_ARG;
+  return kx_dec_launch<0, M_FRAME>(&dp, &L, ws, stream, nullptr);
 }
 #endif  // KX_DEC_PART <= 0

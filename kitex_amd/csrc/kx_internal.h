@@ -51,6 +51,9 @@ struct kx_ctx {
   // grow-only message-header workspace (kx_*_decode_messages)
   void* mws = nullptr;
   size_t mws_size = 0;
+  // grow-only framing-scan scratch (kx_*_decode_frames): frame offsets, payload extents, scan status
+  void* fws = nullptr;
+  size_t fws_size = 0;
   // grow-only encode scratch (per-block sizes)
   void* ews = nullptr;
   size_t ews_size = 0;
@@ -90,6 +93,9 @@ size_t kx_decode_ws_bytes(const KxProgram& hprog, uint64_t in_len, const uint64_
 int kx_launch_skip(const uint8_t* in, uint64_t in_len, uint64_t n, uint64_t* offsets_out,
                    kx_status* status, void* ws, size_t ws_size, uint64_t epoch, hipStream_t stream);
 size_t kx_skip_ws_bytes(uint64_t in_len);
+int kx_launch_frames(const uint8_t* in, uint64_t in_len, uint64_t n, uint64_t max_payload, uint64_t* frame_offsets,
+                     uint64_t* pay_start, uint64_t* pay_end, uint8_t* kinds, kx_status* status, void* ws,
+                     size_t ws_size, uint64_t epoch, hipStream_t stream);
 
 int kx_launch_encode(const KxProgram* dprog, const KxProgram& hprog, const KxLaunchCols& cols,
                      uint64_t n, uint8_t* out, uint64_t out_cap, uint64_t* sizes_out,
@@ -110,9 +116,11 @@ size_t kx_message_ws_bytes(uint64_t n);
 int kx_launch_message_headers(const uint8_t* in, uint64_t in_len, const uint64_t* offsets, uint64_t n,
                               int32_t body_field, bool pb, const KxMsgOut& mo, void* mws,
                               uint64_t** req_start, uint64_t** req_end,
-                              uint8_t** hdr_rc, uint8_t** body_rc, hipStream_t stream);
+                              uint8_t** hdr_rc, uint8_t** body_rc, hipStream_t stream,
+                              const uint64_t* ends = nullptr, const kx_status* pre = nullptr);
 int kx_launch_message_merge(const uint64_t* offsets, uint64_t n, const uint8_t* hdr_rc, const uint8_t* body_rc,
-                            uint8_t* record_status, kx_status* status, void* mws, hipStream_t stream);
+                            uint8_t* record_status, kx_status* status, void* mws, hipStream_t stream,
+                            const kx_status* pre = nullptr);
 
 #define KX_HIP_CHECK(x)                       \
   do {                                        \

@@ -132,7 +132,9 @@ __device__ __forceinline__ int skip_value(const uint8_t* in, uint64_t& pos, uint
 struct MsgParams {
   const uint8_t* in;
   uint64_t in_len;
-  const uint64_t* offsets;   // n + 1 message boundaries
+  const uint64_t* offsets;   // n + 1 message boundaries (with ends: n message starts)
+  const uint64_t* ends;      // message i ends at ends[i] (framed payloads), else offsets[i + 1]
+  const kx_status* pre;      // framing-scan status: messages from its failing frame on are not read
   uint64_t n;
   int32_t body_field;        // 1: Args{1: req}, 0: Result{0: success}
   int pb;                    // Kitex-Protobuf meta header (magic 0x9001, 16-bit type), body = the rest
@@ -153,12 +155,15 @@ __global__ void __launch_bounds__(MT) header_kernel(MsgParams mp) {
     return;
   }
   const uint8_t* in = mp.in;
-  const uint64_t p = mp.offsets[i], e = mp.offsets[i + 1];
+  const bool cut = mp.pre && mp.pre->code && i >= (uint64_t)mp.pre->record;
+  const uint64_t p = cut ? 0 : mp.offsets[i], e = cut ? 0 : mp.ends ? mp.ends[i] : mp.offsets[i + 1];
   int rc = KX_OK;
   uint32_t type = 0;
   int32_t seqid = 0, nl = 0;
   uint64_t rs = p, re = p;
-  if (p > e || e > mp.in_len) {
+  if (cut) {
+    rc = mp.pre->code;  // the frame could not be delimited: neither it nor any later one is decoded
+  } else if (p > e || e > mp.in_len) {
     rc = KX_ERR_INVALID_ARG;
   } else if (e - p < 4) {
     rc = KX_ERR_EOF;
@@ -267,9 +272,19 @@ __global__ void __launch_bounds__(MT) merge_kernel(const uint8_t* hdr_rc, const 
 // the call's status: the first failing message (header or body) wins; else the body decode's own
 // code (an arena overflow), else a name-arena overflow
 __global__ void final_kernel(kx_status* st, const uint64_t* offsets, uint64_t n, unsigned long long* errkey,
-                             uint32_t* overflow) {
+                             uint32_t* overflow, const kx_status* pre) {
   if (threadIdx.x != 0) return;
   const unsigned long long k = *errkey;
+  if (pre && pre->code) {  // a framing error ends the batch at its frame
+    st->code = pre->code;
+    st->record = pre->record;
+    st->offset = pre->offset;
+    st->n_records = n;
+    st->consumed = pre->offset;
+    *errkey = ~0ull;
+    *overflow = 0;
+    return;
+  }
   if (k != ~0ull) {
     st->code = (int32_t)(k & 0xff);
     st->record = k >> 8;
@@ -311,11 +326,13 @@ size_t kx_message_ws_bytes(uint64_t n) { return msg_ws(n).total; }
 
 int kx_launch_message_headers(const uint8_t* in, uint64_t in_len, const uint64_t* offsets, uint64_t n,
                               int32_t body_field, bool pb, const KxMsgOut& mo, void* mws, uint64_t** req_start,
-                              uint64_t** req_end, uint8_t** hdr_rc, uint8_t** body_rc, hipStream_t stream) {
+                              uint64_t** req_end, uint8_t** hdr_rc, uint8_t** body_rc, hipStream_t stream,
+                              const uint64_t* ends, const kx_status* pre) {
   const MsgWs L = msg_ws(n);
   char* b = (char*)mws;
   MsgParams mp{};
   mp.in = in; mp.in_len = in_len; mp.offsets = offsets; mp.n = n; mp.body_field = body_field; mp.mo = mo;
+  mp.ends = ends; mp.pre = pre;
   mp.pb = pb;
   mp.req_start = (uint64_t*)(b + L.req_start);
   mp.req_end = (uint64_t*)(b + L.req_end);
@@ -339,13 +356,14 @@ int kx_launch_message_headers(const uint8_t* in, uint64_t in_len, const uint64_t
 }
 
 int kx_launch_message_merge(const uint64_t* offsets, uint64_t n, const uint8_t* hdr_rc, const uint8_t* body_rc,
-                            uint8_t* record_status, kx_status* status, void* mws, hipStream_t stream) {
+                            uint8_t* record_status, kx_status* status, void* mws, hipStream_t stream,
+                            const kx_status* pre) {
   unsigned long long* errkey = (unsigned long long*)mws;
   uint32_t* overflow = (uint32_t*)((char*)mws + 8);
   const unsigned grid = (unsigned)((n + MT - 1) / MT);
   hipLaunchKernelGGL(merge_kernel, dim3(grid), dim3(MT), 0, stream, hdr_rc, body_rc, record_status, n, errkey);
   KX_HIP_CHECK(hipGetLastError());
-  hipLaunchKernelGGL(final_kernel, dim3(1), dim3(64), 0, stream, status, offsets, n, errkey, overflow);
+  hipLaunchKernelGGL(final_kernel, dim3(1), dim3(64), 0, stream, status, offsets, n, errkey, overflow, pre);
   KX_HIP_CHECK(hipGetLastError());
   return KX_OK;
 }

@@ -195,6 +195,155 @@ int kxo_skip_batch(const uint8_t* b, size_t len, uint64_t n, uint64_t* offsets_o
 }
 
 /* ------------------------------------------------------------------------------------------------
+ * Framing sniff over a socket buffer of n messages: defaultCodec.DecodeMeta + checkPayload
+ * (pkg/remote/codec/default_codec.go:189-221, 328-427), the Mesh header (header_codec.go:192-212,
+ * readStrKVInfo :115-138) and the TTHeader meta / info blocks. TTHeader decoding itself lives in the
+ * un-vendored github.com/cloudwego/gopkg v0.2.0 (protocol/ttheader); restated from its published
+ * layout: u32 LENGTH (bytes after this field), u16 magic 0x1000, u16 flags, u32 seqid, u16 header
+ * size in 4-byte words (2..65536 bytes), then protocol id (0 binary, 3 compact v2, 4 Kitex-PB),
+ * transform count + ids, and info blocks (0x00 padding, 0x01 string KVs, 0x10 int KVs, 0x11 ACL
+ * token). Parity unpinned beyond the reference's sniff-matrix tests (default_codec_test.go:58-199).
+ *
+ * Per frame: its extent, its payload [start, end) (what the payload codec sees: MessageBegin or the
+ * Kitex-PB meta header first) and kind = transport.Protocol (0 PurePayload, 2 TTHeader, 4 Framed,
+ * 6 TTHeaderFramed; transport/keys.go:24-53) | 0x10 Kitex-Protobuf | 0x20 Mesh header.
+ * A payload longer than max_payload (> 0) is INVALID_DATA (checkPayloadSize, :429-434; a PurePayload
+ * length is unknown at that point and never checked). A frame cut short is EOF.
+ * ---------------------------------------------------------------------------------------------- */
+#define KXO_MASK 0xffff0000u
+static int kv_strings(const uint8_t* b, uint64_t len, uint64_t* i) { /* readStrKVInfo */
+  if (*i + 2 > len) return KX_ERR_UNKNOWN_PROTOCOL;
+  uint32_t k = be16(b + *i);
+  *i += 2;
+  for (uint32_t j = 0; j < 2 * k; j++) {  /* key, value: ReadString2BLen */
+    if (*i + 2 > len) return KX_ERR_UNKNOWN_PROTOCOL;
+    uint64_t l = be16(b + *i);
+    if (*i + 2 + l > len) return KX_ERR_UNKNOWN_PROTOCOL;
+    *i += 2 + l;
+  }
+  return KX_OK;
+}
+
+static int tth_info(const uint8_t* b, uint64_t len) {
+  uint8_t proto = b[0];
+  if (proto != 0 && proto != 3 && proto != 4) return KX_ERR_UNKNOWN_PROTOCOL;  /* checkProtocolID */
+  uint64_t nt = b[1], i = 2;
+  if (len - 2 < nt) return KX_ERR_UNKNOWN_PROTOCOL;  /* transform ids */
+  i += nt;
+  while (i < len) {
+    uint8_t id = b[i++];
+    if (id == 0x00) continue;  /* padding */
+    int rc;
+    if (id == 0x01) {
+      rc = kv_strings(b, len, &i);
+    } else if (id == 0x10) {  /* int KVs: u16 count, (u16 key, u16-length string) */
+      if (i + 2 > len) return KX_ERR_UNKNOWN_PROTOCOL;
+      uint32_t k = be16(b + i);
+      i += 2;
+      rc = KX_OK;
+      for (uint32_t j = 0; j < k && !rc; j++) {
+        if (i + 4 > len) { rc = KX_ERR_UNKNOWN_PROTOCOL; break; }
+        uint64_t l = be16(b + i + 2);
+        if (i + 4 + l > len) rc = KX_ERR_UNKNOWN_PROTOCOL;
+        else i += 4 + l;
+      }
+    } else if (id == 0x11) {  /* ACL token: u16-length string */
+      if (i + 2 > len) return KX_ERR_UNKNOWN_PROTOCOL;
+      uint64_t l = be16(b + i);
+      rc = i + 2 + l > len ? KX_ERR_UNKNOWN_PROTOCOL : KX_OK;
+      i += 2 + l;
+    } else {
+      rc = KX_ERR_UNKNOWN_PROTOCOL;  /* invalid info id */
+    }
+    if (rc) return rc;
+  }
+  return KX_OK;
+}
+
+int kxo_frame_one(const uint8_t* b, uint64_t len, uint64_t max_payload, uint64_t* flen, uint64_t* ps,
+                  uint64_t* pe, uint8_t* kind) {
+  if (len < 8) return KX_ERR_EOF;  /* in.Peek(2 * Size32), :191 */
+  uint32_t a = be32(b), c = be32(b + 4);
+  uint64_t p = 0, fend = 0, plen = 0;
+  int tth = 0, mesh = 0;
+  if ((c & KXO_MASK) == 0x10000000u) {  /* IsTTHeader, :328-330 */
+    tth = 1;
+    if (len < 14) return KX_ERR_EOF;
+    uint64_t hs = (uint64_t)be16(b + 12) * 4;
+    if (hs > 65536 || hs < 2) return KX_ERR_UNKNOWN_PROTOCOL;
+    if (14 + hs > len) return KX_ERR_EOF;
+    int rc = tth_info(b + 14, hs);
+    if (rc) return rc;
+    fend = 4 + (uint64_t)a;
+    if (fend < 14 + hs) return KX_ERR_UNKNOWN_PROTOCOL;  /* negative payload length */
+    p = 14 + hs;
+    plen = fend - p;  /* PayloadLen = LENGTH - header size + 4 - 14 */
+  } else if ((a & KXO_MASK) == 0xFFAF0000u) {  /* isMeshHeader, :339-341 */
+    mesh = 1;
+    uint64_t hl = a & 0xffffu;
+    if (4 + hl > len) return KX_ERR_EOF;
+    uint64_t i = 0;
+    int rc = kv_strings(b + 4, hl, &i);
+    if (rc) return rc;
+    p = 4 + hl;
+  }
+  const uint64_t avail = tth ? fend : len;
+  if (tth && fend > len) return KX_ERR_EOF;
+  if (p + 8 > avail) return KX_ERR_EOF;  /* Peek(8) of the payload, :202-204 / :216-218 */
+  uint32_t x = be32(b + p), y = be32(b + p + 4);
+  uint8_t k;
+  if ((x & KXO_MASK) == 0x80010000u) {  /* isThriftBinary: TTHeader / PurePayload, :380-386 */
+    k = tth ? 2 : 0;
+    if (tth) {
+      *ps = p; *pe = fend;
+    } else {  /* the message delimits itself: MessageBegin + the struct after it */
+      uint32_t no, nl; int32_t ty, sq; size_t u = 0, u2 = 0;
+      int rc = kxo_read_message_begin(b + p, len - p, &no, &nl, &ty, &sq, &u);
+      if (rc) return rc;
+      rc = kxo_skip(b + p + u, len - p - u, KX_T_STRUCT, 64, &u2);
+      if (rc) return rc;
+      *ps = p; *pe = p + u + u2;
+      fend = *pe;
+      plen = 0;  /* unknown when checkPayloadSize runs */
+    }
+  } else if ((y & KXO_MASK) == 0x80010000u || (y & KXO_MASK) == 0x90010000u) {  /* Framed, :387-410 */
+    k = (uint8_t)((tth ? 6 : 4) | ((y & KXO_MASK) == 0x90010000u ? 0x10 : 0));
+    plen = x;
+    if (tth) {
+      if (p + 4 + plen > fend) return KX_ERR_EOF;
+    } else {
+      fend = p + 4 + plen;
+      if (fend > len) return KX_ERR_EOF;
+    }
+    *ps = p + 4; *pe = p + 4 + plen;
+  } else {
+    return KX_ERR_UNKNOWN_PROTOCOL;  /* invalid payload, :411-416 */
+  }
+  if (max_payload && plen > max_payload) return KX_ERR_INVALID_DATA;  /* checkPayloadSize */
+  *flen = fend;
+  *kind = (uint8_t)(k | (mesh ? 0x20 : 0));
+  return KX_OK;
+}
+
+/* n frames back to back from in[0]; stops at the first failing frame (n_done = its index) */
+int kxo_frame_scan(const uint8_t* in, uint64_t in_len, uint64_t n, uint64_t max_payload, uint64_t* frame_offsets,
+                   uint64_t* pay_start, uint64_t* pay_end, uint8_t* kinds, uint64_t* n_done) {
+  uint64_t pos = 0;
+  for (uint64_t i = 0; i < n; i++) {
+    frame_offsets[i] = pos;
+    uint64_t fl = 0, ps = 0, pe = 0;
+    uint8_t k = 0;
+    int rc = kxo_frame_one(in + pos, in_len - pos, max_payload, &fl, &ps, &pe, &k);
+    if (rc) { *n_done = i; return rc; }
+    pay_start[i] = pos + ps; pay_end[i] = pos + pe; kinds[i] = k;
+    pos += fl;
+  }
+  frame_offsets[n] = pos;
+  *n_done = n;
+  return KX_OK;
+}
+
+/* ------------------------------------------------------------------------------------------------
  * Schema flattening: depth-first over the IDL, struct fields inlined, a presence bit for every
  * optional / struct / container field (Go represents those as nil-able; struct_tpl.go:405-450).
  * ---------------------------------------------------------------------------------------------- */

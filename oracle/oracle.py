@@ -63,6 +63,8 @@ def lib():
             getattr(L, n).restype = sz
         L.kxo_skip.argtypes = [vp, sz, C.c_uint8, C.c_int, C.POINTER(sz)]
         L.kxo_skip_batch.argtypes = [vp, sz, C.c_uint64, vp, C.POINTER(C.c_uint64)]
+        L.kxo_frame_scan.argtypes = [vp, C.c_uint64, C.c_uint64, C.c_uint64, vp, vp, vp, vp,
+                                     C.POINTER(C.c_uint64)]
         L.kxo_flatten.argtypes = [sdp, C.c_uint32, C.POINTER(A.ColumnInfo), C.POINTER(C.c_uint32),
                                   C.POINTER(C.c_uint32)]
         dec = [sdp, C.c_uint32, vp, C.c_uint64, vp, C.c_uint64, C.POINTER(A.Columns), vp,
@@ -122,6 +124,19 @@ def skip_batch(data: np.ndarray, n: int):
     done = C.c_uint64()
     rc = lib().kxo_skip_batch(data.ctypes.data, data.size, n, offs.ctypes.data, C.byref(done))
     return rc, offs, done.value
+
+
+def frame_scan(data: np.ndarray, n: int, max_payload: int = 0):
+    """framing sniff over n messages (kxo_frame_scan): rc, frame offsets[n+1], payload starts[n],
+    payload ends[n], kinds[n], frames done"""
+    fo = np.zeros(n + 1, dtype=np.uint64)
+    ps = np.zeros(max(1, n), dtype=np.uint64)
+    pe = np.zeros(max(1, n), dtype=np.uint64)
+    kd = np.zeros(max(1, n), dtype=np.uint8)
+    done = C.c_uint64()
+    rc = lib().kxo_frame_scan(data.ctypes.data, data.size, n, max_payload, fo.ctypes.data, ps.ctypes.data,
+                              pe.ctypes.data, kd.ctypes.data, C.byref(done))
+    return rc, fo, ps[:n], pe[:n], kd[:n], done.value
 
 
 def flatten(schema: Schema) -> Tuple[int, List[A.ColumnInfo], int]:

@@ -27,6 +27,8 @@ def lib():
         _lib.emu_decode.restype = C.c_int
         _lib.emu_decode.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64,
                                     C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]
+        _lib.emu_frames.restype = C.c_int
+        _lib.emu_frames.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint64] + [C.c_void_p] * 5
     return _lib
 
 
@@ -53,3 +55,15 @@ def skip(data: np.ndarray, n: int, threads: int = 8):
     rc = lib().emu_decode(None, 0, data.ctypes.data, data.size, None, n, None, None, C.addressof(st), 1,
                           offs.ctypes.data)
     return rc, offs, st
+
+
+def frames(data: np.ndarray, n: int, max_payload: int = 0, threads: int = 8):
+    os.environ["KX_EMU_THREADS"] = str(threads)
+    fo = np.zeros(n + 1, dtype=np.uint64)
+    ps = np.zeros(max(1, n), dtype=np.uint64)
+    pe = np.zeros(max(1, n), dtype=np.uint64)
+    kd = np.zeros(max(1, n), dtype=np.uint8)
+    st = A.Status()
+    rc = lib().emu_frames(data.ctypes.data, data.size, n, max_payload, fo.ctypes.data, ps.ctypes.data,
+                          pe.ctypes.data, kd.ctypes.data, C.addressof(st))
+    return rc, fo, ps[:n], pe[:n], kd[:n], st

@@ -58,3 +58,25 @@ extern "C" int emu_decode(const kx_struct_desc* structs, uint32_t nstructs, cons
   }
   return rc;
 }
+
+// framing sniff (kx_launch_frames) under the emulator, workspace shared with emu_decode's
+extern "C" int emu_frames(const uint8_t* in, uint64_t in_len, uint64_t n, uint64_t max_payload, uint64_t* fo,
+                          uint64_t* ps, uint64_t* pe, uint8_t* kinds, kx_status* status) {
+  const size_t ws_size = kx_skip_ws_bytes(in_len);
+  static char* ws = nullptr;
+  static size_t ws_cap = 0;
+  static uint64_t epoch = 0xffff;
+  if (ws_cap < ws_size) {
+    free(ws);
+    ws_cap = ws_size + ws_size / 4;
+    ws = (char*)malloc(ws_cap);
+    epoch = 0xffff;
+  }
+  if (++epoch > 0xffff) {
+    memset(ws, 0, ws_cap);
+    memset(ws + 8, 0xff, 8);
+    epoch = 1;
+  }
+  status->diag[0] = status->diag[1] = 0;
+  return kx_launch_frames(in, in_len, n, max_payload, fo, ps, pe, kinds, status, ws, ws_cap, epoch, nullptr);
+}

@@ -6,6 +6,7 @@ import numpy as np
 import pytest
 
 from tests import decode_cases as DC
+from tests import frame_cases as FC
 from tests import pb_cases as PC
 from tests.emu import emu
 
@@ -128,3 +129,17 @@ def test_emu_chunked(edec, oracle, case, ahead, monkeypatch):
     monkeypatch.setenv("KX_EMU_CHUNK", "64")
     monkeypatch.setenv("KX_EMU_AHEAD", str(ahead))
     DC.case_chunked(edec, oracle, case)
+
+
+# ---- framing sniff (M_FRAME walker, kx_launch_frames) ----
+def _emu_scan(threads=8):
+    def scan(wire, n, mx):
+        rc, fo, ps, pe, kd, st = emu.frames(wire, n, mx, threads=threads)
+        assert rc == 0, rc
+        return fo, ps, pe, kd, st
+    return scan
+
+
+@pytest.mark.parametrize("case", FC.SCAN_CASES)
+def test_emu_frames(edec, oracle, case):
+    FC.case_scan(_emu_scan(), oracle, case)
