@@ -65,7 +65,7 @@ def same_offsets(a, b) -> bool:
 class Batch:
     """One same-schema batch resident in HBM: source columns, GPU-encoded wire, decode outputs."""
 
-    def __init__(self, cfg, n, dev, start, mode, local):
+    def __init__(self, cfg, n, dev, start, mode, local, views=False):
         import torch
 
         from kitex_amd import _abi as A
@@ -73,7 +73,7 @@ class Batch:
         from kitex_amd import synth
         from kitex_amd.codec import ProtobufCodec, ThriftCodec, status_tensor
         from kitex_amd.columns import alloc_device
-        self.cfg, self.n, self.mode = cfg, n, mode
+        self.cfg, self.n, self.mode, self.views = cfg, n, mode, views
         sch = S.SCHEMAS[cfg]()
         self.cdc = ProtobufCodec(sch, device=local) if cfg == "pf" else ThriftCodec(sch, device=local)
         self.infos = infos = self.cdc.dschema.infos
@@ -84,7 +84,7 @@ class Batch:
         self.var_caps = [0 if ci.kind == A.COL_FIXED else last_offset(self.src.cols[c][0])
                          for c, ci in enumerate(infos)]
         wide = any(v >= (1 << 32) for v in self.var_caps)
-        self.out = alloc_device(infos, n, self.var_caps, self.cdc.dschema.npresence, dev, wide=wide)
+        self.out = alloc_device(infos, n, self.var_caps, self.cdc.dschema.npresence, dev, wide=wide, views=views)
         self.offsets = self.offs if mode == "offsets" else None
         self.st = status_tensor(dev)
 
@@ -105,6 +105,8 @@ class Batch:
         for c, ci in enumerate(self.infos):
             if ci.kind == A.COL_FIXED:
                 ok &= bool(torch.equal(self.out.cols[c], self.src.cols[c]))
+            elif self.views and ci.kind == A.COL_BYTES:
+                ok &= self._verify_views(c)
             else:
                 ok &= same_offsets(self.out.cols[c][0], self.src.cols[c][0])
                 tot = self.var_caps[c]
@@ -113,9 +115,28 @@ class Batch:
             ok &= bool(torch.equal(self.out.presence[:self.n], self.src.presence[:self.n]))
         return ok
 
+    def _verify_views(self, c, limit=1 << 20) -> bool:
+        """view pairs of the first `limit` records name exactly the source strings"""
+        import torch
+        k = min(self.n, limit)
+        pairs = self.out.cols[c].pairs[:k].to(torch.int64) & 0xFFFFFFFF
+        so = self.src.cols[c][0][:k + 1].to(torch.int64) & 0xFFFFFFFF
+        lens = so[1:] - so[:-1]
+        if not torch.equal(pairs[:, 1], lens):
+            return False
+        idx = torch.repeat_interleave(pairs[:, 0] - so[:-1], lens) + torch.arange(int(so[-1] - so[0]),
+                                                                                    device=pairs.device) + so[0]
+        return bool(torch.equal(self.wire[idx], self.src.cols[c][1][int(so[0]):int(so[-1])]))
+
     def out_bytes_per_record(self) -> float:
         from kitex_amd import _abi as A
         n = self.n
+        if self.views:   # zero-copy views: (offset, length) per string, no arena (SURVEY.md §8d, 247 B for R2)
+            return (sum((ci.width if ci.kind == A.COL_FIXED else 8 if ci.kind == A.COL_BYTES else 4)
+                        for ci in self.infos)
+                    + sum(self.var_caps[c] * (ci.width if ci.kind == A.COL_LIST else 1) / n
+                          for c, ci in enumerate(self.infos) if ci.kind not in (A.COL_FIXED, A.COL_BYTES))
+                    + (8 if self.cdc.dschema.npresence else 0))
         return (sum((ci.width if ci.kind == A.COL_FIXED else 4) for ci in self.infos)
                 + sum(self.var_caps[c] * (ci.width if ci.kind == A.COL_LIST else 1) / n
                       for c, ci in enumerate(self.infos) if ci.kind != A.COL_FIXED)
@@ -411,6 +432,12 @@ def extras(args, r2, dev, local):
     try:
         if r2 is not None:
             out["r2_encode"] = {"records": r2.n, **encode_entry(r2)}
+            bv = Batch("r2", r2.n, dev, 0, "concat", local, views=True)
+            e = decode_entry(bv)
+            e["roofline"]["read_only_frac"] = bv.in_bytes / (e["roofline"]["avg_launch_ms"] / 1e3) / 1e9 / HBM_PEAK_GBS
+            out["r2_decode_views"] = {"records": bv.n, "out_bytes_per_record": bv.out_bytes_per_record(), **e}
+            del bv
+            torch.cuda.empty_cache()
         b3 = Batch("r3", 4 << 20, dev, 0, "concat", local)
         out["r3_decode"] = {"records": b3.n, "wire_bytes_per_record": b3.in_bytes / b3.n, **decode_entry(b3)}
         out["r3_encode"] = {"records": b3.n, **encode_entry(b3)}

@@ -141,8 +141,16 @@ typedef struct kx_column {
   void* elem_offsets;     /* LIST_BYTES: byte offset of every element (elem_capacity+1 entries) */
   uint64_t elem_capacity; /* LIST_BYTES: element capacity */
   uint32_t offset_bytes;  /* 4 (or 0) / 8: width of offsets and elem_offsets entries */
-  uint32_t reserved0;
+  uint32_t flags;         /* KX_COLF_* */
 } kx_column;
+
+/* KX_COLF_VIEW (decode, BYTES columns): zero-copy string views instead of copies. `offsets` receives
+ * n (offset, length) pairs of offset_bytes each: record i's string is in[off .. off + len) of the
+ * decode call's input (len 0 => off 0); `data` / `capacity` are ignored and no arena is written. The
+ * input must outlive the columns (the no-copy reads of the generated code, e.g. unsafex string
+ * views). With 4-byte pairs the input must be < 4 GiB (else KX_ERR_SIZE_LIMIT). Not accepted by the
+ * encoders or the kx_host_* calls. */
+#define KX_COLF_VIEW 1u
 
 #define KX_MAX_COLUMNS 32
 #define KX_MAX_STRUCTS 16
@@ -188,7 +196,8 @@ void kx_ctx_destroy(kx_ctx* c);
  * decoded as a pipeline: the index pass of chunk k runs on a second stream of the ctx while chain +
  * emit of chunk k - 1 run on the caller's stream, `ahead` chunks apart at most, so the emit pass
  * re-reads input the index pass has just brought into the Infinity Cache. Results are identical
- * for every setting. Default: KX_CHUNK_MB environment variable, else 64 MiB, ahead 1. */
+ * for every setting. Default: KX_CHUNK_MB environment variable, else 0 (off: on MI355X the
+ * per-chunk chain step costs more than the cache re-read saves), ahead 1. */
 int kx_ctx_set_pipeline(kx_ctx* c, uint64_t chunk_bytes, int ahead);
 
 /* ---- Thrift binary: batched FastRead ----

@@ -38,6 +38,7 @@ REQ_DEFAULT, REQ_REQUIRED, REQ_OPTIONAL = 0, 1, 2
 FIELD_BINARY = 1  # kx_field_desc.reserved0 flag: protobuf `bytes` (no UTF-8 validation)
 
 COL_FIXED, COL_BYTES, COL_LIST, COL_LIST_BYTES = 1, 2, 3, 4
+COLF_VIEW = 1  # kx_column.flags: zero-copy (offset, length) string views
 MAX_COLUMNS = 32
 MAX_STRUCTS = 16
 
@@ -76,7 +77,7 @@ class ColumnInfo(C.Structure):
 class Column(C.Structure):
     _fields_ = [("data", C.c_void_p), ("offsets", C.c_void_p), ("capacity", C.c_uint64),
                 ("elem_offsets", C.c_void_p), ("elem_capacity", C.c_uint64),
-                ("offset_bytes", C.c_uint32), ("reserved0", C.c_uint32)]
+                ("offset_bytes", C.c_uint32), ("flags", C.c_uint32)]
 
 
 class Columns(C.Structure):

@@ -182,14 +182,15 @@ class ThriftCodec:
 
     def Unmarshal(self, buf, n: int, offsets=None, out: ColumnSet = None, var_caps: Sequence[int] = None,
                   record_status: bool = False, stream=None, raise_on_error: bool = True,
-                  status=None) -> DecodeResult:
-        """Decode n records from `buf` (uint8 tensor in HBM). offsets: int64[n+1] tensor or None."""
+                  status=None, views: bool = False) -> DecodeResult:
+        """Decode n records from `buf` (uint8 tensor in HBM). offsets: int64[n+1] tensor or None.
+        views: string/binary columns as zero-copy (offset, length) pairs into `buf` (KX_COLF_VIEW)."""
         import torch
         ds = self.dschema
         if out is None:
             if var_caps is None:
                 var_caps = [0 if ci.kind == A.COL_FIXED else max(1, buf.numel()) for ci in ds.infos]
-            out = alloc_device(ds.infos, n, var_caps, ds.npresence, self.device)
+            out = alloc_device(ds.infos, n, var_caps, ds.npresence, self.device, views=views)
         kc = to_kx_columns(out, ds.infos, var_caps)
         st = status if status is not None else status_tensor(self.device)
         rs = torch.empty(max(1, n), dtype=torch.uint8, device=self.device) if record_status else None

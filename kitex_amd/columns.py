@@ -12,6 +12,17 @@ from .synth import ColumnSet
 _NP_FIXED = {1: np.uint8, 2: np.int16, 4: np.int32, 8: np.int64}
 
 
+class Views:
+    """A BYTES column in zero-copy view mode (KX_COLF_VIEW): pairs[n, 2] = (offset into the decode
+    call's input, length), 4- or 8-byte integers; no arena."""
+
+    def __init__(self, pairs):
+        self.pairs = pairs
+
+    def __repr__(self):
+        return f"Views({tuple(self.pairs.shape)})"
+
+
 def _ptr(x) -> int:
     if x is None:
         return 0
@@ -45,6 +56,11 @@ def to_kx_columns(cs: ColumnSet, infos: Sequence[A.ColumnInfo], caps: Sequence[i
             out.cols[c].capacity = 0
             continue
         parts = cs.cols[c]
+        if isinstance(parts, Views):
+            out.cols[c].offsets = _ptr(parts.pairs)
+            out.cols[c].offset_bytes = _itemsize(parts.pairs)
+            out.cols[c].flags = A.COLF_VIEW
+            continue
         offs, data = parts[0], parts[-1]
         out.cols[c].data = _ptr(data)
         out.cols[c].offsets = _ptr(offs)
@@ -62,12 +78,15 @@ def to_kx_columns(cs: ColumnSet, infos: Sequence[A.ColumnInfo], caps: Sequence[i
 
 
 def alloc_host(infos: Sequence[A.ColumnInfo], n: int, var_caps: Sequence[int], npresence: int,
-               wide: bool = False, elem_caps: Sequence[int] = None) -> ColumnSet:
-    """Host columns. wide: 8-byte offsets. elem_caps[c]: element capacity of LIST_BYTES columns."""
+               wide: bool = False, elem_caps: Sequence[int] = None, views: bool = False) -> ColumnSet:
+    """Host columns. wide: 8-byte offsets. elem_caps[c]: element capacity of LIST_BYTES columns.
+    views: BYTES columns as zero-copy (offset, length) views."""
     odt = np.uint64 if wide else np.uint32
     cols: List[object] = []
     for c, ci in enumerate(infos):
-        if ci.kind == A.COL_FIXED:
+        if views and ci.kind == A.COL_BYTES:
+            cols.append(Views(np.zeros((max(1, n), 2), dtype=odt)))
+        elif ci.kind == A.COL_FIXED:
             cols.append(np.zeros(n, dtype=_NP_FIXED[ci.width]))
         elif ci.kind == A.COL_LIST_BYTES:
             ec = elem_caps[c] if elem_caps is not None else max(1, var_caps[c])
@@ -81,16 +100,19 @@ def alloc_host(infos: Sequence[A.ColumnInfo], n: int, var_caps: Sequence[int], n
 
 
 def alloc_device(infos: Sequence[A.ColumnInfo], n: int, var_caps: Sequence[int], npresence: int,
-                 device, fill: int = None, wide: bool = False, elem_caps: Sequence[int] = None) -> ColumnSet:
+                 device, fill: int = None, wide: bool = False, elem_caps: Sequence[int] = None,
+                 views: bool = False) -> ColumnSet:
     """Device columns (torch). wide: 8-byte offsets (int64) instead of 4-byte (int32 storage of
-    the unsigned offsets)."""
+    the unsigned offsets). views: BYTES columns as zero-copy (offset, length) views."""
     import torch
     tdt = {1: torch.uint8, 2: torch.int16, 4: torch.int32, 8: torch.int64}
     odt = torch.int64 if wide else torch.int32
     mk = torch.empty if fill is None else (lambda *a, **k: torch.full(*a[:1], fill, **k))
     cols: List[object] = []
     for c, ci in enumerate(infos):
-        if ci.kind == A.COL_FIXED:
+        if views and ci.kind == A.COL_BYTES:
+            cols.append(Views(mk((max(1, n), 2), dtype=odt, device=device)))
+        elif ci.kind == A.COL_FIXED:
             cols.append(mk((n,), dtype=tdt[ci.width], device=device))
         elif ci.kind == A.COL_LIST_BYTES:
             ec = elem_caps[c] if elem_caps is not None else max(1, var_caps[c])
@@ -107,7 +129,7 @@ def alloc_device(infos: Sequence[A.ColumnInfo], n: int, var_caps: Sequence[int],
 def var_caps_of(cs: ColumnSet, infos: Sequence[A.ColumnInfo]) -> List[int]:
     caps = []
     for c, ci in enumerate(infos):
-        if ci.kind == A.COL_FIXED:
+        if ci.kind == A.COL_FIXED or isinstance(cs.cols[c], Views):
             caps.append(0)
         else:
             offs = cs.cols[c][0]

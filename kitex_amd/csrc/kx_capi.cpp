@@ -107,7 +107,10 @@ int offset_width(const kx_column& k) {
   return k.offset_bytes == 0 || k.offset_bytes == 4 ? 4 : k.offset_bytes == 8 ? 8 : 0;
 }
 
-int to_launch_cols(const kx_schema* s, const kx_columns* out, KxLaunchCols* lc) {
+// allow_view: decode calls whose input stays in HBM (KX_COLF_VIEW on BYTES columns); in_len then
+// bounds 4-byte views
+int to_launch_cols(const kx_schema* s, const kx_columns* out, KxLaunchCols* lc, bool allow_view = false,
+                   uint64_t in_len = 0) {
   if (!out) return KX_ERR_INVALID_ARG;
   if (out->ncols != s->ncols) return KX_ERR_INVALID_ARG;
   if (s->npres && !out->presence) return KX_ERR_INVALID_ARG;
@@ -115,6 +118,17 @@ int to_launch_cols(const kx_schema* s, const kx_columns* out, KxLaunchCols* lc) 
   for (uint32_t c = 0; c < s->ncols; c++) {
     const kx_column& k = out->cols[c];
     const uint32_t kind = s->info[c].kind;
+    if (k.flags & ~KX_COLF_VIEW) return KX_ERR_INVALID_ARG;
+    if (k.flags & KX_COLF_VIEW) {
+      if (!allow_view || kind != KX_COL_BYTES || !k.offsets) return KX_ERR_INVALID_ARG;
+      const int ow = offset_width(k);
+      if (!ow) return KX_ERR_INVALID_ARG;
+      if (ow == 4 && in_len > 0xffffffffull) return KX_ERR_SIZE_LIMIT;
+      if (ow == 8) lc->owide |= 1u << c;
+      lc->view |= 1u << c;
+      lc->offs[c] = k.offsets;
+      continue;
+    }
     if (kind == KX_COL_FIXED) {
       if (!k.data) return KX_ERR_INVALID_ARG;
     } else {
@@ -266,11 +280,12 @@ int kx_thrift_decode_batch(kx_ctx* c, const kx_schema* s, const uint8_t* in, uin
   if (rc) return rc;
   hipStream_t st = (hipStream_t)stream;
   KxLaunchCols lc;
-  if ((rc = to_launch_cols(s, out, &lc))) return rc;
+  if ((rc = to_launch_cols(s, out, &lc, true, in_len))) return rc;
   if (n == 0) {
     KX_HIP_CHECK(hipMemsetAsync(status, 0, sizeof(kx_status), st));
     for (uint32_t k = 0; k < s->ncols; k++)
-      if (lc.offs[k]) KX_HIP_CHECK(hipMemsetAsync(lc.offs[k], 0, ((lc.owide >> k) & 1) ? 8 : 4, st));
+      if (lc.offs[k] && !((lc.view >> k) & 1))
+        KX_HIP_CHECK(hipMemsetAsync(lc.offs[k], 0, ((lc.owide >> k) & 1) ? 8 : 4, st));
     return KX_OK;
   }
   KxProgram* dp = nullptr;
@@ -349,12 +364,13 @@ int kx_pb_decode_batch(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_
   if (rc) return rc;
   hipStream_t st = (hipStream_t)stream;
   KxLaunchCols lc;
-  if ((rc = to_launch_cols(s, out, &lc))) return rc;
+  if ((rc = to_launch_cols(s, out, &lc, true, in_len))) return rc;
   if ((rc = pb_schema_ok(s))) return rc;
   if (n == 0) {
     KX_HIP_CHECK(hipMemsetAsync(status, 0, sizeof(kx_status), st));
     for (uint32_t k = 0; k < s->ncols; k++)
-      if (lc.offs[k]) KX_HIP_CHECK(hipMemsetAsync(lc.offs[k], 0, ((lc.owide >> k) & 1) ? 8 : 4, st));
+      if (lc.offs[k] && !((lc.view >> k) & 1))
+        KX_HIP_CHECK(hipMemsetAsync(lc.offs[k], 0, ((lc.owide >> k) & 1) ? 8 : 4, st));
     return KX_OK;
   }
   KxProgram* dp = nullptr;
@@ -381,7 +397,7 @@ static int decode_messages(kx_ctx* c, const kx_schema* s, const uint8_t* in, uin
   if (rc) return rc;
   hipStream_t st = (hipStream_t)stream;
   KxLaunchCols lc;
-  if ((rc = to_launch_cols(s, out, &lc))) return rc;
+  if ((rc = to_launch_cols(s, out, &lc, true, in_len))) return rc;
   if (pb && (rc = pb_schema_ok(s))) return rc;
   KxMsgOut mo{};
   if (msg_cols) {
@@ -398,7 +414,8 @@ static int decode_messages(kx_ctx* c, const kx_schema* s, const uint8_t* in, uin
   if (n == 0) {
     KX_HIP_CHECK(hipMemsetAsync(status, 0, sizeof(kx_status), st));
     for (uint32_t k = 0; k < s->ncols; k++)
-      if (lc.offs[k]) KX_HIP_CHECK(hipMemsetAsync(lc.offs[k], 0, ((lc.owide >> k) & 1) ? 8 : 4, st));
+      if (lc.offs[k] && !((lc.view >> k) & 1))
+        KX_HIP_CHECK(hipMemsetAsync(lc.offs[k], 0, ((lc.owide >> k) & 1) ? 8 : 4, st));
     if (mo.name_offs) KX_HIP_CHECK(hipMemsetAsync(mo.name_offs, 0, mo.name_owide ? 8 : 4, st));
     return KX_OK;
   }

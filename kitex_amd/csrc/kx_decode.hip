@@ -350,6 +350,17 @@ __device__ __forceinline__ void put_off(const KAS KxLaunchCols& cols, uint32_t c
   if ((cols.owide >> c) & 1) ((GLB uint64_t*)cols.offs[c])[r] = v;
   else ((GLB uint32_t*)cols.offs[c])[r] = (uint32_t)v;
 }
+// zero-copy view of record r's string (KX_COLF_VIEW): (offset into the input, length); empty -> (0, 0)
+__device__ __forceinline__ void put_view(const KAS KxLaunchCols& cols, uint32_t c, uint64_t r, uint64_t pos,
+                                         uint64_t len) {
+  const uint64_t o = len ? pos : 0;
+  if ((cols.owide >> c) & 1) {
+    ((GLB uint64_t*)cols.offs[c])[2 * r] = o;
+    ((GLB uint64_t*)cols.offs[c])[2 * r + 1] = len;
+  } else {
+    ((GLB uint64_t*)cols.offs[c])[r] = (o & 0xffffffffull) | (len << 32);  // one 8-byte store per pair
+  }
+}
 // the arena limit of column c in arena units: its capacity, and the 4-byte offset range
 __device__ __forceinline__ uint64_t arena_lim(const KAS KxLaunchCols& cols, uint32_t c) {
   return ((cols.owide >> c) & 1) ? cols.cap[c] : kmin64(cols.cap[c], 0xffffffffull);
@@ -406,6 +417,7 @@ __device__ __forceinline__ void close_slots(const KAS KxProgram* P, const KAS Kx
   for (int v = 0; v < NV; v++) {
     if (v >= (int)P->nvar) break;
     const uint32_t c = P->var_col[v];
+    if ((cols.view >> c) & 1) continue;  // views have no closing offset
     const KxpCol K = ld_col(P, c);
     if (K.kind == KXP_K_LISTB) {
       if ((uint32_t)v != K.vslot) continue;
@@ -2200,6 +2212,8 @@ __global__ void __launch_bounds__(NT) emit_kernel(DecParams dp_) {
             if ((uint32_t)u == K.vslot2) { B = atv[u]; nb = vs.len[u]; }
           emit_container(w, P, dp.cols, cc, K, vs.pos[v], vs.len[v], at, B, nb, r, dp.overflow);
         }
+      } else if (act && ((dp.cols.view >> cc) & 1)) {
+        put_view(dp.cols, cc, r, vs.pos[v], vs.len[v]);
       } else if (act) {
         const uint32_t nn = vs.len[v];
         if (at + nn <= arena_lim(dp.cols, cc)) {

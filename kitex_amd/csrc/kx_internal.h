@@ -28,7 +28,7 @@ struct kx_schema {
 // emit of chunk k - 1 run on the caller's stream, so emit re-reads a chunk the index pass has just
 // pulled through the Infinity Cache. Events order the two streams (rings of KX_PIPE_EV).
 #define KX_PIPE_EV 8
-#define KX_CHUNK_MB_DEFAULT 64
+#define KX_CHUNK_MB_DEFAULT 0  // measured: chunking is slower at every size
 struct KxPipe {
   hipStream_t aux = nullptr;
   hipEvent_t fork = nullptr;
@@ -76,7 +76,7 @@ struct KxLaunchCols {
   void* eoffs[KX_MAX_COLUMNS];   // LIST_BYTES: element byte offsets
   uint64_t ecap[KX_MAX_COLUMNS];
   uint32_t owide;                // bit c: column c has 8-byte offsets
-  uint32_t pad;
+  uint32_t view;                 // bit c: BYTES column c receives (offset, length) views (KX_COLF_VIEW)
   uint64_t* presence;
   uint64_t nrec;                 // records of the call (device-side guard of every column store)
   unsigned long long* guard;     // where a refused out-of-range access is reported (kx_status.diag[2])

@@ -476,6 +476,7 @@ typedef struct {
   uint64_t rec;
   int emit;
   uint64_t presence;
+  const uint8_t* in0;               /* start of the call's input (KX_COLF_VIEW offsets) */
   const uint8_t* vptr[KX_MAX_COLUMNS];
   uint64_t vlen[KX_MAX_COLUMNS];    /* bytes / elements */
   uint64_t vbytes[KX_MAX_COLUMNS];  /* LIST_BYTES: payload bytes of the elements */
@@ -699,6 +700,20 @@ static int emit_record_tail(dec_t* d, uint64_t* cursor, int* overflow) {
       emit_container(d, c, cursor, overflow);
       continue;
     }
+    if (col->flags & KX_COLF_VIEW) {  /* zero-copy view: (offset into the input, length), empty -> (0, 0) */
+      if (d->emit) {
+        const uint64_t o = n ? (uint64_t)(d->vptr[c] - d->in0) : 0;
+        if (col->offset_bytes == 8) {
+          ((uint64_t*)col->offsets)[2 * d->rec] = o;
+          ((uint64_t*)col->offsets)[2 * d->rec + 1] = n;
+        } else {
+          ((uint32_t*)col->offsets)[2 * d->rec] = (uint32_t)o;
+          ((uint32_t*)col->offsets)[2 * d->rec + 1] = (uint32_t)n;
+        }
+      }
+      cursor[vs] += n;
+      continue;
+    }
     const uint64_t lim = arena_lim(col);
     if (d->emit && cursor[vs] + n <= lim) {
       off_set(col, d->rec, cursor[vs]);
@@ -746,7 +761,7 @@ static int decode_range(const plan_t* p, rec_reader rd, const uint8_t* in, uint6
                         uint64_t* cursor, int emit, int* overflow) {
   dec_t d;
   memset(&d, 0, sizeof d);
-  d.p = p; d.out = out; d.emit = emit;
+  d.p = p; d.out = out; d.emit = emit; d.in0 = in;
   uint64_t pos = start;
   for (uint64_t r = r0; r < r1; r++) {
     d.rec = r;
@@ -787,7 +802,7 @@ static void finish_status(const plan_t* p, const kx_columns* out, kx_status* st,
     int vs = p->varidx[c], vs2 = p->varidx2[c];
     if (vs < 0) continue;
     const kx_column* col = &out->cols[c];
-    if (col->offsets) {
+    if (col->offsets && !(col->flags & KX_COLF_VIEW)) {
       const uint64_t lim = vs2 >= 0 ? elem_lim(col) : arena_lim(col);
       if (cursor[vs] <= lim) off_set(col, n_rec, cursor[vs]);
       else overflow = 1;
@@ -1296,7 +1311,7 @@ int kxo_pb_decode(const kx_struct_desc* structs, uint32_t nstructs, const uint8_
   uint64_t cursor[KX_MAX_COLUMNS] = {0};
   int overflow = 0;
   dec_t d; memset(&d, 0, sizeof d);
-  d.p = p; d.out = out; d.emit = 1;
+  d.p = p; d.out = out; d.emit = 1; d.in0 = in;
   uint64_t r = 0;
   for (; r < n_ok; r++) {
     d.rec = r; d.presence = 0;

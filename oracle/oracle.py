@@ -155,12 +155,14 @@ def _infos(schema: Schema):
 
 
 def decode(schema: Schema, data: np.ndarray, n: int, offsets: Optional[np.ndarray] = None,
-           var_caps: Optional[Sequence[int]] = None, pb: bool = False, threads: int = 0):
-    """Decode n records with the restated FastRead (or proto3 body when pb=True)."""
+           var_caps: Optional[Sequence[int]] = None, pb: bool = False, threads: int = 0, views: bool = False,
+           wide: bool = False):
+    """Decode n records with the restated FastRead (or proto3 body when pb=True). views: string
+    columns as zero-copy (offset, length) pairs (KX_COLF_VIEW)."""
     infos, npres = _infos(schema)
     if var_caps is None:
         var_caps = [0 if ci.kind == A.COL_FIXED else max(1, data.size) for ci in infos]
-    out = alloc_host(infos, n, var_caps, npres)
+    out = alloc_host(infos, n, var_caps, npres, views=views, wide=wide)
     kc = to_kx_columns(out, infos, var_caps)
     st = A.Status()
     rs = np.zeros(max(1, n), dtype=np.uint8)

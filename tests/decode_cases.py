@@ -7,7 +7,7 @@ import numpy as np
 from kitex_amd import _abi as A
 from kitex_amd import schema as S
 from kitex_amd import synth
-from tests.helpers import assert_columns_equal, to_np
+from tests.helpers import assert_columns_equal, offsets_u64, to_np
 
 
 def check_decode(dec, oracle, sch, wire, n, offsets=None):
@@ -306,3 +306,56 @@ def case_chunked(dec, oracle, case):
     elif case == "fewer":
         cols, st = check_decode(dec, oracle, sch, wire, 6000)   # the chain ends in chunk 1 of 5
         assert st.consumed == int(offs[6000])
+
+
+# ---- zero-copy string views (KX_COLF_VIEW): (offset, length) into the input instead of copies ----
+VIEW_CASES = ["r2_concat", "r2_offsets", "r3_concat", "noncanonical", "errors", "wide", "pb"]
+
+
+def case_views(dec, oracle, case):
+    """the view pairs equal the oracle's, and every view names exactly the bytes the copy mode copies"""
+    if case == "pb":
+        sch = S.schema_pf()
+        rc, wire, _ = oracle.encode(sch, synth.gen_pf(3000, start=4), pb=True)
+        _check_views(dec, oracle, sch, wire, 3000, None, pb=True)
+        return
+    if case in ("r2_concat", "r2_offsets", "r3_concat", "wide"):
+        name = case.split("_")[0] if case != "wide" else "r2"
+        n = 4000 if name == "r3" else 20000
+        sch = S.SCHEMAS[name]()
+        rc, wire, offs = oracle.encode(sch, synth.GENERATORS[name](n, start=21))
+        _check_views(dec, oracle, sch, wire, n, offs if case == "r2_offsets" else None, wide=case == "wide")
+        return
+    sch = S.schema_r2()
+    rng = np.random.default_rng(12)
+    recs = [r2_record(oracle, rng, order=list(rng.permutation(10)) if i % 7 == 3 else None,
+                      strlens=(int(rng.integers(0, 50)), 0 if i % 5 == 0 else 32), dup=i % 11 == 4)
+            for i in range(3000)]
+    if case == "errors":   # a failing record in offsets mode reads as defaults: empty views (0, 0)
+        recs[1234] = rec_bytes(oracle, [(A.T_STRING, 9, bytes.fromhex("fffffff0"))])
+    wire, offs = concat(recs)
+    _check_views(dec, oracle, sch, wire, len(recs), offs)
+    if case == "noncanonical":
+        _check_views(dec, oracle, sch, wire, len(recs), None)
+
+
+def _check_views(dec, oracle, sch, wire, n, offsets, pb=False, wide=False):
+    rc, exp, est, ers = oracle.decode(sch, wire, n, offsets=offsets, pb=pb, views=True, wide=wide)
+    cols, st = dec.decode_views(sch, wire, n, offsets, pb=pb, wide=wide)
+    assert st.code == est.code, (st.code, est.code)
+    _, infos, _ = oracle.flatten(sch)
+    ok = est.n_records if offsets is None else n
+    assert_columns_equal(cols, exp, infos, ok)
+    # each view covers exactly the bytes the copy mode copies
+    rc2, cp, _, _ = oracle.decode(sch, wire, n, offsets=offsets, pb=pb)
+    from kitex_amd.columns import Views
+    for c, ci in enumerate(infos):
+        if not isinstance(exp.cols[c], Views):
+            continue
+        pairs = to_np(cols.cols[c].pairs)[:ok].astype(np.int64)
+        co = offsets_u64(to_np(cp.cols[c][0]))[:ok + 1].astype(np.int64)
+        data = to_np(cp.cols[c][1])
+        for r in range(0, ok, max(1, ok // 200)):
+            o, ln = pairs[r]
+            assert ln == co[r + 1] - co[r]
+            assert bytes(wire[o:o + ln]) == bytes(data[co[r]:co[r + 1]])

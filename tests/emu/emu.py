@@ -33,11 +33,11 @@ def lib():
 
 
 def decode(schema, infos, npres, data: np.ndarray, n: int, offsets=None, var_caps=None, threads: int = 8,
-           pb: bool = False):
+           pb: bool = False, views: bool = False, wide: bool = False):
     os.environ["KX_EMU_THREADS"] = str(threads)
     if var_caps is None:
         var_caps = [0 if ci.kind == A.COL_FIXED else max(1, data.size) for ci in infos]
-    out = alloc_host(infos, n, var_caps, npres)
+    out = alloc_host(infos, n, var_caps, npres, views=views, wide=wide)
     kc = to_kx_columns(out, infos, var_caps)
     st = A.Status()
     rs = np.zeros(max(1, n), dtype=np.uint8)

@@ -21,6 +21,7 @@ extern "C" int emu_decode(const kx_struct_desc* structs, uint32_t nstructs, cons
       lc.eoffs[c] = out->cols[c].elem_offsets;
       lc.ecap[c] = out->cols[c].elem_capacity;
       if (out->cols[c].offset_bytes == 8) lc.owide |= 1u << c;
+      if (out->cols[c].flags & KX_COLF_VIEW) lc.view |= 1u << c;
     }
     lc.presence = out->presence;
   }

@@ -32,7 +32,15 @@ def _assert_list_bytes(got, exp, n, c, ci):
 
 def assert_columns_equal(got, exp, infos, n, check_presence=True):
     """Field-for-field equality of the first n records (fixed values, var bytes/elements, offsets)."""
+    from kitex_amd.columns import Views
     for c, ci in enumerate(infos):
+        if isinstance(got.cols[c], Views) or isinstance(exp.cols[c], Views):
+            assert isinstance(got.cols[c], Views) and isinstance(exp.cols[c], Views), f"column {c}: view vs copy"
+            g = to_np(got.cols[c].pairs)[:n].astype(np.uint64)
+            e = to_np(exp.cols[c].pairs)[:n].astype(np.uint64)
+            bad = np.nonzero((g != e).any(axis=1))[0]
+            assert bad.size == 0, f"view column {c} (field {ci.field_id}) differs at records {bad[:8]}"
+            continue
         if ci.kind == A.COL_FIXED:
             g = to_np(got.cols[c])[:n].view(np.uint8).reshape(n, -1) if n else None
             e = to_np(exp.cols[c])[:n].view(np.uint8).reshape(n, -1) if n else None

@@ -22,6 +22,13 @@ class EmuDecoder:
         assert rc == 0, rc
         return out, st, rs
 
+    def decode_views(self, sch, wire, n, offsets=None, pb=False, wide=False):
+        _, infos, npres = self.oracle.flatten(sch)
+        rc, out, st, rs = emu.decode(sch, infos, npres, wire, n, offsets=offsets, threads=self.threads, pb=pb,
+                                     views=True, wide=wide)
+        assert rc == 0, rc
+        return out, st
+
 
 @pytest.fixture(scope="module")
 def edec(oracle):
@@ -143,3 +150,8 @@ def _emu_scan(threads=8):
 @pytest.mark.parametrize("case", FC.SCAN_CASES)
 def test_emu_frames(edec, oracle, case):
     FC.case_scan(_emu_scan(), oracle, case)
+
+
+@pytest.mark.parametrize("case", DC.VIEW_CASES)
+def test_emu_views(edec, oracle, case):
+    DC.case_views(edec, oracle, case)

@@ -55,6 +55,18 @@ class GpuDecoder:
                             raise_on_error=False)
         return res.columns, res.read_status(), res.record_status
 
+    def decode_views(self, sch, wire, n, offsets=None, pb=False, wide=False):
+        from kitex_amd.codec import ProtobufCodec, ThriftCodec
+        from kitex_amd.columns import alloc_device
+        torch, dev = self.torch, self.dev
+        cdc = ProtobufCodec(sch) if pb else codec(sch)[1]
+        buf = torch.from_numpy(wire.copy()).to(dev)
+        offs = torch.from_numpy(offsets.astype(np.int64)).to(dev) if offsets is not None else None
+        ds = cdc.dschema
+        out = alloc_device(ds.infos, n, [0] * len(ds.infos), ds.npresence, dev, views=True, wide=wide)
+        res = cdc.Unmarshal(buf, n, offsets=offs, out=out, record_status=offsets is not None, raise_on_error=False)
+        return res.columns, res.read_status()
+
 
 @pytest.fixture(scope="module")
 def gdec(torch, dev):
@@ -382,3 +394,8 @@ def test_encode_containers_bit_exact(torch, dev, oracle, name):
     assert np.array_equal(to_np(got), wire)
     assert np.array_equal(to_np(goffs), offs.astype(np.int64))
     DC.check_decode(GpuDecoder(torch, dev), oracle, sch, wire, cs.n)
+
+
+@pytest.mark.parametrize("case", DC.VIEW_CASES)
+def test_decode_views_match_oracle(gdec, oracle, case):
+    DC.case_views(gdec, oracle, case)
