@@ -1221,6 +1221,34 @@ __device__ __forceinline__ Src load_window(KParams& dp, LDS uint32_t* win, uint6
              thrift ? P->canon_pres : 0ull};
 }
 
+// The same window load with the DMA issued from inline assembly, invisible to the compiler's wait
+// insertion: its own tracking would put `s_waitcnt vmcnt(0)` in front of every LDS read (it cannot
+// tell which window a read hits), which serialises a prefetch. The caller owns the wait: exactly
+// WIN_LOADS vector-memory instructions are issued per window.
+__device__ __forceinline__ void dma_lds16(v4u rs, LDS uint32_t* dst, uint32_t voff, uint32_t soff) {
+  const uint32_t m0v = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)dst);
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 1\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds" ::"s"(m0v), "v"(voff), "s"(rs), "s"(soff) : "memory", "m0");
+}
+
+__device__ __forceinline__ Src load_window_async(KParams& dp, LDS uint32_t* win, uint64_t lo, int lane, bool thrift) {
+  const uint64_t abs_in = (uint64_t)dp.in;
+  const uint64_t wbase = (abs_in + kmin64(lo, dp.in_len)) & ~15ull;
+  const uint64_t end = abs_in + dp.in_len;
+  const int32_t wlen = dp.nolds || end < wbase + 16 ? 0 : (int32_t)kmin64((uint64_t)WINB, (end - wbase) & ~15ull);
+  v4u rs;
+  rs.x = __builtin_amdgcn_readfirstlane((uint32_t)wbase);
+  rs.y = __builtin_amdgcn_readfirstlane((uint32_t)(wbase >> 32)) & 0xffffu;
+  rs.z = __builtin_amdgcn_readfirstlane((uint32_t)wlen);
+  rs.w = 0x00020000u;
+  const uint32_t voff = (uint32_t)lane * 16u;
+#pragma unroll
+  for (int k = 0; k < WIN_LOADS; k++)
+    if ((k + 1) * 64 <= WINB / 16 || k * 64 + lane < WINB / 16) dma_lds16(rs, win + k * 256, voff, (uint32_t)k * 1024u);
+  const KAS KxProgram* P = dp.prog;
+  return Src{dp.in, dp.in_len, wbase - abs_in, wlen, win, thrift ? P->steps : nullptr, thrift ? P->nsteps : 0u,
+             thrift ? P->canon_pres : 0ull};
+}
+
 // ---------------------------------------------------------------------------------------------
 // Framing sniff (M_FRAME): one socket-buffer frame at pos. defaultCodec.DecodeMeta + checkPayload
 // (default_codec.go:189-221, 328-427), Mesh header (header_codec.go:192-212), TTHeader meta + info
@@ -1454,7 +1482,8 @@ __device__ __forceinline__ uint64_t frame_scan_segment(KParams& dp, const Src& w
 }
 
 template <int NV, int MODE>
-__device__ __forceinline__ Cand lane_candidate(KParams& dp, const Src& w, uint64_t seg_lo, uint64_t seg_hi, int lane) {
+__device__ __forceinline__ Cand lane_candidate(KParams& dp, const Src& w, uint64_t seg_lo, uint64_t seg_hi, int lane,
+                                               uint32_t dsig) {
   Cand cd;
   cd.ent = X_NONE; cd.plim = seg_lo; cd.sig = 0; cd.smask = 0xffu; cd.s2o = 0; cd.s2 = 0; cd.strict = false;
   if (seg_lo >= seg_hi) return cd;
@@ -1467,7 +1496,6 @@ __device__ __forceinline__ Cand lane_candidate(KParams& dp, const Src& w, uint64
     return cd;
   }
   const KAS KxProgram* P = dp.prog;
-  const uint32_t dsig = data_sig(dp);
   const bool dok = dsig != 0 && canon_t(dsig & 0xff) != 1;  // the first record starts with a field header
   uint32_t sig, slen;
   bool own = false;
@@ -1533,11 +1561,11 @@ __device__ __forceinline__ uint64_t next_hit(KParams& dp, const Src& w, const Ca
 // tlo). Returns the tile aggregate (uniform).
 template <int NV, int MODE>
 __device__ Agg walk_tile(KParams& dp, const Src& w, uint64_t tlo, uint64_t thi, uint64_t seed, int lane,
-                         uint16_t* starts) {
+                         uint16_t* starts, uint32_t dsig) {
   const KAS KxProgram* P = dp.prog;
   const uint64_t seg_lo = tlo + (uint64_t)lane * SEG;
   const uint64_t seg_hi = kmin64(seg_lo + SEG, thi);
-  const Cand cd = lane_candidate<NV, MODE>(dp, w, seg_lo, seg_hi, lane);
+  const Cand cd = lane_candidate<NV, MODE>(dp, w, seg_lo, seg_hi, lane, dsig);
   uint64_t ent = cd.ent;
   if (dp.diag & 512) {  // diagnostics: DMA + candidate scan only
     Agg a;
@@ -1718,7 +1746,7 @@ __device__ Agg tile_agg(KParams& dp, LDS uint32_t* win, uint64_t t, uint64_t see
   const uint64_t t0 = (dp.diag & 64) ? __builtin_amdgcn_s_memtime() : 0;
   const Src w = load_window(dp, win, lo, lane, MODE == M_THRIFT);
   if ((dp.diag & 64) && lane == 0) atomicAdd(&g_phase[0], (unsigned long long)(__builtin_amdgcn_s_memtime() - t0));
-  return walk_tile<NV, MODE>(dp, w, lo, hi, seed, lane, dp.starts + t * dp.slotcap);
+  return walk_tile<NV, MODE>(dp, w, lo, hi, seed, lane, dp.starts + t * dp.slotcap, data_sig(dp));
 }
 
 __device__ __forceinline__ void put_tile(KParams& dp, uint64_t t, const Agg& a, int nv) {
@@ -1865,6 +1893,47 @@ __global__ void __launch_bounds__(NT, 4) index_kernel(DecParams dp_) {  // 4 wav
   }
   if (lane == 0 && !(dp.diag & 4)) put_tile(dp, t, a, NV);
   if ((dp.diag & 64) && lane == 0) atomicAdd(&g_phase[5], (unsigned long long)(__builtin_amdgcn_s_memtime() - t_start));
+}
+
+// ---- kernel 1 (persistent variant, concatenated mode): each wave walks tiles t, t + W, t + 2W ...
+// with two LDS windows: the DMA of its next tile is in flight while it walks the current one
+// (s_waitcnt vmcnt(WIN_LOADS) leaves exactly the next window's loads outstanding). Two LDS windows
+// per wave halve the occupancy (2 waves / SIMD) in exchange for a wave that never waits for its own
+// DMA after the first tile.
+template <int NV, int MODE>
+__global__ void __launch_bounds__(NT, 2) index_kernel_pf(DecParams dp_) {
+  KParams& dp = KX_PARAMS();
+  (void)dp_;
+  __shared__ __attribute__((aligned(16))) uint32_t WINA[WAVES][WINW];
+  __shared__ __attribute__((aligned(16))) uint32_t WINB_[WAVES][WINW];
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const uint64_t W = (uint64_t)gridDim.x * WAVES;
+  uint64_t t = dp.t_lo + (uint64_t)blockIdx.x * WAVES + wv;
+  if (t >= dp.t_hi) return;
+  LDS uint32_t* wa = (LDS uint32_t*)WINA[wv];
+  LDS uint32_t* wb = (LDS uint32_t*)WINB_[wv];
+  const uint32_t dsig = data_sig(dp);  // before the first DMA: its global load must not wait on one
+  uint64_t lo, hi;
+  tile_range(dp, t, lo, hi);
+  Src w = load_window_async(dp, wa, lo, lane, MODE == M_THRIFT);
+  bool odd = false;
+  for (;;) {
+    const uint64_t tn = t + W;
+    uint64_t lon = 0, hin = 0;
+    Src wn = w;
+    if (tn < dp.t_hi) {
+      tile_range(dp, tn, lon, hin);
+      wn = load_window_async(dp, odd ? wa : wb, lon, lane, MODE == M_THRIFT);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WIN_LOADS) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    const Agg a = walk_tile<NV, MODE>(dp, w, lo, hi, t == 0 ? 0ull : X_NONE, lane, dp.starts + t * dp.slotcap, dsig);
+    if (lane == 0) put_tile(dp, t, a, NV);
+    if (tn >= dp.t_hi) break;
+    t = tn; lo = lon; hi = hin; w = wn; odd = !odd;
+  }
 }
 
 // ---- kernel 1b: group scan (one wave per group of 64 tiles) ----
@@ -2374,7 +2443,21 @@ int launch_t(const DecParams& dp0, const WsLayout& L, void* ws, hipStream_t stre
     return KX_OK;
   }
   if (!dp.direct) {
-    hipLaunchKernelGGL((index_kernel<NV, MODE>), dim3(grid), dim3(NT), 0, stream, dp);
+    static int ncu = -1;
+    const char* e = getenv("KX_INDEX_PF");
+    const int pf = e ? atoi(e) : 0;
+    if (pf > 0 && ncu < 0) {
+      int dev = 0;
+      if (hipGetDevice(&dev) != hipSuccess ||
+          hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        ncu = 0;
+    }
+    if (pf > 0 && !dp.offsets && ncu > 0 && !dp.diag) {
+      const unsigned pgrid = (unsigned)kmin64(grid, (uint64_t)ncu * (uint64_t)pf);
+      hipLaunchKernelGGL((index_kernel_pf<NV, MODE>), dim3(pgrid), dim3(NT), 0, stream, dp);
+    } else {
+      hipLaunchKernelGGL((index_kernel<NV, MODE>), dim3(grid), dim3(NT), 0, stream, dp);
+    }
     KX_HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL((group_kernel<NV, MODE>), dim3(ggrid), dim3(NT), 0, stream, dp);
     KX_HIP_CHECK(hipGetLastError());

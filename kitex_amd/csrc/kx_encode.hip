@@ -21,7 +21,14 @@ namespace {
 
 constexpr int NT = 256;
 constexpr int RB = 1024;             // records per block
-constexpr int OUTB = 48 * 1024;      // LDS image bytes per round
+#ifndef KX_ENC_WT
+#define KX_ENC_WT 256
+#endif
+#ifndef KX_ENC_OUTB
+#define KX_ENC_OUTB (48 * 1024)
+#endif
+constexpr int WT = KX_ENC_WT;        // write pass: threads per workgroup (records per round)
+constexpr int OUTB = KX_ENC_OUTB;    // LDS image bytes per round
 
 struct EncParams {
   const KxProgram* prog;
@@ -94,34 +101,41 @@ __device__ uint64_t record_size(const KxProgram& P, const KxLaunchCols& C, uint6
   return sz;
 }
 
-// ---- byte sink: packs bytes into dwords before writing LDS (or global on the direct path) ----
+// ---- byte sink: packs bytes into aligned dwords before writing LDS (or global on the direct path).
+// The sink is kept dword-aligned from the start: `head` bytes of the first dword belong to the
+// previous record (another lane), so that dword is written byte by byte and every later one whole.
+// A put of k bytes stores at most one dword and has no loop, so lanes whose records start at
+// different alignments only differ in a predicated store (the old byte-draining loop diverged on
+// every field).
 struct Sink {
   uint8_t* base;   // LDS image or global output
-  uint64_t off;    // position of the first pending byte
-  uint64_t acc;    // pending bytes, first byte in bits 0..7
-  uint32_t n;      // number of pending bytes (< 8)
+  uint64_t off;    // dword-aligned position of the pending bytes
+  uint64_t acc;    // pending bytes (including `head` placeholder bytes), first in bits 0..7
+  uint32_t n;      // pending bytes (< 4 between puts)
+  uint32_t head;   // leading bytes of the first dword not owned by this record (0 once it is written)
 
-  __device__ __forceinline__ void drain() {
-    while (n) {
-      if (off & 3) {
-        base[off] = (uint8_t)acc;
-        acc >>= 8; off += 1; n -= 1;
-      } else if (n >= 4) {
-        *(uint32_t*)(base + off) = (uint32_t)acc;
-        acc >>= 32; off += 4; n -= 4;
-      } else {
-        break;
-      }
+  __device__ __forceinline__ Sink(uint8_t* b, uint64_t o)
+      : base(b), off(o & ~3ull), acc(0), n((uint32_t)(o & 3)), head((uint32_t)(o & 3)) {}
+
+  __device__ __forceinline__ void emit_dword() {
+    const uint32_t v = (uint32_t)acc;
+    if (head) {
+      for (uint32_t k = head; k < 4; k++) base[off + k] = (uint8_t)(v >> (8 * k));
+      head = 0;
+    } else {
+      *(uint32_t*)(base + off) = v;
     }
+    off += 4; acc >>= 32; n -= 4;
   }
   // append k (1..4) bytes, first byte in bits 0..7 of v
   __device__ __forceinline__ void put(uint32_t v, uint32_t k) {
     acc |= (uint64_t)(k == 4 ? v : (v & ((1u << (8 * k)) - 1))) << (8 * n);
     n += k;
-    drain();
+    if (n >= 4) emit_dword();
   }
   __device__ __forceinline__ void flush() {
-    while (n) { base[off] = (uint8_t)acc; acc >>= 8; off += 1; n -= 1; }
+    for (uint32_t k = head; k < n; k++) base[off + k] = (uint8_t)(acc >> (8 * k));
+    off += n; acc = 0; n = 0; head = 0;
   }
 };
 
@@ -146,19 +160,26 @@ __device__ __forceinline__ uint64_t load_fixed(const void* base, uint32_t w, uin
   }
 }
 
-// raw bytes into the sink, 4 at a time
+// raw bytes into the sink: blocks of up to 64 bytes whose dword loads are all issued before the first
+// is used (one memory round trip per block instead of one per 4 bytes: the encoder's write pass was
+// latency-bound on these loads)
 __device__ __forceinline__ void put_bytes(Sink& s, const uint8_t* src, uint32_t len) {
   const uint64_t sa = (uint64_t)src, se = sa + len;
-  uint32_t i = 0;
-  for (; i + 4 <= len; i += 4) {
-    // unaligned 4-byte read of the source string: aligned dwords that hold string bytes only
-    uint64_t A = (sa + i) & ~3ull;
-    uint32_t sh = (uint32_t)((sa + i) & 3);
-    uint32_t x0 = *(const uint32_t*)A;
-    uint32_t x1 = (sh && A + 4 < se) ? *(const uint32_t*)(A + 4) : 0u;
-    s.put(sh ? __builtin_amdgcn_alignbyte(x1, x0, sh) : x0, 4);
+  const uint32_t sh = (uint32_t)(sa & 3);
+  uint64_t A = sa & ~3ull;  // aligned dwords that hold string bytes only
+  uint32_t done = 0;
+  while (done + 4 <= len) {
+    const uint32_t units = min((len - done) >> 2, 16u);
+    uint32_t W[17];
+#pragma unroll
+    for (int j = 0; j < 17; j++) W[j] = ((uint32_t)j <= units && A + 4 * j < se) ? *(const uint32_t*)(A + 4 * j) : 0u;
+#pragma unroll
+    for (int u = 0; u < 16; u++)
+      if ((uint32_t)u < units) s.put(sh ? __builtin_amdgcn_alignbyte(W[u + 1], W[u], sh) : W[u], 4);
+    A += 4 * units;
+    done += 4 * units;
   }
-  for (; i < len; i++) s.put(src[i], 1);
+  for (; done < len; done++) s.put(src[done], 1);
 }
 
 // FastWriteNocopy for one record into the sink
@@ -398,14 +419,14 @@ __global__ void __launch_bounds__(1024) scan_kernel(EncParams ep) {
   }
 }
 
-__global__ void __launch_bounds__(NT) write_kernel(EncParams ep) {
+__global__ void __launch_bounds__(WT) write_kernel(EncParams ep) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   uint8_t* img = (uint8_t*)smem_raw;                        // OUTB + 32
   uint32_t* progw = (uint32_t*)(smem_raw + OUTB + 32);
   uint64_t* scratch = (uint64_t*)(smem_raw + OUTB + 32 + sizeof(KxProgram));
   __shared__ uint64_t s_take, s_round_bytes;
   if (ep.status->code != 0) return;                         // size limit: write nothing
-  for (int i = threadIdx.x; i < (int)(sizeof(KxProgram) / 4); i += NT) progw[i] = ((const uint32_t*)ep.prog)[i];
+  for (int i = threadIdx.x; i < (int)(sizeof(KxProgram) / 4); i += WT) progw[i] = ((const uint32_t*)ep.prog)[i];
   __syncthreads();
   const KxProgram& P = *reinterpret_cast<const KxProgram*>(progw);
   const uint64_t b = blockIdx.x;
@@ -431,7 +452,7 @@ __global__ void __launch_bounds__(NT) write_kernel(EncParams ep) {
     if (take == 0) {
       // a single record larger than the image: thread 0 writes it straight to HBM
       if (threadIdx.x == 0) {
-        Sink s{ep.out, gpos, 0, 0};
+        Sink s(ep.out, gpos);
         any_write(ep, P, r, s);
         if (ep.offsets_out) ep.offsets_out[r] = gpos;
         s_round_bytes = sz;
@@ -443,7 +464,7 @@ __global__ void __launch_bounds__(NT) write_kernel(EncParams ep) {
       continue;
     }
     if (threadIdx.x < take) {
-      Sink s{img, skew + pre, 0, 0};
+      Sink s(img, skew + pre);
       any_write(ep, P, my, s);
       if (ep.offsets_out) ep.offsets_out[my] = gpos + pre;
     }
@@ -454,7 +475,7 @@ __global__ void __launch_bounds__(NT) write_kernel(EncParams ep) {
     const uint64_t a0 = gstart & ~15ull;                     // image byte 0 <-> a0
     const uint64_t gend = gstart + bytes;
     const uint64_t nch = (gend - a0 + 15) >> 4;
-    for (uint64_t c = threadIdx.x; c < nch; c += NT) {
+    for (uint64_t c = threadIdx.x; c < nch; c += WT) {
       uint64_t ca = a0 + c * 16;
       if (ca >= gstart && ca + 16 <= gend) {
         *(uint4*)ca = *(const uint4*)(img + c * 16);
@@ -493,8 +514,8 @@ int kx_launch_encode(const KxProgram* dprog, const KxProgram& hprog, const KxLau
   if (sizes_only) return KX_OK;
   hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, stream, ep);
   KX_HIP_CHECK(hipGetLastError());
-  size_t shmem = OUTB + 32 + sizeof(KxProgram) + 8 * (NT / 64);
-  hipLaunchKernelGGL(write_kernel, dim3((unsigned)ep.nblocks), dim3(NT), shmem, stream, ep);
+  size_t shmem = OUTB + 32 + sizeof(KxProgram) + 8 * (WT / 64);
+  hipLaunchKernelGGL(write_kernel, dim3((unsigned)ep.nblocks), dim3(WT), shmem, stream, ep);
   KX_HIP_CHECK(hipGetLastError());
   return KX_OK;
 }

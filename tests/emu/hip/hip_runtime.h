@@ -142,6 +142,11 @@ inline void __builtin_amdgcn_raw_ptr_buffer_load_lds(emu_rsrc r, void* dst, unsi
   if (o + (int64_t)size <= r.n) memcpy((char*)dst + (size_t)emu_lane() * size, r.base + o, size);
   else memset((char*)dst + (size_t)emu_lane() * size, 0, size);
 }
+// the inline-assembly LDS DMA of load_window_async: rsrc dwords (base lo, base hi & 0xffff, num_records)
+inline void emu_dma_lds16(uint32_t __attribute__((ext_vector_type(4))) rs, void* dst, uint32_t voff, uint32_t soff) {
+  const char* base = (const char*)(((uint64_t)rs.y << 32) | rs.x);
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(emu_rsrc{base, (int32_t)rs.z}, dst, 16, (int)voff, (int)soff, 0, 0);
+}
 inline int __ffsll(long long x) { return __builtin_ffsll(x); }
 inline int __clzll(long long x) { return x ? __builtin_clzll((unsigned long long)x) : 64; }
 

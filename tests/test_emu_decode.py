@@ -155,3 +155,11 @@ def test_emu_frames(edec, oracle, case):
 @pytest.mark.parametrize("case", DC.VIEW_CASES)
 def test_emu_views(edec, oracle, case):
     DC.case_views(edec, oracle, case)
+
+
+@pytest.mark.parametrize("case", ["r2", "r3", "error", "truncated", "noncanonical", "pb", "containers"])
+def test_emu_index_prefetch(edec, oracle, case, monkeypatch):
+    """the persistent double-buffered index pass (KX_INDEX_PF=2: 2 workgroups per emulated CU, each
+    wave walking many tiles while the next one's DMA is in flight)"""
+    monkeypatch.setenv("KX_INDEX_PF", "2")
+    DC.case_chunked(edec, oracle, case)

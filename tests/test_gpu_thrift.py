@@ -63,8 +63,10 @@ class GpuDecoder:
         buf = torch.from_numpy(wire.copy()).to(dev)
         offs = torch.from_numpy(offsets.astype(np.int64)).to(dev) if offsets is not None else None
         ds = cdc.dschema
-        out = alloc_device(ds.infos, n, [0] * len(ds.infos), ds.npresence, dev, views=True, wide=wide)
-        res = cdc.Unmarshal(buf, n, offsets=offs, out=out, record_status=offsets is not None, raise_on_error=False)
+        caps = [0 if ci.kind == A.COL_FIXED else max(1, wire.size) for ci in ds.infos]
+        out = alloc_device(ds.infos, n, caps, ds.npresence, dev, views=True, wide=wide)
+        res = cdc.Unmarshal(buf, n, offsets=offs, out=out, var_caps=caps, record_status=offsets is not None,
+                            raise_on_error=False)
         return res.columns, res.read_status()
 
 
