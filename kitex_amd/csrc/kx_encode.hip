@@ -42,6 +42,7 @@ struct EncParams {
   uint64_t* block_tot;   // workspace: per-block total size, then (after scan) block base
   uint64_t nblocks;
   bool pb;               // Kitex-Protobuf records (Batch framing) instead of Thrift binary
+  int direct;            // tuning (KX_ENC_DIRECT=1): every round writes straight to HBM
 };
 
 // record offsets are 4 or 8 bytes wide (kx_column.offset_bytes)
@@ -449,6 +450,20 @@ __global__ void __launch_bounds__(WT) write_kernel(EncParams ep) {
     }
     __syncthreads();
     uint64_t take = s_take;
+    const uint64_t cnt = kmin64((uint64_t)WT, rend - r);
+    if (take < cnt / 2 || ep.direct) {
+      // large records (fewer than half of the round fit the image): every thread writes its record
+      // straight to HBM; its aligned dword stores still merge in L2
+      if (my < rend) {
+        Sink s(ep.out, gpos + pre);
+        any_write(ep, P, my, s);
+        if (ep.offsets_out) ep.offsets_out[my] = gpos + pre;
+      }
+      __syncthreads();
+      gpos += tot;
+      r += cnt;
+      continue;
+    }
     if (take == 0) {
       // a single record larger than the image: thread 0 writes it straight to HBM
       if (threadIdx.x == 0) {
@@ -506,6 +521,10 @@ int kx_launch_encode(const KxProgram* dprog, const KxProgram& hprog, const KxLau
   ep.prog = dprog; ep.cols = cols; ep.n = n; ep.out = out; ep.out_cap = out_cap;
   ep.sizes_out = sizes_out; ep.offsets_out = offsets_out; ep.status = status;
   ep.nblocks = (n + RB - 1) / RB;
+  {
+    const char* e = getenv("KX_ENC_DIRECT");
+    ep.direct = e ? atoi(e) : 0;
+  }
   if (ws_size < kx_encode_ws_bytes(n)) return KX_ERR_INVALID_ARG;
   ep.block_tot = (uint64_t*)ws;
   if (status) KX_HIP_CHECK(hipMemsetAsync(status, 0, sizeof(kx_status), stream));
