@@ -429,9 +429,25 @@ def extras(args, r2, dev, local):
                 "decode_diag": {"tile_rewalks": st.diag[0], "group_rescans": st.diag[1]},
                 "roofline": roofline(b.in_bytes + b.out_bytes_per_record() * b.n, avg, "decode")}
 
+    def crc_entry(b):
+        """CRC32C (crcPayloadValidator.Generate, validate.go:187-217) of every encoded R2 record"""
+        from kitex_amd.codec import CRC32PayloadValidator
+        v = CRC32PayloadValidator(device=local)
+        res = {}
+        t, per = time_steps(lambda: res.__setitem__("crc", v.Generate(b.wire, b.offs)), steps, warm, 1, dev)
+        avg = sum(per) / len(per) / 1e3
+        crc = res["crc"]
+        pick = [0, 1, b.n // 3, b.n // 2, b.n - 1]
+        offs = b.offs.cpu()
+        ok = all(crc32c_py(bytes(b.wire[int(offs[i]):int(offs[i + 1])].cpu().numpy())) == int(crc[i]) for i in pick)
+        alg = b.in_bytes + 12 * b.n  # payload bytes + u64 offsets in + u32 CRC out
+        return {"ranges": b.n, "ranges_per_s": b.n * steps / t, "ms_per_step": t / steps * 1e3, "sample_ok": ok,
+                "roofline": roofline(alg, avg, "crc32c")}
+
     try:
         if r2 is not None:
             out["r2_encode"] = {"records": r2.n, **encode_entry(r2)}
+            out["crc32c_generate"] = crc_entry(r2)
             bv = Batch("r2", r2.n, dev, 0, "concat", local, views=True)
             e = decode_entry(bv)
             e["roofline"]["read_only_frac"] = bv.in_bytes / (e["roofline"]["avg_launch_ms"] / 1e3) / 1e9 / HBM_PEAK_GBS
@@ -450,6 +466,16 @@ def extras(args, r2, dev, local):
     except Exception as e:  # the extras must never break the headline line
         out["error"] = repr(e)
     return out
+
+
+def crc32c_py(data: bytes) -> int:
+    """CRC-32C by definition (bench-side spot check of the device values)"""
+    c = 0xFFFFFFFF
+    for x in data:
+        c ^= x
+        for _ in range(8):
+            c = (c >> 1) ^ 0x82F63B78 if c & 1 else c >> 1
+    return c ^ 0xFFFFFFFF
 
 
 def host_inclusive(b, dev):

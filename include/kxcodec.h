@@ -31,6 +31,11 @@
  *   kx_thrift_decode_messages ... thriftCodec.Unmarshal over N framed messages (thrift.go:180-225):
  *                                 MessageBegin + Args{1: req} (k-mock.go:422-517) on the device
  *   kx_pb_decode_messages ....... protobufCodec.Unmarshal over N framed messages (protobuf.go:136-216)
+ *   kx_crc32c_batch ............. crcPayloadValidator.Generate / getCRC32C (pkg/remote/codec/validate.go:
+ *                                 183-217) over N payloads
+ *   kx_frame_crc32c_validate .... payloadChecksumValidate + crcPayloadValidator.Validate (validate.go:91-127,
+ *                                 190-201) of N TTHeader frames, as DecodeMeta runs it (default_codec.go:205-209)
+ *   kx_ctx_set_crc32c_check ..... CodecConfig{CRC32Check: true} (default_codec.go:70-92) for kx_*_decode_frames
  *   kx_strerror ................. error text; codes mirror pkg/remote/codec/perrors/protocol_error.go:28-36
  */
 #ifndef KXCODEC_H_
@@ -73,6 +78,8 @@ enum {
   KX_ERR_UNKNOWN_PROTOCOL = 10, /* framing sniff: no TTHeader / Mesh / Framed / PurePayload / Kitex-PB
                                   magic where one is required, or a malformed TTHeader / Mesh header
                                   (perrors UnknownProtocolError, type 0, default_codec.go:411-416) */
+  KX_ERR_PAYLOAD_VALIDATION = 11, /* payload checksum mismatch (crcPayloadValidator.Validate, validate.go:190-201:
+                                     kerrors.ErrPayloadValidation wrapping perrors.InvalidData) */
   KX_ERR_INVALID_ARG = 100,
   KX_ERR_HIP = 101,            /* a HIP runtime call failed */
   KX_ERR_NO_DEVICE = 102,
@@ -306,6 +313,29 @@ int kx_thrift_decode_frames(kx_ctx* c, const kx_schema* s, const uint8_t* in, ui
 int kx_pb_decode_frames(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len, uint64_t n,
                         uint64_t max_payload, uint64_t* frame_offsets, uint8_t* kinds, const kx_column* msg_cols,
                         const kx_columns* out, uint8_t* record_status, kx_status* status, void* stream);
+
+/* ---- CRC32C payload checksums (crcPayloadValidator, pkg/remote/codec/validate.go:168-217) ----
+ * CRC-32C = crc32.Update(0, crc32.MakeTable(crc32.Castagnoli), payload) (getCRC32C, :208-217); the
+ * header value is its big-endian lowercase hex (8 characters).
+ * kx_crc32c_batch: crc_out[i] (device u32) = CRC-32C of in[offsets[i] .. offsets[i+1]) (n + 1 device u64
+ *   offsets, e.g. kx_thrift_encode_batch's offsets_out): the Generate side. A range outside the input
+ *   gives KX_ERR_INVALID_ARG in status (that range's crc_out = 0).
+ * kx_frame_crc32c_validate: n frames starting at frame_offsets[i] (n + 1 entries, as kx_frame_scan writes
+ *   them). For each TTHeader frame whose string-KV info holds "crc32c" (transmeta.HeaderCRC32C) with a
+ *   non-empty value, the CRC-32C of the TTHeader payload (all bytes after the TTHeader, the Framed length
+ *   prefix included: PayloadLen) must hex-encode to exactly that value, else record_status[i] =
+ *   KX_ERR_PAYLOAD_VALIDATION. Frames of other framings, without the key or with an empty value pass
+ *   (:95-99, :191-195). crc_out (optional) = the payload's CRC-32C (0 for non-TTHeader frames). Status:
+ *   the first failing frame. */
+int kx_crc32c_batch(kx_ctx* c, const uint8_t* in, uint64_t in_len, const uint64_t* offsets, uint64_t n,
+                    uint32_t* crc_out, kx_status* status, void* stream);
+int kx_frame_crc32c_validate(kx_ctx* c, const uint8_t* in, uint64_t in_len, const uint64_t* frame_offsets,
+                             uint64_t n, uint32_t* crc_out, uint8_t* record_status, kx_status* status,
+                             void* stream);
+/* enable != 0: kx_*_decode_frames validate every TTHeader frame's CRC32C after the framing scan, as
+ * NewDefaultCodecWithConfig(CodecConfig{CRC32Check: true}) does (default_codec.go:70-92); a failing frame's
+ * message gets KX_ERR_PAYLOAD_VALIDATION (its record is not decoded). Default off. */
+int kx_ctx_set_crc32c_check(kx_ctx* c, int enable);
 
 /* Kitex-Protobuf meta header (host memory; protobuf.go:77-90 / 136-165). */
 uint64_t kx_pb_meta_length(uint32_t name_len);

@@ -26,6 +26,7 @@ ERR_EOF = 8
 ELEM_MAP_VALUE = 0x80
 ERR_APPLICATION_EXCEPTION = 9
 ERR_UNKNOWN_PROTOCOL = 10
+ERR_PAYLOAD_VALIDATION = 11
 # framing sniff kinds (kx_frame_scan): transport.Protocol | FRAME_PB | FRAME_MESH
 TRANS_PURE, TRANS_TTHEADER, TRANS_FRAMED, TRANS_TTHEADER_FRAMED = 0, 2, 4, 6
 FRAME_PB, FRAME_MESH = 0x10, 0x20
@@ -118,6 +119,7 @@ ERROR_NAMES = {
     ERR_EOF: "unexpected EOF",
     ERR_APPLICATION_EXCEPTION: "application exception message",
     ERR_UNKNOWN_PROTOCOL: "unknown protocol (framing sniff)",
+    ERR_PAYLOAD_VALIDATION: "payload validation failed (crc32c)",
     ERR_INVALID_ARG: "invalid argument",
     ERR_HIP: "HIP runtime error",
     ERR_NO_DEVICE: "no device",

@@ -247,13 +247,15 @@ class ThriftCodec:
 
     def UnmarshalFrames(self, buf, n: int, body_field: int = 1, max_payload: int = 0, out: ColumnSet = None,
                         var_caps: Sequence[int] = None, name_cap: int = None, stream=None,
-                        raise_on_error: bool = True) -> "MessageBatch":
+                        raise_on_error: bool = True, crc32_check: bool = False) -> "MessageBatch":
         """A socket buffer of n frames (TTHeader / Mesh / Framed / PurePayload, default_codec.go:189-221)
         straight to columns: framing sniff on the device, then UnmarshalMessages on the payloads.
         The batch also carries frame_offsets (int64[n+1]) and kinds (uint8[n], transport.Protocol |
-        FRAME_PB | FRAME_MESH)."""
+        FRAME_PB | FRAME_MESH). crc32_check: CodecConfig{CRC32Check: true} (default_codec.go:70-92), every
+        TTHeader frame's "crc32c" header is checked against its payload (ERR_PAYLOAD_VALIDATION)."""
         import torch
         s = _stream(stream)
+        check(lib().kx_ctx_set_crc32c_check(self._ctx(s).handle, 1 if crc32_check else 0), "set crc32c check")
         fo = torch.zeros(n + 1, dtype=torch.int64, device=self.device)
         kinds = torch.zeros(max(1, n), dtype=torch.uint8, device=self.device)
         args = [self._ctx(s).handle, self.dschema.handle, _ptr(buf), buf.numel(), n]
@@ -439,3 +441,60 @@ def frame_scan(buf, n: int, max_payload: int = 0, device: int = 0, stream=None):
 
 
 _SCAN_CTX = {}
+
+
+def _ctx_for(device, s):
+    key = (device, int(s.cuda_stream))
+    ctx = _SCAN_CTX.get(key)
+    if ctx is None:
+        ctx = _SCAN_CTX[key] = Context(device)
+    return ctx
+
+
+class CRC32PayloadValidator:
+    """crcPayloadValidator (pkg/remote/codec/validate.go:168-217) over batches on the device.
+
+    Generate(buf, offsets) = getCRC32C of each payload buf[offsets[i]:offsets[i+1]] (:187-189, :208-217),
+    as uint32 values (the header value is their big-endian lowercase hex, `hex_value`). ValidateFrames
+    runs payloadChecksumValidate (:91-127) over n TTHeader frames located by frame_scan."""
+
+    KEY = "crc32c"  # transmeta.HeaderCRC32C
+
+    def __init__(self, device: int = 0):
+        self.device = device
+
+    def Key(self) -> str:
+        return self.KEY
+
+    @staticmethod
+    def hex_value(crc: int) -> str:
+        return "%08x" % (crc & 0xFFFFFFFF)
+
+    def Generate(self, buf, offsets, stream=None):
+        """-> int64 tensor of CRC-32C values (0..2^32-1), one per range"""
+        import torch
+        s = _stream(stream)
+        n = offsets.numel() - 1
+        out = torch.zeros(max(1, n), dtype=torch.int32, device=buf.device)
+        st = status_tensor(buf.device)
+        check(lib().kx_crc32c_batch(_ctx_for(self.device, s).handle, _ptr(buf), buf.numel(), _ptr(offsets), n,
+                                    _ptr(out), _ptr(st), int(s.cuda_stream)), "kx_crc32c_batch")
+        stt = read_status(st, s)
+        if stt.code:
+            raise KxError(stt.code, "crc32c generate", stt.record, stt.offset)
+        return out[:n].to(torch.int64) & 0xFFFFFFFF
+
+    def ValidateFrames(self, buf, frame_offsets, n: int, stream=None, raise_on_error: bool = False):
+        """-> (per-frame codes uint8[n], per-frame payload CRC int64[n], kx_status)"""
+        import torch
+        s = _stream(stream)
+        crc = torch.zeros(max(1, n), dtype=torch.int32, device=buf.device)
+        rs = torch.zeros(max(1, n), dtype=torch.uint8, device=buf.device)
+        st = status_tensor(buf.device)
+        check(lib().kx_frame_crc32c_validate(_ctx_for(self.device, s).handle, _ptr(buf), buf.numel(),
+                                             _ptr(frame_offsets), n, _ptr(crc), _ptr(rs), _ptr(st),
+                                             int(s.cuda_stream)), "kx_frame_crc32c_validate")
+        stt = read_status(st, s)
+        if raise_on_error and stt.code:
+            raise ProtocolError(stt.code, "payload validation", stt.record, stt.offset)
+        return rs[:n], crc[:n].to(torch.int64) & 0xFFFFFFFF, stt

@@ -171,6 +171,7 @@ const char* kx_strerror(int code) {
     case KX_ERR_EOF: return "unexpected EOF";
     case KX_ERR_APPLICATION_EXCEPTION: return "application exception message";
     case KX_ERR_UNKNOWN_PROTOCOL: return "unknown protocol (framing sniff)";
+    case KX_ERR_PAYLOAD_VALIDATION: return "payload validation failed (crc32c)";
     case KX_ERR_INVALID_ARG: return "invalid argument";
     case KX_ERR_HIP: return "HIP runtime error";
     case KX_ERR_NO_DEVICE: return "no device";
@@ -244,6 +245,7 @@ void kx_ctx_destroy(kx_ctx* c) {
   if (c->ews) (void)hipFree(c->ews);
   if (c->mws) (void)hipFree(c->mws);
   if (c->fws) (void)hipFree(c->fws);
+  if (c->cws) (void)hipFree(c->cws);
   if (c->pin) (void)hipHostFree(c->pin);
   if (c->dstage) (void)hipFree(c->dstage);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
@@ -391,7 +393,8 @@ static int decode_messages(kx_ctx* c, const kx_schema* s, const uint8_t* in, uin
                            const uint64_t* offsets, uint64_t n, int32_t body_field, bool pb,
                            const kx_column* msg_cols, const kx_columns* out, uint8_t* record_status,
                            kx_status* status, void* stream, const uint64_t* ends = nullptr,
-                           const uint64_t* rep = nullptr, const kx_status* pre = nullptr) {
+                           const uint64_t* rep = nullptr, const kx_status* pre = nullptr,
+                           const uint8_t* pre_rc = nullptr) {
   if (!c || !s || !status || !offsets || (!in && in_len)) return KX_ERR_INVALID_ARG;
   int rc = set_device(c);
   if (rc) return rc;
@@ -423,7 +426,7 @@ static int decode_messages(kx_ctx* c, const kx_schema* s, const uint8_t* in, uin
   uint64_t *rs = nullptr, *re = nullptr;
   uint8_t *hrc = nullptr, *brc = nullptr;
   if ((rc = kx_launch_message_headers(in, in_len, offsets, n, body_field, pb, mo, c->mws, &rs, &re, &hrc, &brc,
-                                      st, ends, pre)))
+                                      st, ends, pre, pre_rc)))
     return rc;
   KxProgram* dp = nullptr;
   if ((rc = prog_on_device(const_cast<kx_schema*>(s), c->device, &dp))) return rc;
@@ -469,6 +472,41 @@ int kx_frame_scan(kx_ctx* c, const uint8_t* in, uint64_t in_len, uint64_t n, uin
                           c->ws_size, epoch, st);
 }
 
+// CRC32C scratch: the launcher's error key (8 bytes, ~0 = none; its final kernel re-arms it)
+static int ensure_cws(kx_ctx* c, hipStream_t stream) {
+  if (c->cws) return KX_OK;
+  KX_HIP_CHECK(hipMalloc(&c->cws, 256));
+  KX_HIP_CHECK(hipMemsetAsync(c->cws, 0xff, 8, stream));
+  return KX_OK;
+}
+
+int kx_crc32c_batch(kx_ctx* c, const uint8_t* in, uint64_t in_len, const uint64_t* offsets, uint64_t n,
+                    uint32_t* crc_out, kx_status* status, void* stream) {
+  if (!c || !status || !offsets || (n && !crc_out) || (!in && in_len)) return KX_ERR_INVALID_ARG;
+  int rc = set_device(c);
+  if (rc) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  if ((rc = ensure_cws(c, st))) return rc;
+  return kx_launch_crc32c(in, in_len, offsets, n, false, nullptr, crc_out, nullptr, status, c->cws, st);
+}
+
+int kx_frame_crc32c_validate(kx_ctx* c, const uint8_t* in, uint64_t in_len, const uint64_t* frame_offsets,
+                             uint64_t n, uint32_t* crc_out, uint8_t* record_status, kx_status* status,
+                             void* stream) {
+  if (!c || !status || !frame_offsets || (!in && in_len)) return KX_ERR_INVALID_ARG;
+  int rc = set_device(c);
+  if (rc) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  if ((rc = ensure_cws(c, st))) return rc;
+  return kx_launch_crc32c(in, in_len, frame_offsets, n, true, nullptr, crc_out, record_status, status, c->cws, st);
+}
+
+int kx_ctx_set_crc32c_check(kx_ctx* c, int enable) {
+  if (!c) return KX_ERR_INVALID_ARG;
+  c->crc32c_check = enable != 0;
+  return KX_OK;
+}
+
 // a socket buffer of n frames -> frame scan -> message headers -> record bodies
 static int decode_frames(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len, uint64_t n,
                          int32_t body_field, bool pb, uint64_t max_payload, uint64_t* frame_offsets, uint8_t* kinds,
@@ -483,17 +521,25 @@ static int decode_frames(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint6
     uint64_t z = 0;
     return decode_messages(c, s, in, in_len, &z, 0, body_field, pb, msg_cols, out, record_status, status, stream);
   }
-  // scratch: [scan status 256 B][frame offsets n + 1][payload starts n + 1][payload ends n]
-  const size_t fo_at = 256, ps_at = fo_at + (n + 1) * 8, pe_at = ps_at + (n + 1) * 8;
-  if ((rc = ensure_fws(c, pe_at + n * 8, st))) return rc;
+  // scratch: [scan status 128 B][crc status 128 B][frame offsets n + 1][payload starts n + 1]
+  //          [payload ends n][crc codes n]
+  const size_t fo_at = 256, ps_at = fo_at + (n + 1) * 8, pe_at = ps_at + (n + 1) * 8, vr_at = pe_at + n * 8;
+  if ((rc = ensure_fws(c, vr_at + n, st))) return rc;
   char* f = (char*)c->fws;
   kx_status* pre = (kx_status*)f;
   uint64_t* fo = frame_offsets ? frame_offsets : (uint64_t*)(f + fo_at);
   uint64_t* ps = (uint64_t*)(f + ps_at);
   uint64_t* pe = (uint64_t*)(f + pe_at);
   if ((rc = kx_frame_scan(c, in, in_len, n, max_payload, fo, ps, pe, kinds, pre, stream))) return rc;
+  uint8_t* vrc = nullptr;
+  if (c->crc32c_check) {  // DecodeMeta's payloadChecksumValidate (default_codec.go:205-209)
+    if ((rc = ensure_cws(c, st))) return rc;
+    vrc = (uint8_t*)(f + vr_at);
+    if ((rc = kx_launch_crc32c(in, in_len, fo, n, true, pre, nullptr, vrc, (kx_status*)(f + 128), c->cws, st)))
+      return rc;
+  }
   return decode_messages(c, s, in, in_len, ps, n, body_field, pb, msg_cols, out, record_status, status, stream, pe,
-                         fo, pre);
+                         fo, pre, vrc);
 }
 
 int kx_thrift_decode_frames(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len, uint64_t n,

@@ -54,6 +54,9 @@ struct kx_ctx {
   // grow-only framing-scan scratch (kx_*_decode_frames): frame offsets, payload extents, scan status
   void* fws = nullptr;
   size_t fws_size = 0;
+  // CRC32C: 256 B scratch (error key), armed at allocation; CRC32Check for kx_*_decode_frames
+  void* cws = nullptr;
+  bool crc32c_check = false;
   // grow-only encode scratch (per-block sizes)
   void* ews = nullptr;
   size_t ews_size = 0;
@@ -117,10 +120,17 @@ int kx_launch_message_headers(const uint8_t* in, uint64_t in_len, const uint64_t
                               int32_t body_field, bool pb, const KxMsgOut& mo, void* mws,
                               uint64_t** req_start, uint64_t** req_end,
                               uint8_t** hdr_rc, uint8_t** body_rc, hipStream_t stream,
-                              const uint64_t* ends = nullptr, const kx_status* pre = nullptr);
+                              const uint64_t* ends = nullptr, const kx_status* pre = nullptr,
+                              const uint8_t* pre_rc = nullptr);
 int kx_launch_message_merge(const uint64_t* offsets, uint64_t n, const uint8_t* hdr_rc, const uint8_t* body_rc,
                             uint8_t* record_status, kx_status* status, void* mws, hipStream_t stream,
                             const kx_status* pre = nullptr);
+
+// kx_crc.hip: CRC-32C of n ranges (val = false: [offs[i], offs[i+1])) or of n TTHeader frames' payloads
+// checked against their "crc32c" header (val = true); scratch = 8-byte error key armed to ~0
+int kx_launch_crc32c(const uint8_t* in, uint64_t in_len, const uint64_t* offs, uint64_t n, bool val,
+                     const kx_status* pre, uint32_t* crc_out, uint8_t* rs, kx_status* status, void* scratch,
+                     hipStream_t stream);
 
 #define KX_HIP_CHECK(x)                       \
   do {                                        \

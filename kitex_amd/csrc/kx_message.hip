@@ -135,6 +135,7 @@ struct MsgParams {
   const uint64_t* offsets;   // n + 1 message boundaries (with ends: n message starts)
   const uint64_t* ends;      // message i ends at ends[i] (framed payloads), else offsets[i + 1]
   const kx_status* pre;      // framing-scan status: messages from its failing frame on are not read
+  const uint8_t* pre_rc;     // per-frame code found before the payload is read (CRC32C validation)
   uint64_t n;
   int32_t body_field;        // 1: Args{1: req}, 0: Result{0: success}
   int pb;                    // Kitex-Protobuf meta header (magic 0x9001, 16-bit type), body = the rest
@@ -163,6 +164,8 @@ __global__ void __launch_bounds__(MT) header_kernel(MsgParams mp) {
   uint64_t rs = p, re = p;
   if (cut) {
     rc = mp.pre->code;  // the frame could not be delimited: neither it nor any later one is decoded
+  } else if (mp.pre_rc && mp.pre_rc[i]) {
+    rc = mp.pre_rc[i];  // DecodeMeta failed (payload checksum): the payload codec never runs
   } else if (p > e || e > mp.in_len) {
     rc = KX_ERR_INVALID_ARG;
   } else if (e - p < 4) {
@@ -327,12 +330,12 @@ size_t kx_message_ws_bytes(uint64_t n) { return msg_ws(n).total; }
 int kx_launch_message_headers(const uint8_t* in, uint64_t in_len, const uint64_t* offsets, uint64_t n,
                               int32_t body_field, bool pb, const KxMsgOut& mo, void* mws, uint64_t** req_start,
                               uint64_t** req_end, uint8_t** hdr_rc, uint8_t** body_rc, hipStream_t stream,
-                              const uint64_t* ends, const kx_status* pre) {
+                              const uint64_t* ends, const kx_status* pre, const uint8_t* pre_rc) {
   const MsgWs L = msg_ws(n);
   char* b = (char*)mws;
   MsgParams mp{};
   mp.in = in; mp.in_len = in_len; mp.offsets = offsets; mp.n = n; mp.body_field = body_field; mp.mo = mo;
-  mp.ends = ends; mp.pre = pre;
+  mp.ends = ends; mp.pre = pre; mp.pre_rc = pre_rc;
   mp.pb = pb;
   mp.req_start = (uint64_t*)(b + L.req_start);
   mp.req_end = (uint64_t*)(b + L.req_end);

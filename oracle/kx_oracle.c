@@ -344,6 +344,107 @@ int kxo_frame_scan(const uint8_t* in, uint64_t in_len, uint64_t n, uint64_t max_
 }
 
 /* ------------------------------------------------------------------------------------------------
+ * CRC32C payload validator: crcPayloadValidator (pkg/remote/codec/validate.go:168-217). getCRC32C
+ * (:208-217) = crc32.Update(0, crc32.MakeTable(crc32.Castagnoli), payload), Go's hash/crc32 (standard
+ * library, not in the reference tree): the reflected CRC-32 over polynomial 0x82F63B78, pre- and
+ * post-inverted. Restated bit by bit (no tables) so that the device's slicing-by-8 tables and chunk
+ * combination are checked against the definition; pinned by the RFC 3720 B.4 / "123456789" check
+ * values in tests/test_oracle_crc.py. kxo_crc32c(crc, p, n) continues crc like crc32.Update.
+ * ---------------------------------------------------------------------------------------------- */
+uint32_t kxo_crc32c(uint32_t crc, const uint8_t* p, uint64_t n) {
+  crc = ~crc;
+  for (uint64_t i = 0; i < n; i++) {
+    crc ^= p[i];
+    for (int k = 0; k < 8; k++) crc = (crc & 1) ? (crc >> 1) ^ 0x82F63B78u : crc >> 1;
+  }
+  return ~crc;
+}
+
+/* Generate over n ranges [offsets[i], offsets[i+1]) (crcPayloadValidator.Generate, :187-189) */
+int kxo_crc32c_batch(const uint8_t* in, uint64_t in_len, const uint64_t* offsets, uint64_t n, uint32_t* crc_out) {
+  int rc = KX_OK;
+  for (uint64_t i = 0; i < n; i++) {
+    uint64_t a = offsets[i], b = offsets[i + 1];
+    if (a > b || b > in_len) { crc_out[i] = 0; if (!rc) rc = KX_ERR_INVALID_ARG; continue; }
+    crc_out[i] = kxo_crc32c(0, in + a, b - a);
+  }
+  return rc;
+}
+
+/* payloadChecksumValidate (:91-127) for one frame at b (DecodeMeta runs it right after the TTHeader,
+ * default_codec.go:205-209): expectedValue = strInfo["crc32c"] (transmeta.HeaderCRC32C; the TTHeader
+ * string-KV info, last pair wins like the map assignment), payload = PayloadLen bytes after the TTHeader
+ * (the Framed length prefix included). Validate (:190-201): "" passes, else hex(BE crc) == value. */
+static int frame_crc_one(const uint8_t* b, uint64_t len, uint32_t* crc) {
+  *crc = 0;
+  if (len < 14 || (be32(b + 4) & KXO_MASK) != 0x10000000u) return KX_OK;  /* not TTHeader: no validator */
+  uint64_t flen = (uint64_t)be32(b) + 4, hs = (uint64_t)be16(b + 12) * 4;
+  if (hs < 2 || 14 + hs > flen || flen > len) return KX_ERR_UNKNOWN_PROTOCOL;
+  const uint8_t* info = b + 14;
+  const uint8_t* want = NULL;
+  uint64_t want_len = 0, i = 2 + (uint64_t)info[1];
+  if (i > hs) return KX_ERR_UNKNOWN_PROTOCOL;
+  while (i < hs) {
+    uint8_t id = info[i++];
+    if (id == 0x00) continue;
+    if (id == 0x01) {
+      if (i + 2 > hs) return KX_ERR_UNKNOWN_PROTOCOL;
+      uint32_t k = be16(info + i);
+      i += 2;
+      for (uint32_t j = 0; j < k; j++) {
+        if (i + 2 > hs) return KX_ERR_UNKNOWN_PROTOCOL;
+        uint64_t kl = be16(info + i);
+        if (i + 2 + kl + 2 > hs) return KX_ERR_UNKNOWN_PROTOCOL;
+        const uint8_t* key = info + i + 2;
+        i += 2 + kl;
+        uint64_t vl = be16(info + i);
+        if (i + 2 + vl > hs) return KX_ERR_UNKNOWN_PROTOCOL;
+        if (kl == 6 && memcmp(key, "crc32c", 6) == 0) { want = info + i + 2; want_len = vl; }
+        i += 2 + vl;
+      }
+    } else if (id == 0x10) {
+      if (i + 2 > hs) return KX_ERR_UNKNOWN_PROTOCOL;
+      uint32_t k = be16(info + i);
+      i += 2;
+      for (uint32_t j = 0; j < k; j++) {
+        if (i + 4 > hs) return KX_ERR_UNKNOWN_PROTOCOL;
+        uint64_t l = be16(info + i + 2);
+        if (i + 4 + l > hs) return KX_ERR_UNKNOWN_PROTOCOL;
+        i += 4 + l;
+      }
+    } else if (id == 0x11) {
+      if (i + 2 > hs) return KX_ERR_UNKNOWN_PROTOCOL;
+      uint64_t l = be16(info + i);
+      if (i + 2 + l > hs) return KX_ERR_UNKNOWN_PROTOCOL;
+      i += 2 + l;
+    } else {
+      return KX_ERR_UNKNOWN_PROTOCOL;
+    }
+  }
+  *crc = kxo_crc32c(0, b + 14 + hs, flen - 14 - hs);
+  if (!want || want_len == 0) return KX_OK;
+  static const char hexd[] = "0123456789abcdef";
+  char real[8];
+  for (int q = 0; q < 8; q++) real[q] = hexd[(*crc >> (28 - 4 * q)) & 15];  /* hex.EncodeToString(BE) */
+  return want_len == 8 && memcmp(real, want, 8) == 0 ? KX_OK : KX_ERR_PAYLOAD_VALIDATION;
+}
+
+int kxo_frame_crc32c_validate(const uint8_t* in, uint64_t in_len, const uint64_t* frame_offsets, uint64_t n,
+                              uint32_t* crc_out, uint8_t* record_status, uint64_t* first_bad) {
+  int first = KX_OK;
+  *first_bad = n;
+  for (uint64_t i = 0; i < n; i++) {
+    uint64_t f = frame_offsets[i];
+    uint32_t crc = 0;
+    int rc = f > in_len ? KX_OK : frame_crc_one(in + f, in_len - f, &crc);
+    if (crc_out) crc_out[i] = rc == KX_ERR_UNKNOWN_PROTOCOL ? 0 : crc;
+    if (record_status) record_status[i] = (uint8_t)rc;
+    if (rc && !first) { first = rc; *first_bad = i; }
+  }
+  return first;
+}
+
+/* ------------------------------------------------------------------------------------------------
  * Schema flattening: depth-first over the IDL, struct fields inlined, a presence bit for every
  * optional / struct / container field (Go represents those as nil-able; struct_tpl.go:405-450).
  * ---------------------------------------------------------------------------------------------- */

@@ -87,6 +87,16 @@ int kxo_pb_decode_mt(const kx_struct_desc* structs, uint32_t nstructs, const uin
 int kxo_pb_encode(const kx_struct_desc* structs, uint32_t nstructs, const kx_columns* in,
                   uint64_t n, uint8_t* out, uint64_t cap, uint64_t* offsets_out, uint64_t* total);
 
+/* -------- framing sniff and CRC32C payload validation (default_codec.go, validate.go) -------- */
+int kxo_frame_one(const uint8_t* b, uint64_t len, uint64_t max_payload, uint64_t* flen, uint64_t* ps,
+                  uint64_t* pe, uint8_t* kind);
+int kxo_frame_scan(const uint8_t* in, uint64_t in_len, uint64_t n, uint64_t max_payload, uint64_t* frame_offsets,
+                   uint64_t* pay_start, uint64_t* pay_end, uint8_t* kinds, uint64_t* n_done);
+uint32_t kxo_crc32c(uint32_t crc, const uint8_t* p, uint64_t n);
+int kxo_crc32c_batch(const uint8_t* in, uint64_t in_len, const uint64_t* offsets, uint64_t n, uint32_t* crc_out);
+int kxo_frame_crc32c_validate(const uint8_t* in, uint64_t in_len, const uint64_t* frame_offsets, uint64_t n,
+                              uint32_t* crc_out, uint8_t* record_status, uint64_t* first_bad);
+
 /* -------- synthetic inputs: splitmix64 -------- */
 uint64_t kxo_splitmix64(uint64_t x);
 

@@ -65,6 +65,10 @@ def lib():
         L.kxo_skip_batch.argtypes = [vp, sz, C.c_uint64, vp, C.POINTER(C.c_uint64)]
         L.kxo_frame_scan.argtypes = [vp, C.c_uint64, C.c_uint64, C.c_uint64, vp, vp, vp, vp,
                                      C.POINTER(C.c_uint64)]
+        L.kxo_crc32c.argtypes = [C.c_uint32, vp, C.c_uint64]
+        L.kxo_crc32c.restype = C.c_uint32
+        L.kxo_crc32c_batch.argtypes = [vp, C.c_uint64, vp, C.c_uint64, vp]
+        L.kxo_frame_crc32c_validate.argtypes = [vp, C.c_uint64, vp, C.c_uint64, vp, vp, C.POINTER(C.c_uint64)]
         L.kxo_flatten.argtypes = [sdp, C.c_uint32, C.POINTER(A.ColumnInfo), C.POINTER(C.c_uint32),
                                   C.POINTER(C.c_uint32)]
         dec = [sdp, C.c_uint32, vp, C.c_uint64, vp, C.c_uint64, C.POINTER(A.Columns), vp,
@@ -137,6 +141,33 @@ def frame_scan(data: np.ndarray, n: int, max_payload: int = 0):
     rc = lib().kxo_frame_scan(data.ctypes.data, data.size, n, max_payload, fo.ctypes.data, ps.ctypes.data,
                               pe.ctypes.data, kd.ctypes.data, C.byref(done))
     return rc, fo, ps[:n], pe[:n], kd[:n], done.value
+
+
+def crc32c(data: bytes, crc: int = 0) -> int:
+    """crc32.Update(crc, Castagnoli, data) (validate.go:208-217 getCRC32C with crc = 0)"""
+    buf = np.frombuffer(bytes(data), dtype=np.uint8)
+    return lib().kxo_crc32c(crc, buf.ctypes.data if buf.size else None, buf.size)
+
+
+def crc32c_batch(data: np.ndarray, offsets: np.ndarray):
+    """rc, CRC-32C of each range [offsets[i], offsets[i+1])"""
+    n = offsets.size - 1
+    out = np.zeros(max(1, n), dtype=np.uint32)
+    offs = np.ascontiguousarray(offsets, dtype=np.uint64)
+    rc = lib().kxo_crc32c_batch(data.ctypes.data if data.size else None, data.size, offs.ctypes.data, n,
+                                out.ctypes.data)
+    return rc, out[:n]
+
+
+def frame_crc32c_validate(data: np.ndarray, frame_offsets: np.ndarray, n: int):
+    """rc, per-frame CRC-32C of the TTHeader payload, per-frame codes, first failing frame (n: none)"""
+    crc = np.zeros(max(1, n), dtype=np.uint32)
+    rs = np.zeros(max(1, n), dtype=np.uint8)
+    first = C.c_uint64()
+    fo = np.ascontiguousarray(frame_offsets, dtype=np.uint64)
+    rc = lib().kxo_frame_crc32c_validate(data.ctypes.data if data.size else None, data.size, fo.ctypes.data, n,
+                                         crc.ctypes.data, rs.ctypes.data, C.byref(first))
+    return rc, crc[:n], rs[:n], first.value
 
 
 def flatten(schema: Schema) -> Tuple[int, List[A.ColumnInfo], int]:

@@ -20,6 +20,8 @@ sed -e 's/^#define LDS __attribute__((address_space(3)))/#define LDS/' \
 CXX=${CXX:-/opt/rocm/lib/llvm/bin/clang++}
 FLAGS="-std=c++17 -O1 -g -fPIC -Wno-unknown-attributes -Wno-unused-function -I. -I$ROOT/kitex_amd/csrc ${EMU_EXTRA:-}"
 $CXX $FLAGS -c _build/kx_decode_emu.cpp -o _build/kx_decode_emu.o
+cp $ROOT/kitex_amd/csrc/kx_crc.hip _build/kx_crc_emu.cpp
+$CXX $FLAGS -c _build/kx_crc_emu.cpp -o _build/kx_crc_emu.o
 $CXX $FLAGS -c $ROOT/kitex_amd/csrc/kx_schema.cpp -o _build/kx_schema.o
 $CXX $FLAGS -c emu_rt.cpp -o _build/emu_rt.o
 $CXX $FLAGS -c emu_driver.cpp -o _build/emu_driver.o

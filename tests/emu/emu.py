@@ -20,13 +20,18 @@ def build():
 def lib():
     global _lib
     if _lib is None:
-        src = os.path.join(HERE, "..", "..", "kitex_amd", "csrc", "kx_decode.hip")
-        if not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(src):
+        csrc = os.path.join(HERE, "..", "..", "kitex_amd", "csrc")
+        srcs = [os.path.join(csrc, f) for f in ("kx_decode.hip", "kx_crc.hip")] + \
+            [os.path.join(HERE, f) for f in ("emu_driver.cpp", "emu_rt.cpp", os.path.join("hip", "hip_runtime.h"))]
+        if not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(f) for f in srcs):
             build()
         _lib = C.CDLL(LIB)
         _lib.emu_decode.restype = C.c_int
         _lib.emu_decode.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64,
                                     C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]
+        _lib.emu_crc.restype = C.c_int
+        _lib.emu_crc.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_int, C.c_void_p, C.c_void_p,
+                                 C.c_void_p]
         _lib.emu_frames.restype = C.c_int
         _lib.emu_frames.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint64] + [C.c_void_p] * 5
     return _lib
@@ -67,3 +72,16 @@ def frames(data: np.ndarray, n: int, max_payload: int = 0, threads: int = 8):
     rc = lib().emu_frames(data.ctypes.data, data.size, n, max_payload, fo.ctypes.data, ps.ctypes.data,
                           pe.ctypes.data, kd.ctypes.data, C.addressof(st))
     return rc, fo, ps[:n], pe[:n], kd[:n], st
+
+
+def crc32c(data: np.ndarray, offs: np.ndarray, n: int, val: bool, threads: int = 8):
+    """the CRC32C kernel source: crc per range (val=False) or per TTHeader frame (val=True), codes, status"""
+    os.environ["KX_EMU_THREADS"] = str(threads)
+    crc = np.zeros(max(1, n), dtype=np.uint32)
+    rs = np.zeros(max(1, n), dtype=np.uint8)
+    st = A.Status()
+    o = np.ascontiguousarray(offs, dtype=np.uint64)
+    rc = lib().emu_crc(data.ctypes.data if data.size else None, data.size, o.ctypes.data, n, 1 if val else 0,
+                       crc.ctypes.data, rs.ctypes.data, C.addressof(st))
+    assert rc == 0, rc
+    return crc[:n], rs[:n], st

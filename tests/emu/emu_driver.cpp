@@ -81,3 +81,10 @@ extern "C" int emu_frames(const uint8_t* in, uint64_t in_len, uint64_t n, uint64
   status->diag[0] = status->diag[1] = 0;
   return kx_launch_frames(in, in_len, n, max_payload, fo, ps, pe, kinds, status, ws, ws_cap, epoch, nullptr);
 }
+
+// CRC32C kernel source (kx_crc.hip): val = 0 ranges [offs[i], offs[i+1]), 1 TTHeader frames at offs[i]
+extern "C" int emu_crc(const uint8_t* in, uint64_t in_len, const uint64_t* offs, uint64_t n, int val,
+                       uint32_t* crc_out, uint8_t* rs, kx_status* status) {
+  static unsigned long long errkey = ~0ull;
+  return kx_launch_crc32c(in, in_len, offs, n, val != 0, nullptr, crc_out, rs, status, &errkey, nullptr);
+}

@@ -66,3 +66,26 @@ def assert_columns_equal(got, exp, infos, n, check_presence=True):
     if check_presence and exp.presence is not None:
         assert got.presence is not None
         assert np.array_equal(to_np(got.presence)[:n].view(np.uint64), to_np(exp.presence)[:n].view(np.uint64))
+
+
+def assert_rows_equal(got, exp, infos, rows):
+    """got's records `rows` equal exp's records 0..len(rows)-1 (FIXED and BYTES columns)."""
+    rows = np.asarray(rows, dtype=np.int64)
+    m = rows.size
+    for c, ci in enumerate(infos):
+        if ci.kind == A.COL_FIXED:
+            g = to_np(got.cols[c]).view(np.uint8).reshape(len(to_np(got.cols[c])), -1)[rows]
+            e = to_np(exp.cols[c])[:m].view(np.uint8).reshape(m, -1)
+            bad = np.nonzero((g != e).any(axis=1))[0]
+            assert bad.size == 0, f"column {c} (field {ci.field_id}) differs at rows {rows[bad[:8]]}"
+        elif ci.kind == A.COL_BYTES:
+            go, gd = (to_np(v) for v in got.cols[c])
+            eo, ed = (to_np(v) for v in exp.cols[c])
+            go, eo = offsets_u64(go), offsets_u64(eo)
+            gd, ed = gd.view(np.uint8), ed.view(np.uint8)
+            for k, r in enumerate(rows):
+                a = gd[int(go[r]):int(go[r + 1])]
+                b = ed[int(eo[k]):int(eo[k + 1])]
+                assert np.array_equal(a, b), f"var column {c} (field {ci.field_id}) differs at row {r}"
+        else:
+            raise NotImplementedError(ci.kind)
