@@ -35,6 +35,8 @@
  *                                 183-217) over N payloads
  *   kx_frame_crc32c_validate .... payloadChecksumValidate + crcPayloadValidator.Validate (validate.go:91-127,
  *                                 190-201) of N TTHeader frames, as DecodeMeta runs it (default_codec.go:205-209)
+ *   kx_grpc_frame_scan .......... decodeGRPCFrame (pkg/remote/codec/grpc/grpc_compress.go:37-60) over N
+ *                                 messages; kx_*_decode_grpc = grpcCodec.Decode bodies (grpc.go:202-270)
  *   kx_ctx_set_crc32c_check ..... CodecConfig{CRC32Check: true} (default_codec.go:70-92) for kx_*_decode_frames
  *   kx_strerror ................. error text; codes mirror pkg/remote/codec/perrors/protocol_error.go:28-36
  */
@@ -313,6 +315,28 @@ int kx_thrift_decode_frames(kx_ctx* c, const kx_schema* s, const uint8_t* in, ui
 int kx_pb_decode_frames(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len, uint64_t n,
                         uint64_t max_payload, uint64_t* frame_offsets, uint8_t* kinds, const kx_column* msg_cols,
                         const kx_columns* out, uint8_t* record_status, kx_status* status, void* stream);
+
+/* ---- gRPC length-prefixed messages (decodeGRPCFrame, pkg/remote/codec/grpc/grpc_compress.go:37-60;
+ *      grpcCodec.Decode, grpc.go:202-260) ----
+ * in = n messages back to back, each [u8 compressed flag][u32 BE length][payload] (the DATA frames of one
+ * stream, HTTP/2 framing already removed). kx_grpc_frame_scan: frame_offsets (n + 1), payload
+ * [payload_start[i], payload_end[i]) (the 5-byte prefix removed), flags[i] (optional) = the compressed-flag
+ * byte; boundaries found in parallel on the device; a message cut short is KX_ERR_EOF, a payload longer
+ * than max_payload (> 0) KX_ERR_INVALID_DATA; status as kx_frame_scan.
+ * kx_thrift_decode_grpc / kx_pb_decode_grpc: scan, then each payload decoded as one record
+ * (thrift.UnmarshalThriftData -> fastUnmarshal with dataLen = the payload, grpc.go:241-249; proto.Unmarshal
+ * of the payload, :251-270). A compressed message (flag 1) gets KX_ERR_NOT_IMPLEMENTED (no decompressor
+ * on the device: the reference's "kitex compression algorithm not found" when none is registered);
+ * record_status / status as kx_*_decode_frames. */
+int kx_grpc_frame_scan(kx_ctx* c, const uint8_t* in, uint64_t in_len, uint64_t n, uint64_t max_payload,
+                       uint64_t* frame_offsets, uint64_t* payload_start, uint64_t* payload_end, uint8_t* flags,
+                       kx_status* status, void* stream);
+int kx_thrift_decode_grpc(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len, uint64_t n,
+                          uint64_t max_payload, uint64_t* frame_offsets, const kx_columns* out,
+                          uint8_t* record_status, kx_status* status, void* stream);
+int kx_pb_decode_grpc(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len, uint64_t n,
+                      uint64_t max_payload, uint64_t* frame_offsets, const kx_columns* out, uint8_t* record_status,
+                      kx_status* status, void* stream);
 
 /* ---- CRC32C payload checksums (crcPayloadValidator, pkg/remote/codec/validate.go:168-217) ----
  * CRC-32C = crc32.Update(0, crc32.MakeTable(crc32.Castagnoli), payload) (getCRC32C, :208-217); the

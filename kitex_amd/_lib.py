@@ -26,6 +26,7 @@ EXPORTS = [
     "kx_thrift_decode_messages", "kx_pb_decode_messages", "kx_pb_meta_length", "kx_pb_write_meta",
     "kx_pb_read_meta", "kx_ctx_set_pipeline", "kx_frame_scan", "kx_thrift_decode_frames",
     "kx_pb_decode_frames", "kx_crc32c_batch", "kx_frame_crc32c_validate", "kx_ctx_set_crc32c_check",
+    "kx_grpc_frame_scan", "kx_thrift_decode_grpc", "kx_pb_decode_grpc",
 ]
 
 
@@ -97,6 +98,9 @@ def lib():
     L.kx_crc32c_batch.argtypes = [vp, vp, u64, vp, u64, vp, vp, vp]
     L.kx_frame_crc32c_validate.argtypes = [vp, vp, u64, vp, u64, vp, vp, vp, vp]
     L.kx_ctx_set_crc32c_check.argtypes = [vp, C.c_int]
+    L.kx_grpc_frame_scan.argtypes = L.kx_frame_scan.argtypes
+    L.kx_thrift_decode_grpc.argtypes = [vp, vp, vp, u64, u64, u64, vp, C.POINTER(A.Columns), vp, vp, vp]
+    L.kx_pb_decode_grpc.argtypes = L.kx_thrift_decode_grpc.argtypes
     L.kx_pb_meta_length.argtypes = [u32]
     L.kx_pb_meta_length.restype = u64
     L.kx_pb_write_meta.argtypes = L.kx_thrift_write_message_begin.argtypes

@@ -232,6 +232,7 @@ class ThriftCodec:
 
     _MESSAGES = "kx_thrift_decode_messages"
     _FRAMES = "kx_thrift_decode_frames"
+    _GRPC = "kx_thrift_decode_grpc"
 
     def UnmarshalMessages(self, buf, n: int, offsets, body_field: int = 1, out: ColumnSet = None,
                           var_caps: Sequence[int] = None, name_cap: int = None, stream=None,
@@ -264,6 +265,35 @@ class ThriftCodec:
         args += [max_payload, _ptr(fo), _ptr(kinds)]
         res = self._messages(self._FRAMES, args, buf, n, out, var_caps, name_cap, s, raise_on_error)
         res.frame_offsets, res.kinds = fo, kinds[:n]
+        return res
+
+    def UnmarshalGRPC(self, buf, n: int, max_payload: int = 0, out: ColumnSet = None,
+                      var_caps: Sequence[int] = None, stream=None, raise_on_error: bool = True) -> "DecodeResult":
+        """grpcCodec.Decode (pkg/remote/codec/grpc/grpc.go:202-270) over n gRPC messages back to back
+        ([u8 compressed][u32 BE length][payload], decodeGRPCFrame grpc_compress.go:37-60): each payload is
+        one record. The result also carries frame_offsets (int64[n+1]); a compressed message's code is
+        ERR_NOT_IMPLEMENTED (no decompressor on the device)."""
+        import torch
+        s = _stream(stream)
+        ds = self.dschema
+        if out is None:
+            if var_caps is None:
+                var_caps = [0 if ci.kind == A.COL_FIXED else max(1, buf.numel()) for ci in ds.infos]
+            out = alloc_device(ds.infos, n, var_caps, ds.npresence, self.device)
+        kc = to_kx_columns(out, ds.infos, var_caps)
+        fo = torch.zeros(n + 1, dtype=torch.int64, device=self.device)
+        st = status_tensor(self.device)
+        rs = torch.empty(max(1, n), dtype=torch.uint8, device=self.device)
+        fn = self._GRPC
+        rc = getattr(lib(), fn)(self._ctx(s).handle, ds.handle, _ptr(buf), buf.numel(), n, max_payload, _ptr(fo),
+                                C.byref(kc), _ptr(rs), _ptr(st), int(s.cuda_stream))
+        check(rc, fn)
+        res = DecodeResult(out, st, rs, s)
+        res.frame_offsets = fo
+        if raise_on_error:
+            stt = res.read_status()
+            if stt.code:
+                raise ProtocolError(stt.code, self._WHAT, stt.record, stt.offset)
         return res
 
     def _messages(self, fn, args, buf, n, out, var_caps, name_cap, s, raise_on_error):
@@ -363,6 +393,7 @@ class ProtobufCodec(ThriftCodec):
     _HOST = "kx_host_pb_decode_batch"
     _MESSAGES = "kx_pb_decode_messages"
     _FRAMES = "kx_pb_decode_frames"
+    _GRPC = "kx_pb_decode_grpc"
     _ENCODE = "kx_pb_encode_batch"
     _SIZE = "kx_pb_encoded_size_batch"
     _WHAT = "protobuf unmarshal"
@@ -418,6 +449,23 @@ def read_pb_meta(data: bytes):
         raise ProtocolError(rc, "pb read meta")
     off = C.cast(name, C.c_void_p).value - C.addressof(arr)
     return bytes(data[off:off + nl.value]).decode(), t.value, s.value, u.value
+
+
+def grpc_frame_scan(buf, n: int, max_payload: int = 0, device: int = 0, stream=None):
+    """kx_grpc_frame_scan over a device buffer of n gRPC messages. Returns (frame offsets int64[n+1],
+    payload starts int64[n], payload ends int64[n], compressed flags uint8[n], status tensor)."""
+    import torch
+    dev = torch.device("cuda", device)
+    s = _stream(stream)
+    ctx = _ctx_for(device, s)
+    fo = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    ps = torch.zeros(max(1, n), dtype=torch.int64, device=dev)
+    pe = torch.zeros(max(1, n), dtype=torch.int64, device=dev)
+    fl = torch.zeros(max(1, n), dtype=torch.uint8, device=dev)
+    st = status_tensor(dev)
+    check(lib().kx_grpc_frame_scan(ctx.handle, _ptr(buf), buf.numel(), n, max_payload, _ptr(fo), _ptr(ps),
+                                   _ptr(pe), _ptr(fl), _ptr(st), int(s.cuda_stream)), "kx_grpc_frame_scan")
+    return fo, ps[:n], pe[:n], fl[:n], st
 
 
 def frame_scan(buf, n: int, max_payload: int = 0, device: int = 0, stream=None):

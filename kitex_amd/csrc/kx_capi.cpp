@@ -394,7 +394,8 @@ static int decode_messages(kx_ctx* c, const kx_schema* s, const uint8_t* in, uin
                            const kx_column* msg_cols, const kx_columns* out, uint8_t* record_status,
                            kx_status* status, void* stream, const uint64_t* ends = nullptr,
                            const uint64_t* rep = nullptr, const kx_status* pre = nullptr,
-                           const uint8_t* pre_rc = nullptr) {
+                           const uint8_t* pre_rc = nullptr, const uint8_t* raw_flags = nullptr,
+                           bool raw = false) {
   if (!c || !s || !status || !offsets || (!in && in_len)) return KX_ERR_INVALID_ARG;
   int rc = set_device(c);
   if (rc) return rc;
@@ -426,7 +427,7 @@ static int decode_messages(kx_ctx* c, const kx_schema* s, const uint8_t* in, uin
   uint64_t *rs = nullptr, *re = nullptr;
   uint8_t *hrc = nullptr, *brc = nullptr;
   if ((rc = kx_launch_message_headers(in, in_len, offsets, n, body_field, pb, mo, c->mws, &rs, &re, &hrc, &brc,
-                                      st, ends, pre, pre_rc)))
+                                      st, ends, pre, pre_rc, raw_flags, raw)))
     return rc;
   KxProgram* dp = nullptr;
   if ((rc = prog_on_device(const_cast<kx_schema*>(s), c->device, &dp))) return rc;
@@ -540,6 +541,64 @@ static int decode_frames(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint6
   }
   return decode_messages(c, s, in, in_len, ps, n, body_field, pb, msg_cols, out, record_status, status, stream, pe,
                          fo, pre, vrc);
+}
+
+int kx_grpc_frame_scan(kx_ctx* c, const uint8_t* in, uint64_t in_len, uint64_t n, uint64_t max_payload,
+                       uint64_t* frame_offsets, uint64_t* payload_start, uint64_t* payload_end, uint8_t* flags,
+                       kx_status* status, void* stream) {
+  if (!c || !status || !frame_offsets || (n && (!payload_start || !payload_end)) || (!in && in_len))
+    return KX_ERR_INVALID_ARG;
+  int rc = set_device(c);
+  if (rc) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  if (n == 0) {
+    KX_HIP_CHECK(hipMemsetAsync(status, 0, sizeof(kx_status), st));
+    KX_HIP_CHECK(hipMemsetAsync(frame_offsets, 0, 8, st));
+    return KX_OK;
+  }
+  uint64_t epoch = 0;
+  if ((rc = ensure_ws(c, kx_skip_ws_bytes(in_len), st, &epoch))) return rc;
+  return kx_launch_frames(in, in_len, n, max_payload, frame_offsets, payload_start, payload_end, flags, status, c->ws,
+                          c->ws_size, epoch, st, true);
+}
+
+// n gRPC messages -> framing scan -> bodies (no message header: the payload is the record)
+static int decode_grpc(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len, uint64_t n, bool pb,
+                       uint64_t max_payload, uint64_t* frame_offsets, const kx_columns* out, uint8_t* record_status,
+                       kx_status* status, void* stream) {
+  if (!c || !s || !status || (!in && in_len)) return KX_ERR_INVALID_ARG;
+  int rc = set_device(c);
+  if (rc) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  if (n == 0) {
+    if (frame_offsets) KX_HIP_CHECK(hipMemsetAsync(frame_offsets, 0, 8, st));
+    uint64_t z = 0;
+    return decode_messages(c, s, in, in_len, &z, 0, 0, pb, nullptr, out, record_status, status, stream);
+  }
+  // scratch: [scan status 256 B][frame offsets n + 1][payload starts n + 1][payload ends n][flags n]
+  const size_t fo_at = 256, ps_at = fo_at + (n + 1) * 8, pe_at = ps_at + (n + 1) * 8, fl_at = pe_at + n * 8;
+  if ((rc = ensure_fws(c, fl_at + n, st))) return rc;
+  char* f = (char*)c->fws;
+  kx_status* pre = (kx_status*)f;
+  uint64_t* fo = frame_offsets ? frame_offsets : (uint64_t*)(f + fo_at);
+  uint64_t* ps = (uint64_t*)(f + ps_at);
+  uint64_t* pe = (uint64_t*)(f + pe_at);
+  uint8_t* fl = (uint8_t*)(f + fl_at);
+  if ((rc = kx_grpc_frame_scan(c, in, in_len, n, max_payload, fo, ps, pe, fl, pre, stream))) return rc;
+  return decode_messages(c, s, in, in_len, ps, n, 0, pb, nullptr, out, record_status, status, stream, pe, fo, pre,
+                         nullptr, fl, true);
+}
+
+int kx_thrift_decode_grpc(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len, uint64_t n,
+                          uint64_t max_payload, uint64_t* frame_offsets, const kx_columns* out,
+                          uint8_t* record_status, kx_status* status, void* stream) {
+  return decode_grpc(c, s, in, in_len, n, false, max_payload, frame_offsets, out, record_status, status, stream);
+}
+
+int kx_pb_decode_grpc(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len, uint64_t n,
+                      uint64_t max_payload, uint64_t* frame_offsets, const kx_columns* out, uint8_t* record_status,
+                      kx_status* status, void* stream) {
+  return decode_grpc(c, s, in, in_len, n, true, max_payload, frame_offsets, out, record_status, status, stream);
 }
 
 int kx_thrift_decode_frames(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len, uint64_t n,

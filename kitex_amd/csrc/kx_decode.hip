@@ -81,6 +81,7 @@ struct DecParams {
   uint64_t* fr_pe;
   uint8_t* fr_kind;
   uint64_t fr_max;           // M_FRAME: payload size limit (0: none)
+  int fr_grpc;               // M_FRAME: gRPC length-prefixed messages instead of the default-codec sniff
   uint64_t* tdesc;           // tile words
   uint64_t* gdesc;           // group words
   uint16_t* starts;          // concatenated mode: record starts per tile (slotcap slots each)
@@ -1375,6 +1376,23 @@ __device__ __forceinline__ int frame_one(const Src& w, uint64_t pos, uint64_t li
   return KX_OK;
 }
 
+// gRPC message (decodeGRPCFrame, pkg/remote/codec/grpc/grpc_compress.go:37-60): u8 compressed flag,
+// u32 BE length, payload. kind = the flag byte (1 = compressed; the reference treats every other value as
+// uncompressed). A payload over maxp (> 0) is INVALID_DATA.
+__device__ __forceinline__ int frame_grpc(const Src& w, uint64_t pos, uint64_t lim, uint64_t maxp, uint64_t* end,
+                                          uint64_t& ps, uint64_t& pe, uint32_t& kind) {
+  if (pos > lim || lim - pos < 5) return KX_ERR_EOF;  // in.Next(5)
+  const uint64_t len = ((uint64_t)ld1(w, pos + 1) << 24) | ((uint64_t)ld1(w, pos + 2) << 16) |
+                       ((uint64_t)ld1(w, pos + 3) << 8) | ld1(w, pos + 4);
+  if (len > lim - pos - 5) return KX_ERR_EOF;  // in.Next(dLen)
+  if (maxp && len > maxp) return KX_ERR_INVALID_DATA;
+  kind = ld1(w, pos);
+  ps = pos + 5;
+  pe = pos + 5 + len;
+  *end = pe;
+  return KX_OK;
+}
+
 // One record: FastRead (emit) or its length / var extents only (measure).
 template <int NV, int MODE>
 __device__ __forceinline__ int parse_record(KParams& dp, const Src& w, uint64_t pos, uint64_t lim, uint64_t r,
@@ -1414,7 +1432,8 @@ __device__ __forceinline__ int parse_record(KParams& dp, const Src& w, uint64_t 
   if (MODE == M_FRAME) {
     uint64_t ps, pe;
     uint32_t kind;
-    const int rc = frame_one(w, pos, lim, dp.fr_max, end, ps, pe, kind);
+    const int rc = dp.fr_grpc ? frame_grpc(w, pos, lim, dp.fr_max, end, ps, pe, kind)
+                              : frame_one(w, pos, lim, dp.fr_max, end, ps, pe, kind);
     if (emit && !rc) {
       dp.fr_ps[r] = ps;
       dp.fr_pe[r] = pe;
@@ -1458,8 +1477,34 @@ struct Cand {
 // M_FRAME candidates: positions that start a frame of the batch's first frame's class (batches from
 // one connection are homogeneous; frames of another class are still reached by the chain walk)
 __device__ __forceinline__ uint64_t frame_scan_segment(KParams& dp, const Src& w, uint64_t lo, uint64_t hi) {
-  if (dp.in_len < 8) return lo < hi && lo == 0 ? 0 : X_NONE;
   const GLB uint8_t* g = (const GLB uint8_t*)dp.in;
+  if (dp.fr_grpc) {
+    // gRPC: the first message's flag byte, the top byte of its length, and the first (up to) 3 bytes of
+    // its payload (records of one stream start alike: the Thrift field header / proto tag)
+    if (dp.in_len < 5) return lo < hi && lo == 0 ? 0 : X_NONE;
+    const uint32_t f0 = __builtin_amdgcn_readfirstlane((uint32_t)g[0]);
+    const uint32_t l0 = __builtin_amdgcn_readfirstlane(((uint32_t)g[1] << 24) | ((uint32_t)g[2] << 16) |
+                                                       ((uint32_t)g[3] << 8) | g[4]);
+    const uint32_t np = l0 < 3 ? l0 : 3u;
+    const uint32_t nb = dp.in_len - 5 < np ? 0u : np;
+    uint32_t sig = 0;
+    for (uint32_t k = 0; k < nb; k++) sig |= (uint32_t)g[5 + k] << (8 * k);
+    sig = __builtin_amdgcn_readfirstlane(sig);
+    const uint64_t plim = kmin64(hi, dp.in_len - 4);
+    for (uint64_t p = lo; p < plim; p++) {
+      if (ld1(w, p) != f0 || ld1(w, p + 1) != (l0 >> 24)) continue;
+      const uint64_t l = be32(w, p + 1);
+      if (l + 5 > dp.in_len - p || (l < nb && l != l0)) continue;
+      if (l >= nb) {
+        uint32_t s2 = 0;
+        for (uint32_t k = 0; k < nb; k++) s2 |= ld1(w, p + 5 + k) << (8 * k);
+        if (s2 != sig) continue;
+      }
+      return p;
+    }
+    return X_NONE;
+  }
+  if (dp.in_len < 8) return lo < hi && lo == 0 ? 0 : X_NONE;
   const uint32_t a0 = __builtin_amdgcn_readfirstlane(((uint32_t)g[0] << 24) | ((uint32_t)g[1] << 16) |
                                                      ((uint32_t)g[2] << 8) | g[3]);
   const uint32_t c0 = __builtin_amdgcn_readfirstlane(((uint32_t)g[4] << 24) | ((uint32_t)g[5] << 16) |
@@ -2589,12 +2634,13 @@ int kx_launch_skip(const uint8_t* in, uint64_t in_len, uint64_t n, uint64_t* off
 
 int kx_launch_frames(const uint8_t* in, uint64_t in_len, uint64_t n, uint64_t max_payload, uint64_t* frame_offsets,
                      uint64_t* pay_start, uint64_t* pay_end, uint8_t* kinds, kx_status* status, void* ws,
-                     size_t ws_size, uint64_t epoch, hipStream_t stream) {
+                     size_t ws_size, uint64_t epoch, hipStream_t stream, bool grpc) {
   DecParams dp{};
   fill_diag_flags(dp);
   dp.in = in; dp.in_len = in_len; dp.offsets = nullptr; dp.n = n; dp.prog = nullptr;
   dp.status = status; dp.skip_out = frame_offsets; dp.epoch = epoch;
   dp.fr_ps = pay_start; dp.fr_pe = pay_end; dp.fr_kind = kinds; dp.fr_max = max_payload;
+  dp.fr_grpc = grpc ? 1 : 0;
   dp.krec = 64;
   const WsLayout L = ws_layout(1, in_len, nullptr, n);
   if (ws_size < L.total) return KX_ERR_INVALID_ARG;

@@ -98,7 +98,7 @@ int kx_launch_skip(const uint8_t* in, uint64_t in_len, uint64_t n, uint64_t* off
 size_t kx_skip_ws_bytes(uint64_t in_len);
 int kx_launch_frames(const uint8_t* in, uint64_t in_len, uint64_t n, uint64_t max_payload, uint64_t* frame_offsets,
                      uint64_t* pay_start, uint64_t* pay_end, uint8_t* kinds, kx_status* status, void* ws,
-                     size_t ws_size, uint64_t epoch, hipStream_t stream);
+                     size_t ws_size, uint64_t epoch, hipStream_t stream, bool grpc = false);
 
 int kx_launch_encode(const KxProgram* dprog, const KxProgram& hprog, const KxLaunchCols& cols,
                      uint64_t n, uint8_t* out, uint64_t out_cap, uint64_t* sizes_out,
@@ -121,7 +121,8 @@ int kx_launch_message_headers(const uint8_t* in, uint64_t in_len, const uint64_t
                               uint64_t** req_start, uint64_t** req_end,
                               uint8_t** hdr_rc, uint8_t** body_rc, hipStream_t stream,
                               const uint64_t* ends = nullptr, const kx_status* pre = nullptr,
-                              const uint8_t* pre_rc = nullptr);
+                              const uint8_t* pre_rc = nullptr, const uint8_t* raw_flags = nullptr,
+                              bool raw = false);
 int kx_launch_message_merge(const uint64_t* offsets, uint64_t n, const uint8_t* hdr_rc, const uint8_t* body_rc,
                             uint8_t* record_status, kx_status* status, void* mws, hipStream_t stream,
                             const kx_status* pre = nullptr);

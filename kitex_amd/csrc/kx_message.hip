@@ -139,6 +139,8 @@ struct MsgParams {
   uint64_t n;
   int32_t body_field;        // 1: Args{1: req}, 0: Result{0: success}
   int pb;                    // Kitex-Protobuf meta header (magic 0x9001, 16-bit type), body = the rest
+  const uint8_t* raw_flags;  // raw mode (gRPC): no message header, the body is the whole payload;
+  int raw;                   // a message whose compressed flag is 1 cannot be decoded here
   KxMsgOut mo;
   uint64_t* req_start;       // n + 1 (req_start[n] = in_len)
   uint64_t* req_end;
@@ -168,6 +170,11 @@ __global__ void __launch_bounds__(MT) header_kernel(MsgParams mp) {
     rc = mp.pre_rc[i];  // DecodeMeta failed (payload checksum): the payload codec never runs
   } else if (p > e || e > mp.in_len) {
     rc = KX_ERR_INVALID_ARG;
+  } else if (mp.raw) {
+    // decodeGRPCFrame (grpc_compress.go:53-58): a compressed message needs a registered decompressor
+    if (mp.raw_flags && mp.raw_flags[i] == 1) rc = KX_ERR_NOT_IMPLEMENTED;
+    rs = p;
+    re = e;
   } else if (e - p < 4) {
     rc = KX_ERR_EOF;
   } else {
@@ -187,7 +194,8 @@ __global__ void __launch_bounds__(MT) header_kernel(MsgParams mp) {
     }
   }
   if (!rc && type == KX_MSG_EXCEPTION) rc = KX_ERR_APPLICATION_EXCEPTION;
-  if (!rc && mp.pb) {  // protobuf.go:136-165: the body is the rest of the payload
+  if (mp.raw) {
+  } else if (!rc && mp.pb) {  // protobuf.go:136-165: the body is the rest of the payload
     rs = p + 12 + (uint64_t)nl;
     re = e;
   } else if (!rc) {  // the Args / Result struct: fields until STOP, the record field kept, the rest skipped
@@ -330,12 +338,14 @@ size_t kx_message_ws_bytes(uint64_t n) { return msg_ws(n).total; }
 int kx_launch_message_headers(const uint8_t* in, uint64_t in_len, const uint64_t* offsets, uint64_t n,
                               int32_t body_field, bool pb, const KxMsgOut& mo, void* mws, uint64_t** req_start,
                               uint64_t** req_end, uint8_t** hdr_rc, uint8_t** body_rc, hipStream_t stream,
-                              const uint64_t* ends, const kx_status* pre, const uint8_t* pre_rc) {
+                              const uint64_t* ends, const kx_status* pre, const uint8_t* pre_rc,
+                              const uint8_t* raw_flags, bool raw) {
   const MsgWs L = msg_ws(n);
   char* b = (char*)mws;
   MsgParams mp{};
   mp.in = in; mp.in_len = in_len; mp.offsets = offsets; mp.n = n; mp.body_field = body_field; mp.mo = mo;
   mp.ends = ends; mp.pre = pre; mp.pre_rc = pre_rc;
+  mp.raw = raw ? 1 : 0; mp.raw_flags = raw_flags;
   mp.pb = pb;
   mp.req_start = (uint64_t*)(b + L.req_start);
   mp.req_end = (uint64_t*)(b + L.req_end);

@@ -343,6 +343,29 @@ int kxo_frame_scan(const uint8_t* in, uint64_t in_len, uint64_t n, uint64_t max_
   return KX_OK;
 }
 
+/* gRPC messages (decodeGRPCFrame, pkg/remote/codec/grpc/grpc_compress.go:37-60): in.Next(5) -> u8
+ * compressed flag, u32 BE length; in.Next(dLen) -> payload (EOF when short). flags[i] = the flag byte.
+ * max_payload > 0: a longer payload is INVALID_DATA. Stops at the first message that cannot be read. */
+int kxo_grpc_frame_scan(const uint8_t* in, uint64_t in_len, uint64_t n, uint64_t max_payload,
+                        uint64_t* frame_offsets, uint64_t* pay_start, uint64_t* pay_end, uint8_t* flags,
+                        uint64_t* n_done) {
+  uint64_t pos = 0;
+  for (uint64_t i = 0; i < n; i++) {
+    frame_offsets[i] = pos;
+    if (in_len - pos < 5) { *n_done = i; return KX_ERR_EOF; }
+    uint64_t len = be32(in + pos + 1);
+    if (len > in_len - pos - 5) { *n_done = i; return KX_ERR_EOF; }
+    if (max_payload && len > max_payload) { *n_done = i; return KX_ERR_INVALID_DATA; }
+    flags[i] = in[pos];
+    pay_start[i] = pos + 5;
+    pay_end[i] = pos + 5 + len;
+    pos += 5 + len;
+  }
+  frame_offsets[n] = pos;
+  *n_done = n;
+  return KX_OK;
+}
+
 /* ------------------------------------------------------------------------------------------------
  * CRC32C payload validator: crcPayloadValidator (pkg/remote/codec/validate.go:168-217). getCRC32C
  * (:208-217) = crc32.Update(0, crc32.MakeTable(crc32.Castagnoli), payload), Go's hash/crc32 (standard

@@ -92,6 +92,9 @@ int kxo_frame_one(const uint8_t* b, uint64_t len, uint64_t max_payload, uint64_t
                   uint64_t* pe, uint8_t* kind);
 int kxo_frame_scan(const uint8_t* in, uint64_t in_len, uint64_t n, uint64_t max_payload, uint64_t* frame_offsets,
                    uint64_t* pay_start, uint64_t* pay_end, uint8_t* kinds, uint64_t* n_done);
+int kxo_grpc_frame_scan(const uint8_t* in, uint64_t in_len, uint64_t n, uint64_t max_payload,
+                        uint64_t* frame_offsets, uint64_t* pay_start, uint64_t* pay_end, uint8_t* flags,
+                        uint64_t* n_done);
 uint32_t kxo_crc32c(uint32_t crc, const uint8_t* p, uint64_t n);
 int kxo_crc32c_batch(const uint8_t* in, uint64_t in_len, const uint64_t* offsets, uint64_t n, uint32_t* crc_out);
 int kxo_frame_crc32c_validate(const uint8_t* in, uint64_t in_len, const uint64_t* frame_offsets, uint64_t n,

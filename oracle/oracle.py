@@ -65,6 +65,7 @@ def lib():
         L.kxo_skip_batch.argtypes = [vp, sz, C.c_uint64, vp, C.POINTER(C.c_uint64)]
         L.kxo_frame_scan.argtypes = [vp, C.c_uint64, C.c_uint64, C.c_uint64, vp, vp, vp, vp,
                                      C.POINTER(C.c_uint64)]
+        L.kxo_grpc_frame_scan.argtypes = L.kxo_frame_scan.argtypes
         L.kxo_crc32c.argtypes = [C.c_uint32, vp, C.c_uint64]
         L.kxo_crc32c.restype = C.c_uint32
         L.kxo_crc32c_batch.argtypes = [vp, C.c_uint64, vp, C.c_uint64, vp]
@@ -141,6 +142,19 @@ def frame_scan(data: np.ndarray, n: int, max_payload: int = 0):
     rc = lib().kxo_frame_scan(data.ctypes.data, data.size, n, max_payload, fo.ctypes.data, ps.ctypes.data,
                               pe.ctypes.data, kd.ctypes.data, C.byref(done))
     return rc, fo, ps[:n], pe[:n], kd[:n], done.value
+
+
+def grpc_frame_scan(data: np.ndarray, n: int, max_payload: int = 0):
+    """gRPC length-prefixed messages (kxo_grpc_frame_scan): rc, frame offsets[n+1], payload starts[n],
+    payload ends[n], flags[n], messages done"""
+    fo = np.zeros(n + 1, dtype=np.uint64)
+    ps = np.zeros(max(1, n), dtype=np.uint64)
+    pe = np.zeros(max(1, n), dtype=np.uint64)
+    fl = np.zeros(max(1, n), dtype=np.uint8)
+    done = C.c_uint64()
+    rc = lib().kxo_grpc_frame_scan(data.ctypes.data if data.size else None, data.size, n, max_payload,
+                                   fo.ctypes.data, ps.ctypes.data, pe.ctypes.data, fl.ctypes.data, C.byref(done))
+    return rc, fo, ps[:n], pe[:n], fl[:n], done.value
 
 
 def crc32c(data: bytes, crc: int = 0) -> int:

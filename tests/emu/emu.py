@@ -33,7 +33,7 @@ def lib():
         _lib.emu_crc.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_int, C.c_void_p, C.c_void_p,
                                  C.c_void_p]
         _lib.emu_frames.restype = C.c_int
-        _lib.emu_frames.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint64] + [C.c_void_p] * 5
+        _lib.emu_frames.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint64] + [C.c_void_p] * 5 + [C.c_int]
     return _lib
 
 
@@ -62,7 +62,7 @@ def skip(data: np.ndarray, n: int, threads: int = 8):
     return rc, offs, st
 
 
-def frames(data: np.ndarray, n: int, max_payload: int = 0, threads: int = 8):
+def frames(data: np.ndarray, n: int, max_payload: int = 0, threads: int = 8, grpc: bool = False):
     os.environ["KX_EMU_THREADS"] = str(threads)
     fo = np.zeros(n + 1, dtype=np.uint64)
     ps = np.zeros(max(1, n), dtype=np.uint64)
@@ -70,7 +70,7 @@ def frames(data: np.ndarray, n: int, max_payload: int = 0, threads: int = 8):
     kd = np.zeros(max(1, n), dtype=np.uint8)
     st = A.Status()
     rc = lib().emu_frames(data.ctypes.data, data.size, n, max_payload, fo.ctypes.data, ps.ctypes.data,
-                          pe.ctypes.data, kd.ctypes.data, C.addressof(st))
+                          pe.ctypes.data, kd.ctypes.data, C.addressof(st), 1 if grpc else 0)
     return rc, fo, ps[:n], pe[:n], kd[:n], st
 
 

@@ -62,7 +62,7 @@ extern "C" int emu_decode(const kx_struct_desc* structs, uint32_t nstructs, cons
 
 // framing sniff (kx_launch_frames) under the emulator, workspace shared with emu_decode's
 extern "C" int emu_frames(const uint8_t* in, uint64_t in_len, uint64_t n, uint64_t max_payload, uint64_t* fo,
-                          uint64_t* ps, uint64_t* pe, uint8_t* kinds, kx_status* status) {
+                          uint64_t* ps, uint64_t* pe, uint8_t* kinds, kx_status* status, int grpc) {
   const size_t ws_size = kx_skip_ws_bytes(in_len);
   static char* ws = nullptr;
   static size_t ws_cap = 0;
@@ -79,7 +79,7 @@ extern "C" int emu_frames(const uint8_t* in, uint64_t in_len, uint64_t n, uint64
     epoch = 1;
   }
   status->diag[0] = status->diag[1] = 0;
-  return kx_launch_frames(in, in_len, n, max_payload, fo, ps, pe, kinds, status, ws, ws_cap, epoch, nullptr);
+  return kx_launch_frames(in, in_len, n, max_payload, fo, ps, pe, kinds, status, ws, ws_cap, epoch, nullptr, grpc != 0);
 }
 
 // CRC32C kernel source (kx_crc.hip): val = 0 ranges [offs[i], offs[i+1]), 1 TTHeader frames at offs[i]

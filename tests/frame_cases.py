@@ -207,3 +207,27 @@ def sniff_matrix_frames():
         "pb_ttheader_framed": (ttheader(be32(10) + pb1 + ten[:6], proto=4), 0x16),
         "pb_framed": (be32(10) + pb1 + ten[:6], 0x14),
     }
+
+
+# ---- gRPC length-prefixed messages (decodeGRPCFrame, grpc_compress.go:37-60) ----
+def grpc_message(payload: bytes, flag: int = 0) -> bytes:
+    return bytes([flag]) + be32(len(payload)) + payload
+
+
+def grpc_batch(n, pb=False, start=0, compressed=(), sizes=None):
+    """n gRPC messages whose payloads are R2 record bodies (Thrift) or PF bodies (pb); message indices in
+    `compressed` carry flag 1; sizes (optional) replaces record i by a string-heavy record of that size"""
+    if pb:
+        from oracle import oracle as o
+        from tests import pb_cases as PC
+        sch = S.schema_pf()
+        rc, w, _ = o.encode(sch, synth.gen_pf(n, start=start), pb=True)
+        assert rc == 0
+        recs = [bytes(b) for b in PC.split_frames(w)]
+    else:
+        sch, recs = records(n, start)
+    msgs = [grpc_message(recs[i], 1 if i in compressed else (2 if i % 97 == 5 else 0)) for i in range(n)]
+    wire = np.frombuffer(b"".join(msgs), dtype=np.uint8).copy()
+    fo = np.zeros(n + 1, dtype=np.uint64)
+    fo[1:] = np.cumsum([len(m) for m in msgs])
+    return sch, recs, msgs, wire, fo
