@@ -35,6 +35,9 @@
  *                                 183-217) over N payloads
  *   kx_frame_crc32c_validate .... payloadChecksumValidate + crcPayloadValidator.Validate (validate.go:91-127,
  *                                 190-201) of N TTHeader frames, as DecodeMeta runs it (default_codec.go:205-209)
+ *   kx_thrift_raw_messages ...... binaryThriftCodec.Unmarshal (pkg/generic/binarythrift_codec.go:83-115,
+ *                                 readBinaryMethod :185-199) over N raw messages; kx_thrift_set_seqids =
+ *                                 SetSeqID (:117-175) in place
  *   kx_grpc_frame_scan .......... decodeGRPCFrame (pkg/remote/codec/grpc/grpc_compress.go:37-60) over N
  *                                 messages; kx_*_decode_grpc = grpcCodec.Decode bodies (grpc.go:202-270)
  *   kx_ctx_set_crc32c_check ..... CodecConfig{CRC32Check: true} (default_codec.go:70-92) for kx_*_decode_frames
@@ -315,6 +318,22 @@ int kx_thrift_decode_frames(kx_ctx* c, const kx_schema* s, const uint8_t* in, ui
 int kx_pb_decode_frames(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len, uint64_t n,
                         uint64_t max_payload, uint64_t* frame_offsets, uint8_t* kinds, const kx_column* msg_cols,
                         const kx_columns* out, uint8_t* record_status, kx_status* status, void* stream);
+
+/* ---- binary generic (raw) ingress: binaryThriftCodec (pkg/generic/binarythrift_codec.go) ----
+ * kx_thrift_raw_messages: Unmarshal (:83-115) over n messages in[offsets[i] .. offsets[i+1]) (u64, n + 1):
+ *   the request stays the raw message bytes (zero copy, nothing is parsed past the method name);
+ *   msg_cols (optional, as kx_thrift_decode_messages) receive the method name (readBinaryMethod :185-199:
+ *   u32 length at [4, 8), 0 < length <= size - 8), the message type (first u32 & 0xffff) and the seqid
+ *   (the u32 after the name, 0 if absent). record_status: INVALID_DATA for a bad method length;
+ *   APPLICATION_EXCEPTION for an EXCEPTION message (it takes the regular thriftCodec path, :88-90).
+ * kx_thrift_set_seqids: SetSeqID (:117-134, getSeqID4Bytes :147-175) in place over n raw messages:
+ *   the seqid of message i becomes seqids[i] (device i32); a message without a strict version is
+ *   BAD_VERSION (INVALID_DATA when the first word is positive), a negative name length or a message
+ *   too short for the seqid INVALID_DATA (that message is left untouched). */
+int kx_thrift_raw_messages(kx_ctx* c, const uint8_t* in, uint64_t in_len, const uint64_t* offsets, uint64_t n,
+                           const kx_column* msg_cols, uint8_t* record_status, kx_status* status, void* stream);
+int kx_thrift_set_seqids(kx_ctx* c, uint8_t* in, uint64_t in_len, const uint64_t* offsets, uint64_t n,
+                         const int32_t* seqids, uint8_t* record_status, kx_status* status, void* stream);
 
 /* ---- gRPC length-prefixed messages (decodeGRPCFrame, pkg/remote/codec/grpc/grpc_compress.go:37-60;
  *      grpcCodec.Decode, grpc.go:202-260) ----

@@ -26,7 +26,8 @@ EXPORTS = [
     "kx_thrift_decode_messages", "kx_pb_decode_messages", "kx_pb_meta_length", "kx_pb_write_meta",
     "kx_pb_read_meta", "kx_ctx_set_pipeline", "kx_frame_scan", "kx_thrift_decode_frames",
     "kx_pb_decode_frames", "kx_crc32c_batch", "kx_frame_crc32c_validate", "kx_ctx_set_crc32c_check",
-    "kx_grpc_frame_scan", "kx_thrift_decode_grpc", "kx_pb_decode_grpc",
+    "kx_grpc_frame_scan", "kx_thrift_decode_grpc", "kx_pb_decode_grpc", "kx_thrift_raw_messages",
+    "kx_thrift_set_seqids",
 ]
 
 
@@ -99,6 +100,8 @@ def lib():
     L.kx_frame_crc32c_validate.argtypes = [vp, vp, u64, vp, u64, vp, vp, vp, vp]
     L.kx_ctx_set_crc32c_check.argtypes = [vp, C.c_int]
     L.kx_grpc_frame_scan.argtypes = L.kx_frame_scan.argtypes
+    L.kx_thrift_raw_messages.argtypes = [vp, vp, u64, vp, u64, C.POINTER(A.Column), vp, vp, vp]
+    L.kx_thrift_set_seqids.argtypes = [vp, vp, u64, vp, u64, vp, vp, vp, vp]
     L.kx_thrift_decode_grpc.argtypes = [vp, vp, vp, u64, u64, u64, vp, C.POINTER(A.Columns), vp, vp, vp]
     L.kx_pb_decode_grpc.argtypes = L.kx_thrift_decode_grpc.argtypes
     L.kx_pb_meta_length.argtypes = [u32]

@@ -601,6 +601,49 @@ int kx_pb_decode_grpc(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t
   return decode_grpc(c, s, in, in_len, n, true, max_payload, frame_offsets, out, record_status, status, stream);
 }
 
+int kx_thrift_raw_messages(kx_ctx* c, const uint8_t* in, uint64_t in_len, const uint64_t* offsets, uint64_t n,
+                           const kx_column* msg_cols, uint8_t* record_status, kx_status* status, void* stream) {
+  if (!c || !status || !offsets || (!in && in_len)) return KX_ERR_INVALID_ARG;
+  int rc = set_device(c);
+  if (rc) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  KxMsgOut mo{};
+  if (msg_cols) {
+    const kx_column& nm = msg_cols[0];
+    const int w = offset_width(nm);
+    if (!w) return KX_ERR_INVALID_ARG;
+    mo.name_offs = nm.offsets;
+    mo.name_data = (uint8_t*)nm.data;
+    mo.name_cap = nm.data ? nm.capacity : 0;
+    mo.name_owide = w == 8;
+    mo.msg_type = (int32_t*)msg_cols[1].data;
+    mo.seqid = (int32_t*)msg_cols[2].data;
+  }
+  KX_HIP_CHECK(hipMemsetAsync(status, 0, sizeof(kx_status), st));
+  if (n == 0) {
+    if (mo.name_offs) KX_HIP_CHECK(hipMemsetAsync(mo.name_offs, 0, mo.name_owide ? 8 : 4, st));
+    return KX_OK;
+  }
+  if ((rc = ensure_mws(c, kx_message_ws_bytes(n), st))) return rc;
+  uint64_t *rs = nullptr, *re = nullptr;
+  uint8_t *hrc = nullptr, *brc = nullptr;
+  if ((rc = kx_launch_message_headers(in, in_len, offsets, n, 0, false, mo, c->mws, &rs, &re, &hrc, &brc, st,
+                                      nullptr, nullptr, nullptr, nullptr, 2)))
+    return rc;
+  KX_HIP_CHECK(hipMemsetAsync(brc, 0, n, st));  // no body is decoded: the request stays raw
+  return kx_launch_message_merge(offsets, n, hrc, brc, record_status, status, c->mws, st, nullptr);
+}
+
+int kx_thrift_set_seqids(kx_ctx* c, uint8_t* in, uint64_t in_len, const uint64_t* offsets, uint64_t n,
+                         const int32_t* seqids, uint8_t* record_status, kx_status* status, void* stream) {
+  if (!c || !status || !offsets || (n && !seqids) || (!in && in_len)) return KX_ERR_INVALID_ARG;
+  int rc = set_device(c);
+  if (rc) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  if ((rc = ensure_mws(c, kx_message_ws_bytes(n), st))) return rc;
+  return kx_launch_set_seqids(in, in_len, offsets, n, seqids, record_status, status, c->mws, st);
+}
+
 int kx_thrift_decode_frames(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len, uint64_t n,
                             int32_t body_field, uint64_t max_payload, uint64_t* frame_offsets, uint8_t* kinds,
                             const kx_column* msg_cols, const kx_columns* out, uint8_t* record_status,

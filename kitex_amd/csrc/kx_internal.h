@@ -122,7 +122,9 @@ int kx_launch_message_headers(const uint8_t* in, uint64_t in_len, const uint64_t
                               uint8_t** hdr_rc, uint8_t** body_rc, hipStream_t stream,
                               const uint64_t* ends = nullptr, const kx_status* pre = nullptr,
                               const uint8_t* pre_rc = nullptr, const uint8_t* raw_flags = nullptr,
-                              bool raw = false);
+                              int raw = 0);
+int kx_launch_set_seqids(uint8_t* in, uint64_t in_len, const uint64_t* offsets, uint64_t n, const int32_t* seqids,
+                         uint8_t* record_status, kx_status* status, void* mws, hipStream_t stream);
 int kx_launch_message_merge(const uint64_t* offsets, uint64_t n, const uint8_t* hdr_rc, const uint8_t* body_rc,
                             uint8_t* record_status, kx_status* status, void* mws, hipStream_t stream,
                             const kx_status* pre = nullptr);

@@ -170,6 +170,31 @@ __global__ void __launch_bounds__(MT) header_kernel(MsgParams mp) {
     rc = mp.pre_rc[i];  // DecodeMeta failed (payload checksum): the payload codec never runs
   } else if (p > e || e > mp.in_len) {
     rc = KX_ERR_INVALID_ARG;
+  } else if (mp.raw == 2) {
+    // binary generic ingress (binaryThriftCodec.Unmarshal, pkg/generic/binarythrift_codec.go:83-115): the
+    // request stays the raw message; PeekUint32 & FrontMask == Exception takes the regular thrift path;
+    // readBinaryMethod (:185-199): u32 length at [4, 8), 0 < length <= size - 8, name at [8, 8 + length)
+    if (e - p < 4) {
+      rc = KX_ERR_EOF;
+    } else {
+      const uint32_t v = be32(in + p);
+      type = v & 0xffffu;
+      if (type == KX_MSG_EXCEPTION) {
+        rc = KX_ERR_APPLICATION_EXCEPTION;
+      } else if (e - p < 8) {
+        rc = KX_ERR_INVALID_DATA;
+      } else {
+        const uint64_t ml = be32(in + p + 4);
+        if (ml == 0 || ml > 0x7fffffffull || e - p - 8 < ml) {
+          rc = KX_ERR_INVALID_DATA;
+        } else {
+          nl = (int32_t)ml;
+          seqid = e - p - 8 - ml >= 4 ? (int32_t)be32(in + p + 8 + ml) : 0;
+        }
+      }
+    }
+    rs = p;
+    re = p;
   } else if (mp.raw) {
     // decodeGRPCFrame (grpc_compress.go:53-58): a compressed message needs a registered decompressor
     if (mp.raw_flags && mp.raw_flags[i] == 1) rc = KX_ERR_NOT_IMPLEMENTED;
@@ -225,6 +250,38 @@ __global__ void __launch_bounds__(MT) header_kernel(MsgParams mp) {
   mp.hdr_rc[i] = (uint8_t)rc;
   if (mp.mo.msg_type) mp.mo.msg_type[i] = (int32_t)type;
   if (mp.mo.seqid) mp.mo.seqid[i] = seqid;
+}
+
+// SetSeqID (binarythrift_codec.go:117-134 via getSeqID4Bytes :147-175) of raw message i in place
+__global__ void __launch_bounds__(MT) setseq_kernel(uint8_t* in, uint64_t in_len, const uint64_t* offsets,
+                                                    uint64_t n, const int32_t* seqids, uint8_t* rs,
+                                                    unsigned long long* errkey) {
+  const uint64_t i = (uint64_t)blockIdx.x * MT + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t p = offsets[i], e = offsets[i + 1];
+  int rc = KX_OK;
+  if (p > e || e > in_len) {
+    rc = KX_ERR_INVALID_ARG;
+  } else if (e - p < 4) {
+    rc = KX_ERR_INVALID_DATA;
+  } else {
+    const int32_t first = (int32_t)be32(in + p);
+    if (first > 0) rc = KX_ERR_INVALID_DATA;                                  // missing version
+    else if (((uint32_t)first & 0xffff0000u) != 0x80010000u) rc = KX_ERR_BAD_VERSION;
+    else if (e - p < 8) rc = KX_ERR_INVALID_DATA;
+    else {
+      const int32_t nl = (int32_t)be32(in + p + 4);
+      if (nl < 0) rc = KX_ERR_INVALID_DATA;                                    // perrors.InvalidDataLength
+      else if (e - p < 12ull + (uint64_t)nl) rc = KX_ERR_INVALID_DATA;         // invalid trans buffer
+      else {
+        const uint32_t v = (uint32_t)seqids[i];
+        uint8_t* q = in + p + 8 + nl;
+        q[0] = (uint8_t)(v >> 24); q[1] = (uint8_t)(v >> 16); q[2] = (uint8_t)(v >> 8); q[3] = (uint8_t)v;
+      }
+    }
+  }
+  if (rs) rs[i] = (uint8_t)rc;
+  if (rc) atomicMin(errkey, (unsigned long long)((i << 8) | (uint64_t)(rc & 0xff)));
 }
 
 // exclusive scan of name_len[0..n] in place (one workgroup; each thread a contiguous run)
@@ -339,13 +396,13 @@ int kx_launch_message_headers(const uint8_t* in, uint64_t in_len, const uint64_t
                               int32_t body_field, bool pb, const KxMsgOut& mo, void* mws, uint64_t** req_start,
                               uint64_t** req_end, uint8_t** hdr_rc, uint8_t** body_rc, hipStream_t stream,
                               const uint64_t* ends, const kx_status* pre, const uint8_t* pre_rc,
-                              const uint8_t* raw_flags, bool raw) {
+                              const uint8_t* raw_flags, int raw) {
   const MsgWs L = msg_ws(n);
   char* b = (char*)mws;
   MsgParams mp{};
   mp.in = in; mp.in_len = in_len; mp.offsets = offsets; mp.n = n; mp.body_field = body_field; mp.mo = mo;
   mp.ends = ends; mp.pre = pre; mp.pre_rc = pre_rc;
-  mp.raw = raw ? 1 : 0; mp.raw_flags = raw_flags;
+  mp.raw = raw; mp.raw_flags = raw_flags;
   mp.pb = pb;
   mp.req_start = (uint64_t*)(b + L.req_start);
   mp.req_end = (uint64_t*)(b + L.req_end);
@@ -365,6 +422,23 @@ int kx_launch_message_headers(const uint8_t* in, uint64_t in_len, const uint64_t
   *req_end = mp.req_end;
   *hdr_rc = mp.hdr_rc;
   *body_rc = (uint8_t*)(b + L.body_rc);
+  return KX_OK;
+}
+
+int kx_launch_set_seqids(uint8_t* in, uint64_t in_len, const uint64_t* offsets, uint64_t n, const int32_t* seqids,
+                         uint8_t* record_status, kx_status* status, void* mws, hipStream_t stream) {
+  unsigned long long* errkey = (unsigned long long*)mws;
+  uint32_t* overflow = (uint32_t*)((char*)mws + 8);
+  const unsigned grid = (unsigned)((n + MT - 1) / MT);
+  if (grid) {
+    hipLaunchKernelGGL(setseq_kernel, dim3(grid), dim3(MT), 0, stream, in, in_len, offsets, n, seqids, record_status,
+                       errkey);
+    KX_HIP_CHECK(hipGetLastError());
+  }
+  KX_HIP_CHECK(hipMemsetAsync(status, 0, sizeof(kx_status), stream));
+  hipLaunchKernelGGL(final_kernel, dim3(1), dim3(64), 0, stream, status, offsets, n, errkey, overflow,
+                     (const kx_status*)nullptr);
+  KX_HIP_CHECK(hipGetLastError());
   return KX_OK;
 }
 

@@ -343,6 +343,63 @@ int kxo_frame_scan(const uint8_t* in, uint64_t in_len, uint64_t n, uint64_t max_
   return KX_OK;
 }
 
+/* Binary generic ingress (pkg/generic/binarythrift_codec.go). Unmarshal (:83-115): PeekUint32 &
+ * FrontMask (0xffff, codec/util.go:31) == Exception -> the regular thrift path (APPLICATION_EXCEPTION
+ * here); readBinaryMethod (:185-199): size >= 8, methodLen = u32 [4, 8), 0 < methodLen <= size - 8.
+ * The seqid reported is the u32 after the name when present (GetSeqID's position, :137-175). */
+int kxo_raw_messages(const uint8_t* in, uint64_t in_len, const uint64_t* offsets, uint64_t n, uint64_t* name_pos,
+                     uint64_t* name_len, int32_t* msg_type, int32_t* seqid, uint8_t* rs) {
+  int first = KX_OK;
+  for (uint64_t i = 0; i < n; i++) {
+    uint64_t p = offsets[i], e = offsets[i + 1];
+    int rc = KX_OK;
+    uint32_t ty = 0, sq = 0;
+    uint64_t ml = 0;
+    if (p > e || e > in_len) rc = KX_ERR_INVALID_ARG;
+    else if (e - p < 4) rc = KX_ERR_EOF;
+    else {
+      ty = be32(in + p) & 0xffffu;
+      if (ty == KX_MSG_EXCEPTION) rc = KX_ERR_APPLICATION_EXCEPTION;
+      else if (e - p < 8) rc = KX_ERR_INVALID_DATA;
+      else {
+        ml = be32(in + p + 4);
+        if (ml == 0 || ml > 0x7fffffffu || e - p - 8 < ml) rc = KX_ERR_INVALID_DATA;
+        else if (e - p - 8 - ml >= 4) sq = be32(in + p + 8 + ml);
+      }
+    }
+    if (rc) { ty = 0; sq = 0; ml = 0; }
+    name_pos[i] = p + 8; name_len[i] = ml; msg_type[i] = (int32_t)ty; seqid[i] = (int32_t)sq; rs[i] = (uint8_t)rc;
+    if (rc && !first) first = rc;
+  }
+  return first;
+}
+
+/* SetSeqID (:117-134) via getSeqID4Bytes (:147-175), in place */
+int kxo_set_seqids(uint8_t* in, uint64_t in_len, const uint64_t* offsets, uint64_t n, const int32_t* seqids,
+                   uint8_t* rs) {
+  int first = KX_OK;
+  for (uint64_t i = 0; i < n; i++) {
+    uint64_t p = offsets[i], e = offsets[i + 1];
+    int rc = KX_OK;
+    if (p > e || e > in_len) rc = KX_ERR_INVALID_ARG;
+    else if (e - p < 4) rc = KX_ERR_INVALID_DATA;
+    else {
+      int32_t f = (int32_t)be32(in + p);
+      if (f > 0) rc = KX_ERR_INVALID_DATA;                            /* missing version */
+      else if (((uint32_t)f & KXO_MASK) != 0x80010000u) rc = KX_ERR_BAD_VERSION;
+      else if (e - p < 8) rc = KX_ERR_INVALID_DATA;
+      else {
+        int32_t nl = (int32_t)be32(in + p + 4);
+        if (nl < 0 || e - p < 12ull + (uint64_t)nl) rc = KX_ERR_INVALID_DATA;
+        else put32(in + p + 8 + nl, (uint32_t)seqids[i]);
+      }
+    }
+    rs[i] = (uint8_t)rc;
+    if (rc && !first) first = rc;
+  }
+  return first;
+}
+
 /* gRPC messages (decodeGRPCFrame, pkg/remote/codec/grpc/grpc_compress.go:37-60): in.Next(5) -> u8
  * compressed flag, u32 BE length; in.Next(dLen) -> payload (EOF when short). flags[i] = the flag byte.
  * max_payload > 0: a longer payload is INVALID_DATA. Stops at the first message that cannot be read. */

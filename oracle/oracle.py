@@ -66,6 +66,8 @@ def lib():
         L.kxo_frame_scan.argtypes = [vp, C.c_uint64, C.c_uint64, C.c_uint64, vp, vp, vp, vp,
                                      C.POINTER(C.c_uint64)]
         L.kxo_grpc_frame_scan.argtypes = L.kxo_frame_scan.argtypes
+        L.kxo_raw_messages.argtypes = [vp, C.c_uint64, vp, C.c_uint64, vp, vp, vp, vp, vp]
+        L.kxo_set_seqids.argtypes = [vp, C.c_uint64, vp, C.c_uint64, vp, vp]
         L.kxo_crc32c.argtypes = [C.c_uint32, vp, C.c_uint64]
         L.kxo_crc32c.restype = C.c_uint32
         L.kxo_crc32c_batch.argtypes = [vp, C.c_uint64, vp, C.c_uint64, vp]
@@ -142,6 +144,33 @@ def frame_scan(data: np.ndarray, n: int, max_payload: int = 0):
     rc = lib().kxo_frame_scan(data.ctypes.data, data.size, n, max_payload, fo.ctypes.data, ps.ctypes.data,
                               pe.ctypes.data, kd.ctypes.data, C.byref(done))
     return rc, fo, ps[:n], pe[:n], kd[:n], done.value
+
+
+def raw_messages(data: np.ndarray, offsets: np.ndarray):
+    """binary generic ingress (kxo_raw_messages): rc, names (list of bytes), msg types, seqids, codes"""
+    n = offsets.size - 1
+    npos = np.zeros(max(1, n), dtype=np.uint64)
+    nlen = np.zeros(max(1, n), dtype=np.uint64)
+    ty = np.zeros(max(1, n), dtype=np.int32)
+    sq = np.zeros(max(1, n), dtype=np.int32)
+    rs = np.zeros(max(1, n), dtype=np.uint8)
+    offs = np.ascontiguousarray(offsets, dtype=np.uint64)
+    rc = lib().kxo_raw_messages(data.ctypes.data if data.size else None, data.size, offs.ctypes.data, n,
+                                npos.ctypes.data, nlen.ctypes.data, ty.ctypes.data, sq.ctypes.data, rs.ctypes.data)
+    names = [data[int(npos[i]):int(npos[i]) + int(nlen[i])].tobytes() for i in range(n)]
+    return rc, names, ty[:n], sq[:n], rs[:n]
+
+
+def set_seqids(data: np.ndarray, offsets: np.ndarray, seqids: np.ndarray):
+    """SetSeqID over n raw messages, in place on a copy: rc, new bytes, codes"""
+    out = data.copy()
+    n = offsets.size - 1
+    rs = np.zeros(max(1, n), dtype=np.uint8)
+    offs = np.ascontiguousarray(offsets, dtype=np.uint64)
+    sq = np.ascontiguousarray(seqids, dtype=np.int32)
+    rc = lib().kxo_set_seqids(out.ctypes.data if out.size else None, out.size, offs.ctypes.data, n, sq.ctypes.data,
+                              rs.ctypes.data)
+    return rc, out, rs[:n]
 
 
 def grpc_frame_scan(data: np.ndarray, n: int, max_payload: int = 0):

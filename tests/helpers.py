@@ -89,3 +89,40 @@ def assert_rows_equal(got, exp, infos, rows):
                 assert np.array_equal(a, b), f"var column {c} (field {ci.field_id}) differs at row {r}"
         else:
             raise NotImplementedError(ci.kind)
+
+
+def random_columns(infos, npres, n, seed=0):
+    """Random host columns for any flattened schema (test infrastructure): fixed values (bools 0/1),
+    strings 0..40 bytes, lists of 0..5 elements, string lists of 0..4 strings of 0..12 bytes; a map's
+    value column shares its key column's entry counts; every presence bit set."""
+    from kitex_amd.synth import ColumnSet
+    rng = np.random.default_rng(seed)
+    fixed = {1: np.uint8, 2: np.int16, 4: np.int32, 8: np.int64}
+    cols, counts = [], None
+    for c, ci in enumerate(infos):
+        is_val = bool(ci.elem_ttype & A.ELEM_MAP_VALUE) if hasattr(A, "ELEM_MAP_VALUE") else bool(ci.elem_ttype & 0x80)
+        et = ci.elem_ttype & 0x7F
+        if ci.kind == A.COL_FIXED:
+            v = rng.integers(0, 2, size=n) if ci.ttype == A.T_BOOL else rng.integers(-(1 << 62), 1 << 62, size=n)
+            cols.append(v.astype(fixed[ci.width]))
+            continue
+        cnt = counts if is_val else rng.integers(0, 6 if ci.kind == A.COL_LIST else 5 if ci.kind == A.COL_LIST_BYTES
+                                                 else 41, size=n)
+        if ci.ttype == A.T_MAP and not is_val:
+            counts = cnt
+        offs = np.zeros(n + 1, dtype=np.uint32)
+        offs[1:] = np.cumsum(cnt)
+        tot = int(offs[-1])
+        if ci.kind == A.COL_BYTES:
+            cols.append((offs, rng.integers(0, 256, size=max(1, tot), dtype=np.uint8)))
+        elif ci.kind == A.COL_LIST:
+            v = rng.integers(0, 2, size=max(1, tot)) if et == A.T_BOOL else rng.integers(-(1 << 62), 1 << 62,
+                                                                                         size=max(1, tot))
+            cols.append((offs, v.astype(fixed[ci.width])))
+        else:
+            el = rng.integers(0, 13, size=max(1, tot))[:tot]
+            eo = np.zeros(tot + 1, dtype=np.uint32)
+            eo[1:] = np.cumsum(el)
+            cols.append((offs, eo, rng.integers(0, 256, size=max(1, int(eo[-1])), dtype=np.uint8)))
+    pres = np.full(n, (1 << 64) - 1, dtype=np.uint64) if npres else None
+    return ColumnSet(cols, pres, n)
