@@ -99,10 +99,11 @@ typedef struct kx_field_desc {
   int16_t id;            /* thrift field id */
   uint8_t ttype;         /* KX_T_* of the field */
   uint8_t req;           /* KX_REQ_* */
-  uint8_t elem_ttype;    /* LIST/SET: element KX_T_* (a scalar, or STRING);
+  uint8_t elem_ttype;    /* LIST/SET: element KX_T_* (a scalar, STRING, or STRUCT: see below);
                             MAP: key KX_T_* | value KX_T_* << 4 (each a scalar or STRING) */
   uint8_t reserved0;
-  int16_t child;         /* STRUCT: index of the child struct in the schema's struct table; else -1 */
+  int16_t child;         /* STRUCT (or LIST/SET of STRUCT): index of the (element) struct in the schema's
+                            struct table; else -1 */
   int64_t default_bits;  /* scalar default value (two's complement / IEEE bits); ignored otherwise */
 } kx_field_desc;
 
@@ -126,9 +127,18 @@ enum {
 /* A MAP field flattens to two consecutive columns, keys then values (each LIST or LIST_BYTES,
  * record offsets in entries); the value column's elem_ttype carries KX_ELEM_MAP_VALUE. Encoding
  * writes entries in column order (Go iterates a map in random order: its bytes are only
- * deterministic for maps of <= 1 entry, k-mock.go:225,259). list<struct> is not supported
- * (KX_ERR_NOT_IMPLEMENTED at kx_schema_create). */
+ * deterministic for maps of <= 1 entry, k-mock.go:225,259).
+ * A LIST/SET of a struct S (field elem_ttype = KX_T_STRUCT, child = S) whose fields are all fixed-width
+ * scalars (default or required) flattens to one LIST column per field of S, in S's IDL order, sharing
+ * the record offsets (in elements); each column's elem_ttype is the field's type | KX_ELEM_STRUCT_FIELD,
+ * its field_id / path end with S's field id. Decoding runs each element's FastRead (fields in any order,
+ * unknown or mistyped fields skipped, the last duplicate wins, a missing field takes its default, a
+ * missing required field is INVALID_DATA; FieldFastReadList + StructLikeFastRead, struct_tpl.go:583-625);
+ * encoding writes every field of S in IDL order, then STOP (FieldFastWriteList, :1011-1036). Other
+ * element structs (strings, nested structs or containers, optional fields) and nested containers are
+ * KX_ERR_NOT_IMPLEMENTED at kx_schema_create. */
 #define KX_ELEM_MAP_VALUE 0x80
+#define KX_ELEM_STRUCT_FIELD 0x40
 
 typedef struct kx_column_info {
   uint32_t kind;        /* KX_COL_* */

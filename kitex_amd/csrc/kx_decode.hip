@@ -437,6 +437,49 @@ __device__ __forceinline__ void close_slots(const KAS KxProgram* P, const KAS Kx
   }
 }
 
+// One element of a list<S> (S of fixed-width scalars) at q: S's FastRead (struct_tpl.go:41-149): fields
+// until STOP, unknown / mistyped ids skipped, the last duplicate wins, required fields checked. S's fields
+// are the columns c0 .. c0 + ns - 1 (sel_id / sel_req / elem / width / defv). want >= 0: *val = the value
+// of S's field `want` (host order), or its default when the element lacks it. *qe = the element's end.
+__device__ __forceinline__ int elem_struct(const Src& w, const KAS KxProgram* P, uint32_t c0, uint32_t ns, uint64_t q,
+                                           uint64_t limit, uint64_t* qe, int want, uint64_t* val) {
+  uint32_t isset = 0;
+  if (want >= 0) *val = (uint64_t)ldk(&P->col[c0 + want]).defv;
+  for (;;) {
+    if (q >= limit) return KX_ERR_EOF;
+    const uint32_t h = ld4(w, q);
+    const uint32_t t = h & 0xff;
+    if (t == KX_T_STOP) { q += 1; break; }
+    if (limit - q < 3) return KX_ERR_EOF;
+    const int16_t id = (int16_t)((((h >> 8) & 0xffu) << 8) | ((h >> 16) & 0xffu));
+    q += 3;
+    int k = -1;
+    for (uint32_t j = 0; j < ns; j++)
+      if (P->sel_id[c0 + j] == id) { k = (int)j; break; }
+    const KxpCol K = ldk(&P->col[c0 + (k < 0 ? 0 : k)]);
+    if (k < 0 || K.elem != t) {
+      const int rc = dskip_body(w, q, limit, t, 64);
+      if (rc) return rc;
+      continue;
+    }
+    if (limit - q < K.width) return KX_ERR_EOF;
+    if (k == want) {
+      uint64_t v;
+      if (K.width == 1) v = t == KX_T_BOOL ? (ld1(w, q) == 1) : ld1(w, q);
+      else if (K.width == 2) v = __builtin_bswap32(ld4(w, q)) >> 16;
+      else if (K.width == 4) v = __builtin_bswap32(ld4(w, q));
+      else v = be64(w, q);
+      *val = v;
+    }
+    q += K.width;
+    isset |= 1u << k;
+  }
+  for (uint32_t j = 0; j < ns; j++)
+    if (P->sel_req[c0 + j] && !((isset >> j) & 1)) return KX_ERR_INVALID_DATA;
+  *qe = q;
+  return KX_OK;
+}
+
 // Canonical fast path: the record is checked against the schema's canonical plan (header bytes in
 // encoder order, STOP bytes). The step index is wave-uniform (scalar loads); a lane whose record
 // deviates returns false and the record is re-parsed by the generic loop.
@@ -624,6 +667,17 @@ __device__ __forceinline__ int generic_record(const Src& w, const KAS KxProgram*
         vset<NV>(vs, K.vslot, vp + 6, (uint32_t)l);
         if (K.vslot2 != 0xff) vset<NV>(vs, K.vslot2, vp + 6, (uint32_t)nb[side]);
       }
+      pos = q;
+    } else if (F.kind == KXP_K_LSTRUCT) {                    // list/set<S>: size x S.FastRead (:583-625)
+      if (limit - vp < 5) return KX_ERR_EOF;
+      const int32_t l = (int32_t)__builtin_bswap32(fx.w1);
+      if (l < 0) return KX_ERR_NEGATIVE_SIZE;
+      uint64_t q = vp + 5, v0;
+      for (int32_t j = 0; j < l; j++) {
+        const int rc = elem_struct(w, P, (uint32_t)F.col, F.width, q, limit, &q, -1, &v0);
+        if (rc) return rc;
+      }
+      for (uint32_t k = 0; k < F.width; k++) vset<NV>(vs, ldk(&P->col[F.col + k]).vslot, vp + 5, (uint32_t)l);
       pos = q;
     } else if (F.kind == KXP_K_LIST) {                       // ReadListBegin: elem type ignored (:587)
       if (limit - vp < 5) return KX_ERR_EOF;
@@ -2195,6 +2249,16 @@ __device__ __forceinline__ void emit_container(const Src& w, const KAS KxProgram
   const bool fits = lb ? (E + n <= elem_lim(cols, c) && B + nb <= arena_lim(cols, c)) : E + n <= arena_lim(cols, c);
   if (!fits) { atomicOr(overflow, 1u); return; }
   put_off(cols, c, r, E);
+  if (K.mside == 3) {  // a field of list<S>: walk each element for this column's field
+    const uint32_t c0 = P->sel_first[c], ns = P->sel_n[c];
+    uint64_t q = pos;
+    for (uint32_t j = 0; j < n; j++) {
+      uint64_t v = 0;
+      (void)elem_struct(w, P, c0, ns, q, ~0ull, &q, (int)(c - c0), &v);  // validated by the record's walk
+      store_col(cols.data[c], K.width, E + j, v);
+    }
+    return;
+  }
   uint32_t kt = KX_T_STRING, vt = KX_T_STRING;
   if (K.mside) {
     const KxpField F = ld_field(P, K.field);

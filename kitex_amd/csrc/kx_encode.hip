@@ -87,7 +87,11 @@ __device__ uint64_t record_size(const KxProgram& P, const KxLaunchCols& C, uint6
     if (F.kind == KXP_K_FIXED) sz += F.width;
     else if (F.kind == KXP_K_BYTES) sz += 4 + var_len(C, F.col, r);
     else if (F.kind == KXP_K_LIST) sz += 5 + var_len(C, F.col, r) * F.width;
-    else if (F.kind == KXP_K_LISTB)  // list/set<string> (FieldListLength, struct_tpl.go:1038-1061)
+    else if (F.kind == KXP_K_LSTRUCT) {  // list/set<S>: every field of S + STOP per element
+      uint64_t es = 1;
+      for (int c = F.col; c < F.col + F.width; c++) es += 3 + P.col[c].width;
+      sz += 5 + var_len(C, F.col, r) * es;
+    } else if (F.kind == KXP_K_LISTB)  // list/set<string> (FieldListLength, struct_tpl.go:1038-1061)
       sz += 5 + side_bytes(P, C, F.col, off_at(C, F.col, r), var_len(C, F.col, r));
     else if (F.kind == KXP_K_MAP) {  // map (FieldMapLength): both sides, the keys' entry count
       const uint64_t cnt = var_len(C, F.col, r);
@@ -221,6 +225,25 @@ __device__ void write_record(const KxProgram& P, const KxLaunchCols& C, uint64_t
         if (F.elem == KX_T_BOOL) v = (v & 0xff) ? 1 : 0;
         put_be(s, v, F.width);
       }
+    } else if (F.kind == KXP_K_LSTRUCT) {
+      // FieldFastWriteList of S (struct_tpl.go:1011-1036): S.FastWriteNocopy per element, every field of
+      // S in IDL order (all fixed-length: the encoder reorder keeps it), then STOP
+      const uint64_t o = off_at(C, F.col, r);
+      const uint32_t cnt = (uint32_t)var_len(C, F.col, r);
+      s.put(KX_T_STRUCT, 1);
+      put_be(s, cnt, 4);
+      for (uint32_t j = 0; j < cnt; j++) {
+        for (int c = F.col; c < F.col + F.width; c++) {
+          const KxpCol& K = P.col[c];
+          const uint32_t sid = (uint16_t)P.sel_id[c];
+          s.put((uint32_t)K.elem | ((sid >> 8) << 8) | ((sid & 0xff) << 16), 3);
+          uint64_t v = load_fixed(C.data[c], K.width, off_at(C, c, r) + j);
+          if (K.elem == KX_T_BOOL) v = (v & 0xff) ? 1 : 0;
+          put_be(s, v, K.width);
+        }
+        s.put(KX_T_STOP, 1);
+      }
+      (void)o;
     } else if (F.kind == KXP_K_LISTB || F.kind == KXP_K_MAP) {
       // FieldFastWriteList of strings / FieldFastWriteMap (struct_tpl.go:875-912, 1011-1036); a map
       // in column order (Go iterates its maps in random order)

@@ -21,7 +21,9 @@
 
 enum : uint8_t { KXP_K_FIXED = 1, KXP_K_BYTES = 2, KXP_K_LIST = 3, KXP_K_STRUCT = 4,
                  KXP_K_LISTB = 5,   // list/set<string>: column LIST_BYTES, slots vslot (elements) + vslot2 (bytes)
-                 KXP_K_MAP = 6 };   // map<K,V>: field kind only; columns col (keys), col + 1 (values)
+                 KXP_K_MAP = 6,     // map<K,V>: field kind only; columns col (keys), col + 1 (values)
+                 KXP_K_LSTRUCT = 7 };  // list/set<S>, S of fixed scalars: field kind only; columns col ..
+                                       // col + width - 1 (one per field of S, mside 3, sel_* below)
 
 struct KxpField {      // 16 B
   int16_t id;
@@ -63,7 +65,7 @@ struct KxpCol {        // 16 B
   int8_t field;        // flat field
   uint8_t ttype;
   uint8_t vslot2;      // LISTB: the bytes slot, else 0xff
-  uint8_t mside;       // 1: map keys, 2: map values, 0: not a map side
+  uint8_t mside;       // 1: map keys, 2: map values, 3: a field of a list<struct> element, 0: neither
   int64_t defv;        // FIXED default (bits)
 };
 
@@ -104,6 +106,12 @@ struct KxProgram {
   // Protobuf canonical plan: one step per root field in field-number order (proto.Marshal's order);
   // hdr = tag bytes (bits 0-15) | tag length (16-17) | bool (bit 24) | bytes, no UTF-8 check (25)
   KxpStep pbsteps[KXP_MAX_FIELDS];
+  // list<struct> element fields, per column (mside 3): the field id in S, required (1) or not, and the
+  // column of S's first field (the element walker scans S's fields sel_first .. sel_first + n - 1)
+  int16_t sel_id[KXP_MAX_COLS];
+  uint8_t sel_req[KXP_MAX_COLS];
+  uint8_t sel_first[KXP_MAX_COLS];
+  uint8_t sel_n[KXP_MAX_COLS];
 };
 
 static_assert(sizeof(KxpField) == 16, "KxpField layout");

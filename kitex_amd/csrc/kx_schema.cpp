@@ -44,6 +44,7 @@ struct Builder {
   std::vector<std::vector<PendField>> inst_fields;
   std::vector<int> inst_parent, inst_self;  // self: index into parent's field list
   int stack[8];
+  int64_t sel_def[KX_MAX_COLUMNS] = {};     // list<struct> element field defaults, per column
 
   int rec(int sidx, int depth, int parent, int self_idx, int16_t* path, int* out) {
     if (sidx < 0 || (uint32_t)sidx >= nstructs) return KX_ERR_INVALID_ARG;
@@ -94,7 +95,40 @@ struct Builder {
             ci.elem_ttype = KX_T_STRING;
             break;
           }
-          if (type_size(f->elem_ttype) == 0) return KX_ERR_NOT_IMPLEMENTED;  // list<struct|container>
+          if (f->elem_ttype == KX_T_STRUCT) {  // list/set<S> of fixed scalars: one LIST column per field of S
+            if (f->child < 0 || (uint32_t)f->child >= nstructs || depth + 1 >= 8) return KX_ERR_NOT_IMPLEMENTED;
+            const kx_struct_desc& es = structs[f->child];
+            if (es.nfields == 0 || es.nfields > 8 || !es.fields || s->ncols + es.nfields > KX_MAX_COLUMNS)
+              return KX_ERR_NOT_IMPLEMENTED;
+            for (uint32_t k = 0; k < es.nfields; k++) {
+              const kx_field_desc& g = es.fields[k];
+              for (uint32_t j = 0; j < k; j++)
+                if (es.fields[j].id == g.id) return KX_ERR_INVALID_ARG;
+              if (type_size(g.ttype) == 0 || g.req == KX_REQ_OPTIONAL) return KX_ERR_NOT_IMPLEMENTED;
+              if (g.req > KX_REQ_OPTIONAL) return KX_ERR_INVALID_ARG;
+            }
+            pf.col = (int)s->ncols;
+            KxProgram& P = s->prog;
+            for (uint32_t k = 0; k < es.nfields; k++) {
+              const kx_field_desc& g = es.fields[k];
+              kx_column_info cs = ci;
+              cs.kind = KX_COL_LIST;
+              cs.width = (uint32_t)type_size(g.ttype);
+              cs.elem_ttype = (uint8_t)(g.ttype | KX_ELEM_STRUCT_FIELD);
+              cs.field_id = g.id;
+              cs.depth = (uint32_t)depth + 1;
+              cs.path[depth + 1] = g.id;
+              P.sel_id[s->ncols] = g.id;
+              P.sel_req[s->ncols] = g.req == KX_REQ_REQUIRED ? 1 : 0;
+              P.sel_first[s->ncols] = (uint8_t)pf.col;
+              P.sel_n[s->ncols] = (uint8_t)es.nfields;
+              sel_def[s->ncols] = g.default_bits;
+              s->info[s->ncols++] = cs;
+            }
+            inst_fields[me].push_back(pf);
+            continue;
+          }
+          if (type_size(f->elem_ttype) == 0) return KX_ERR_NOT_IMPLEMENTED;  // list<container>
           ci.kind = KX_COL_LIST;
           ci.width = (uint32_t)type_size(f->elem_ttype);
           ci.elem_ttype = f->elem_ttype;
@@ -178,7 +212,8 @@ int kx_build_program(const kx_struct_desc* structs, uint32_t nstructs, kx_schema
     kc.ttype = ci.ttype;
     kc.vslot = 0xff;
     kc.vslot2 = 0xff;
-    kc.mside = ci.ttype == KX_T_MAP ? ((ci.elem_ttype & KX_ELEM_MAP_VALUE) ? 2 : 1) : 0;
+    kc.mside = ci.ttype == KX_T_MAP ? ((ci.elem_ttype & KX_ELEM_MAP_VALUE) ? 2 : 1)
+             : (ci.elem_ttype & KX_ELEM_STRUCT_FIELD) ? 3 : 0;
     if (ci.kind != KX_COL_FIXED) {
       if (nvar + (ci.kind == KX_COL_LIST_BYTES ? 2 : 1) > KXP_NV_MAX) return KX_ERR_NOT_IMPLEMENTED;
       kc.vslot = (uint8_t)nvar;
@@ -219,7 +254,16 @@ int kx_build_program(const kx_struct_desc* structs, uint32_t nstructs, kx_schema
       F.flags = d->reserved0;
       F.pb_wt = (uint8_t)pb_wire_type(d->ttype);
       F.enc_next = -1;
-      if (fl[k].col >= 0) {
+      if (fl[k].col >= 0 && P.col[fl[k].col].mside == 3) {  // list<struct>: width = fields of S
+        const int c0 = fl[k].col, ns = P.sel_n[c0];
+        F.kind = KXP_K_LSTRUCT;
+        F.width = (uint8_t)ns;
+        F.vslot = P.col[c0].vslot;
+        for (int c = c0; c < c0 + ns; c++) {
+          P.col[c].field = (int8_t)ff;
+          P.col[c].defv = b.sel_def[c];
+        }
+      } else if (fl[k].col >= 0) {
         const KxpCol& kc = P.col[fl[k].col];
         F.kind = d->ttype == KX_T_MAP ? KXP_K_MAP : kc.kind;
         F.width = kc.width;
@@ -247,7 +291,7 @@ int kx_build_program(const kx_struct_desc* structs, uint32_t nstructs, kx_schema
       m |= 1ull << (I.first + k);
       if (F.pbit >= 0) pm |= 1ull << F.pbit;
       if (F.col >= 0)  // every var slot of the field's columns (map: both sides; LISTB: both slots)
-        for (int cc = F.col; cc <= F.col + (F.kind == KXP_K_MAP ? 1 : 0); cc++) {
+        for (int cc = F.col; cc <= F.col + (F.kind == KXP_K_MAP ? 1 : F.kind == KXP_K_LSTRUCT ? F.width - 1 : 0); cc++) {
           if (P.col[cc].vslot != 0xff) vm |= (uint8_t)(1u << P.col[cc].vslot);
           if (P.col[cc].vslot2 != 0xff) vm |= (uint8_t)(1u << P.col[cc].vslot2);
         }
@@ -336,7 +380,7 @@ int kx_build_program(const kx_struct_desc* structs, uint32_t nstructs, kx_schema
     mn += 3;
     if (F.kind == KXP_K_FIXED) mn += F.width;
     else if (F.kind == KXP_K_BYTES) mn += 4;
-    else if (F.kind == KXP_K_LIST || F.kind == KXP_K_LISTB) mn += 5;
+    else if (F.kind == KXP_K_LIST || F.kind == KXP_K_LISTB || F.kind == KXP_K_LSTRUCT) mn += 5;
     else if (F.kind == KXP_K_MAP) mn += 6;
     else mn += 1;
   }
@@ -357,7 +401,10 @@ int kx_build_program(const kx_struct_desc* structs, uint32_t nstructs, kx_schema
       const KxpInst& I = P.inst[i];
       for (int f = I.enc_first; f >= 0; f = P.f[f].enc_next) {
         const KxpField& F = P.f[f];
-        if (F.req == KX_REQ_OPTIONAL || F.kind == KXP_K_LISTB || F.kind == KXP_K_MAP) { ok = false; return; }
+        if (F.req == KX_REQ_OPTIONAL || F.kind == KXP_K_LISTB || F.kind == KXP_K_MAP || F.kind == KXP_K_LSTRUCT) {
+          ok = false;
+          return;
+        }
         KxpStep st{};
         st.hdr = (uint32_t)F.ttype | ((uint32_t)((uint16_t)F.id >> 8) << 8) | ((uint32_t)(F.id & 0xff) << 16);
         st.col = F.col;

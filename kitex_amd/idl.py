@@ -12,8 +12,8 @@ front end for the batch codec:
                                     them and k-mock.go:422-517 generates them)
   to_schema(struct descriptor)   -> kitex_amd.schema.Schema (the flattened table kx_schema_create takes)
 
-Shapes the device codec does not hold (list/set/map of structs, nested containers, recursive structs,
-non-empty string defaults) raise NotImplementedError at compile time, the Python face of
+Shapes the device codec does not hold (maps of structs, lists of structs with string / nested / optional
+fields, nested containers, recursive structs, non-empty string defaults) raise NotImplementedError at compile time, the Python face of
 KX_ERR_NOT_IMPLEMENTED. Supported grammar: namespace / include / cpp_include, typedef, const (skipped),
 enum (-> i32), struct / union / exception, service (extends, oneway, throws), annotations `(k = "v")`,
 `//`, `#` and `/* */` comments, `,` / `;` separators.
@@ -469,9 +469,19 @@ def _field(fd: FieldDescriptor, stack) -> Field:
     if td.type == A.T_STRUCT:
         f.child = _struct_of(td.struct, stack)
     elif td.type in (A.T_LIST, A.T_SET):
-        if td.elem.type not in _LEAF:
-            raise NotImplementedError(f"field {fd.name}: {td.name}<{td.elem.name}> (only scalar / string elements)")
-        f.elem = td.elem.type
+        if td.elem.type == A.T_STRUCT:  # list<S>: S of fixed-width, non-optional scalars (kxcodec.h)
+            es = td.elem.struct
+            bad = [g.name for g in es.fields if g.type.type not in _LEAF or g.type.type == A.T_STRING or g.optional]
+            if bad or not es.fields:
+                raise NotImplementedError(f"field {fd.name}: {td.name}<{es.name}> (element fields must be fixed-width, "
+                                          f"non-optional scalars; not {bad})")
+            f.elem = A.T_STRUCT
+            f.child = _struct_of(es, stack)
+        elif td.elem.type not in _LEAF:
+            raise NotImplementedError(f"field {fd.name}: {td.name}<{td.elem.name}> (only scalar / string / "
+                                      "fixed-struct elements)")
+        else:
+            f.elem = td.elem.type
     elif td.type == A.T_MAP:
         if td.key.type not in _LEAF or td.elem.type not in _LEAF:
             raise NotImplementedError(f"field {fd.name}: map<{td.key.name},{td.elem.name}> (only scalar / string "

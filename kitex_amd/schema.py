@@ -137,4 +137,16 @@ def schema_cx2() -> Schema:
                                  Field(7, A.T_MAP, "names", elem=A.T_I32, val=A.T_STRING, req=A.REQ_OPTIONAL)]))
 
 
+def schema_ls1() -> Schema:
+    """list<struct>: Point{1: i64 x; 2: required i32 y; 3: double w = 1.5; 4: bool b} in a list and a set
+    next to an i64 (internal/mocks style; FieldFastReadList of structs, struct_tpl.go:583-625)."""
+    import struct as _st
+    pt = Struct("Point", [Field(1, A.T_I64, "x"), Field(2, A.T_I32, "y", req=A.REQ_REQUIRED),
+                          Field(3, A.T_DOUBLE, "w", default=_st.unpack("<q", _st.pack("<d", 1.5))[0]),
+                          Field(4, A.T_BOOL, "b")])
+    tag = Struct("Tag", [Field(7, A.T_I16, "k"), Field(9, A.T_BYTE, "v")])
+    return Schema(Struct("LS1", [Field(1, A.T_I64, "id"), Field(2, A.T_LIST, "pts", elem=A.T_STRUCT, child=pt),
+                                 Field(3, A.T_SET, "tags", elem=A.T_STRUCT, child=tag, req=A.REQ_OPTIONAL)]))
+
+
 SCHEMAS = {"r1": schema_r1, "r2": schema_r2, "r3": schema_r3, "pf": schema_pf}

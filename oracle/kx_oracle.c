@@ -544,6 +544,8 @@ typedef struct {
   int varidx2[KX_MAX_COLUMNS]; /* LIST_BYTES column -> its bytes slot, else -1 */
   uint8_t mside[KX_MAX_COLUMNS]; /* 1: map key column, 2: map value column, 0: neither */
   uint8_t mkt[KX_MAX_COLUMNS], mvt[KX_MAX_COLUMNS]; /* map key / value types (map columns) */
+  uint8_t sside[KX_MAX_COLUMNS];  /* list<struct> element field column: 1 + index of the field in S */
+  const kx_struct_desc* ssd[KX_MAX_COLUMNS];  /* ... and S */
   int is_pb;
 } plan_t;
 
@@ -582,7 +584,30 @@ static int flatten_rec(plan_t* p, int sidx, int depth, int16_t* path, int* stack
         if (f->elem_ttype == KX_T_STRING) {                /* list/set<string>: FieldFastReadList (:582-625) */
           ci.kind = KX_COL_LIST_BYTES; ci.width = 1; ci.elem_ttype = KX_T_STRING; break;
         }
-        if (type_size(f->elem_ttype) == 0) return KX_ERR_NOT_IMPLEMENTED;  /* list<struct|container> */
+        if (f->elem_ttype == KX_T_STRUCT) {                /* list/set<S>: one LIST column per field of S */
+          if (f->child < 0 || (uint32_t)f->child >= p->nstructs || depth + 1 >= 8) return KX_ERR_NOT_IMPLEMENTED;
+          const kx_struct_desc* es = &p->structs[f->child];
+          if (es->nfields == 0 || es->nfields > 8 || p->ncols + es->nfields > KX_MAX_COLUMNS)
+            return KX_ERR_NOT_IMPLEMENTED;
+          for (uint32_t k = 0; k < es->nfields; k++) {
+            const kx_field_desc* g = &es->fields[k];
+            for (uint32_t j = 0; j < k; j++) if (es->fields[j].id == g->id) return KX_ERR_INVALID_ARG;
+            if (type_size(g->ttype) == 0 || g->req == KX_REQ_OPTIONAL) return KX_ERR_NOT_IMPLEMENTED;
+            if (g->req > KX_REQ_OPTIONAL) return KX_ERR_INVALID_ARG;
+          }
+          m->col = (int)p->ncols;
+          for (uint32_t k = 0; k < es->nfields; k++) {
+            const kx_field_desc* g = &es->fields[k];
+            kx_column_info cs = ci;
+            cs.kind = KX_COL_LIST; cs.width = (uint32_t)type_size(g->ttype);
+            cs.elem_ttype = (uint8_t)(g->ttype | KX_ELEM_STRUCT_FIELD);
+            cs.field_id = g->id; cs.depth = (uint32_t)depth + 1; cs.path[depth + 1] = g->id;
+            p->sside[p->ncols] = (uint8_t)(1 + k); p->ssd[p->ncols] = es;
+            p->cols[p->ncols++] = cs;
+          }
+          continue;
+        }
+        if (type_size(f->elem_ttype) == 0) return KX_ERR_NOT_IMPLEMENTED;  /* list<container> */
         ci.kind = KX_COL_LIST; ci.width = (uint32_t)type_size(f->elem_ttype); ci.elem_ttype = f->elem_ttype; break;
       case KX_T_MAP: {                                     /* FieldFastReadMap (:466-533): keys, values columns */
         const uint8_t kt = f->elem_ttype & 15, vt = (uint8_t)(f->elem_ttype >> 4);
@@ -684,7 +709,10 @@ static void set_defaults(dec_t* d, int inst) {
     if (m->inst >= 0) { set_defaults(d, m->inst); continue; }
     if (d->p->cols[m->col].kind == KX_COL_FIXED) store_fixed(d, m->col, (uint64_t)sd->fields[i].default_bits);
     else {
-      const int nc = sd->fields[i].ttype == KX_T_MAP ? 2 : 1;
+      const kx_field_desc* f = &sd->fields[i];
+      const int nc = f->ttype == KX_T_MAP ? 2
+                   : (f->ttype == KX_T_LIST || f->ttype == KX_T_SET) && f->elem_ttype == KX_T_STRUCT
+                     ? (int)d->p->structs[f->child].nfields : 1;
       for (int k = 0; k < nc; k++) { d->vptr[m->col + k] = NULL; d->vlen[m->col + k] = 0; d->vbytes[m->col + k] = 0; }
     }
   }
@@ -704,6 +732,41 @@ static uint64_t read_scalar(uint8_t t, const uint8_t* b) {
     case KX_T_I32: return be32(b);
     default: return be64(b);
   }
+}
+
+/* One element of a list<S> (S: fixed-width scalar fields): S's FastRead (struct_tpl.go:41-149) over
+ * [b, b + len): fields until STOP, unknown / mistyped ids skipped, the last duplicate wins, required
+ * fields checked. want >= 0: *val = the value of S's field `want`, or its default when absent. */
+static int read_elem_struct(const kx_struct_desc* es, const uint8_t* b, size_t len, size_t* used, int want,
+                            uint64_t* val) {
+  uint64_t isset = 0;
+  size_t off = 0;
+  if (want >= 0) *val = (uint64_t)es->fields[want].default_bits;
+  for (;;) {
+    if (len - off < 1) return KX_ERR_EOF;
+    uint8_t t = b[off];
+    if (t == KX_T_STOP) { off += 1; break; }
+    if (len - off < 3) return KX_ERR_EOF;
+    int16_t id = (int16_t)be16(b + off + 1);
+    off += 3;
+    int fi = find_field(es, id);
+    if (fi < 0 || es->fields[fi].ttype != t) {
+      size_t u = 0;
+      int rc = kxo_skip(b + off, len - off, t, 64, &u);
+      if (rc) return rc;
+      off += u;
+      continue;
+    }
+    size_t w = (size_t)type_size(t);
+    if (len - off < w) return KX_ERR_EOF;
+    if (fi == want) *val = read_scalar(t, b + off);
+    off += w;
+    isset |= 1ull << fi;
+  }
+  for (uint32_t i = 0; i < es->nfields; i++)
+    if (es->fields[i].req == KX_REQ_REQUIRED && !(isset & (1ull << i))) return KX_ERR_INVALID_DATA;
+  *used = off;
+  return KX_OK;
 }
 
 static int read_struct(dec_t* d, int inst, const uint8_t* b, size_t len, size_t* used) {
@@ -752,6 +815,22 @@ static int read_struct(dec_t* d, int inst, const uint8_t* b, size_t len, size_t*
         if (rem < 5) return KX_ERR_EOF;
         int32_t n = (int32_t)be32(v + 1);
         if (n < 0) return KX_ERR_NEGATIVE_SIZE;
+        if (f->elem_ttype == KX_T_STRUCT) {                /* n x S.FastRead (FieldFastReadList :583-625) */
+          const kx_struct_desc* es = &d->p->structs[f->child];
+          size_t q = 5;
+          for (int32_t j = 0; j < n; j++) {
+            size_t u = 0;
+            uint64_t dummy;
+            int rc = read_elem_struct(es, v + q, rem - q, &u, -1, &dummy);
+            if (rc) return rc;
+            q += u;
+          }
+          for (uint32_t k = 0; k < es->nfields; k++) {
+            d->vptr[m->col + k] = v + 5; d->vlen[m->col + k] = (uint64_t)n; d->vbytes[m->col + k] = 0;
+          }
+          off += q;
+          break;
+        }
         if (f->elem_ttype == KX_T_STRING) {                /* n x ReadString */
           size_t q = 5;
           uint64_t bytes = 0;
@@ -844,6 +923,15 @@ static void emit_container(dec_t* d, uint32_t c, uint64_t* cursor, int* overflow
     for (uint64_t j = 0; j < n; j++) {
       const uint8_t *kd, *vd, *x;
       uint64_t kl, vl, xl;
+      if (p->sside[c]) {  /* list<S>: this column's field of element j, or its default */
+        size_t u = 0;
+        uint64_t v = 0;
+        (void)read_elem_struct(p->ssd[c], q, (size_t)-1 / 2, &u, p->sside[c] - 1, &v);  /* validated */
+        q += u;
+        const uint32_t w = p->cols[c].width;
+        memcpy((uint8_t*)col->data + (E + j) * w, &v, w);
+        continue;
+      }
       if (p->mside[c]) {
         q = elem_at(q, p->mkt[c], &kd, &kl);
         q = elem_at(q, p->mvt[c], &vd, &vl);
@@ -877,7 +965,7 @@ static int emit_record_tail(dec_t* d, uint64_t* cursor, int* overflow) {
     if (vs < 0) continue;
     const kx_column* col = &d->out->cols[c];
     uint64_t n = d->vlen[c];
-    if (p->cols[c].kind == KX_COL_LIST_BYTES || p->mside[c]) {  /* element by element */
+    if (p->cols[c].kind == KX_COL_LIST_BYTES || p->mside[c] || p->sside[c]) {  /* element by element */
       emit_container(d, c, cursor, overflow);
       continue;
     }
@@ -1164,6 +1252,33 @@ static uint64_t write_struct(enc_t* e, int inst, uint64_t pres, uint8_t* b) {
               const uint64_t a0 = eoff_get(c, E + k), l = eoff_get(c, E + k + 1) - a0;
               if (b) kxo_write_string(b + off, (const uint8_t*)c->data + a0, (uint32_t)l);
               off += 4 + l;
+            }
+            break;
+          }
+          if (f->elem_ttype == KX_T_STRUCT) {                  /* FieldFastWriteList of S: fields, STOP */
+            const kx_struct_desc* es = &e->p->structs[f->child];
+            if (b) kxo_write_list_begin(b + off, KX_T_STRUCT, (int32_t)n);
+            off += 5;
+            for (uint64_t k = 0; k < n; k++) {
+              for (uint32_t g = 0; g < es->nfields; g++) {
+                const kx_column* c = &e->in->cols[m->col + g];
+                const uint8_t t = es->fields[g].ttype;
+                const int w = type_size(t);
+                uint64_t v = 0;
+                memcpy(&v, (const uint8_t*)c->data + (off_get(c, e->rec) + k) * (uint64_t)w, (size_t)w);
+                if (b) {
+                  kxo_write_field_begin(b + off, t, es->fields[g].id);
+                  uint8_t* q = b + off + 3;
+                  if (t == KX_T_BOOL) q[0] = v ? 1 : 0;
+                  else if (w == 1) q[0] = (uint8_t)v;
+                  else if (w == 2) put16(q, (uint16_t)v);
+                  else if (w == 4) put32(q, (uint32_t)v);
+                  else put64(q, v);
+                }
+                off += 3 + (uint64_t)w;
+              }
+              if (b) b[off] = KX_T_STOP;
+              off += 1;
             }
             break;
           }

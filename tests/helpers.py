@@ -100,15 +100,19 @@ def random_columns(infos, npres, n, seed=0):
     fixed = {1: np.uint8, 2: np.int16, 4: np.int32, 8: np.int64}
     cols, counts = [], None
     for c, ci in enumerate(infos):
-        is_val = bool(ci.elem_ttype & A.ELEM_MAP_VALUE) if hasattr(A, "ELEM_MAP_VALUE") else bool(ci.elem_ttype & 0x80)
-        et = ci.elem_ttype & 0x7F
+        is_val = bool(ci.elem_ttype & 0x80)
+        # a list<struct> element field after the first of its list shares that list's counts
+        if ci.elem_ttype & 0x40 and c > 0 and infos[c - 1].elem_ttype & 0x40 and \
+                list(infos[c - 1].path[:ci.depth]) == list(ci.path[:ci.depth]):
+            is_val = True
+        et = ci.elem_ttype & 0x3F
         if ci.kind == A.COL_FIXED:
             v = rng.integers(0, 2, size=n) if ci.ttype == A.T_BOOL else rng.integers(-(1 << 62), 1 << 62, size=n)
             cols.append(v.astype(fixed[ci.width]))
             continue
         cnt = counts if is_val else rng.integers(0, 6 if ci.kind == A.COL_LIST else 5 if ci.kind == A.COL_LIST_BYTES
                                                  else 41, size=n)
-        if ci.ttype == A.T_MAP and not is_val:
+        if (ci.ttype == A.T_MAP or ci.elem_ttype & 0x40) and not is_val:
             counts = cnt
         offs = np.zeros(n + 1, dtype=np.uint32)
         offs[1:] = np.cumsum(cnt)

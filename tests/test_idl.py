@@ -46,7 +46,7 @@ def test_baseline_simple_and_nesting():
     assert [(f.id, f.ttype) for f in fields] == [(1, A.T_BYTE), (2, A.T_I64), (3, A.T_DOUBLE), (4, A.T_I32),
                                                 (5, A.T_STRING), (6, A.T_STRING)]
     assert fields[5].binary and not fields[4].binary
-    with pytest.raises(NotImplementedError, match="list<Simple>"):
+    with pytest.raises(NotImplementedError, match="list<Simple>"):  # Simple holds strings
         idl.request_schema(doc, "NestingMethod")
 
 
@@ -115,3 +115,13 @@ def test_idl_schema_creates_and_round_trips(oracle):
     rc, out, st, rs = oracle.decode(base, wire, 300, offsets=offs)
     assert rc == 0 and st.code == 0
     assert_columns_equal(out, cs, infos, 300, check_presence=False)
+
+
+def test_list_of_fixed_structs_compiles():
+    doc = idl.parse_idl("""
+        struct Point { 1: i64 x; 2: required i32 y; 3: double w = 1.5; 4: bool b }
+        struct Tag { 7: i16 k; 9: byte v }
+        struct LS1 { 1: i64 id; 2: list<Point> pts; 3: optional set<Tag> tags }
+        service S { void put(1: LS1 r) }
+    """)
+    assert _table_bytes(idl.request_schema(doc, "put")) == _table_bytes(S.schema_ls1())
