@@ -454,6 +454,16 @@ def extras(args, r2, dev, local):
             out["r2_decode_views"] = {"records": bv.n, "out_bytes_per_record": bv.out_bytes_per_record(), **e}
             del bv
             torch.cuda.empty_cache()
+            # known message lengths (fastUnmarshal with dataLen, codec_fast.go:60-71): the u64 offsets array
+            # is read too, so it counts in the algorithmic bytes (8 B / record)
+            bo = Batch("r2", r2.n, dev, 0, "offsets", local)
+            e = decode_entry(bo)
+            avg = e["roofline"]["avg_launch_ms"] / 1e3
+            e["roofline"] = roofline(bo.in_bytes + 8 * (bo.n + 1) + bo.out_bytes_per_record() * bo.n, avg,
+                                     "decode (known offsets)")
+            out["r2_decode_offsets"] = {"records": bo.n, **e}
+            del bo
+            torch.cuda.empty_cache()
         b3 = Batch("r3", 4 << 20, dev, 0, "concat", local)
         out["r3_decode"] = {"records": b3.n, "wire_bytes_per_record": b3.in_bytes / b3.n, **decode_entry(b3)}
         out["r3_encode"] = {"records": b3.n, **encode_entry(b3)}
