@@ -570,12 +570,46 @@ __device__ __forceinline__ int generic_record(const Src& w, const KAS KxProgram*
   int inst = 0;
   int pred = P->inst[0].enc_first;
   uint64_t seen = 0;
+  // inside a list<S> field (S of fixed scalars): its elements are read by this same loop (one skip
+  // decoder instance per kernel: a second inlined copy doubled the index pass's scratch and halved it)
+  uint32_t lrem = 0, lisset = 0, lcnt = 0, lcol = 0, lns = 0;
+  int lfi = 0, lpbit = -1;
+  uint64_t lstart = 0;
   for (;;) {
     if (pos >= limit) return KX_ERR_EOF;
     const Fetch fx = fetch12(w, pos);
     KxpField F = ld_field(P, pred >= 0 ? pred : 0);
     const uint32_t t = fx.w0 & 0xff;
-    if (t == KX_T_STOP) {
+    int fi = -1;
+    if (lrem) {  // an element of list<S>: S.FastRead (struct_tpl.go:41-149)
+      if (t == KX_T_STOP) {
+        pos += 1;
+        for (uint32_t j = 0; j < lns; j++)
+          if (P->sel_req[lcol + j] && !((lisset >> j) & 1)) return KX_ERR_INVALID_DATA;
+        lisset = 0;
+        if (--lrem == 0) {
+          for (uint32_t k = 0; k < lns; k++) vset<NV>(vs, ldk(&P->col[lcol + k]).vslot, lstart, lcnt);
+          seen |= 1ull << lfi;
+          if (lpbit >= 0) pres |= 1ull << lpbit;
+        }
+        continue;
+      }
+      if (limit - pos < 3) return KX_ERR_EOF;
+      const int16_t eid = (int16_t)((((fx.w0 >> 8) & 0xffu) << 8) | ((fx.w0 >> 16) & 0xffu));
+      int k = -1;
+      for (uint32_t j = 0; j < lns; j++)
+        if (P->sel_id[lcol + j] == eid) { k = (int)j; break; }
+      if (k >= 0) {
+        const KxpCol K = ldk(&P->col[lcol + k]);
+        if (K.elem == t) {
+          if (limit - pos - 3 < K.width) return KX_ERR_EOF;
+          pos += 3 + K.width;
+          lisset |= 1u << k;
+          continue;
+        }
+      }
+      // an unknown or mistyped element field: the skip decoder below
+    } else if (t == KX_T_STOP) {
       pos += 1;
       const KxpInst I = ld_inst(P, inst);
       if ((seen & I.req_mask) != I.req_mask) return KX_ERR_INVALID_DATA;  // RequiredFieldNotSetError (struct_tpl.go:124-145)
@@ -586,8 +620,8 @@ __device__ __forceinline__ int generic_record(const Src& w, const KAS KxProgram*
     }
     if (limit - pos < 3) return KX_ERR_EOF;
     const int id = (int)(int16_t)((((fx.w0 >> 8) & 0xffu) << 8) | ((fx.w0 >> 16) & 0xffu));
-    int fi = -1;
-    if (pred >= 0 && F.id == id) {
+    if (lrem) {
+    } else if (pred >= 0 && F.id == id) {
       fi = pred;
     } else {
       const KxpInst I = ld_inst(P, inst);
@@ -672,13 +706,13 @@ __device__ __forceinline__ int generic_record(const Src& w, const KAS KxProgram*
       if (limit - vp < 5) return KX_ERR_EOF;
       const int32_t l = (int32_t)__builtin_bswap32(fx.w1);
       if (l < 0) return KX_ERR_NEGATIVE_SIZE;
-      uint64_t q = vp + 5, v0;
-      for (int32_t j = 0; j < l; j++) {
-        const int rc = elem_struct(w, P, (uint32_t)F.col, F.width, q, limit, &q, -1, &v0);
-        if (rc) return rc;
+      pos = vp + 5;
+      if (l > 0) {  // the elements follow through this loop; the list is recorded after its last one
+        lrem = (uint32_t)l; lcnt = (uint32_t)l; lisset = 0;
+        lcol = (uint32_t)F.col; lns = F.width; lfi = fi; lpbit = F.pbit; lstart = pos;
+        continue;
       }
-      for (uint32_t k = 0; k < F.width; k++) vset<NV>(vs, ldk(&P->col[F.col + k]).vslot, vp + 5, (uint32_t)l);
-      pos = q;
+      for (uint32_t k = 0; k < F.width; k++) vset<NV>(vs, ldk(&P->col[F.col + k]).vslot, pos, 0u);
     } else if (F.kind == KXP_K_LIST) {                       // ReadListBegin: elem type ignored (:587)
       if (limit - vp < 5) return KX_ERR_EOF;
       const int32_t l = (int32_t)__builtin_bswap32(fx.w1);
@@ -2297,7 +2331,7 @@ __device__ __forceinline__ void emit_container(const Src& w, const KAS KxProgram
 
 // ---- kernel 3: emit pass (one wave per tile, lane = record) ----
 template <int NV, int MODE>
-__global__ void __launch_bounds__(NT) emit_kernel(DecParams dp_) {
+__global__ void __launch_bounds__(NT, 4) emit_kernel(DecParams dp_) {  // 4 waves per SIMD: <= 128 VGPRs
   KParams& dp = KX_PARAMS();
   (void)dp_;
   __shared__ __attribute__((aligned(16))) uint32_t WIN[WAVES][WINW];

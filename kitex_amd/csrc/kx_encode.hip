@@ -68,7 +68,10 @@ __device__ __forceinline__ uint64_t side_bytes(const KxProgram& P, const KxLaunc
 }
 
 // BLength (struct_tpl.go:266-391)
-__device__ uint64_t record_size(const KxProgram& P, const KxLaunchCols& C, uint64_t r) {
+// LS: the schema has list<struct> fields (a separate instantiation: the extra branch changes the
+// register allocation of the write pass, which ran 2.4x slower for every schema with it compiled in)
+template <bool LS>
+__device__ __forceinline__ uint64_t record_size(const KxProgram& P, const KxLaunchCols& C, uint64_t r) {
   uint64_t pres = C.presence ? C.presence[r] : 0;
   int inst = 0;
   int f = P.inst[0].enc_first;
@@ -87,7 +90,7 @@ __device__ uint64_t record_size(const KxProgram& P, const KxLaunchCols& C, uint6
     if (F.kind == KXP_K_FIXED) sz += F.width;
     else if (F.kind == KXP_K_BYTES) sz += 4 + var_len(C, F.col, r);
     else if (F.kind == KXP_K_LIST) sz += 5 + var_len(C, F.col, r) * F.width;
-    else if (F.kind == KXP_K_LSTRUCT) {  // list/set<S>: every field of S + STOP per element
+    else if (LS && F.kind == KXP_K_LSTRUCT) {  // list/set<S>: every field of S + STOP per element
       uint64_t es = 1;
       for (int c = F.col; c < F.col + F.width; c++) es += 3 + P.col[c].width;
       sz += 5 + var_len(C, F.col, r) * es;
@@ -188,7 +191,8 @@ __device__ __forceinline__ void put_bytes(Sink& s, const uint8_t* src, uint32_t 
 }
 
 // FastWriteNocopy for one record into the sink
-__device__ void write_record(const KxProgram& P, const KxLaunchCols& C, uint64_t r, Sink& s) {
+template <bool LS>
+__device__ __forceinline__ void write_record(const KxProgram& P, const KxLaunchCols& C, uint64_t r, Sink& s) {
   uint64_t pres = C.presence ? C.presence[r] : 0;
   int inst = 0;
   int f = P.inst[0].enc_first;
@@ -225,10 +229,9 @@ __device__ void write_record(const KxProgram& P, const KxLaunchCols& C, uint64_t
         if (F.elem == KX_T_BOOL) v = (v & 0xff) ? 1 : 0;
         put_be(s, v, F.width);
       }
-    } else if (F.kind == KXP_K_LSTRUCT) {
+    } else if (LS && F.kind == KXP_K_LSTRUCT) {
       // FieldFastWriteList of S (struct_tpl.go:1011-1036): S.FastWriteNocopy per element, every field of
       // S in IDL order (all fixed-length: the encoder reorder keeps it), then STOP
-      const uint64_t o = off_at(C, F.col, r);
       const uint32_t cnt = (uint32_t)var_len(C, F.col, r);
       s.put(KX_T_STRUCT, 1);
       put_be(s, cnt, 4);
@@ -243,7 +246,6 @@ __device__ void write_record(const KxProgram& P, const KxLaunchCols& C, uint64_t
         }
         s.put(KX_T_STOP, 1);
       }
-      (void)o;
     } else if (F.kind == KXP_K_LISTB || F.kind == KXP_K_MAP) {
       // FieldFastWriteList of strings / FieldFastWriteMap (struct_tpl.go:875-912, 1011-1036); a map
       // in column order (Go iterates its maps in random order)
@@ -308,7 +310,7 @@ __device__ __forceinline__ uint64_t pb_value(const KxpField& F, const KxLaunchCo
   return v;
 }
 
-__device__ uint64_t pb_body_size(const KxProgram& P, const KxLaunchCols& C, uint64_t r) {
+__device__ __forceinline__ uint64_t pb_body_size(const KxProgram& P, const KxLaunchCols& C, uint64_t r) {
   const uint64_t pres = C.presence ? C.presence[r] : 0;
   uint64_t sz = 0;
   for (int f = P.pb_first; f >= 0; f = P.f[f].pb_next) {
@@ -334,7 +336,7 @@ __device__ __forceinline__ uint64_t pb_record_size(const KxProgram& P, const KxL
   return 1 + uvarint_len(b) + b;
 }
 
-__device__ void pb_write_record(const KxProgram& P, const KxLaunchCols& C, uint64_t r, Sink& s) {
+__device__ __forceinline__ void pb_write_record(const KxProgram& P, const KxLaunchCols& C, uint64_t r, Sink& s) {
   s.put(0x0Au, 1);
   put_uvarint(s, pb_body_size(P, C, r));
   const uint64_t pres = C.presence ? C.presence[r] : 0;
@@ -364,13 +366,15 @@ __device__ void pb_write_record(const KxProgram& P, const KxLaunchCols& C, uint6
   s.flush();
 }
 
+template <bool LS>
 __device__ __forceinline__ uint64_t any_size(const EncParams& ep, const KxProgram& P, uint64_t r) {
-  return ep.pb ? pb_record_size(P, ep.cols, r) : record_size(P, ep.cols, r);
+  return ep.pb ? pb_record_size(P, ep.cols, r) : record_size<LS>(P, ep.cols, r);
 }
 
+template <bool LS>
 __device__ __forceinline__ void any_write(const EncParams& ep, const KxProgram& P, uint64_t r, Sink& s) {
   if (ep.pb) pb_write_record(P, ep.cols, r, s);
-  else write_record(P, ep.cols, r, s);
+  else write_record<LS>(P, ep.cols, r, s);
 }
 
 __device__ __forceinline__ uint64_t wave_incl_scan(uint64_t v, int lane) {
@@ -398,6 +402,7 @@ __device__ uint64_t block_excl_scan(uint64_t v, uint64_t* tot, uint64_t* scratch
   return base + inc - v;
 }
 
+template <bool LS>
 __global__ void __launch_bounds__(NT) size_kernel(EncParams ep) {
   __shared__ uint64_t scratch[NT / 64];
   __shared__ uint32_t progw[sizeof(KxProgram) / 4];
@@ -410,7 +415,7 @@ __global__ void __launch_bounds__(NT) size_kernel(EncParams ep) {
     uint64_t r = b * RB + k * NT + threadIdx.x;
     uint64_t sz = 0;
     if (r < ep.n) {
-      sz = any_size(ep, P, r);
+      sz = any_size<LS>(ep, P, r);
       if (ep.sizes_out) ep.sizes_out[r] = sz;
     }
     acc += sz;
@@ -443,6 +448,7 @@ __global__ void __launch_bounds__(1024) scan_kernel(EncParams ep) {
   }
 }
 
+template <bool LS>
 __global__ void __launch_bounds__(WT) write_kernel(EncParams ep) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   uint8_t* img = (uint8_t*)smem_raw;                        // OUTB + 32
@@ -459,7 +465,7 @@ __global__ void __launch_bounds__(WT) write_kernel(EncParams ep) {
   uint64_t gpos = ep.block_tot[b];
   while (r < rend) {
     uint64_t my = r + threadIdx.x;
-    uint64_t sz = my < rend ? any_size(ep, P, my) : 0;
+    uint64_t sz = my < rend ? any_size<LS>(ep, P, my) : 0;
     uint64_t tot;
     uint64_t pre = block_excl_scan(sz, &tot, scratch);
     const uint32_t skew = (uint32_t)(((uint64_t)ep.out + gpos) & 15);
@@ -479,7 +485,7 @@ __global__ void __launch_bounds__(WT) write_kernel(EncParams ep) {
       // straight to HBM; its aligned dword stores still merge in L2
       if (my < rend) {
         Sink s(ep.out, gpos + pre);
-        any_write(ep, P, my, s);
+        any_write<LS>(ep, P, my, s);
         if (ep.offsets_out) ep.offsets_out[my] = gpos + pre;
       }
       __syncthreads();
@@ -491,7 +497,7 @@ __global__ void __launch_bounds__(WT) write_kernel(EncParams ep) {
       // a single record larger than the image: thread 0 writes it straight to HBM
       if (threadIdx.x == 0) {
         Sink s(ep.out, gpos);
-        any_write(ep, P, r, s);
+        any_write<LS>(ep, P, r, s);
         if (ep.offsets_out) ep.offsets_out[r] = gpos;
         s_round_bytes = sz;
       }
@@ -503,7 +509,7 @@ __global__ void __launch_bounds__(WT) write_kernel(EncParams ep) {
     }
     if (threadIdx.x < take) {
       Sink s(img, skew + pre);
-      any_write(ep, P, my, s);
+      any_write<LS>(ep, P, my, s);
       if (ep.offsets_out) ep.offsets_out[my] = gpos + pre;
     }
     __syncthreads();
@@ -551,13 +557,17 @@ int kx_launch_encode(const KxProgram* dprog, const KxProgram& hprog, const KxLau
   if (ws_size < kx_encode_ws_bytes(n)) return KX_ERR_INVALID_ARG;
   ep.block_tot = (uint64_t*)ws;
   if (status) KX_HIP_CHECK(hipMemsetAsync(status, 0, sizeof(kx_status), stream));
-  hipLaunchKernelGGL(size_kernel, dim3((unsigned)ep.nblocks), dim3(NT), 0, stream, ep);
+  bool ls = false;
+  for (uint32_t f = 0; f < hprog.nfields; f++) ls |= hprog.f[f].kind == KXP_K_LSTRUCT;
+  if (ls) hipLaunchKernelGGL(size_kernel<true>, dim3((unsigned)ep.nblocks), dim3(NT), 0, stream, ep);
+  else hipLaunchKernelGGL(size_kernel<false>, dim3((unsigned)ep.nblocks), dim3(NT), 0, stream, ep);
   KX_HIP_CHECK(hipGetLastError());
   if (sizes_only) return KX_OK;
   hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, stream, ep);
   KX_HIP_CHECK(hipGetLastError());
   size_t shmem = OUTB + 32 + sizeof(KxProgram) + 8 * (WT / 64);
-  hipLaunchKernelGGL(write_kernel, dim3((unsigned)ep.nblocks), dim3(WT), shmem, stream, ep);
+  if (ls) hipLaunchKernelGGL(write_kernel<true>, dim3((unsigned)ep.nblocks), dim3(WT), shmem, stream, ep);
+  else hipLaunchKernelGGL(write_kernel<false>, dim3((unsigned)ep.nblocks), dim3(WT), shmem, stream, ep);
   KX_HIP_CHECK(hipGetLastError());
   return KX_OK;
 }
