@@ -61,7 +61,10 @@ enum { T_ENT = 0, T_EXIT, T_CNT, T_ERRC, T_ERRP, T_VAR, T_PCNT = T_VAR + KXP_NV_
 enum { G_ENT = 0, G_EXIT, G_CNT, G_ERRC, G_ERRP, G_VAR, G_BCNT = G_VAR + KXP_NV_MAX, G_BVAR,
        G_NF = G_BVAR + KXP_NV_MAX };
 
-enum Mode { M_THRIFT = 0, M_SKIP = 1, M_PB = 2, M_FRAME = 3 };  // M_FRAME: framing sniff
+// M_FRAME: framing sniff; M_THRIFT_LS: Thrift with list<struct> fields (its own instantiation, so that the
+// element loop does not change the register allocation of every other schema's kernels)
+enum Mode { M_THRIFT = 0, M_SKIP = 1, M_PB = 2, M_FRAME = 3, M_THRIFT_LS = 4 };
+__host__ __device__ constexpr bool is_thrift(int m) { return m == M_THRIFT || m == M_THRIFT_LS; }
 
 // diagnostics (KX_DIAG & 64): shader-clock cycles per index-pass phase, summed over tiles (lane 0)
 __device__ unsigned long long g_phase[8];
@@ -559,7 +562,7 @@ __device__ __forceinline__ bool canon_record(const Src& w, const KAS KxLaunchCol
 
 // Generic FastRead field loop: any field order, unknown / mistyped fields skipped, repeated ids
 // (last wins; a repeated struct field is a fresh NewX()), required fields checked.
-template <int NV>
+template <int NV, bool LS>
 __device__ __forceinline__ int generic_record(const Src& w, const KAS KxProgram* P, const KAS KxLaunchCols& cols,
                                               uint64_t start, uint64_t limit, uint64_t rec, bool emit,
                                               uint64_t* endp, VarState<NV>& vs, uint64_t& pres_out) {
@@ -581,7 +584,7 @@ __device__ __forceinline__ int generic_record(const Src& w, const KAS KxProgram*
     KxpField F = ld_field(P, pred >= 0 ? pred : 0);
     const uint32_t t = fx.w0 & 0xff;
     int fi = -1;
-    if (lrem) {  // an element of list<S>: S.FastRead (struct_tpl.go:41-149)
+    if (LS && lrem) {  // an element of list<S>: S.FastRead (struct_tpl.go:41-149)
       if (t == KX_T_STOP) {
         pos += 1;
         for (uint32_t j = 0; j < lns; j++)
@@ -620,7 +623,7 @@ __device__ __forceinline__ int generic_record(const Src& w, const KAS KxProgram*
     }
     if (limit - pos < 3) return KX_ERR_EOF;
     const int id = (int)(int16_t)((((fx.w0 >> 8) & 0xffu) << 8) | ((fx.w0 >> 16) & 0xffu));
-    if (lrem) {
+    if (LS && lrem) {
     } else if (pred >= 0 && F.id == id) {
       fi = pred;
     } else {
@@ -702,7 +705,7 @@ __device__ __forceinline__ int generic_record(const Src& w, const KAS KxProgram*
         if (K.vslot2 != 0xff) vset<NV>(vs, K.vslot2, vp + 6, (uint32_t)nb[side]);
       }
       pos = q;
-    } else if (F.kind == KXP_K_LSTRUCT) {                    // list/set<S>: size x S.FastRead (:583-625)
+    } else if (LS && F.kind == KXP_K_LSTRUCT) {              // list/set<S>: size x S.FastRead (:583-625)
       if (limit - vp < 5) return KX_ERR_EOF;
       const int32_t l = (int32_t)__builtin_bswap32(fx.w1);
       if (l < 0) return KX_ERR_NEGATIVE_SIZE;
@@ -1489,13 +1492,13 @@ __device__ __forceinline__ int parse_record(KParams& dp, const Src& w, uint64_t 
 #pragma unroll
   for (int v = 0; v < NV; v++) { vs.len[v] = 0; vs.pos[v] = 0; }
   pres = 0;
-  if (MODE == M_THRIFT) {
+  if (is_thrift(MODE)) {
     if (w.nsteps && canon_record<NV>(w, dp.cols, pos, lim, r, emit, end, vs)) {
       pres = w.canon_pres;
       return KX_OK;
     }
     if (canon_only) return KX_ERR_INVALID_DATA;
-    return generic_record<NV>(w, dp.prog, dp.cols, pos, lim, r, emit, end, vs, pres);
+    return generic_record<NV, MODE == M_THRIFT_LS>(w, dp.prog, dp.cols, pos, lim, r, emit, end, vs, pres);
   }
   if (MODE == M_PB) {
     uint64_t b = pos, e = lim;
@@ -1632,11 +1635,11 @@ __device__ __forceinline__ Cand lane_candidate(KParams& dp, const Src& w, uint64
   const bool dok = dsig != 0 && canon_t(dsig & 0xff) != 1;  // the first record starts with a field header
   uint32_t sig, slen;
   bool own = false;
-  if (MODE == M_THRIFT && P->sig_len == 3 && (!dok || dsig == P->sig)) {
+  if (is_thrift(MODE) && P->sig_len == 3 && (!dok || dsig == P->sig)) {
     sig = P->sig; slen = 3; own = true;
   } else if (dok) {
     sig = dsig; slen = 3;
-  } else if (MODE == M_THRIFT) {
+  } else if (is_thrift(MODE)) {
     sig = P->sig; slen = P->sig_len;
   } else {
     sig = KX_T_STOP; slen = 1;
@@ -1873,11 +1876,11 @@ __device__ Agg tile_agg(KParams& dp, LDS uint32_t* win, uint64_t t, uint64_t see
   uint64_t lo, hi;
   tile_range(dp, t, lo, hi);
   if (dp.offsets) {
-    const Src w = load_window(dp, win, dp.offsets[lo], lane, MODE == M_THRIFT);
+    const Src w = load_window(dp, win, dp.offsets[lo], lane, is_thrift(MODE));
     return measure_records<NV, MODE>(dp, w, lo, hi, lane);
   }
   const uint64_t t0 = (dp.diag & 64) ? __builtin_amdgcn_s_memtime() : 0;
-  const Src w = load_window(dp, win, lo, lane, MODE == M_THRIFT);
+  const Src w = load_window(dp, win, lo, lane, is_thrift(MODE));
   if ((dp.diag & 64) && lane == 0) atomicAdd(&g_phase[0], (unsigned long long)(__builtin_amdgcn_s_memtime() - t0));
   return walk_tile<NV, MODE>(dp, w, lo, hi, seed, lane, dp.starts + t * dp.slotcap, data_sig(dp));
 }
@@ -2018,7 +2021,7 @@ __global__ void __launch_bounds__(NT, 4) index_kernel(DecParams dp_) {  // 4 wav
   if (dp.diag & 1) {
     uint64_t lo, hi;
     tile_range(dp, t, lo, hi);
-    const Src w = load_window(dp, win, dp.offsets ? dp.offsets[lo] : lo, lane, MODE == M_THRIFT);
+    const Src w = load_window(dp, win, dp.offsets ? dp.offsets[lo] : lo, lane, is_thrift(MODE));
     a.ent = lo + (w.win[lane] & 1); a.ex = hi; a.cnt = 0; a.errc = 0; a.errp = 0;
     for (int v = 0; v < NV; v++) a.var[v] = 0;
   } else {
@@ -2049,7 +2052,7 @@ __global__ void __launch_bounds__(NT, 2) index_kernel_pf(DecParams dp_) {
   const uint32_t dsig = data_sig(dp);  // before the first DMA: its global load must not wait on one
   uint64_t lo, hi;
   tile_range(dp, t, lo, hi);
-  Src w = load_window_async(dp, wa, lo, lane, MODE == M_THRIFT);
+  Src w = load_window_async(dp, wa, lo, lane, is_thrift(MODE));
   bool odd = false;
   for (;;) {
     const uint64_t tn = t + W;
@@ -2057,7 +2060,7 @@ __global__ void __launch_bounds__(NT, 2) index_kernel_pf(DecParams dp_) {
     Src wn = w;
     if (tn < dp.t_hi) {
       tile_range(dp, tn, lon, hin);
-      wn = load_window_async(dp, odd ? wa : wb, lon, lane, MODE == M_THRIFT);
+      wn = load_window_async(dp, odd ? wa : wb, lon, lane, is_thrift(MODE));
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WIN_LOADS) : "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -2276,6 +2279,7 @@ __device__ __forceinline__ uint64_t elem_at(const Src& w, uint64_t q, uint32_t t
 // A list/set<string> column or one side of a map for record r: record offsets in elements at E,
 // element byte offsets from B (LIST_BYTES) or host-order scalars (a map's fixed side). The record's
 // walk already checked every length against its extent.
+template <bool LS>
 __device__ __forceinline__ void emit_container(const Src& w, const KAS KxProgram* P, const KAS KxLaunchCols& cols,
                                                uint32_t c, const KxpCol& K, uint64_t pos, uint32_t n, uint64_t E,
                                                uint64_t B, uint64_t nb, uint64_t r, uint32_t* overflow) {
@@ -2283,7 +2287,7 @@ __device__ __forceinline__ void emit_container(const Src& w, const KAS KxProgram
   const bool fits = lb ? (E + n <= elem_lim(cols, c) && B + nb <= arena_lim(cols, c)) : E + n <= arena_lim(cols, c);
   if (!fits) { atomicOr(overflow, 1u); return; }
   put_off(cols, c, r, E);
-  if (K.mside == 3) {  // a field of list<S>: walk each element for this column's field
+  if (LS && K.mside == 3) {  // a field of list<S>: walk each element for this column's field
     const uint32_t c0 = P->sel_first[c], ns = P->sel_n[c];
     uint64_t q = pos;
     for (uint32_t j = 0; j < n; j++) {
@@ -2347,7 +2351,7 @@ __global__ void __launch_bounds__(NT, 4) emit_kernel(DecParams dp_) {  // 4 wave
   // the window DMA is issued first; the tile's bases are read while it is in flight
   LDS uint32_t* win = (LDS uint32_t*)WIN[wv];
   const uint16_t* starts = dp.starts + t * dp.slotcap;
-  const Src w = load_window(dp, win, known ? dp.offsets[lo] : lo, lane, MODE == M_THRIFT, false);
+  const Src w = load_window(dp, win, known ? dp.offsets[lo] : lo, lane, is_thrift(MODE), false);
   uint64_t base = 0, cnt = 0, run[NV > 0 ? NV : 1];
 #pragma unroll
   for (int v = 0; v < (NV > 0 ? NV : 1); v++) run[v] = 0;
@@ -2422,7 +2426,7 @@ __global__ void __launch_bounds__(NT, 4) emit_kernel(DecParams dp_) {  // 4 wave
 #pragma unroll
           for (int u = 0; u < NV; u++)
             if ((uint32_t)u == K.vslot2) { B = atv[u]; nb = vs.len[u]; }
-          emit_container(w, P, dp.cols, cc, K, vs.pos[v], vs.len[v], at, B, nb, r, dp.overflow);
+          emit_container<MODE == M_THRIFT_LS>(w, P, dp.cols, cc, K, vs.pos[v], vs.len[v], at, B, nb, r, dp.overflow);
         }
       } else if (act && ((dp.cols.view >> cc) & 1)) {
         put_view(dp.cols, cc, r, vs.pos[v], vs.len[v]);
@@ -2642,9 +2646,9 @@ int kx_dec_launch(const void* dp, const void* L, void* ws, hipStream_t stream, c
 #define KX_EXT(NV, MODE) \
   extern template int kx_dec_launch<NV, MODE>(const void*, const void*, void*, hipStream_t, const KxPipe*);
 #if KX_OWNS(0)
-KX_DEF(0, M_THRIFT) KX_DEF(1, M_THRIFT)
+KX_DEF(0, M_THRIFT) KX_DEF(1, M_THRIFT) KX_DEF(1, M_THRIFT_LS)
 #else
-KX_EXT(0, M_THRIFT) KX_EXT(1, M_THRIFT)
+KX_EXT(0, M_THRIFT) KX_EXT(1, M_THRIFT) KX_EXT(1, M_THRIFT_LS)
 #endif
 #if KX_OWNS(1)
 KX_DEF(2, M_THRIFT) KX_DEF(0, M_SKIP) KX_DEF(0, M_FRAME)
@@ -2652,14 +2656,19 @@ KX_DEF(2, M_THRIFT) KX_DEF(0, M_SKIP) KX_DEF(0, M_FRAME)
 KX_EXT(2, M_THRIFT) KX_EXT(0, M_SKIP) KX_EXT(0, M_FRAME)
 #endif
 #if KX_OWNS(2)
-KX_DEF(4, M_THRIFT)
+KX_DEF(4, M_THRIFT) KX_DEF(2, M_THRIFT_LS)
 #else
-KX_EXT(4, M_THRIFT)
+KX_EXT(4, M_THRIFT) KX_EXT(2, M_THRIFT_LS)
 #endif
 #if KX_OWNS(3)
-KX_DEF(8, M_THRIFT)
+KX_DEF(8, M_THRIFT) KX_DEF(4, M_THRIFT_LS)
 #else
-KX_EXT(8, M_THRIFT)
+KX_EXT(8, M_THRIFT) KX_EXT(4, M_THRIFT_LS)
+#endif
+#if KX_OWNS(5)
+KX_DEF(8, M_THRIFT_LS)
+#else
+KX_EXT(8, M_THRIFT_LS)
 #endif
 #if KX_OWNS(4)
 KX_DEF(0, M_PB) KX_DEF(1, M_PB) KX_DEF(2, M_PB)
@@ -2676,12 +2685,21 @@ KX_EXT(4, M_PB) KX_EXT(8, M_PB)
 template <int MODE>
 static int launch_nv(const DecParams& dp, const WsLayout& L, void* ws, hipStream_t stream, uint32_t nvar,
                      const KxPipe* pp) {
-  switch (nvar) {
-    case 0: return kx_dec_launch<0, MODE>(&dp, &L, ws, stream, pp);
-    case 1: return kx_dec_launch<1, MODE>(&dp, &L, ws, stream, pp);
-    case 2: return kx_dec_launch<2, MODE>(&dp, &L, ws, stream, pp);
-    case 3: case 4: return kx_dec_launch<4, MODE>(&dp, &L, ws, stream, pp);
-    default: return kx_dec_launch<8, MODE>(&dp, &L, ws, stream, pp);
+  if constexpr (MODE == M_THRIFT_LS) {  // a list<struct> field holds >= 1 var slot
+    switch (nvar) {
+      case 0: case 1: return kx_dec_launch<1, M_THRIFT_LS>(&dp, &L, ws, stream, pp);
+      case 2: return kx_dec_launch<2, M_THRIFT_LS>(&dp, &L, ws, stream, pp);
+      case 3: case 4: return kx_dec_launch<4, M_THRIFT_LS>(&dp, &L, ws, stream, pp);
+      default: return kx_dec_launch<8, M_THRIFT_LS>(&dp, &L, ws, stream, pp);
+    }
+  } else {
+    switch (nvar) {
+      case 0: return kx_dec_launch<0, MODE>(&dp, &L, ws, stream, pp);
+      case 1: return kx_dec_launch<1, MODE>(&dp, &L, ws, stream, pp);
+      case 2: return kx_dec_launch<2, MODE>(&dp, &L, ws, stream, pp);
+      case 3: case 4: return kx_dec_launch<4, MODE>(&dp, &L, ws, stream, pp);
+      default: return kx_dec_launch<8, MODE>(&dp, &L, ws, stream, pp);
+    }
   }
 }
 
@@ -2714,8 +2732,11 @@ int kx_launch_decode(const KxProgram* dprog, const KxProgram& hprog, const uint8
   dp.krec = krec_for(in_len, n);
   const WsLayout L = ws_layout(hprog.fixed_min, in_len, offsets, n);
   if (ws_size < L.total) return KX_ERR_INVALID_ARG;
+  bool ls = false;
+  for (uint32_t f = 0; f < hprog.nfields; f++) ls |= hprog.f[f].kind == KXP_K_LSTRUCT;
   return pb ? launch_nv<M_PB>(dp, L, ws, stream, hprog.nvar, pipe)
-            : launch_nv<M_THRIFT>(dp, L, ws, stream, hprog.nvar, pipe);
+            : ls ? launch_nv<M_THRIFT_LS>(dp, L, ws, stream, hprog.nvar, pipe)
+                 : launch_nv<M_THRIFT>(dp, L, ws, stream, hprog.nvar, pipe);
 }
 
 int kx_launch_skip(const uint8_t* in, uint64_t in_len, uint64_t n, uint64_t* offsets_out, kx_status* status,
