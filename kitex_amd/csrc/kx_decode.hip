@@ -1206,8 +1206,51 @@ __device__ __forceinline__ uint64_t scan_segment(const Src& w, int32_t q0, uint6
   return (best < (uint32_t)SEG && seg_lo + best < plim) ? seg_lo + best : X_NONE;
 }
 
-// the two lowest signature offsets of the segment (same scan; >= SEG when absent), for schemas
-// whose signature also starts a nested struct
+// the two lowest signature offsets of the segment (>= SEG when absent), for the canonical-record
+// candidate checks. The 33-dword loop only records which dwords hold a hit (one bit per dword); the
+// hit positions are then recomputed for the (one or two) lowest such dwords. Positions are exact: bytes
+// of dword 0 below the segment start and bytes of dword 32 at or past its end are masked off.
+#ifndef KX_SCAN2_OLD
+__device__ __forceinline__ void scan_segment2(const Src& w, int32_t q0, uint32_t sig, int lane, uint32_t& c1,
+                                              uint32_t& c2) {
+  const LDS uint32_t* s = w.win + (q0 >> 2);
+  const uint32_t sh0 = q0 & 3;
+  const uint32_t b0 = (sig & 0xff) * 0x01010101u, b1 = ((sig >> 8) & 0xff) * 0x01010101u;
+  const uint32_t b2 = ((sig >> 16) & 0xff) * 0x01010101u;
+  uint64_t hb = 0;
+  int idx = lane % 33;
+  for (int i = 0; i < 33; i++) {
+    const uint32_t x0 = s[idx], x1 = s[idx + 1];
+    const uint32_t m = zero_bytes((x0 ^ b0) | (__builtin_amdgcn_alignbyte(x1, x0, 1) ^ b1) |
+                                  (__builtin_amdgcn_alignbyte(x1, x0, 2) ^ b2));
+    hb |= (uint64_t)(m != 0) << idx;
+    idx = idx == 32 ? 0 : idx + 1;
+  }
+  c1 = ~0u;
+  c2 = ~0u;
+  const uint32_t lowm = sh0 ? (0xffffffffu >> (32 - 8 * sh0)) : 0u;  // bytes j < sh0 of a dword
+  while (hb) {
+    const int d = __ffsll((long long)hb) - 1;
+    hb &= hb - 1;
+    const uint32_t x0 = s[d], x1 = s[d + 1];
+    uint32_t m = zero_bytes((x0 ^ b0) | (__builtin_amdgcn_alignbyte(x1, x0, 1) ^ b1) |
+                            (__builtin_amdgcn_alignbyte(x1, x0, 2) ^ b2));
+    if (d == 0) m &= ~lowm;
+    else if (d == 32) m &= lowm;
+    while (m) {
+      const uint32_t h = (uint32_t)(4 * d) - sh0 + first_hit(m);
+      m &= m - 1;
+      if (c1 == ~0u) {
+        c1 = h;
+      } else {
+        c2 = h;
+        break;
+      }
+    }
+    if (c2 != ~0u) break;
+  }
+}
+#else
 __device__ __forceinline__ void scan_segment2(const Src& w, int32_t q0, uint32_t sig, int lane, uint32_t& c1,
                                               uint32_t& c2) {
   const LDS uint32_t* s = w.win + (q0 >> 2);
@@ -1231,6 +1274,8 @@ __device__ __forceinline__ void scan_segment2(const Src& w, int32_t q0, uint32_t
     idx = idx == 32 ? 0 : idx + 1;
   }
 }
+
+#endif
 
 // Kitex-Protobuf record candidate at p: a Batch frame header (0x0A, uvarint length) whose body fits
 // the input, starts with a plausible tag, and is followed by the next frame's 0x0A (or the end).
