@@ -42,6 +42,52 @@ class CodecType(IntFlag):
     EnableSkipDecoder = 0b10000
 
 
+@dataclass(frozen=True)
+class TypeCodec:
+    """typeCodec (pkg/remote/codec/thrift/codec.go:26-47): the codecs a record type implements. Every type
+    compiled into a kx schema has the generated FastCodec trio (kx_thrift_* are its batch form)."""
+    FastCodec: bool = True
+    Frugal: bool = False
+    Apache: bool = False
+
+
+def is_data_len_deterministic(codec_type: "CodecType", data_len: int) -> bool:
+    """IsDataLenDeterministic (thrift.go:102-105)"""
+    return data_len > 0 or bool(codec_type & CodecType.EnableSkipDecoder)
+
+
+def select_unmarshal(codec_type: "CodecType", data_len: int, tc: TypeCodec = TypeCodec()) -> str:
+    """unmarshalThriftData (thrift_data.go:106-127): "frugal" | "fast" | "apache". A "fast" read with
+    data_len 0 is fastUnmarshal's skip-then-read (codec_fast.go:72-81): the concatenated batch decode."""
+    ok = is_data_len_deterministic(codec_type, data_len)
+    if ok and codec_type & CodecType.FrugalRead and tc.Frugal:
+        return "frugal"
+    if ok and codec_type & CodecType.FastRead and tc.FastCodec:
+        return "fast"
+    if tc.Apache:
+        return "apache"
+    if tc.FastCodec:  # fallback even though CodecType=Basic or EnableSkipDecoder not set
+        return "fast"
+    if tc.Frugal:
+        return "frugal"
+    raise KxError(A.ERR_INVALID_DATA, "decode failed, msg type not match with thriftCodec")  # errDecodeMismatchMsgType
+
+
+def select_marshal(codec_type: "CodecType", tc: TypeCodec = TypeCodec()) -> str:
+    """marshalThriftData (thrift_data.go:56-78)"""
+    if codec_type & CodecType.FrugalWrite and tc.Frugal:
+        return "frugal"
+    if codec_type & CodecType.FastWrite and tc.FastCodec:
+        return "fast"
+    if tc.Apache:
+        return "apache"
+    if tc.FastCodec:
+        return "fast"
+    if tc.Frugal:
+        return "frugal"
+    raise KxError(A.ERR_INVALID_DATA, "encode failed, msg type not match with thriftCodec")
+
+
 class ProtocolError(KxError):
     """remote.NewTransError(remote.ProtocolError, err) equivalent (trans_errors.go:35)."""
 
@@ -199,6 +245,9 @@ class ThriftCodec:
                                           C.byref(kc), _ptr(rs), _ptr(st), int(s.cuda_stream))
         check(rc, self._DECODE)
         res = DecodeResult(out, st, rs, s)
+        # the reference's codec choice for this call (every choice reads the same struct; the device
+        # runs the batch FastRead, with the skip decoder finding the records when no dataLen is known)
+        res.path = self._PATH_FN(self.codec_type, 1 if offsets is not None else 0)
         if raise_on_error:
             s = res.read_status()
             if s.code:
@@ -233,6 +282,7 @@ class ThriftCodec:
     _MESSAGES = "kx_thrift_decode_messages"
     _FRAMES = "kx_thrift_decode_frames"
     _GRPC = "kx_thrift_decode_grpc"
+    _PATH_FN = staticmethod(select_unmarshal)
 
     def UnmarshalMessages(self, buf, n: int, offsets, body_field: int = 1, out: ColumnSet = None,
                           var_caps: Sequence[int] = None, name_cap: int = None, stream=None,
@@ -394,6 +444,7 @@ class ProtobufCodec(ThriftCodec):
     _MESSAGES = "kx_pb_decode_messages"
     _FRAMES = "kx_pb_decode_frames"
     _GRPC = "kx_pb_decode_grpc"
+    _PATH_FN = staticmethod(lambda codec_type, data_len: "protobuf")
     _ENCODE = "kx_pb_encode_batch"
     _SIZE = "kx_pb_encoded_size_batch"
     _WHAT = "protobuf unmarshal"
