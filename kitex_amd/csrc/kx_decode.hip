@@ -40,8 +40,9 @@ constexpr int NT = 256;                  // threads per workgroup (4 independent
 constexpr int WAVES = NT / 64;
 constexpr int SEG = 128;                 // bytes per lane segment
 constexpr int TILE = 64 * SEG;           // 8 KiB of input per wave
-constexpr int HALO = 512;                // the record straddling the tile end is read from LDS up to here
-constexpr int WINB = TILE + HALO + 16;   // LDS window bytes (+16 for the aligned-down start)
+constexpr int HALO = 512;                // default halo: the record straddling the tile end is read from LDS
+constexpr int HALO_MAX = 1536;           // up to here (the halo grows with the batch's mean record size)
+constexpr int WINB = TILE + HALO_MAX + 16;  // LDS window bytes allocated (+16 for the aligned-down start)
 constexpr int WINW = WINB / 4 + 4;       // window dwords (+ pad for the last aligned read pair)
 constexpr int WIN_LOADS = (WINB / 16 + 63) / 64;
 constexpr int GT = 64;                   // tiles per group (one group-scan lane per tile)
@@ -100,6 +101,7 @@ struct DecParams {
   int chunk_first, chunk_last;
   uint64_t epoch;            // 16-bit call epoch (never 0)
   uint32_t krec;             // offsets mode: records per tile (<= 64)
+  uint32_t winb;             // window bytes loaded per tile: TILE + halo + 16 (<= WINB)
   int direct;                // offsets mode without var columns: emit pass only
   int nolds;                 // diagnostics (KX_NOLDS=1): read every byte from global memory
   int diag;                  // diagnostics (KX_DIAG bits, timing experiments only; output is wrong):
@@ -1343,7 +1345,7 @@ __device__ __forceinline__ Src load_window(KParams& dp, LDS uint32_t* win, uint6
   const uint64_t abs_in = (uint64_t)dp.in;
   const uint64_t wbase = (abs_in + kmin64(lo, dp.in_len)) & ~15ull;
   const uint64_t end = abs_in + dp.in_len;
-  const int32_t wlen = dp.nolds || end < wbase + 16 ? 0 : (int32_t)kmin64((uint64_t)WINB, (end - wbase) & ~15ull);
+  const int32_t wlen = dp.nolds || end < wbase + 16 ? 0 : (int32_t)kmin64((uint64_t)dp.winb, (end - wbase) & ~15ull);
   const uint32_t blo = __builtin_amdgcn_readfirstlane((uint32_t)wbase);
   const uint32_t bhi = __builtin_amdgcn_readfirstlane((uint32_t)(wbase >> 32));
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
@@ -1371,7 +1373,7 @@ __device__ __forceinline__ Src load_window_async(KParams& dp, LDS uint32_t* win,
   const uint64_t abs_in = (uint64_t)dp.in;
   const uint64_t wbase = (abs_in + kmin64(lo, dp.in_len)) & ~15ull;
   const uint64_t end = abs_in + dp.in_len;
-  const int32_t wlen = dp.nolds || end < wbase + 16 ? 0 : (int32_t)kmin64((uint64_t)WINB, (end - wbase) & ~15ull);
+  const int32_t wlen = dp.nolds || end < wbase + 16 ? 0 : (int32_t)kmin64((uint64_t)dp.winb, (end - wbase) & ~15ull);
   v4u rs;
   rs.x = __builtin_amdgcn_readfirstlane((uint32_t)wbase);
   rs.y = __builtin_amdgcn_readfirstlane((uint32_t)(wbase >> 32)) & 0xffffu;
@@ -2763,6 +2765,15 @@ extern "C" int kx_debug_phase_cycles(unsigned long long* out, int n) {
 
 size_t kx_skip_ws_bytes(uint64_t in_len) { return ws_layout(1, in_len, nullptr, 0).total; }
 
+// window bytes per tile: a halo of about two mean records (the walk of a tile's last records stays in
+// LDS: R3's 576-byte records left the 512-byte halo and walked global memory), 512 .. HALO_MAX
+static uint32_t win_bytes(uint64_t in_len, uint64_t n) {
+  const uint64_t mean = n ? in_len / n : 0;
+  uint64_t h = (2 * mean + 255) & ~255ull;
+  h = h < (uint64_t)HALO ? (uint64_t)HALO : h > (uint64_t)HALO_MAX ? (uint64_t)HALO_MAX : h;
+  return (uint32_t)(TILE + h + 16);
+}
+
 int kx_launch_decode(const KxProgram* dprog, const KxProgram& hprog, const uint8_t* in, uint64_t in_len,
                      const uint64_t* offsets, uint64_t n, const KxLaunchCols& cols, uint8_t* record_status,
                      kx_status* status, void* ws, size_t ws_size, uint64_t epoch, hipStream_t stream, bool pb,
@@ -2775,6 +2786,7 @@ int kx_launch_decode(const KxProgram* dprog, const KxProgram& hprog, const uint8
   dp.prog = (const KAS KxProgram*)dprog;
   dp.cols = cols; dp.rstat = record_status; dp.status = status; dp.epoch = epoch;
   dp.krec = krec_for(in_len, n);
+  dp.winb = win_bytes(in_len, n);
   const WsLayout L = ws_layout(hprog.fixed_min, in_len, offsets, n);
   if (ws_size < L.total) return KX_ERR_INVALID_ARG;
   bool ls = false;
@@ -2791,6 +2803,7 @@ int kx_launch_skip(const uint8_t* in, uint64_t in_len, uint64_t n, uint64_t* off
   dp.in = in; dp.in_len = in_len; dp.offsets = nullptr; dp.n = n; dp.prog = nullptr;
   dp.status = status; dp.skip_out = offsets_out; dp.epoch = epoch;
   dp.krec = 64;
+  dp.winb = TILE + HALO + 16;
   const WsLayout L = ws_layout(1, in_len, nullptr, n);
   if (ws_size < L.total) return KX_ERR_INVALID_ARG;
   return kx_dec_launch<0, M_SKIP>(&dp, &L, ws, stream, nullptr);
@@ -2806,6 +2819,7 @@ int kx_launch_frames(const uint8_t* in, uint64_t in_len, uint64_t n, uint64_t ma
   dp.fr_ps = pay_start; dp.fr_pe = pay_end; dp.fr_kind = kinds; dp.fr_max = max_payload;
   dp.fr_grpc = grpc ? 1 : 0;
   dp.krec = 64;
+  dp.winb = TILE + HALO + 16;
   const WsLayout L = ws_layout(1, in_len, nullptr, n);
   if (ws_size < L.total) return KX_ERR_INVALID_ARG;
   return kx_dec_launch<0, M_FRAME>(&dp, &L, ws, stream, nullptr);
