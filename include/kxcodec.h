@@ -28,6 +28,8 @@
  *   kx_host_decode_batch ........ fastUnmarshal end to end from host (netpoll) memory: pinned H2D ->
  *                                 decode -> D2H (codec_fast.go:60-82 with the Next(dataLen) slice);
  *                                 kx_host_pb_decode_batch the same for protobufCodec.Unmarshal bodies
+ *   kx_thrift_encode_messages ... fastMarshal (codec_fast.go:40-58) over N messages: MessageBegin + Args wrapper
+ *                                 + record + STOP on the device
  *   kx_thrift_decode_messages ... thriftCodec.Unmarshal over N framed messages (thrift.go:180-225):
  *                                 MessageBegin + Args{1: req} (k-mock.go:422-517) on the device
  *   kx_pb_decode_messages ....... protobufCodec.Unmarshal over N framed messages (protobuf.go:136-216)
@@ -246,6 +248,19 @@ int kx_thrift_encoded_size_batch(kx_ctx* c, const kx_schema* s, const kx_columns
 int kx_thrift_encode_batch(kx_ctx* c, const kx_schema* s, const kx_columns* in, uint64_t n,
                            uint8_t* out, uint64_t out_cap, uint64_t* offsets_out,
                            kx_status* status, void* stream);
+
+/* fastMarshal over n messages (codec_fast.go:40-58; thriftCodec.Marshal, thrift.go:106-160): message i =
+ * WriteMessageBegin(name, msg_type, seqids[i]) (strict binary, binary_test.go:387-457) + the method's
+ * Args / Result struct whose field `body_field` (1 = Args{1: req}, 0 = Result{0: success}) is record i
+ * (its FastWriteNocopy bytes, kx_thrift_encode_batch) + STOP (MockTestArgs.FastWriteNocopy,
+ * k-mock.go:422-517). The records are first written to body_scratch (device, >= their total size, e.g.
+ * the sum of kx_thrift_encoded_size_batch); out receives the n messages back to back
+ * (sum of record sizes + n * (16 + name_len) bytes), offsets_out (n + 1, optional) their starts.
+ * name: host memory. seqids: device i32[n]. Status: SIZE_LIMIT when scratch or out is too small. */
+int kx_thrift_encode_messages(kx_ctx* c, const kx_schema* s, const kx_columns* in, uint64_t n, const char* name,
+                              uint32_t name_len, int32_t msg_type, const int32_t* seqids, int32_t body_field,
+                              uint8_t* body_scratch, uint64_t scratch_cap, uint8_t* out, uint64_t out_cap,
+                              uint64_t* offsets_out, kx_status* status, void* stream);
 
 /* ---- Kitex-Protobuf (proto3 body) ----
  * The schema's field ids are proto field numbers; ttype selects the proto scalar mapping

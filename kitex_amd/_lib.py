@@ -27,7 +27,7 @@ EXPORTS = [
     "kx_pb_read_meta", "kx_ctx_set_pipeline", "kx_frame_scan", "kx_thrift_decode_frames",
     "kx_pb_decode_frames", "kx_crc32c_batch", "kx_frame_crc32c_validate", "kx_ctx_set_crc32c_check",
     "kx_grpc_frame_scan", "kx_thrift_decode_grpc", "kx_pb_decode_grpc", "kx_thrift_raw_messages",
-    "kx_thrift_set_seqids",
+    "kx_thrift_set_seqids", "kx_thrift_encode_messages",
 ]
 
 
@@ -102,6 +102,8 @@ def lib():
     L.kx_grpc_frame_scan.argtypes = L.kx_frame_scan.argtypes
     L.kx_thrift_raw_messages.argtypes = [vp, vp, u64, vp, u64, C.POINTER(A.Column), vp, vp, vp]
     L.kx_thrift_set_seqids.argtypes = [vp, vp, u64, vp, u64, vp, vp, vp, vp]
+    L.kx_thrift_encode_messages.argtypes = [vp, vp, C.POINTER(A.Columns), u64, C.c_char_p, u32, i32, vp, i32, vp,
+                                            u64, vp, u64, vp, vp, vp]
     L.kx_thrift_decode_grpc.argtypes = [vp, vp, vp, u64, u64, u64, vp, C.POINTER(A.Columns), vp, vp, vp]
     L.kx_pb_decode_grpc.argtypes = L.kx_thrift_decode_grpc.argtypes
     L.kx_pb_meta_length.argtypes = [u32]

@@ -403,6 +403,34 @@ class ThriftCodec:
             raise ProtocolError(s.code, self._ENCODE)
         return out[:s.consumed], offs
 
+    def MarshalMessages(self, cols: ColumnSet, method: str, seqids, msg_type: int = 1, body_field: int = 1,
+                        stream=None):
+        """fastMarshal (codec_fast.go:40-58) of n messages: MessageBegin(method, msg_type, seqids[i]) + the
+        Args{body_field: record i} (or Result{0: success}) struct + STOP, on the device. Returns (messages
+        uint8 tensor, message offsets int64[n+1])."""
+        import torch
+        if self._ENCODE != "kx_thrift_encode_batch":
+            raise KxError(A.ERR_NOT_IMPLEMENTED, "MarshalMessages: Thrift only")
+        ds = self.dschema
+        n = cols.n
+        kc = to_kx_columns(cols, ds.infos)
+        body = int(self.BLength(cols, stream=stream).sum().item()) if n else 0
+        nb = method.encode()
+        total = body + n * (16 + len(nb))
+        scratch = torch.empty(max(1, body), dtype=torch.uint8, device=self.device)
+        out = torch.empty(max(1, total), dtype=torch.uint8, device=self.device)
+        offs = torch.empty(n + 1, dtype=torch.int64, device=self.device)
+        st = status_tensor(self.device)
+        ss = _stream(stream)
+        rc = lib().kx_thrift_encode_messages(self._ctx(ss).handle, ds.handle, C.byref(kc), n, nb, len(nb), msg_type,
+                                             _ptr(seqids), body_field, _ptr(scratch), scratch.numel(), _ptr(out),
+                                             out.numel(), _ptr(offs), _ptr(st), int(ss.cuda_stream))
+        check(rc, "kx_thrift_encode_messages")
+        s = read_status(st, ss)
+        if s.code:
+            raise ProtocolError(s.code, "fastMarshal")
+        return out[:s.consumed], offs
+
     def BLength(self, cols: ColumnSet, stream=None):
         import torch
         ds = self.dschema

@@ -352,6 +352,52 @@ int kx_thrift_encode_batch(kx_ctx* c, const kx_schema* s, const kx_columns* in, 
                           st, false);
 }
 
+int kx_thrift_encode_messages(kx_ctx* c, const kx_schema* s, const kx_columns* in, uint64_t n, const char* name,
+                              uint32_t name_len, int32_t msg_type, const int32_t* seqids, int32_t body_field,
+                              uint8_t* body_scratch, uint64_t scratch_cap, uint8_t* out, uint64_t out_cap,
+                              uint64_t* offsets_out, kx_status* status, void* stream) {
+  if (!c || !s || !status || (!out && out_cap) || (!body_scratch && scratch_cap) || (n && !seqids) ||
+      (name_len && !name) || body_field < 0 || body_field > 32767 || msg_type < 1 || msg_type > 4)
+    return KX_ERR_INVALID_ARG;
+  int rc = set_device(c);
+  if (rc) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  KxLaunchCols lc;
+  if ((rc = to_launch_cols(s, in, &lc))) return rc;
+  // scratch: record offsets (n + 1), then the name
+  const size_t need = (n + 1) * 8 + name_len + 8;
+  if (c->xws_size < need) {
+    if (c->xws) {
+      KX_HIP_CHECK(hipStreamSynchronize(st));
+      KX_HIP_CHECK(hipFree(c->xws));
+      c->xws = nullptr;
+      c->xws_size = 0;
+    }
+    const size_t sz = need < (1u << 20) ? (1u << 20) : need + need / 4;
+    KX_HIP_CHECK(hipMalloc(&c->xws, sz));
+    c->xws_size = sz;
+  }
+  uint64_t* boff = (uint64_t*)c->xws;
+  uint8_t* dname = (uint8_t*)c->xws + (n + 1) * 8;
+  if (name_len) KX_HIP_CHECK(hipMemcpyAsync(dname, name, name_len, hipMemcpyHostToDevice, st));
+  if (n == 0) {
+    KX_HIP_CHECK(hipMemsetAsync(boff, 0, 8, st));
+    KX_HIP_CHECK(hipMemsetAsync(status, 0, sizeof(kx_status), st));
+  } else {
+    KxProgram* dp = nullptr;
+    if ((rc = prog_on_device(const_cast<kx_schema*>(s), c->device, &dp))) return rc;
+    if ((rc = ensure_ews(c, kx_encode_ws_bytes(n), st))) return rc;
+    // the records back to back (FastWriteNocopy), then each wrapped into its message
+    if ((rc = kx_launch_encode(dp, s->prog, lc, n, body_scratch, scratch_cap, nullptr, boff, status, c->ews,
+                               c->ews_size, st, false)))
+      return rc;
+  }
+  // the status keeps the record encoder's code (SIZE_LIMIT: the scratch is too small); the message pass
+  // sets consumed / n_records and SIZE_LIMIT when `out` is too small
+  return kx_launch_message_encode(body_scratch, boff, n, dname, name_len, msg_type, seqids, body_field, out,
+                                  out_cap, offsets_out, status, st);
+}
+
 static int pb_schema_ok(const kx_schema* s) {
   for (uint32_t f = 0; f < s->prog.nfields; f++)
     if (s->prog.f[f].pb_wt == 7 || s->prog.ninst != 1) return KX_ERR_NOT_IMPLEMENTED;

@@ -57,6 +57,9 @@ struct kx_ctx {
   // CRC32C: 256 B scratch (error key), armed at allocation; CRC32Check for kx_*_decode_frames
   void* cws = nullptr;
   bool crc32c_check = false;
+  // grow-only message-encode scratch: record offsets (n + 1) and the method name
+  void* xws = nullptr;
+  size_t xws_size = 0;
   // grow-only encode scratch (per-block sizes)
   void* ews = nullptr;
   size_t ews_size = 0;
@@ -125,6 +128,10 @@ int kx_launch_message_headers(const uint8_t* in, uint64_t in_len, const uint64_t
                               int raw = 0);
 int kx_launch_set_seqids(uint8_t* in, uint64_t in_len, const uint64_t* offsets, uint64_t n, const int32_t* seqids,
                          uint8_t* record_status, kx_status* status, void* mws, hipStream_t stream);
+int kx_launch_message_encode(const uint8_t* bodies, const uint64_t* body_off, uint64_t n, const uint8_t* name,
+                             uint32_t name_len, int32_t msg_type, const int32_t* seqids, int32_t body_field,
+                             uint8_t* out, uint64_t out_cap, uint64_t* offsets_out, kx_status* status,
+                             hipStream_t stream);
 int kx_launch_message_merge(const uint64_t* offsets, uint64_t n, const uint8_t* hdr_rc, const uint8_t* body_rc,
                             uint8_t* record_status, kx_status* status, void* mws, hipStream_t stream,
                             const kx_status* pre = nullptr);

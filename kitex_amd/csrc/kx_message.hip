@@ -284,6 +284,54 @@ __global__ void __launch_bounds__(MT) setseq_kernel(uint8_t* in, uint64_t in_len
   if (rc) atomicMin(errkey, (unsigned long long)((i << 8) | (uint64_t)(rc & 0xff)));
 }
 
+// fastMarshal (codec_fast.go:40-58) of message i: WriteMessageBegin(name, type, seqid[i]) + the Args /
+// Result struct whose field `body_field` holds record i (STRUCT header) + the record + STOP. Every
+// message adds the same H + 1 bytes around its record, so its position is body_off[i] + i * (H + 1): no
+// scan. Lane = message; the record's bytes are copied from the encoder's output.
+struct MsgEnc {
+  const uint8_t* bodies;
+  const uint64_t* body_off;  // n + 1
+  uint64_t n;
+  const uint8_t* name;       // device copy of the method name
+  uint32_t name_len;
+  int32_t msg_type;
+  const int32_t* seqids;
+  int32_t body_field;
+  uint8_t* out;
+  uint64_t out_cap;
+  uint64_t* offsets_out;     // n + 1 (optional)
+  kx_status* status;
+};
+
+__global__ void __launch_bounds__(MT) msgenc_kernel(MsgEnc me) {
+  const uint64_t i = (uint64_t)blockIdx.x * MT + threadIdx.x;
+  if (i > me.n) return;
+  const uint64_t H = 12ull + me.name_len + 3ull;
+  const uint64_t at = me.body_off[i] + i * (H + 1);
+  if (me.offsets_out) me.offsets_out[i] = at;
+  if (i == me.n) {
+    me.status->n_records = me.n;
+    me.status->consumed = at;
+    if (at > me.out_cap) me.status->code = KX_ERR_SIZE_LIMIT;
+    return;
+  }
+  const uint64_t bl = me.body_off[i + 1] - me.body_off[i];
+  if (at + H + bl + 1 > me.out_cap) return;  // the call fails with SIZE_LIMIT (thread n)
+  uint8_t* o = me.out + at;
+  const uint32_t v = 0x80010000u | ((uint32_t)me.msg_type & 0xffu);  // strict version | type
+  const uint32_t nl = me.name_len, sq = (uint32_t)me.seqids[i];
+  o[0] = (uint8_t)(v >> 24); o[1] = (uint8_t)(v >> 16); o[2] = (uint8_t)(v >> 8); o[3] = (uint8_t)v;
+  o[4] = (uint8_t)(nl >> 24); o[5] = (uint8_t)(nl >> 16); o[6] = (uint8_t)(nl >> 8); o[7] = (uint8_t)nl;
+  for (uint32_t k = 0; k < nl; k++) o[8 + k] = me.name[k];
+  uint8_t* q = o + 8 + nl;
+  q[0] = (uint8_t)(sq >> 24); q[1] = (uint8_t)(sq >> 16); q[2] = (uint8_t)(sq >> 8); q[3] = (uint8_t)sq;
+  q[4] = KX_T_STRUCT; q[5] = (uint8_t)((uint32_t)me.body_field >> 8); q[6] = (uint8_t)me.body_field;
+  const uint8_t* b = me.bodies + me.body_off[i];
+  uint8_t* d = q + 7;
+  for (uint64_t k = 0; k < bl; k++) d[k] = b[k];
+  d[bl] = KX_T_STOP;
+}
+
 // exclusive scan of name_len[0..n] in place (one workgroup; each thread a contiguous run)
 __global__ void __launch_bounds__(ST) scan_kernel(uint64_t* v, uint64_t n1) {
   __shared__ uint64_t part[ST];
@@ -438,6 +486,17 @@ int kx_launch_set_seqids(uint8_t* in, uint64_t in_len, const uint64_t* offsets, 
   KX_HIP_CHECK(hipMemsetAsync(status, 0, sizeof(kx_status), stream));
   hipLaunchKernelGGL(final_kernel, dim3(1), dim3(64), 0, stream, status, offsets, n, errkey, overflow,
                      (const kx_status*)nullptr);
+  KX_HIP_CHECK(hipGetLastError());
+  return KX_OK;
+}
+
+int kx_launch_message_encode(const uint8_t* bodies, const uint64_t* body_off, uint64_t n, const uint8_t* name,
+                             uint32_t name_len, int32_t msg_type, const int32_t* seqids, int32_t body_field,
+                             uint8_t* out, uint64_t out_cap, uint64_t* offsets_out, kx_status* status,
+                             hipStream_t stream) {
+  MsgEnc me{bodies, body_off, n, name, name_len, msg_type, seqids, body_field, out, out_cap, offsets_out, status};
+  const unsigned grid = (unsigned)((n + 1 + MT - 1) / MT);
+  hipLaunchKernelGGL(msgenc_kernel, dim3(grid), dim3(MT), 0, stream, me);
   KX_HIP_CHECK(hipGetLastError());
   return KX_OK;
 }

@@ -179,3 +179,36 @@ def test_pb_messages_match_oracle(torch, oracle):
             assert np.array_equal(to_np(res.columns.cols[j])[rows], to_np(exp.cols[j])[rows])
     assert to_np(res.seqid)[rows].tolist() == rows
     assert res.name(5) == "pb2"
+
+
+@pytest.mark.parametrize("name,body_field,mtype", [("r2", 1, 1), ("r3", 0, 2)])
+def test_marshal_messages_matches_oracle_and_round_trips(torch, oracle, name, body_field, mtype):
+    """fastMarshal on the device (kx_thrift_encode_messages): every message equals the oracle's
+    WriteMessageBegin + Args/Result wrapper + the oracle-encoded record + STOP, and decodes back"""
+    import numpy as np
+    from kitex_amd import schema as S, synth
+    from kitex_amd.codec import ThriftCodec, write_message_begin
+    from kitex_amd.columns import alloc_device  # noqa: F401
+    from tests.helpers import assert_columns_equal
+    n = 3000
+    sch = S.SCHEMAS[name]()
+    cs = synth.GENERATORS[name](n, start=11)
+    rc, wire, offs = oracle.encode(sch, cs)
+    assert rc == 0
+    dev = torch.device("cuda:0")
+    dcs = synth.ColumnSet([torch.from_numpy(c).to(dev) if not isinstance(c, tuple) else
+                           tuple(torch.from_numpy(x.view(np.int32) if x.dtype == np.uint32 else x).to(dev) for x in c)
+                           for c in cs.cols],
+                          torch.from_numpy(cs.presence.view(np.int64)).to(dev) if cs.presence is not None else None, n)
+    seq = torch.arange(n, dtype=torch.int32, device=dev) * 3 - 7
+    cdc = ThriftCodec(sch)
+    msgs, moffs = cdc.MarshalMessages(dcs, "Method_%s" % name, seq, msg_type=mtype, body_field=body_field)
+    exp = b"".join(write_message_begin("Method_%s" % name, mtype, i * 3 - 7) + bytes([12, 0, body_field])
+                   + bytes(wire[int(offs[i]):int(offs[i + 1])]) + b"\x00" for i in range(n))
+    assert bytes(msgs.cpu().numpy()) == exp
+    res = cdc.UnmarshalMessages(msgs, n, moffs, body_field=body_field)
+    _, infos, _ = oracle.flatten(sch)
+    rc, eout, est, _ = oracle.decode(sch, wire, n, offsets=offs)
+    assert_columns_equal(res.columns, eout, infos, n)
+    assert np.array_equal(res.seqid.cpu().numpy(), np.arange(n) * 3 - 7)
+    assert (res.msg_type.cpu().numpy() == mtype).all()
