@@ -102,6 +102,7 @@ struct DecParams {
   uint64_t epoch;            // 16-bit call epoch (never 0)
   uint32_t krec;             // offsets mode: records per tile (<= 64)
   uint32_t winb;             // window bytes loaded per tile: TILE + halo + 16 (<= WINB)
+  uint32_t nlist;            // numeric list columns (thrift): emit copies them wave-cooperatively
   int direct;                // offsets mode without var columns: emit pass only
   int nolds;                 // diagnostics (KX_NOLDS=1): read every byte from global memory
   int diag;                  // diagnostics (KX_DIAG bits, timing experiments only; output is wrong):
@@ -1119,6 +1120,17 @@ __device__ __forceinline__ uint64_t rl64(uint64_t v, int l) {
   uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), l);
   return ((uint64_t)hi << 32) | lo;
 }
+
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, int l) {
+  const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, l, 64);
+  const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), l, 64);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// emit: numeric list columns copied by the whole wave, one element per lane (1), or record by record (0)
+#ifndef KX_EMIT_COOP
+#define KX_EMIT_COOP 1
+#endif
 
 
 __device__ __forceinline__ uint64_t aload64(const uint64_t* p) {
@@ -2381,7 +2393,9 @@ __device__ __forceinline__ void emit_container(const Src& w, const KAS KxProgram
 }
 
 // ---- kernel 3: emit pass (one wave per tile, lane = record) ----
-template <int NV, int MODE>
+// COOP: numeric list columns are copied by the whole wave (its own instantiation, so that schemas
+// without such a column keep the record-by-record kernel's code)
+template <int NV, int MODE, bool COOP = false>
 __global__ void __launch_bounds__(NT, 4) emit_kernel(DecParams dp_) {  // 4 waves per SIMD: <= 128 VGPRs
   KParams& dp = KX_PARAMS();
   (void)dp_;
@@ -2477,6 +2491,43 @@ __global__ void __launch_bounds__(NT, 4) emit_kernel(DecParams dp_) {  // 4 wave
         }
       } else if (act && ((dp.cols.view >> cc) & 1)) {
         put_view(dp.cols, cc, r, vs.pos[v], vs.len[v]);
+      } else if (COOP && K.kind == KXP_K_LIST && K.width > 1 && !((dp.cols.view >> cc) & 1)) {
+        // wave-cooperative list copy: the wave's elements are one contiguous arena run [at0, at0 + T);
+        // lane e copies element e of it, finding its record by a binary search over the lanes' starts
+        const uint32_t nn = act ? vs.len[v] : 0;
+        const bool fits = act && at + nn <= arena_lim(dp.cols, cc);
+        if (act) {
+          if (fits) put_off(dp.cols, cc, r, at);
+          else atomicOr(dp.overflow, 1u);
+        }
+        const uint64_t at0 = rl64(at, 0);
+        const uint64_t rel = at - at0;
+        const uint64_t T = rl64(at + nn, 63) - at0;
+        const uint32_t okm = fits ? 1u : 0u;
+        const uint64_t psrc = vs.pos[v];
+        GLB uint8_t* cbase = (GLB uint8_t*)dp.cols.data[cc];
+        for (uint64_t e0 = 0; e0 < T; e0 += 64) {
+          const uint64_t e = e0 + lane;
+          int sl = 0;
+#pragma unroll
+          for (int step = 32; step >= 1; step >>= 1) {
+            const int c = sl + step;
+            if (shfl64(rel, c) <= e) sl = c;
+          }
+          const uint64_t rr = shfl64(rel, sl);
+          const uint64_t pr = shfl64(psrc, sl);
+          const uint32_t ok = (uint32_t)__shfl((int)okm, sl, 64);
+          if (e < T && ok) {
+            const uint64_t s = pr + (e - rr) * K.width;
+            const uint64_t d = at0 + e;
+            if (K.width == 8) ((GLB uint64_t*)cbase)[d] = be64(w, s);
+            else if (K.width == 4) ((GLB uint32_t*)cbase)[d] = be32(w, s);
+            else {
+              const uint32_t x = ld1(w, s) << 8 | ld1(w, s + 1);
+              ((GLB uint16_t*)cbase)[d] = (uint16_t)x;
+            }
+          }
+        }
       } else if (act) {
         const uint32_t nn = vs.len[v];
         if (at + nn <= arena_lim(dp.cols, cc)) {
@@ -2575,6 +2626,17 @@ DecParams chunk_params(const DecParams& dp, uint64_t k, uint64_t nch, uint64_t c
 }
 
 template <int NV, int MODE>
+void launch_emit(dim3 grid, hipStream_t stream, const DecParams& dp) {
+  if constexpr (is_thrift(MODE) && NV > 0) {
+    if (KX_EMIT_COOP && dp.nlist) {
+      hipLaunchKernelGGL((emit_kernel<NV, MODE, true>), grid, dim3(NT), 0, stream, dp);
+      return;
+    }
+  }
+  hipLaunchKernelGGL((emit_kernel<NV, MODE>), grid, dim3(NT), 0, stream, dp);
+}
+
+template <int NV, int MODE>
 int launch_t(const DecParams& dp0, const WsLayout& L, void* ws, hipStream_t stream, const KxPipe* pp) {
   DecParams dp = dp0;
   char* base = (char*)ws;
@@ -2626,7 +2688,7 @@ int launch_t(const DecParams& dp0, const WsLayout& L, void* ws, hipStream_t stre
         KX_HIP_CHECK(hipStreamWaitEvent(stream, pp->ev_idx[k % KX_PIPE_EV], 0));
         hipLaunchKernelGGL((chain_kernel<NV, MODE>), dim3(1), dim3(CT), 0, stream, c);
         KX_HIP_CHECK(hipGetLastError());
-        hipLaunchKernelGGL((emit_kernel<NV, MODE>), dim3(cg), dim3(NT), 0, stream, c);
+        launch_emit<NV, MODE>(dim3(cg), stream, c);
         KX_HIP_CHECK(hipGetLastError());
         KX_HIP_CHECK(hipEventRecord(pp->ev_emit[k % KX_PIPE_EV], stream));
       }
@@ -2658,7 +2720,7 @@ int launch_t(const DecParams& dp0, const WsLayout& L, void* ws, hipStream_t stre
     hipLaunchKernelGGL((chain_kernel<NV, MODE>), dim3(1), dim3(CT), 0, stream, dp);
     KX_HIP_CHECK(hipGetLastError());
   }
-  hipLaunchKernelGGL((emit_kernel<NV, MODE>), dim3(grid), dim3(NT), 0, stream, dp);
+  launch_emit<NV, MODE>(dim3(grid), stream, dp);
   KX_HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(64), 0, stream, dp.status, dp.errkey, dp.overflow, dp.nstop,
                      dp.offsets, dp.n);
@@ -2787,6 +2849,10 @@ int kx_launch_decode(const KxProgram* dprog, const KxProgram& hprog, const uint8
   dp.cols = cols; dp.rstat = record_status; dp.status = status; dp.epoch = epoch;
   dp.krec = krec_for(in_len, n);
   dp.winb = win_bytes(in_len, n);
+  for (uint32_t c = 0; c < hprog.ncols; c++) {
+    const KxpCol& K = hprog.col[c];
+    dp.nlist += K.kind == KXP_K_LIST && K.width > 1 && !K.mside && !((cols.view >> c) & 1);
+  }
   const WsLayout L = ws_layout(hprog.fixed_min, in_len, offsets, n);
   if (ws_size < L.total) return KX_ERR_INVALID_ARG;
   bool ls = false;
