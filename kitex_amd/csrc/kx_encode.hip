@@ -29,6 +29,10 @@ constexpr int RB = 1024;             // records per block
 #ifndef KX_ENC_LISTPF
 #define KX_ENC_LISTPF 1
 #endif
+// the write pass stages a round through the LDS image when at least cnt >> KX_ENC_MINTAKE of its records fit
+#ifndef KX_ENC_MINTAKE
+#define KX_ENC_MINTAKE 1
+#endif
 #ifndef KX_ENC_OUTB
 #define KX_ENC_OUTB (48 * 1024)
 #endif
@@ -505,7 +509,7 @@ __global__ void __launch_bounds__(WT, KX_ENC_LB) write_kernel(EncParams ep) {
     __syncthreads();
     uint64_t take = s_take;
     const uint64_t cnt = kmin64((uint64_t)WT, rend - r);
-    if (take < cnt / 2 || ep.direct) {
+    if (take < (cnt >> KX_ENC_MINTAKE) || ep.direct) {
       // large records (fewer than half of the round fit the image): every thread writes its record
       // straight to HBM; its aligned dword stores still merge in L2
       if (my < rend) {
