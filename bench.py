@@ -46,7 +46,41 @@ def parse():
     ap.add_argument("--no-extra", action="store_true")
     ap.add_argument("--no-concat", action="store_true", help="N>1: skip the RCCL concatenation into rank 0")
     ap.add_argument("--cpu-records", type=int, default=4 * 1024 * 1024)
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launch / rendezvous check only: no GPU call, gloo between the ranks")
     return ap.parse_args()
+
+
+def launch_ranks(args) -> int:
+    """--gpus N > 1 without a torch.distributed launcher around us: start N ranks (one process per GPU)
+    with torch.distributed.run as a CHILD (this process has not touched the GPU, and never execs) and
+    return its exit code. Every rank re-enters main() with WORLD_SIZE set."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    return subprocess.run(cmd, env=env).returncode
+
+
+def dry_run(args, world, rank):
+    """the launch path without the GPU: ranks meet over gloo, agree on the world size, rank 0 prints"""
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo")
+        t = torch.tensor([1], dtype=torch.int64)
+        dist.all_reduce(t)
+        seen = int(t.item())
+        dist.destroy_process_group()
+    else:
+        seen = 1
+    if rank == 0:
+        print(json.dumps({"metric": "dry-run", "n_gpus": world, "ranks_seen": seen, "gpus_flag": args.gpus,
+                          "dry_run": True}), flush=True)
 
 
 def last_offset(off) -> int:
@@ -209,12 +243,18 @@ def roofline(alg_bytes, avg_launch_s, kernel, traffic=None, note=None):
 
 def main():
     args = parse()
-    import torch
-    import torch.distributed as dist
-
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU")
+    if args.dry_run:
+        dry_run(args, world, rank)
+        return
+    import torch
+    import torch.distributed as dist
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -363,7 +403,7 @@ def concat_shards(batches, world, rank, dev):
     dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    outs = concat_batches_to_root([(b.out, b.n, b.infos) for b in batches])
+    outs = concat_batches_to_root([(b.out, b.n, b.infos, b.in_bytes) for b in batches])
     torch.cuda.synchronize()
     dist.barrier()
     tc = time.perf_counter() - t0

@@ -413,6 +413,18 @@ class ThriftCodec:
             raise KxError(A.ERR_NOT_IMPLEMENTED, "MarshalMessages: Thrift only")
         ds = self.dschema
         n = cols.n
+        # the kernel reads int32[n] seqids from device memory: anything else is converted or refused here
+        if not isinstance(seqids, torch.Tensor):
+            seqids = torch.as_tensor(seqids, dtype=torch.int32)
+        if seqids.dtype != torch.int32:
+            if seqids.dtype.is_floating_point or seqids.dtype == torch.bool:
+                raise KxError(A.ERR_INVALID_ARG, f"MarshalMessages: seqids must be integers, got {seqids.dtype}")
+            if n and (int(seqids.min()) < -(1 << 31) or int(seqids.max()) >= (1 << 31)):
+                raise KxError(A.ERR_INVALID_ARG, "MarshalMessages: a seqid does not fit in int32")
+            seqids = seqids.to(torch.int32)
+        if seqids.dim() != 1 or seqids.numel() < n:
+            raise KxError(A.ERR_INVALID_ARG, f"MarshalMessages: need {n} seqids, got shape {tuple(seqids.shape)}")
+        seqids = seqids.to(self.device).contiguous()
         kc = to_kx_columns(cols, ds.infos)
         body = int(self.BLength(cols, stream=stream).sum().item()) if n else 0
         nb = method.encode()

@@ -394,7 +394,7 @@ int kx_thrift_encode_messages(kx_ctx* c, const kx_schema* s, const kx_columns* i
   }
   // the status keeps the record encoder's code (SIZE_LIMIT: the scratch is too small); the message pass
   // sets consumed / n_records and SIZE_LIMIT when `out` is too small
-  return kx_launch_message_encode(body_scratch, boff, n, dname, name_len, msg_type, seqids, body_field, out,
+  return kx_launch_message_encode(body_scratch, boff, scratch_cap, n, dname, name_len, msg_type, seqids, body_field, out,
                                   out_cap, offsets_out, status, st);
 }
 

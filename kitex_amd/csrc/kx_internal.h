@@ -128,7 +128,8 @@ int kx_launch_message_headers(const uint8_t* in, uint64_t in_len, const uint64_t
                               int raw = 0);
 int kx_launch_set_seqids(uint8_t* in, uint64_t in_len, const uint64_t* offsets, uint64_t n, const int32_t* seqids,
                          uint8_t* record_status, kx_status* status, void* mws, hipStream_t stream);
-int kx_launch_message_encode(const uint8_t* bodies, const uint64_t* body_off, uint64_t n, const uint8_t* name,
+int kx_launch_message_encode(const uint8_t* bodies, const uint64_t* body_off, uint64_t scratch_cap, uint64_t n,
+                             const uint8_t* name,
                              uint32_t name_len, int32_t msg_type, const int32_t* seqids, int32_t body_field,
                              uint8_t* out, uint64_t out_cap, uint64_t* offsets_out, kx_status* status,
                              hipStream_t stream);

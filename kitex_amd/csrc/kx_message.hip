@@ -291,6 +291,7 @@ __global__ void __launch_bounds__(MT) setseq_kernel(uint8_t* in, uint64_t in_len
 struct MsgEnc {
   const uint8_t* bodies;
   const uint64_t* body_off;  // n + 1
+  uint64_t scratch_cap;      // bytes readable at `bodies`
   uint64_t n;
   const uint8_t* name;       // device copy of the method name
   uint32_t name_len;
@@ -306,8 +307,16 @@ struct MsgEnc {
 __global__ void __launch_bounds__(MT) msgenc_kernel(MsgEnc me) {
   const uint64_t i = (uint64_t)blockIdx.x * MT + threadIdx.x;
   if (i > me.n) return;
+  // the record encoder failed (SIZE_LIMIT: the scratch is too small, or a record error): its offsets were
+  // never written, so nothing here may read them; the status keeps the encoder's code and counts
+  if (me.status->code != 0) return;
   const uint64_t H = 12ull + me.name_len + 3ull;
-  const uint64_t at = me.body_off[i] + i * (H + 1);
+  const uint64_t bo = me.body_off[i];
+  if (bo > me.scratch_cap || me.body_off[me.n] > me.scratch_cap) {  // inconsistent offsets: never read past them
+    if (i == me.n) me.status->code = KX_ERR_SIZE_LIMIT;
+    return;
+  }
+  const uint64_t at = bo + i * (H + 1);
   if (me.offsets_out) me.offsets_out[i] = at;
   if (i == me.n) {
     me.status->n_records = me.n;
@@ -315,8 +324,10 @@ __global__ void __launch_bounds__(MT) msgenc_kernel(MsgEnc me) {
     if (at > me.out_cap) me.status->code = KX_ERR_SIZE_LIMIT;
     return;
   }
-  const uint64_t bl = me.body_off[i + 1] - me.body_off[i];
-  if (at + H + bl + 1 > me.out_cap) return;  // the call fails with SIZE_LIMIT (thread n)
+  const uint64_t bn = me.body_off[i + 1];
+  if (bn < bo || bn > me.scratch_cap) return;  // (thread n reports the inconsistency)
+  const uint64_t bl = bn - bo;
+  if (at > me.out_cap || me.out_cap - at < H + bl + 1) return;  // the call fails with SIZE_LIMIT (thread n)
   uint8_t* o = me.out + at;
   const uint32_t v = 0x80010000u | ((uint32_t)me.msg_type & 0xffu);  // strict version | type
   const uint32_t nl = me.name_len, sq = (uint32_t)me.seqids[i];
@@ -490,11 +501,12 @@ int kx_launch_set_seqids(uint8_t* in, uint64_t in_len, const uint64_t* offsets, 
   return KX_OK;
 }
 
-int kx_launch_message_encode(const uint8_t* bodies, const uint64_t* body_off, uint64_t n, const uint8_t* name,
+int kx_launch_message_encode(const uint8_t* bodies, const uint64_t* body_off, uint64_t scratch_cap, uint64_t n,
+                             const uint8_t* name,
                              uint32_t name_len, int32_t msg_type, const int32_t* seqids, int32_t body_field,
                              uint8_t* out, uint64_t out_cap, uint64_t* offsets_out, kx_status* status,
                              hipStream_t stream) {
-  MsgEnc me{bodies, body_off, n, name, name_len, msg_type, seqids, body_field, out, out_cap, offsets_out, status};
+  MsgEnc me{bodies, body_off, scratch_cap, n, name, name_len, msg_type, seqids, body_field, out, out_cap, offsets_out, status};
   const unsigned grid = (unsigned)((n + 1 + MT - 1) / MT);
   hipLaunchKernelGGL(msgenc_kernel, dim3(grid), dim3(MT), 0, stream, me);
   KX_HIP_CHECK(hipGetLastError());

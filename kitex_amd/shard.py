@@ -37,114 +37,251 @@ def _unsigned(t):
     return t if t.dtype == torch.int64 else t.to(torch.int64) & 0xFFFFFFFF
 
 
-def concat_to_root(cols: ColumnSet, n_local: int, infos: Sequence[A.ColumnInfo], root: int = 0,
-                   group=None) -> Optional[ColumnSet]:
-    """Concatenate every rank's decoded shard (records in rank order) into `root`.
+def _kind(col, ci) -> str:
+    """how a decoded column is laid out: 'fixed' values[n]; 'var' (offsets[n+1], arena) for strings /
+    numeric lists / a map's fixed side; 'lb' (record offsets in elements, element byte offsets, bytes) for
+    list/set<string> and a map's string side; 'view' (offset, length) pairs into the decode input"""
+    from .columns import Views
+    if isinstance(col, Views):
+        return "view"
+    if ci.kind == A.COL_FIXED:
+        return "fixed"
+    return "lb" if len(col) == 3 else "var"
 
-    `cols` holds this rank's decoded columns (torch tensors on this rank's device, or CPU for
-    gloo): FIXED -> tensor[>= n_local], BYTES/LIST -> (offsets[>= n_local + 1] int32 (uint32 values)
-    or int64, arena). Returns the concatenated ColumnSet on root (int64 offsets), None elsewhere."""
+
+def _meta(cols: ColumnSet, n: int, infos, in_len: int, dev):
+    """this rank's exchange header, built on the device: n, input bytes, then per var column its first
+    offset and units (and for 'lb' the first element byte offset and bytes)"""
     import torch
-    import torch.distributed as dist
+    parts = [torch.tensor([n, in_len], dtype=torch.int64, device=dev)]
+    for c, ci in enumerate(infos):
+        k = _kind(cols.cols[c], ci)
+        if k in ("var", "lb"):
+            off = cols.cols[c][0]
+            f, l = _unsigned(off[0:1]), _unsigned(off[n:n + 1])
+            parts += [f, l - f]
+            if k == "lb":
+                eo = cols.cols[c][1]
+                ef, el = _unsigned(eo.index_select(0, f)), _unsigned(eo.index_select(0, l))
+                parts += [ef, el - ef]
+    return torch.cat(parts)
 
-    rank = dist.get_rank(group)
-    world = dist.get_world_size(group)
-    dev = cols.cols[0][0].device if isinstance(cols.cols[0], tuple) else cols.cols[0].device
-    var = [c for c, ci in enumerate(infos) if ci.kind != A.COL_FIXED]
-    # meta: n, then per var column (first offset, units); built on the device, one exchange
-    firsts = [_unsigned(cols.cols[c][0][0:1]) for c in var]
-    lasts = [_unsigned(cols.cols[c][0][n_local:n_local + 1]) for c in var]
-    parts = [torch.tensor([n_local], dtype=torch.int64, device=dev)]
-    for f, l in zip(firsts, lasts):
-        parts += [f, l - f]
-    meta = torch.cat(parts)
-    metas = [torch.empty_like(meta) for _ in range(world)]
-    dist.all_gather(metas, meta, group=group)
-    metas = torch.stack(metas).cpu().tolist()
-    counts = [m[0] for m in metas]
-    first = [m[1::2] for m in metas]
-    units = [m[2::2] for m in metas]
-    N = sum(counts)
-    rec0 = [sum(counts[:r]) for r in range(world)]
-    arena0 = [[sum(units[q][j] for q in range(r)) for j in range(len(var))] for r in range(world)]
 
-    # what this rank sends / root receives, in a fixed order: per column then presence
-    def local_parts(cs: ColumnSet, r: int, n: int):
+def rebase(dst, src, delta: int):
+    """dst[:] = src (uint32 values in int32, or int64) + delta, as int64, on src's device: the offset
+    rebase of the concatenation (one add per rank slice, no host round trip)"""
+    if dst.numel():
+        dst.copy_(_unsigned(src) + delta)
+
+
+def rebase_views(dst, src, delta: int):
+    """(offset, length) pairs moved by `delta` input bytes; empty views stay (0, 0) (put_view)"""
+    import torch
+    if not dst.numel():
+        return
+    s = _unsigned(src)
+    dst[:, 1] = s[:, 1]
+    dst[:, 0] = torch.where(s[:, 1] != 0, s[:, 0] + delta, torch.zeros_like(s[:, 0]))
+
+
+class _Plan:
+    """Where every rank's slice lands in the concatenation, from the ranks' exchange headers (_meta)."""
+
+    def __init__(self, metas, kinds):
+        self.kinds = kinds
+        self.world = world = len(metas)
+        self.counts = [m[0] for m in metas]
+        inl = [m[1] for m in metas]
+        self.info = []  # per rank, per var column: (first, units, first element byte, bytes)
+        for m in metas:
+            i, d = 2, {}
+            for c, k in enumerate(kinds):
+                if k == "var":
+                    d[c] = (m[i], m[i + 1], 0, 0)
+                    i += 2
+                elif k == "lb":
+                    d[c] = (m[i], m[i + 1], m[i + 2], m[i + 3])
+                    i += 4
+            self.info.append(d)
+        self.N = sum(self.counts)
+        self.rec0 = [sum(self.counts[:r]) for r in range(world)]
+        self.in0 = [sum(inl[:r]) for r in range(world)]
+        cs = [c for c, k in enumerate(kinds) if k in ("var", "lb")]
+        self.ub = {c: [sum(self.info[q][c][1] for q in range(r)) for r in range(world + 1)] for c in cs}
+        self.bb = {c: [sum(self.info[q][c][3] for q in range(r)) for r in range(world + 1)] for c in cs}
+
+    def local_parts(self, cs: ColumnSet, r: int, n: int):
+        """what rank r contributes, in a fixed order: per column its pieces, then presence"""
         out = []
-        for c, ci in enumerate(infos):
-            if ci.kind == A.COL_FIXED:
-                out.append(cs.cols[c][:n])
+        for c, k in enumerate(self.kinds):
+            col = cs.cols[c]
+            if k == "fixed":
+                out.append(col[:n])
+            elif k == "view":
+                out.append(col.pairs[:n])
             else:
-                j = var.index(c)
-                off, data = cs.cols[c]
-                o0 = first[r][j]
-                out.append(off[:n])
-                out.append(data[o0:o0 + units[r][j]])
+                f, u, ef, eb = self.info[r][c]
+                out.append(col[0][:n])
+                out.append(col[1][f:f + u])
+                if k == "lb":
+                    out.append(col[2][ef:ef + eb])
         if cs.presence is not None:
             out.append(cs.presence[:n])
         return out
 
-    if rank != root:
-        ops = [dist.P2POp(dist.isend, t.contiguous(), root, group) for t in local_parts(cols, rank, n_local)
-               if t.numel()]
-        for req in dist.batch_isend_irecv(ops) if ops else []:
-            req.wait()
-        return None
+    def alloc(self, like: ColumnSet, dev):
+        """the concatenated batch (int64 offsets / views) and the staging of the ranks' offsets / views
+        (in the senders' dtypes) that the rebase reads"""
+        import torch
 
-    # root: receive buffers (offsets in the senders' dtype), the concatenated batch (int64 offsets)
-    out_cols: List[object] = []
-    recv_off = {}
-    for c, ci in enumerate(infos):
-        if ci.kind == A.COL_FIXED:
-            t = cols.cols[c]
-            out_cols.append(torch.empty(N, dtype=t.dtype, device=dev))
-        else:
-            j = var.index(c)
-            off, data = cols.cols[c]
-            tot = sum(units[r][j] for r in range(world))
-            out_cols.append((torch.empty(N + 1, dtype=torch.int64, device=dev),
-                             torch.empty(max(1, tot), dtype=data.dtype, device=dev)))
-            recv_off[c] = torch.empty(max(1, N), dtype=off.dtype, device=dev)
-    out_pres = torch.empty(N, dtype=cols.presence.dtype, device=dev) if cols.presence is not None else None
-    out = ColumnSet(out_cols, out_pres, N)
-
-    def dest_parts(r: int):
-        d = []
-        a, b = rec0[r], rec0[r] + counts[r]
-        for c, ci in enumerate(infos):
-            if ci.kind == A.COL_FIXED:
-                d.append(out.cols[c][a:b])
+        from .columns import Views
+        N, W = self.N, self.world
+        out_cols, self.recv = [], {}
+        for c, k in enumerate(self.kinds):
+            col = like.cols[c]
+            if k == "fixed":
+                out_cols.append(torch.empty(N, dtype=col.dtype, device=dev))
+            elif k == "view":
+                out_cols.append(Views(torch.empty((max(1, N), 2), dtype=torch.int64, device=dev)))
+                self.recv[c] = (torch.empty((max(1, N), 2), dtype=col.pairs.dtype, device=dev),)
+            elif k == "var":
+                out_cols.append((torch.empty(N + 1, dtype=torch.int64, device=dev),
+                                 torch.empty(max(1, self.ub[c][W]), dtype=col[1].dtype, device=dev)))
+                self.recv[c] = (torch.empty(max(1, N), dtype=col[0].dtype, device=dev),)
             else:
-                j = var.index(c)
-                _, data = out.cols[c]
-                d.append(recv_off[c][a:b])
-                d.append(data[arena0[r][j]:arena0[r][j] + units[r][j]])
+                E = self.ub[c][W]
+                out_cols.append((torch.empty(N + 1, dtype=torch.int64, device=dev),
+                                 torch.empty(E + 1, dtype=torch.int64, device=dev),
+                                 torch.empty(max(1, self.bb[c][W]), dtype=col[2].dtype, device=dev)))
+                self.recv[c] = (torch.empty(max(1, N), dtype=col[0].dtype, device=dev),
+                                torch.empty(max(1, E), dtype=col[1].dtype, device=dev))
+        pres = torch.empty(N, dtype=like.presence.dtype, device=dev) if like.presence is not None else None
+        self.out = ColumnSet(out_cols, pres, N)
+        return self.out
+
+    def dest_parts(self, r: int):
+        """where rank r's pieces (local_parts order) are received"""
+        out, d = self.out, []
+        a, b = self.rec0[r], self.rec0[r] + self.counts[r]
+        for c, k in enumerate(self.kinds):
+            if k == "fixed":
+                d.append(out.cols[c][a:b])
+            elif k == "view":
+                d.append(self.recv[c][0][a:b])
+            else:
+                f, u, ef, eb = self.info[r][c]
+                u0 = self.ub[c][r]
+                d.append(self.recv[c][0][a:b])
+                if k == "lb":
+                    d.append(self.recv[c][1][u0:u0 + u])
+                    d.append(out.cols[c][2][self.bb[c][r]:self.bb[c][r] + eb])
+                else:
+                    d.append(out.cols[c][1][u0:u0 + u])
         if out.presence is not None:
             d.append(out.presence[a:b])
         return d
 
+    def rebase_all(self):
+        """every rank's slice, on the device: record offsets by the units before it, element byte offsets
+        by the bytes before it, views by the input bytes before it; then the closing offsets"""
+        out, W = self.out, self.world
+        for c, k in enumerate(self.kinds):
+            if k == "fixed":
+                continue
+            for r in range(W):
+                a, b = self.rec0[r], self.rec0[r] + self.counts[r]
+                if k == "view":
+                    rebase_views(out.cols[c].pairs[a:b], self.recv[c][0][a:b], self.in0[r])
+                    continue
+                f, u, ef, eb = self.info[r][c]
+                u0 = self.ub[c][r]
+                rebase(out.cols[c][0][a:b], self.recv[c][0][a:b], u0 - f)
+                if k == "lb":
+                    rebase(out.cols[c][1][u0:u0 + u], self.recv[c][1][u0:u0 + u], self.bb[c][r] - ef)
+            if k == "view":
+                continue
+            out.cols[c][0][self.N] = self.ub[c][W]
+            if k == "lb":
+                out.cols[c][1][self.ub[c][W]] = self.bb[c][W]
+
+
+def _check_views(kinds, in_len):
+    from ._lib import KxError
+    if "view" in kinds and in_len is None:
+        raise KxError(A.ERR_NOT_IMPLEMENTED, "concat: view columns need in_len (the shard's input bytes)")
+
+
+def _device_of(cols: ColumnSet):
+    from .columns import Views
+    t = cols.cols[0]
+    return (t.pairs if isinstance(t, Views) else t[0] if isinstance(t, tuple) else t).device
+
+
+def concat_to_root(cols: ColumnSet, n_local: int, infos: Sequence[A.ColumnInfo], root: int = 0,
+                   group=None, in_len: Optional[int] = None) -> Optional[ColumnSet]:
+    """Concatenate every rank's decoded shard (records in rank order) into `root`.
+
+    `cols` holds this rank's decoded columns (torch tensors on this rank's device, or CPU for gloo),
+    as the decoder writes them (kitex_amd.columns): FIXED -> tensor[>= n_local]; BYTES / LIST / a map's
+    fixed side -> (offsets[>= n_local + 1], arena); LIST_BYTES (list/set<string>, a map's string side)
+    -> (record offsets in elements, element byte offsets, bytes); offsets int32 (uint32 values) or
+    int64; zero-copy string views -> Views(pairs[n, 2]). Views point into this rank's decode input: they
+    are rebased into the concatenation of the ranks' inputs in rank order, so `in_len` (this rank's input
+    bytes) is required for them. Returns the concatenated ColumnSet on root (int64 offsets and views),
+    None elsewhere."""
+    import torch
+    import torch.distributed as dist
+
+    kinds = [_kind(cols.cols[c], ci) for c, ci in enumerate(infos)]
+    _check_views(kinds, in_len)
+    rank = dist.get_rank(group)
+    world = dist.get_world_size(group)
+    dev = _device_of(cols)
+    meta = _meta(cols, n_local, infos, int(in_len or 0), dev)
+    metas = [torch.empty_like(meta) for _ in range(world)]
+    dist.all_gather(metas, meta, group=group)
+    plan = _Plan(torch.stack(metas).cpu().tolist(), kinds)
+    if rank != root:
+        ops = [dist.P2POp(dist.isend, t.contiguous(), root, group) for t in plan.local_parts(cols, rank, n_local)
+               if t.numel()]
+        for req in dist.batch_isend_irecv(ops) if ops else []:
+            req.wait()
+        return None
+    out = plan.alloc(cols, dev)
     ops = []
     for r in range(world):
         if r == root:
-            for d, s_ in zip(dest_parts(r), local_parts(cols, r, n_local)):
+            for d, s_ in zip(plan.dest_parts(r), plan.local_parts(cols, r, n_local)):
                 d.copy_(s_)
         else:
-            ops += [dist.P2POp(dist.irecv, d, r, group) for d in dest_parts(r) if d.numel()]
+            ops += [dist.P2POp(dist.irecv, d, r, group) for d in plan.dest_parts(r) if d.numel()]
     for req in dist.batch_isend_irecv(ops) if ops else []:
         req.wait()
-    # rebase: rank r's offsets start at its own first offset, move them to arena0[r] (device adds)
-    for c in var:
-        j = var.index(c)
-        off, _ = out.cols[c]
-        for r in range(world):
-            a, b = rec0[r], rec0[r] + counts[r]
-            if b > a:
-                off[a:b] = _unsigned(recv_off[c][a:b]) + (arena0[r][j] - first[r][j])
-        off[N] = sum(units[r][j] for r in range(world))
+    plan.rebase_all()
     return out
+
+
+def concat_local(shards, infos: Sequence[A.ColumnInfo]) -> ColumnSet:
+    """The same concatenation of decoded shards that live in one process (one device): shards =
+    [(ColumnSet, n, in_len or None)] in record order. What concat_to_root does on the root, with the
+    exchange replaced by device copies (single-GPU tests of config 5, several ctxs / streams)."""
+    kinds = [_kind(shards[0][0].cols[c], ci) for c, ci in enumerate(infos)]
+    for s_ in shards:
+        _check_views(kinds, s_[2] if len(s_) > 2 else None)
+    dev = _device_of(shards[0][0])
+    metas = [_meta(cs, n, infos, int((rest[0] if rest else 0) or 0), dev).cpu().tolist()
+             for cs, n, *rest in shards]
+    plan = _Plan(metas, kinds)
+    plan.alloc(shards[0][0], dev)
+    for r, (cs, n, *_) in enumerate(shards):
+        for d, s_ in zip(plan.dest_parts(r), plan.local_parts(cs, r, n)):
+            if d.numel():
+                d.copy_(s_)
+    plan.rebase_all()
+    return plan.out
 
 
 def concat_batches_to_root(batches, root: int = 0, group=None):
     """Config 5: several decoded batches per rank (one per schema, e.g. R2 and R3), each
-    concatenated across the ranks into root. batches: [(ColumnSet, n_local, infos)]."""
-    return [concat_to_root(cs, n, infos, root, group) for cs, n, infos in batches]
+    concatenated across the ranks into root. batches: [(ColumnSet, n_local, infos[, in_len])]."""
+    return [concat_to_root(b[0], b[1], b[2], root, group, *(b[3:4])) for b in batches]

@@ -212,3 +212,55 @@ def test_marshal_messages_matches_oracle_and_round_trips(torch, oracle, name, bo
     assert_columns_equal(res.columns, eout, infos, n)
     assert np.array_equal(res.seqid.cpu().numpy(), np.arange(n) * 3 - 7)
     assert (res.msg_type.cpu().numpy() == mtype).all()
+
+
+def test_marshal_messages_short_scratch_is_size_limit(torch, oracle):
+    """kx_thrift_encode_messages with a record scratch too small for the bodies and a large `out`: the
+    call reports SIZE_LIMIT and the message pass never reads the (unwritten) record offsets"""
+    import ctypes as C
+    from kitex_amd import schema as S, synth
+    from kitex_amd._lib import lib
+    from kitex_amd.codec import ThriftCodec, read_status, status_tensor
+    from kitex_amd.columns import to_kx_columns
+    n = 4000
+    dev = torch.device("cuda:0")
+    sch = S.schema_r2()
+    cdc = ThriftCodec(sch)
+    src = synth.TORCH_GENERATORS["r2"](n, dev)
+    body = int(cdc.BLength(src).sum().item())
+    seq = torch.arange(n, dtype=torch.int32, device=dev)
+    # run a bigger call first so the context's offset buffer holds stale entries past this call's n + 1
+    big = synth.TORCH_GENERATORS["r2"](2 * n, dev)
+    cdc.MarshalMessages(big, "m", torch.arange(2 * n, dtype=torch.int32, device=dev))
+    nb = b"Method"
+    for scratch_len in (1, body // 2, body - 1):
+        scratch = torch.empty(scratch_len, dtype=torch.uint8, device=dev)
+        out = torch.full((body * 4 + n * 64,), 0xAB, dtype=torch.uint8, device=dev)
+        offs = torch.empty(n + 1, dtype=torch.int64, device=dev)
+        st = status_tensor(dev)
+        kc = to_kx_columns(src, cdc.dschema.infos)
+        s = torch.cuda.current_stream()
+        rc = lib().kx_thrift_encode_messages(cdc.ctx.handle, cdc.dschema.handle, C.byref(kc), n, nb, len(nb), 1,
+                                             seq.data_ptr(), 1, scratch.data_ptr(), scratch.numel(), out.data_ptr(),
+                                             out.numel(), offs.data_ptr(), st.data_ptr(), int(s.cuda_stream))
+        assert rc == 0
+        stt = read_status(st, s)
+        assert stt.code == A.ERR_SIZE_LIMIT, (scratch_len, stt.code)
+        assert bool((out == 0xAB).all()), "no message may be written from unwritten offsets"
+
+
+def test_marshal_messages_checks_seqids(torch):
+    from kitex_amd import schema as S, synth
+    from kitex_amd._lib import KxError
+    from kitex_amd.codec import ThriftCodec
+    dev = torch.device("cuda:0")
+    cdc = ThriftCodec(S.schema_r2())
+    src = synth.TORCH_GENERATORS["r2"](100, dev)
+    with pytest.raises(KxError):
+        cdc.MarshalMessages(src, "m", torch.arange(50, dtype=torch.int32, device=dev))      # too short
+    with pytest.raises(KxError):
+        cdc.MarshalMessages(src, "m", torch.zeros(100, dtype=torch.float32, device=dev))   # not integers
+    # int64 host tensor: converted (values fit) and moved to the device
+    msgs, offs = cdc.MarshalMessages(src, "m", torch.arange(100, dtype=torch.int64))
+    res = cdc.UnmarshalMessages(msgs, 100, offs)
+    assert res.seqid.cpu().tolist() == list(range(100))

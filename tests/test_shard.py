@@ -31,12 +31,24 @@ def _free_port():
 
 def _to_torch(cs):
     import torch
+
+    from kitex_amd.columns import Views
+
+    def t(a):
+        a = np.ascontiguousarray(a)
+        if a.dtype == np.uint32:
+            a = a.view(np.int32)
+        elif a.dtype == np.uint64:
+            a = a.view(np.int64)
+        return torch.from_numpy(a.copy())
     cols = []
     for c in cs.cols:
-        if isinstance(c, tuple):
-            cols.append((torch.from_numpy(c[0].view(np.int32).copy()), torch.from_numpy(c[1].copy())))
+        if isinstance(c, Views):
+            cols.append(Views(t(c.pairs)))
+        elif isinstance(c, tuple):
+            cols.append(tuple(t(x) for x in c))
         else:
-            cols.append(torch.from_numpy(c.copy()))
+            cols.append(t(c))
     pres = torch.from_numpy(cs.presence.view(np.int64).copy()) if cs.presence is not None else None
     return synth.ColumnSet(cols, pres, cs.n)
 
@@ -156,3 +168,100 @@ def test_concat_mixed_emulator_decoded_shards_gloo():
     for p in ps:
         p.join(timeout=60)
     assert all(v == "ok" for v in res.values()), res
+
+
+_CX = {"cx1": (S.schema_cx1, synth.gen_cx1), "cx2": (S.schema_cx2, synth.gen_cx2)}
+
+
+def _oracle_worker(rank, world, port, name, n, views, q):
+    """every rank holds the oracle decode of its own shard (containers: list<string>, set<string>,
+    maps; or R2 with zero-copy string views); rank 0 compares the concatenation with the oracle's decode
+    of the ranks' wires concatenated"""
+    import torch.distributed as dist
+
+    from kitex_amd.shard import concat_to_root
+    from oracle import oracle
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        mk_s, gen = _CX.get(name, (S.SCHEMAS.get(name), synth.GENERATORS.get(name)))
+        sch = mk_s()
+        _, infos, _ = oracle.flatten(sch)
+        shards = [shard_range(n, world, r) for r in range(world)]
+        wires = []
+        for s0, cnt in shards:
+            rc, w, _ = oracle.encode(sch, gen(cnt, start=s0))
+            assert rc == 0
+            wires.append(w)
+        s0, cnt = shards[rank]
+        rc, local, st, _ = oracle.decode(sch, wires[rank], cnt, views=views)
+        assert rc == 0 and st.code == 0
+        out = concat_to_root(_to_torch(local), cnt, infos, in_len=wires[rank].size)
+        if rank == 0:
+            from tests.helpers import assert_columns_equal, offsets_u64
+            whole = np.concatenate(wires)
+            rc, exp, est, _ = oracle.decode(sch, whole, n, views=views)
+            assert rc == 0 and est.code == 0 and out.n == n
+            assert_columns_equal(out, exp, infos, n)
+            for c, ci in enumerate(infos):
+                if isinstance(exp.cols[c], tuple):
+                    assert int(offsets_u64(out.cols[c][0])[n]) == int(offsets_u64(exp.cols[c][0])[n])
+        q.put((rank, "ok"))
+    except Exception as e:  # report to the parent
+        import traceback
+        q.put((rank, repr(e) + traceback.format_exc()[-800:]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,name,n,views", [(2, "cx1", 3001, False), (3, "cx2", 2500, False),
+                                                 (2, "r2", 4001, True), (3, "r3", 1200, False)])
+def test_concat_containers_and_views_gloo(world, name, n, views):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_oracle_worker, args=(r, world, port, name, n, views, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in range(world))
+    for p in ps:
+        p.join(timeout=60)
+    assert all(v == "ok" for v in res.values()), res
+
+
+def test_concat_views_need_in_len():
+    """views point into the rank's own input: without its length they cannot be rebased"""
+    from kitex_amd import _abi as A
+    from kitex_amd._lib import KxError
+    from kitex_amd.columns import Views
+    from kitex_amd.shard import concat_to_root
+    import torch
+    cs = synth.ColumnSet([Views(torch.zeros((4, 2), dtype=torch.int32))], None, 4)
+    ci = A.ColumnInfo()
+    ci.kind = A.COL_BYTES
+    with pytest.raises(KxError):
+        concat_to_root(cs, 4, [ci])
+
+
+@pytest.mark.parametrize("name,views", [("cx1", False), ("r2", True), ("r3", False)])
+def test_concat_local_matches_whole(oracle, name, views):
+    """concat_local (one process, several shards): same plan and rebase as concat_to_root"""
+    from kitex_amd.shard import concat_local
+    from tests.helpers import assert_columns_equal
+    mk_s, gen = _CX.get(name, (S.SCHEMAS.get(name), synth.GENERATORS.get(name)))
+    sch = mk_s()
+    _, infos, _ = oracle.flatten(sch)
+    n, parts = 2003, 3
+    shards, wires = [], []
+    for r in range(parts):
+        s0, cnt = shard_range(n, parts, r)
+        rc, w, _ = oracle.encode(sch, gen(cnt, start=s0))
+        rc, local, st, _ = oracle.decode(sch, w, cnt, views=views)
+        assert rc == 0 and st.code == 0
+        shards.append((_to_torch(local), cnt, w.size))
+        wires.append(w)
+    out = concat_local(shards, infos)
+    rc, exp, est, _ = oracle.decode(sch, np.concatenate(wires), n, views=views)
+    assert est.code == 0
+    assert_columns_equal(out, exp, infos, n)
