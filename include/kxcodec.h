@@ -405,6 +405,46 @@ int kx_frame_crc32c_validate(kx_ctx* c, const uint8_t* in, uint64_t in_len, cons
  * message gets KX_ERR_PAYLOAD_VALIDATION (its record is not decoded). Default off. */
 int kx_ctx_set_crc32c_check(kx_ctx* c, int enable);
 
+/* ---- TTHeader streaming frames (ttstream DecodeFrame, pkg/remote/trans/ttstream/frame.go:137-185) ----
+ * in = n frames of one connection back to back, each a TTHeader (gopkg protocol/ttheader) whose payload is
+ * a bare struct (ProtocolIDThriftStruct / ProtobufStruct: gopkgthrift.FastMarshal, no MessageBegin,
+ * frame.go:92-130, 192-233). Per frame: frame_offsets[i] (n + 1), payload [payload_start[i], payload_end[i])
+ * (PayloadLen bytes after the header), frame_types[i] = KX_TTS_* from IntInfo[frame_type_key] (an
+ * unknown value is KX_ERR_INVALID_DATA: "unexpected frame type", :166-167), stream_ids[i] = the TTHeader
+ * seqid (the stream id, :170), method_pos[i] / method_len[i] = IntInfo[to_method_key] inside `in` (0 / 0
+ * when absent, :169). A frame without the streaming flag is KX_ERR_INVALID_DATA (:143-145); a frame whose
+ * magic is not TTHeader's, or whose header blocks are malformed, KX_ERR_UNKNOWN_PROTOCOL; a frame cut short
+ * KX_ERR_EOF. Outputs other than frame_offsets are optional. Status as kx_frame_scan.
+ * The int-info key of the frame type, its five values and the streaming flag live in the un-vendored
+ * gopkg (ttheader.FrameType, FrameType*, HeaderFlagsStreaming): kx_ttstream_default_keys fills the values
+ * this library assumes (parity unpinned); a caller with other constants passes its own.
+ * ToMethod is transmeta.ToMethod (pkg/remote/transmeta/metakey.go:33, key 9). */
+typedef struct kx_ttstream_keys {
+  uint16_t frame_type_key;    /* IntInfo key of the frame type (ttheader.FrameType) */
+  uint16_t to_method_key;     /* IntInfo key of the method (ttheader.ToMethod) */
+  uint16_t streaming_flag;    /* ttheader.HeaderFlagsStreaming */
+  uint16_t reserved;
+  char type_names[5][8];      /* values for META, HEADER, DATA, TRAILER, RST (NUL-padded, <= 8 bytes) */
+} kx_ttstream_keys;
+enum { KX_TTS_META = 1, KX_TTS_HEADER = 2, KX_TTS_DATA = 3, KX_TTS_TRAILER = 4, KX_TTS_RST = 5 };
+void kx_ttstream_default_keys(kx_ttstream_keys* keys);
+int kx_ttstream_frame_scan(kx_ctx* c, const uint8_t* in, uint64_t in_len, uint64_t n, const kx_ttstream_keys* keys,
+                           uint64_t* frame_offsets, uint64_t* payload_start, uint64_t* payload_end,
+                           uint8_t* frame_types, int32_t* stream_ids, uint64_t* method_pos, uint32_t* method_len,
+                           kx_status* status, void* stream);
+
+/* ---- records at explicit extents (gopkgthrift.FastUnmarshal of each payload, ttstream DecodePayload
+ *      frame.go:223-233; proto.Unmarshal for ProtobufStruct) ----
+ * Record i = in[starts[i] .. ends[i]) (device u64 arrays, n entries each; extents may leave gaps, e.g. the
+ * DATA-frame payloads kx_ttstream_frame_scan located). Semantics, record_status and status as the
+ * known-offsets decode (offset = the failing record's start). */
+int kx_thrift_decode_extents(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len,
+                             const uint64_t* starts, const uint64_t* ends, uint64_t n, const kx_columns* out,
+                             uint8_t* record_status, kx_status* status, void* stream);
+int kx_pb_decode_extents(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len,
+                         const uint64_t* starts, const uint64_t* ends, uint64_t n, const kx_columns* out,
+                         uint8_t* record_status, kx_status* status, void* stream);
+
 /* Kitex-Protobuf meta header (host memory; protobuf.go:77-90 / 136-165). */
 uint64_t kx_pb_meta_length(uint32_t name_len);
 int kx_pb_write_meta(uint8_t* buf, uint64_t cap, const char* name, uint32_t name_len, int32_t msg_type,

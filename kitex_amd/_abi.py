@@ -103,6 +103,15 @@ class Status(C.Structure):
     ]
 
 
+class TTStreamKeys(C.Structure):
+    """kx_ttstream_keys: the gopkg ttheader streaming constants the frame scan uses (include/kxcodec.h)"""
+    _fields_ = [("frame_type_key", C.c_uint16), ("to_method_key", C.c_uint16), ("streaming_flag", C.c_uint16),
+                ("reserved", C.c_uint16), ("type_names", (C.c_char * 8) * 5)]
+
+
+TTS_META, TTS_HEADER, TTS_DATA, TTS_TRAILER, TTS_RST = 1, 2, 3, 4, 5
+
+assert C.sizeof(TTStreamKeys) == 48
 assert C.sizeof(FieldDesc) == 16
 assert C.sizeof(Status) == 128
 assert C.sizeof(Column) == 48

@@ -99,6 +99,12 @@ def lib():
     L.kx_crc32c_batch.argtypes = [vp, vp, u64, vp, u64, vp, vp, vp]
     L.kx_frame_crc32c_validate.argtypes = [vp, vp, u64, vp, u64, vp, vp, vp, vp]
     L.kx_ctx_set_crc32c_check.argtypes = [vp, C.c_int]
+    L.kx_ttstream_default_keys.argtypes = [C.POINTER(A.TTStreamKeys)]
+    L.kx_ttstream_default_keys.restype = None
+    L.kx_ttstream_frame_scan.argtypes = [vp, vp, u64, u64, C.POINTER(A.TTStreamKeys), vp, vp, vp, vp, vp, vp, vp,
+                                         vp, vp]
+    L.kx_thrift_decode_extents.argtypes = [vp, vp, vp, u64, vp, vp, u64, C.POINTER(A.Columns), vp, vp, vp]
+    L.kx_pb_decode_extents.argtypes = L.kx_thrift_decode_extents.argtypes
     L.kx_grpc_frame_scan.argtypes = L.kx_frame_scan.argtypes
     L.kx_thrift_raw_messages.argtypes = [vp, vp, u64, vp, u64, C.POINTER(A.Column), vp, vp, vp]
     L.kx_thrift_set_seqids.argtypes = [vp, vp, u64, vp, u64, vp, vp, vp, vp]

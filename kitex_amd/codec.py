@@ -176,6 +176,55 @@ class MessageBatch(DecodeResult):
         return bytes(self.names[1][a:b].cpu().numpy()).decode()
 
 
+@dataclass
+class StreamBatch(DecodeResult):
+    """UnmarshalStream: the frames of a ttstream connection buffer and the records of its DATA frames."""
+    frame_offsets: "object" = None   # int64[n + 1]
+    frame_types: "object" = None     # uint8[n], A.TTS_*
+    stream_ids: "object" = None      # int32[n]
+    method_pos: "object" = None      # int64[n] (IntInfo[ToMethod] inside buf)
+    method_len: "object" = None      # int32[n]
+    payload_start: "object" = None   # int64[n]
+    payload_end: "object" = None     # int64[n]
+    data_frames: "object" = None     # int64[records]: the DATA frame each record came from
+    scan_status: "object" = None     # A.Status of the frame scan
+    buf: "object" = None
+
+    def method(self, i: int) -> str:
+        p, l = int(self.method_pos[i].item()), int(self.method_len[i].item())
+        return bytes(self.buf[p:p + l].cpu().numpy()).decode()
+
+
+def default_ttstream_keys() -> A.TTStreamKeys:
+    """kx_ttstream_default_keys: the gopkg ttheader streaming constants this library assumes"""
+    k = A.TTStreamKeys()
+    lib().kx_ttstream_default_keys(C.byref(k))
+    return k
+
+
+def ttstream_frame_scan(buf, n: int, keys: Optional[A.TTStreamKeys] = None, device: int = 0, stream=None):
+    """kx_ttstream_frame_scan over a device buffer of n ttstream frames. Returns (frame offsets int64[n+1],
+    payload starts int64[n], payload ends int64[n], frame types uint8[n], stream ids int32[n], method
+    positions int64[n], method lengths int32[n], status tensor)."""
+    import torch
+    dev = torch.device("cuda", device)
+    s = _stream(stream)
+    ctx = _ctx_for(device, s)
+    keys = keys if keys is not None else default_ttstream_keys()
+    fo = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    ps = torch.zeros(max(1, n), dtype=torch.int64, device=dev)
+    pe = torch.zeros(max(1, n), dtype=torch.int64, device=dev)
+    ft = torch.zeros(max(1, n), dtype=torch.uint8, device=dev)
+    sid = torch.zeros(max(1, n), dtype=torch.int32, device=dev)
+    mp = torch.zeros(max(1, n), dtype=torch.int64, device=dev)
+    ml = torch.zeros(max(1, n), dtype=torch.int32, device=dev)
+    st = status_tensor(dev)
+    check(lib().kx_ttstream_frame_scan(ctx.handle, _ptr(buf), buf.numel(), n, C.byref(keys), _ptr(fo), _ptr(ps),
+                                       _ptr(pe), _ptr(ft), _ptr(sid), _ptr(mp), _ptr(ml), _ptr(st),
+                                       int(s.cuda_stream)), "kx_ttstream_frame_scan")
+    return fo, ps[:n], pe[:n], ft[:n], sid[:n], mp[:n], ml[:n], st
+
+
 def status_tensor(device):
     import torch
     return torch.zeros(16, dtype=torch.int64, device=device)
@@ -346,6 +395,55 @@ class ThriftCodec:
                 raise ProtocolError(stt.code, self._WHAT, stt.record, stt.offset)
         return res
 
+    _EXTENTS = "kx_thrift_decode_extents"
+
+    def UnmarshalExtents(self, buf, starts, ends, out: ColumnSet = None, var_caps: Sequence[int] = None,
+                         stream=None, raise_on_error: bool = True) -> DecodeResult:
+        """FastUnmarshal of n bare bodies at explicit extents buf[starts[i]:ends[i]) (int64 device tensors;
+        ttstream DecodePayload, frame.go:223-233). record_status per body."""
+        import torch
+        ds = self.dschema
+        n = int(starts.numel())
+        if out is None:
+            if var_caps is None:
+                var_caps = [0 if ci.kind == A.COL_FIXED else max(1, buf.numel()) for ci in ds.infos]
+            out = alloc_device(ds.infos, n, var_caps, ds.npresence, self.device)
+        kc = to_kx_columns(out, ds.infos, var_caps)
+        st = status_tensor(self.device)
+        rs = torch.empty(max(1, n), dtype=torch.uint8, device=self.device)
+        s = _stream(stream)
+        starts = starts.to(torch.int64).contiguous()
+        ends = ends.to(torch.int64).contiguous()
+        rc = getattr(lib(), self._EXTENTS)(self._ctx(s).handle, ds.handle, _ptr(buf), buf.numel(), _ptr(starts),
+                                           _ptr(ends), n, C.byref(kc), _ptr(rs), _ptr(st), int(s.cuda_stream))
+        check(rc, self._EXTENTS)
+        res = DecodeResult(out, st, rs, s)
+        if raise_on_error:
+            stt = res.read_status()
+            if stt.code:
+                raise ProtocolError(stt.code, self._WHAT, stt.record, stt.offset)
+        return res
+
+    def UnmarshalStream(self, buf, n_frames: int, keys: Optional[A.TTStreamKeys] = None, stream=None,
+                        raise_on_error: bool = True) -> "StreamBatch":
+        """ttstream's receive side over a connection buffer of n TTHeader streaming frames (DecodeFrame,
+        pkg/remote/trans/ttstream/frame.go:137-185): every frame located and classified on the device
+        (kx_ttstream_frame_scan), then the DATA frames' payloads decoded as records (DecodePayload ->
+        FastUnmarshal, :223-233; kx_*_decode_extents). Records are in DATA-frame order; data_frames[j]
+        is the frame record j came from."""
+        import torch
+        s = _stream(stream)
+        fo, ps, pe, ft, sid, mp, ml, st = ttstream_frame_scan(buf, n_frames, keys, self.device.index or 0, s)
+        stt = read_status(st, s)
+        if stt.code and raise_on_error:
+            raise ProtocolError(stt.code, "ttstream DecodeFrame", stt.record, stt.offset)
+        nf = stt.n_records if stt.code else n_frames
+        data = torch.nonzero(ft[:nf] == A.TTS_DATA).flatten()
+        res = self.UnmarshalExtents(buf, ps[data], pe[data], stream=s, raise_on_error=raise_on_error)
+        return StreamBatch(res.columns, res.status, res.record_status, s, frame_offsets=fo, frame_types=ft,
+                           stream_ids=sid, method_pos=mp, method_len=ml, payload_start=ps, payload_end=pe,
+                           data_frames=data, scan_status=stt, buf=buf)
+
     def _messages(self, fn, args, buf, n, out, var_caps, name_cap, s, raise_on_error):
         import torch
         ds = self.dschema
@@ -485,6 +583,7 @@ class ProtobufCodec(ThriftCodec):
     _FRAMES = "kx_pb_decode_frames"
     _GRPC = "kx_pb_decode_grpc"
     _PATH_FN = staticmethod(lambda codec_type, data_len: "protobuf")
+    _EXTENTS = "kx_pb_decode_extents"
     _ENCODE = "kx_pb_encode_batch"
     _SIZE = "kx_pb_encoded_size_batch"
     _WHAT = "protobuf unmarshal"

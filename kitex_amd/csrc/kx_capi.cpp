@@ -64,6 +64,9 @@ static int ensure_pipe(kx_ctx* c) {
   const char* a = getenv("KX_CHUNK_AHEAD");
   p.ahead = a ? atoi(a) : 1;
   p.chunk_tiles = (mb * 128 + 63) & ~63ull;  // 128 tiles of 8 KiB per MiB, whole groups of 64 tiles
+  const char* cb = getenv("KX_COMBO_MB");
+  const uint64_t cmb = cb ? strtoull(cb, nullptr, 10) : KX_COMBO_MB_DEFAULT;
+  p.combo_tiles = (cmb * 128 + 63) & ~63ull;
   KX_HIP_CHECK(hipEventCreateWithFlags(&p.fork, hipEventDisableTiming));
   for (int k = 0; k < KX_PIPE_EV; k++) {
     KX_HIP_CHECK(hipEventCreateWithFlags(&p.ev_idx[k], hipEventDisableTiming));
@@ -645,6 +648,75 @@ int kx_pb_decode_grpc(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t
                       uint64_t max_payload, uint64_t* frame_offsets, const kx_columns* out, uint8_t* record_status,
                       kx_status* status, void* stream) {
   return decode_grpc(c, s, in, in_len, n, true, max_payload, frame_offsets, out, record_status, status, stream);
+}
+
+// the values this library assumes for the un-vendored gopkg ttheader streaming constants (parity
+// unpinned: DESIGN.md §3.6); ToMethod is transmeta.ToMethod (pkg/remote/transmeta/metakey.go:33)
+void kx_ttstream_default_keys(kx_ttstream_keys* k) {
+  if (!k) return;
+  memset(k, 0, sizeof *k);
+  k->frame_type_key = 27;   // ttheader.FrameType
+  k->to_method_key = 9;     // ttheader.ToMethod = transmeta.ToMethod
+  k->streaming_flag = 0x2;  // ttheader.HeaderFlagsStreaming
+  const char* names[5] = {"1", "2", "3", "4", "5"};  // ttheader.FrameTypeMeta .. FrameTypeRst
+  for (int i = 0; i < 5; i++) strncpy(k->type_names[i], names[i], 8);
+}
+
+int kx_ttstream_frame_scan(kx_ctx* c, const uint8_t* in, uint64_t in_len, uint64_t n, const kx_ttstream_keys* keys,
+                           uint64_t* frame_offsets, uint64_t* payload_start, uint64_t* payload_end,
+                           uint8_t* frame_types, int32_t* stream_ids, uint64_t* method_pos, uint32_t* method_len,
+                           kx_status* status, void* stream) {
+  if (!c || !status || !keys || !frame_offsets || (n && (!payload_start || !payload_end)) || (!in && in_len))
+    return KX_ERR_INVALID_ARG;
+  int rc = set_device(c);
+  if (rc) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  if (n == 0) {
+    KX_HIP_CHECK(hipMemsetAsync(status, 0, sizeof(kx_status), st));
+    KX_HIP_CHECK(hipMemsetAsync(frame_offsets, 0, 8, st));
+    return KX_OK;
+  }
+  uint64_t epoch = 0;
+  if ((rc = ensure_ws(c, kx_skip_ws_bytes(in_len), st, &epoch))) return rc;
+  return kx_launch_frames(in, in_len, n, 0, frame_offsets, payload_start, payload_end, frame_types, status, c->ws,
+                          c->ws_size, epoch, st, false, keys, stream_ids, method_pos, method_len);
+}
+
+static int decode_extents(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len, const uint64_t* starts,
+                          const uint64_t* ends, uint64_t n, bool pb, const kx_columns* out, uint8_t* record_status,
+                          kx_status* status, void* stream) {
+  if (!c || !s || !status || (!in && in_len) || (n && (!starts || !ends))) return KX_ERR_INVALID_ARG;
+  int rc = set_device(c);
+  if (rc) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  KxLaunchCols lc;
+  if ((rc = to_launch_cols(s, out, &lc, true, in_len))) return rc;
+  if (n == 0) {
+    KX_HIP_CHECK(hipMemsetAsync(status, 0, sizeof(kx_status), st));
+    for (uint32_t k = 0; k < s->ncols; k++)
+      if (lc.offs[k] && !((lc.view >> k) & 1))
+        KX_HIP_CHECK(hipMemsetAsync(lc.offs[k], 0, ((lc.owide >> k) & 1) ? 8 : 4, st));
+    return KX_OK;
+  }
+  KxProgram* dp = nullptr;
+  if ((rc = prog_on_device(const_cast<kx_schema*>(s), c->device, &dp))) return rc;
+  size_t ws = kx_decode_ws_bytes(s->prog, in_len, starts, n);
+  uint64_t epoch = 0;
+  if ((rc = ensure_ws(c, ws, st, &epoch))) return rc;
+  return kx_launch_decode(dp, s->prog, in, in_len, starts, n, lc, record_status, status, c->ws, c->ws_size, epoch, st,
+                          pb, ends, nullptr, nullptr);
+}
+
+int kx_thrift_decode_extents(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len,
+                             const uint64_t* starts, const uint64_t* ends, uint64_t n, const kx_columns* out,
+                             uint8_t* record_status, kx_status* status, void* stream) {
+  return decode_extents(c, s, in, in_len, starts, ends, n, false, out, record_status, status, stream);
+}
+
+int kx_pb_decode_extents(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len,
+                         const uint64_t* starts, const uint64_t* ends, uint64_t n, const kx_columns* out,
+                         uint8_t* record_status, kx_status* status, void* stream) {
+  return decode_extents(c, s, in, in_len, starts, ends, n, true, out, record_status, status, stream);
 }
 
 int kx_thrift_raw_messages(kx_ctx* c, const uint8_t* in, uint64_t in_len, const uint64_t* offsets, uint64_t n,

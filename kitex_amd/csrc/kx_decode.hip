@@ -85,7 +85,14 @@ struct DecParams {
   uint64_t* fr_pe;
   uint8_t* fr_kind;
   uint64_t fr_max;           // M_FRAME: payload size limit (0: none)
-  int fr_grpc;               // M_FRAME: gRPC length-prefixed messages instead of the default-codec sniff
+  int fr_grpc;               // M_FRAME: 0 default-codec sniff, 1 gRPC length-prefixed messages, 2 ttstream
+  int32_t* fr_sid;           // ttstream: stream id (TTHeader seqid), method position / length per frame
+  uint64_t* fr_mpos;
+  uint32_t* fr_mlen;
+  uint32_t tts_keys;         // ttstream: frame-type key | ToMethod key << 16
+  uint32_t tts_flag;         // ttstream: HeaderFlagsStreaming
+  uint64_t tts_name[5];      // ttstream: frame-type values (little-endian packed, NUL-padded)
+  uint32_t tts_nlen[5];
   uint64_t* tdesc;           // tile words
   uint64_t* gdesc;           // group words
   uint16_t* starts;          // concatenated mode: record starts per tile (slotcap slots each)
@@ -104,6 +111,7 @@ struct DecParams {
   uint32_t winb;             // window bytes loaded per tile: TILE + halo + 16 (<= WINB)
   uint32_t nlist;            // numeric list columns (thrift): emit copies them wave-cooperatively
   int direct;                // offsets mode without var columns: emit pass only
+  int fast;                  // concatenated Thrift with a canonical plan: fast_tile before walk_tile
   int nolds;                 // diagnostics (KX_NOLDS=1): read every byte from global memory
   int diag;                  // diagnostics (KX_DIAG bits, timing experiments only; output is wrong):
                              // 1 no walk, 2 no group arrival, 4 no tile words, 256 index pass only
@@ -113,6 +121,7 @@ struct DecParams {
 // parameter (cols.data[c]) would otherwise make the compiler copy the whole block to scratch per lane.
 typedef const KAS DecParams KParams;
 #define KX_PARAMS() (*(KParams*)__builtin_amdgcn_kernarg_segment_ptr())
+#define KX_CPARAMS() (*(const KAS ComboParams*)__builtin_amdgcn_kernarg_segment_ptr())
 
 // known-offsets mode: where record r ends (message bodies: an explicit end per record)
 __device__ __forceinline__ uint64_t rec_end(KParams& dp, uint64_t r) {
@@ -1543,6 +1552,78 @@ __device__ __forceinline__ int frame_grpc(const Src& w, uint64_t pos, uint64_t l
   return KX_OK;
 }
 
+// ttstream DecodeFrame (pkg/remote/trans/ttstream/frame.go:137-185): a TTHeader whose payload is a bare
+// struct. kind = the frame type (KX_TTS_*, from IntInfo[frame type key]); *sid the TTHeader seqid, *mp /
+// *ml IntInfo[ToMethod] (input position, 0 / 0 when absent); the last occurrence of a key wins. Same
+// restatement as oracle kxo_ttstream_frame_one.
+__device__ __forceinline__ int frame_tts(KParams& dp, const Src& w, uint64_t pos, uint64_t lim, uint64_t* end,
+                                         uint64_t& ps, uint64_t& pe, uint32_t& kind, int32_t& sid, uint64_t& mp,
+                                         uint32_t& ml) {
+  if (pos > lim || lim - pos < 8) return KX_ERR_EOF;
+  const uint64_t len = lim - pos;
+  const uint32_t a = be32(w, pos), c = be32(w, pos + 4);
+  if ((c & 0xffff0000u) != 0x10000000u) return KX_ERR_UNKNOWN_PROTOCOL;
+  if (len < 14) return KX_ERR_EOF;
+  const uint64_t hs = (uint64_t)be16s(w, pos + 12) * 4;
+  if (hs > 65536 || hs < 2) return KX_ERR_UNKNOWN_PROTOCOL;
+  if (14 + hs > len) return KX_ERR_EOF;
+  const uint64_t b = pos + 14;
+  const uint32_t proto = ld1(w, b);
+  if (proto != 0 && proto != 3 && proto != 4 && proto != 0x10 && proto != 0x11) return KX_ERR_UNKNOWN_PROTOCOL;
+  const uint64_t nt = ld1(w, b + 1);
+  if (hs - 2 < nt) return KX_ERR_UNKNOWN_PROTOCOL;
+  uint64_t i = 2 + nt, ftp = 0, ftl = ~0ull;
+  mp = 0;
+  ml = 0;
+  const uint32_t ftk = dp.tts_keys & 0xffffu, tmk = dp.tts_keys >> 16;
+  while (i < hs) {
+    const uint32_t id = ld1(w, b + i++);
+    if (id == 0x00) continue;
+    if (id == 0x01) {
+      const int rc = fr_kv_strings(w, b, hs, i);
+      if (rc) return rc;
+    } else if (id == 0x10) {
+      if (i + 2 > hs) return KX_ERR_UNKNOWN_PROTOCOL;
+      const uint32_t k = be16s(w, b + i);
+      i += 2;
+      for (uint32_t j = 0; j < k; j++) {
+        if (i + 4 > hs) return KX_ERR_UNKNOWN_PROTOCOL;
+        const uint32_t key = be16s(w, b + i);
+        const uint64_t l = be16s(w, b + i + 2);
+        if (i + 4 + l > hs) return KX_ERR_UNKNOWN_PROTOCOL;
+        if (key == ftk) { ftp = b + i + 4; ftl = l; }
+        if (key == tmk) { mp = b + i + 4; ml = (uint32_t)l; }
+        i += 4 + l;
+      }
+    } else if (id == 0x11) {
+      if (i + 2 > hs) return KX_ERR_UNKNOWN_PROTOCOL;
+      const uint64_t l = be16s(w, b + i);
+      if (i + 2 + l > hs) return KX_ERR_UNKNOWN_PROTOCOL;
+      i += 2 + l;
+    } else {
+      return KX_ERR_UNKNOWN_PROTOCOL;
+    }
+  }
+  const uint64_t fend = 4 + (uint64_t)a;
+  if (fend < 14 + hs) return KX_ERR_UNKNOWN_PROTOCOL;
+  if (!(c & 0xffffu & dp.tts_flag)) return KX_ERR_INVALID_DATA;  // unexpected header flags
+  kind = 0;
+  if (ftl <= 8) {
+    uint64_t v = 0;
+    for (uint64_t j = 0; j < ftl; j++) v |= (uint64_t)ld1(w, ftp + j) << (8 * j);
+    for (int k = 0; k < 5; k++)
+      if (!kind && dp.tts_nlen[k] == ftl && dp.tts_name[k] == v) kind = (uint32_t)(k + 1);
+  }
+  if (!kind) return KX_ERR_INVALID_DATA;  // unexpected frame type
+  if (fend > len) return KX_ERR_EOF;
+  sid = (int32_t)be32(w, pos + 8);
+  ps = pos + 14 + hs;
+  pe = pos + fend;
+  *end = pos + fend;
+  if (!ml) mp = 0;
+  return KX_OK;
+}
+
 // One record: FastRead (emit) or its length / var extents only (measure).
 template <int NV, int MODE>
 __device__ __forceinline__ int parse_record(KParams& dp, const Src& w, uint64_t pos, uint64_t lim, uint64_t r,
@@ -1580,14 +1661,19 @@ __device__ __forceinline__ int parse_record(KParams& dp, const Src& w, uint64_t 
     return pb_body<NV>(w, dp.prog, dp.cols, b, e, r, emit, vs, pres, utf8);
   }
   if (MODE == M_FRAME) {
-    uint64_t ps, pe;
-    uint32_t kind;
-    const int rc = dp.fr_grpc ? frame_grpc(w, pos, lim, dp.fr_max, end, ps, pe, kind)
-                              : frame_one(w, pos, lim, dp.fr_max, end, ps, pe, kind);
+    uint64_t ps, pe, mp = 0;
+    uint32_t kind, ml = 0;
+    int32_t sid = 0;
+    const int rc = dp.fr_grpc == 2 ? frame_tts(dp, w, pos, lim, end, ps, pe, kind, sid, mp, ml)
+                   : dp.fr_grpc ? frame_grpc(w, pos, lim, dp.fr_max, end, ps, pe, kind)
+                                : frame_one(w, pos, lim, dp.fr_max, end, ps, pe, kind);
     if (emit && !rc) {
       dp.fr_ps[r] = ps;
       dp.fr_pe[r] = pe;
       if (dp.fr_kind) dp.fr_kind[r] = (uint8_t)kind;
+      if (dp.fr_sid) dp.fr_sid[r] = sid;
+      if (dp.fr_mpos) dp.fr_mpos[r] = mp;
+      if (dp.fr_mlen) dp.fr_mlen[r] = ml;
     }
     return rc;
   }
@@ -1628,7 +1714,7 @@ struct Cand {
 // one connection are homogeneous; frames of another class are still reached by the chain walk)
 __device__ __forceinline__ uint64_t frame_scan_segment(KParams& dp, const Src& w, uint64_t lo, uint64_t hi) {
   const GLB uint8_t* g = (const GLB uint8_t*)dp.in;
-  if (dp.fr_grpc) {
+  if (dp.fr_grpc == 1) {
     // gRPC: the first message's flag byte, the top byte of its length, and the first (up to) 3 bytes of
     // its payload (records of one stream start alike: the Thrift field header / proto tag)
     if (dp.in_len < 5) return lo < hi && lo == 0 ? 0 : X_NONE;
@@ -1918,6 +2004,200 @@ __device__ __forceinline__ Agg measure_records(KParams& dp, const Src& w, uint64
   return g;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Fast index path (concatenated Thrift, batches whose records start with the schema's canonical
+// signature): the same tile aggregate and record starts as walk_tile, for tiles whose records are all
+// canonical and whose speculation is right the first time, at a fraction of the instructions:
+//  * segments on the window's dword grid (segment s = window dwords D0 + 32 s .. + 31, the last one
+//    runs to the tile end); the signature scan is interleaved (iteration k: lane l tests dword
+//    D0 + 64 k + l) and a ballot per iteration hands segment 2k / 2k + 1 its dword-hit mask
+//    (writelane), so every LDS read is conflict-free and no lane loops over its own bytes;
+//  * a lane walks from its first hit (its second one when the first does not parse canonically: a
+//    nested struct with the same first header) with `fast_record`: the canonical plan's headers and
+//    lengths only, one window bounds check per step;
+//  * one consistency check (every lane's entry = the exit of the walking lane below it). Anything
+//    else (a non-canonical record, a false signature hit, a record leaving the window, > 4 records in
+//    a segment) returns false and the tile takes walk_tile from scratch.
+// ---------------------------------------------------------------------------------------------
+// v_writelane_b32: lane L of `old` takes the wave-uniform value v
+template <int L>
+__device__ __forceinline__ uint32_t writelane(uint32_t old, uint32_t v) {
+  asm("v_writelane_b32 %0, %1, %2" : "+v"(old) : "s"(v), "i"(L));
+  return old;
+}
+
+// iteration K of the interleaved signature scan: lane l tests window dword D0 + 64 K + l; the ballot's
+// halves are the dword-hit masks of segments 2K and 2K + 1, written into those lanes
+template <int K>
+__device__ __forceinline__ void fast_scan(const Src& w, uint32_t D0, uint32_t b0, uint32_t b1, uint32_t b2, int lane,
+                                          uint32_t& hm) {
+  const uint32_t d = D0 + 64u * K + (uint32_t)lane;
+  const uint32_t x0 = w.win[d], x1 = w.win[d + 1];
+  const uint32_t e = (x0 ^ b0) | (__builtin_amdgcn_alignbyte(x1, x0, 1) ^ b1) |
+                     (__builtin_amdgcn_alignbyte(x1, x0, 2) ^ b2);
+  const uint64_t bal = __ballot(low_zero_byte(e) != 0);
+  hm = writelane<2 * K>(hm, (uint32_t)bal);
+  hm = writelane<2 * K + 1>(hm, (uint32_t)(bal >> 32));
+  if constexpr (K + 1 < 32) fast_scan<K + 1>(w, D0, b0, b1, b2, lane, hm);
+}
+
+__device__ __forceinline__ uint32_t win_ld(const Src& w, uint32_t q) {  // 4 bytes at window offset q
+  return __builtin_amdgcn_alignbyte(w.win[(q >> 2) + 1], w.win[q >> 2], q & 3);
+}
+
+// one canonical record at window offset q (measure: headers, lengths, STOP); var lengths added to vl
+template <int NV>
+__device__ __forceinline__ bool fast_record(const Src& w, uint32_t& q, uint64_t* vl) {
+  const KAS KxpStep* __restrict__ steps = w.steps;
+  const uint32_t wl = (uint32_t)w.wlen;
+  bool ok = true;
+  uint32_t k = 0;
+  while (k < w.nsteps) {
+    k = __builtin_amdgcn_readfirstlane(k);
+    const KxpStep st = ldk(&steps[k]);
+    ok &= q + 64 <= wl;             // a step reads < 64 bytes from q
+    const uint32_t qq = ok ? q : 0u;
+    if (st.kind == KXP_S_FIXED) {
+      const uint32_t m = min(st.hdr >> 24, 4u);
+      const KxpStep s1 = ldk(&steps[k + (m > 1 ? 1 : 0)]);
+      const KxpStep s2 = ldk(&steps[k + (m > 2 ? 2 : 0)]);
+      const KxpStep s3 = ldk(&steps[k + (m > 3 ? 3 : 0)]);
+      const uint32_t o1 = 3 + st.width, o2 = o1 + 3 + s1.width, o3 = o2 + 3 + s2.width;
+      const uint32_t len = m == 1 ? o1 : m == 2 ? o2 : m == 3 ? o3 : o3 + 3 + s3.width;
+      ok &= ((win_ld(w, qq) ^ st.hdr) & 0xffffffu) == 0;
+      if (m > 1) ok &= ((win_ld(w, qq + o1) ^ s1.hdr) & 0xffffffu) == 0;
+      if (m > 2) ok &= ((win_ld(w, qq + o2) ^ s2.hdr) & 0xffffffu) == 0;
+      if (m > 3) ok &= ((win_ld(w, qq + o3) ^ s3.hdr) & 0xffffffu) == 0;
+      q += len;
+      k += m;
+      continue;
+    }
+    k++;
+    const uint32_t h = win_ld(w, qq);
+    if (st.kind == KXP_S_END) {
+      ok &= (h & 0xffu) == KX_T_STOP;
+      q += 1;
+      continue;
+    }
+    ok &= ((h ^ st.hdr) & 0xffffffu) == 0;
+    if (st.kind == KXP_S_STRUCT) {
+      q += 3;
+      continue;
+    }
+    const bool list = st.kind == KXP_S_LIST;
+    const uint32_t l = __builtin_bswap32(win_ld(w, qq + (list ? 4u : 3u)));
+    const uint64_t b = (uint64_t)l * (list ? st.width : 1u);
+    ok &= l <= wl && b <= wl;       // also rejects a negative length (the generic path reports it)
+#pragma unroll
+    for (int v = 0; v < NV; v++)
+      if ((uint32_t)v == st.vslot) vl[v] += ok ? l : 0u;
+    q += (list ? 8u : 7u) + (ok ? (uint32_t)b : 0u);
+  }
+  return ok;
+}
+
+template <int NV>
+__device__ __forceinline__ bool fast_tile(KParams& dp, const Src& w, uint64_t tlo, uint64_t thi, uint64_t seed,
+                                          int lane, uint16_t* starts, Agg& a) {
+  const KAS KxProgram* P = dp.prog;
+  const uint32_t sig = P->sig;
+  const uint32_t b0 = (sig & 0xff) * 0x01010101u, b1 = ((sig >> 8) & 0xff) * 0x01010101u;
+  const uint32_t b2 = ((sig >> 16) & 0xff) * 0x01010101u;
+  const uint32_t q0 = (uint32_t)(tlo - w.wpos);   // < 16
+  const uint32_t D0 = q0 >> 2;
+  // ---- interleaved scan: hm = the dword-hit mask of this lane's segment ----
+  uint32_t hm = 0;
+  fast_scan<0>(w, D0, b0, b1, b2, lane, hm);
+  const uint32_t sq = 4 * D0 + 128u * (uint32_t)lane;   // window offset of the segment's first dword
+  const uint64_t seg_lo = lane == 0 ? tlo : w.wpos + sq;
+  const uint64_t seg_hi = lane == 63 ? thi : kmin64(w.wpos + sq + 128, thi);
+  const uint64_t plim = kmin64(seg_hi, dp.in_len >= 3 ? dp.in_len - 2 : 0ull);
+  // ---- the first two hits in [seg_lo, plim) (lane 63 also tests dword 32: the up to 3 bytes of the
+  //      tile past the dword grid) ----
+  uint64_t c1 = X_NONE, c2 = X_NONE;
+  {
+    uint64_t hb = (uint64_t)hm | (lane == 63 ? (1ull << 32) : 0ull);   // lane 63 also looks at dword 32
+    while (hb && c2 == X_NONE) {
+      const int di = __ffsll((long long)hb) - 1;
+      hb &= hb - 1;
+      const uint32_t dq = sq + 4u * (uint32_t)di;
+      const uint32_t x0 = w.win[dq >> 2], x1 = w.win[(dq >> 2) + 1];
+      uint32_t m = zero_bytes((x0 ^ b0) | (__builtin_amdgcn_alignbyte(x1, x0, 1) ^ b1) |
+                              (__builtin_amdgcn_alignbyte(x1, x0, 2) ^ b2));
+      while (m) {
+        const uint64_t p = w.wpos + dq + first_hit(m);
+        m &= m - 1;
+        if (p < seg_lo || p >= plim) continue;
+        if (c1 == X_NONE) c1 = p;
+        else { c2 = p; break; }
+      }
+    }
+  }
+  // ---- walk: records of the segment from c1 (c2 when c1's record is not canonical) ----
+  uint64_t ent = c1, ex = X_NONE, cnt = 0, st0 = 0, st1 = 0, st2 = 0, st3 = 0;
+  uint64_t vsum[NV > 0 ? NV : 1];
+#pragma unroll
+  for (int v = 0; v < (NV > 0 ? NV : 1); v++) vsum[v] = 0;
+  bool bad = false;
+  for (int attempt = 0; attempt < 2; attempt++) {
+    bool again = false;
+    if (ent != X_NONE) {
+      uint32_t q = (uint32_t)(ent - w.wpos);
+      uint64_t acc[NV > 0 ? NV : 1];
+#pragma unroll
+      for (int v = 0; v < (NV > 0 ? NV : 1); v++) acc[v] = 0;
+      uint64_t c = 0;
+      bool ok = true;
+      while (ok && w.wpos + q < seg_hi) {
+        const uint64_t start = w.wpos + q;
+        ok = fast_record<NV>(w, q, acc);
+        if (!ok) break;
+        st0 = c == 0 ? start : st0; st1 = c == 1 ? start : st1;
+        st2 = c == 2 ? start : st2; st3 = c == 3 ? start : st3;
+        c++;
+      }
+      if (!ok && c == 0) {
+        // the hit does not start a canonical record (a nested struct's header, a false hit): try the
+        // segment's next hit, else the lane has no candidate (the consistency check below then catches
+        // a record start that is there but not canonical)
+        ent = attempt == 0 ? c2 : X_NONE;
+        again = ent != X_NONE;
+      } else {
+        bad = !ok || c > 4;
+        ex = w.wpos + q;
+        cnt = c;
+#pragma unroll
+        for (int v = 0; v < NV; v++) vsum[v] = acc[v];
+      }
+    }
+    if (!__ballot(again)) break;
+  }
+  if (__ballot(bad)) return false;
+  // ---- consistency: every walking lane starts where the chain of the walking lane below it exits ----
+  const uint64_t hmk = __ballot(ent != X_NONE);
+  const uint64_t below = hmk & ((1ull << lane) - 1);
+  const int pc = below ? 63 - __clzll((long long)below) : -1;
+  const uint64_t pex = __shfl(ex, pc < 0 ? 0 : pc, 64);
+  const uint64_t E = pc >= 0 ? pex : seed;
+  const bool agree = E == X_NONE || (ent != X_NONE ? E == ent : E >= seg_hi);
+  if (__ballot(!agree)) return false;
+  // ---- tile aggregate and record starts (as walk_tile) ----
+  const uint64_t inc = wave_incl_scan(cnt, lane);
+  const uint64_t cpre = inc - cnt;
+  a.cnt = rl64(inc, 63);
+#pragma unroll
+  for (int v = 0; v < NV; v++) a.var[v] = wave_sum(vsum[v]);
+  a.ent = hmk ? rl64(ent, __ffsll((long long)hmk) - 1) : X_NONE;
+  a.ex = hmk ? rl64(ex, 63 - __clzll((long long)hmk)) : seed;
+  a.errc = 0;
+  a.errp = 0;
+  if (cnt > 0) starts[cpre + 0] = (uint16_t)(st0 - tlo);
+  if (cnt > 1) starts[cpre + 1] = (uint16_t)(st1 - tlo);
+  if (cnt > 2) starts[cpre + 2] = (uint16_t)(st2 - tlo);
+  if (cnt > 3) starts[cpre + 3] = (uint16_t)(st3 - tlo);
+  return true;
+}
+
 // tile geometry
 __device__ __forceinline__ void tile_range(KParams& dp, uint64_t t, uint64_t& lo, uint64_t& hi) {
   if (dp.offsets) {
@@ -1941,7 +2221,15 @@ __device__ Agg tile_agg(KParams& dp, LDS uint32_t* win, uint64_t t, uint64_t see
   const uint64_t t0 = (dp.diag & 64) ? __builtin_amdgcn_s_memtime() : 0;
   const Src w = load_window(dp, win, lo, lane, is_thrift(MODE));
   if ((dp.diag & 64) && lane == 0) atomicAdd(&g_phase[0], (unsigned long long)(__builtin_amdgcn_s_memtime() - t0));
-  return walk_tile<NV, MODE>(dp, w, lo, hi, seed, lane, dp.starts + t * dp.slotcap, data_sig(dp));
+  const uint32_t dsig = data_sig(dp);
+  if constexpr (MODE == M_THRIFT) {
+    if (dp.fast && dsig == dp.prog->sig && w.wlen >= TILE + 64) {
+      Agg a;
+      if (fast_tile<NV>(dp, w, lo, hi, seed, lane, dp.starts + t * dp.slotcap, a)) return a;
+      if (lane == 0) atomicAdd((unsigned long long*)&dp.status->diag[2], 1ull);  // fell back to walk_tile
+    }
+  }
+  return walk_tile<NV, MODE>(dp, w, lo, hi, seed, lane, dp.starts + t * dp.slotcap, dsig);
 }
 
 __device__ __forceinline__ void put_tile(KParams& dp, uint64_t t, const Agg& a, int nv) {
@@ -2066,15 +2354,7 @@ __device__ void group_scan(KParams& dp, LDS uint32_t* win, uint64_t g, uint64_t 
 
 // ---- kernel 1: index pass (one wave per tile) ----
 template <int NV, int MODE>
-__global__ void __launch_bounds__(NT, 4) index_kernel(DecParams dp_) {  // 4 waves per SIMD: <= 128 VGPRs
-  KParams& dp = KX_PARAMS();
-  (void)dp_;
-  __shared__ __attribute__((aligned(16))) uint32_t WIN[WAVES][WINW];
-  const int lane = threadIdx.x & 63;
-  const int wv = threadIdx.x >> 6;
-  const uint64_t t = dp.t_lo + (uint64_t)blockIdx.x * WAVES + wv;
-  if (t >= dp.t_hi) return;
-  LDS uint32_t* win = (LDS uint32_t*)WIN[wv];
+__device__ __forceinline__ void index_tile(KParams& dp, LDS uint32_t* win, uint64_t t, int lane) {
   const uint64_t t_start = (dp.diag & 64) ? __builtin_amdgcn_s_memtime() : 0;
   Agg a;
   if (dp.diag & 1) {
@@ -2088,6 +2368,18 @@ __global__ void __launch_bounds__(NT, 4) index_kernel(DecParams dp_) {  // 4 wav
   }
   if (lane == 0 && !(dp.diag & 4)) put_tile(dp, t, a, NV);
   if ((dp.diag & 64) && lane == 0) atomicAdd(&g_phase[5], (unsigned long long)(__builtin_amdgcn_s_memtime() - t_start));
+}
+
+template <int NV, int MODE>
+__global__ void __launch_bounds__(NT, 4) index_kernel(DecParams dp_) {  // 4 waves per SIMD: <= 128 VGPRs
+  KParams& dp = KX_PARAMS();
+  (void)dp_;
+  __shared__ __attribute__((aligned(16))) uint32_t WIN[WAVES][WINW];
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const uint64_t t = dp.t_lo + (uint64_t)blockIdx.x * WAVES + wv;
+  if (t >= dp.t_hi) return;
+  index_tile<NV, MODE>(dp, (LDS uint32_t*)WIN[wv], t, lane);
 }
 
 // ---- kernel 1 (persistent variant, concatenated mode): each wave walks tiles t, t + W, t + 2W ...
@@ -2395,22 +2687,14 @@ __device__ __forceinline__ void emit_container(const Src& w, const KAS KxProgram
 // ---- kernel 3: emit pass (one wave per tile, lane = record) ----
 // COOP: numeric list columns are copied by the whole wave (its own instantiation, so that schemas
 // without such a column keep the record-by-record kernel's code)
-template <int NV, int MODE, bool COOP = false>
-__global__ void __launch_bounds__(NT, 4) emit_kernel(DecParams dp_) {  // 4 waves per SIMD: <= 128 VGPRs
-  KParams& dp = KX_PARAMS();
-  (void)dp_;
-  __shared__ __attribute__((aligned(16))) uint32_t WIN[WAVES][WINW];
-  const int lane = threadIdx.x & 63;
-  const int wv = threadIdx.x >> 6;
-  const uint64_t t = dp.t_lo + (uint64_t)blockIdx.x * WAVES + wv;
-  if (t >= dp.t_hi) return;
+template <int NV, int MODE, bool COOP>
+__device__ __forceinline__ void emit_tile(KParams& dp, LDS uint32_t* win, uint64_t t, int lane) {
   const KAS KxProgram* P = dp.prog;
   const bool known = dp.offsets != nullptr;
   const uint64_t nstop = known ? dp.n : *(volatile uint64_t*)dp.nstop;
   uint64_t lo, hi;
   tile_range(dp, t, lo, hi);
   // the window DMA is issued first; the tile's bases are read while it is in flight
-  LDS uint32_t* win = (LDS uint32_t*)WIN[wv];
   const uint16_t* starts = dp.starts + t * dp.slotcap;
   const Src w = load_window(dp, win, known ? dp.offsets[lo] : lo, lane, is_thrift(MODE), false);
   uint64_t base = 0, cnt = 0, run[NV > 0 ? NV : 1];
@@ -2556,6 +2840,45 @@ __global__ void __launch_bounds__(NT, 4) emit_kernel(DecParams dp_) {  // 4 wave
   }
 }
 
+template <int NV, int MODE, bool COOP = false>
+__global__ void __launch_bounds__(NT, 4) emit_kernel(DecParams dp_) {  // 4 waves per SIMD: <= 128 VGPRs
+  KParams& dp = KX_PARAMS();
+  (void)dp_;
+  __shared__ __attribute__((aligned(16))) uint32_t WIN[WAVES][WINW];
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const uint64_t t = dp.t_lo + (uint64_t)blockIdx.x * WAVES + wv;
+  if (t >= dp.t_hi) return;
+  emit_tile<NV, MODE, COOP>(dp, (LDS uint32_t*)WIN[wv], t, lane);
+}
+
+// ---- index of chunk k and emit of chunk k - 1 in one launch (KX_COMBO_MB): the first `nib` workgroups
+// index, the rest emit, so the index pass's VALU-bound waves and the emit pass's memory-bound waves share
+// every CU instead of running one after the other ----
+struct ComboParams {
+  DecParams ix, em;
+  uint32_t nib;
+};
+
+template <int NV, int MODE, bool COOP>
+__global__ void __launch_bounds__(NT, 4) combo_kernel(ComboParams cp_) {
+  const KAS ComboParams& C = KX_CPARAMS();
+  (void)cp_;
+  __shared__ __attribute__((aligned(16))) uint32_t WIN[WAVES][WINW];
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  LDS uint32_t* win = (LDS uint32_t*)WIN[wv];
+  if (blockIdx.x < C.nib) {
+    KParams& dp = C.ix;
+    const uint64_t t = dp.t_lo + (uint64_t)blockIdx.x * WAVES + wv;
+    if (t < dp.t_hi) index_tile<NV, MODE>(dp, win, t, lane);
+  } else {
+    KParams& dp = C.em;
+    const uint64_t t = dp.t_lo + (uint64_t)(blockIdx.x - C.nib) * WAVES + wv;
+    if (t < dp.t_hi) emit_tile<NV, MODE, COOP>(dp, win, t, lane);
+  }
+}
+
 // Completes a call and re-arms the workspace for the next one (error key, overflow, nstop).
 __global__ void finalize_kernel(kx_status* st, unsigned long long* errkey, uint32_t* overflow, uint64_t* nstop,
                                 const uint64_t* offsets, uint64_t n) {
@@ -2637,6 +2960,17 @@ void launch_emit(dim3 grid, hipStream_t stream, const DecParams& dp) {
 }
 
 template <int NV, int MODE>
+void launch_combo(unsigned grid, hipStream_t stream, const ComboParams& cp, uint32_t nlist) {
+  if constexpr (is_thrift(MODE) && NV > 0) {
+    if (KX_EMIT_COOP && nlist) {
+      hipLaunchKernelGGL((combo_kernel<NV, MODE, true>), dim3(grid), dim3(NT), 0, stream, cp);
+      return;
+    }
+  }
+  hipLaunchKernelGGL((combo_kernel<NV, MODE, false>), dim3(grid), dim3(NT), 0, stream, cp);
+}
+
+template <int NV, int MODE>
 int launch_t(const DecParams& dp0, const WsLayout& L, void* ws, hipStream_t stream, const KxPipe* pp) {
   DecParams dp = dp0;
   char* base = (char*)ws;
@@ -2658,6 +2992,38 @@ int launch_t(const DecParams& dp0, const WsLayout& L, void* ws, hipStream_t stre
   const unsigned ggrid = (unsigned)((dp.ngroups + WAVES - 1) / WAVES);
   if (dp.diag & 256) {
     hipLaunchKernelGGL((index_kernel<NV, MODE>), dim3(grid), dim3(NT), 0, stream, dp);
+    return KX_OK;
+  }
+  const uint64_t cbt = pp ? pp->combo_tiles : 0;
+  if (!dp.direct && cbt && dp.ntiles >= 2 * cbt && !dp.diag) {
+    // one stream: launch s = index(s) + emit(s - 1), then group(s) + chain(s); the emit of chunk s - 1
+    // reads the bases chain(s - 1) wrote one launch earlier
+    const uint64_t nch = (dp.ntiles + cbt - 1) / cbt;
+    for (uint64_t s = 0; s <= nch; s++) {
+      ComboParams cp{};
+      uint64_t ni = 0, ne = 0;
+      if (s < nch) {
+        cp.ix = chunk_params(dp, s, nch, cbt);
+        ni = (cp.ix.t_hi - cp.ix.t_lo + WAVES - 1) / WAVES;
+      }
+      if (s >= 1) {
+        cp.em = chunk_params(dp, s - 1, nch, cbt);
+        ne = (cp.em.t_hi - cp.em.t_lo + WAVES - 1) / WAVES;
+      }
+      cp.nib = (uint32_t)ni;
+      launch_combo<NV, MODE>((unsigned)(ni + ne), stream, cp, dp.nlist);
+      KX_HIP_CHECK(hipGetLastError());
+      if (s < nch) {
+        const unsigned gg = (unsigned)((cp.ix.g_hi - cp.ix.g_lo + WAVES - 1) / WAVES);
+        hipLaunchKernelGGL((group_kernel<NV, MODE>), dim3(gg), dim3(NT), 0, stream, cp.ix);
+        KX_HIP_CHECK(hipGetLastError());
+        hipLaunchKernelGGL((chain_kernel<NV, MODE>), dim3(1), dim3(CT), 0, stream, cp.ix);
+        KX_HIP_CHECK(hipGetLastError());
+      }
+    }
+    hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(64), 0, stream, dp.status, dp.errkey, dp.overflow, dp.nstop,
+                       dp.offsets, dp.n);
+    KX_HIP_CHECK(hipGetLastError());
     return KX_OK;
   }
   const uint64_t cht = pp && pp->aux ? pp->chunk_tiles : 0;
@@ -2849,6 +3215,11 @@ int kx_launch_decode(const KxProgram* dprog, const KxProgram& hprog, const uint8
   dp.cols = cols; dp.rstat = record_status; dp.status = status; dp.epoch = epoch;
   dp.krec = krec_for(in_len, n);
   dp.winb = win_bytes(in_len, n);
+  {
+    static int fast_env = -1;
+    if (fast_env < 0) { const char* e = getenv("KX_FAST"); fast_env = e ? atoi(e) : 1; }
+    dp.fast = fast_env && !pb && !offsets && hprog.nsteps && hprog.sig_len == 3;
+  }
   for (uint32_t c = 0; c < hprog.ncols; c++) {
     const KxpCol& K = hprog.col[c];
     dp.nlist += K.kind == KXP_K_LIST && K.width > 1 && !K.mside && !((cols.view >> c) & 1);
@@ -2877,13 +3248,26 @@ int kx_launch_skip(const uint8_t* in, uint64_t in_len, uint64_t n, uint64_t* off
 
 int kx_launch_frames(const uint8_t* in, uint64_t in_len, uint64_t n, uint64_t max_payload, uint64_t* frame_offsets,
                      uint64_t* pay_start, uint64_t* pay_end, uint8_t* kinds, kx_status* status, void* ws,
-                     size_t ws_size, uint64_t epoch, hipStream_t stream, bool grpc) {
+                     size_t ws_size, uint64_t epoch, hipStream_t stream, bool grpc, const kx_ttstream_keys* tts,
+                     int32_t* sids, uint64_t* mpos, uint32_t* mlen) {
   DecParams dp{};
   fill_diag_flags(dp);
   dp.in = in; dp.in_len = in_len; dp.offsets = nullptr; dp.n = n; dp.prog = nullptr;
   dp.status = status; dp.skip_out = frame_offsets; dp.epoch = epoch;
   dp.fr_ps = pay_start; dp.fr_pe = pay_end; dp.fr_kind = kinds; dp.fr_max = max_payload;
-  dp.fr_grpc = grpc ? 1 : 0;
+  dp.fr_grpc = tts ? 2 : grpc ? 1 : 0;
+  if (tts) {
+    dp.fr_sid = sids; dp.fr_mpos = mpos; dp.fr_mlen = mlen;
+    dp.tts_keys = (uint32_t)tts->frame_type_key | ((uint32_t)tts->to_method_key << 16);
+    dp.tts_flag = tts->streaming_flag;
+    for (int k = 0; k < 5; k++) {
+      uint64_t v = 0;
+      uint32_t l = 0;
+      while (l < 8 && tts->type_names[k][l]) { v |= (uint64_t)(uint8_t)tts->type_names[k][l] << (8 * l); l++; }
+      dp.tts_name[k] = v;
+      dp.tts_nlen[k] = l;
+    }
+  }
   dp.krec = 64;
   dp.winb = TILE + HALO + 16;
   const WsLayout L = ws_layout(1, in_len, nullptr, n);

@@ -28,6 +28,7 @@ struct kx_schema {
 // emit of chunk k - 1 run on the caller's stream, so emit re-reads a chunk the index pass has just
 // pulled through the Infinity Cache. Events order the two streams (rings of KX_PIPE_EV).
 #define KX_PIPE_EV 8
+#define KX_COMBO_MB_DEFAULT 0  // KX_COMBO_MB: chunk MiB of the one-stream index(k) + emit(k - 1) schedule
 #define KX_CHUNK_MB_DEFAULT 0  // measured: chunking is slower at every size
 struct KxPipe {
   hipStream_t aux = nullptr;
@@ -36,6 +37,7 @@ struct KxPipe {
   hipEvent_t ev_emit[KX_PIPE_EV] = {};  // chunk k emitted (caller's stream) -> throttles aux
   uint64_t chunk_tiles = 0;             // tiles per chunk (a multiple of 64), 0 = one chunk
   int ahead = 1;                        // chunks the index pass may run ahead of emit
+  uint64_t combo_tiles = 0;             // one-stream schedule: index(k) + emit(k - 1) per launch (0: off)
 };
 
 struct kx_ctx {
@@ -101,7 +103,9 @@ int kx_launch_skip(const uint8_t* in, uint64_t in_len, uint64_t n, uint64_t* off
 size_t kx_skip_ws_bytes(uint64_t in_len);
 int kx_launch_frames(const uint8_t* in, uint64_t in_len, uint64_t n, uint64_t max_payload, uint64_t* frame_offsets,
                      uint64_t* pay_start, uint64_t* pay_end, uint8_t* kinds, kx_status* status, void* ws,
-                     size_t ws_size, uint64_t epoch, hipStream_t stream, bool grpc = false);
+                     size_t ws_size, uint64_t epoch, hipStream_t stream, bool grpc = false,
+                     const kx_ttstream_keys* tts = nullptr, int32_t* sids = nullptr, uint64_t* mpos = nullptr,
+                     uint32_t* mlen = nullptr);
 
 int kx_launch_encode(const KxProgram* dprog, const KxProgram& hprog, const KxLaunchCols& cols,
                      uint64_t n, uint8_t* out, uint64_t out_cap, uint64_t* sizes_out,

@@ -325,6 +325,103 @@ int kxo_frame_one(const uint8_t* b, uint64_t len, uint64_t max_payload, uint64_t
   return KX_OK;
 }
 
+/* ttstream DecodeFrame (pkg/remote/trans/ttstream/frame.go:137-185) of the frame at b: ttheader.Decode
+ * (the same TTHeader layout as above; checkProtocolID also admits the streaming struct protocols 0x10
+ * ThriftStruct / 0x11 ProtobufStruct), the streaming flag check (:143-145), IntInfo[frame type key] ->
+ * frame type (:151-168; unknown -> error), IntInfo[ToMethod] (:169; readIntKVInfo: the last occurrence of
+ * a key wins), the TTHeader seqid as the stream id (:170), payload = the PayloadLen bytes after the
+ * header (:173-182). Keys / values of the un-vendored gopkg are the caller's (kx_ttstream_keys). */
+static int tts_match(const uint8_t* v, uint64_t l, const char* name) {
+  uint64_t nl = 0;
+  while (nl < 8 && name[nl]) nl++;
+  return nl == l && memcmp(v, name, l) == 0;
+}
+
+int kxo_ttstream_frame_one(const uint8_t* b, uint64_t len, const kx_ttstream_keys* keys, uint64_t* flen,
+                           uint64_t* ps, uint64_t* pe, uint8_t* ftype, int32_t* sid, uint64_t* mpos,
+                           uint32_t* mlen) {
+  if (len < 8) return KX_ERR_EOF;
+  uint32_t a = be32(b), c = be32(b + 4);
+  if ((c & KXO_MASK) != 0x10000000u) return KX_ERR_UNKNOWN_PROTOCOL;  /* not a TTHeader */
+  if (len < 14) return KX_ERR_EOF;
+  uint64_t hs = (uint64_t)be16(b + 12) * 4;
+  if (hs > 65536 || hs < 2) return KX_ERR_UNKNOWN_PROTOCOL;
+  if (14 + hs > len) return KX_ERR_EOF;
+  const uint8_t* h = b + 14;
+  uint8_t proto = h[0];
+  if (proto != 0 && proto != 3 && proto != 4 && proto != 0x10 && proto != 0x11) return KX_ERR_UNKNOWN_PROTOCOL;
+  uint64_t nt = h[1], i = 2;
+  if (hs - 2 < nt) return KX_ERR_UNKNOWN_PROTOCOL;
+  i += nt;
+  const uint8_t* ftv = NULL;
+  uint64_t ftl = 0;
+  *mpos = 0;
+  *mlen = 0;
+  while (i < hs) {
+    uint8_t id = h[i++];
+    if (id == 0x00) continue;
+    if (id == 0x01) {
+      int rc = kv_strings(h, hs, &i);
+      if (rc) return rc;
+    } else if (id == 0x10) {
+      if (i + 2 > hs) return KX_ERR_UNKNOWN_PROTOCOL;
+      uint32_t k = be16(h + i);
+      i += 2;
+      for (uint32_t j = 0; j < k; j++) {
+        if (i + 4 > hs) return KX_ERR_UNKNOWN_PROTOCOL;
+        uint32_t key = be16(h + i);
+        uint64_t l = be16(h + i + 2);
+        if (i + 4 + l > hs) return KX_ERR_UNKNOWN_PROTOCOL;
+        if (key == keys->frame_type_key) { ftv = h + i + 4; ftl = l; }
+        if (key == keys->to_method_key) { *mpos = 14 + i + 4; *mlen = (uint32_t)l; }
+        i += 4 + l;
+      }
+    } else if (id == 0x11) {
+      if (i + 2 > hs) return KX_ERR_UNKNOWN_PROTOCOL;
+      uint64_t l = be16(h + i);
+      if (i + 2 + l > hs) return KX_ERR_UNKNOWN_PROTOCOL;
+      i += 2 + l;
+    } else {
+      return KX_ERR_UNKNOWN_PROTOCOL;
+    }
+  }
+  uint64_t fend = 4 + (uint64_t)a;
+  if (fend < 14 + hs) return KX_ERR_UNKNOWN_PROTOCOL;
+  if ((c & 0xffffu & keys->streaming_flag) == 0) return KX_ERR_INVALID_DATA;  /* unexpected header flags */
+  uint8_t t = 0;
+  for (int k = 0; k < 5 && !t; k++)
+    if (ftv && tts_match(ftv, ftl, keys->type_names[k])) t = (uint8_t)(k + 1);
+  if (!t) return KX_ERR_INVALID_DATA;  /* unexpected frame type */
+  if (fend > len) return KX_ERR_EOF;   /* reader.ReadBinary(payload) */
+  *flen = fend;
+  *ps = 14 + hs;
+  *pe = fend;
+  *ftype = t;
+  *sid = (int32_t)be32(b + 8);
+  return KX_OK;
+}
+
+int kxo_ttstream_frame_scan(const uint8_t* in, uint64_t in_len, uint64_t n, const kx_ttstream_keys* keys,
+                            uint64_t* frame_offsets, uint64_t* pay_start, uint64_t* pay_end, uint8_t* ftypes,
+                            int32_t* sids, uint64_t* mpos, uint32_t* mlen, uint64_t* n_done) {
+  uint64_t pos = 0;
+  for (uint64_t i = 0; i < n; i++) {
+    frame_offsets[i] = pos;
+    uint64_t fl = 0, ps = 0, pe = 0, mp = 0;
+    uint32_t ml = 0;
+    uint8_t t = 0;
+    int32_t sd = 0;
+    int rc = kxo_ttstream_frame_one(in + pos, in_len - pos, keys, &fl, &ps, &pe, &t, &sd, &mp, &ml);
+    if (rc) { *n_done = i; return rc; }
+    pay_start[i] = pos + ps; pay_end[i] = pos + pe; ftypes[i] = t; sids[i] = sd;
+    mpos[i] = ml ? pos + mp : 0; mlen[i] = ml;
+    pos += fl;
+  }
+  frame_offsets[n] = pos;
+  *n_done = n;
+  return KX_OK;
+}
+
 /* n frames back to back from in[0]; stops at the first failing frame (n_done = its index) */
 int kxo_frame_scan(const uint8_t* in, uint64_t in_len, uint64_t n, uint64_t max_payload, uint64_t* frame_offsets,
                    uint64_t* pay_start, uint64_t* pay_end, uint8_t* kinds, uint64_t* n_done) {

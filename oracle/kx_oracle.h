@@ -92,6 +92,11 @@ int kxo_frame_one(const uint8_t* b, uint64_t len, uint64_t max_payload, uint64_t
                   uint64_t* pe, uint8_t* kind);
 int kxo_frame_scan(const uint8_t* in, uint64_t in_len, uint64_t n, uint64_t max_payload, uint64_t* frame_offsets,
                    uint64_t* pay_start, uint64_t* pay_end, uint8_t* kinds, uint64_t* n_done);
+int kxo_ttstream_frame_one(const uint8_t* b, uint64_t len, const kx_ttstream_keys* keys, uint64_t* flen,
+                           uint64_t* ps, uint64_t* pe, uint8_t* ftype, int32_t* sid, uint64_t* mpos, uint32_t* mlen);
+int kxo_ttstream_frame_scan(const uint8_t* in, uint64_t in_len, uint64_t n, const kx_ttstream_keys* keys,
+                            uint64_t* frame_offsets, uint64_t* pay_start, uint64_t* pay_end, uint8_t* ftypes,
+                            int32_t* sids, uint64_t* mpos, uint32_t* mlen, uint64_t* n_done);
 int kxo_raw_messages(const uint8_t* in, uint64_t in_len, const uint64_t* offsets, uint64_t n, uint64_t* name_pos,
                      uint64_t* name_len, int32_t* msg_type, int32_t* seqid, uint8_t* rs);
 int kxo_set_seqids(uint8_t* in, uint64_t in_len, const uint64_t* offsets, uint64_t n, const int32_t* seqids,

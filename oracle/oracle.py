@@ -66,6 +66,8 @@ def lib():
         L.kxo_frame_scan.argtypes = [vp, C.c_uint64, C.c_uint64, C.c_uint64, vp, vp, vp, vp,
                                      C.POINTER(C.c_uint64)]
         L.kxo_grpc_frame_scan.argtypes = L.kxo_frame_scan.argtypes
+        L.kxo_ttstream_frame_scan.argtypes = [vp, C.c_uint64, C.c_uint64, C.POINTER(A.TTStreamKeys), vp, vp, vp, vp,
+                                              vp, vp, vp, C.POINTER(C.c_uint64)]
         L.kxo_raw_messages.argtypes = [vp, C.c_uint64, vp, C.c_uint64, vp, vp, vp, vp, vp]
         L.kxo_set_seqids.argtypes = [vp, C.c_uint64, vp, C.c_uint64, vp, vp]
         L.kxo_crc32c.argtypes = [C.c_uint32, vp, C.c_uint64]
@@ -184,6 +186,24 @@ def grpc_frame_scan(data: np.ndarray, n: int, max_payload: int = 0):
     rc = lib().kxo_grpc_frame_scan(data.ctypes.data if data.size else None, data.size, n, max_payload,
                                    fo.ctypes.data, ps.ctypes.data, pe.ctypes.data, fl.ctypes.data, C.byref(done))
     return rc, fo, ps[:n], pe[:n], fl[:n], done.value
+
+
+def ttstream_frame_scan(data: np.ndarray, n: int, keys):
+    """ttstream DecodeFrame over n frames (kxo_ttstream_frame_scan): rc, frame offsets[n+1], payload
+    starts[n], payload ends[n], frame types[n], stream ids[n], method positions[n], method lengths[n],
+    frames done"""
+    fo = np.zeros(n + 1, dtype=np.uint64)
+    ps = np.zeros(max(1, n), dtype=np.uint64)
+    pe = np.zeros(max(1, n), dtype=np.uint64)
+    ft = np.zeros(max(1, n), dtype=np.uint8)
+    sd = np.zeros(max(1, n), dtype=np.int32)
+    mp = np.zeros(max(1, n), dtype=np.uint64)
+    ml = np.zeros(max(1, n), dtype=np.uint32)
+    done = C.c_uint64()
+    rc = lib().kxo_ttstream_frame_scan(data.ctypes.data if data.size else None, data.size, n, C.byref(keys),
+                                       fo.ctypes.data, ps.ctypes.data, pe.ctypes.data, ft.ctypes.data, sd.ctypes.data,
+                                       mp.ctypes.data, ml.ctypes.data, C.byref(done))
+    return rc, fo, ps[:n], pe[:n], ft[:n], sd[:n], mp[:n], ml[:n], done.value
 
 
 def crc32c(data: bytes, crc: int = 0) -> int:

@@ -11,11 +11,13 @@ sed -e 's/^#define LDS __attribute__((address_space(3)))/#define LDS/' \
     -e 's/^#define GLB __attribute__((address_space(1)))/#define GLB/' \
     -e 's/^#define KAS __attribute__((address_space(4))).*/#define KAS/' \
     -e 's/^#define KX_PARAMS() .*/#define KX_PARAMS() (dp_)/' \
+    -e 's/^#define KX_CPARAMS() .*/#define KX_CPARAMS() (cp_)/' \
     -e 's/__attribute__((amdgpu_waves_per_eu([0-9]*))) //' \
     -e 's/asm volatile("s_waitcnt vmcnt(0)" ::: "memory");/emu_wait_vmcnt0();/' \
     -e 's/asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");/emu_wait_vmcnt0();/' \
     -e 's/asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WIN_LOADS) : "memory");/emu_wait_vmcnt0();/' \
     -e 's/^  asm volatile("s_mov_b32 m0, %0.*offen lds".*$/  emu_dma_lds16(rs, dst, voff, soff); (void)m0v;/' \
+    -e 's/^  asm("v_writelane_b32 .*$/  old = (uint32_t)emu_writelane((int)old, (int)v, L);/' \
     $ROOT/kitex_amd/csrc/kx_decode.hip > _build/kx_decode_emu.cpp
 CXX=${CXX:-/opt/rocm/lib/llvm/bin/clang++}
 FLAGS="-std=c++17 -O1 -g -fPIC -Wno-unknown-attributes -Wno-unused-function -I. -I$ROOT/kitex_amd/csrc ${EMU_EXTRA:-}"

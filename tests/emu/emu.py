@@ -34,7 +34,27 @@ def lib():
                                  C.c_void_p]
         _lib.emu_frames.restype = C.c_int
         _lib.emu_frames.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint64] + [C.c_void_p] * 5 + [C.c_int]
+        _lib.emu_tts_frames.restype = C.c_int
+        _lib.emu_tts_frames.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.POINTER(A.TTStreamKeys)] + \
+            [C.c_void_p] * 8
     return _lib
+
+
+def tts_frames(data: np.ndarray, n: int, keys, threads: int = 8):
+    """the ttstream frame scan of the kernel source: rc, fo, ps, pe, frame types, stream ids, method pos, len, st"""
+    os.environ["KX_EMU_THREADS"] = str(threads)
+    fo = np.zeros(n + 1, dtype=np.uint64)
+    ps = np.zeros(max(1, n), dtype=np.uint64)
+    pe = np.zeros(max(1, n), dtype=np.uint64)
+    ft = np.zeros(max(1, n), dtype=np.uint8)
+    sd = np.zeros(max(1, n), dtype=np.int32)
+    mp = np.zeros(max(1, n), dtype=np.uint64)
+    ml = np.zeros(max(1, n), dtype=np.uint32)
+    st = A.Status()
+    rc = lib().emu_tts_frames(data.ctypes.data, data.size, n, C.byref(keys), fo.ctypes.data, ps.ctypes.data,
+                              pe.ctypes.data, ft.ctypes.data, sd.ctypes.data, mp.ctypes.data, ml.ctypes.data,
+                              C.addressof(st))
+    return rc, fo, ps[:n], pe[:n], ft[:n], sd[:n], mp[:n], ml[:n], st
 
 
 def decode(schema, infos, npres, data: np.ndarray, n: int, offsets=None, var_caps=None, threads: int = 8,

@@ -42,7 +42,7 @@ extern "C" int emu_decode(const kx_struct_desc* structs, uint32_t nstructs, cons
     memset(ws + 8, 0xff, 8);
     epoch = 1;
   }
-  status->diag[0] = status->diag[1] = 0;
+  status->diag[0] = status->diag[1] = status->diag[2] = 0;
   if (skip)
     rc = kx_launch_skip(in, in_len, n, skip_out, status, ws, ws_cap, epoch, nullptr);
   else
@@ -54,6 +54,9 @@ extern "C" int emu_decode(const kx_struct_desc* structs, uint32_t nstructs, cons
     const char* a = getenv("KX_EMU_AHEAD");
     pipe.ahead = a ? atoi(a) : 1;
     pipe.aux = (hipStream_t)&pipe;  // any non-null handle
+    // KX_EMU_COMBO = tiles per chunk of the one-stream index(k) + emit(k - 1) schedule
+    const char* cb = getenv("KX_EMU_COMBO");
+    pipe.combo_tiles = cb ? strtoull(cb, nullptr, 10) : 0;
     rc = kx_launch_decode(&s.prog, s.prog, in, in_len, offsets, n, lc, record_status, status, ws, ws_cap, epoch,
                           nullptr, mode == 2, nullptr, nullptr, &pipe);
   }
@@ -80,6 +83,30 @@ extern "C" int emu_frames(const uint8_t* in, uint64_t in_len, uint64_t n, uint64
   }
   status->diag[0] = status->diag[1] = 0;
   return kx_launch_frames(in, in_len, n, max_payload, fo, ps, pe, kinds, status, ws, ws_cap, epoch, nullptr, grpc != 0);
+}
+
+// ttstream frame scan (kx_launch_frames with keys) under the emulator
+extern "C" int emu_tts_frames(const uint8_t* in, uint64_t in_len, uint64_t n, const kx_ttstream_keys* keys,
+                              uint64_t* fo, uint64_t* ps, uint64_t* pe, uint8_t* ft, int32_t* sid, uint64_t* mp,
+                              uint32_t* ml, kx_status* status) {
+  const size_t ws_size = kx_skip_ws_bytes(in_len);
+  static char* ws = nullptr;
+  static size_t ws_cap = 0;
+  static uint64_t epoch = 0xffff;
+  if (ws_cap < ws_size) {
+    free(ws);
+    ws_cap = ws_size + ws_size / 4;
+    ws = (char*)malloc(ws_cap);
+    epoch = 0xffff;
+  }
+  if (++epoch > 0xffff) {
+    memset(ws, 0, ws_cap);
+    memset(ws + 8, 0xff, 8);
+    epoch = 1;
+  }
+  status->diag[0] = status->diag[1] = 0;
+  return kx_launch_frames(in, in_len, n, 0, fo, ps, pe, ft, status, ws, ws_cap, epoch, nullptr, false, keys, sid, mp,
+                          ml);
 }
 
 // CRC32C kernel source (kx_crc.hip): val = 0 ranges [offs[i], offs[i+1]), 1 TTHeader frames at offs[i]

@@ -103,6 +103,8 @@ inline int __builtin_amdgcn_readlane(int v, int l) {
 }
 // only used where every active lane holds the same value
 inline int __builtin_amdgcn_readfirstlane(int v) { return v; }
+// src and l are wave-uniform where the kernels use it
+inline int emu_writelane(int old, int src, int l) { return emu_lane() == (l & 63) ? src : old; }
 
 inline uint32_t __builtin_amdgcn_alignbyte(uint32_t hi, uint32_t lo, uint32_t s) {
   return (uint32_t)((((uint64_t)hi << 32) | lo) >> ((s & 3) * 8));

@@ -5,6 +5,8 @@ CPU test run; the emulator is test infrastructure and is never linked into the p
 import numpy as np
 import pytest
 
+from kitex_amd import schema as S
+from kitex_amd import synth
 from tests import decode_cases as DC
 from tests import frame_cases as FC
 from tests import pb_cases as PC
@@ -138,6 +140,13 @@ def test_emu_chunked(edec, oracle, case, ahead, monkeypatch):
     DC.case_chunked(edec, oracle, case)
 
 
+@pytest.mark.parametrize("case", DC.CHUNK_CASES)
+def test_emu_combo(edec, oracle, case, monkeypatch):
+    """the one-stream schedule: index of chunk k and emit of chunk k - 1 in one launch (64-tile chunks)"""
+    monkeypatch.setenv("KX_EMU_COMBO", "64")
+    DC.case_chunked(edec, oracle, case)
+
+
 # ---- framing sniff (M_FRAME walker, kx_launch_frames) ----
 def _emu_scan(threads=8):
     def scan(wire, n, mx):
@@ -163,3 +172,19 @@ def test_emu_index_prefetch(edec, oracle, case, monkeypatch):
     wave walking many tiles while the next one's DMA is in flight)"""
     monkeypatch.setenv("KX_INDEX_PF", "2")
     DC.case_chunked(edec, oracle, case)
+
+
+@pytest.mark.parametrize("name,n", [("r1", 20000), ("r2", 15000), ("r3", 4000)])
+def test_emu_fast_index_path_taken(edec, oracle, name, n):
+    """canonical batches: every tile but the last few takes the fast index path (status diag[2] counts
+    the tiles that fell back to walk_tile), and the decode equals the oracle's"""
+    from tests.helpers import assert_columns_equal
+    sch = S.SCHEMAS[name]()
+    _, infos, npres = oracle.flatten(sch)
+    rc, wire, _ = oracle.encode(sch, synth.GENERATORS[name](n, start=5))
+    erc, cols, st, _ = emu.decode(sch, infos, npres, wire, n, threads=8)
+    assert erc == 0 and st.code == 0 and st.n_records == n
+    tiles = (wire.size + 8191) // 8192
+    assert st.diag[2] <= 2, (st.diag[2], tiles)
+    rc, exp, est, _ = oracle.decode(sch, wire, n)
+    assert_columns_equal(cols, exp, infos, n)
