@@ -27,7 +27,8 @@ EXPORTS = [
     "kx_pb_read_meta", "kx_ctx_set_pipeline", "kx_frame_scan", "kx_thrift_decode_frames",
     "kx_pb_decode_frames", "kx_crc32c_batch", "kx_frame_crc32c_validate", "kx_ctx_set_crc32c_check",
     "kx_grpc_frame_scan", "kx_thrift_decode_grpc", "kx_pb_decode_grpc", "kx_thrift_raw_messages",
-    "kx_thrift_set_seqids", "kx_thrift_encode_messages",
+    "kx_thrift_set_seqids", "kx_thrift_encode_messages", "kx_ttstream_default_keys", "kx_ttstream_frame_scan",
+    "kx_thrift_decode_extents", "kx_pb_decode_extents",
 ]
 
 
