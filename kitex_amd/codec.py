@@ -151,6 +151,24 @@ def _ptr(t) -> Optional[int]:
     return None if t is None else t.data_ptr()
 
 
+def on_call_stream(fn):
+    """Run the call with its `stream` argument as torch's current stream, so the outputs it allocates
+    (and their zero fills) are ordered on the stream its kernels run on: the caching allocator then
+    never hands a buffer a side-stream kernel still writes to another call, and no fill on the default
+    stream can land after the kernel (the caller's `stream` keyword; current stream when absent)."""
+    import functools
+
+    @functools.wraps(fn)
+    def run(*args, **kw):
+        st = kw.get("stream")
+        if st is None:
+            return fn(*args, **kw)
+        import torch
+        with torch.cuda.stream(st):
+            return fn(*args, **kw)
+    return run
+
+
 @dataclass
 class DecodeResult:
     columns: ColumnSet
@@ -202,6 +220,7 @@ def default_ttstream_keys() -> A.TTStreamKeys:
     return k
 
 
+@on_call_stream
 def ttstream_frame_scan(buf, n: int, keys: Optional[A.TTStreamKeys] = None, device: int = 0, stream=None):
     """kx_ttstream_frame_scan over a device buffer of n ttstream frames. Returns (frame offsets int64[n+1],
     payload starts int64[n], payload ends int64[n], frame types uint8[n], stream ids int32[n], method
@@ -275,6 +294,7 @@ class ThriftCodec:
     def Name(self) -> str:
         return "Thrift"
 
+    @on_call_stream
     def Unmarshal(self, buf, n: int, offsets=None, out: ColumnSet = None, var_caps: Sequence[int] = None,
                   record_status: bool = False, stream=None, raise_on_error: bool = True,
                   status=None, views: bool = False) -> DecodeResult:
@@ -333,6 +353,7 @@ class ThriftCodec:
     _GRPC = "kx_thrift_decode_grpc"
     _PATH_FN = staticmethod(select_unmarshal)
 
+    @on_call_stream
     def UnmarshalMessages(self, buf, n: int, offsets, body_field: int = 1, out: ColumnSet = None,
                           var_caps: Sequence[int] = None, name_cap: int = None, stream=None,
                           raise_on_error: bool = True) -> "MessageBatch":
@@ -345,6 +366,7 @@ class ThriftCodec:
             args.append(body_field)
         return self._messages(self._MESSAGES, args, buf, n, out, var_caps, name_cap, s, raise_on_error)
 
+    @on_call_stream
     def UnmarshalFrames(self, buf, n: int, body_field: int = 1, max_payload: int = 0, out: ColumnSet = None,
                         var_caps: Sequence[int] = None, name_cap: int = None, stream=None,
                         raise_on_error: bool = True, crc32_check: bool = False) -> "MessageBatch":
@@ -366,6 +388,7 @@ class ThriftCodec:
         res.frame_offsets, res.kinds = fo, kinds[:n]
         return res
 
+    @on_call_stream
     def UnmarshalGRPC(self, buf, n: int, max_payload: int = 0, out: ColumnSet = None,
                       var_caps: Sequence[int] = None, stream=None, raise_on_error: bool = True) -> "DecodeResult":
         """grpcCodec.Decode (pkg/remote/codec/grpc/grpc.go:202-270) over n gRPC messages back to back
@@ -397,6 +420,7 @@ class ThriftCodec:
 
     _EXTENTS = "kx_thrift_decode_extents"
 
+    @on_call_stream
     def UnmarshalExtents(self, buf, starts, ends, out: ColumnSet = None, var_caps: Sequence[int] = None,
                          stream=None, raise_on_error: bool = True) -> DecodeResult:
         """FastUnmarshal of n bare bodies at explicit extents buf[starts[i]:ends[i]) (int64 device tensors;
@@ -424,6 +448,7 @@ class ThriftCodec:
                 raise ProtocolError(stt.code, self._WHAT, stt.record, stt.offset)
         return res
 
+    @on_call_stream
     def UnmarshalStream(self, buf, n_frames: int, keys: Optional[A.TTStreamKeys] = None, stream=None,
                         raise_on_error: bool = True) -> "StreamBatch":
         """ttstream's receive side over a connection buffer of n TTHeader streaming frames (DecodeFrame,
@@ -473,6 +498,7 @@ class ThriftCodec:
                 raise ProtocolError(stt.code, self._WHAT, stt.record, stt.offset)
         return res
 
+    @on_call_stream
     def Marshal(self, cols: ColumnSet, with_offsets: bool = True, stream=None, out=None, status=None,
                 check_status: bool = True):
         """Encode the columns; returns (wire uint8 tensor, record offsets int64[n+1] or None).
@@ -501,6 +527,7 @@ class ThriftCodec:
             raise ProtocolError(s.code, self._ENCODE)
         return out[:s.consumed], offs
 
+    @on_call_stream
     def MarshalMessages(self, cols: ColumnSet, method: str, seqids, msg_type: int = 1, body_field: int = 1,
                         stream=None):
         """fastMarshal (codec_fast.go:40-58) of n messages: MessageBegin(method, msg_type, seqids[i]) + the
@@ -541,6 +568,7 @@ class ThriftCodec:
             raise ProtocolError(s.code, "fastMarshal")
         return out[:s.consumed], offs
 
+    @on_call_stream
     def BLength(self, cols: ColumnSet, stream=None):
         import torch
         ds = self.dschema
@@ -552,6 +580,7 @@ class ThriftCodec:
         check(rc, self._SIZE)
         return sizes[:cols.n]
 
+    @on_call_stream
     def Skip(self, buf, n: int, stream=None):
         """skipThriftStruct over n concatenated records -> int64[n+1] record offsets."""
         import torch
@@ -594,6 +623,7 @@ class ProtobufCodec(ThriftCodec):
     def Name(self) -> str:
         return "protobuf"
 
+    @on_call_stream
     def Skip(self, buf, n: int, stream=None):
         raise KxError(A.ERR_NOT_IMPLEMENTED, "protobuf has no skip decoder")
 
@@ -641,6 +671,7 @@ def read_pb_meta(data: bytes):
     return bytes(data[off:off + nl.value]).decode(), t.value, s.value, u.value
 
 
+@on_call_stream
 def grpc_frame_scan(buf, n: int, max_payload: int = 0, device: int = 0, stream=None):
     """kx_grpc_frame_scan over a device buffer of n gRPC messages. Returns (frame offsets int64[n+1],
     payload starts int64[n], payload ends int64[n], compressed flags uint8[n], status tensor)."""
@@ -658,6 +689,7 @@ def grpc_frame_scan(buf, n: int, max_payload: int = 0, device: int = 0, stream=N
     return fo, ps[:n], pe[:n], fl[:n], st
 
 
+@on_call_stream
 def frame_scan(buf, n: int, max_payload: int = 0, device: int = 0, stream=None):
     """kx_frame_scan: the framing sniff alone over a device buffer of n frames. Returns (frame offsets
     int64[n+1], payload starts int64[n], payload ends int64[n], kinds uint8[n], status tensor)."""
@@ -708,6 +740,7 @@ class CRC32PayloadValidator:
     def hex_value(crc: int) -> str:
         return "%08x" % (crc & 0xFFFFFFFF)
 
+    @on_call_stream
     def Generate(self, buf, offsets, stream=None):
         """-> int64 tensor of CRC-32C values (0..2^32-1), one per range"""
         import torch
@@ -722,6 +755,7 @@ class CRC32PayloadValidator:
             raise KxError(stt.code, "crc32c generate", stt.record, stt.offset)
         return out[:n].to(torch.int64) & 0xFFFFFFFF
 
+    @on_call_stream
     def ValidateFrames(self, buf, frame_offsets, n: int, stream=None, raise_on_error: bool = False):
         """-> (per-frame codes uint8[n], per-frame payload CRC int64[n], kx_status)"""
         import torch

@@ -58,6 +58,9 @@ constexpr uint64_t X_BAD = V48 - 3;      // group whose speculative tile chain d
 // exclusive prefix inside the group written by the group scan
 enum { T_ENT = 0, T_EXIT, T_CNT, T_ERRC, T_ERRP, T_VAR, T_PCNT = T_VAR + KXP_NV_MAX, T_PVAR,
        T_NF = T_PVAR + KXP_NV_MAX };
+// T_ERRC of a tile indexed by the fast path (no error possible): its records are canonical and inside the
+// window, so the emit pass reads them with the plan alone (emit_canon)
+constexpr uint64_t T_CANON = 0x100;
 // group words: group aggregate, then the global exclusive base written by the chain pass
 enum { G_ENT = 0, G_EXIT, G_CNT, G_ERRC, G_ERRP, G_VAR, G_BCNT = G_VAR + KXP_NV_MAX, G_BVAR,
        G_NF = G_BVAR + KXP_NV_MAX };
@@ -2011,7 +2014,7 @@ __device__ __forceinline__ Agg measure_records(KParams& dp, const Src& w, uint64
 //  * segments on the window's dword grid (segment s = window dwords D0 + 32 s .. + 31, the last one
 //    runs to the tile end); the signature scan is interleaved (iteration k: lane l tests dword
 //    D0 + 64 k + l) and a ballot per iteration hands segment 2k / 2k + 1 its dword-hit mask
-//    (writelane), so every LDS read is conflict-free and no lane loops over its own bytes;
+//    (a select per lane), so every LDS read is conflict-free and no lane loops over its own bytes;
 //  * a lane walks from its first hit (its second one when the first does not parse canonically: a
 //    nested struct with the same first header) with `fast_record`: the canonical plan's headers and
 //    lengths only, one window bounds check per step;
@@ -2019,26 +2022,20 @@ __device__ __forceinline__ Agg measure_records(KParams& dp, const Src& w, uint64
 //    else (a non-canonical record, a false signature hit, a record leaving the window, > 4 records in
 //    a segment) returns false and the tile takes walk_tile from scratch.
 // ---------------------------------------------------------------------------------------------
-// v_writelane_b32: lane L of `old` takes the wave-uniform value v
-template <int L>
-__device__ __forceinline__ uint32_t writelane(uint32_t old, uint32_t v) {
-  asm("v_writelane_b32 %0, %1, %2" : "+v"(old) : "s"(v), "i"(L));
-  return old;
-}
-
 // iteration K of the interleaved signature scan: lane l tests window dword D0 + 64 K + l; the ballot's
-// halves are the dword-hit masks of segments 2K and 2K + 1, written into those lanes
+// halves are the dword-hit masks of segments 2K and 2K + 1, picked up by those lanes (kk = lane / 2,
+// sh = 32 * (lane % 2)). (v_writelane would save an instruction, but from inline assembly the compiler
+// cannot see its SGPR read-after-VALU-write hazard.)
 template <int K>
 __device__ __forceinline__ void fast_scan(const Src& w, uint32_t D0, uint32_t b0, uint32_t b1, uint32_t b2, int lane,
-                                          uint32_t& hm) {
+                                          uint32_t kk, uint32_t sh, uint32_t& hm) {
   const uint32_t d = D0 + 64u * K + (uint32_t)lane;
   const uint32_t x0 = w.win[d], x1 = w.win[d + 1];
   const uint32_t e = (x0 ^ b0) | (__builtin_amdgcn_alignbyte(x1, x0, 1) ^ b1) |
                      (__builtin_amdgcn_alignbyte(x1, x0, 2) ^ b2);
   const uint64_t bal = __ballot(low_zero_byte(e) != 0);
-  hm = writelane<2 * K>(hm, (uint32_t)bal);
-  hm = writelane<2 * K + 1>(hm, (uint32_t)(bal >> 32));
-  if constexpr (K + 1 < 32) fast_scan<K + 1>(w, D0, b0, b1, b2, lane, hm);
+  hm = kk == (uint32_t)K ? (uint32_t)(bal >> sh) : hm;
+  if constexpr (K + 1 < 32) fast_scan<K + 1>(w, D0, b0, b1, b2, lane, kk, sh, hm);
 }
 
 __device__ __forceinline__ uint32_t win_ld(const Src& w, uint32_t q) {  // 4 bytes at window offset q
@@ -2107,7 +2104,7 @@ __device__ __forceinline__ bool fast_tile(KParams& dp, const Src& w, uint64_t tl
   const uint32_t D0 = q0 >> 2;
   // ---- interleaved scan: hm = the dword-hit mask of this lane's segment ----
   uint32_t hm = 0;
-  fast_scan<0>(w, D0, b0, b1, b2, lane, hm);
+  fast_scan<0>(w, D0, b0, b1, b2, lane, (uint32_t)lane >> 1, 32u * ((uint32_t)lane & 1u), hm);
   const uint32_t sq = 4 * D0 + 128u * (uint32_t)lane;   // window offset of the segment's first dword
   const uint64_t seg_lo = lane == 0 ? tlo : w.wpos + sq;
   const uint64_t seg_hi = lane == 63 ? thi : kmin64(w.wpos + sq + 128, thi);
@@ -2189,7 +2186,7 @@ __device__ __forceinline__ bool fast_tile(KParams& dp, const Src& w, uint64_t tl
   for (int v = 0; v < NV; v++) a.var[v] = wave_sum(vsum[v]);
   a.ent = hmk ? rl64(ent, __ffsll((long long)hmk) - 1) : X_NONE;
   a.ex = hmk ? rl64(ex, 63 - __clzll((long long)hmk)) : seed;
-  a.errc = 0;
+  a.errc = T_CANON;   // every record of the tile is canonical and inside the window: emit trusts the plan
   a.errp = 0;
   if (cnt > 0) starts[cpre + 0] = (uint16_t)(st0 - tlo);
   if (cnt > 1) starts[cpre + 1] = (uint16_t)(st1 - tlo);
@@ -2338,7 +2335,7 @@ __device__ void group_scan(KParams& dp, LDS uint32_t* win, uint64_t g, uint64_t 
   const uint64_t gent = hm ? rl64(ent, __ffsll((long long)hm) - 1) : X_NONE;
   const uint64_t gex = fe < 64 ? X_ERR : hm ? rl64(ex, 63 - __clzll((long long)hm)) : entry;
   const uint64_t gcnt = rl64(ci, 63);
-  const uint64_t gerrc = fe < 64 ? rl64(errc, fe) : 0;
+  const uint64_t gerrc = fe < 64 ? rl64(errc, fe) & 0xff : 0;
   const uint64_t gerrp = fe < 64 ? rl64(errp, fe) : 0;
   if (lane == 0) {
     const uint64_t ng = dp.ngroups;
@@ -2615,6 +2612,47 @@ __global__ void __launch_bounds__(CT) chain_kernel(DecParams dp_) {
   }
 }
 
+// Emit of a record the fast index path validated (T_CANON tile): the canonical plan alone, no header
+// checks and no bounds checks (every step of the record lies inside the window). Fixed fields are
+// stored, var fields recorded for the copy; returns the record's end.
+template <int NV>
+__device__ __forceinline__ uint64_t emit_canon(const Src& w, const KAS KxLaunchCols& cols, uint64_t pos, uint64_t r,
+                                               VarState<NV>& vs) {
+  const KAS KxpStep* __restrict__ steps = w.steps;
+  uint32_t q = (uint32_t)(pos - w.wpos);
+  uint32_t k = 0;
+  while (k < w.nsteps) {
+    const KxpStep st = ldk(&steps[k]);
+    if (st.kind == KXP_S_FIXED) {
+      const uint32_t m = min(st.hdr >> 24, 4u);
+#pragma unroll
+      for (uint32_t j = 0; j < 4; j++) {
+        if (j >= m) break;
+        const KxpStep sj = j == 0 ? st : ldk(&steps[k + j]);
+        const LDS uint32_t* s0 = w.win + (q >> 2);
+        const uint32_t sh = q & 3;
+        Fetch f;
+        f.w0 = __builtin_amdgcn_alignbyte(s0[1], s0[0], sh);
+        f.w1 = __builtin_amdgcn_alignbyte(s0[2], s0[1], sh);
+        f.w2 = __builtin_amdgcn_alignbyte(s0[3], s0[2], sh);
+        store_col(cols.data[sj.col], sj.width, r, fixed_after_header(f, sj.hdr & 0xff));
+        q += 3 + sj.width;
+      }
+      k += m;
+      continue;
+    }
+    k++;
+    if (st.kind == KXP_S_END) { q += 1; continue; }
+    if (st.kind == KXP_S_STRUCT) { q += 3; continue; }
+    const bool list = st.kind == KXP_S_LIST;
+    const uint32_t l = __builtin_bswap32(win_ld(w, q + (list ? 4u : 3u)));
+    const uint32_t vp = q + (list ? 8u : 7u);
+    vset<NV>(vs, st.vslot, w.wpos + vp, l);
+    q = vp + l * (list ? st.width : 1u);
+  }
+  return w.wpos + q;
+}
+
 // one element of wire type t at q: its payload position and length (strings) or width (scalars)
 __device__ __forceinline__ uint64_t elem_at(const Src& w, uint64_t q, uint32_t t, uint64_t& xp, uint32_t& xl) {
   if (t == KX_T_STRING) {
@@ -2715,6 +2753,9 @@ __device__ __forceinline__ void emit_tile(KParams& dp, LDS uint32_t* win, uint64
     for (int v = 0; v < NV; v++)
       run[v] = (gd[(uint64_t)(G_BVAR + v) * dp.ngroups + g] & V48) + (td[(uint64_t)(T_PVAR + v) * dp.ntiles + t] & V48);
   }
+  // a tile the fast index path validated: records are read with the plan alone
+  const bool canon = is_thrift(MODE) && !known && !dp.direct && MODE != M_THRIFT_LS &&
+                     ((dp.tdesc[(uint64_t)T_ERRC * dp.ntiles + t] & V48) == T_CANON);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (cnt == 0 || base >= nstop) return;
   cnt = kmin64(cnt, nstop - base);
@@ -2735,7 +2776,12 @@ __device__ __forceinline__ void emit_tile(KParams& dp, LDS uint32_t* win, uint64
       } else {
         pos = lo + starts[j];
       }
-      if (!rc) rc = parse_record<NV, MODE>(dp, w, pos, lim, r, MODE != M_SKIP, &end, vs, pres);
+      if (canon) {
+        end = emit_canon<NV>(w, dp.cols, pos, r, vs);
+        pres = w.canon_pres;
+      } else if (!rc) {
+        rc = parse_record<NV, MODE>(dp, w, pos, lim, r, MODE != M_SKIP, &end, vs, pres);
+      }
       if (rc) {  // offsets mode: the failed record reads as all defaults, empty payloads
 #pragma unroll
         for (int v = 0; v < NV; v++) vs.len[v] = 0;

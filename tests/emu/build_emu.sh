@@ -17,7 +17,6 @@ sed -e 's/^#define LDS __attribute__((address_space(3)))/#define LDS/' \
     -e 's/asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");/emu_wait_vmcnt0();/' \
     -e 's/asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WIN_LOADS) : "memory");/emu_wait_vmcnt0();/' \
     -e 's/^  asm volatile("s_mov_b32 m0, %0.*offen lds".*$/  emu_dma_lds16(rs, dst, voff, soff); (void)m0v;/' \
-    -e 's/^  asm("v_writelane_b32 .*$/  old = (uint32_t)emu_writelane((int)old, (int)v, L);/' \
     $ROOT/kitex_amd/csrc/kx_decode.hip > _build/kx_decode_emu.cpp
 CXX=${CXX:-/opt/rocm/lib/llvm/bin/clang++}
 FLAGS="-std=c++17 -O1 -g -fPIC -Wno-unknown-attributes -Wno-unused-function -I. -I$ROOT/kitex_amd/csrc ${EMU_EXTRA:-}"
