@@ -450,15 +450,14 @@ def extras(args, r2, dev, local):
         buf = torch.empty_like(b.wire)
         st = status_tensor(dev)
 
-        def enc():
-            b.cdc.BLength(b.src)
+        def enc():  # fastMarshal: BLength (the size pass inside the call) + FastWriteNocopy
             b.cdc.Marshal(b.src, with_offsets=False, out=buf, status=st, check_status=False)
         t, per = time_steps(enc, steps, warm, 1, dev)
         ok = bool(torch.equal(buf, b.wire))
         avg = sum(per) / len(per) / 1e3
         alg = b.out_bytes_per_record() * b.n + b.in_bytes      # columns in + wire out
         return {"records_per_s": b.n * steps / t, "ms_per_step": t / steps * 1e3, "bit_exact": ok,
-                "roofline": roofline(alg, avg, "BLength + encode")}
+                "roofline": roofline(alg, avg, "encode (size pass + scan + write pass)")}
 
     def decode_entry(b):
         t, per = time_steps(b.step, steps, warm, 1, dev)

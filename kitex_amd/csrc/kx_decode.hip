@@ -115,6 +115,7 @@ struct DecParams {
   uint32_t nlist;            // numeric list columns (thrift): emit copies them wave-cooperatively
   int direct;                // offsets mode without var columns: emit pass only
   int fast;                  // concatenated Thrift with a canonical plan: fast_tile before walk_tile
+  int all_view;              // every var column is a zero-copy view (no arena to lay out)
   int nolds;                 // diagnostics (KX_NOLDS=1): read every byte from global memory
   int diag;                  // diagnostics (KX_DIAG bits, timing experiments only; output is wrong):
                              // 1 no walk, 2 no group arrival, 4 no tile words, 256 index pass only
@@ -1983,30 +1984,6 @@ __device__ Agg walk_tile(KParams& dp, const Src& w, uint64_t tlo, uint64_t thi, 
   return a;
 }
 
-// Known-offsets mode: lane = record. Measures the var extents (failed records count as empty).
-template <int NV, int MODE>
-__device__ __forceinline__ Agg measure_records(KParams& dp, const Src& w, uint64_t r0, uint64_t r1, int lane) {
-  const uint64_t r = r0 + lane;
-  VarState<NV> vs;
-#pragma unroll
-  for (int v = 0; v < NV; v++) vs.len[v] = 0;
-  if (r < r1) {
-    const uint64_t a = dp.offsets[r], b = rec_end(dp, r);
-    uint64_t end, pres;
-    int rc = (a > b || b > dp.in_len) ? KX_ERR_INVALID_ARG : parse_record<NV, MODE>(dp, w, a, b, r, false, &end, vs, pres);
-    if (rc) {
-#pragma unroll
-      for (int v = 0; v < NV; v++) vs.len[v] = 0;
-    }
-  }
-  Agg g;
-  g.ent = X_NONE; g.ex = X_NONE; g.errc = 0; g.errp = 0;
-  g.cnt = r1 - r0;
-#pragma unroll
-  for (int v = 0; v < NV; v++) g.var[v] = wave_sum(vs.len[v]);
-  return g;
-}
-
 // ---------------------------------------------------------------------------------------------
 // Fast index path (concatenated Thrift, batches whose records start with the schema's canonical
 // signature): the same tile aggregate and record starts as walk_tile, for tiles whose records are all
@@ -2195,6 +2172,49 @@ __device__ __forceinline__ bool fast_tile(KParams& dp, const Src& w, uint64_t tl
   return true;
 }
 
+// Known-offsets mode: lane = record. Measures the var extents (failed records count as empty). A record
+// that lies in the window and parses canonically is measured with fast_record (headers and lengths of
+// the plan); any other takes parse_record, which also reports its error.
+template <int NV, int MODE>
+__device__ __forceinline__ Agg measure_records(KParams& dp, const Src& w, uint64_t r0, uint64_t r1, int lane) {
+  const uint64_t r = r0 + lane;
+  VarState<NV> vs;
+#pragma unroll
+  for (int v = 0; v < NV; v++) vs.len[v] = 0;
+  if (r < r1) {
+    const uint64_t a = dp.offsets[r], b = rec_end(dp, r);
+    bool done = false;
+    if constexpr (MODE == M_THRIFT) {
+      if (dp.fast && a <= b && b <= dp.in_len && a >= w.wpos && a - w.wpos < (uint64_t)w.wlen) {
+        uint64_t vl[NV > 0 ? NV : 1];
+#pragma unroll
+        for (int v = 0; v < (NV > 0 ? NV : 1); v++) vl[v] = 0;
+        uint32_t q = (uint32_t)(a - w.wpos);
+        if (fast_record<NV>(w, q, vl) && w.wpos + q <= b) {
+#pragma unroll
+          for (int v = 0; v < NV; v++) vs.len[v] = (uint32_t)vl[v];
+          done = true;
+        }
+      }
+    }
+    if (!done) {
+      uint64_t end, pres;
+      int rc = (a > b || b > dp.in_len) ? KX_ERR_INVALID_ARG
+                                        : parse_record<NV, MODE>(dp, w, a, b, r, false, &end, vs, pres);
+      if (rc) {
+#pragma unroll
+        for (int v = 0; v < NV; v++) vs.len[v] = 0;
+      }
+    }
+  }
+  Agg g;
+  g.ent = X_NONE; g.ex = X_NONE; g.errc = 0; g.errp = 0;
+  g.cnt = r1 - r0;
+#pragma unroll
+  for (int v = 0; v < NV; v++) g.var[v] = wave_sum(vs.len[v]);
+  return g;
+}
+
 // tile geometry
 __device__ __forceinline__ void tile_range(KParams& dp, uint64_t t, uint64_t& lo, uint64_t& hi) {
   if (dp.offsets) {
@@ -2220,7 +2240,7 @@ __device__ Agg tile_agg(KParams& dp, LDS uint32_t* win, uint64_t t, uint64_t see
   if ((dp.diag & 64) && lane == 0) atomicAdd(&g_phase[0], (unsigned long long)(__builtin_amdgcn_s_memtime() - t0));
   const uint32_t dsig = data_sig(dp);
   if constexpr (MODE == M_THRIFT) {
-    if (dp.fast && dsig == dp.prog->sig && w.wlen >= TILE + 64) {
+    if (dp.fast && !dp.offsets && dsig == dp.prog->sig && w.wlen >= TILE + 64) {
       Agg a;
       if (fast_tile<NV>(dp, w, lo, hi, seed, lane, dp.starts + t * dp.slotcap, a)) return a;
       if (lane == 0) atomicAdd((unsigned long long*)&dp.status->diag[2], 1ull);  // fell back to walk_tile
@@ -2738,7 +2758,7 @@ __device__ __forceinline__ void emit_tile(KParams& dp, LDS uint32_t* win, uint64
   uint64_t base = 0, cnt = 0, run[NV > 0 ? NV : 1];
 #pragma unroll
   for (int v = 0; v < (NV > 0 ? NV : 1); v++) run[v] = 0;
-  if (dp.direct) {  // offsets mode without var columns: no index pass
+  if (dp.direct) {  // offsets mode without arena columns: no index pass
     base = lo;
     cnt = hi - lo;
   } else {
@@ -3030,7 +3050,7 @@ int launch_t(const DecParams& dp0, const WsLayout& L, void* ws, hipStream_t stre
   dp.ntiles = L.ntiles;
   dp.ngroups = L.ngroups;
   dp.slotcap = L.slotcap;
-  dp.direct = dp.offsets && NV == 0;
+  dp.direct = dp.offsets && (NV == 0 || dp.all_view);  // no arena positions to scan: emit alone
   dp.t_lo = 0; dp.t_hi = dp.ntiles; dp.g_lo = 0; dp.g_hi = dp.ngroups;
   dp.chunk_first = dp.chunk_last = 1;
   KX_HIP_CHECK(hipMemsetAsync(dp.status, 0, sizeof(kx_status), stream));
@@ -3261,10 +3281,13 @@ int kx_launch_decode(const KxProgram* dprog, const KxProgram& hprog, const uint8
   dp.cols = cols; dp.rstat = record_status; dp.status = status; dp.epoch = epoch;
   dp.krec = krec_for(in_len, n);
   dp.winb = win_bytes(in_len, n);
+  dp.all_view = 1;
+  for (uint32_t v = 0; v < hprog.nvar; v++) dp.all_view &= (int)((cols.view >> hprog.var_col[v]) & 1);
   {
     static int fast_env = -1;
     if (fast_env < 0) { const char* e = getenv("KX_FAST"); fast_env = e ? atoi(e) : 1; }
-    dp.fast = fast_env && !pb && !offsets && hprog.nsteps && hprog.sig_len == 3;
+    // concatenated: the fast index path; known offsets: the fast record measure (index) pass
+    dp.fast = fast_env && !pb && hprog.nsteps && (offsets || hprog.sig_len == 3);
   }
   for (uint32_t c = 0; c < hprog.ncols; c++) {
     const KxpCol& K = hprog.col[c];

@@ -154,6 +154,8 @@ struct Sink {
     for (uint32_t k = head; k < n; k++) base[off + k] = (uint8_t)(acc >> (8 * k));
     off += n; acc = 0; n = 0; head = 0;
   }
+  // the position of the next byte
+  __device__ __forceinline__ uint64_t pos() const { return off + n; }
 };
 
 __device__ __forceinline__ void put_be(Sink& s, uint64_t v, uint32_t w) {
@@ -199,9 +201,92 @@ __device__ __forceinline__ void put_bytes(Sink& s, const uint8_t* src, uint32_t 
   for (; done < len; done++) s.put(src[done], 1);
 }
 
+// ---- wave-cooperative payload copies (the direct write path) ----
+// A lane writing its record straight to HBM leaves the bulk of it -- list elements and long strings --
+// to its whole wave: it flushes its sink before the payload, queues (destination, source, count, element
+// width) in the wave's LDS queue and restarts the sink after it. The wave then copies every queued payload
+// with all 64 lanes: lane k assembles aligned output dword k of the payload's big-endian byte stream from
+// the (coalesced) source elements and stores it, so each store instruction writes 256 contiguous bytes
+// instead of one dword in each of 64 records. Edge dwords shared with the record's own bytes are written
+// byte by byte, so no store ever covers a byte another store writes.
+constexpr int QCAP = 128;            // queued payloads per wave (a full queue: the lane copies inline)
+constexpr uint32_t DEFER_MIN = 32;   // strings shorter than this stay in the lane's sink
+
+struct PayItem {
+  uint64_t dst;      // output position (absolute address)
+  uint64_t src;      // source elements (absolute address)
+  uint32_t n;        // elements
+  uint32_t w;        // element width (1: raw bytes, 2 / 4 / 8: big-endian scalars)
+};
+
+struct PayQueue {
+  PayItem* q;        // this wave's LDS queue (QCAP items)
+  uint32_t* cnt;     // LDS counter
+};
+
+// the aligned source dword i of a payload's big-endian byte stream (i < ceil(n * w / 4))
+__device__ __forceinline__ uint32_t be_stream_dword(const PayItem& it, uint64_t i) {
+  const uint64_t total = (uint64_t)it.n * it.w;
+  const uint64_t b = 4 * i;
+  if (b >= total) return 0u;
+  if (it.w == 8) {
+    const uint64_t v = ((const uint64_t*)it.src)[i >> 1];
+    return __builtin_bswap32((i & 1) ? (uint32_t)v : (uint32_t)(v >> 32));
+  }
+  if (it.w == 4) return __builtin_bswap32(((const uint32_t*)it.src)[i]);
+  if (it.w == 2) {
+    const uint32_t lo = ((const uint16_t*)it.src)[2 * i];
+    const uint32_t hi = b + 2 < total ? ((const uint16_t*)it.src)[2 * i + 1] : 0u;
+    return ((lo >> 8) | ((lo & 0xff) << 8)) | (((hi >> 8) | ((hi & 0xff) << 8)) << 16);
+  }
+  // raw bytes: the source may be unaligned; never read past its last byte's dword
+  const uint64_t a = it.src + b;
+  const uint64_t A = a & ~3ull, end = it.src + total;
+  const uint32_t x0 = *(const uint32_t*)A;
+  const uint32_t x1 = A + 4 < end ? *(const uint32_t*)(A + 4) : 0u;
+  return __builtin_amdgcn_alignbyte(x1, x0, (uint32_t)(a & 3));
+}
+
+__device__ __forceinline__ void wave_copy(const PayItem& it, int lane) {
+  const uint64_t total = (uint64_t)it.n * it.w;
+  if (!total) return;
+  const uint64_t d0 = it.dst, d1 = it.dst + total;
+  const uint64_t A0 = d0 & ~3ull;
+  const uint64_t nd = ((d1 + 3) & ~3ull) - A0 >> 2;            // output dwords touched
+  const uint32_t sh = (uint32_t)(d0 & 3);                       // stream byte p sits at output A0 + sh + p
+  for (uint64_t k = (uint64_t)lane; k < nd; k += 64) {
+    // output dword k = stream bytes [4k - sh, 4k - sh + 4)
+    uint32_t v;
+    if (sh == 0) {
+      v = be_stream_dword(it, k);
+    } else {
+      const uint32_t lo = k ? be_stream_dword(it, k - 1) : 0u;
+      const uint32_t hi = be_stream_dword(it, k);
+      v = __builtin_amdgcn_alignbyte(hi, lo, 4 - sh);
+    }
+    const uint64_t a = A0 + 4 * k;
+    if (a >= d0 && a + 4 <= d1) {
+      *(uint32_t*)a = v;
+    } else {
+      for (int j = 0; j < 4; j++)
+        if (a + j >= d0 && a + j < d1) *(uint8_t*)(a + j) = (uint8_t)(v >> (8 * j));
+    }
+  }
+}
+
+// queue a payload (false: the queue is full, the caller copies inline)
+__device__ __forceinline__ bool defer(const PayQueue& pq, uint64_t dst, const void* src, uint32_t n, uint32_t w) {
+  if (!pq.q) return false;
+  const uint32_t slot = atomicAdd(pq.cnt, 1u);
+  if (slot >= QCAP) return false;
+  pq.q[slot] = PayItem{dst, (uint64_t)src, n, w};
+  return true;
+}
+
 // FastWriteNocopy for one record into the sink
 template <bool LS>
-__device__ __forceinline__ void write_record(const KxProgram& P, const KxLaunchCols& C, uint64_t r, Sink& s) {
+__device__ __forceinline__ void write_record(const KxProgram& P, const KxLaunchCols& C, uint64_t r, Sink& s,
+                                             const PayQueue& pq) {
   uint64_t pres = C.presence ? C.presence[r] : 0;
   int inst = 0;
   int f = P.inst[0].enc_first;
@@ -226,13 +311,32 @@ __device__ __forceinline__ void write_record(const KxProgram& P, const KxLaunchC
       uint64_t o = off_at(C, F.col, r);
       uint32_t len = (uint32_t)var_len(C, F.col, r);
       put_be(s, len, 4);
-      put_bytes(s, (const uint8_t*)C.data[F.col] + o, len);
+      const uint8_t* src = (const uint8_t*)C.data[F.col] + o;
+      if (len >= DEFER_MIN && pq.q) {
+        const uint64_t at = s.pos();
+        if (defer(pq, (uint64_t)s.base + at, src, len, 1)) {
+          s.flush();
+          s = Sink(s.base, at + len);
+          f = F.enc_next;
+          continue;
+        }
+      }
+      put_bytes(s, src, len);
     } else if (F.kind == KXP_K_LIST) {
       uint64_t o = off_at(C, F.col, r);
       uint32_t cnt = (uint32_t)var_len(C, F.col, r);
       s.put(F.elem, 1);
       put_be(s, cnt, 4);
       const void* src = C.data[F.col];
+      if (cnt && pq.q && F.elem != KX_T_BOOL && F.width > 1) {
+        const uint64_t at = s.pos();
+        if (defer(pq, (uint64_t)s.base + at, (const uint8_t*)src + o * F.width, cnt, F.width)) {
+          s.flush();
+          s = Sink(s.base, at + (uint64_t)cnt * F.width);
+          f = F.enc_next;
+          continue;
+        }
+      }
 #if KX_ENC_LISTPF
       // blocks of 4 elements whose loads are all issued before the first is written (one memory round
       // trip per block instead of one per element, as put_bytes does for strings)
@@ -398,9 +502,10 @@ __device__ __forceinline__ uint64_t any_size(const EncParams& ep, const KxProgra
 }
 
 template <bool LS>
-__device__ __forceinline__ void any_write(const EncParams& ep, const KxProgram& P, uint64_t r, Sink& s) {
+__device__ __forceinline__ void any_write(const EncParams& ep, const KxProgram& P, uint64_t r, Sink& s,
+                                          const PayQueue& pq = PayQueue{nullptr, nullptr}) {
   if (ep.pb) pb_write_record(P, ep.cols, r, s);
-  else write_record<LS>(P, ep.cols, r, s);
+  else write_record<LS>(P, ep.cols, r, s, pq);
 }
 
 __device__ __forceinline__ uint64_t wave_incl_scan(uint64_t v, int lane) {
@@ -484,6 +589,10 @@ __global__ void __launch_bounds__(WT, KX_ENC_LB) write_kernel(EncParams ep) {
   uint32_t* progw = (uint32_t*)(smem_raw + OUTB + 32);
   uint64_t* scratch = (uint64_t*)(smem_raw + OUTB + 32 + sizeof(KxProgram));
   __shared__ uint64_t s_take, s_round_bytes;
+  __shared__ uint32_t qcnt[WT / 64];
+  // the direct path's payload queues live in the (then unused) LDS image
+  PayItem* qbase = (PayItem*)smem_raw;
+  static_assert((WT / 64) * QCAP * sizeof(PayItem) <= OUTB, "payload queues fit the image");
   if (ep.status->code != 0) return;                         // size limit: write nothing
   for (int i = threadIdx.x; i < (int)(sizeof(KxProgram) / 4); i += WT) progw[i] = ((const uint32_t*)ep.prog)[i];
   __syncthreads();
@@ -509,31 +618,27 @@ __global__ void __launch_bounds__(WT, KX_ENC_LB) write_kernel(EncParams ep) {
     __syncthreads();
     uint64_t take = s_take;
     const uint64_t cnt = kmin64((uint64_t)WT, rend - r);
-    if (take < (cnt >> KX_ENC_MINTAKE) || ep.direct) {
-      // large records (fewer than half of the round fit the image): every thread writes its record
-      // straight to HBM; its aligned dword stores still merge in L2
+    if (take < (cnt >> KX_ENC_MINTAKE) || take == 0 || ep.direct) {
+      // large records (fewer than half of the round fit the image, or one larger than the whole image):
+      // every lane writes its record straight to HBM, leaving list elements and long strings to its wave
+      // (wave_copy: coalesced loads, 256 contiguous bytes per store instruction)
+      const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+      if (lane == 0) qcnt[wv] = 0;
+      __builtin_amdgcn_wave_barrier();
+      const PayQueue pq{qbase + wv * QCAP, &qcnt[wv]};
       if (my < rend) {
         Sink s(ep.out, gpos + pre);
-        any_write<LS>(ep, P, my, s);
+        any_write<LS>(ep, P, my, s, ep.pb ? PayQueue{nullptr, nullptr} : pq);
         if (ep.offsets_out) ep.offsets_out[my] = gpos + pre;
       }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      const uint32_t nq = min(qcnt[wv], (uint32_t)QCAP);
+      for (uint32_t i = 0; i < nq; i++) wave_copy(qbase[wv * QCAP + i], lane);
       __syncthreads();
       gpos += tot;
       r += cnt;
-      continue;
-    }
-    if (take == 0) {
-      // a single record larger than the image: thread 0 writes it straight to HBM
-      if (threadIdx.x == 0) {
-        Sink s(ep.out, gpos);
-        any_write<LS>(ep, P, r, s);
-        if (ep.offsets_out) ep.offsets_out[r] = gpos;
-        s_round_bytes = sz;
-      }
-      __syncthreads();
-      gpos += s_round_bytes;
-      r += 1;
-      __syncthreads();
       continue;
     }
     if (threadIdx.x < take) {

@@ -401,3 +401,62 @@ def test_encode_containers_bit_exact(torch, dev, oracle, name):
 @pytest.mark.parametrize("case", DC.VIEW_CASES)
 def test_decode_views_match_oracle(gdec, oracle, case):
     DC.case_views(gdec, oracle, case)
+
+
+def _r2_with_big_strings(n, big, seed=0):
+    """R2 columns where a few records carry a huge string (the encoder's direct path and its
+    wave-cooperative payload copies), the rest 0..40-byte strings at arbitrary alignments"""
+    rng = np.random.default_rng(seed)
+    cs = synth.gen_r2(n, start=seed)
+    cols = list(cs.cols)
+    for c in (8, 9):
+        lens = rng.integers(0, 41, size=n)
+        for i, L in big.items():
+            if c == 8:
+                lens[i] = L
+        off = np.zeros(n + 1, np.uint32)
+        off[1:] = np.cumsum(lens)
+        cols[c] = (off, rng.integers(0, 256, size=max(1, int(off[-1])), dtype=np.uint8))
+    return synth.ColumnSet(cols, None, n)
+
+
+@pytest.mark.parametrize("big", [{5: 1 << 20}, {0: 8 << 20, 777: 1 << 20, 4999: 3000}])
+def test_encode_huge_strings_bit_exact(torch, dev, oracle, big):
+    """1 MiB and 8 MiB strings mixed into an R2 batch: bit-exact with the oracle, and decoded back"""
+    sch, cdc = codec("r2")
+    n = 5000
+    cs = _r2_with_big_strings(n, big, seed=len(big))
+    rc, wire, offs = oracle.encode(sch, cs)
+    assert rc == 0
+    got, goffs = cdc.Marshal(cs_to_device(torch, dev, cs))
+    assert np.array_equal(to_np(got), wire)
+    assert np.array_equal(to_np(goffs).astype(np.uint64), offs)
+
+
+@pytest.mark.parametrize("et,w", [(A.T_I64, 8), (A.T_I32, 4), (A.T_I16, 2), (A.T_DOUBLE, 8), (A.T_BYTE, 1)])
+def test_encode_long_lists_bit_exact(torch, dev, oracle, et, w):
+    """list<scalar> of 0..3000 elements (R3-like large records: direct path, lists copied by the wave
+    with every destination alignment), strings of 0..200 bytes between them"""
+    from kitex_amd.codec import ThriftCodec
+    sch = S.Schema(S.Struct("L", [S.Field(1, A.T_I32, "a"), S.Field(2, A.T_LIST, "v", elem=et),
+                                  S.Field(3, A.T_STRING, "s"), S.Field(4, A.T_LIST, "u", elem=A.T_I64)]))
+    cdc = ThriftCodec(sch)
+    n = 3000
+    rng = np.random.default_rng(w)
+    dt = {1: np.uint8, 2: np.int16, 4: np.int32, 8: np.int64}[w]
+    l1 = rng.integers(0, 3001, size=n)
+    l1[::7] = 0
+    o1 = np.zeros(n + 1, np.uint32); o1[1:] = np.cumsum(l1)
+    v1 = rng.integers(-(1 << 62), 1 << 62, size=max(1, int(o1[-1]))).astype(dt)
+    ls = rng.integers(0, 201, size=n)
+    os_ = np.zeros(n + 1, np.uint32); os_[1:] = np.cumsum(ls)
+    sd = rng.integers(0, 256, size=max(1, int(os_[-1])), dtype=np.uint8)
+    l2 = rng.integers(0, 9, size=n)
+    o2 = np.zeros(n + 1, np.uint32); o2[1:] = np.cumsum(l2)
+    v2 = rng.integers(-(1 << 62), 1 << 62, size=max(1, int(o2[-1]))).astype(np.int64)
+    cs = synth.ColumnSet([rng.integers(-9, 9, size=n).astype(np.int32), (o1, v1), (os_, sd), (o2, v2)], None, n)
+    rc, wire, offs = oracle.encode(sch, cs)
+    assert rc == 0
+    got, goffs = cdc.Marshal(cs_to_device(torch, dev, cs))
+    assert np.array_equal(to_np(got), wire)
+    assert np.array_equal(to_np(goffs).astype(np.uint64), offs)
