@@ -2090,6 +2090,9 @@ __device__ __forceinline__ bool fast_tile(KParams& dp, const Src& w, uint64_t tl
   //      tile past the dword grid) ----
   uint64_t c1 = X_NONE, c2 = X_NONE;
   {
+    // a hit whose second field header (at the plan's fixed offset) does not match is not a candidate:
+    // payload bytes saturated with the signature cost a few compares instead of failed walks
+    const uint32_t s2o = P->sig2_off, s2 = P->sig2;
     uint64_t hb = (uint64_t)hm | (lane == 63 ? (1ull << 32) : 0ull);   // lane 63 also looks at dword 32
     while (hb && c2 == X_NONE) {
       const int di = __ffsll((long long)hb) - 1;
@@ -2102,6 +2105,8 @@ __device__ __forceinline__ bool fast_tile(KParams& dp, const Src& w, uint64_t tl
         const uint64_t p = w.wpos + dq + first_hit(m);
         m &= m - 1;
         if (p < seg_lo || p >= plim) continue;
+        const uint32_t pq = (uint32_t)(p - w.wpos) + s2o;
+        if (s2o && pq + 8 <= (uint32_t)w.wlen && ((win_ld(w, pq) ^ s2) & 0xffffffu)) continue;
         if (c1 == X_NONE) c1 = p;
         else { c2 = p; break; }
       }

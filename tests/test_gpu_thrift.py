@@ -454,7 +454,8 @@ def test_encode_long_lists_bit_exact(torch, dev, oracle, et, w):
     l2 = rng.integers(0, 9, size=n)
     o2 = np.zeros(n + 1, np.uint32); o2[1:] = np.cumsum(l2)
     v2 = rng.integers(-(1 << 62), 1 << 62, size=max(1, int(o2[-1]))).astype(np.int64)
-    cs = synth.ColumnSet([rng.integers(-9, 9, size=n).astype(np.int32), (o1, v1), (os_, sd), (o2, v2)], None, n)
+    cs = synth.ColumnSet([rng.integers(-9, 9, size=n).astype(np.int32), (o1, v1), (os_, sd), (o2, v2)],
+                          np.zeros(n, np.uint64), n)   # containers: the schema has a presence word
     rc, wire, offs = oracle.encode(sch, cs)
     assert rc == 0
     got, goffs = cdc.Marshal(cs_to_device(torch, dev, cs))
