@@ -46,7 +46,10 @@ constexpr int WINB = TILE + HALO_MAX + 16;  // LDS window bytes allocated (+16 f
 constexpr int WINW = WINB / 4 + 4;       // window dwords (+ pad for the last aligned read pair)
 constexpr int WIN_LOADS = (WINB / 16 + 63) / 64;
 constexpr int GT = 64;                   // tiles per group (one group-scan lane per tile)
-constexpr int CT = 256, CW = CT / 64;    // chain pass: one workgroup, lane = group
+#ifndef KX_CT
+#define KX_CT 1024
+#endif
+constexpr int CT = KX_CT, CW = CT / 64;  // chain pass: one workgroup, lane = group (fewer serial rounds at 1024)
 
 constexpr uint64_t V48 = (1ull << 48) - 1;
 constexpr uint64_t X_ERR = V48;          // chain terminated by a decode error
