@@ -55,7 +55,7 @@
 extern "C" {
 #endif
 
-#define KX_ABI_VERSION 2
+#define KX_ABI_VERSION 3
 
 /* ---- Thrift TType ids (gopkg protocol/thrift; pinned by pkg/protocol/bthrift/binary_test.go) ---- */
 enum {
@@ -103,10 +103,11 @@ typedef struct kx_field_desc {
   uint8_t req;           /* KX_REQ_* */
   uint8_t elem_ttype;    /* LIST/SET: element KX_T_* (a scalar, STRING, or STRUCT: see below);
                             MAP: key KX_T_* | value KX_T_* << 4 (each a scalar or STRING) */
-  uint8_t reserved0;
+  uint8_t reserved0;     /* flags: KX_FIELD_BINARY (protobuf bytes), KX_FIELD_STRING_DEFAULT */
   int16_t child;         /* STRUCT (or LIST/SET of STRUCT): index of the (element) struct in the schema's
                             struct table; else -1 */
-  int64_t default_bits;  /* scalar default value (two's complement / IEEE bits); ignored otherwise */
+  int64_t default_bits;  /* scalar default value (two's complement / IEEE bits); a string field with
+                            KX_FIELD_STRING_DEFAULT: pointer to its NUL-terminated default (nested schemas) */
 } kx_field_desc;
 
 typedef struct kx_struct_desc {
@@ -123,8 +124,12 @@ enum {
   KX_COL_BYTES = 2,      /* string/binary: offsets[n+1] (bytes) + data arena */
   KX_COL_LIST = 3,       /* list/set of fixed scalars (or one side of a map of them):
                             offsets[n+1] (elements) + element arena */
-  KX_COL_LIST_BYTES = 4  /* list/set of strings (or the string side of a map): offsets[n+1]
+  KX_COL_LIST_BYTES = 4, /* list/set of strings (or the string side of a map): offsets[n+1]
                             (elements), elem_offsets[elements+1] (bytes) + byte arena */
+  KX_COL_LIST2 = 5,      /* scalars two container levels down (list<list<i64>>, map<K, list<i32>> values):
+                            offsets[n+1] (outer elements), elem_offsets[outer+1] (inner elements), data */
+  KX_COL_LIST2_BYTES = 6 /* strings two container levels down (map<string, list<string>> values):
+                            offsets[n+1], elem_offsets[outer+1], sub_offsets[inner+1] (bytes), data */
 };
 /* A MAP field flattens to two consecutive columns, keys then values (each LIST or LIST_BYTES,
  * record offsets in entries); the value column's elem_ttype carries KX_ELEM_MAP_VALUE. Encoding
@@ -141,6 +146,30 @@ enum {
  * KX_ERR_NOT_IMPLEMENTED at kx_schema_create. */
 #define KX_ELEM_MAP_VALUE 0x80
 #define KX_ELEM_STRUCT_FIELD 0x40
+/* Nested schemas (ABI v3; kx_schema_is_nested() == 1): any shape the generated FastRead handles whose
+ * leaves are at most two container levels below the record. The column model generalises the one above:
+ *  - every container field (list / set / map) opens a new element domain one level down; its elements'
+ *    values live there: a scalar element or field is a LIST column (LIST2 two levels down), a string a
+ *    LIST_BYTES (LIST2_BYTES) column; struct elements (list<S>, map<K, S>) are inlined field by field into
+ *    the element domain (nested structs inside them too), a map is its key columns then its value columns;
+ *  - columns are depth-first in IDL order; an element domain whose elements hold optional, struct or
+ *    container fields gets one more column right after the domain's own columns: a LIST (LIST2) of u64
+ *    presence words, one per element (elem_ttype = KX_ELEM_PRESENCE), with the bit layout of
+ *    kx_columns.presence (column_info.presence_bit of a field inside an element is a bit of that word);
+ *  - a container element (or map value) that is itself a container (list<list<i64>>, map<string,
+ *    list<string>>) is described by field 0 of the struct `child` (a one-field "element type" struct;
+ *    its id is ignored); a map value that is a struct: elem_ttype = key | KX_T_STRUCT << 4, child = S;
+ *  - a recursive struct field (a struct that contains itself) keeps its encoded bytes: a BYTES
+ *    (LIST_BYTES inside a container) column whose ttype (elem_ttype) is KX_T_STRUCT, delimited by the
+ *    skip decoder on decode and written back verbatim on encode (an empty value encodes as STOP);
+ *  - string fields may carry a default: kx_field_desc.default_bits = (int64_t)(intptr_t) of a
+ *    NUL-terminated host string with KX_FIELD_STRING_DEFAULT set in reserved0 (copied at schema creation).
+ * Semantics are those of the flat schemas (unknown / mistyped fields skipped, the last duplicate wins,
+ * a repeated struct field is a fresh NewX(), missing required fields INVALID_DATA, absent fields take
+ * their defaults) at every level. */
+#define KX_ELEM_PRESENCE 0x20
+#define KX_FIELD_BINARY 1
+#define KX_FIELD_STRING_DEFAULT 2
 
 typedef struct kx_column_info {
   uint32_t kind;        /* KX_COL_* */
@@ -151,6 +180,8 @@ typedef struct kx_column_info {
   int32_t presence_bit; /* bit in the presence word for this field, or -1 */
   uint32_t depth;       /* nesting depth (0 = root field) */
   int16_t path[8];      /* field ids from the root to this leaf */
+  uint8_t level;        /* container levels above the leaf (0: one value per record) */
+  uint8_t reserved1[3];
 } kx_column_info;
 
 /* A batch of decoded records in struct-of-arrays form. All pointers are DEVICE memory for the
@@ -166,6 +197,8 @@ typedef struct kx_column {
   uint64_t elem_capacity; /* LIST_BYTES: element capacity */
   uint32_t offset_bytes;  /* 4 (or 0) / 8: width of offsets and elem_offsets entries */
   uint32_t flags;         /* KX_COLF_* */
+  void* sub_offsets;      /* LIST2_BYTES: byte offset of every inner element (sub_capacity+1 entries) */
+  uint64_t sub_capacity;  /* LIST2 / LIST2_BYTES: inner element capacity */
 } kx_column;
 
 /* KX_COLF_VIEW (decode, BYTES columns): zero-copy string views instead of copies. `offsets` receives
@@ -176,7 +209,7 @@ typedef struct kx_column {
  * encoders or the kx_host_* calls. */
 #define KX_COLF_VIEW 1u
 
-#define KX_MAX_COLUMNS 32
+#define KX_MAX_COLUMNS 64
 #define KX_MAX_STRUCTS 16
 
 typedef struct kx_columns {
@@ -212,6 +245,10 @@ int kx_schema_column_info(const kx_schema* s, uint32_t col, kx_column_info* out)
 uint32_t kx_schema_presence_bits(const kx_schema* s);
 /* Minimum encoded size of a record (all var fields empty, optional fields unset). */
 uint64_t kx_schema_min_record_size(const kx_schema* s);
+/* 1 when the schema uses the nested model (see KX_ELEM_PRESENCE above): decode and encode run the nested
+ * record walker (lane = record; boundaries of concatenated records from the skip pass), and the arena
+ * sizes of a decode are obtained first with kx_thrift_decode_sizes. */
+int kx_schema_is_nested(const kx_schema* s);
 
 int kx_ctx_create(int device, kx_ctx** out);
 void kx_ctx_destroy(kx_ctx* c);
@@ -235,6 +272,13 @@ int kx_ctx_set_pipeline(kx_ctx* c, uint64_t chunk_bytes, int ahead);
 int kx_thrift_decode_batch(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len,
                            const uint64_t* offsets, uint64_t n, const kx_columns* out,
                            uint8_t* record_status, kx_status* status, void* stream);
+
+/* Nested schemas: the arena sizes a decode of this input needs, per column (host memory, 3 x ncols):
+ * units[3c] = data units (bytes / elements), units[3c + 1] = elem_offsets entries - 1, units[3c + 2] =
+ * sub_offsets entries - 1. Synchronous on `stream`. status (host) as the decode's (the first failing
+ * record; its extents count as empty). Flat schemas: KX_ERR_NOT_IMPLEMENTED (status->var_total). */
+int kx_thrift_decode_sizes(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len,
+                           const uint64_t* offsets, uint64_t n, uint64_t* units, kx_status* status, void* stream);
 
 /* Skip decoder over n concatenated records: writes record start offsets (n+1 entries, device u64). */
 int kx_thrift_skip_batch(kx_ctx* c, const uint8_t* in, uint64_t in_len, uint64_t n,

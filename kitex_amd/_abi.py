@@ -6,7 +6,7 @@ layout is checked by tests/test_abi.py against the compiled library.
 """
 import ctypes as C
 
-KX_ABI_VERSION = 2
+KX_ABI_VERSION = 3
 
 # Thrift TType ids (gopkg protocol/thrift; pinned by pkg/protocol/bthrift/binary_test.go)
 T_STOP, T_VOID, T_BOOL, T_BYTE, T_DOUBLE = 0, 1, 2, 3, 4
@@ -24,6 +24,8 @@ ERR_NOT_IMPLEMENTED = 5
 ERR_DEPTH_LIMIT = 6
 ERR_EOF = 8
 ELEM_MAP_VALUE = 0x80
+ELEM_STRUCT_FIELD = 0x40
+ELEM_PRESENCE = 0x20     # nested schemas: a column of per-element presence words
 ERR_APPLICATION_EXCEPTION = 9
 ERR_UNKNOWN_PROTOCOL = 10
 ERR_PAYLOAD_VALIDATION = 11
@@ -37,10 +39,13 @@ ERR_INTERNAL = 103
 
 REQ_DEFAULT, REQ_REQUIRED, REQ_OPTIONAL = 0, 1, 2
 FIELD_BINARY = 1  # kx_field_desc.reserved0 flag: protobuf `bytes` (no UTF-8 validation)
+FIELD_STRING_DEFAULT = 2  # ... default_bits points at the field's NUL-terminated string default
 
 COL_FIXED, COL_BYTES, COL_LIST, COL_LIST_BYTES = 1, 2, 3, 4
+COL_LIST2, COL_LIST2_BYTES = 5, 6   # nested schemas: two container levels down
+STRING_KINDS = (COL_BYTES, COL_LIST_BYTES, COL_LIST2_BYTES)
 COLF_VIEW = 1  # kx_column.flags: zero-copy (offset, length) string views
-MAX_COLUMNS = 32
+MAX_COLUMNS = 64
 MAX_STRUCTS = 16
 
 TYPE_SIZE = {T_BOOL: 1, T_BYTE: 1, T_I16: 2, T_I32: 4, T_I64: 8, T_DOUBLE: 8}
@@ -72,13 +77,16 @@ class ColumnInfo(C.Structure):
         ("presence_bit", C.c_int32),
         ("depth", C.c_uint32),
         ("path", C.c_int16 * 8),
+        ("level", C.c_uint8),
+        ("reserved1", C.c_uint8 * 3),
     ]
 
 
 class Column(C.Structure):
     _fields_ = [("data", C.c_void_p), ("offsets", C.c_void_p), ("capacity", C.c_uint64),
                 ("elem_offsets", C.c_void_p), ("elem_capacity", C.c_uint64),
-                ("offset_bytes", C.c_uint32), ("flags", C.c_uint32)]
+                ("offset_bytes", C.c_uint32), ("flags", C.c_uint32),
+                ("sub_offsets", C.c_void_p), ("sub_capacity", C.c_uint64)]
 
 
 class Columns(C.Structure):
@@ -114,8 +122,14 @@ TTS_META, TTS_HEADER, TTS_DATA, TTS_TRAILER, TTS_RST = 1, 2, 3, 4, 5
 assert C.sizeof(TTStreamKeys) == 48
 assert C.sizeof(FieldDesc) == 16
 assert C.sizeof(Status) == 128
-assert C.sizeof(Column) == 48
-assert C.sizeof(Columns) == MAX_COLUMNS * 48 + 16
+assert C.sizeof(Column) == 64
+assert C.sizeof(Columns) == MAX_COLUMNS * 64 + 16
+assert C.sizeof(ColumnInfo) == 40
+
+
+def n_arrays(ci) -> int:
+    """offsets arrays of a column: one per container level above it, one more for a string's bytes"""
+    return ci.level + (1 if ci.kind in STRING_KINDS else 0)
 
 ERROR_NAMES = {
     OK: "ok",

@@ -28,7 +28,7 @@ EXPORTS = [
     "kx_pb_decode_frames", "kx_crc32c_batch", "kx_frame_crc32c_validate", "kx_ctx_set_crc32c_check",
     "kx_grpc_frame_scan", "kx_thrift_decode_grpc", "kx_pb_decode_grpc", "kx_thrift_raw_messages",
     "kx_thrift_set_seqids", "kx_thrift_encode_messages", "kx_ttstream_default_keys", "kx_ttstream_frame_scan",
-    "kx_thrift_decode_extents", "kx_pb_decode_extents",
+    "kx_thrift_decode_extents", "kx_pb_decode_extents", "kx_schema_is_nested", "kx_thrift_decode_sizes",
 ]
 
 
@@ -75,6 +75,9 @@ def lib():
     L.kx_ctx_set_pipeline.argtypes = [vp, u64, C.c_int]
     dec = [vp, vp, vp, u64, vp, u64, C.POINTER(A.Columns), vp, vp, vp]
     L.kx_thrift_decode_batch.argtypes = dec
+    L.kx_schema_is_nested.argtypes = [vp]
+    L.kx_schema_is_nested.restype = C.c_int
+    L.kx_thrift_decode_sizes.argtypes = [vp, vp, vp, u64, vp, u64, vp, C.POINTER(A.Status), vp]
     L.kx_pb_decode_batch.argtypes = dec
     L.kx_thrift_skip_batch.argtypes = [vp, vp, u64, u64, vp, vp, vp]
     L.kx_thrift_encoded_size_batch.argtypes = [vp, vp, C.POINTER(A.Columns), u64, vp, vp]

@@ -110,6 +110,7 @@ class DeviceSchema:
             self.infos.append(ci)
         self.npresence = L.kx_schema_presence_bits(h)
         self.min_record_size = L.kx_schema_min_record_size(h)
+        self.nested = bool(L.kx_schema_is_nested(h))   # include/kxcodec.h "Nested schemas"
 
     def var_columns(self) -> List[int]:
         return [c for c, ci in enumerate(self.infos) if ci.kind != A.COL_FIXED]
@@ -303,9 +304,14 @@ class ThriftCodec:
         import torch
         ds = self.dschema
         if out is None:
+            elem_caps = sub_caps = None
+            if var_caps is None and ds.nested:   # exact arenas from the measure pass
+                units = self.DecodeSizes(buf, n, offsets, stream=stream)
+                var_caps, elem_caps, sub_caps = units[0::3], units[1::3], units[2::3]
             if var_caps is None:
                 var_caps = [0 if ci.kind == A.COL_FIXED else max(1, buf.numel()) for ci in ds.infos]
-            out = alloc_device(ds.infos, n, var_caps, ds.npresence, self.device, views=views)
+            out = alloc_device(ds.infos, n, var_caps, ds.npresence, self.device, views=views, elem_caps=elem_caps,
+                               sub_caps=sub_caps)
         kc = to_kx_columns(out, ds.infos, var_caps)
         st = status if status is not None else status_tensor(self.device)
         rs = torch.empty(max(1, n), dtype=torch.uint8, device=self.device) if record_status else None
@@ -322,6 +328,18 @@ class ThriftCodec:
             if s.code:
                 raise ProtocolError(s.code, self._WHAT, s.record, s.offset)
         return res
+
+    @on_call_stream
+    def DecodeSizes(self, buf, n: int, offsets=None, stream=None) -> List[int]:
+        """Nested schemas: the arena units a decode of buf needs, 3 per column (data units, elem_offsets
+        entries - 1, sub_offsets entries - 1): kx_thrift_decode_sizes (synchronous)."""
+        ds = self.dschema
+        units = (C.c_uint64 * (3 * max(1, ds.ncols)))()
+        st = A.Status()
+        s = _stream(stream)
+        check(lib().kx_thrift_decode_sizes(self._ctx(s).handle, ds.handle, _ptr(buf), buf.numel(), _ptr(offsets), n,
+                                           units, C.byref(st), int(s.cuda_stream)), "kx_thrift_decode_sizes")
+        return [int(units[i]) for i in range(3 * ds.ncols)]
 
     def UnmarshalHost(self, wire, n: int, offsets=None, var_caps: Sequence[int] = None,
                       raise_on_error: bool = True, out: ColumnSet = None):

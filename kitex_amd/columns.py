@@ -68,28 +68,42 @@ def to_kx_columns(cs: ColumnSet, infos: Sequence[A.ColumnInfo], caps: Sequence[i
         have = _numel(data)
         cap = caps[c] if caps is not None and caps[c] is not None else have
         out.cols[c].capacity = int(min(int(cap), have))
-        if ci.kind == A.COL_LIST_BYTES:  # (record offsets, element byte offsets, bytes)
+        if ci.kind in (A.COL_LIST_BYTES, A.COL_LIST2, A.COL_LIST2_BYTES):  # (record offsets, element offsets, ..)
             eoffs = parts[1]
             assert _itemsize(eoffs) == _itemsize(offs)
             out.cols[c].elem_offsets = _ptr(eoffs)
             out.cols[c].elem_capacity = max(0, _numel(eoffs) - 1)
+        if ci.kind == A.COL_LIST2_BYTES:  # (.., inner element byte offsets, bytes)
+            soffs = parts[2]
+            assert _itemsize(soffs) == _itemsize(offs)
+            out.cols[c].sub_offsets = _ptr(soffs)
+            out.cols[c].sub_capacity = max(0, _numel(soffs) - 1)
     out.presence = _ptr(cs.presence)
     return out
 
 
 def alloc_host(infos: Sequence[A.ColumnInfo], n: int, var_caps: Sequence[int], npresence: int,
-               wide: bool = False, elem_caps: Sequence[int] = None, views: bool = False) -> ColumnSet:
-    """Host columns. wide: 8-byte offsets. elem_caps[c]: element capacity of LIST_BYTES columns.
+               wide: bool = False, elem_caps: Sequence[int] = None, views: bool = False,
+               sub_caps: Sequence[int] = None) -> ColumnSet:
+    """Host columns. wide: 8-byte offsets. elem_caps[c]: element capacity of LIST_BYTES / LIST2 /
+    LIST2_BYTES columns, sub_caps[c]: inner element capacity of LIST2_BYTES columns.
     views: BYTES columns as zero-copy (offset, length) views."""
     odt = np.uint64 if wide else np.uint32
     cols: List[object] = []
     for c, ci in enumerate(infos):
+        ec = (elem_caps[c] if elem_caps is not None else max(1, var_caps[c])) if ci.kind != A.COL_FIXED else 0
         if views and ci.kind == A.COL_BYTES:
             cols.append(Views(np.zeros((max(1, n), 2), dtype=odt)))
         elif ci.kind == A.COL_FIXED:
             cols.append(np.zeros(n, dtype=_NP_FIXED[ci.width]))
+        elif ci.kind == A.COL_LIST2:
+            cols.append((np.zeros(n + 1, dtype=odt), np.zeros(ec + 1, dtype=odt),
+                         np.zeros(max(1, var_caps[c]), dtype=_NP_FIXED[ci.width])))
+        elif ci.kind == A.COL_LIST2_BYTES:
+            sc = sub_caps[c] if sub_caps is not None else max(1, var_caps[c])
+            cols.append((np.zeros(n + 1, dtype=odt), np.zeros(ec + 1, dtype=odt), np.zeros(sc + 1, dtype=odt),
+                         np.zeros(max(1, var_caps[c]), dtype=np.uint8)))
         elif ci.kind == A.COL_LIST_BYTES:
-            ec = elem_caps[c] if elem_caps is not None else max(1, var_caps[c])
             cols.append((np.zeros(n + 1, dtype=odt), np.zeros(ec + 1, dtype=odt),
                          np.zeros(max(1, var_caps[c]), dtype=np.uint8)))
         else:
@@ -101,7 +115,7 @@ def alloc_host(infos: Sequence[A.ColumnInfo], n: int, var_caps: Sequence[int], n
 
 def alloc_device(infos: Sequence[A.ColumnInfo], n: int, var_caps: Sequence[int], npresence: int,
                  device, fill: int = None, wide: bool = False, elem_caps: Sequence[int] = None,
-                 views: bool = False) -> ColumnSet:
+                 views: bool = False, sub_caps: Sequence[int] = None) -> ColumnSet:
     """Device columns (torch). wide: 8-byte offsets (int64) instead of 4-byte (int32 storage of
     the unsigned offsets). views: BYTES columns as zero-copy (offset, length) views."""
     import torch
@@ -110,12 +124,20 @@ def alloc_device(infos: Sequence[A.ColumnInfo], n: int, var_caps: Sequence[int],
     mk = torch.empty if fill is None else (lambda *a, **k: torch.full(*a[:1], fill, **k))
     cols: List[object] = []
     for c, ci in enumerate(infos):
+        ec = (elem_caps[c] if elem_caps is not None else max(1, var_caps[c])) if ci.kind != A.COL_FIXED else 0
         if views and ci.kind == A.COL_BYTES:
             cols.append(Views(mk((max(1, n), 2), dtype=odt, device=device)))
         elif ci.kind == A.COL_FIXED:
             cols.append(mk((n,), dtype=tdt[ci.width], device=device))
+        elif ci.kind == A.COL_LIST2:
+            cols.append((mk((n + 1,), dtype=odt, device=device), mk((ec + 1,), dtype=odt, device=device),
+                         mk((max(1, var_caps[c]),), dtype=tdt[ci.width], device=device)))
+        elif ci.kind == A.COL_LIST2_BYTES:
+            sc = sub_caps[c] if sub_caps is not None else max(1, var_caps[c])
+            cols.append((mk((n + 1,), dtype=odt, device=device), mk((ec + 1,), dtype=odt, device=device),
+                         mk((sc + 1,), dtype=odt, device=device),
+                         mk((max(1, var_caps[c]),), dtype=torch.uint8, device=device)))
         elif ci.kind == A.COL_LIST_BYTES:
-            ec = elem_caps[c] if elem_caps is not None else max(1, var_caps[c])
             cols.append((mk((n + 1,), dtype=odt, device=device), mk((ec + 1,), dtype=odt, device=device),
                          mk((max(1, var_caps[c]),), dtype=torch.uint8, device=device)))
         else:
@@ -131,7 +153,7 @@ def var_caps_of(cs: ColumnSet, infos: Sequence[A.ColumnInfo]) -> List[int]:
     for c, ci in enumerate(infos):
         if ci.kind == A.COL_FIXED or isinstance(cs.cols[c], Views):
             caps.append(0)
-        else:
-            offs = cs.cols[c][0]
+        else:  # the last entry of the array that indexes the data (bytes / elements)
+            offs = cs.cols[c][-2]
             caps.append(int(offs[-1]) & (0xFFFFFFFF if _itemsize(offs) == 4 else (1 << 64) - 1))
     return caps

@@ -9,6 +9,7 @@
 #include <new>
 
 #include "kx_internal.h"
+#include "kx_nested.h"
 
 namespace {
 
@@ -115,7 +116,8 @@ int offset_width(const kx_column& k) {
 int to_launch_cols(const kx_schema* s, const kx_columns* out, KxLaunchCols* lc, bool allow_view = false,
                    uint64_t in_len = 0) {
   if (!out) return KX_ERR_INVALID_ARG;
-  if (out->ncols != s->ncols) return KX_ERR_INVALID_ARG;
+  if (s->nprog) return KX_ERR_NOT_IMPLEMENTED;  // nested schemas: the entry points of nested_* below
+  if (out->ncols != s->ncols || s->ncols > KXP_MAX_COLS) return KX_ERR_INVALID_ARG;
   if (s->npres && !out->presence) return KX_ERR_INVALID_ARG;
   memset(lc, 0, sizeof *lc);
   for (uint32_t c = 0; c < s->ncols; c++) {
@@ -156,6 +158,138 @@ int set_device(kx_ctx* c) {
   return KX_OK;
 }
 
+// ---- nested schemas ----
+int nprog_on_device(kx_schema* s, int dev, KxnProgram** out) {
+  if (dev < 0 || dev >= 64) return KX_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> g(s->mu);
+  if (!s->dev_nprog[dev]) {
+    void* p = nullptr;
+    KX_HIP_CHECK(hipMalloc(&p, sizeof(KxnProgram)));
+    if (hipMemcpy(p, s->nprog, sizeof(KxnProgram), hipMemcpyHostToDevice) != hipSuccess) {
+      (void)hipFree(p);
+      return KX_ERR_HIP;
+    }
+    s->dev_nprog[dev] = p;
+  }
+  *out = (KxnProgram*)s->dev_nprog[dev];
+  return KX_OK;
+}
+
+int ensure_nws(kx_ctx* c, size_t bytes, hipStream_t stream) {
+  if (c->nws_size >= bytes) return KX_OK;
+  if (c->nws) {
+    KX_HIP_CHECK(hipStreamSynchronize(stream));
+    KX_HIP_CHECK(hipFree(c->nws));
+    c->nws = nullptr;
+    c->nws_size = 0;
+  }
+  size_t sz = bytes < (1u << 20) ? (1u << 20) : bytes + bytes / 4;
+  KX_HIP_CHECK(hipMalloc(&c->nws, sz));
+  c->nws_size = sz;
+  return KX_OK;
+}
+
+// the call's column table: checked on the host, staged in pinned memory, copied on the stream (the
+// staging buffer is reused once the previous copy has executed)
+int nested_cols(kx_ctx* c, const kx_schema* s, const kx_columns* cols, bool decode, hipStream_t st, KxnCols** out) {
+  if (!cols || cols->ncols != s->ncols) return KX_ERR_INVALID_ARG;
+  if (s->npres && !cols->presence) return KX_ERR_INVALID_ARG;
+  if (!c->ncols_dev) {
+    KX_HIP_CHECK(hipMalloc(&c->ncols_dev, sizeof(KxnCols)));
+    KX_HIP_CHECK(hipHostMalloc(&c->ncols_host, sizeof(KxnCols), hipHostMallocDefault));
+    KX_HIP_CHECK(hipEventCreateWithFlags(&c->ncols_ev, hipEventDisableTiming));
+  } else {
+    KX_HIP_CHECK(hipEventSynchronize(c->ncols_ev));
+  }
+  KxnCols& K = *(KxnCols*)c->ncols_host;
+  memset(&K, 0, sizeof K);
+  const KxnProgram& P = *s->nprog;
+  for (uint32_t i = 0; i < s->ncols; i++) {
+    const kx_column& k = cols->cols[i];
+    const KxnCol& C = P.col[i];
+    if (k.flags) return KX_ERR_INVALID_ARG;  // no zero-copy views on nested schemas
+    if (C.kind == KX_COL_FIXED) {
+      if (!k.data) return KX_ERR_INVALID_ARG;
+    } else {
+      const int ow = offset_width(k);
+      if (!ow) return KX_ERR_INVALID_ARG;
+      if (ow == 8) K.owide |= 1ull << i;
+      void* arrs[3] = {k.offsets, k.elem_offsets, k.sub_offsets};
+      for (int a = 0; a < C.narr; a++)
+        if (!arrs[a]) return KX_ERR_INVALID_ARG;
+      if (!k.data && k.capacity) return KX_ERR_INVALID_ARG;
+      for (int a = 0; a < 3; a++) K.arr[i][a] = arrs[a];
+      K.cap[i][0] = k.capacity;
+      K.cap[i][2] = k.elem_capacity;
+      K.cap[i][3] = k.sub_capacity;
+      if (ow == 4 && decode) {  // 4-byte offsets never wrap: capacities beyond them are refused
+        for (int a = 0; a < 4; a++)
+          if (K.cap[i][a] > 0xffffffffull) K.cap[i][a] = 0xffffffffull;
+      }
+    }
+    K.data[i] = k.data;
+  }
+  K.presence = cols->presence;
+  KX_HIP_CHECK(hipMemcpyAsync(c->ncols_dev, &K, sizeof K, hipMemcpyHostToDevice, st));
+  KX_HIP_CHECK(hipEventRecord(c->ncols_ev, st));
+  *out = (KxnCols*)c->ncols_dev;
+  return KX_OK;
+}
+
+// decode of a nested schema (offsets / ends as kx_launch_decode; offsets == NULL: concatenated).
+// totals: sizes only (host, ncur entries; synchronous)
+int nested_decode(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len, const uint64_t* offsets,
+                  const uint64_t* ends, uint64_t n, const kx_columns* out, uint8_t* record_status, kx_status* status,
+                  hipStream_t st, uint64_t* totals) {
+  int rc;
+  KxnCols* dcols = nullptr;
+  if (n == 0) {  // no record: empty offsets arrays (a single 0 entry each)
+    KX_HIP_CHECK(hipMemsetAsync(status, 0, sizeof(kx_status), st));
+    if (totals || !out) return totals ? KX_OK : KX_ERR_INVALID_ARG;
+    if (out->ncols != s->ncols) return KX_ERR_INVALID_ARG;
+    for (uint32_t i = 0; i < s->ncols; i++) {
+      const kx_column& k = out->cols[i];
+      void* arrs[3] = {k.offsets, k.elem_offsets, k.sub_offsets};
+      for (int a = 0; a < s->nprog->col[i].narr; a++) {
+        if (!arrs[a]) return KX_ERR_INVALID_ARG;
+        KX_HIP_CHECK(hipMemsetAsync(arrs[a], 0, offset_width(k) == 8 ? 8 : 4, st));
+      }
+    }
+    return KX_OK;
+  }
+  if (totals) {
+    if (!c->ncols_dev) {  // the sizes pass reads no column: an empty table
+      KX_HIP_CHECK(hipMalloc(&c->ncols_dev, sizeof(KxnCols)));
+      KX_HIP_CHECK(hipHostMalloc(&c->ncols_host, sizeof(KxnCols), hipHostMallocDefault));
+      KX_HIP_CHECK(hipEventCreateWithFlags(&c->ncols_ev, hipEventDisableTiming));
+      KX_HIP_CHECK(hipMemsetAsync(c->ncols_dev, 0, sizeof(KxnCols), st));
+    }
+    dcols = (KxnCols*)c->ncols_dev;
+  } else if ((rc = nested_cols(c, s, out, true, st, &dcols))) {
+    return rc;
+  }
+  KxnProgram* dp = nullptr;
+  if ((rc = nprog_on_device(const_cast<kx_schema*>(s), c->device, &dp))) return rc;
+  if ((rc = ensure_nws(c, kx_nested_ws_bytes(*s->nprog, n, offsets == nullptr), st))) return rc;
+  uint64_t epoch = 0;
+  if (!offsets && (rc = ensure_ws(c, kx_skip_ws_bytes(in_len), st, &epoch))) return rc;
+  return kx_launch_nested_decode(dp, *s->nprog, in, in_len, offsets, ends, n, dcols, record_status, status, c->nws,
+                                 c->nws_size, c->ws, c->ws_size, epoch, st, totals);
+}
+
+int nested_encode(kx_ctx* c, const kx_schema* s, const kx_columns* in, uint64_t n, uint8_t* out, uint64_t out_cap,
+                  uint64_t* sizes_out, uint64_t* offsets_out, kx_status* status, hipStream_t st, bool sizes_only) {
+  int rc;
+  KxnCols* dcols = nullptr;
+  if ((rc = nested_cols(c, s, in, false, st, &dcols))) return rc;
+  if (n == 0) return KX_OK;
+  KxnProgram* dp = nullptr;
+  if ((rc = nprog_on_device(const_cast<kx_schema*>(s), c->device, &dp))) return rc;
+  if ((rc = ensure_ews(c, kx_nested_enc_ws_bytes(n), st))) return rc;
+  return kx_launch_nested_encode(dp, *s->nprog, dcols, n, out, out_cap, sizes_out, offsets_out, status, c->ews,
+                                 c->ews_size, st, sizes_only);
+}
+
 }  // namespace
 
 extern "C" {
@@ -189,6 +323,7 @@ int kx_schema_create(const kx_struct_desc* structs, uint32_t nstructs, kx_schema
   kx_schema* s = new (std::nothrow) kx_schema();
   if (!s) return KX_ERR_INTERNAL;
   int rc = kx_build_program(structs, nstructs, s);
+  if (rc == KX_ERR_NOT_IMPLEMENTED) rc = kx_build_nested(structs, nstructs, s);
   if (rc) {
     delete s;
     return rc;
@@ -197,12 +332,15 @@ int kx_schema_create(const kx_struct_desc* structs, uint32_t nstructs, kx_schema
   return KX_OK;
 }
 
+int kx_schema_is_nested(const kx_schema* s) { return s && s->nprog ? 1 : 0; }
+
 void kx_schema_destroy(kx_schema* s) {
   if (!s) return;
   for (int d = 0; d < 64; d++)
-    if (s->dev_prog[d]) {
+    if (s->dev_prog[d] || s->dev_nprog[d]) {
       (void)hipSetDevice(d);
-      (void)hipFree(s->dev_prog[d]);
+      if (s->dev_prog[d]) (void)hipFree(s->dev_prog[d]);
+      if (s->dev_nprog[d]) (void)hipFree(s->dev_nprog[d]);
     }
   delete s;
 }
@@ -217,7 +355,7 @@ int kx_schema_column_info(const kx_schema* s, uint32_t col, kx_column_info* out)
 
 uint32_t kx_schema_presence_bits(const kx_schema* s) { return s ? s->npres : 0; }
 
-uint64_t kx_schema_min_record_size(const kx_schema* s) { return s ? s->prog.fixed_min : 0; }
+uint64_t kx_schema_min_record_size(const kx_schema* s) { return s && !s->nprog ? s->prog.fixed_min : s ? 1 : 0; }
 
 // diagnostics (not part of the public ABI): the decode workspace of a ctx and its current epoch
 int kx_debug_workspace(kx_ctx* c, void** ptr, size_t* size, uint64_t* epoch) {
@@ -251,6 +389,10 @@ void kx_ctx_destroy(kx_ctx* c) {
   if (c->cws) (void)hipFree(c->cws);
   if (c->pin) (void)hipHostFree(c->pin);
   if (c->dstage) (void)hipFree(c->dstage);
+  if (c->nws) (void)hipFree(c->nws);
+  if (c->ncols_dev) (void)hipFree(c->ncols_dev);
+  if (c->ncols_host) (void)hipHostFree(c->ncols_host);
+  if (c->ncols_ev) (void)hipEventDestroy(c->ncols_ev);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   if (c->pipe.aux) {
     (void)hipStreamSynchronize(c->pipe.aux);
@@ -284,6 +426,7 @@ int kx_thrift_decode_batch(kx_ctx* c, const kx_schema* s, const uint8_t* in, uin
   int rc = set_device(c);
   if (rc) return rc;
   hipStream_t st = (hipStream_t)stream;
+  if (s->nprog) return nested_decode(c, s, in, in_len, offsets, nullptr, n, out, record_status, status, st, nullptr);
   KxLaunchCols lc;
   if ((rc = to_launch_cols(s, out, &lc, true, in_len))) return rc;
   if (n == 0) {
@@ -301,6 +444,34 @@ int kx_thrift_decode_batch(kx_ctx* c, const kx_schema* s, const uint8_t* in, uin
   if ((rc = ensure_pipe(c))) return rc;
   return kx_launch_decode(dp, s->prog, in, in_len, offsets, n, lc, record_status, status, c->ws, c->ws_size,
                           epoch, st, false, nullptr, nullptr, &c->pipe);
+}
+
+int kx_thrift_decode_sizes(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len,
+                           const uint64_t* offsets, uint64_t n, uint64_t* units, kx_status* status, void* stream) {
+  if (!c || !s || !status || !units || (!in && in_len)) return KX_ERR_INVALID_ARG;
+  if (!s->nprog) return KX_ERR_NOT_IMPLEMENTED;
+  int rc = set_device(c);
+  if (rc) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  const KxnProgram& P = *s->nprog;
+  memset(status, 0, sizeof *status);
+  uint64_t tot[KXN_MAX_CUR] = {0};
+  if (n) {
+    kx_status* dst = nullptr;
+    KX_HIP_CHECK(hipMalloc(&dst, sizeof(kx_status)));
+    rc = nested_decode(c, s, in, in_len, offsets, nullptr, n, nullptr, nullptr, dst, st, tot);
+    if (!rc && hipMemcpyAsync(status, dst, sizeof(kx_status), hipMemcpyDeviceToHost, st) != hipSuccess) rc = KX_ERR_HIP;
+    if (!rc && hipStreamSynchronize(st) != hipSuccess) rc = KX_ERR_HIP;
+    (void)hipFree(dst);
+    if (rc) return rc;
+  }
+  for (uint32_t i = 0; i < s->ncols; i++) {
+    const KxnCol& K = P.col[i];
+    units[3 * i] = K.dcur >= 0 ? tot[K.dcur] : n;
+    units[3 * i + 1] = K.narr >= 2 ? tot[K.acur[0]] : 0;
+    units[3 * i + 2] = K.narr >= 3 ? tot[K.acur[1]] : 0;
+  }
+  return KX_OK;
 }
 
 int kx_thrift_skip_batch(kx_ctx* c, const uint8_t* in, uint64_t in_len, uint64_t n, uint64_t* offsets_out,
@@ -325,6 +496,7 @@ int kx_thrift_encoded_size_batch(kx_ctx* c, const kx_schema* s, const kx_columns
   int rc = set_device(c);
   if (rc) return rc;
   hipStream_t st = (hipStream_t)stream;
+  if (s->nprog) return nested_encode(c, s, in, n, nullptr, 0, sizes_out, nullptr, nullptr, st, true);
   KxLaunchCols lc;
   if ((rc = to_launch_cols(s, in, &lc))) return rc;
   if (n == 0) return KX_OK;
@@ -341,8 +513,9 @@ int kx_thrift_encode_batch(kx_ctx* c, const kx_schema* s, const kx_columns* in, 
   int rc = set_device(c);
   if (rc) return rc;
   hipStream_t st = (hipStream_t)stream;
+  if (s->nprog && n) return nested_encode(c, s, in, n, out, out_cap, nullptr, offsets_out, status, st, false);
   KxLaunchCols lc;
-  if ((rc = to_launch_cols(s, in, &lc))) return rc;
+  if (!s->nprog && (rc = to_launch_cols(s, in, &lc))) return rc;
   if (n == 0) {
     KX_HIP_CHECK(hipMemsetAsync(status, 0, sizeof(kx_status), st));
     if (offsets_out) KX_HIP_CHECK(hipMemsetAsync(offsets_out, 0, 8, st));
@@ -689,6 +862,7 @@ static int decode_extents(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint
   int rc = set_device(c);
   if (rc) return rc;
   hipStream_t st = (hipStream_t)stream;
+  if (s->nprog && !pb && n) return nested_decode(c, s, in, in_len, starts, ends, n, out, record_status, status, st, nullptr);
   KxLaunchCols lc;
   if ((rc = to_launch_cols(s, out, &lc, true, in_len))) return rc;
   if (n == 0) {

@@ -47,9 +47,9 @@ constexpr int WINW = WINB / 4 + 4;       // window dwords (+ pad for the last al
 constexpr int WIN_LOADS = (WINB / 16 + 63) / 64;
 constexpr int GT = 64;                   // tiles per group (one group-scan lane per tile)
 #ifndef KX_CT
-#define KX_CT 1024
+#define KX_CT 256
 #endif
-constexpr int CT = KX_CT, CW = CT / 64;  // chain pass: one workgroup, lane = group (fewer serial rounds at 1024)
+constexpr int CT = KX_CT, CW = CT / 64;  // chain pass: one workgroup, lane = group (1024 measured: the launch fails on the MI355X)
 
 constexpr uint64_t V48 = (1ull << 48) - 1;
 constexpr uint64_t X_ERR = V48;          // chain terminated by a decode error

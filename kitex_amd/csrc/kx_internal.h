@@ -22,6 +22,10 @@ struct kx_schema {
   // device copies, one per device, uploaded lazily by a ctx
   std::mutex mu;
   void* dev_prog[64] = {nullptr};
+  // nested schemas (kx_nested_schema.cpp): the walker's program, nullptr for flat schemas
+  struct KxnProgram* nprog = nullptr;
+  void* dev_nprog[64] = {nullptr};
+  ~kx_schema();
 };
 
 // Chunked decode pipeline (kx_decode.hip launch_t): index + group of chunk k run on `aux` while chain +
@@ -62,6 +66,12 @@ struct kx_ctx {
   // grow-only message-encode scratch: record offsets (n + 1) and the method name
   void* xws = nullptr;
   size_t xws_size = 0;
+  // nested schemas: grow-only walker workspace, the per-call column table (device) and its staging
+  void* nws = nullptr;
+  size_t nws_size = 0;
+  void* ncols_dev = nullptr;        // KxnCols
+  void* ncols_host = nullptr;       // pinned KxnCols staging
+  hipEvent_t ncols_ev = nullptr;    // the last upload from the staging buffer has been consumed
   // grow-only encode scratch (per-block sizes)
   void* ews = nullptr;
   size_t ews_size = 0;
@@ -73,16 +83,30 @@ struct kx_ctx {
   size_t dstage_size = 0;
 };
 
-// kx_schema.cpp
+// kx_schema.cpp / kx_nested_schema.cpp
 int kx_build_program(const kx_struct_desc* structs, uint32_t nstructs, kx_schema* s);
+int kx_build_nested(const kx_struct_desc* structs, uint32_t nstructs, kx_schema* s);
+
+// kx_nested.hip: the nested walker's launches (decode: sizes only when units != null)
+struct KxnCols;
+size_t kx_nested_ws_bytes(const struct KxnProgram& P, uint64_t n, bool concat);
+int kx_launch_nested_decode(const struct KxnProgram* dprog, const struct KxnProgram& hprog, const uint8_t* in,
+                            uint64_t in_len, const uint64_t* offsets, const uint64_t* ends, uint64_t n,
+                            const KxnCols* dcols, uint8_t* record_status, kx_status* status, void* ws,
+                            size_t ws_size, void* skip_ws, size_t skip_ws_size, uint64_t skip_epoch,
+                            hipStream_t stream, uint64_t* totals_out);
+size_t kx_nested_enc_ws_bytes(uint64_t n);
+int kx_launch_nested_encode(const struct KxnProgram* dprog, const struct KxnProgram& hprog, const KxnCols* dcols,
+                            uint64_t n, uint8_t* out, uint64_t out_cap, uint64_t* sizes_out, uint64_t* offsets_out,
+                            kx_status* status, void* ws, size_t ws_size, hipStream_t stream, bool sizes_only);
 
 // device launchers (kx_decode.hip / kx_encode.hip)
-struct KxLaunchCols {
-  void* data[KX_MAX_COLUMNS];
-  void* offs[KX_MAX_COLUMNS];    // record offsets (u32 or u64, see owide)
-  uint64_t cap[KX_MAX_COLUMNS];
-  void* eoffs[KX_MAX_COLUMNS];   // LIST_BYTES: element byte offsets
-  uint64_t ecap[KX_MAX_COLUMNS];
+struct KxLaunchCols {            // flat schemas (<= KXP_MAX_COLS columns)
+  void* data[KXP_MAX_COLS];
+  void* offs[KXP_MAX_COLS];      // record offsets (u32 or u64, see owide)
+  uint64_t cap[KXP_MAX_COLS];
+  void* eoffs[KXP_MAX_COLS];     // LIST_BYTES: element byte offsets
+  uint64_t ecap[KXP_MAX_COLS];
   uint32_t owide;                // bit c: column c has 8-byte offsets
   uint32_t view;                 // bit c: BYTES column c receives (offset, length) views (KX_COLF_VIEW)
   uint64_t* presence;

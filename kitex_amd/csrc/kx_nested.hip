@@ -1,0 +1,433 @@
+// kx_nested.hip — nested schemas on the device: the record walker of kx_nested.h, lane = record.
+//
+// Decode (records' extents from the caller's offsets / ends, or from the skip pass for concatenated
+// records, pkg/remote/codec/thrift/codec_apache.go:166-172):
+//   1. measure: each lane walks its record counting cursor advances (kx_nested.h, W = false) and writes
+//      them per cursor (u32, cursor-major: lanes store adjacent words) with its record's code;
+//   2. block sums per (1024-record block, cursor), then one workgroup per cursor scans the block sums
+//      into block bases and the cursor's total; a one-thread check compares the totals with the
+//      columns' capacities (SIZE_LIMIT: nothing is written);
+//   3. write: a workgroup per block re-scans its records' counts (one workgroup scan per cursor) into
+//      per-lane cursor bases and re-walks each record writing values, offsets entries and presence;
+//   4. finalize: the last entry of every offsets array, the call status.
+// Encode: size pass (lane = record, BLength) -> block scan -> write pass (FastWriteNocopy at the
+// record's offset); struct_tpl.go:225-391.
+#include <hip/hip_runtime.h>
+
+#include "kx_internal.h"
+#include "kx_nested.h"
+
+namespace {
+
+constexpr int NT = 256;       // threads per workgroup
+constexpr int RB = 1024;      // records per block
+constexpr int SNAP = 128;     // snapshot slots per lane (schemas needing more: NOT_IMPLEMENTED)
+constexpr int CUR = 64;       // cursors per lane
+
+struct NParams {
+  const KxnProgram* P;
+  const KxnCols* C;
+  const uint8_t* in;
+  uint64_t in_len;
+  const uint64_t* offsets;    // known offsets (n + 1), or the skip pass's starts (concat)
+  const uint64_t* ends;       // explicit ends (optional)
+  uint64_t n;
+  bool concat;
+  const kx_status* skip_st;   // concat: the skip pass's status (records delimited)
+  uint32_t* counts;           // [ncur][n]
+  uint64_t* bsum;             // [ncur][nblk]
+  uint64_t* totals;           // [ncur]
+  uint8_t* rcode;             // [n] record codes of the measure pass
+  unsigned long long* errkey; // (record << 8) | code, min
+  uint32_t* flag;             // size limit: write nothing
+  uint8_t* record_status;     // caller's (optional)
+  kx_status* status;
+  uint64_t nblk;
+  uint32_t ncur;
+  bool sizes_only;            // kx_thrift_decode_sizes: no column is written
+};
+
+// record r's extent; false when the record is not decoded at all (concat: past the failing one)
+__device__ __forceinline__ int extent(const NParams& p, uint64_t r, uint64_t* a, uint64_t* b) {
+  if (p.concat) {
+    const uint64_t ok = p.skip_st->code ? p.skip_st->n_records : p.n;
+    if (r > ok || (r == ok && !p.skip_st->code)) return -1;
+    *a = p.offsets[r];
+    *b = r < ok ? p.offsets[r + 1] : p.in_len;   // the failing record: FastRead finds its error
+    return 0;
+  }
+  *a = p.offsets[r];
+  *b = p.ends ? p.ends[r] : p.offsets[r + 1];
+  return (*a > *b || *b > p.in_len) ? KX_ERR_INVALID_ARG : 0;
+}
+
+__global__ void __launch_bounds__(NT) measure_kernel(NParams p) {
+  const uint64_t r = (uint64_t)blockIdx.x * NT + threadIdx.x;
+  if (r >= p.n) return;
+  const KxnProgram& P = *p.P;
+  uint64_t cur[CUR], snap[SNAP];
+  for (uint32_t k = 0; k < p.ncur; k++) cur[k] = 0;
+  uint64_t a = 0, b = 0, used = 0;
+  int rc = extent(p, r, &a, &b);
+  if (rc < 0) {
+    rc = 0;  // not decoded: empty
+    p.rcode[r] = 0xff;
+  } else {
+    if (!rc) rc = kxn_read_record<false>(P, *p.C, p.in + a, b - a, r, cur, snap, &used);
+    if (!rc && p.concat && r < p.n && p.skip_st->code && r == p.skip_st->n_records) rc = p.skip_st->code;
+    p.rcode[r] = (uint8_t)rc;
+    if (rc) atomicMin(p.errkey, (unsigned long long)((r << 8) | (uint64_t)(rc & 0xff)));
+  }
+  for (uint32_t k = 0; k < p.ncur; k++) p.counts[(uint64_t)k * p.n + r] = rc ? 0u : (uint32_t)cur[k];
+}
+
+__device__ __forceinline__ uint64_t wave_incl(uint64_t v, int lane) {
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t o = __shfl_up(v, d, 64);
+    if (lane >= d) v += o;
+  }
+  return v;
+}
+
+// exclusive scan over the workgroup (NT threads); *tot = the sum
+__device__ uint64_t wg_excl(uint64_t v, uint64_t* tot, uint64_t* sh) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint64_t inc = wave_incl(v, lane);
+  __syncthreads();
+  if (lane == 63) sh[wv] = inc;
+  __syncthreads();
+  uint64_t base = 0, t = 0;
+  for (int i = 0; i < (int)(blockDim.x >> 6); i++) {
+    const uint64_t s = sh[i];
+    if (i < wv) base += s;
+    t += s;
+  }
+  *tot = t;
+  return base + inc - v;
+}
+
+// grid (nblk, ncur): block sums
+__global__ void __launch_bounds__(NT) bsum_kernel(NParams p) {
+  __shared__ uint64_t sh[NT / 64];
+  const uint64_t b = blockIdx.x, k = blockIdx.y;
+  uint64_t acc = 0;
+  for (int j = 0; j < RB / NT; j++) {
+    const uint64_t r = b * RB + (uint64_t)j * NT + threadIdx.x;
+    if (r < p.n) acc += p.counts[k * p.n + r];
+  }
+  uint64_t tot;
+  (void)wg_excl(acc, &tot, sh);
+  if (threadIdx.x == 0) p.bsum[k * p.nblk + b] = tot;
+}
+
+// one workgroup per cursor: block sums -> block bases, the cursor's total
+__global__ void __launch_bounds__(1024) bscan_kernel(NParams p) {
+  __shared__ uint64_t sh[16];
+  const uint64_t k = blockIdx.x, nb = p.nblk;
+  uint64_t* s = p.bsum + k * nb;
+  const uint64_t per = (nb + 1023) / 1024;
+  const uint64_t lo = threadIdx.x * per, hi = kmin64(lo + per, nb);
+  uint64_t acc = 0;
+  for (uint64_t i = lo; i < hi; i++) acc += s[i];
+  uint64_t tot;
+  uint64_t run = wg_excl(acc, &tot, sh);
+  for (uint64_t i = lo; i < hi; i++) {
+    const uint64_t v = s[i];
+    s[i] = run;
+    run += v;
+  }
+  if (threadIdx.x == 0) p.totals[k] = tot;
+}
+
+// the parent domain size of column c's offsets array k
+__device__ __forceinline__ uint64_t parent_size(const NParams& p, const KxnCol& K, int k) {
+  return k == 0 ? p.n : p.totals[K.acur[k - 1]];
+}
+
+// capacities vs totals (one thread); status of a sizes-only call
+__global__ void check_kernel(NParams p) {
+  if (threadIdx.x != 0) return;
+  const KxnProgram& P = *p.P;
+  bool over = false;
+  for (uint32_t c = 0; c < P.ncols; c++) {
+    const KxnCol& K = P.col[c];
+    if (K.dcur >= 0 && p.totals[K.dcur] > p.C->cap[c][0]) over = true;
+    for (int k = 1; k < K.narr; k++)
+      if (parent_size(p, K, k) > p.C->cap[c][1 + k]) over = true;
+  }
+  *p.flag = over ? 1u : 0u;
+}
+
+__global__ void __launch_bounds__(NT) write_kernel(NParams p) {
+  __shared__ uint64_t sh[NT / 64];
+  if (*p.flag) return;
+  const KxnProgram& P = *p.P;
+  const uint64_t b = blockIdx.x;
+  uint64_t carry[CUR];
+  for (uint32_t k = 0; k < p.ncur; k++) carry[k] = p.bsum[(uint64_t)k * p.nblk + b];
+  for (int j = 0; j < RB / NT; j++) {
+    const uint64_t r = b * RB + (uint64_t)j * NT + threadIdx.x;
+    const bool act = r < p.n;
+    uint64_t cur[CUR], snap[SNAP];
+    for (uint32_t k = 0; k < p.ncur; k++) {
+      const uint64_t x = act ? p.counts[(uint64_t)k * p.n + r] : 0;
+      uint64_t tot;
+      const uint64_t pre = wg_excl(x, &tot, sh);
+      cur[k] = carry[k] + pre;
+      carry[k] += tot;
+    }
+    if (!act) continue;
+    const uint8_t rc = p.rcode[r];
+    uint64_t a = 0, e = 0, used = 0;
+    if (rc == 0 && extent(p, r, &a, &e) == 0) {
+      (void)kxn_read_record<true>(P, *p.C, p.in + a, e - a, r, cur, snap, &used);
+    } else {
+      kxn_failed_record(P, *p.C, r, cur);
+    }
+    if (p.record_status && !p.concat) p.record_status[r] = rc == 0xff ? 0 : rc;
+  }
+}
+
+__global__ void finalize_kernel(NParams p) {
+  const KxnProgram& P = *p.P;
+  if (*p.flag && !p.sizes_only) {
+    if (threadIdx.x == 0) {
+      p.status->code = KX_ERR_SIZE_LIMIT;
+      p.status->n_records = 0;
+      *p.errkey = ~0ull;
+    }
+    return;
+  }
+  for (uint32_t c = threadIdx.x; c < P.ncols && !p.sizes_only; c += blockDim.x) {
+    const KxnCol& K = P.col[c];
+    for (int k = 0; k < K.narr; k++) kxn_put_arr(*p.C, (int)c, k, parent_size(p, K, k), p.totals[K.acur[k]]);
+  }
+  if (threadIdx.x != 0) return;
+  kx_status* st = p.status;
+  const unsigned long long key = *p.errkey;
+  st->n_records = p.n;
+  st->consumed = p.concat ? p.offsets[p.n] : (p.n ? (p.ends ? p.ends[p.n - 1] : p.offsets[p.n]) : 0);
+  if (key != ~0ull) {
+    const uint64_t r = key >> 8;
+    st->code = (int32_t)(key & 0xff);
+    st->record = r;
+    st->offset = p.offsets[r];
+    if (p.concat) {
+      st->n_records = r;
+      st->consumed = p.offsets[r];
+    }
+  }
+  for (int v = 0; v < 8; v++) st->var_total[v] = v < (int)p.ncur ? p.totals[v] : 0;
+  *p.errkey = ~0ull;
+}
+
+// ---- encode ----
+struct EParams {
+  const KxnProgram* P;
+  const KxnCols* C;
+  uint64_t n;
+  uint8_t* out;
+  uint64_t out_cap;
+  uint64_t* sizes;       // [n] (caller's or workspace)
+  uint64_t* bsum;        // [nblk]
+  uint64_t* offsets_out; // optional
+  kx_status* status;
+  uint64_t nblk;
+};
+
+__global__ void __launch_bounds__(NT) esize_kernel(EParams p) {
+  __shared__ uint64_t sh[NT / 64];
+  const uint64_t b = blockIdx.x;
+  uint64_t acc = 0;
+  for (int j = 0; j < RB / NT; j++) {
+    const uint64_t r = b * RB + (uint64_t)j * NT + threadIdx.x;
+    if (r < p.n) {
+      const uint64_t sz = kxn_write_record<false>(*p.P, *p.C, r, nullptr, 0);
+      p.sizes[r] = sz;
+      acc += sz;
+    }
+  }
+  uint64_t tot;
+  (void)wg_excl(acc, &tot, sh);
+  if (threadIdx.x == 0 && p.bsum) p.bsum[b] = tot;
+}
+
+__global__ void __launch_bounds__(1024) escan_kernel(EParams p) {
+  __shared__ uint64_t sh[16];
+  const uint64_t nb = p.nblk;
+  const uint64_t per = (nb + 1023) / 1024;
+  const uint64_t lo = threadIdx.x * per, hi = kmin64(lo + per, nb);
+  uint64_t acc = 0;
+  for (uint64_t i = lo; i < hi; i++) acc += p.bsum[i];
+  uint64_t tot;
+  uint64_t run = wg_excl(acc, &tot, sh);
+  for (uint64_t i = lo; i < hi; i++) {
+    const uint64_t v = p.bsum[i];
+    p.bsum[i] = run;
+    run += v;
+  }
+  if (threadIdx.x == 0) {
+    kx_status* st = p.status;
+    st->n_records = p.n;
+    st->consumed = tot;
+    st->code = tot > p.out_cap ? KX_ERR_SIZE_LIMIT : 0;
+    if (p.offsets_out && tot <= p.out_cap) p.offsets_out[p.n] = tot;
+  }
+}
+
+__global__ void __launch_bounds__(NT) ewrite_kernel(EParams p) {
+  __shared__ uint64_t sh[NT / 64];
+  if (p.status->code != 0) return;
+  const uint64_t b = blockIdx.x;
+  uint64_t base = p.bsum[b];
+  for (int j = 0; j < RB / NT; j++) {
+    const uint64_t r = b * RB + (uint64_t)j * NT + threadIdx.x;
+    const uint64_t sz = r < p.n ? p.sizes[r] : 0;
+    uint64_t tot;
+    const uint64_t pre = wg_excl(sz, &tot, sh);
+    if (r < p.n) {
+      (void)kxn_write_record<true>(*p.P, *p.C, r, p.out, base + pre);
+      if (p.offsets_out) p.offsets_out[r] = base + pre;
+    }
+    base += tot;
+  }
+}
+
+}  // namespace
+
+// workspace: [0] errkey u64, [8] flag u32, [64] rcode[n], counts [ncur][n] u32, bsum [ncur][nblk],
+// totals [ncur], then (concat) the skip pass's starts (n + 1) and its status
+size_t kx_nested_ws_bytes(const KxnProgram& P, uint64_t n, bool concat) {
+  const uint64_t nblk = (n + RB - 1) / RB;
+  size_t s = 64 + ((n + 63) & ~63ull) + (size_t)P.ncur * n * 4 + 64 + (size_t)P.ncur * nblk * 8 + P.ncur * 8 + 64;
+  if (concat) s += (n + 1) * 8 + 64 + sizeof(kx_status) + 64;
+  return s + 4096;
+}
+
+namespace {
+struct NwsLayout {
+  unsigned long long* errkey;
+  uint32_t* flag;
+  uint8_t* rcode;
+  uint32_t* counts;
+  uint64_t* bsum;
+  uint64_t* totals;
+  uint64_t* starts;
+  kx_status* skip_st;
+};
+NwsLayout layout(void* ws, const KxnProgram& P, uint64_t n) {
+  NwsLayout L;
+  char* p = (char*)ws;
+  const uint64_t nblk = (n + RB - 1) / RB;
+  L.errkey = (unsigned long long*)p;
+  L.flag = (uint32_t*)(p + 8);
+  p += 64;
+  L.rcode = (uint8_t*)p;
+  p += (n + 63) & ~63ull;
+  L.counts = (uint32_t*)p;
+  p += ((size_t)P.ncur * n * 4 + 63) & ~63ull;
+  L.bsum = (uint64_t*)p;
+  p += (size_t)P.ncur * nblk * 8;
+  L.totals = (uint64_t*)p;
+  p += ((size_t)P.ncur * 8 + 63) & ~63ull;
+  L.starts = (uint64_t*)p;
+  p += ((n + 1) * 8 + 63) & ~63ull;
+  L.skip_st = (kx_status*)p;
+  return L;
+}
+}  // namespace
+
+// decode (totals_out != null: sizes only, the cursor totals are copied there and the status is final
+// when the stream reaches this point)
+int kx_launch_nested_decode(const KxnProgram* dprog, const KxnProgram& hprog, const uint8_t* in, uint64_t in_len,
+                            const uint64_t* offsets, const uint64_t* ends, uint64_t n, const KxnCols* dcols,
+                            uint8_t* record_status, kx_status* status, void* ws, size_t ws_size,
+                            void* skip_ws, size_t skip_ws_size, uint64_t skip_epoch, hipStream_t stream,
+                            uint64_t* totals_out) {
+  if (hprog.nsnap > SNAP || hprog.ncur > CUR || hprog.ncur == 0) return KX_ERR_NOT_IMPLEMENTED;
+  const bool concat = offsets == nullptr;
+  if (ws_size < kx_nested_ws_bytes(hprog, n, concat)) return KX_ERR_INVALID_ARG;
+  NwsLayout L = layout(ws, hprog, n);
+  NParams p{};
+  p.P = dprog;
+  p.C = dcols;
+  p.in = in;
+  p.in_len = in_len;
+  p.n = n;
+  p.concat = concat;
+  p.ends = ends;
+  p.counts = L.counts;
+  p.bsum = L.bsum;
+  p.totals = L.totals;
+  p.rcode = L.rcode;
+  p.errkey = L.errkey;
+  p.flag = L.flag;
+  p.record_status = record_status;
+  p.status = status;
+  p.nblk = (n + RB - 1) / RB;
+  p.ncur = hprog.ncur;
+  p.sizes_only = totals_out != nullptr;
+  KX_HIP_CHECK(hipMemsetAsync(status, 0, sizeof(kx_status), stream));
+  KX_HIP_CHECK(hipMemsetAsync(L.errkey, 0xff, 8, stream));
+  KX_HIP_CHECK(hipMemsetAsync(L.flag, 0, 4, stream));
+  if (concat) {
+    // record boundaries: the skip decoder (codec_apache.go:166-172) on the pipeline of kx_decode.hip
+    int rc = kx_launch_skip(in, in_len, n, L.starts, L.skip_st, skip_ws, skip_ws_size, skip_epoch, stream);
+    if (rc) return rc;
+    p.offsets = L.starts;
+    p.skip_st = L.skip_st;
+  } else {
+    p.offsets = offsets;
+  }
+  const unsigned gm = (unsigned)((n + NT - 1) / NT);
+  hipLaunchKernelGGL(measure_kernel, dim3(gm), dim3(NT), 0, stream, p);
+  KX_HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(bsum_kernel, dim3((unsigned)p.nblk, hprog.ncur), dim3(NT), 0, stream, p);
+  KX_HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(bscan_kernel, dim3(hprog.ncur), dim3(1024), 0, stream, p);
+  KX_HIP_CHECK(hipGetLastError());
+  if (totals_out) {
+    KX_HIP_CHECK(hipMemcpyAsync(totals_out, L.totals, hprog.ncur * 8, hipMemcpyDeviceToHost, stream));
+    // the status of the measure pass: the first failing record
+    hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(64), 0, stream, p);
+    KX_HIP_CHECK(hipGetLastError());
+    return KX_OK;
+  }
+  hipLaunchKernelGGL(check_kernel, dim3(1), dim3(64), 0, stream, p);
+  KX_HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(write_kernel, dim3((unsigned)p.nblk), dim3(NT), 0, stream, p);
+  KX_HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(64), 0, stream, p);
+  KX_HIP_CHECK(hipGetLastError());
+  return KX_OK;
+}
+
+size_t kx_nested_enc_ws_bytes(uint64_t n) { return (n + 64) * 8 + ((n + RB - 1) / RB) * 8 + 256; }
+
+int kx_launch_nested_encode(const KxnProgram* dprog, const KxnProgram& hprog, const KxnCols* dcols, uint64_t n,
+                            uint8_t* out, uint64_t out_cap, uint64_t* sizes_out, uint64_t* offsets_out,
+                            kx_status* status, void* ws, size_t ws_size, hipStream_t stream, bool sizes_only) {
+  (void)hprog;
+  if (ws_size < kx_nested_enc_ws_bytes(n)) return KX_ERR_INVALID_ARG;
+  EParams p{};
+  p.P = dprog;
+  p.C = dcols;
+  p.n = n;
+  p.out = out;
+  p.out_cap = out_cap;
+  p.nblk = (n + RB - 1) / RB;
+  p.bsum = (uint64_t*)ws;
+  p.sizes = sizes_out ? sizes_out : (uint64_t*)ws + ((p.nblk + 63) & ~63ull);
+  p.offsets_out = offsets_out;
+  p.status = status;
+  if (status) KX_HIP_CHECK(hipMemsetAsync(status, 0, sizeof(kx_status), stream));
+  hipLaunchKernelGGL(esize_kernel, dim3((unsigned)p.nblk), dim3(NT), 0, stream, p);
+  KX_HIP_CHECK(hipGetLastError());
+  if (sizes_only) return KX_OK;
+  hipLaunchKernelGGL(escan_kernel, dim3(1), dim3(1024), 0, stream, p);
+  KX_HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(ewrite_kernel, dim3((unsigned)p.nblk), dim3(NT), 0, stream, p);
+  KX_HIP_CHECK(hipGetLastError());
+  return KX_OK;
+}

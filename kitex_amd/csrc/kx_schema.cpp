@@ -44,7 +44,7 @@ struct Builder {
   std::vector<std::vector<PendField>> inst_fields;
   std::vector<int> inst_parent, inst_self;  // self: index into parent's field list
   int stack[8];
-  int64_t sel_def[KX_MAX_COLUMNS] = {};     // list<struct> element field defaults, per column
+  int64_t sel_def[KXP_MAX_COLS] = {};     // list<struct> element field defaults, per column
 
   int rec(int sidx, int depth, int parent, int self_idx, int16_t* path, int* out) {
     if (sidx < 0 || (uint32_t)sidx >= nstructs) return KX_ERR_INVALID_ARG;
@@ -85,6 +85,9 @@ struct Builder {
           ci.width = (uint32_t)type_size(f->ttype);
           break;
         case KX_T_STRING:
+          // a non-empty string default: the nested program (kx_nested_schema.cpp)
+          if ((f->reserved0 & KX_FIELD_STRING_DEFAULT) && f->default_bits && *(const char*)(intptr_t)f->default_bits)
+            return KX_ERR_NOT_IMPLEMENTED;
           ci.kind = KX_COL_BYTES;
           ci.width = 1;
           break;
@@ -98,7 +101,7 @@ struct Builder {
           if (f->elem_ttype == KX_T_STRUCT) {  // list/set<S> of fixed scalars: one LIST column per field of S
             if (f->child < 0 || (uint32_t)f->child >= nstructs || depth + 1 >= 8) return KX_ERR_NOT_IMPLEMENTED;
             const kx_struct_desc& es = structs[f->child];
-            if (es.nfields == 0 || es.nfields > 8 || !es.fields || s->ncols + es.nfields > KX_MAX_COLUMNS)
+            if (es.nfields == 0 || es.nfields > 8 || !es.fields || s->ncols + es.nfields > KXP_MAX_COLS)
               return KX_ERR_NOT_IMPLEMENTED;
             for (uint32_t k = 0; k < es.nfields; k++) {
               const kx_field_desc& g = es.fields[k];
@@ -147,7 +150,7 @@ struct Builder {
           const uint8_t kt = f->elem_ttype & 15, vt = (uint8_t)(f->elem_ttype >> 4);
           if ((type_size(kt) == 0 && kt != KX_T_STRING) || (type_size(vt) == 0 && vt != KX_T_STRING))
             return KX_ERR_NOT_IMPLEMENTED;  // map<.., struct|container>
-          if (s->ncols + 2 > KX_MAX_COLUMNS) return KX_ERR_NOT_IMPLEMENTED;
+          if (s->ncols + 2 > KXP_MAX_COLS) return KX_ERR_NOT_IMPLEMENTED;
           pf.col = (int)s->ncols;
           for (int side = 0; side < 2; side++) {
             const uint8_t t = side ? vt : kt;
@@ -163,7 +166,7 @@ struct Builder {
         default:
           return KX_ERR_INVALID_ARG;
       }
-      if (s->ncols >= KX_MAX_COLUMNS) return KX_ERR_NOT_IMPLEMENTED;
+      if (s->ncols >= KXP_MAX_COLS) return KX_ERR_NOT_IMPLEMENTED;
       pf.col = (int)s->ncols;
       s->info[s->ncols++] = ci;
       inst_fields[me].push_back(pf);

@@ -12,9 +12,10 @@ front end for the batch codec:
                                     them and k-mock.go:422-517 generates them)
   to_schema(struct descriptor)   -> kitex_amd.schema.Schema (the flattened table kx_schema_create takes)
 
-Shapes the device codec does not hold (maps of structs, lists of structs with string / nested / optional
-fields, nested containers, recursive structs, non-empty string defaults) raise NotImplementedError at compile time, the Python face of
-KX_ERR_NOT_IMPLEMENTED. Supported grammar: namespace / include / cpp_include, typedef, const (skipped),
+Every shape compiles: what the flat column model cannot hold (maps of structs, lists of structs with
+string / nested / optional fields, containers of containers, recursive structs, string defaults) becomes a
+nested schema (include/kxcodec.h "Nested schemas"); map keys that are structs or containers, and leaves
+more than two container levels down, raise NotImplementedError (KX_ERR_NOT_IMPLEMENTED). Supported grammar: namespace / include / cpp_include, typedef, const (skipped),
 enum (-> i32), struct / union / exception, service (extends, oneway, throws), annotations `(k = "v")`,
 `//`, `#` and `/* */` comments, `,` / `;` separators.
 """
@@ -445,16 +446,15 @@ def parse_idl(src: str, include_dirs=()) -> Document:
 _LEAF = (A.T_BOOL, A.T_BYTE, A.T_I16, A.T_I32, A.T_I64, A.T_DOUBLE, A.T_STRING)
 
 
-def _default_bits(fd: FieldDescriptor) -> int:
+def _default_bits(fd: FieldDescriptor):
+    """a scalar default as its bits, a string default as the string (include/kxcodec.h: string defaults
+    are nested-schema data)"""
     d = fd.default_value
     if d is None:
         return 0
     t = fd.type.type
     if t == A.T_STRING:
-        if d == "":
-            return 0
-        raise NotImplementedError(f"field {fd.name}: non-empty string default {d!r} (decode fills only scalar "
-                                  "defaults)")
+        return d if d != "" else 0
     if t == A.T_DOUBLE:
         return _struct.unpack("<q", _struct.pack("<d", float(d)))[0]
     if t in (A.T_BOOL, A.T_BYTE, A.T_I16, A.T_I32, A.T_I64):
@@ -462,41 +462,50 @@ def _default_bits(fd: FieldDescriptor) -> int:
     raise NotImplementedError(f"field {fd.name}: default value for a container or struct")
 
 
-def _field(fd: FieldDescriptor, stack) -> Field:
+def _elem(td: TypeDescriptor, memo):
+    """a container's element (or map value) type: (wire type or element-type Field, element struct)"""
+    if td.type in _LEAF:
+        return td.type, None
+    if td.type == A.T_STRUCT:
+        return A.T_STRUCT, _struct_of(td.struct, memo)
+    if td.type in (A.T_LIST, A.T_SET, A.T_MAP):   # a container of containers: described by a Field
+        return _container(Field(0, td.type, td.name, binary=td.binary), td, memo), None
+    raise NotImplementedError(f"element type {td.name}")
+
+
+def _container(f: Field, td: TypeDescriptor, memo) -> Field:
+    if td.type == A.T_MAP:
+        if td.key.type not in _LEAF:
+            raise NotImplementedError(f"map<{td.key.name},{td.elem.name}>: struct / container keys")
+        f.elem = td.key.type
+        f.val, child = _elem(td.elem, memo)
+    else:
+        f.elem, child = _elem(td.elem, memo)
+    if child is not None:
+        f.child = child
+    return f
+
+
+def _field(fd: FieldDescriptor, memo) -> Field:
     td = fd.type
     req = A.REQ_REQUIRED if fd.required else A.REQ_OPTIONAL if fd.optional else A.REQ_DEFAULT
     f = Field(fd.id, td.type, fd.name, req=req, default=_default_bits(fd), binary=td.binary)
     if td.type == A.T_STRUCT:
-        f.child = _struct_of(td.struct, stack)
-    elif td.type in (A.T_LIST, A.T_SET):
-        if td.elem.type == A.T_STRUCT:  # list<S>: S of fixed-width, non-optional scalars (kxcodec.h)
-            es = td.elem.struct
-            bad = [g.name for g in es.fields if g.type.type not in _LEAF or g.type.type == A.T_STRING or g.optional]
-            if bad or not es.fields:
-                raise NotImplementedError(f"field {fd.name}: {td.name}<{es.name}> (element fields must be fixed-width, "
-                                          f"non-optional scalars; not {bad})")
-            f.elem = A.T_STRUCT
-            f.child = _struct_of(es, stack)
-        elif td.elem.type not in _LEAF:
-            raise NotImplementedError(f"field {fd.name}: {td.name}<{td.elem.name}> (only scalar / string / "
-                                      "fixed-struct elements)")
-        else:
-            f.elem = td.elem.type
-    elif td.type == A.T_MAP:
-        if td.key.type not in _LEAF or td.elem.type not in _LEAF:
-            raise NotImplementedError(f"field {fd.name}: map<{td.key.name},{td.elem.name}> (only scalar / string "
-                                      "keys and values)")
-        f.elem, f.val = td.key.type, td.elem.type
+        f.child = _struct_of(td.struct, memo)
+    elif td.type in (A.T_LIST, A.T_SET, A.T_MAP):
+        _container(f, td, memo)
     elif td.type not in _LEAF:
         raise NotImplementedError(f"field {fd.name}: type {td.name}")
     return f
 
 
-def _struct_of(sd: StructDescriptor, stack) -> Struct:
-    if id(sd) in stack:
-        raise NotImplementedError(f"struct {sd.name} is recursive (a columnar layout needs a finite nesting)")
-    stack = stack | {id(sd)}
-    return Struct(sd.name, [_field(f, stack) for f in sd.fields])
+def _struct_of(sd: StructDescriptor, memo) -> Struct:
+    # one Struct per descriptor: a recursive type refers to itself (the codec keeps such a field's bytes)
+    s = memo.get(id(sd))
+    if s is None:
+        s = memo[id(sd)] = Struct(sd.name, [])
+        s.fields.extend(_field(f, memo) for f in sd.fields)
+    return s
 
 
 def to_schema(sd: Union[StructDescriptor, TypeDescriptor]) -> Schema:
@@ -506,7 +515,7 @@ def to_schema(sd: Union[StructDescriptor, TypeDescriptor]) -> Schema:
         if sd.struct is None:
             raise ValueError(f"{sd.name} is not a struct")
         sd = sd.struct
-    return Schema(_struct_of(sd, frozenset()))
+    return Schema(_struct_of(sd, {}))
 
 
 def request_schema(doc: Document, method: str, service: Optional[str] = None) -> Schema:

@@ -24,10 +24,11 @@ class Field:
     ttype: int
     name: str = ""
     req: int = A.REQ_DEFAULT
-    elem: int = 0                       # LIST/SET element type; MAP key type
-    val: int = 0                        # MAP value type
-    child: Optional["Struct"] = None    # STRUCT fields
-    default: int = 0                    # scalar default (two's complement / IEEE bits)
+    elem: object = 0                    # LIST/SET element type; MAP key type. A container element: a Field
+                                        # describing it (its id is ignored), e.g. list<list<i64>>
+    val: object = 0                     # MAP value type (a Field for a container value)
+    child: Optional["Struct"] = None    # STRUCT fields; the struct of list<S> / set<S> / map<K, S>
+    default: object = 0                 # scalar default (two's complement / IEEE bits) or a string default
     binary: bool = False                # protobuf `bytes` (no UTF-8 check); thrift: same wire as string
 
 
@@ -44,6 +45,8 @@ class Schema:
         self.root = root
         self.structs: List[Struct] = []
         self._index = {}
+        self._elem_struct = {}     # id(field) -> the one-field struct describing its container element
+        self._strings = []         # string defaults kept alive for the C-ABI
         self._collect(root)
         self._field_arrays = []
         self._table = (A.StructDesc * len(self.structs))()
@@ -53,10 +56,22 @@ class Schema:
                 arr[j].id = f.id
                 arr[j].ttype = f.ttype
                 arr[j].req = f.req
-                arr[j].elem_ttype = f.elem | (f.val << 4 if f.ttype == A.T_MAP else 0)
+                et = f.elem.ttype if isinstance(f.elem, Field) else f.elem
+                vt = f.val.ttype if isinstance(f.val, Field) else f.val
+                arr[j].elem_ttype = et | (vt << 4 if f.ttype == A.T_MAP else 0)
                 arr[j].reserved0 = A.FIELD_BINARY if f.binary else 0
-                arr[j].child = self._index[id(f.child)] if f.child is not None else -1
-                arr[j].default_bits = _signed64(f.default)
+                if id(f) in self._elem_struct:
+                    arr[j].child = self._index[id(self._elem_struct[id(f)])]
+                else:
+                    arr[j].child = self._index[id(f.child)] if f.child is not None else -1
+                if isinstance(f.default, (str, bytes)):
+                    b = f.default.encode() if isinstance(f.default, str) else f.default
+                    buf = C.create_string_buffer(b)
+                    self._strings.append(buf)
+                    arr[j].default_bits = C.addressof(buf) if b else 0
+                    arr[j].reserved0 |= A.FIELD_STRING_DEFAULT if b else 0
+                else:
+                    arr[j].default_bits = _signed64(f.default)
             self._field_arrays.append(arr)
             self._table[i].fields = C.cast(arr, C.POINTER(A.FieldDesc))
             self._table[i].nfields = len(s.fields)
@@ -67,8 +82,16 @@ class Schema:
         self._index[id(s)] = len(self.structs)
         self.structs.append(s)
         for f in s.fields:
-            if f.child is not None:
-                self._collect(f.child)
+            self._collect_field(f)
+
+    def _collect_field(self, f: Field):
+        sub = f.val if f.ttype == A.T_MAP else f.elem
+        if isinstance(sub, Field):   # a container element / map value that is a container
+            es = Struct(f"{f.name or f.id}.elem", [sub])
+            self._elem_struct[id(f)] = es
+            self._collect(es)
+        elif f.child is not None:
+            self._collect(f.child)
 
     def struct_table(self):
         return self._table, len(self.structs)
@@ -147,6 +170,51 @@ def schema_ls1() -> Schema:
     tag = Struct("Tag", [Field(7, A.T_I16, "k"), Field(9, A.T_BYTE, "v")])
     return Schema(Struct("LS1", [Field(1, A.T_I64, "id"), Field(2, A.T_LIST, "pts", elem=A.T_STRUCT, child=pt),
                                  Field(3, A.T_SET, "tags", elem=A.T_STRUCT, child=tag, req=A.REQ_OPTIONAL)]))
+
+
+def schema_simple() -> Struct:
+    """baseline.thrift Simple (pkg/generic/json_test/idl/baseline.thrift:3-10)"""
+    return Struct("Simple", [Field(1, A.T_BYTE, "ByteField"), Field(2, A.T_I64, "I64Field"),
+                             Field(3, A.T_DOUBLE, "DoubleField"), Field(4, A.T_I32, "I32Field"),
+                             Field(5, A.T_STRING, "StringField"), Field(6, A.T_STRING, "BinaryField", binary=True)])
+
+
+def schema_nesting() -> Schema:
+    """baseline.thrift Nesting (:12-28): list<Simple>, map<string, Simple>, a Simple field and maps /
+    lists of scalars and strings: 42 columns, a nested schema"""
+    sim = schema_simple()
+    S = A.T_STRING
+    return Schema(Struct("Nesting", [
+        Field(1, S, "String"), Field(2, A.T_LIST, "ListSimple", elem=A.T_STRUCT, child=sim),
+        Field(3, A.T_DOUBLE, "Double"), Field(4, A.T_I32, "I32"), Field(5, A.T_LIST, "ListI32", elem=A.T_I32),
+        Field(6, A.T_I64, "I64"), Field(7, A.T_MAP, "MapStringString", elem=S, val=S),
+        Field(8, A.T_STRUCT, "SimpleStruct", child=sim), Field(9, A.T_MAP, "MapI32I64", elem=A.T_I32, val=A.T_I64),
+        Field(10, A.T_LIST, "ListString", elem=S), Field(11, S, "Binary", binary=True),
+        Field(12, A.T_MAP, "MapI64String", elem=A.T_I64, val=S), Field(13, A.T_LIST, "ListI64", elem=A.T_I64),
+        Field(14, A.T_BYTE, "Byte"), Field(15, A.T_MAP, "MapStringSimple", elem=S, val=A.T_STRUCT, child=sim),
+    ]))
+
+
+def schema_nx() -> Schema:
+    """Shapes beyond baseline.thrift: nested containers one level down (list<list<i64>>, map<string,
+    list<string>>, list<set<i32>>), a list of structs with optional fields, a nested struct and a
+    list inside, a string default, and a recursive struct kept as bytes."""
+    S = A.T_STRING
+    leaf = Struct("Leaf", [Field(1, A.T_I32, "k", req=A.REQ_REQUIRED), Field(2, S, "v", default="none")])
+    item = Struct("Item", [Field(1, A.T_I64, "id"), Field(2, S, "name", req=A.REQ_OPTIONAL),
+                           Field(3, A.T_STRUCT, "leaf", child=leaf, req=A.REQ_OPTIONAL),
+                           Field(4, A.T_LIST, "tags", elem=A.T_I32), Field(5, A.T_BOOL, "on", req=A.REQ_OPTIONAL)])
+    node = Struct("Node", [Field(1, A.T_I64, "v")])
+    node.fields.append(Field(2, A.T_STRUCT, "next", child=node, req=A.REQ_OPTIONAL))
+    return Schema(Struct("NX", [
+        Field(1, A.T_I64, "id"), Field(2, S, "title", default="untitled"),
+        Field(3, A.T_LIST, "grid", elem=Field(0, A.T_LIST, elem=A.T_I64)),
+        Field(4, A.T_MAP, "index", elem=S, val=Field(0, A.T_LIST, elem=S)),
+        Field(5, A.T_LIST, "items", elem=A.T_STRUCT, child=item),
+        Field(6, A.T_SET, "groups", elem=Field(0, A.T_SET, elem=A.T_I32), req=A.REQ_OPTIONAL),
+        Field(7, A.T_STRUCT, "node", child=node),
+        Field(8, A.T_MAP, "byid", elem=A.T_I32, val=A.T_STRUCT, child=leaf),
+    ]))
 
 
 SCHEMAS = {"r1": schema_r1, "r2": schema_r2, "r3": schema_r3, "pf": schema_pf}

@@ -676,6 +676,8 @@ static int flatten_rec(plan_t* p, int sidx, int depth, int16_t* path, int* stack
       case KX_T_BOOL: case KX_T_BYTE: case KX_T_I16: case KX_T_I32: case KX_T_I64: case KX_T_DOUBLE:
         ci.kind = KX_COL_FIXED; ci.width = (uint32_t)type_size(f->ttype); break;
       case KX_T_STRING:
+        if ((f->reserved0 & KX_FIELD_STRING_DEFAULT) && f->default_bits && *(const char*)(intptr_t)f->default_bits)
+          return KX_ERR_NOT_IMPLEMENTED;                   /* a string default: nested */
         ci.kind = KX_COL_BYTES; ci.width = 1; break;
       case KX_T_LIST: case KX_T_SET:
         if (f->elem_ttype == KX_T_STRING) {                /* list/set<string>: FieldFastReadList (:582-625) */
@@ -747,12 +749,24 @@ static int plan_build(plan_t* p, const kx_struct_desc* structs, uint32_t nstruct
   int16_t path[8]; int stack[8]; int root = -1;
   int rc = flatten_rec(p, 0, 0, path, stack, &root);
   if (rc) return rc;
+  /* the flat model's limits (the library's kx_program.h): beyond them a schema is nested */
+  int nfields = 0;
+  for (int i = 0; i < p->ninst; i++) nfields += (int)p->structs[p->inst[i].sidx].nfields;
+  if (p->ncols > 32 || p->ninst > 16 || nfields > 64) return KX_ERR_NOT_IMPLEMENTED;
   p->nvar = 0;
   for (uint32_t c = 0; c < p->ncols; c++) {  /* var slots in column order; LIST_BYTES: elements, bytes */
     p->varidx[c] = p->cols[c].kind == KX_COL_FIXED ? -1 : p->nvar++;
     p->varidx2[c] = p->cols[c].kind == KX_COL_LIST_BYTES ? p->nvar++ : -1;
   }
+  if (p->nvar > 8) return KX_ERR_NOT_IMPLEMENTED;
   return KX_OK;
+}
+
+int kxo_is_nested(const kx_struct_desc* structs, uint32_t nstructs) {
+  plan_t* p = (plan_t*)malloc(sizeof(plan_t));
+  const int rc = plan_build(p, structs, nstructs);
+  free(p);
+  return rc == KX_ERR_NOT_IMPLEMENTED;
 }
 
 int kxo_flatten(const kx_struct_desc* structs, uint32_t nstructs, kx_column_info* cols,
@@ -764,6 +778,7 @@ int kxo_flatten(const kx_struct_desc* structs, uint32_t nstructs, kx_column_info
     *ncols = p->ncols; *npresence = p->npres;
   }
   free(p);
+  if (rc == KX_ERR_NOT_IMPLEMENTED) return kxo_nflatten(structs, nstructs, cols, ncols, npresence);
   return rc;
 }
 
@@ -1207,6 +1222,8 @@ static int decode_common(const kx_struct_desc* structs, uint32_t nstructs, rec_r
 int kxo_thrift_decode(const kx_struct_desc* structs, uint32_t nstructs, const uint8_t* in,
                       uint64_t in_len, const uint64_t* offsets, uint64_t n, const kx_columns* out,
                       uint8_t* record_status, kx_status* st) {
+  if (kxo_is_nested(structs, nstructs))
+    return kxo_nthrift_decode(structs, nstructs, in, in_len, offsets, n, out, record_status, st);
   return decode_common(structs, nstructs, thrift_reader, 0, in, in_len, offsets, n, out, record_status, st);
 }
 
@@ -1273,6 +1290,8 @@ static int decode_mt(const kx_struct_desc* structs, uint32_t nstructs, rec_reade
 int kxo_thrift_decode_mt(const kx_struct_desc* structs, uint32_t nstructs, const uint8_t* in,
                          uint64_t in_len, const uint64_t* offsets, uint64_t n, const kx_columns* out,
                          kx_status* st, int threads) {
+  if (kxo_is_nested(structs, nstructs))
+    return kxo_nthrift_decode(structs, nstructs, in, in_len, offsets, n, out, NULL, st);
   return decode_mt(structs, nstructs, thrift_reader, 0, in, in_len, offsets, n, out, st, threads);
 }
 
@@ -1448,6 +1467,10 @@ static uint64_t rec_presence(const enc_t* e) { return e->in->presence ? e->in->p
 
 int kxo_thrift_sizes(const kx_struct_desc* structs, uint32_t nstructs, const kx_columns* in,
                      uint64_t n, uint64_t* sizes) {
+  if (kxo_is_nested(structs, nstructs)) {
+    uint64_t total = 0;
+    return kxo_nthrift_encode(structs, nstructs, in, n, NULL, 0, sizes, NULL, &total);
+  }
   plan_t* p = (plan_t*)malloc(sizeof(plan_t));
   int rc = plan_build(p, structs, nstructs);
   if (!rc) rc = check_out(p, in);
@@ -1476,6 +1499,8 @@ static void* enc_worker(void* arg) {
 int kxo_thrift_encode_mt(const kx_struct_desc* structs, uint32_t nstructs, const kx_columns* in,
                          uint64_t n, uint8_t* out, uint64_t cap, uint64_t* offsets_out,
                          uint64_t* total, int threads) {
+  if (kxo_is_nested(structs, nstructs))
+    return kxo_nthrift_encode(structs, nstructs, in, n, out, cap, NULL, offsets_out, total);
   if (threads < 1) threads = 1;
   if (threads > 256) threads = 256;
   plan_t* p = (plan_t*)malloc(sizeof(plan_t));

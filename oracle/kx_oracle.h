@@ -112,6 +112,16 @@ int kxo_frame_crc32c_validate(const uint8_t* in, uint64_t in_len, const uint64_t
 /* -------- synthetic inputs: splitmix64 -------- */
 uint64_t kxo_splitmix64(uint64_t x);
 
+/* nested schemas (kx_oracle_nested.c; include/kxcodec.h "Nested schemas") */
+int kxo_nflatten(const kx_struct_desc* structs, uint32_t nstructs, kx_column_info* cols, uint32_t* ncols,
+                 uint32_t* npresence);
+int kxo_nthrift_decode(const kx_struct_desc* structs, uint32_t nstructs, const uint8_t* in, uint64_t in_len,
+                       const uint64_t* offsets, uint64_t n, const kx_columns* out, uint8_t* record_status,
+                       kx_status* st);
+int kxo_nthrift_encode(const kx_struct_desc* structs, uint32_t nstructs, const kx_columns* in, uint64_t n,
+                       uint8_t* out, uint64_t cap, uint64_t* sizes, uint64_t* offsets_out, uint64_t* total);
+int kxo_is_nested(const kx_struct_desc* structs, uint32_t nstructs);
+
 #ifdef __cplusplus
 }
 #endif

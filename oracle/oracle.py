@@ -93,6 +93,8 @@ def lib():
         L.kxo_pb_read_meta.argtypes = L.kxo_read_message_begin.argtypes
         L.kxo_put_uvarint.argtypes = [vp, C.c_uint64]
         L.kxo_get_uvarint.argtypes = [vp, sz, C.POINTER(C.c_uint64), C.POINTER(sz)]
+        L.kxo_is_nested.argtypes = [sdp, C.c_uint32]
+        L.kxo_is_nested.restype = C.c_int
         L.kxo_splitmix64.argtypes = [C.c_uint64]
         L.kxo_splitmix64.restype = C.c_uint64
         _lib = L

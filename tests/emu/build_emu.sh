@@ -24,6 +24,8 @@ $CXX $FLAGS -c _build/kx_decode_emu.cpp -o _build/kx_decode_emu.o
 cp $ROOT/kitex_amd/csrc/kx_crc.hip _build/kx_crc_emu.cpp
 $CXX $FLAGS -c _build/kx_crc_emu.cpp -o _build/kx_crc_emu.o
 $CXX $FLAGS -c $ROOT/kitex_amd/csrc/kx_schema.cpp -o _build/kx_schema.o
+$CXX $FLAGS -c $ROOT/kitex_amd/csrc/kx_nested_schema.cpp -o _build/kx_nested_schema.o
+$CXX $FLAGS -c nested_host.cpp -o _build/nested_host.o
 $CXX $FLAGS -c emu_rt.cpp -o _build/emu_rt.o
 $CXX $FLAGS -c emu_driver.cpp -o _build/emu_driver.o
 $CXX -shared -o _build/libkxemu.so _build/*.o -lpthread

@@ -21,14 +21,22 @@ def lib():
     global _lib
     if _lib is None:
         csrc = os.path.join(HERE, "..", "..", "kitex_amd", "csrc")
-        srcs = [os.path.join(csrc, f) for f in ("kx_decode.hip", "kx_crc.hip")] + \
-            [os.path.join(HERE, f) for f in ("emu_driver.cpp", "emu_rt.cpp", os.path.join("hip", "hip_runtime.h"))]
+        srcs = [os.path.join(csrc, f) for f in ("kx_decode.hip", "kx_crc.hip", "kx_nested.h", "kx_nested_schema.cpp",
+                                                "kx_schema.cpp", "kx_internal.h")] + \
+            [os.path.join(HERE, f) for f in ("emu_driver.cpp", "emu_rt.cpp", "nested_host.cpp",
+                                             os.path.join("hip", "hip_runtime.h"))]
         if not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(f) for f in srcs):
             build()
         _lib = C.CDLL(LIB)
         _lib.emu_decode.restype = C.c_int
         _lib.emu_decode.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64,
                                     C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]
+        _lib.emu_nested_decode.restype = C.c_int
+        _lib.emu_nested_decode.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64,
+                                           C.c_void_p, C.c_void_p, C.c_void_p]
+        _lib.emu_nested_encode.restype = C.c_int
+        _lib.emu_nested_encode.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64,
+                                           C.c_void_p, C.c_void_p]
         _lib.emu_crc.restype = C.c_int
         _lib.emu_crc.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_int, C.c_void_p, C.c_void_p,
                                  C.c_void_p]
@@ -105,3 +113,35 @@ def crc32c(data: np.ndarray, offs: np.ndarray, n: int, val: bool, threads: int =
                        crc.ctypes.data, rs.ctypes.data, C.addressof(st))
     assert rc == 0, rc
     return crc[:n], rs[:n], st
+
+
+def nested_decode(schema, infos, npres, data: np.ndarray, n: int, offsets=None, var_caps=None, elem_caps=None,
+                  sub_caps=None, wide: bool = False):
+    """the nested walker of the kernel source on the host: rc, columns, status, record codes"""
+    if var_caps is None:
+        var_caps = [0 if ci.kind == A.COL_FIXED else max(1, data.size) for ci in infos]
+    out = alloc_host(infos, n, var_caps, npres, wide=wide, elem_caps=elem_caps, sub_caps=sub_caps)
+    kc = to_kx_columns(out, infos, var_caps)
+    st = A.Status()
+    rs = np.zeros(max(1, n), dtype=np.uint8)
+    tab, ns = schema.struct_table()
+    offs = None if offsets is None else np.ascontiguousarray(offsets, dtype=np.uint64)
+    rc = lib().emu_nested_decode(C.cast(tab, C.c_void_p), ns, data.ctypes.data if data.size else None, data.size,
+                                 None if offs is None else offs.ctypes.data, n, C.addressof(kc), rs.ctypes.data,
+                                 C.addressof(st))
+    return rc, out, st, rs[:n]
+
+
+def nested_encode(schema, infos, cs):
+    """rc, wire bytes, record offsets of the kernel source's nested encoder on the host"""
+    kc = to_kx_columns(cs, infos)
+    tab, ns = schema.struct_table()
+    total = C.c_uint64()
+    offs = np.zeros(cs.n + 1, dtype=np.uint64)
+    rc = lib().emu_nested_encode(C.cast(tab, C.c_void_p), ns, C.addressof(kc), cs.n, None, 0, None, C.byref(total))
+    if rc and rc != A.ERR_SIZE_LIMIT:
+        return rc, None, None
+    out = np.zeros(max(1, total.value), dtype=np.uint8)
+    rc = lib().emu_nested_encode(C.cast(tab, C.c_void_p), ns, C.addressof(kc), cs.n, out.ctypes.data, total.value,
+                                 offs.ctypes.data, C.byref(total))
+    return rc, out[:total.value], offs

@@ -30,6 +30,24 @@ def _assert_list_bytes(got, exp, n, c, ci):
     assert np.array_equal(gb, eb), f"list column {c} (field {ci.field_id}) bytes differ"
 
 
+def _assert_levels(got, exp, n, c, ci):
+    """any var column: each offsets array level by level (counts per parent), then the data they reach"""
+    g = [to_np(v) for v in got]
+    e = [to_np(v) for v in exp]
+    glo, ghi, elo, ehi = 0, n, 0, n
+    for k in range(len(g) - 1):
+        ga = offsets_u64(g[k])[glo:ghi + 1]
+        ea = offsets_u64(e[k])[elo:ehi + 1]
+        bad = np.nonzero(np.diff(ga) != np.diff(ea))[0]
+        assert bad.size == 0, f"column {c} (field {ci.field_id}) array {k} counts differ at {bad[:8]}"
+        glo, ghi, elo, ehi = int(ga[0]), int(ga[-1]), int(ea[0]), int(ea[-1])
+    gd, ed = g[-1], e[-1]
+    w = gd.itemsize
+    gb = gd.view(np.uint8)[glo * w:ghi * w]
+    eb = ed.view(np.uint8)[elo * w:ehi * w]
+    assert np.array_equal(gb, eb), f"column {c} (field {ci.field_id}) data differ"
+
+
 def assert_columns_equal(got, exp, infos, n, check_presence=True):
     """Field-for-field equality of the first n records (fixed values, var bytes/elements, offsets)."""
     from kitex_amd.columns import Views
@@ -47,8 +65,8 @@ def assert_columns_equal(got, exp, infos, n, check_presence=True):
             if n:
                 bad = np.nonzero((g != e).any(axis=1))[0]
                 assert bad.size == 0, f"column {c} (field {ci.field_id}) differs at records {bad[:8]}"
-        elif ci.kind == A.COL_LIST_BYTES:
-            _assert_list_bytes(got.cols[c], exp.cols[c], n, c, ci)
+        elif ci.kind in (A.COL_LIST_BYTES, A.COL_LIST2, A.COL_LIST2_BYTES) or ci.level > 0:
+            _assert_levels(got.cols[c], exp.cols[c], n, c, ci)
         else:
             go, gd = (to_np(v) for v in got.cols[c])
             eo, ed = (to_np(v) for v in exp.cols[c])

@@ -67,8 +67,13 @@ def test_schema_rejects(kxlib):
     from kitex_amd._lib import KxError
     node = S.Struct("Node", [S.Field(1, A.T_I64)])
     node.fields.append(S.Field(2, A.T_STRUCT, child=node))
-    with pytest.raises(KxError) as e:
-        DeviceSchema(S.Schema(node))
+    assert DeviceSchema(S.Schema(node)).nested      # a recursive field is kept as its bytes (nested schema)
+    deep = S.Field(0, A.T_LIST, elem=S.Field(0, A.T_LIST, elem=A.T_I64))
+    with pytest.raises(KxError) as e:               # leaves three container levels down
+        DeviceSchema(S.Schema(S.Struct("D3", [S.Field(1, A.T_LIST, elem=deep)])))
+    assert e.value.code == A.ERR_NOT_IMPLEMENTED
+    with pytest.raises(KxError) as e:               # struct map keys
+        DeviceSchema(S.Schema(S.Struct("MK", [S.Field(1, A.T_MAP, elem=A.T_STRUCT, val=A.T_I64, child=node)])))
     assert e.value.code == A.ERR_NOT_IMPLEMENTED
     with pytest.raises(KxError):
         DeviceSchema(S.Schema(S.Struct("D", [S.Field(1, A.T_I64), S.Field(1, A.T_I32)])))

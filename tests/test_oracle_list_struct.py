@@ -23,16 +23,19 @@ def test_columns_match_device_schema(oracle):
     assert [ci.elem_ttype for ci in infos[1:5]] == [A.T_I64 | 0x40, A.T_I32 | 0x40, A.T_DOUBLE | 0x40, A.T_BOOL | 0x40]
 
 
-def test_unsupported_element_structs(oracle):
-    from kitex_amd._lib import KxError
+def test_other_element_structs_are_nested(oracle):
+    """element structs with strings or optional fields: the nested model (include/kxcodec.h), in both the
+    library and the oracle; the optional field's bit lives in the elements' presence column"""
     from kitex_amd.codec import DeviceSchema
-    bad = [S.Struct("E", [S.Field(1, A.T_STRING, "s")]),
-           S.Struct("E", [S.Field(1, A.T_I64, "x", req=A.REQ_OPTIONAL)])]
-    for es in bad:
+    wide = [S.Struct("E", [S.Field(1, A.T_STRING, "s")]),
+            S.Struct("E", [S.Field(1, A.T_I64, "x", req=A.REQ_OPTIONAL)])]
+    for k, es in enumerate(wide):
         sch = S.Schema(S.Struct("R", [S.Field(1, A.T_LIST, "l", elem=A.T_STRUCT, child=es)]))
-        assert oracle.flatten(sch)[0] == A.ERR_NOT_IMPLEMENTED
-        with pytest.raises(KxError):
-            DeviceSchema(sch)
+        rc, infos, _ = oracle.flatten(sch)
+        assert rc == 0 and DeviceSchema(sch).nested
+        assert infos[0].kind == (A.COL_LIST_BYTES if k == 0 else A.COL_LIST)
+        if k == 1:
+            assert infos[-1].elem_ttype == A.ELEM_PRESENCE and infos[0].presence_bit == 0
 
 
 def test_handmade_semantics(oracle):
