@@ -306,41 +306,56 @@ struct MsgEnc {
 
 __global__ void __launch_bounds__(MT) msgenc_kernel(MsgEnc me) {
   const uint64_t i = (uint64_t)blockIdx.x * MT + threadIdx.x;
-  if (i > me.n) return;
+  const int lane = threadIdx.x & 63;
   // the record encoder failed (SIZE_LIMIT: the scratch is too small, or a record error): its offsets were
   // never written, so nothing here may read them; the status keeps the encoder's code and counts
-  if (me.status->code != 0) return;
+  if (me.status->code != 0) return;  // uniform
   const uint64_t H = 12ull + me.name_len + 3ull;
-  const uint64_t bo = me.body_off[i];
-  if (bo > me.scratch_cap || me.body_off[me.n] > me.scratch_cap) {  // inconsistent offsets: never read past them
+  bool ok = i <= me.n;
+  const uint64_t bo = ok ? me.body_off[i] : 0;
+  if (ok && (bo > me.scratch_cap || me.body_off[me.n] > me.scratch_cap)) {  // never read past the offsets
     if (i == me.n) me.status->code = KX_ERR_SIZE_LIMIT;
-    return;
+    ok = false;
   }
   const uint64_t at = bo + i * (H + 1);
-  if (me.offsets_out) me.offsets_out[i] = at;
-  if (i == me.n) {
+  if (ok && me.offsets_out) me.offsets_out[i] = at;
+  if (ok && i == me.n) {
     me.status->n_records = me.n;
     me.status->consumed = at;
     if (at > me.out_cap) me.status->code = KX_ERR_SIZE_LIMIT;
-    return;
+    ok = false;
   }
-  const uint64_t bn = me.body_off[i + 1];
-  if (bn < bo || bn > me.scratch_cap) return;  // (thread n reports the inconsistency)
-  const uint64_t bl = bn - bo;
-  if (at > me.out_cap || me.out_cap - at < H + bl + 1) return;  // the call fails with SIZE_LIMIT (thread n)
-  uint8_t* o = me.out + at;
-  const uint32_t v = 0x80010000u | ((uint32_t)me.msg_type & 0xffu);  // strict version | type
-  const uint32_t nl = me.name_len, sq = (uint32_t)me.seqids[i];
-  o[0] = (uint8_t)(v >> 24); o[1] = (uint8_t)(v >> 16); o[2] = (uint8_t)(v >> 8); o[3] = (uint8_t)v;
-  o[4] = (uint8_t)(nl >> 24); o[5] = (uint8_t)(nl >> 16); o[6] = (uint8_t)(nl >> 8); o[7] = (uint8_t)nl;
-  for (uint32_t k = 0; k < nl; k++) o[8 + k] = me.name[k];
-  uint8_t* q = o + 8 + nl;
-  q[0] = (uint8_t)(sq >> 24); q[1] = (uint8_t)(sq >> 16); q[2] = (uint8_t)(sq >> 8); q[3] = (uint8_t)sq;
-  q[4] = KX_T_STRUCT; q[5] = (uint8_t)((uint32_t)me.body_field >> 8); q[6] = (uint8_t)me.body_field;
-  const uint8_t* b = me.bodies + me.body_off[i];
-  uint8_t* d = q + 7;
-  for (uint64_t k = 0; k < bl; k++) d[k] = b[k];
-  d[bl] = KX_T_STOP;
+  uint64_t bl = 0;
+  if (ok) {
+    const uint64_t bn = me.body_off[i + 1];
+    ok = bn >= bo && bn <= me.scratch_cap;                       // (thread n reports the inconsistency)
+    bl = ok ? bn - bo : 0;
+    ok = ok && at <= me.out_cap && me.out_cap - at >= H + bl + 1;  // else SIZE_LIMIT (thread n)
+  }
+  uint8_t* d = nullptr;
+  if (ok) {
+    uint8_t* o = me.out + at;
+    const uint32_t v = 0x80010000u | ((uint32_t)me.msg_type & 0xffu);  // strict version | type
+    const uint32_t nl = me.name_len, sq = (uint32_t)me.seqids[i];
+    o[0] = (uint8_t)(v >> 24); o[1] = (uint8_t)(v >> 16); o[2] = (uint8_t)(v >> 8); o[3] = (uint8_t)v;
+    o[4] = (uint8_t)(nl >> 24); o[5] = (uint8_t)(nl >> 16); o[6] = (uint8_t)(nl >> 8); o[7] = (uint8_t)nl;
+    for (uint32_t k = 0; k < nl; k++) o[8 + k] = me.name[k];
+    uint8_t* q = o + 8 + nl;
+    q[0] = (uint8_t)(sq >> 24); q[1] = (uint8_t)(sq >> 16); q[2] = (uint8_t)(sq >> 8); q[3] = (uint8_t)sq;
+    q[4] = KX_T_STRUCT; q[5] = (uint8_t)((uint32_t)me.body_field >> 8); q[6] = (uint8_t)me.body_field;
+    d = q + 7;
+    d[bl] = KX_T_STOP;
+  }
+  // the records' bytes: copied by the whole wave, one message after the other, 64 adjacent bytes per
+  // store instruction (a lane copying its own record would touch 64 records' lines per instruction)
+  const uint64_t src = ok ? (uint64_t)(me.bodies + bo) : 0, dst = (uint64_t)d, len = ok ? bl : 0;
+  for (int j = 0; j < 64; j++) {
+    const uint64_t lj = (uint64_t)__shfl((long long)len, j, 64);
+    if (lj == 0) continue;
+    const uint8_t* sj = (const uint8_t*)(uint64_t)__shfl((long long)src, j, 64);
+    uint8_t* dj = (uint8_t*)(uint64_t)__shfl((long long)dst, j, 64);
+    for (uint64_t k = (uint64_t)lane; k < lj; k += 64) dj[k] = sj[k];
+  }
 }
 
 // exclusive scan of name_len[0..n] in place (one workgroup; each thread a contiguous run)

@@ -7,7 +7,7 @@ import sys
 from collections import defaultdict
 
 d = sys.argv[1]
-KS = ("index_kernel<", "group_kernel<", "chain_kernel<", "emit_kernel<", "combo_kernel<")
+KS = ("index_kernel<", "group_kernel<", "chain_kernel<", "emit_kernel<", "combo_kernel<", "write_kernel<", "size_kernel<")
 agg = defaultdict(lambda: defaultdict(list))
 for p in ("p1", "p2"):
     for f in glob.glob(f"{d}/{p}/**/*counter_collection.csv", recursive=True):

@@ -359,3 +359,42 @@ def _check_views(dec, oracle, sch, wire, n, offsets, pb=False, wide=False):
             o, ln = pairs[r]
             assert ln == co[r + 1] - co[r]
             assert bytes(wire[o:o + ln]) == bytes(data[co[r]:co[r + 1]])
+
+
+# ---- the wave-cooperative numeric list emit (kx_decode.hip COOP): edge cases ----
+COOP_TYPES = [(A.T_I16, 2), (A.T_I32, 4), (A.T_I64, 8), (A.T_DOUBLE, 8)]
+
+
+def coop_schema(et):
+    return S.Schema(S.Struct("CL", [S.Field(1, A.T_I64, "id"), S.Field(2, A.T_LIST, "v", elem=et),
+                                    S.Field(3, A.T_LIST, "u", elem=A.T_I64)]))
+
+
+def coop_columns(et, w, n, seed=0):
+    """lists mostly empty, a few of 1..70 elements, one of 1500 elements (a list longer than a wave),
+    records inactive lanes of a partial last wave"""
+    from kitex_amd.synth import ColumnSet
+    rng = np.random.default_rng(seed)
+    dt = {2: np.int16, 4: np.int32, 8: np.int64}[w]
+    l1 = np.where(rng.random(n) < 0.7, 0, rng.integers(1, 71, size=n))
+    l1[n // 3] = 1500
+    o1 = np.zeros(n + 1, np.uint32)
+    o1[1:] = np.cumsum(l1)
+    v1 = rng.integers(-(1 << 62), 1 << 62, size=max(1, int(o1[-1]))).astype(dt)
+    l2 = np.where(rng.random(n) < 0.5, 0, rng.integers(1, 5, size=n))
+    o2 = np.zeros(n + 1, np.uint32)
+    o2[1:] = np.cumsum(l2)
+    v2 = rng.integers(-(1 << 62), 1 << 62, size=max(1, int(o2[-1]))).astype(np.int64)
+    ids = rng.integers(-(1 << 62), 1 << 62, size=n).astype(np.int64)
+    return ColumnSet([ids, (o1, v1), (o2, v2)], np.zeros(n, np.uint64), n)
+
+
+def case_coop_lists(dec, oracle, et, w, mode, n=1000):
+    sch = coop_schema(et)
+    cs = coop_columns(et, w, n, seed=w)
+    rc, wire, offs = oracle.encode(sch, cs)
+    assert rc == 0
+    cols, st = check_decode(dec, oracle, sch, wire, n, offsets=offs if mode == "offsets" else None)
+    assert st.code == 0
+    _, infos, _ = oracle.flatten(sch)
+    assert_columns_equal(cols, cs, infos, n, check_presence=False)

@@ -127,6 +127,12 @@ def test_emu_containers(edec, oracle, name, mode):
     DC.case_containers(edec, oracle, name, 3000, mode)
 
 
+@pytest.mark.parametrize("et,w", DC.COOP_TYPES)
+@pytest.mark.parametrize("mode", ["concat", "offsets"])
+def test_emu_coop_list_edges(edec, oracle, et, w, mode):
+    DC.case_coop_lists(edec, oracle, et, w, mode, n=300)
+
+
 def test_emu_mock_req_fault(edec, oracle):
     DC.case_mock_req_fault(edec, oracle)
 

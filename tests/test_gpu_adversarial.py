@@ -170,3 +170,49 @@ def test_binary_strings_saturated_with_signature(torch, oracle, canonical_s_per_
     _, infos, _ = oracle.flatten(sch)
     assert_columns_equal(res.columns, exp, infos, k)
     _check_time(t, wire.numel(), canonical_s_per_byte, "signature-saturated binary strings", st)
+
+
+def _nested_payload_batch(n, k=16, seed=0):
+    """{1: i64 id; 2: binary payload} whose payload is an encoded record of the same schema (a proxy
+    forwarding a request as bytes): every record holds a canonical false candidate at its payload start"""
+    rng = np.random.default_rng(seed)
+    ids = rng.integers(-(1 << 62), 1 << 62, size=n).astype(">i8")
+    iid = rng.integers(-(1 << 62), 1 << 62, size=n).astype(">i8")
+    body = rng.integers(0, 256, size=(n, k), dtype=np.uint8)
+    inner = np.zeros((n, 19 + k), dtype=np.uint8)
+    inner[:, 0:3] = [A.T_I64, 0, 1]
+    inner[:, 3:11] = iid.view(np.uint8).reshape(n, 8)
+    inner[:, 11:14] = [A.T_STRING, 0, 2]
+    inner[:, 14:18] = np.array([k], dtype=">u4").view(np.uint8)
+    inner[:, 18:18 + k] = body
+    rec = np.zeros((n, 11 + 7 + 19 + k + 1), dtype=np.uint8)
+    rec[:, 0:3] = [A.T_I64, 0, 1]
+    rec[:, 3:11] = ids.view(np.uint8).reshape(n, 8)
+    rec[:, 11:14] = [A.T_STRING, 0, 2]
+    rec[:, 14:18] = np.array([19 + k], dtype=">u4").view(np.uint8)
+    rec[:, 18:18 + 19 + k] = inner
+    return ids.astype(np.int64), inner, rec.reshape(-1)
+
+
+def test_binary_payload_holds_encoded_record(torch, oracle, canonical_s_per_byte):
+    """a binary field carrying an encoded record of the same schema (canonical, so the
+    multi-hit canonical check alone cannot reject it) -- decoded correctly within 2x canonical per byte"""
+    from kitex_amd.codec import ThriftCodec
+    dev = torch.device("cuda", 0)
+    sch = S.Schema(S.Struct("Fwd", [S.Field(1, A.T_I64, "id"), S.Field(2, A.T_STRING, "payload", binary=True)]))
+    cdc = ThriftCodec(sch)
+    ids, inner, wire_np = _nested_payload_batch(N)
+    wire = torch.from_numpy(wire_np).to(dev)
+    res, st, t = _time_decode(torch, cdc, wire, N)
+    assert st.code == 0 and st.n_records == N and st.consumed == wire.numel()
+    got = res.columns
+    assert np.array_equal(to_np(got.cols[0]), ids)
+    po, pd = got.cols[1]
+    assert np.array_equal(np.diff(to_np(po).astype(np.int64) & 0xFFFFFFFF), np.full(N, inner.shape[1]))
+    assert np.array_equal(to_np(pd[:inner.size]), inner.reshape(-1))
+    k = 3000
+    rc, exp, est, _ = oracle.decode(sch, wire_np[:k * (wire_np.size // N)], k)
+    _, infos, _ = oracle.flatten(sch)
+    assert est.code == 0
+    assert_columns_equal(got, exp, infos, k)
+    _check_time(t, wire.numel(), canonical_s_per_byte, "binary payload holding an encoded record", st)

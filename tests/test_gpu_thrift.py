@@ -378,6 +378,26 @@ def test_decode_containers_match_oracle(gdec, oracle, name, mode, n):
     DC.case_containers(gdec, oracle, name, n, mode)
 
 
+@pytest.mark.parametrize("et,w", DC.COOP_TYPES)
+@pytest.mark.parametrize("mode", ["concat", "offsets"])
+def test_coop_list_edges(gdec, oracle, et, w, mode):
+    """the wave-cooperative list copy: i16 .. double elements, a 1500-element list, mostly empty lists"""
+    DC.case_coop_lists(gdec, oracle, et, w, mode, n=5000)
+
+
+@pytest.mark.parametrize("mode", ["concat", "offsets"])
+def test_coop_list_arena_too_small(gdec, oracle, mode):
+    """a list arena one element short: SIZE_LIMIT, as the oracle reports"""
+    sch = DC.coop_schema(A.T_I64)
+    cs = DC.coop_columns(A.T_I64, 8, 3000, seed=9)
+    rc, wire, offs = oracle.encode(sch, cs)
+    need = int(cs.cols[1][0][-1])
+    caps = [0, need - 1, int(cs.cols[2][0][-1])]
+    _, st, _ = gdec.decode(sch, wire, 3000, offsets=offs if mode == "offsets" else None, caps=caps)
+    rc, _, est, _ = oracle.decode(sch, wire, 3000, offsets=offs if mode == "offsets" else None, var_caps=caps)
+    assert st.code == est.code == A.ERR_SIZE_LIMIT
+
+
 def test_mock_req_fault_vector_on_gpu(gdec, oracle):
     DC.case_mock_req_fault(gdec, oracle)
 
