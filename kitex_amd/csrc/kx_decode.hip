@@ -2091,13 +2091,13 @@ __device__ __forceinline__ bool fast_tile(KParams& dp, const Src& w, uint64_t tl
   const uint64_t plim = kmin64(seg_hi, dp.in_len >= 3 ? dp.in_len - 2 : 0ull);
   // ---- the first two hits in [seg_lo, plim) (lane 63 also tests dword 32: the up to 3 bytes of the
   //      tile past the dword grid) ----
-  uint64_t c1 = X_NONE, c2 = X_NONE;
+  uint64_t c1 = X_NONE, c2 = X_NONE, c3 = X_NONE;
   {
     // a hit whose second field header (at the plan's fixed offset) does not match is not a candidate:
     // payload bytes saturated with the signature cost a few compares instead of failed walks
     const uint32_t s2o = P->sig2_off, s2 = P->sig2;
     uint64_t hb = (uint64_t)hm | (lane == 63 ? (1ull << 32) : 0ull);   // lane 63 also looks at dword 32
-    while (hb && c2 == X_NONE) {
+    while (hb && c3 == X_NONE) {
       const int di = __ffsll((long long)hb) - 1;
       hb &= hb - 1;
       const uint32_t dq = sq + 4u * (uint32_t)di;
@@ -2111,17 +2111,20 @@ __device__ __forceinline__ bool fast_tile(KParams& dp, const Src& w, uint64_t tl
         const uint32_t pq = (uint32_t)(p - w.wpos) + s2o;
         if (s2o && pq + 8 <= (uint32_t)w.wlen && ((win_ld(w, pq) ^ s2) & 0xffffffu)) continue;
         if (c1 == X_NONE) c1 = p;
-        else { c2 = p; break; }
+        else if (c2 == X_NONE) c2 = p;
+        else { c3 = p; break; }
       }
     }
   }
-  // ---- walk: records of the segment from c1 (c2 when c1's record is not canonical) ----
+  // ---- walk: records of the segment from c1, else c2, else c3: a candidate whose walk fails anywhere
+  //      (not canonical, or a record nested in a payload: it parses, but the bytes after it do not) is
+  //      replaced by the next; the consistency check below accepts only an unbroken chain ----
   uint64_t ent = c1, ex = X_NONE, cnt = 0, st0 = 0, st1 = 0, st2 = 0, st3 = 0;
   uint64_t vsum[NV > 0 ? NV : 1];
 #pragma unroll
   for (int v = 0; v < (NV > 0 ? NV : 1); v++) vsum[v] = 0;
   bool bad = false;
-  for (int attempt = 0; attempt < 2; attempt++) {
+  for (int attempt = 0; attempt < 3; attempt++) {
     bool again = false;
     if (ent != X_NONE) {
       uint32_t q = (uint32_t)(ent - w.wpos);
@@ -2138,14 +2141,15 @@ __device__ __forceinline__ bool fast_tile(KParams& dp, const Src& w, uint64_t tl
         st2 = c == 2 ? start : st2; st3 = c == 3 ? start : st3;
         c++;
       }
-      if (!ok && c == 0) {
-        // the hit does not start a canonical record (a nested struct's header, a false hit): try the
-        // segment's next hit, else the lane has no candidate (the consistency check below then catches
-        // a record start that is there but not canonical)
-        ent = attempt == 0 ? c2 : X_NONE;
+      if (!ok) {
+        // not a record start of a canonical chain (a nested struct's header, a false hit, a record inside
+        // a binary payload): try the segment's next hit, else the lane has no candidate (the consistency
+        // check below then catches a record start that is there but not canonical)
+        ent = attempt == 0 ? c2 : attempt == 1 ? c3 : X_NONE;
         again = ent != X_NONE;
+        if (!again) { ex = X_NONE; cnt = 0; }
       } else {
-        bad = !ok || c > 4;
+        bad = c > 4;
         ex = w.wpos + q;
         cnt = c;
 #pragma unroll

@@ -15,6 +15,8 @@
 //      before they touch LDS.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "kx_internal.h"
 
 namespace {
@@ -124,14 +126,17 @@ __device__ __forceinline__ uint64_t record_size(const KxProgram& P, const KxLaun
 // A put of k bytes stores at most one dword and has no loop, so lanes whose records start at
 // different alignments only differ in a predicated store (the old byte-draining loop diverged on
 // every field).
-struct Sink {
-  uint8_t* base;   // LDS image or global output
+typedef __attribute__((address_space(3))) uint8_t LDSB;  // the LDS image (ds_write, not flat stores)
+
+template <class B>
+struct SinkT {
+  B* base;         // LDS image or global output
   uint64_t off;    // dword-aligned position of the pending bytes
   uint64_t acc;    // pending bytes (including `head` placeholder bytes), first in bits 0..7
   uint32_t n;      // pending bytes (< 4 between puts)
   uint32_t head;   // leading bytes of the first dword not owned by this record (0 once it is written)
 
-  __device__ __forceinline__ Sink(uint8_t* b, uint64_t o)
+  __device__ __forceinline__ SinkT(B* b, uint64_t o)
       : base(b), off(o & ~3ull), acc(0), n((uint32_t)(o & 3)), head((uint32_t)(o & 3)) {}
 
   __device__ __forceinline__ void emit_dword() {
@@ -140,7 +145,8 @@ struct Sink {
       for (uint32_t k = head; k < 4; k++) base[off + k] = (uint8_t)(v >> (8 * k));
       head = 0;
     } else {
-      *(uint32_t*)(base + off) = v;
+      *(typename std::conditional<std::is_same<B, LDSB>::value, __attribute__((address_space(3))) uint32_t,
+                                  uint32_t>::type*)(base + off) = v;
     }
     off += 4; acc >>= 32; n -= 4;
   }
@@ -157,8 +163,11 @@ struct Sink {
   // the position of the next byte
   __device__ __forceinline__ uint64_t pos() const { return off + n; }
 };
+using Sink = SinkT<uint8_t>;   // global (the direct path)
+using LSink = SinkT<LDSB>;     // the LDS image
 
-__device__ __forceinline__ void put_be(Sink& s, uint64_t v, uint32_t w) {
+template <class SK>
+__device__ __forceinline__ void put_be(SK& s, uint64_t v, uint32_t w) {
   switch (w) {
     case 1: s.put((uint32_t)v, 1); break;
     case 2: s.put(((uint32_t)v >> 8 & 0xff) | (((uint32_t)v & 0xff) << 8), 2); break;
@@ -182,7 +191,8 @@ __device__ __forceinline__ uint64_t load_fixed(const void* base, uint32_t w, uin
 // raw bytes into the sink: blocks of up to 64 bytes whose dword loads are all issued before the first
 // is used (one memory round trip per block instead of one per 4 bytes: the encoder's write pass was
 // latency-bound on these loads)
-__device__ __forceinline__ void put_bytes(Sink& s, const uint8_t* src, uint32_t len) {
+template <class SK>
+__device__ __forceinline__ void put_bytes(SK& s, const uint8_t* src, uint32_t len) {
   const uint64_t sa = (uint64_t)src, se = sa + len;
   const uint32_t sh = (uint32_t)(sa & 3);
   uint64_t A = sa & ~3ull;  // aligned dwords that hold string bytes only
@@ -284,9 +294,10 @@ __device__ __forceinline__ bool defer(const PayQueue& pq, uint64_t dst, const vo
 }
 
 // FastWriteNocopy for one record into the sink
-template <bool LS>
-__device__ __forceinline__ void write_record(const KxProgram& P, const KxLaunchCols& C, uint64_t r, Sink& s,
+template <bool LS, class SK>
+__device__ __forceinline__ void write_record(const KxProgram& P, const KxLaunchCols& C, uint64_t r, SK& s,
                                              const PayQueue& pq) {
+  constexpr bool GL = std::is_same<SK, Sink>::value;   // payload queueing: the global (direct) path only
   uint64_t pres = C.presence ? C.presence[r] : 0;
   int inst = 0;
   int f = P.inst[0].enc_first;
@@ -312,13 +323,15 @@ __device__ __forceinline__ void write_record(const KxProgram& P, const KxLaunchC
       uint32_t len = (uint32_t)var_len(C, F.col, r);
       put_be(s, len, 4);
       const uint8_t* src = (const uint8_t*)C.data[F.col] + o;
-      if (len >= DEFER_MIN && pq.q) {
-        const uint64_t at = s.pos();
-        if (defer(pq, (uint64_t)s.base + at, src, len, 1)) {
-          s.flush();
-          s = Sink(s.base, at + len);
-          f = F.enc_next;
-          continue;
+      if constexpr (GL) {
+        if (len >= DEFER_MIN && pq.q) {
+          const uint64_t at = s.pos();
+          if (defer(pq, (uint64_t)s.base + at, src, len, 1)) {
+            s.flush();
+            s = Sink(s.base, at + len);
+            f = F.enc_next;
+            continue;
+          }
         }
       }
       put_bytes(s, src, len);
@@ -328,13 +341,15 @@ __device__ __forceinline__ void write_record(const KxProgram& P, const KxLaunchC
       s.put(F.elem, 1);
       put_be(s, cnt, 4);
       const void* src = C.data[F.col];
-      if (cnt && pq.q && F.elem != KX_T_BOOL && F.width > 1) {
-        const uint64_t at = s.pos();
-        if (defer(pq, (uint64_t)s.base + at, (const uint8_t*)src + o * F.width, cnt, F.width)) {
-          s.flush();
-          s = Sink(s.base, at + (uint64_t)cnt * F.width);
-          f = F.enc_next;
-          continue;
+      if constexpr (GL) {
+        if (cnt && pq.q && F.elem != KX_T_BOOL && F.width > 1) {
+          const uint64_t at = s.pos();
+          if (defer(pq, (uint64_t)s.base + at, (const uint8_t*)src + o * F.width, cnt, F.width)) {
+            s.flush();
+            s = Sink(s.base, at + (uint64_t)cnt * F.width);
+            f = F.enc_next;
+            continue;
+          }
         }
       }
 #if KX_ENC_LISTPF
@@ -421,7 +436,8 @@ __device__ __forceinline__ uint32_t uvarint_len(uint64_t v) {
   return (uint32_t)((bits + 6) / 7);
 }
 
-__device__ __forceinline__ void put_uvarint(Sink& s, uint64_t v) {
+template <class SK>
+__device__ __forceinline__ void put_uvarint(SK& s, uint64_t v) {
   while (v >= 0x80) {
     s.put((uint32_t)(v & 0x7f) | 0x80u, 1);
     v >>= 7;
@@ -466,7 +482,8 @@ __device__ __forceinline__ uint64_t pb_record_size(const KxProgram& P, const KxL
   return 1 + uvarint_len(b) + b;
 }
 
-__device__ __forceinline__ void pb_write_record(const KxProgram& P, const KxLaunchCols& C, uint64_t r, Sink& s) {
+template <class SK>
+__device__ __forceinline__ void pb_write_record(const KxProgram& P, const KxLaunchCols& C, uint64_t r, SK& s) {
   s.put(0x0Au, 1);
   put_uvarint(s, pb_body_size(P, C, r));
   const uint64_t pres = C.presence ? C.presence[r] : 0;
@@ -501,11 +518,70 @@ __device__ __forceinline__ uint64_t any_size(const EncParams& ep, const KxProgra
   return ep.pb ? pb_record_size(P, ep.cols, r) : record_size<LS>(P, ep.cols, r);
 }
 
-template <bool LS>
-__device__ __forceinline__ void any_write(const EncParams& ep, const KxProgram& P, uint64_t r, Sink& s,
+template <bool LS, class SK>
+__device__ __forceinline__ void any_write(const EncParams& ep, const KxProgram& P, uint64_t r, SK& s,
                                           const PayQueue& pq = PayQueue{nullptr, nullptr}) {
   if (ep.pb) pb_write_record(P, ep.cols, r, s);
   else write_record<LS>(P, ep.cols, r, s, pq);
+}
+
+// FastWriteNocopy of a record with the canonical plan (kx_program.h: encoder order, every field present,
+// nil-free structs): a run of fixed-width fields loads all its values before the first is written (one
+// memory round trip per run), strings and lists follow their headers. Same bytes as write_record.
+template <class SK>
+__device__ __forceinline__ void write_canon(const KxProgram& P, const KxLaunchCols& C, uint64_t r, SK& s) {
+  const uint32_t ns = P.nsteps;
+  for (uint32_t k = 0; k < ns;) {
+    const KxpStep st = P.steps[k];
+    if (st.kind == KXP_S_FIXED) {
+      const uint32_t m = min(st.hdr >> 24, 8u);
+      uint64_t v[8];
+#pragma unroll
+      for (uint32_t j = 0; j < 8; j++) {
+        const KxpStep sj = P.steps[k + (j < m ? j : 0)];
+        v[j] = j < m ? load_fixed(C.data[sj.col], sj.width, r) : 0;
+      }
+#pragma unroll
+      for (uint32_t j = 0; j < 8; j++) {
+        if (j >= m) break;
+        const KxpStep sj = P.steps[k + j];
+        s.put(sj.hdr & 0xffffffu, 3);
+        uint64_t x = v[j];
+        if ((sj.hdr & 0xffu) == KX_T_BOOL) x = (x & 0xff) ? 1 : 0;
+        put_be(s, x, sj.width);
+      }
+      k += m;
+      continue;
+    }
+    k++;
+    if (st.kind == KXP_S_END) { s.put(KX_T_STOP, 1); continue; }
+    s.put(st.hdr & 0xffffffu, 3);
+    if (st.kind == KXP_S_STRUCT) continue;
+    const uint64_t o = off_at(C, st.col, r);
+    const uint32_t len = (uint32_t)(off_at(C, st.col, r + 1) - o);
+    if (st.kind == KXP_S_BYTES) {
+      put_be(s, len, 4);
+      put_bytes(s, (const uint8_t*)C.data[st.col] + o, len);
+      continue;
+    }
+    const KxpCol& K = P.col[st.col];   // KXP_S_LIST: list<scalar>
+    s.put(K.elem, 1);
+    put_be(s, len, 4);
+    const void* src = C.data[st.col];
+    for (uint32_t i0 = 0; i0 < len; i0 += 4) {
+      uint64_t V[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) V[u] = i0 + u < len ? load_fixed(src, K.width, o + i0 + u) : 0;
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        if (i0 + u >= len) break;
+        uint64_t x = V[u];
+        if (K.elem == KX_T_BOOL) x = (x & 0xff) ? 1 : 0;
+        put_be(s, x, K.width);
+      }
+    }
+  }
+  s.flush();
 }
 
 __device__ __forceinline__ uint64_t wave_incl_scan(uint64_t v, int lane) {
@@ -579,10 +655,12 @@ __global__ void __launch_bounds__(1024) scan_kernel(EncParams ep) {
   }
 }
 
-template <bool LS>
 #ifndef KX_ENC_LB
 #define KX_ENC_LB 1
 #endif
+// CANON: the schema has a canonical plan (flat Thrift, no optional field): records whose structs are all
+// present are written by write_canon into the LDS image (its own instantiation)
+template <bool LS, bool CANON>
 __global__ void __launch_bounds__(WT, KX_ENC_LB) write_kernel(EncParams ep) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   uint8_t* img = (uint8_t*)smem_raw;                        // OUTB + 32
@@ -642,8 +720,11 @@ __global__ void __launch_bounds__(WT, KX_ENC_LB) write_kernel(EncParams ep) {
       continue;
     }
     if (threadIdx.x < take) {
-      Sink s(img, skew + pre);
-      any_write<LS>(ep, P, my, s);
+      LSink s((LDSB*)img, skew + pre);
+      if (CANON && (!ep.cols.presence || (ep.cols.presence[my] & P.canon_pres) == P.canon_pres))
+        write_canon(P, ep.cols, my, s);
+      else
+        any_write<LS>(ep, P, my, s);
       if (ep.offsets_out) ep.offsets_out[my] = gpos + pre;
     }
     __syncthreads();
@@ -700,8 +781,12 @@ int kx_launch_encode(const KxProgram* dprog, const KxProgram& hprog, const KxLau
   hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, stream, ep);
   KX_HIP_CHECK(hipGetLastError());
   size_t shmem = OUTB + 32 + sizeof(KxProgram) + 8 * (WT / 64);
-  if (ls) hipLaunchKernelGGL(write_kernel<true>, dim3((unsigned)ep.nblocks), dim3(WT), shmem, stream, ep);
-  else hipLaunchKernelGGL(write_kernel<false>, dim3((unsigned)ep.nblocks), dim3(WT), shmem, stream, ep);
+  static int canon_env = -1;  // KX_ENC_CANON=0: the generic writer for every record (A/B)
+  if (canon_env < 0) { const char* e = getenv("KX_ENC_CANON"); canon_env = e ? atoi(e) : 1; }
+  const bool canon = canon_env && !pb && hprog.nsteps > 0;
+  if (ls) hipLaunchKernelGGL((write_kernel<true, false>), dim3((unsigned)ep.nblocks), dim3(WT), shmem, stream, ep);
+  else if (canon) hipLaunchKernelGGL((write_kernel<false, true>), dim3((unsigned)ep.nblocks), dim3(WT), shmem, stream, ep);
+  else hipLaunchKernelGGL((write_kernel<false, false>), dim3((unsigned)ep.nblocks), dim3(WT), shmem, stream, ep);
   KX_HIP_CHECK(hipGetLastError());
   return KX_OK;
 }

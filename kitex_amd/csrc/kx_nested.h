@@ -92,6 +92,8 @@ struct KxnRoot {        // an instance root: the record, or one element / entry 
   uint8_t level;
   uint8_t pad;
   int16_t pres_col;     // level >= 1: column of its presence words, -1 (level 0: kx_columns.presence)
+  int16_t dcur;         // level >= 1: the cursor of its element domain (-1 for the record)
+  int16_t pad2;
   uint16_t ent_lo, ent_hi;  // offsets entries written when an instance starts (P.ent)
   uint16_t dfl_lo, dfl_hi;  // scalar defaults written when it starts (P.dfl)
   uint16_t sdf_lo, sdf_hi;  // string defaults written at its end when the field was not seen (P.sdf)
@@ -347,10 +349,16 @@ struct KxnFrame {
   int64_t rem;      // LIST / MAP: elements left
 };
 
+// Writes are clipped to the record's own extent of every cursor ([base, lim) from the measure pass):
+// an occurrence that a later one of the same field replaces may have been longer, and what it wrote
+// past the record's final extent belongs to the next record (another lane). Inside the extent every
+// byte / element is written again by a later, final occurrence.
 struct KxnState {
   uint64_t idx[3];    // index of the open instance per level
   uint64_t seen[3];   // seen masks per level
   uint64_t pres[3];   // presence words per level
+  bool live[3];       // the open instance lies inside the record's extent of its domain (writes allowed)
+  const uint64_t* lim;  // W: per cursor, the end of the record's extent
 };
 
 // an instance of root R at index e starts: offsets entries, scalar defaults
@@ -362,6 +370,8 @@ KXN_HD void kxn_inst_start(const KxnProgram& P, const KxnCols& C, int R, uint64_
   S.seen[RT.level] = 0;
   S.pres[RT.level] = 0;
   if (!W) return;
+  S.live[RT.level] = RT.level == 0 || e < S.lim[RT.dcur];
+  if (!S.live[RT.level]) return;
   for (int k = RT.ent_lo; k < RT.ent_hi; k++) {
     const KxnEntry& E = P.ent[k];
     kxn_put_arr(C, E.col, E.arr, e, cur[E.cur]);
@@ -378,10 +388,11 @@ KXN_HD void kxn_inst_end(const KxnProgram& P, const KxnCols& C, int R, uint64_t*
     const KxnSdef& D = P.sdf[k];
     if ((S.seen[L] >> D.sbit) & 1) continue;
     if (W)
-      for (uint32_t j = 0; j < D.len; j++) ((uint8_t*)C.data[D.col])[cur[D.cur] + j] = P.defb[D.off + j];
+      for (uint32_t j = 0; j < D.len; j++)
+        if (cur[D.cur] + j < S.lim[D.cur]) ((uint8_t*)C.data[D.col])[cur[D.cur] + j] = P.defb[D.off + j];
     cur[D.cur] += D.len;
   }
-  if (!W) return;
+  if (!W || !S.live[L]) return;
   if (L == 0) {
     if (C.presence) C.presence[S.idx[0]] = S.pres[0];
   } else if (RT.pres_col >= 0) {
@@ -398,7 +409,7 @@ KXN_HD int kxn_value(const KxnProgram& P, const KxnCols& C, const uint8_t* b, ui
   switch (N.kind) {
     case KN_SCALAR: {
       if (*q + N.width > len) return KX_ERR_EOF;
-      if (W) kxn_put_val(C, N.col, N.width, S.idx[N.level], kxn_scalar(N.ttype, b + *q));
+      if (W && S.live[N.level]) kxn_put_val(C, N.col, N.width, S.idx[N.level], kxn_scalar(N.ttype, b + *q));
       *q += N.width;
       return KX_OK;
     }
@@ -409,7 +420,9 @@ KXN_HD int kxn_value(const KxnProgram& P, const KxnCols& C, const uint8_t* b, ui
       if (*q + 4 + (uint64_t)l > len) return KX_ERR_EOF;
       if (W) {
         uint8_t* dst = (uint8_t*)C.data[N.col] + cur[N.cur];
-        for (int32_t j = 0; j < l; j++) dst[j] = b[*q + 4 + j];
+        const uint64_t room = S.lim[N.cur] > cur[N.cur] ? S.lim[N.cur] - cur[N.cur] : 0;
+        const uint64_t m = (uint64_t)l < room ? (uint64_t)l : room;
+        for (uint64_t j = 0; j < m; j++) dst[j] = b[*q + 4 + j];
       }
       cur[N.cur] += (uint64_t)l;
       *q += 4 + (uint64_t)l;
@@ -421,7 +434,9 @@ KXN_HD int kxn_value(const KxnProgram& P, const KxnCols& C, const uint8_t* b, ui
       if (rc) return rc;
       if (W) {
         uint8_t* dst = (uint8_t*)C.data[N.col] + cur[N.cur];
-        for (uint64_t j = *q; j < e; j++) dst[j - *q] = b[j];
+        const uint64_t room = S.lim[N.cur] > cur[N.cur] ? S.lim[N.cur] - cur[N.cur] : 0;
+        const uint64_t m = e - *q < room ? e - *q : room;
+        for (uint64_t j = 0; j < m; j++) dst[j] = b[*q + j];
       }
       cur[N.cur] += e - *q;
       *q = e;
@@ -456,12 +471,14 @@ KXN_HD int kxn_value(const KxnProgram& P, const KxnCols& C, const uint8_t* b, ui
 }
 
 // FastRead of record r = b[0 .. len). cur: cursors (measure: from 0, write: at the record's bases);
-// snap: KXN_MAX_SNAP slots. *used = bytes of the struct.
+// lim (write): the ends of the record's extents; snap: KXN_MAX_SNAP slots. *used = bytes of the struct.
 template <bool W>
 KXN_HD int kxn_read_record(const KxnProgram& P, const KxnCols& C, const uint8_t* b, uint64_t len, uint64_t r,
-                           uint64_t* cur, uint64_t* snap, uint64_t* used) {
+                           uint64_t* cur, uint64_t* snap, uint64_t* used, const uint64_t* lim = nullptr) {
   KxnFrame stk[KXN_STACK];
   KxnState S;
+  S.lim = lim;
+  S.live[0] = S.live[1] = S.live[2] = true;
   S.idx[0] = S.idx[1] = S.idx[2] = 0;
   S.seen[0] = S.seen[1] = S.seen[2] = 0;
   S.pres[0] = S.pres[1] = S.pres[2] = 0;
@@ -500,7 +517,7 @@ KXN_HD int kxn_read_record(const KxnProgram& P, const KxnCols& C, const uint8_t*
           for (int k = N.cur_lo; k < N.cur_hi; k++) cur[k] = snap[G.snap + k - N.cur_lo];
           if (N.kind == KN_STRUCT) {                            // a fresh NewX()
             const KxnStruct& U = P.st[N.a];
-            if (W)
+            if (W && S.live[L])
               for (int k = U.dfl_lo; k < U.dfl_hi; k++)
                 kxn_put_val(C, P.dfl[k].col, P.dfl[k].width, S.idx[L], (uint64_t)P.dfl[k].v);
             S.seen[L] &= ~U.sub_mask;
@@ -511,7 +528,7 @@ KXN_HD int kxn_read_record(const KxnProgram& P, const KxnCols& C, const uint8_t*
         }
       } else if (N.kind == KN_STRUCT && (S.seen[L] & bit)) {  // repeated struct without var fields
         const KxnStruct& U = P.st[N.a];
-        if (W)
+        if (W && S.live[L])
           for (int k = U.dfl_lo; k < U.dfl_hi; k++)
             kxn_put_val(C, P.dfl[k].col, P.dfl[k].width, S.idx[L], (uint64_t)P.dfl[k].v);
         S.seen[L] &= ~U.sub_mask;

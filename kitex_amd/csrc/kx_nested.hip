@@ -169,19 +169,20 @@ __global__ void __launch_bounds__(NT) write_kernel(NParams p) {
   for (int j = 0; j < RB / NT; j++) {
     const uint64_t r = b * RB + (uint64_t)j * NT + threadIdx.x;
     const bool act = r < p.n;
-    uint64_t cur[CUR], snap[SNAP];
+    uint64_t cur[CUR], lim[CUR], snap[SNAP];
     for (uint32_t k = 0; k < p.ncur; k++) {
       const uint64_t x = act ? p.counts[(uint64_t)k * p.n + r] : 0;
       uint64_t tot;
       const uint64_t pre = wg_excl(x, &tot, sh);
       cur[k] = carry[k] + pre;
+      lim[k] = cur[k] + x;
       carry[k] += tot;
     }
     if (!act) continue;
     const uint8_t rc = p.rcode[r];
     uint64_t a = 0, e = 0, used = 0;
     if (rc == 0 && extent(p, r, &a, &e) == 0) {
-      (void)kxn_read_record<true>(P, *p.C, p.in + a, e - a, r, cur, snap, &used);
+      (void)kxn_read_record<true>(P, *p.C, p.in + a, e - a, r, cur, snap, &used, lim);
     } else {
       kxn_failed_record(P, *p.C, r, cur);
     }

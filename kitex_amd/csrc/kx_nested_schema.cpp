@@ -205,6 +205,7 @@ struct NB {
       P.node[X].kind = map ? KN_MAP : KN_LIST;
       P.node[X].cur = (int16_t)dc;
       P.node[X].root = (int16_t)ER;
+      P.root[ER].dcur = (int16_t)dc;
       const int16_t save = chain[level];
       chain[level] = (int16_t)dc;
       roots[ER].c_lo = (int)s->ncols;
@@ -267,6 +268,7 @@ struct NB {
     memset(&P.root[R], 0, sizeof(KxnRoot));
     P.root[R].level = (uint8_t)level;
     P.root[R].pres_col = -1;
+    P.root[R].dcur = -1;
     roots.emplace_back();
     roots.back().level = level;
     return R;

@@ -17,3 +17,11 @@ if [ "${SQ:-1}" = 1 ]; then
 fi
 [ "${BENCH:-1}" = 1 ] && step bench 400 python -u bench.py --steps 10 --warmup 3 --no-cpu --no-host
 echo r3_run2 done
+if [ "${ENC_AB:-0}" = 1 ]; then
+  for c in 0 1; do
+    KX_ENC_CANON=$c step enc_canon$c 300 python -u bench.py --steps 10 --warmup 3 --no-cpu --no-host
+    python3 -c "
+import json; d=json.loads(open('gpurun_out/enc_canon$c.log').read().strip().splitlines()[-1]); x=d['extra']
+print('canon=$c', {k:(round(v['ms_per_step'],3), v.get('bit_exact')) for k,v in x.items() if k.endswith('encode')})"
+  done
+fi

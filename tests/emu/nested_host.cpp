@@ -63,7 +63,7 @@ extern "C" int emu_nested_decode(const kx_struct_desc* structs, uint32_t ns, con
   // measure
   std::vector<uint64_t> cnt((size_t)P.ncur * n, 0);
   std::vector<uint8_t> code(n, 0);
-  std::vector<uint64_t> cur(KXN_MAX_CUR), snap(KXN_MAX_SNAP);
+  std::vector<uint64_t> cur(KXN_MAX_CUR), lim(KXN_MAX_CUR), snap(KXN_MAX_SNAP);
   uint64_t first = n;
   for (uint64_t r = 0; r < n; r++) {
     if (!offsets && (r > nok || (r == nok && !skip_rc))) { code[r] = 0xff; continue; }
@@ -88,11 +88,17 @@ extern "C" int emu_nested_decode(const kx_struct_desc* structs, uint32_t ns, con
     for (int k = 1; k < K.narr; k++) over |= tot[K.acur[k - 1]] > C.cap[c][1 + k];
     if (over) { st->code = KX_ERR_SIZE_LIMIT; return KX_ERR_SIZE_LIMIT; }
   }
-  // write
-  for (uint64_t r = 0; r < n; r++) {
-    for (uint32_t k = 0; k < P.ncur; k++) cur[k] = base[(size_t)k * n + r];
+  // write (records in reverse order: what a replaced occurrence writes past its record's extent would
+  // corrupt the next record if it were not clipped, as on the device where records run in parallel)
+  for (uint64_t rr = n; rr-- > 0;) {
+    const uint64_t r = rr;
+    for (uint32_t k = 0; k < P.ncur; k++) {
+      cur[k] = base[(size_t)k * n + r];
+      lim[k] = cur[k] + cnt[(size_t)k * n + r];
+    }
     uint64_t used = 0;
-    if (code[r] == 0) (void)kxn_read_record<true>(P, C, in + a[r], b[r] - a[r], r, cur.data(), snap.data(), &used);
+    if (code[r] == 0)
+      (void)kxn_read_record<true>(P, C, in + a[r], b[r] - a[r], r, cur.data(), snap.data(), &used, lim.data());
     else kxn_failed_record(P, C, r, cur.data());
     if (rstat && offsets) rstat[r] = code[r] == 0xff ? 0 : code[r];
   }

@@ -141,8 +141,8 @@ class Writer:
             g = []
             if r.random() < 0.25:   # an earlier occurrence of the same field with other content: overwritten
                 ty = field_type(f)
-                other = Gen(int(r.integers(0, 1 << 30))).value(ty)
-                g.append(bytes([wire_type(ty)]) + _st.pack(">h", f.id) + self.value(ty, other))
+                other = Gen(int(r.integers(0, 1 << 30))).value(ty)   # written plainly: bounded depth
+                g.append(bytes([wire_type(ty)]) + _st.pack(">h", f.id) + Writer().value(ty, other))
             g.append(b)
             groups.append(g)
             if r.random() < 0.2:    # an unknown field id (skipped)
