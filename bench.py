@@ -456,17 +456,19 @@ def extras(args, r2, dev, local):
         ok = bool(torch.equal(buf, b.wire))
         avg = sum(per) / len(per) / 1e3
         alg = b.out_bytes_per_record() * b.n + b.in_bytes      # columns in + wire out
+        traffic, tnote = pmc_traffic(f"{b.cfg}_encode")
         return {"records_per_s": b.n * steps / t, "ms_per_step": t / steps * 1e3, "bit_exact": ok,
-                "roofline": roofline(alg, avg, "encode (size pass + scan + write pass)")}
+                "roofline": roofline(alg, avg, "encode (size pass + scan + write pass)", traffic, tnote)}
 
     def decode_entry(b):
         t, per = time_steps(b.step, steps, warm, 1, dev)
         avg = sum(per) / len(per) / 1e3
         ok = b.verify()
         st = b.status()
+        traffic, tnote = pmc_traffic(f"{b.cfg}_{b.mode}") if not getattr(b, "views", False) else (None, None)
         return {"records_per_s": b.n * steps / t, "ms_per_step": t / steps * 1e3, "verified": ok,
                 "decode_diag": {"tile_rewalks": st.diag[0], "group_rescans": st.diag[1]},
-                "roofline": roofline(b.in_bytes + b.out_bytes_per_record() * b.n, avg, "decode")}
+                "roofline": roofline(b.in_bytes + b.out_bytes_per_record() * b.n, avg, "decode", traffic, tnote)}
 
     def crc_entry(b):
         """CRC32C (crcPayloadValidator.Generate, validate.go:187-217) of every encoded R2 record"""

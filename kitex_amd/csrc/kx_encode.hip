@@ -32,8 +32,9 @@ constexpr int RB = 1024;             // records per block
 #define KX_ENC_LISTPF 1
 #endif
 // the write pass stages a round through the LDS image when at least cnt >> KX_ENC_MINTAKE of its records fit
+// (2: a quarter; measured R3 encode 5.91 -> 5.34 ms on the MI355X with the LDS sink, R2 unchanged)
 #ifndef KX_ENC_MINTAKE
-#define KX_ENC_MINTAKE 1
+#define KX_ENC_MINTAKE 2
 #endif
 #ifndef KX_ENC_OUTB
 #define KX_ENC_OUTB (48 * 1024)

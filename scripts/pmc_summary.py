@@ -3,6 +3,7 @@ and HBM bytes per decode call from the PMC passes (MI355X_MICROARCH.md HBM secti
 WRITE_SIZE are in KiB; gfx950 FETCH_SIZE counts half of a wide streaming read -> x2).
 
   python scripts/pmc_summary.py <gpurun_out/prof_TAG> <cfg> <mode>  -> profiles/pmc_<cfg>_<mode>.json
+  mode "encode": the encode kernels (size pass, scan, write pass) of scripts/run_encode.py instead
 """
 import csv
 import glob
@@ -12,10 +13,12 @@ import sys
 from collections import defaultdict
 
 DECODE = ("index_kernel", "group_kernel", "chain_kernel", "emit_kernel", "finalize_kernel")
+ENCODE = ("size_kernel", "scan_kernel", "write_kernel")
+KERNELS = DECODE
 
 
 def short(name):
-    for k in DECODE:
+    for k in KERNELS:
         if "namespace)::" + k in name:
             return k
     return None
@@ -33,15 +36,18 @@ def counter_sums(path, counter):
 
 
 def main():
+    global KERNELS
     d, cfg, mode = sys.argv[1], sys.argv[2], sys.argv[3]
+    KERNELS = ENCODE if mode == "encode" else DECODE
+    last = "write_kernel" if mode == "encode" else "emit_kernel"
     fetch = counter_sums(os.path.join(d, "fetch"), "FETCH_SIZE")
     write = counter_sums(os.path.join(d, "write"), "WRITE_SIZE")
-    calls = len(fetch.get("emit_kernel", [])) or 1
+    calls = len(fetch.get(last, [])) or 1
     kib = 1024.0
     fetch_b = sum(sum(v) for v in fetch.values()) * kib * 2 / calls
     write_b = sum(sum(v) for v in write.values()) * kib / calls
     per_kernel = {k: {"fetch_bytes": sum(fetch.get(k, [])) * kib * 2 / calls,
-                      "write_bytes": sum(write.get(k, [])) * kib / calls} for k in DECODE}
+                      "write_bytes": sum(write.get(k, [])) * kib / calls} for k in KERNELS}
     dur = defaultdict(list)
     for f in glob.glob(os.path.join(d, "stats", "**", "*kernel_trace.csv"), recursive=True):
         with open(f) as fh:
@@ -55,12 +61,12 @@ def main():
             sha = fh.read().strip()
     except OSError:
         pass
-    res = {"workload": f"{cfg}_decode_{mode}", "calls": calls, "lib_sha256": sha,
+    res = {"workload": f"{cfg}_encode" if mode == "encode" else f"{cfg}_decode_{mode}", "calls": calls, "lib_sha256": sha,
            "hbm_bytes_per_launch": fetch_b + write_b, "fetch_bytes_per_call": fetch_b,
            "write_bytes_per_call": write_b, "per_kernel": per_kernel,
            "avg_ms": {k: sum(v) / len(v) for k, v in dur.items() if v},
            "note": "FETCH_SIZE x2 (gfx950 wide-read correction) + WRITE_SIZE, KiB -> bytes, summed over the "
-                   "decode kernels of one call; Infinity-Cache hits are counted by these counters; bench.py "
+                   "kernels of one call; Infinity-Cache hits are counted by these counters; bench.py "
                    "uses it only when lib_sha256 matches the library it times"}
     out = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles",
                        f"pmc_{cfg}_{mode}.json")

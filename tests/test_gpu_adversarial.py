@@ -201,17 +201,18 @@ def test_binary_payload_holds_encoded_record(torch, oracle, canonical_s_per_byte
     dev = torch.device("cuda", 0)
     sch = S.Schema(S.Struct("Fwd", [S.Field(1, A.T_I64, "id"), S.Field(2, A.T_STRING, "payload", binary=True)]))
     cdc = ThriftCodec(sch)
-    ids, inner, wire_np = _nested_payload_batch(N)
+    n = 3 << 20          # 54-byte records: about the other batches' 175 MB
+    ids, inner, wire_np = _nested_payload_batch(n)
     wire = torch.from_numpy(wire_np).to(dev)
-    res, st, t = _time_decode(torch, cdc, wire, N)
-    assert st.code == 0 and st.n_records == N and st.consumed == wire.numel()
+    res, st, t = _time_decode(torch, cdc, wire, n)
+    assert st.code == 0 and st.n_records == n and st.consumed == wire.numel()
     got = res.columns
     assert np.array_equal(to_np(got.cols[0]), ids)
     po, pd = got.cols[1]
-    assert np.array_equal(np.diff(to_np(po).astype(np.int64) & 0xFFFFFFFF), np.full(N, inner.shape[1]))
+    assert np.array_equal(np.diff(to_np(po).astype(np.int64) & 0xFFFFFFFF), np.full(n, inner.shape[1]))
     assert np.array_equal(to_np(pd[:inner.size]), inner.reshape(-1))
     k = 3000
-    rc, exp, est, _ = oracle.decode(sch, wire_np[:k * (wire_np.size // N)], k)
+    rc, exp, est, _ = oracle.decode(sch, wire_np[:k * (wire_np.size // n)], k)
     _, infos, _ = oracle.flatten(sch)
     assert est.code == 0
     assert_columns_equal(got, exp, infos, k)
