@@ -514,8 +514,25 @@ __device__ __forceinline__ void pb_write_record(const KxProgram& P, const KxLaun
   s.flush();
 }
 
-template <bool LS>
+// BLength of a canonical record (every field present, structs non-nil): the plan's fixed bytes plus the
+// payloads of its var steps
+__device__ __forceinline__ uint64_t canon_size(const KxProgram& P, const KxLaunchCols& C, uint64_t r) {
+  uint64_t sz = P.canon_fixed;
+  for (uint32_t k = 0; k < P.nsteps; k++) {
+    const KxpStep st = P.steps[k];
+    if (st.kind == KXP_S_BYTES || st.kind == KXP_S_LIST)
+      sz += var_len(C, st.col, r) * (st.kind == KXP_S_LIST ? st.width : 1u);
+  }
+  return sz;
+}
+
+__device__ __forceinline__ bool is_canon(const KxProgram& P, const KxLaunchCols& C, uint64_t r) {
+  return !C.presence || (C.presence[r] & P.canon_pres) == P.canon_pres;
+}
+
+template <bool LS, bool CANON = false>
 __device__ __forceinline__ uint64_t any_size(const EncParams& ep, const KxProgram& P, uint64_t r) {
+  if (CANON && is_canon(P, ep.cols, r)) return canon_size(P, ep.cols, r);
   return ep.pb ? pb_record_size(P, ep.cols, r) : record_size<LS>(P, ep.cols, r);
 }
 
@@ -610,7 +627,7 @@ __device__ uint64_t block_excl_scan(uint64_t v, uint64_t* tot, uint64_t* scratch
   return base + inc - v;
 }
 
-template <bool LS>
+template <bool LS, bool CANON>
 __global__ void __launch_bounds__(NT) size_kernel(EncParams ep) {
   __shared__ uint64_t scratch[NT / 64];
   __shared__ uint32_t progw[sizeof(KxProgram) / 4];
@@ -623,7 +640,7 @@ __global__ void __launch_bounds__(NT) size_kernel(EncParams ep) {
     uint64_t r = b * RB + k * NT + threadIdx.x;
     uint64_t sz = 0;
     if (r < ep.n) {
-      sz = any_size<LS>(ep, P, r);
+      sz = any_size<LS, CANON>(ep, P, r);
       if (ep.sizes_out) ep.sizes_out[r] = sz;
     }
     acc += sz;
@@ -682,7 +699,7 @@ __global__ void __launch_bounds__(WT, KX_ENC_LB) write_kernel(EncParams ep) {
   uint64_t gpos = ep.block_tot[b];
   while (r < rend) {
     uint64_t my = r + threadIdx.x;
-    uint64_t sz = my < rend ? any_size<LS>(ep, P, my) : 0;
+    uint64_t sz = my < rend ? any_size<LS, CANON>(ep, P, my) : 0;
     uint64_t tot;
     uint64_t pre = block_excl_scan(sz, &tot, scratch);
     const uint32_t skew = (uint32_t)(((uint64_t)ep.out + gpos) & 15);
@@ -722,7 +739,7 @@ __global__ void __launch_bounds__(WT, KX_ENC_LB) write_kernel(EncParams ep) {
     }
     if (threadIdx.x < take) {
       LSink s((LDSB*)img, skew + pre);
-      if (CANON && (!ep.cols.presence || (ep.cols.presence[my] & P.canon_pres) == P.canon_pres))
+      if (CANON && is_canon(P, ep.cols, my))
         write_canon(P, ep.cols, my, s);
       else
         any_write<LS>(ep, P, my, s);
@@ -775,16 +792,17 @@ int kx_launch_encode(const KxProgram* dprog, const KxProgram& hprog, const KxLau
   if (status) KX_HIP_CHECK(hipMemsetAsync(status, 0, sizeof(kx_status), stream));
   bool ls = false;
   for (uint32_t f = 0; f < hprog.nfields; f++) ls |= hprog.f[f].kind == KXP_K_LSTRUCT;
-  if (ls) hipLaunchKernelGGL(size_kernel<true>, dim3((unsigned)ep.nblocks), dim3(NT), 0, stream, ep);
-  else hipLaunchKernelGGL(size_kernel<false>, dim3((unsigned)ep.nblocks), dim3(NT), 0, stream, ep);
+  static int canon_env = -1;  // KX_ENC_CANON=0: the generic sizes and writer for every record (A/B)
+  if (canon_env < 0) { const char* e = getenv("KX_ENC_CANON"); canon_env = e ? atoi(e) : 1; }
+  const bool canon = canon_env && !pb && !ls && hprog.nsteps > 0;
+  if (ls) hipLaunchKernelGGL((size_kernel<true, false>), dim3((unsigned)ep.nblocks), dim3(NT), 0, stream, ep);
+  else if (canon) hipLaunchKernelGGL((size_kernel<false, true>), dim3((unsigned)ep.nblocks), dim3(NT), 0, stream, ep);
+  else hipLaunchKernelGGL((size_kernel<false, false>), dim3((unsigned)ep.nblocks), dim3(NT), 0, stream, ep);
   KX_HIP_CHECK(hipGetLastError());
   if (sizes_only) return KX_OK;
   hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, stream, ep);
   KX_HIP_CHECK(hipGetLastError());
   size_t shmem = OUTB + 32 + sizeof(KxProgram) + 8 * (WT / 64);
-  static int canon_env = -1;  // KX_ENC_CANON=0: the generic writer for every record (A/B)
-  if (canon_env < 0) { const char* e = getenv("KX_ENC_CANON"); canon_env = e ? atoi(e) : 1; }
-  const bool canon = canon_env && !pb && hprog.nsteps > 0;
   if (ls) hipLaunchKernelGGL((write_kernel<true, false>), dim3((unsigned)ep.nblocks), dim3(WT), shmem, stream, ep);
   else if (canon) hipLaunchKernelGGL((write_kernel<false, true>), dim3((unsigned)ep.nblocks), dim3(WT), shmem, stream, ep);
   else hipLaunchKernelGGL((write_kernel<false, false>), dim3((unsigned)ep.nblocks), dim3(WT), shmem, stream, ep);

@@ -112,6 +112,9 @@ struct KxProgram {
   uint8_t sel_req[KXP_MAX_COLS];
   uint8_t sel_first[KXP_MAX_COLS];
   uint8_t sel_n[KXP_MAX_COLS];
+  // canonical plan: encoded bytes of a canonical record besides its var payloads (headers, fixed values,
+  // string lengths, list headers, STOPs): BLength = canon_fixed + the var steps' payload bytes
+  uint64_t canon_fixed;
 };
 
 static_assert(sizeof(KxpField) == 16, "KxpField layout");

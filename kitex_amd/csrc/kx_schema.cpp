@@ -438,6 +438,12 @@ int kx_build_program(const kx_struct_desc* structs, uint32_t nstructs, kx_schema
     P.steps[k].hdr = (P.steps[k].hdr & 0xffffffu) | (run << 24);
   }
   P.canon_pres = pb.pres;
+  P.canon_fixed = 0;
+  for (uint32_t k = 0; k < P.nsteps; k++) {
+    const KxpStep& st = P.steps[k];
+    P.canon_fixed += st.kind == KXP_S_FIXED ? 3u + st.width : st.kind == KXP_S_BYTES ? 7u
+                   : st.kind == KXP_S_LIST ? 8u : st.kind == KXP_S_STRUCT ? 3u : 1u;
+  }
   s->ncols = P.ncols;
   return KX_OK;
 }
