@@ -250,6 +250,12 @@ uint64_t kx_schema_min_record_size(const kx_schema* s);
  * sizes of a decode are obtained first with kx_thrift_decode_sizes. */
 int kx_schema_is_nested(const kx_schema* s);
 
+/* Device workspace (bytes) a kx_ctx holds for a decode of n records over in_len input bytes (known_offsets
+ * != 0: offsets given), grow-only per ctx and stream. No reference counterpart (capacity planning): the
+ * concatenated modes keep per-tile aggregates plus record-start slots sized from the mean record size
+ * (DESIGN.md §2), e.g. 0.28 GB for 16 M R2 records (2.8 GB of input). */
+uint64_t kx_decode_workspace_bytes(const kx_schema* s, uint64_t in_len, int known_offsets, uint64_t n);
+
 int kx_ctx_create(int device, kx_ctx** out);
 void kx_ctx_destroy(kx_ctx* c);
 /* Decode pipelining of this ctx (a tuning knob; no reference counterpart). A batch of more than two

@@ -272,7 +272,7 @@ int nested_decode(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_
   if ((rc = nprog_on_device(const_cast<kx_schema*>(s), c->device, &dp))) return rc;
   if ((rc = ensure_nws(c, kx_nested_ws_bytes(*s->nprog, n, offsets == nullptr), st))) return rc;
   uint64_t epoch = 0;
-  if (!offsets && (rc = ensure_ws(c, kx_skip_ws_bytes(in_len), st, &epoch))) return rc;
+  if (!offsets && (rc = ensure_ws(c, kx_skip_ws_bytes(in_len, n), st, &epoch))) return rc;
   return kx_launch_nested_decode(dp, *s->nprog, in, in_len, offsets, ends, n, dcols, record_status, status, c->nws,
                                  c->nws_size, c->ws, c->ws_size, epoch, st, totals);
 }
@@ -446,6 +446,13 @@ int kx_thrift_decode_batch(kx_ctx* c, const kx_schema* s, const uint8_t* in, uin
                           epoch, st, false, nullptr, nullptr, &c->pipe);
 }
 
+uint64_t kx_decode_workspace_bytes(const kx_schema* s, uint64_t in_len, int known_offsets, uint64_t n) {
+  if (!s) return 0;
+  const uint64_t* offs = known_offsets ? (const uint64_t*)(uintptr_t)1 : nullptr;  // only its presence is read
+  if (s->nprog) return kx_nested_ws_bytes(*s->nprog, n, !known_offsets) + (known_offsets ? 0 : kx_skip_ws_bytes(in_len, n));
+  return kx_decode_ws_bytes(s->prog, in_len, offs, n);
+}
+
 int kx_thrift_decode_sizes(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len,
                            const uint64_t* offsets, uint64_t n, uint64_t* units, kx_status* status, void* stream) {
   if (!c || !s || !status || !units || (!in && in_len)) return KX_ERR_INVALID_ARG;
@@ -486,7 +493,7 @@ int kx_thrift_skip_batch(kx_ctx* c, const uint8_t* in, uint64_t in_len, uint64_t
     return KX_OK;
   }
   uint64_t epoch = 0;
-  if ((rc = ensure_ws(c, kx_skip_ws_bytes(in_len), st, &epoch))) return rc;
+  if ((rc = ensure_ws(c, kx_skip_ws_bytes(in_len, n), st, &epoch))) return rc;
   return kx_launch_skip(in, in_len, n, offsets_out, status, c->ws, c->ws_size, epoch, st);
 }
 
@@ -690,7 +697,7 @@ int kx_frame_scan(kx_ctx* c, const uint8_t* in, uint64_t in_len, uint64_t n, uin
     return KX_OK;
   }
   uint64_t epoch = 0;
-  if ((rc = ensure_ws(c, kx_skip_ws_bytes(in_len), st, &epoch))) return rc;
+  if ((rc = ensure_ws(c, kx_skip_ws_bytes(in_len, n), st, &epoch))) return rc;
   return kx_launch_frames(in, in_len, n, max_payload, frame_offsets, payload_start, payload_end, kinds, status, c->ws,
                           c->ws_size, epoch, st);
 }
@@ -779,7 +786,7 @@ int kx_grpc_frame_scan(kx_ctx* c, const uint8_t* in, uint64_t in_len, uint64_t n
     return KX_OK;
   }
   uint64_t epoch = 0;
-  if ((rc = ensure_ws(c, kx_skip_ws_bytes(in_len), st, &epoch))) return rc;
+  if ((rc = ensure_ws(c, kx_skip_ws_bytes(in_len, n), st, &epoch))) return rc;
   return kx_launch_frames(in, in_len, n, max_payload, frame_offsets, payload_start, payload_end, flags, status, c->ws,
                           c->ws_size, epoch, st, true);
 }
@@ -850,7 +857,7 @@ int kx_ttstream_frame_scan(kx_ctx* c, const uint8_t* in, uint64_t in_len, uint64
     return KX_OK;
   }
   uint64_t epoch = 0;
-  if ((rc = ensure_ws(c, kx_skip_ws_bytes(in_len), st, &epoch))) return rc;
+  if ((rc = ensure_ws(c, kx_skip_ws_bytes(in_len, n), st, &epoch))) return rc;
   return kx_launch_frames(in, in_len, n, 0, frame_offsets, payload_start, payload_end, frame_types, status, c->ws,
                           c->ws_size, epoch, st, false, keys, stream_ids, method_pos, method_len);
 }

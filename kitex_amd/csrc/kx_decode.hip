@@ -1897,7 +1897,7 @@ __device__ Agg walk_tile(KParams& dp, const Src& w, uint64_t tlo, uint64_t thi, 
         if (!enumerate) {
           st0 = c == 0 ? pos : st0; st1 = c == 1 ? pos : st1;
           st2 = c == 2 ? pos : st2; st3 = c == 3 ? pos : st3;
-        } else if (c >= 4) {
+        } else if (c >= 4 && sbase + c < dp.slotcap) {
           starts[sbase + c] = (uint16_t)(pos - tlo);
         }
         c++;
@@ -1968,16 +1968,16 @@ __device__ Agg walk_tile(KParams& dp, const Src& w, uint64_t tlo, uint64_t thi, 
     a.errc = fel < 64 ? (uint64_t)__builtin_amdgcn_readlane(errc, fel) : 0;
     a.errp = fel < 64 ? rl64(errp, fel) : 0;
     phase(3);
-    if (live) {
-      const uint64_t b = cpre;
-      if (cnt > 0) starts[b + 0] = (uint16_t)(st0 - tlo);
-      if (cnt > 1) starts[b + 1] = (uint16_t)(st1 - tlo);
-      if (cnt > 2) starts[b + 2] = (uint16_t)(st2 - tlo);
-      if (cnt > 3) starts[b + 3] = (uint16_t)(st3 - tlo);
+    if (live) {  // slots past slotcap are not kept (emit_tile follows the chain past them)
+      const uint64_t b = cpre, sc = dp.slotcap;
+      if (cnt > 0 && b + 0 < sc) starts[b + 0] = (uint16_t)(st0 - tlo);
+      if (cnt > 1 && b + 1 < sc) starts[b + 1] = (uint16_t)(st1 - tlo);
+      if (cnt > 2 && b + 2 < sc) starts[b + 2] = (uint16_t)(st2 - tlo);
+      if (cnt > 3 && b + 3 < sc) starts[b + 3] = (uint16_t)(st3 - tlo);
     }
-    if (__ballot(live && cnt > 4)) {
+    if (__ballot(live && cnt > 4 && cpre + 4 < dp.slotcap)) {
       enumerate = true;
-      need = live && cnt > 4;
+      need = live && cnt > 4 && cpre + 4 < dp.slotcap;
       sbase = cpre;
       continue;
     }
@@ -2177,10 +2177,11 @@ __device__ __forceinline__ bool fast_tile(KParams& dp, const Src& w, uint64_t tl
   a.ex = hmk ? rl64(ex, 63 - __clzll((long long)hmk)) : seed;
   a.errc = T_CANON;   // every record of the tile is canonical and inside the window: emit trusts the plan
   a.errp = 0;
-  if (cnt > 0) starts[cpre + 0] = (uint16_t)(st0 - tlo);
-  if (cnt > 1) starts[cpre + 1] = (uint16_t)(st1 - tlo);
-  if (cnt > 2) starts[cpre + 2] = (uint16_t)(st2 - tlo);
-  if (cnt > 3) starts[cpre + 3] = (uint16_t)(st3 - tlo);
+  const uint64_t sc = dp.slotcap;
+  if (cnt > 0 && cpre + 0 < sc) starts[cpre + 0] = (uint16_t)(st0 - tlo);
+  if (cnt > 1 && cpre + 1 < sc) starts[cpre + 1] = (uint16_t)(st1 - tlo);
+  if (cnt > 2 && cpre + 2 < sc) starts[cpre + 2] = (uint16_t)(st2 - tlo);
+  if (cnt > 3 && cpre + 3 < sc) starts[cpre + 3] = (uint16_t)(st3 - tlo);
   return true;
 }
 
@@ -2791,9 +2792,15 @@ __device__ __forceinline__ void emit_tile(KParams& dp, LDS uint32_t* win, uint64
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (cnt == 0 || base >= nstop) return;
   cnt = kmin64(cnt, nstop - base);
-  for (uint64_t j0 = 0; j0 < cnt; j0 += 64) {
+  // records past the tile's slots (slotcap, a multiple of 64; ws_layout) are emitted one per round,
+  // each starting where the previous one ended
+  uint64_t chain = 0;
+  uint64_t step = 64;
+  for (uint64_t j0 = 0; j0 < cnt; j0 += step) {
+    const bool past = !known && j0 >= dp.slotcap;
+    step = past ? 1 : 64;
     const uint64_t j = j0 + lane;
-    const bool act = j < cnt;
+    const bool act = j < cnt && (uint64_t)lane < step;
     const uint64_t r = base + j;
     VarState<NV> vs;
 #pragma unroll
@@ -2806,7 +2813,7 @@ __device__ __forceinline__ void emit_tile(KParams& dp, LDS uint32_t* win, uint64
         lim = rec_end(dp, r);
         if (pos > lim || lim > dp.in_len) rc = KX_ERR_INVALID_ARG;
       } else {
-        pos = lo + starts[j];
+        pos = past ? chain : lo + starts[j];
       }
       if (canon) {
         end = emit_canon<NV>(w, dp.cols, pos, r, vs);
@@ -2915,6 +2922,7 @@ __device__ __forceinline__ void emit_tile(KParams& dp, LDS uint32_t* win, uint64
       st->consumed = known ? rec_end(dp, dp.n - 1) : end;
       if (MODE == M_SKIP || MODE == M_FRAME) dp.skip_out[dp.n] = end;
     }
+    if (!known) chain = rl64(end, (int)(kmin64(step, cnt - j0) - 1));   // the round's last record ends here
   }
 }
 
@@ -2990,6 +2998,27 @@ uint32_t krec_for(uint64_t in_len, uint64_t n) {
   return (uint32_t)(k < 1 ? 1 : k > 64 ? 64 : k);
 }
 
+// record-start slots per tile (concatenated modes), a multiple of 64: four times the records a tile
+// holds at the batch's mean record size (in_len / n) plus a wave, at most one per byte (a record can be a
+// single STOP byte). A tile with more records than slots keeps the first slotcap starts and the emit
+// pass follows the chain record by record past them (emit_tile), so the cap bounds the workspace, not
+// what decodes: 16 M R2 records (2.8 GB) need 0.22 GB of slots instead of 5.6 GB at one slot per byte.
+// KX_SLOTCAP overrides it (tests force the record-by-record path with 64).
+uint64_t slot_cap(uint64_t in_len, uint64_t n) {
+  const char* e = getenv("KX_SLOTCAP");
+  const long long forced = e ? atoll(e) : -1;
+  const uint64_t full = ((uint64_t)TILE + 1 + 63) & ~63ull;
+  uint64_t cap = full;
+  if (forced > 0) {
+    cap = (uint64_t)forced;
+  } else if (n) {
+    const uint64_t mean = in_len / n;
+    if (mean >= 4) cap = 4 * ((uint64_t)TILE / mean) + 64;
+  }
+  cap = (cap + 63) & ~63ull;
+  return cap < 64 ? 64 : cap > full ? full : cap;
+}
+
 WsLayout ws_layout(uint64_t min_rec, uint64_t in_len, const uint64_t* offsets, uint64_t n) {
   WsLayout L{};
   if (offsets) {
@@ -2998,13 +3027,10 @@ WsLayout ws_layout(uint64_t min_rec, uint64_t in_len, const uint64_t* offsets, u
     L.slotcap = 0;
   } else {
     L.ntiles = (in_len + TILE - 1) / TILE;
-    // a record can be a single STOP byte whatever the schema's encoded minimum: every byte of
-    // the tile may start one
-    (void)min_rec;
-    L.slotcap = (uint64_t)TILE + 1;
+    L.slotcap = slot_cap(in_len, n);
   }
+  (void)min_rec;
   if (!L.ntiles) L.ntiles = 1;
-  L.slotcap = (L.slotcap + 3) & ~3ull;
   L.ngroups = (L.ntiles + GT - 1) / GT;
   size_t o = WS_HDR;
   L.tdesc = o; o += (size_t)L.ntiles * T_NF * 8;
@@ -3269,7 +3295,7 @@ extern "C" int kx_debug_phase_cycles(unsigned long long* out, int n) {
   return KX_OK;
 }
 
-size_t kx_skip_ws_bytes(uint64_t in_len) { return ws_layout(1, in_len, nullptr, 0).total; }
+size_t kx_skip_ws_bytes(uint64_t in_len, uint64_t n) { return ws_layout(1, in_len, nullptr, n).total; }
 
 // window bytes per tile: a halo of about two mean records (the walk of a tile's last records stays in
 // LDS: R3's 576-byte records left the 512-byte halo and walked global memory), 512 .. HALO_MAX

@@ -148,6 +148,25 @@ def case_empty(dec, oracle):
     check_decode(dec, oracle, sch, wire, len(recs), offsets=offs)
 
 
+def case_slot_overflow(dec, oracle):
+    """tiles holding far more records than the batch's mean size predicts (large records, then a run of
+    1-byte records): the first slotcap record starts of such a tile are kept, the rest are emitted one per
+    round from the previous record's end (kx_decode.hip ws_layout / emit_tile)"""
+    sch = S.Schema(S.Struct("D", [S.Field(1, A.T_I64, default=42), S.Field(2, A.T_I32, default=-7),
+                                  S.Field(3, A.T_BOOL), S.Field(4, A.T_STRING)]))
+    recs = []
+    for i in range(24):
+        recs.append(rec_bytes(oracle, [(A.T_I64, 1, i64(oracle, i)), (A.T_STRING, 4, sbytes(oracle, b"x" * 30000))]))
+    for i in range(30000):
+        recs.append(rec_bytes(oracle, [(A.T_BOOL, 3, bytes([1]))]) if i % 1000 == 7 else b"\x00")
+    for i in range(24):
+        recs.append(rec_bytes(oracle, [(A.T_STRING, 4, sbytes(oracle, b"y" * (i * 37)))]))
+    wire, offs = concat(recs)
+    assert wire.size / len(recs) > 20          # the mean-size slot estimate is far below the 1-byte run's
+    check_decode(dec, oracle, sch, wire, len(recs))
+    check_decode(dec, oracle, sch, wire, len(recs), offsets=offs)
+
+
 def case_nested(dec, oracle):
     inner = S.Struct("In", [S.Field(1, A.T_I64, req=A.REQ_REQUIRED), S.Field(2, A.T_STRING, req=A.REQ_OPTIONAL),
                             S.Field(3, A.T_I16, default=9)])

@@ -25,7 +25,7 @@ extern "C" int emu_decode(const kx_struct_desc* structs, uint32_t nstructs, cons
     }
     lc.presence = out->presence;
   }
-  size_t ws_size = skip ? kx_skip_ws_bytes(in_len) : kx_decode_ws_bytes(s.prog, in_len, offsets, n);
+  size_t ws_size = skip ? kx_skip_ws_bytes(in_len, n) : kx_decode_ws_bytes(s.prog, in_len, offsets, n);
   // one workspace reused across calls with a fresh epoch each time, exactly like a kx_ctx
   // (kx_capi.cpp ensure_ws): stale words / counters of earlier calls must never leak into a call
   static char* ws = nullptr;
@@ -66,7 +66,7 @@ extern "C" int emu_decode(const kx_struct_desc* structs, uint32_t nstructs, cons
 // framing sniff (kx_launch_frames) under the emulator, workspace shared with emu_decode's
 extern "C" int emu_frames(const uint8_t* in, uint64_t in_len, uint64_t n, uint64_t max_payload, uint64_t* fo,
                           uint64_t* ps, uint64_t* pe, uint8_t* kinds, kx_status* status, int grpc) {
-  const size_t ws_size = kx_skip_ws_bytes(in_len);
+  const size_t ws_size = kx_skip_ws_bytes(in_len, n);
   static char* ws = nullptr;
   static size_t ws_cap = 0;
   static uint64_t epoch = 0xffff;
@@ -89,7 +89,7 @@ extern "C" int emu_frames(const uint8_t* in, uint64_t in_len, uint64_t n, uint64
 extern "C" int emu_tts_frames(const uint8_t* in, uint64_t in_len, uint64_t n, const kx_ttstream_keys* keys,
                               uint64_t* fo, uint64_t* ps, uint64_t* pe, uint8_t* ft, int32_t* sid, uint64_t* mp,
                               uint32_t* ml, kx_status* status) {
-  const size_t ws_size = kx_skip_ws_bytes(in_len);
+  const size_t ws_size = kx_skip_ws_bytes(in_len, n);
   static char* ws = nullptr;
   static size_t ws_cap = 0;
   static uint64_t epoch = 0xffff;

@@ -62,6 +62,21 @@ def test_schema_min_record_size(kxlib):
     assert DeviceSchema(S.schema_r2()).min_record_size == 89 + 14
 
 
+def test_decode_workspace_bytes(kxlib):
+    """config-2 decode (16 M R2 records concatenated, 2.8 GB): record-start slots sized from the mean record
+    size keep the workspace under 1 GB (one u16 slot per input byte was 5.6 GB)"""
+    from kitex_amd.codec import DeviceSchema
+    L = kxlib
+    n = 16 << 20
+    r2 = DeviceSchema(S.schema_r2())
+    ws = L.kx_decode_workspace_bytes(r2.handle, 167 * n, 0, n)
+    assert 0 < ws < 1 << 30, ws
+    assert L.kx_decode_workspace_bytes(r2.handle, 167 * n, 1, n) < ws
+    # n unknown / tiny records: one slot per byte again (every byte may start a record)
+    assert L.kx_decode_workspace_bytes(r2.handle, 8192 * 64, 0, 8192 * 64) > 2 * 8192 * 64
+    assert L.kx_decode_workspace_bytes(DeviceSchema(S.schema_r3()).handle, 576 * (4 << 20), 0, 4 << 20) < 1 << 30
+
+
 def test_schema_rejects(kxlib):
     from kitex_amd.codec import DeviceSchema
     from kitex_amd._lib import KxError

@@ -68,6 +68,31 @@ def test_emu_empty_records(edec, oracle):
     DC.case_empty(edec, oracle)
 
 
+def test_emu_slot_overflow(edec, oracle):
+    DC.case_slot_overflow(edec, oracle)
+
+
+@pytest.mark.parametrize("case", ["r1", "r2", "r3", "pb", "containers", "noncanonical", "empty", "ragged", "skip"])
+def test_emu_slotcap_64(edec, oracle, case, monkeypatch):
+    """64 record-start slots per tile (KX_SLOTCAP): every record past a tile's first 64 is emitted one per
+    round from the previous record's end"""
+    monkeypatch.setenv("KX_SLOTCAP", "64")
+    if case in ("r1", "r2", "r3"):
+        DC.case_concat(edec, oracle, case, 3000)
+    elif case == "pb":
+        PC.case_pb_concat(edec, oracle, 3000)
+    elif case == "containers":
+        DC.case_containers(edec, oracle, "cx1", 3000, "concat")
+    elif case == "noncanonical":
+        DC.case_noncanonical(edec, oracle, "concat")
+    elif case == "empty":
+        DC.case_empty(edec, oracle)
+    elif case == "ragged":
+        DC.case_ragged(edec, oracle, "concat")
+    else:
+        DC.case_skip(lambda wire, n: emu.skip(wire, n)[1], oracle)
+
+
 def test_emu_nested(edec, oracle):
     DC.case_nested(edec, oracle)
 

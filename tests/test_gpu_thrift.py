@@ -105,6 +105,21 @@ def test_empty_records_and_defaults(gdec, oracle):
     DC.case_empty(gdec, oracle)
 
 
+def test_slot_overflow(gdec, oracle):
+    """a run of 1-byte records after large ones: tiles with more records than the mean-size slot estimate"""
+    DC.case_slot_overflow(gdec, oracle)
+
+
+@pytest.mark.parametrize("name", ["r2", "r3", "cx1"])
+def test_slotcap_64(gdec, oracle, name, monkeypatch):
+    """64 record-start slots per tile (KX_SLOTCAP): records past them are emitted from the chain"""
+    monkeypatch.setenv("KX_SLOTCAP", "64")
+    if name == "cx1":
+        DC.case_containers(gdec, oracle, "cx1", 3000, "concat")
+    else:
+        DC.case_concat(gdec, oracle, name, 20000)
+
+
 def test_nested_struct_repeated_and_required(gdec, oracle):
     DC.case_nested(gdec, oracle)
 
