@@ -25,3 +25,14 @@ import json; d=json.loads(open('gpurun_out/enc_canon$c.log').read().strip().spli
 print('canon=$c', {k:(round(v['ms_per_step'],3), v.get('bit_exact')) for k,v in x.items() if k.endswith('encode')})"
   done
 fi
+# AB="VAR v1 v2 ...": the bench once per value of environment variable VAR, extras' times side by side
+if [ -n "${AB:-}" ]; then
+  set -- $AB
+  var=$1; shift
+  for c in "$@"; do
+    env "$var=$c" timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 --no-cpu --no-host > gpurun_out/ab_$c.log 2>&1 || { echo "ab $c failed"; tail -5 gpurun_out/ab_$c.log; exit 1; }
+    python3 -c "
+import json; d=json.loads(open('gpurun_out/ab_$c.log').read().strip().splitlines()[-1]); x=d['extra']
+print('$var=$c', 'headline', round(d['ms_per_step'],3), {k:(round(v['ms_per_step'],3), v.get('bit_exact', v.get('verified'))) for k,v in x.items()})"
+  done
+fi
