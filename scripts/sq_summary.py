@@ -7,7 +7,8 @@ import sys
 from collections import defaultdict
 
 d = sys.argv[1]
-KS = ("index_kernel<", "group_kernel<", "chain_kernel<", "emit_kernel<", "combo_kernel<", "write_kernel<", "size_kernel<")
+KS = ("index_kernel<", "group_kernel<", "chain_kernel<", "emit_kernel<", "combo_kernel<", "write_kernel<", "size_kernel<",
+      "crc_kernel(")
 agg = defaultdict(lambda: defaultdict(list))
 for p in ("p1", "p2"):
     for f in glob.glob(f"{d}/{p}/**/*counter_collection.csv", recursive=True):
@@ -15,7 +16,7 @@ for p in ("p1", "p2"):
             name = r["Kernel_Name"]
             for k in KS:
                 if "(anonymous namespace)::" + k in name:
-                    agg[k.rstrip("<")][r["Counter_Name"]].append(float(r["Counter_Value"]))
+                    agg[k.rstrip("<(")][r["Counter_Name"]].append(float(r["Counter_Value"]))
 out = {}
 for k, cs in agg.items():
     waves = sum(cs["SQ_WAVES"]) / max(1, len(cs["SQ_WAVES"])) if "SQ_WAVES" in cs else None
