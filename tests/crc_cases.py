@@ -39,11 +39,12 @@ def ref_payload() -> bytes:
     return bytes(i & 0xFF for i in range(1024))
 
 
-def ragged_ranges(seed: int, n: int, big: bool = True):
+def ragged_ranges(seed: int, n: int, big: bool = True, maxlen: int = 600):
     """a buffer and n+1 offsets over it: empty ranges, 1..15 bytes, thresholds 2048 / 4096 +- 1, and
-    (big) a few ranges of 100 KiB .. 1.3 MiB, all at unaligned starts"""
+    (big) a few ranges of 100 KiB .. 1.3 MiB, all at unaligned starts. maxlen <= 190: most waves' 64
+    consecutive ranges fit the kernel's 12 KiB LDS stage (kx_crc.hip), the rest read global memory"""
     rng = np.random.default_rng(seed)
-    lens = rng.integers(0, 600, size=n)
+    lens = rng.integers(0, maxlen, size=n)
     special = [0, 0, 1, 7, 15, 16, 17, 2047, 2048, 2049, 4095, 4096, 4097, 8191, 8193, 64 * 4096 + 3]
     if big:
         special += [100_000, 1_300_001]

@@ -56,6 +56,7 @@ uint64_t emu_clock_ns();
 #define gridDim (emu_grid_dim())
 #define blockDim (EmuTid{256, 1, 1})
 inline void __syncthreads() { emu_sync_wg(); }
+inline void __builtin_amdgcn_fence(int, const char*) {}
 
 inline uint64_t __ballot(int pred) {
   uint64_t all[64];
@@ -94,6 +95,10 @@ inline T __shfl_xor(T v, int m, int width = 64) {
   uint64_t all[64];
   emu_wave_xchg(emu_bits(v), all);
   return emu_from<T>(all[(emu_lane() ^ m) & 63]);
+}
+inline void __builtin_amdgcn_wave_barrier() {
+  uint64_t all[64];
+  emu_wave_xchg(0, all);
 }
 // like the real builtins these return int (a sign-extension trap the emulator must reproduce)
 inline int __builtin_amdgcn_readlane(int v, int l) {

@@ -23,10 +23,11 @@ def _u32(t):
     return to_np(t).astype(np.uint64).astype(np.uint32)
 
 
-@pytest.mark.parametrize("seed,n,big", [(1, 1, False), (2, 257, False), (3, 3000, True), (4, 40000, False)])
-def test_generate_matches_oracle(torch, oracle, seed, n, big):
+@pytest.mark.parametrize("seed,n,big,maxlen", [(1, 1, False, 600), (2, 257, False, 600), (3, 3000, True, 600),
+                                                (4, 40000, False, 600), (5, 40000, False, 180), (6, 9000, True, 120)])
+def test_generate_matches_oracle(torch, oracle, seed, n, big, maxlen):
     from kitex_amd.codec import CRC32PayloadValidator
-    data, offs = CC.ragged_ranges(seed, n, big)
+    data, offs = CC.ragged_ranges(seed, n, big, maxlen)
     rc, exp = oracle.crc32c_batch(data, offs)
     assert rc == 0
     v = CRC32PayloadValidator()

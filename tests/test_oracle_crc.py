@@ -71,10 +71,11 @@ def test_frame_modes(oracle):
 
 
 # ---- the CRC32C kernel source under the SIMT emulator (tests/emu), oracle-checked ----
-@pytest.mark.parametrize("seed,n,big", [(1, 1, False), (2, 300, False), (5, 700, True)])
-def test_emu_generate(oracle, seed, n, big):
+@pytest.mark.parametrize("seed,n,big,maxlen", [(1, 1, False, 600), (2, 300, False, 600), (5, 700, True, 600),
+                                                (6, 700, False, 180), (7, 1000, True, 120)])
+def test_emu_generate(oracle, seed, n, big, maxlen):
     from tests.emu import emu
-    data, offs = CC.ragged_ranges(seed, n, big)
+    data, offs = CC.ragged_ranges(seed, n, big, maxlen)
     rc, exp = oracle.crc32c_batch(data, offs)
     crc, _, st = emu.crc32c(data, offs, n, False)
     assert rc == 0 and st.code == 0 and st.n_records == n and st.consumed == offs[n]
