@@ -598,6 +598,19 @@ def host_inclusive(b, dev):
     return res
 
 
+def physical_cores():
+    """distinct physical cores (package id, core id) among the CPUs this process may run on"""
+    try:
+        seen = set()
+        for cpu in os.sched_getaffinity(0):
+            base = f"/sys/devices/system/cpu/cpu{cpu}/topology/"
+            with open(base + "physical_package_id") as a, open(base + "core_id") as b:
+                seen.add((a.read().strip(), b.read().strip()))
+        return len(seen) or None
+    except Exception:
+        return None
+
+
 def cpu_baseline(cfg, nrec):
     """The CPU restatement of the reference FastRead (oracle, 'port') on every core this process may
     run on (sched_getaffinity): offsets known (per-message fastUnmarshal, parallel over records),
@@ -610,6 +623,7 @@ def cpu_baseline(cfg, nrec):
         from oracle import oracle
         oracle.build()
         threads = max(1, min(len(os.sched_getaffinity(0)), 256))
+        phys = physical_cores()
         sch = S.SCHEMAS[cfg]()
         cs = synth.GENERATORS[cfg](nrec)
         pb = cfg == "pf"
@@ -653,6 +667,9 @@ def cpu_baseline(cfg, nrec):
         return {"value": nrec / best, "unit": "records/s", "cores": threads, "kind": "port",
                 "sample": f"{nrec} {cfg} records, FastRead restatement (oracle/kx_oracle.c) with message "
                           f"offsets known, best of 3, {threads} threads (len(sched_getaffinity))",
+                "threads": threads, "physical_cores": phys,
+                "cores_note": "cores = worker threads used (one per logical CPU of the affinity mask); "
+                              "physical_cores = distinct (package, core) pairs among them",
                 "gib_s": wire.size / best / 2**30, "one_thread_records_per_s": one / t1,
                 "concat_one_thread_records_per_s": (one / tc) if not pb else None,
                 "concat_note": f"{one} records as one concatenated list<{cfg}> body, walked sequentially "

@@ -142,8 +142,8 @@ enum {
  * unknown or mistyped fields skipped, the last duplicate wins, a missing field takes its default, a
  * missing required field is INVALID_DATA; FieldFastReadList + StructLikeFastRead, struct_tpl.go:583-625);
  * encoding writes every field of S in IDL order, then STOP (FieldFastWriteList, :1011-1036). Other
- * element structs (strings, nested structs or containers, optional fields) and nested containers are
- * KX_ERR_NOT_IMPLEMENTED at kx_schema_create. */
+ * element structs (strings, nested structs or containers, optional fields) and containers of containers
+ * compile to the nested model below (kx_schema_create falls back to it). */
 #define KX_ELEM_MAP_VALUE 0x80
 #define KX_ELEM_STRUCT_FIELD 0x40
 /* Nested schemas (ABI v3; kx_schema_is_nested() == 1): any shape the generated FastRead handles whose
@@ -285,6 +285,11 @@ int kx_thrift_decode_batch(kx_ctx* c, const kx_schema* s, const uint8_t* in, uin
  * record; its extents count as empty). Flat schemas: KX_ERR_NOT_IMPLEMENTED (status->var_total). */
 int kx_thrift_decode_sizes(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len,
                            const uint64_t* offsets, uint64_t n, uint64_t* units, kx_status* status, void* stream);
+/* The same for bare bodies at explicit extents in[starts[i], ends[i]) (the sizing step of
+ * kx_thrift_decode_extents; ttstream DecodePayload, pkg/remote/trans/ttstream/frame.go:223-233). */
+int kx_thrift_decode_sizes_extents(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len,
+                                   const uint64_t* starts, const uint64_t* ends, uint64_t n, uint64_t* units,
+                                   kx_status* status, void* stream);
 
 /* Skip decoder over n concatenated records: writes record start offsets (n+1 entries, device u64). */
 int kx_thrift_skip_batch(kx_ctx* c, const uint8_t* in, uint64_t in_len, uint64_t n,

@@ -29,7 +29,7 @@ EXPORTS = [
     "kx_grpc_frame_scan", "kx_thrift_decode_grpc", "kx_pb_decode_grpc", "kx_thrift_raw_messages",
     "kx_thrift_set_seqids", "kx_thrift_encode_messages", "kx_ttstream_default_keys", "kx_ttstream_frame_scan",
     "kx_thrift_decode_extents", "kx_pb_decode_extents", "kx_schema_is_nested", "kx_thrift_decode_sizes",
-    "kx_decode_workspace_bytes",
+    "kx_decode_workspace_bytes", "kx_thrift_decode_sizes_extents",
 ]
 
 
@@ -79,6 +79,7 @@ def lib():
     L.kx_schema_is_nested.argtypes = [vp]
     L.kx_schema_is_nested.restype = C.c_int
     L.kx_thrift_decode_sizes.argtypes = [vp, vp, vp, u64, vp, u64, vp, C.POINTER(A.Status), vp]
+    L.kx_thrift_decode_sizes_extents.argtypes = [vp, vp, vp, u64, vp, vp, u64, vp, C.POINTER(A.Status), vp]
     L.kx_pb_decode_batch.argtypes = dec
     L.kx_decode_workspace_bytes.argtypes = [vp, u64, C.c_int, u64]
     L.kx_decode_workspace_bytes.restype = u64

@@ -330,15 +330,21 @@ class ThriftCodec:
         return res
 
     @on_call_stream
-    def DecodeSizes(self, buf, n: int, offsets=None, stream=None) -> List[int]:
+    def DecodeSizes(self, buf, n: int, offsets=None, stream=None, ends=None) -> List[int]:
         """Nested schemas: the arena units a decode of buf needs, 3 per column (data units, elem_offsets
-        entries - 1, sub_offsets entries - 1): kx_thrift_decode_sizes (synchronous)."""
+        entries - 1, sub_offsets entries - 1): kx_thrift_decode_sizes (synchronous). With `ends`,
+        `offsets` are the bodies' starts (explicit extents, kx_thrift_decode_sizes_extents)."""
         ds = self.dschema
         units = (C.c_uint64 * (3 * max(1, ds.ncols)))()
         st = A.Status()
         s = _stream(stream)
-        check(lib().kx_thrift_decode_sizes(self._ctx(s).handle, ds.handle, _ptr(buf), buf.numel(), _ptr(offsets), n,
-                                           units, C.byref(st), int(s.cuda_stream)), "kx_thrift_decode_sizes")
+        if ends is not None:
+            check(lib().kx_thrift_decode_sizes_extents(self._ctx(s).handle, ds.handle, _ptr(buf), buf.numel(),
+                                                       _ptr(offsets), _ptr(ends), n, units, C.byref(st),
+                                                       int(s.cuda_stream)), "kx_thrift_decode_sizes_extents")
+        else:
+            check(lib().kx_thrift_decode_sizes(self._ctx(s).handle, ds.handle, _ptr(buf), buf.numel(), _ptr(offsets),
+                                               n, units, C.byref(st), int(s.cuda_stream)), "kx_thrift_decode_sizes")
         return [int(units[i]) for i in range(3 * ds.ncols)]
 
     def UnmarshalHost(self, wire, n: int, offsets=None, var_caps: Sequence[int] = None,
@@ -446,16 +452,23 @@ class ThriftCodec:
         import torch
         ds = self.dschema
         n = int(starts.numel())
+        starts = starts.to(torch.int64).contiguous()
+        ends = ends.to(torch.int64).contiguous()
         if out is None:
+            elem_caps = sub_caps = None
+            if var_caps is None and ds.nested and self._EXTENTS == "kx_thrift_decode_extents":
+                # exact arenas from the measure pass over the same extents (a connection buffer's worth of
+                # buf-sized arenas per column would not fit for wide nested schemas)
+                units = self.DecodeSizes(buf, n, starts, stream=stream, ends=ends)
+                var_caps, elem_caps, sub_caps = units[0::3], units[1::3], units[2::3]
             if var_caps is None:
                 var_caps = [0 if ci.kind == A.COL_FIXED else max(1, buf.numel()) for ci in ds.infos]
-            out = alloc_device(ds.infos, n, var_caps, ds.npresence, self.device)
+            out = alloc_device(ds.infos, n, var_caps, ds.npresence, self.device, elem_caps=elem_caps,
+                               sub_caps=sub_caps)
         kc = to_kx_columns(out, ds.infos, var_caps)
         st = status_tensor(self.device)
         rs = torch.empty(max(1, n), dtype=torch.uint8, device=self.device)
         s = _stream(stream)
-        starts = starts.to(torch.int64).contiguous()
-        ends = ends.to(torch.int64).contiguous()
         rc = getattr(lib(), self._EXTENTS)(self._ctx(s).handle, ds.handle, _ptr(buf), buf.numel(), _ptr(starts),
                                            _ptr(ends), n, C.byref(kc), _ptr(rs), _ptr(st), int(s.cuda_stream))
         check(rc, self._EXTENTS)

@@ -453,9 +453,9 @@ uint64_t kx_decode_workspace_bytes(const kx_schema* s, uint64_t in_len, int know
   return kx_decode_ws_bytes(s->prog, in_len, offs, n);
 }
 
-int kx_thrift_decode_sizes(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len,
-                           const uint64_t* offsets, uint64_t n, uint64_t* units, kx_status* status, void* stream) {
-  if (!c || !s || !status || !units || (!in && in_len)) return KX_ERR_INVALID_ARG;
+static int decode_sizes(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len, const uint64_t* offsets,
+                        const uint64_t* ends, uint64_t n, uint64_t* units, kx_status* status, void* stream) {
+  if (!c || !s || !status || !units || (!in && in_len) || (ends && !offsets)) return KX_ERR_INVALID_ARG;
   if (!s->nprog) return KX_ERR_NOT_IMPLEMENTED;
   int rc = set_device(c);
   if (rc) return rc;
@@ -466,7 +466,7 @@ int kx_thrift_decode_sizes(kx_ctx* c, const kx_schema* s, const uint8_t* in, uin
   if (n) {
     kx_status* dst = nullptr;
     KX_HIP_CHECK(hipMalloc(&dst, sizeof(kx_status)));
-    rc = nested_decode(c, s, in, in_len, offsets, nullptr, n, nullptr, nullptr, dst, st, tot);
+    rc = nested_decode(c, s, in, in_len, offsets, ends, n, nullptr, nullptr, dst, st, tot);
     if (!rc && hipMemcpyAsync(status, dst, sizeof(kx_status), hipMemcpyDeviceToHost, st) != hipSuccess) rc = KX_ERR_HIP;
     if (!rc && hipStreamSynchronize(st) != hipSuccess) rc = KX_ERR_HIP;
     (void)hipFree(dst);
@@ -479,6 +479,18 @@ int kx_thrift_decode_sizes(kx_ctx* c, const kx_schema* s, const uint8_t* in, uin
     units[3 * i + 2] = K.narr >= 3 ? tot[K.acur[1]] : 0;
   }
   return KX_OK;
+}
+
+int kx_thrift_decode_sizes(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len,
+                           const uint64_t* offsets, uint64_t n, uint64_t* units, kx_status* status, void* stream) {
+  return decode_sizes(c, s, in, in_len, offsets, nullptr, n, units, status, stream);
+}
+
+int kx_thrift_decode_sizes_extents(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len,
+                                   const uint64_t* starts, const uint64_t* ends, uint64_t n, uint64_t* units,
+                                   kx_status* status, void* stream) {
+  if (!starts || !ends) return KX_ERR_INVALID_ARG;
+  return decode_sizes(c, s, in, in_len, starts, ends, n, units, status, stream);
 }
 
 int kx_thrift_skip_batch(kx_ctx* c, const uint8_t* in, uint64_t in_len, uint64_t n, uint64_t* offsets_out,

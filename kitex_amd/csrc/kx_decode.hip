@@ -2083,8 +2083,17 @@ __device__ __forceinline__ bool fast_tile(KParams& dp, const Src& w, uint64_t tl
   const uint32_t q0 = (uint32_t)(tlo - w.wpos);   // < 16
   const uint32_t D0 = q0 >> 2;
   // ---- interleaved scan: hm = the dword-hit mask of this lane's segment ----
+  uint64_t tp = (dp.diag & 64) ? __builtin_amdgcn_s_memtime() : 0;
+  auto phase = [&](int k) {   // diagnostics (KX_DIAG & 64): cycles per phase, summed over tiles
+    if (dp.diag & 64) {
+      const uint64_t now = __builtin_amdgcn_s_memtime();
+      if (lane == 0) atomicAdd(&g_phase[k], (unsigned long long)(now - tp));
+      tp = now;
+    }
+  };
   uint32_t hm = 0;
   fast_scan<0>(w, D0, b0, b1, b2, lane, (uint32_t)lane >> 1, 32u * ((uint32_t)lane & 1u), hm);
+  phase(1);
   const uint32_t sq = 4 * D0 + 128u * (uint32_t)lane;   // window offset of the segment's first dword
   const uint64_t seg_lo = lane == 0 ? tlo : w.wpos + sq;
   const uint64_t seg_hi = lane == 63 ? thi : kmin64(w.wpos + sq + 128, thi);
@@ -2116,6 +2125,7 @@ __device__ __forceinline__ bool fast_tile(KParams& dp, const Src& w, uint64_t tl
       }
     }
   }
+  phase(2);
   // ---- walk: records of the segment from c1, else c2, else c3: a candidate whose walk fails anywhere
   //      (not canonical, or a record nested in a payload: it parses, but the bytes after it do not) is
   //      replaced by the next; the consistency check below accepts only an unbroken chain ----
@@ -2158,6 +2168,7 @@ __device__ __forceinline__ bool fast_tile(KParams& dp, const Src& w, uint64_t tl
     }
     if (!__ballot(again)) break;
   }
+  phase(3);
   if (__ballot(bad)) return false;
   // ---- consistency: every walking lane starts where the chain of the walking lane below it exits ----
   const uint64_t hmk = __ballot(ent != X_NONE);
@@ -2182,6 +2193,7 @@ __device__ __forceinline__ bool fast_tile(KParams& dp, const Src& w, uint64_t tl
   if (cnt > 1 && cpre + 1 < sc) starts[cpre + 1] = (uint16_t)(st1 - tlo);
   if (cnt > 2 && cpre + 2 < sc) starts[cpre + 2] = (uint16_t)(st2 - tlo);
   if (cnt > 3 && cpre + 3 < sc) starts[cpre + 3] = (uint16_t)(st3 - tlo);
+  phase(4);
   return true;
 }
 

@@ -36,11 +36,12 @@
 #define KXN_MAX_FIELDS 192
 #define KXN_MAX_STRUCTS 64
 #define KXN_MAX_ROOTS 32
-#define KXN_MAX_CUR 96
+#define KXN_MAX_CUR 64          // = the device walker's per-lane cursor array (kx_nested.hip)
 #define KXN_MAX_ENT 384
 #define KXN_MAX_DFL 256
 #define KXN_MAX_SDF 64
-#define KXN_MAX_SNAP 768
+#define KXN_MAX_SNAP 128        // = the device walker's per-lane snapshot slots: a schema needing more is
+                                // refused at kx_schema_create, not at its first decode
 #define KXN_MAX_DEFB 4096
 #define KXN_STACK 32          // walker frames (struct nesting + containers)
 #define KXN_SKIP_DEPTH 64     // codec_apache.go:167

@@ -21,8 +21,8 @@ namespace {
 
 constexpr int NT = 256;       // threads per workgroup
 constexpr int RB = 1024;      // records per block
-constexpr int SNAP = 128;     // snapshot slots per lane (schemas needing more: NOT_IMPLEMENTED)
-constexpr int CUR = 64;       // cursors per lane
+constexpr int SNAP = KXN_MAX_SNAP;  // snapshot slots per lane (kx_schema_create refuses schemas needing more)
+constexpr int CUR = KXN_MAX_CUR;    // cursors per lane
 
 struct NParams {
   const KxnProgram* P;

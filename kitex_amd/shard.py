@@ -37,33 +37,44 @@ def _unsigned(t):
     return t if t.dtype == torch.int64 else t.to(torch.int64) & 0xFFFFFFFF
 
 
-def _kind(col, ci) -> str:
-    """how a decoded column is laid out: 'fixed' values[n]; 'var' (offsets[n+1], arena) for strings /
-    numeric lists / a map's fixed side; 'lb' (record offsets in elements, element byte offsets, bytes) for
-    list/set<string> and a map's string side; 'view' (offset, length) pairs into the decode input"""
+# offsets arrays above the data array, per column kind (kitex_amd.columns): a column is a chain
+# o_0[n + 1] -> o_1 -> ... -> o_{k-1} -> data, where o_j indexes o_{j+1} (the last one indexes data)
+_DEPTH = {A.COL_BYTES: 1, A.COL_LIST: 1, A.COL_LIST_BYTES: 2, A.COL_LIST2: 2, A.COL_LIST2_BYTES: 3}
+
+
+def _kind(col, ci):
+    """how a decoded column is laid out: 'fixed' values[n]; 'view' (offset, length) pairs into the decode
+    input; else the depth k of its offsets chain (1: strings / numeric lists / a map's fixed side as
+    (offsets[n+1], arena); 2: list/set<string>, a map's string side, list<list<scalar>> as (record
+    offsets, element offsets, data); 3: two container levels over strings as (record offsets, element
+    offsets, inner element byte offsets, bytes)). Decided by the column's kind, checked against the tuple."""
+    from ._lib import KxError
     from .columns import Views
     if isinstance(col, Views):
         return "view"
     if ci.kind == A.COL_FIXED:
         return "fixed"
-    return "lb" if len(col) == 3 else "var"
+    k = _DEPTH.get(ci.kind)
+    if k is None or not isinstance(col, tuple) or len(col) != k + 1:
+        raise KxError(A.ERR_INVALID_ARG, f"concat: column kind {ci.kind} does not match its layout")
+    return k
 
 
 def _meta(cols: ColumnSet, n: int, infos, in_len: int, dev):
-    """this rank's exchange header, built on the device: n, input bytes, then per var column its first
-    offset and units (and for 'lb' the first element byte offset and bytes)"""
+    """this rank's exchange header, built on the device: n, input bytes, then per var column and per
+    level j of its offsets chain the first entry f_j and the units u_j it spans (f_0 = o_0[0],
+    u_0 = o_0[n] - f_0; f_{j+1} = o_{j+1}[f_j], u_{j+1} = o_{j+1}[f_j + u_j] - f_{j+1})"""
     import torch
     parts = [torch.tensor([n, in_len], dtype=torch.int64, device=dev)]
     for c, ci in enumerate(infos):
         k = _kind(cols.cols[c], ci)
-        if k in ("var", "lb"):
-            off = cols.cols[c][0]
-            f, l = _unsigned(off[0:1]), _unsigned(off[n:n + 1])
+        if isinstance(k, int):
+            col = cols.cols[c]
+            f, l = _unsigned(col[0][0:1]), _unsigned(col[0][n:n + 1])
             parts += [f, l - f]
-            if k == "lb":
-                eo = cols.cols[c][1]
-                ef, el = _unsigned(eo.index_select(0, f)), _unsigned(eo.index_select(0, l))
-                parts += [ef, el - ef]
+            for j in range(1, k):
+                f, l = _unsigned(col[j].index_select(0, f)), _unsigned(col[j].index_select(0, l))
+                parts += [f, l - f]
     return torch.cat(parts)
 
 
@@ -85,30 +96,40 @@ def rebase_views(dst, src, delta: int):
 
 
 class _Plan:
-    """Where every rank's slice lands in the concatenation, from the ranks' exchange headers (_meta)."""
+    """Where every rank's slice lands in the concatenation, from the ranks' exchange headers (_meta).
+    For a column of depth k, rank r sends o_0[:n] and, for j = 1 .. k-1, the o_j entries its o_{j-1}
+    slice spans, then its data; the root rebases its o_j slice by (the units of o_{j+1} (or data) the
+    ranks before it hold) - f_{j+1}(r), and closes every level with the total."""
 
     def __init__(self, metas, kinds):
         self.kinds = kinds
         self.world = world = len(metas)
         self.counts = [m[0] for m in metas]
         inl = [m[1] for m in metas]
-        self.info = []  # per rank, per var column: (first, units, first element byte, bytes)
+        self.info = []  # per rank, per var column: [(f_j, u_j) for each level j]
         for m in metas:
             i, d = 2, {}
             for c, k in enumerate(kinds):
-                if k == "var":
-                    d[c] = (m[i], m[i + 1], 0, 0)
-                    i += 2
-                elif k == "lb":
-                    d[c] = (m[i], m[i + 1], m[i + 2], m[i + 3])
-                    i += 4
+                if isinstance(k, int):
+                    d[c] = [(m[i + 2 * j], m[i + 2 * j + 1]) for j in range(k)]
+                    i += 2 * k
             self.info.append(d)
         self.N = sum(self.counts)
         self.rec0 = [sum(self.counts[:r]) for r in range(world)]
         self.in0 = [sum(inl[:r]) for r in range(world)]
-        cs = [c for c, k in enumerate(kinds) if k in ("var", "lb")]
-        self.ub = {c: [sum(self.info[q][c][1] for q in range(r)) for r in range(world + 1)] for c in cs}
-        self.bb = {c: [sum(self.info[q][c][3] for q in range(r)) for r in range(world + 1)] for c in cs}
+        # base[c][j][r]: units of level j held by the ranks before r (r = world: the total)
+        self.base = {c: [[sum(self.info[q][c][j][1] for q in range(r)) for r in range(world + 1)]
+                         for j in range(k)]
+                     for c, k in enumerate(kinds) if isinstance(k, int)}
+
+    def _slices(self, c, k, r, n):
+        """(start, length) of rank r's piece of each array o_0 .. o_{k-1}, data, in its own column"""
+        info = self.info[r][c]
+        out = [(0, n)]
+        for j in range(1, k):
+            out.append(info[j - 1])       # o_j entries spanned by the o_{j-1} slice
+        out.append(info[k - 1])           # data units spanned by o_{k-1}
+        return out
 
     def local_parts(self, cs: ColumnSet, r: int, n: int):
         """what rank r contributes, in a fixed order: per column its pieces, then presence"""
@@ -120,11 +141,8 @@ class _Plan:
             elif k == "view":
                 out.append(col.pairs[:n])
             else:
-                f, u, ef, eb = self.info[r][c]
-                out.append(col[0][:n])
-                out.append(col[1][f:f + u])
-                if k == "lb":
-                    out.append(col[2][ef:ef + eb])
+                for j, (a, u) in enumerate(self._slices(c, k, r, n)):
+                    out.append(col[j][a:a + u])
         if cs.presence is not None:
             out.append(cs.presence[:n])
         return out
@@ -144,20 +162,20 @@ class _Plan:
             elif k == "view":
                 out_cols.append(Views(torch.empty((max(1, N), 2), dtype=torch.int64, device=dev)))
                 self.recv[c] = (torch.empty((max(1, N), 2), dtype=col.pairs.dtype, device=dev),)
-            elif k == "var":
-                out_cols.append((torch.empty(N + 1, dtype=torch.int64, device=dev),
-                                 torch.empty(max(1, self.ub[c][W]), dtype=col[1].dtype, device=dev)))
-                self.recv[c] = (torch.empty(max(1, N), dtype=col[0].dtype, device=dev),)
             else:
-                E = self.ub[c][W]
-                out_cols.append((torch.empty(N + 1, dtype=torch.int64, device=dev),
-                                 torch.empty(E + 1, dtype=torch.int64, device=dev),
-                                 torch.empty(max(1, self.bb[c][W]), dtype=col[2].dtype, device=dev)))
-                self.recv[c] = (torch.empty(max(1, N), dtype=col[0].dtype, device=dev),
-                                torch.empty(max(1, E), dtype=col[1].dtype, device=dev))
+                sizes = [N] + [self.base[c][j - 1][W] for j in range(1, k)]   # entries of o_j before closing
+                parts = [torch.empty(s + 1, dtype=torch.int64, device=dev) for s in sizes]
+                parts.append(torch.empty(max(1, self.base[c][k - 1][W]), dtype=col[k].dtype, device=dev))
+                out_cols.append(tuple(parts))
+                self.recv[c] = tuple(torch.empty(max(1, s), dtype=col[j].dtype, device=dev)
+                                     for j, s in enumerate(sizes))
         pres = torch.empty(N, dtype=like.presence.dtype, device=dev) if like.presence is not None else None
         self.out = ColumnSet(out_cols, pres, N)
         return self.out
+
+    def _dest_off(self, c, j, r):
+        """where rank r's piece of o_j (j >= 1: entries of level j - 1) or data (j = k) starts"""
+        return self.rec0[r] if j == 0 else self.base[c][j - 1][r]
 
     def dest_parts(self, r: int):
         """where rank r's pieces (local_parts order) are received"""
@@ -169,21 +187,16 @@ class _Plan:
             elif k == "view":
                 d.append(self.recv[c][0][a:b])
             else:
-                f, u, ef, eb = self.info[r][c]
-                u0 = self.ub[c][r]
-                d.append(self.recv[c][0][a:b])
-                if k == "lb":
-                    d.append(self.recv[c][1][u0:u0 + u])
-                    d.append(out.cols[c][2][self.bb[c][r]:self.bb[c][r] + eb])
-                else:
-                    d.append(out.cols[c][1][u0:u0 + u])
+                for j, (_, u) in enumerate(self._slices(c, k, r, self.counts[r])):
+                    s0 = self._dest_off(c, j, r)
+                    d.append((self.recv[c][j] if j < k else out.cols[c][k])[s0:s0 + u])
         if out.presence is not None:
             d.append(out.presence[a:b])
         return d
 
     def rebase_all(self):
-        """every rank's slice, on the device: record offsets by the units before it, element byte offsets
-        by the bytes before it, views by the input bytes before it; then the closing offsets"""
+        """every rank's slice, on the device: level j's entries by the units of level j + 1 (or data)
+        before it, views by the input bytes before it; then the closing entry of every level"""
         out, W = self.out, self.world
         for c, k in enumerate(self.kinds):
             if k == "fixed":
@@ -193,16 +206,15 @@ class _Plan:
                 if k == "view":
                     rebase_views(out.cols[c].pairs[a:b], self.recv[c][0][a:b], self.in0[r])
                     continue
-                f, u, ef, eb = self.info[r][c]
-                u0 = self.ub[c][r]
-                rebase(out.cols[c][0][a:b], self.recv[c][0][a:b], u0 - f)
-                if k == "lb":
-                    rebase(out.cols[c][1][u0:u0 + u], self.recv[c][1][u0:u0 + u], self.bb[c][r] - ef)
+                for j, (_, u) in enumerate(self._slices(c, k, r, self.counts[r])[:k]):
+                    s0 = self._dest_off(c, j, r)
+                    f_next = self.info[r][c][j][0]
+                    rebase(out.cols[c][j][s0:s0 + u], self.recv[c][j][s0:s0 + u], self.base[c][j][r] - f_next)
             if k == "view":
                 continue
-            out.cols[c][0][self.N] = self.ub[c][W]
-            if k == "lb":
-                out.cols[c][1][self.ub[c][W]] = self.bb[c][W]
+            for j in range(k):
+                end = self.N if j == 0 else self.base[c][j - 1][W]
+                out.cols[c][j][end] = self.base[c][j][W]
 
 
 def _check_views(kinds, in_len):

@@ -164,3 +164,31 @@ def test_large_batch_timed(torch, dev, oracle):
     assert_columns_equal(res.columns, exp, infos, k)
     rc, back, _ = oracle.encode(sch, oracle.decode(sch, wire, n)[1])
     assert np.array_equal(to_np(got), back)
+
+
+def test_unmarshal_extents_sized_exactly(torch, dev, oracle):
+    """UnmarshalExtents of a nested schema without var_caps sizes its arenas with the measure pass over
+    the same extents (kx_thrift_decode_sizes_extents) instead of one buf-sized arena per column; the
+    bodies sit at gaps (ttstream frames between them) and decode as the oracle does"""
+    cdc = codec("nx")
+    sch = SCHEMAS["nx"]
+    n = 900
+    _, wire, offs = NC.batch(sch, n, seed=8)
+    gap = 5
+    buf_np = np.zeros(wire.size + gap * (n + 1), dtype=np.uint8)
+    starts = np.zeros(n, dtype=np.int64)
+    ends = np.zeros(n, dtype=np.int64)
+    for i in range(n):
+        a, b = int(offs[i]), int(offs[i + 1])
+        s0 = a + gap * (i + 1)
+        buf_np[s0:s0 + b - a] = wire[a:b]
+        starts[i], ends[i] = s0, s0 + b - a
+    buf = torch.from_numpy(buf_np).to(dev)
+    res = cdc.UnmarshalExtents(buf, torch.from_numpy(starts).to(dev), torch.from_numpy(ends).to(dev))
+    rc, exp, _, _ = oracle.decode(sch, wire, n, offsets=offs)
+    _, infos, _ = oracle.flatten(sch)
+    for c, ci in enumerate(infos):
+        col = res.columns.cols[c]
+        if isinstance(col, tuple):   # arenas sized to the decoded units, not to the buffer
+            assert col[-1].numel() <= max(1, wire.size)
+    assert_columns_equal(res.columns, exp, infos, n)

@@ -15,6 +15,7 @@ import pytest
 from kitex_amd import _abi as A
 from kitex_amd import idl
 from kitex_amd import schema as S
+from kitex_amd.schema import Field
 from tests import nested_cases as NC
 from tests.helpers import assert_columns_equal
 
@@ -235,3 +236,19 @@ def test_idl_example_method_columns(oracle):
     rc, infos, npres = oracle.flatten(sch)
     assert rc == 0 and len(infos) == 25 and npres == 14
     assert sum(1 for ci in infos if ci.kind == A.COL_LIST_BYTES) == 4    # two Extra maps: keys, values
+
+
+def test_device_limits_enforced_at_schema_create():
+    """a nested program needing more cursors than the device walker holds per lane (KXN_MAX_CUR) is
+    refused when the schema is created, not at its first decode"""
+    from kitex_amd._lib import KxError
+    from kitex_amd.codec import DeviceSchema
+
+    def wide(k):
+        return S.Schema(S.Struct("W", [Field(i + 1, A.T_MAP, f"f{i}", elem=A.T_STRING, val=A.T_STRING)
+                                       for i in range(k)]))
+    ds = DeviceSchema(wide(12))       # 12 x (entry domain + key bytes + value bytes) cursors: fine
+    assert ds.nested
+    with pytest.raises(KxError) as e:
+        DeviceSchema(wide(30))        # 90 cursors > 64, 60 columns
+    assert e.value.code == A.ERR_NOT_IMPLEMENTED

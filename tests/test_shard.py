@@ -265,3 +265,46 @@ def test_concat_local_matches_whole(oracle, name, views):
     rc, exp, est, _ = oracle.decode(sch, np.concatenate(wires), n, views=views)
     assert est.code == 0
     assert_columns_equal(out, exp, infos, n)
+
+
+@pytest.mark.parametrize("name", ["nesting", "nx"])
+def test_concat_local_nested(oracle, name):
+    """nested schemas: LIST2 (record -> element -> value) and LIST2_BYTES (record -> element -> inner
+    element -> bytes) columns keep every level of their offsets chain through the concatenation"""
+    from kitex_amd import _abi as A
+    from kitex_amd.shard import concat_local
+    from tests import nested_cases as NC
+    from tests.helpers import assert_columns_equal
+    sch = {"nesting": S.schema_nesting, "nx": S.schema_nx}[name]()
+    rc, infos, _ = oracle.flatten(sch)
+    assert rc == 0
+    kinds = {ci.kind for ci in infos}
+    assert A.COL_LIST2_BYTES in kinds or name == "nesting"
+    n, parts = 700, 3
+    _, wire, offs = NC.batch(sch, n, seed=3)
+    shards = []
+    for r in range(parts):
+        s0, cnt = shard_range(n, parts, r)
+        w = wire[int(offs[s0]):int(offs[s0 + cnt])]
+        rc, local, st, _ = oracle.decode(sch, w, cnt)
+        assert rc == 0 and st.code == 0
+        shards.append((_to_torch(local), cnt, w.size))
+    out = concat_local(shards, infos)
+    rc, exp, est, _ = oracle.decode(sch, wire, n)
+    assert est.code == 0
+    assert_columns_equal(out, exp, infos, n)
+
+
+def test_concat_kind_layout_mismatch():
+    """a column whose tuple does not match its kind is refused (was: silently mis-concatenated)"""
+    import torch
+
+    from kitex_amd import _abi as A
+    from kitex_amd._lib import KxError
+    from kitex_amd.shard import concat_local
+    ci = A.ColumnInfo()
+    ci.kind = A.COL_LIST2_BYTES
+    cs = synth.ColumnSet([(torch.zeros(5, dtype=torch.int32), torch.zeros(1, dtype=torch.int32),
+                           torch.zeros(1, dtype=torch.uint8))], None, 4)
+    with pytest.raises(KxError):
+        concat_local([(cs, 4, 0)], [ci])
