@@ -55,7 +55,7 @@
 extern "C" {
 #endif
 
-#define KX_ABI_VERSION 3
+#define KX_ABI_VERSION 4
 
 /* ---- Thrift TType ids (gopkg protocol/thrift; pinned by pkg/protocol/bthrift/binary_test.go) ---- */
 enum {
@@ -113,8 +113,37 @@ typedef struct kx_field_desc {
 typedef struct kx_struct_desc {
   const kx_field_desc* fields; /* host memory, IDL order */
   uint32_t nfields;
-  uint32_t reserved0;
+  uint32_t reserved0;          /* flags; of the root struct (index 0): KX_STRUCT_PROTOBUF */
 } kx_struct_desc;
+
+/* Kitex-Protobuf schemas (ABI v4). KX_STRUCT_PROTOBUF in the root struct's reserved0 marks every struct
+ * of the table as a proto3 message: field ids are proto field numbers, and since proto3 fields have no
+ * defaults, default_bits carries the proto scalar kind instead: bits 0..7 of the field itself (of its
+ * elements for a repeated field, of its key for a map), bits 8..15 of a map's value.
+ *   proto type                    ttype        kind
+ *   int32, enum / int64           I32 / I64    KX_PB_NATURAL (varint; int32 sign-extends on the wire)
+ *   uint32 / uint64               I32 / I64    KX_PB_UINT (uint32 zero-extends)
+ *   sint32 / sint64               I32 / I64    KX_PB_SINT (zig-zag varint)
+ *   fixed32, sfixed32, float      I32          KX_PB_FIXED (4 bytes LE; a float column holds its bits)
+ *   fixed64, sfixed64             I64          KX_PB_FIXED (8 bytes LE)
+ *   double / bool                 DOUBLE / BOOL KX_PB_NATURAL
+ *   string / bytes                STRING       KX_PB_NATURAL (UTF-8 checked) / KX_PB_BYTES (or KX_FIELD_BINARY)
+ *   message M                     STRUCT       child = M
+ *   repeated T                    LIST         elem_ttype = T (child for messages), kind of T
+ *   map<K, V>                     MAP          elem_ttype = K | V << 4, kinds K | V << 8
+ * Columns follow the nested model below (flat proto3 schemas keep the flat layout). Decoding is
+ * proto.Unmarshal (protobuf-go, google.golang.org/protobuf/encoding/protowire): a singular scalar or
+ * string takes its last occurrence, a message field merges its occurrences, a repeated field appends
+ * (packed and unpacked runs alike for scalars), a map appends its entries in wire order (building a Go
+ * map by inserting them in order gives proto.Unmarshal's map: the last duplicate key wins; a missing key
+ * or value is the zero value); unknown numbers and known numbers with another wire type are skipped;
+ * `string` must be valid UTF-8 (KX_ERR_INVALID_DATA). Presence bits: message fields, proto3 `optional`
+ * scalars (KX_REQ_OPTIONAL), repeated and map fields (the field occurred). Encoding is proto.Marshal:
+ * field-number order, zero scalars and empty strings omitted (unless `optional` and present), a present
+ * message written even when empty, repeated scalars packed, map entries with key and value always
+ * written, in column order. */
+#define KX_STRUCT_PROTOBUF 1u
+enum { KX_PB_NATURAL = 0, KX_PB_SINT = 1, KX_PB_FIXED = 2, KX_PB_UINT = 3, KX_PB_BYTES = 4 };
 
 typedef struct kx_schema kx_schema; /* opaque */
 
@@ -318,11 +347,12 @@ int kx_thrift_encode_messages(kx_ctx* c, const kx_schema* s, const kx_columns* i
                               uint64_t* offsets_out, kx_status* status, void* stream);
 
 /* ---- Kitex-Protobuf (proto3 body) ----
- * The schema's field ids are proto field numbers; ttype selects the proto scalar mapping
- * (I64 = int64 varint, I32 = int32 varint, BOOL, DOUBLE = fixed64, STRING = string/bytes).
- * Repeated / packed fields, maps and nested messages are not supported on this path
- * (KX_ERR_NOT_IMPLEMENTED); unknown fields are skipped. offsets semantics as kx_thrift_decode_batch; with
- * offsets == NULL the input is the body of `message Batch { repeated Rec recs = 1; }`. */
+ * The schema's field ids are proto field numbers; ttype (and, with KX_STRUCT_PROTOBUF, the kind in
+ * default_bits) selects the proto type, see KX_STRUCT_PROTOBUF above: scalars of every proto3 type,
+ * strings / bytes, nested messages, repeated fields (packed and unpacked), maps, proto3 `optional`.
+ * Flat messages run on the tile pipeline; anything else on the nested record walker. offsets semantics
+ * as kx_thrift_decode_batch; with offsets == NULL the input is the body of
+ * `message Batch { repeated Rec recs = 1; }`. */
 int kx_pb_decode_batch(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len,
                        const uint64_t* offsets, uint64_t n, const kx_columns* out,
                        uint8_t* record_status, kx_status* status, void* stream);

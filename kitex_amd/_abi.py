@@ -6,7 +6,7 @@ layout is checked by tests/test_abi.py against the compiled library.
 """
 import ctypes as C
 
-KX_ABI_VERSION = 3
+KX_ABI_VERSION = 4
 
 # Thrift TType ids (gopkg protocol/thrift; pinned by pkg/protocol/bthrift/binary_test.go)
 T_STOP, T_VOID, T_BOOL, T_BYTE, T_DOUBLE = 0, 1, 2, 3, 4
@@ -40,6 +40,9 @@ ERR_INTERNAL = 103
 REQ_DEFAULT, REQ_REQUIRED, REQ_OPTIONAL = 0, 1, 2
 FIELD_BINARY = 1  # kx_field_desc.reserved0 flag: protobuf `bytes` (no UTF-8 validation)
 FIELD_STRING_DEFAULT = 2  # ... default_bits points at the field's NUL-terminated string default
+STRUCT_PROTOBUF = 1  # kx_struct_desc.reserved0 of the root struct: a Kitex-Protobuf schema (ABI v4)
+# proto scalar kinds (default_bits of a Kitex-Protobuf field: bits 0..7 field / element / key, 8..15 map value)
+PB_NATURAL, PB_SINT, PB_FIXED, PB_UINT, PB_BYTES = 0, 1, 2, 3, 4
 
 COL_FIXED, COL_BYTES, COL_LIST, COL_LIST_BYTES = 1, 2, 3, 4
 COL_LIST2, COL_LIST2_BYTES = 5, 6   # nested schemas: two container levels down

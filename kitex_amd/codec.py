@@ -456,7 +456,7 @@ class ThriftCodec:
         ends = ends.to(torch.int64).contiguous()
         if out is None:
             elem_caps = sub_caps = None
-            if var_caps is None and ds.nested and self._EXTENTS == "kx_thrift_decode_extents":
+            if var_caps is None and ds.nested:
                 # exact arenas from the measure pass over the same extents (a connection buffer's worth of
                 # buf-sized arenas per column would not fit for wide nested schemas)
                 units = self.DecodeSizes(buf, n, starts, stream=stream, ends=ends)

@@ -317,12 +317,27 @@ const char* kx_strerror(int code) {
   }
 }
 
+// A Kitex-Protobuf schema stays on the flat program only as a flat proto3 message the tile pipeline's
+// proto walker reads: scalars of the natural kinds (int32 / int64 varint, bool, double) and strings /
+// bytes. Everything else (other kinds, messages, repeated, maps) goes to the nested walker.
+static bool pb_flat_ok(const kx_struct_desc* structs, uint32_t nstructs) {
+  if (!structs || nstructs != 1 || (structs[0].nfields && !structs[0].fields)) return false;
+  for (uint32_t i = 0; i < structs[0].nfields; i++) {
+    const kx_field_desc& f = structs[0].fields[i];
+    const bool ok_t = f.ttype == KX_T_BOOL || f.ttype == KX_T_I32 || f.ttype == KX_T_I64 ||
+                      f.ttype == KX_T_DOUBLE || f.ttype == KX_T_STRING;
+    if (!ok_t || (f.default_bits & 0xffff) != 0 || f.req == KX_REQ_REQUIRED) return false;
+  }
+  return true;
+}
+
 int kx_schema_create(const kx_struct_desc* structs, uint32_t nstructs, kx_schema** out) {
   if (!out) return KX_ERR_INVALID_ARG;
   *out = nullptr;
   kx_schema* s = new (std::nothrow) kx_schema();
   if (!s) return KX_ERR_INTERNAL;
-  int rc = kx_build_program(structs, nstructs, s);
+  const bool pb = structs && nstructs && (structs[0].reserved0 & KX_STRUCT_PROTOBUF);
+  int rc = pb && !pb_flat_ok(structs, nstructs) ? KX_ERR_NOT_IMPLEMENTED : kx_build_program(structs, nstructs, s);
   if (rc == KX_ERR_NOT_IMPLEMENTED) rc = kx_build_nested(structs, nstructs, s);
   if (rc) {
     delete s;
@@ -426,7 +441,10 @@ int kx_thrift_decode_batch(kx_ctx* c, const kx_schema* s, const uint8_t* in, uin
   int rc = set_device(c);
   if (rc) return rc;
   hipStream_t st = (hipStream_t)stream;
-  if (s->nprog) return nested_decode(c, s, in, in_len, offsets, nullptr, n, out, record_status, status, st, nullptr);
+  if (s->nprog) {
+    if (s->nprog->pb) return KX_ERR_NOT_IMPLEMENTED;   // a Kitex-Protobuf schema: kx_pb_decode_batch
+    return nested_decode(c, s, in, in_len, offsets, nullptr, n, out, record_status, status, st, nullptr);
+  }
   KxLaunchCols lc;
   if ((rc = to_launch_cols(s, out, &lc, true, in_len))) return rc;
   if (n == 0) {
@@ -515,7 +533,10 @@ int kx_thrift_encoded_size_batch(kx_ctx* c, const kx_schema* s, const kx_columns
   int rc = set_device(c);
   if (rc) return rc;
   hipStream_t st = (hipStream_t)stream;
-  if (s->nprog) return nested_encode(c, s, in, n, nullptr, 0, sizes_out, nullptr, nullptr, st, true);
+  if (s->nprog) {
+    if (s->nprog->pb) return KX_ERR_NOT_IMPLEMENTED;   // a Kitex-Protobuf schema: kx_pb_encoded_size_batch
+    return nested_encode(c, s, in, n, nullptr, 0, sizes_out, nullptr, nullptr, st, true);
+  }
   KxLaunchCols lc;
   if ((rc = to_launch_cols(s, in, &lc))) return rc;
   if (n == 0) return KX_OK;
@@ -532,6 +553,7 @@ int kx_thrift_encode_batch(kx_ctx* c, const kx_schema* s, const kx_columns* in, 
   int rc = set_device(c);
   if (rc) return rc;
   hipStream_t st = (hipStream_t)stream;
+  if (s->nprog && s->nprog->pb) return KX_ERR_NOT_IMPLEMENTED;   // a Kitex-Protobuf schema: kx_pb_encode_batch
   if (s->nprog && n) return nested_encode(c, s, in, n, out, out_cap, nullptr, offsets_out, status, st, false);
   KxLaunchCols lc;
   if (!s->nprog && (rc = to_launch_cols(s, in, &lc))) return rc;
@@ -606,6 +628,10 @@ int kx_pb_decode_batch(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_
   int rc = set_device(c);
   if (rc) return rc;
   hipStream_t st = (hipStream_t)stream;
+  if (s->nprog) {   // nested proto3 messages (KX_STRUCT_PROTOBUF): the nested walker in proto mode
+    if (!s->nprog->pb) return KX_ERR_NOT_IMPLEMENTED;
+    return nested_decode(c, s, in, in_len, offsets, nullptr, n, out, record_status, status, st, nullptr);
+  }
   KxLaunchCols lc;
   if ((rc = to_launch_cols(s, out, &lc, true, in_len))) return rc;
   if ((rc = pb_schema_ok(s))) return rc;
@@ -881,7 +907,10 @@ static int decode_extents(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint
   int rc = set_device(c);
   if (rc) return rc;
   hipStream_t st = (hipStream_t)stream;
-  if (s->nprog && !pb && n) return nested_decode(c, s, in, in_len, starts, ends, n, out, record_status, status, st, nullptr);
+  if (s->nprog && n) {   // nested schemas: the walker of the call's wire format
+    if ((s->nprog->pb != 0) != pb) return KX_ERR_NOT_IMPLEMENTED;
+    return nested_decode(c, s, in, in_len, starts, ends, n, out, record_status, status, st, nullptr);
+  }
   KxLaunchCols lc;
   if ((rc = to_launch_cols(s, out, &lc, true, in_len))) return rc;
   if (n == 0) {
@@ -989,8 +1018,12 @@ int kx_pb_encoded_size_batch(kx_ctx* c, const kx_schema* s, const kx_columns* in
   if (!c || !s || !sizes_out) return KX_ERR_INVALID_ARG;
   int rc = set_device(c);
   if (rc) return rc;
-  if ((rc = pb_schema_ok(s))) return rc;
   hipStream_t st = (hipStream_t)stream;
+  if (s->nprog) {
+    if (!s->nprog->pb) return KX_ERR_NOT_IMPLEMENTED;
+    return nested_encode(c, s, in, n, nullptr, 0, sizes_out, nullptr, nullptr, st, true);
+  }
+  if ((rc = pb_schema_ok(s))) return rc;
   KxLaunchCols lc;
   if ((rc = to_launch_cols(s, in, &lc))) return rc;
   if (n == 0) return KX_OK;
@@ -1006,8 +1039,17 @@ int kx_pb_encode_batch(kx_ctx* c, const kx_schema* s, const kx_columns* in, uint
   if (!c || !s || !status || (!out && out_cap)) return KX_ERR_INVALID_ARG;
   int rc = set_device(c);
   if (rc) return rc;
-  if ((rc = pb_schema_ok(s))) return rc;
   hipStream_t st = (hipStream_t)stream;
+  if (s->nprog) {
+    if (!s->nprog->pb) return KX_ERR_NOT_IMPLEMENTED;
+    if (n == 0) {
+      KX_HIP_CHECK(hipMemsetAsync(status, 0, sizeof(kx_status), st));
+      if (offsets_out) KX_HIP_CHECK(hipMemsetAsync(offsets_out, 0, 8, st));
+      return KX_OK;
+    }
+    return nested_encode(c, s, in, n, out, out_cap, nullptr, offsets_out, status, st, false);
+  }
+  if ((rc = pb_schema_ok(s))) return rc;
   KxLaunchCols lc;
   if ((rc = to_launch_cols(s, in, &lc))) return rc;
   if (n == 0) {

@@ -91,7 +91,8 @@ struct DecParams {
   uint64_t* fr_pe;
   uint8_t* fr_kind;
   uint64_t fr_max;           // M_FRAME: payload size limit (0: none)
-  int fr_grpc;               // M_FRAME: 0 default-codec sniff, 1 gRPC length-prefixed messages, 2 ttstream
+  int fr_grpc;               // M_FRAME: 0 default-codec sniff, 1 gRPC length-prefixed messages, 2 ttstream,
+                             // 3 Kitex-PB Batch frames (nested proto schemas' record extents)
   int32_t* fr_sid;           // ttstream: stream id (TTHeader seqid), method position / length per frame
   uint64_t* fr_mpos;
   uint32_t* fr_mlen;
@@ -1559,6 +1560,24 @@ __device__ __forceinline__ int frame_grpc(const Src& w, uint64_t pos, uint64_t l
   return KX_OK;
 }
 
+// Kitex-Protobuf Batch frame (`message Batch { repeated Rec recs = 1; }`): 0x0A, uvarint body length,
+// body; payload = the body (the nested proto walker's record extent)
+__device__ __forceinline__ int frame_pbb(const Src& w, uint64_t pos, uint64_t lim, uint64_t* end, uint64_t& ps,
+                                         uint64_t& pe, uint32_t& kind) {
+  if (pos >= lim) return KX_ERR_EOF;
+  if (ld1(w, pos) != 0x0Au) return KX_ERR_INVALID_DATA;
+  uint64_t l;
+  uint32_t u;
+  const int rc = pb_varint(w, pos + 1, lim - pos - 1, l, u);
+  if (rc) return rc;
+  if (l > lim - pos - 1 - u) return KX_ERR_EOF;
+  kind = 0;
+  ps = pos + 1 + u;
+  pe = ps + l;
+  *end = pe;
+  return KX_OK;
+}
+
 // ttstream DecodeFrame (pkg/remote/trans/ttstream/frame.go:137-185): a TTHeader whose payload is a bare
 // struct. kind = the frame type (KX_TTS_*, from IntInfo[frame type key]); *sid the TTHeader seqid, *mp /
 // *ml IntInfo[ToMethod] (input position, 0 / 0 when absent); the last occurrence of a key wins. Same
@@ -1671,7 +1690,8 @@ __device__ __forceinline__ int parse_record(KParams& dp, const Src& w, uint64_t 
     uint64_t ps, pe, mp = 0;
     uint32_t kind, ml = 0;
     int32_t sid = 0;
-    const int rc = dp.fr_grpc == 2 ? frame_tts(dp, w, pos, lim, end, ps, pe, kind, sid, mp, ml)
+    const int rc = dp.fr_grpc == 3 ? frame_pbb(w, pos, lim, end, ps, pe, kind)
+                   : dp.fr_grpc == 2 ? frame_tts(dp, w, pos, lim, end, ps, pe, kind, sid, mp, ml)
                    : dp.fr_grpc ? frame_grpc(w, pos, lim, dp.fr_max, end, ps, pe, kind)
                                 : frame_one(w, pos, lim, dp.fr_max, end, ps, pe, kind);
     if (emit && !rc) {
@@ -1775,7 +1795,7 @@ __device__ __forceinline__ Cand lane_candidate(KParams& dp, const Src& w, uint64
   Cand cd;
   cd.ent = X_NONE; cd.plim = seg_lo; cd.sig = 0; cd.smask = 0xffu; cd.s2o = 0; cd.s2 = 0; cd.strict = false;
   if (seg_lo >= seg_hi) return cd;
-  if (MODE == M_PB) {
+  if (MODE == M_PB || (MODE == M_FRAME && dp.fr_grpc == 3)) {   // Kitex-PB Batch frames
     cd.ent = pb_scan_segment(w, seg_lo, seg_hi, dp.in_len, lane);
     return cd;
   }
@@ -3480,6 +3500,21 @@ int kx_launch_skip(const uint8_t* in, uint64_t in_len, uint64_t n, uint64_t* off
   const WsLayout L = ws_layout(1, in_len, nullptr, n);
   if (ws_size < L.total) return KX_ERR_INVALID_ARG;
   return kx_dec_launch<0, M_SKIP>(&dp, &L, ws, stream, nullptr);
+}
+
+int kx_launch_pb_frames(const uint8_t* in, uint64_t in_len, uint64_t n, uint64_t* frame_offsets, uint64_t* body_start,
+                        uint64_t* body_end, kx_status* status, void* ws, size_t ws_size, uint64_t epoch,
+                        hipStream_t stream) {
+  DecParams dp{};
+  fill_diag_flags(dp);
+  dp.in = in; dp.in_len = in_len; dp.offsets = nullptr; dp.n = n; dp.prog = nullptr;
+  dp.status = status; dp.skip_out = frame_offsets; dp.epoch = epoch;
+  dp.fr_ps = body_start; dp.fr_pe = body_end; dp.fr_grpc = 3;
+  dp.krec = 64;
+  dp.winb = TILE + HALO + 16;
+  const WsLayout L = ws_layout(1, in_len, nullptr, n);
+  if (ws_size < L.total) return KX_ERR_INVALID_ARG;
+  return kx_dec_launch<0, M_FRAME>(&dp, &L, ws, stream, nullptr);
 }
 
 int kx_launch_frames(const uint8_t* in, uint64_t in_len, uint64_t n, uint64_t max_payload, uint64_t* frame_offsets,

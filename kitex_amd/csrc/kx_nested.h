@@ -61,6 +61,8 @@ struct KxnNode {        // a value position: a field's value, a container's elem
   int16_t rep_col;      // LIST / MAP: a column whose array `level` counts its elements (encode)
   uint8_t etype, vtype; // LIST: element wire type; MAP: key, value wire types (encode headers)
   uint16_t cur_lo, cur_hi;  // cursors of this value's subtree
+  uint8_t pbk;          // Kitex-Protobuf: proto scalar kind (KX_PB_*) of a SCALAR / STRING value
+  uint8_t pad;
 };
 
 struct KxnField {       // 32 B
@@ -137,7 +139,8 @@ struct KxnCol {         // per column (16 B)
 struct KxnProgram {
   uint32_t nnodes, nfields, nstructs, nroots, ncur, nent, ndfl, nsdf, nsnap, ncols, npres, ndefb;
   int16_t rec_node;     // the record's STRUCT node
-  int16_t pad[3];
+  int16_t pb;           // a Kitex-Protobuf schema: proto3 wire format (kxn_pb_*), field-number encoder order
+  int16_t pad[2];
   KxnNode node[KXN_MAX_NODES];
   KxnField f[KXN_MAX_FIELDS];
   KxnStruct st[KXN_MAX_STRUCTS];
@@ -693,4 +696,588 @@ KXN_HD uint64_t kxn_write_record(const KxnProgram& P, const KxnCols& C, uint64_t
     }
   }
   return pos - pos0;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Kitex-Protobuf (proto3) on the same program and columns (KxnProgram.pb): proto.Unmarshal and
+// proto.Marshal as protobuf-go does them (google.golang.org/protobuf: encoding/protowire for the wire
+// format, internal/impl for the message semantics; not vendored in the reference, which calls them from
+// pkg/remote/codec/protobuf/protobuf.go:64-134,209-216). A singular scalar or string keeps its last
+// occurrence (a string rewinds its byte cursor to the first occurrence's snapshot), a message field merges
+// its occurrences (no rewind, no reset), a repeated field appends one element per occurrence (scalars also
+// as packed runs), a map appends one entry per occurrence (its key and value default to zero); unknown
+// numbers and known numbers with another wire type are skipped.
+
+KXN_HD int kxn_uvarint(const uint8_t* b, uint64_t end, uint64_t* q, uint64_t* v) {  // protowire.ConsumeVarint
+  uint64_t x = 0;
+  for (int i = 0; i < 10; i++) {
+    if (*q + (uint64_t)i >= end) return KX_ERR_EOF;
+    const uint32_t c = b[*q + (uint64_t)i];
+    if (i == 9 && c > 1) return KX_ERR_INVALID_DATA;   // more than 64 bits
+    x |= (uint64_t)(c & 0x7f) << (7 * i);
+    if (c < 0x80) {
+      *v = x;
+      *q += (uint64_t)i + 1;
+      return KX_OK;
+    }
+  }
+  return KX_ERR_INVALID_DATA;
+}
+
+KXN_HD uint32_t kxn_uvlen(uint64_t v) {
+  uint32_t n = 1;
+  while (v >= 0x80) { v >>= 7; n++; }
+  return n;
+}
+
+// wire type of one value of node N (scalars by kind; strings, bytes, messages and map entries: 2)
+KXN_HD uint32_t kxn_pb_wt(const KxnNode& N) {
+  if (N.kind != KN_SCALAR) return 2;
+  if (N.ttype == KX_T_DOUBLE) return 1;
+  if (N.pbk == KX_PB_FIXED) return N.ttype == KX_T_I32 ? 5u : 1u;
+  return 0;
+}
+
+KXN_HD int kxn_pb_skip(const uint8_t* b, uint64_t end, uint64_t* q, uint32_t wt) {
+  uint64_t v;
+  switch (wt) {
+    case 0: return kxn_uvarint(b, end, q, &v);
+    case 1: if (end - *q < 8) return KX_ERR_EOF; *q += 8; return KX_OK;
+    case 2: {
+      const int rc = kxn_uvarint(b, end, q, &v);
+      if (rc) return rc;
+      if (v > end - *q) return KX_ERR_EOF;
+      *q += v;
+      return KX_OK;
+    }
+    case 5: if (end - *q < 4) return KX_ERR_EOF; *q += 4; return KX_OK;
+    default: return KX_ERR_INVALID_DATA;   // groups (3, 4) and 6, 7: rejected (as the flat proto path)
+  }
+}
+
+KXN_HD uint64_t kxn_le(const uint8_t* p, int n) {
+  uint64_t v = 0;
+  for (int k = n - 1; k >= 0; k--) v = (v << 8) | p[k];
+  return v;
+}
+
+// one scalar of node N at b[*q] (its wire type already matched), in the column's host form
+KXN_HD int kxn_pb_scalar(const KxnNode& N, const uint8_t* b, uint64_t end, uint64_t* q, uint64_t* out) {
+  const uint32_t wt = kxn_pb_wt(N);
+  uint64_t v;
+  if (wt == 0) {
+    const int rc = kxn_uvarint(b, end, q, &v);
+    if (rc) return rc;
+    if (N.ttype == KX_T_BOOL) {
+      v = v != 0;
+    } else if (N.pbk == KX_PB_SINT) {   // protowire.DecodeZigZag (sint32: of the low 32 bits)
+      if (N.ttype == KX_T_I32) {
+        const uint32_t u = (uint32_t)v;
+        v = (uint64_t)((u >> 1) ^ (0u - (u & 1u)));
+      } else {
+        v = (v >> 1) ^ (0ull - (v & 1ull));
+      }
+    }                                   // int32 / uint32 / enum: the column keeps the low 32 bits
+  } else {
+    const int n = wt == 1 ? 8 : 4;
+    if (end - *q < (uint64_t)n) return KX_ERR_EOF;
+    v = kxn_le(b + *q, n);
+    *q += (uint64_t)n;
+  }
+  *out = v;
+  return KX_OK;
+}
+
+// utf8.Valid, as protobuf-go checks proto3 `string` fields
+KXN_HD bool kxn_utf8(const uint8_t* s, uint64_t n) {
+  uint64_t i = 0;
+  while (i < n) {
+    const uint32_t c = s[i];
+    if (c < 0x80) { i++; continue; }
+    int k;
+    uint32_t cp;
+    if ((c & 0xe0) == 0xc0) { k = 1; cp = c & 0x1f; }
+    else if ((c & 0xf0) == 0xe0) { k = 2; cp = c & 0x0f; }
+    else if ((c & 0xf8) == 0xf0) { k = 3; cp = c & 0x07; }
+    else return false;
+    if (i + (uint64_t)k >= n) return false;
+    for (int j = 1; j <= k; j++) {
+      const uint32_t d = s[i + (uint64_t)j];
+      if ((d & 0xc0) != 0x80) return false;
+      cp = (cp << 6) | (d & 0x3f);
+    }
+    if ((k == 1 && cp < 0x80) || (k == 2 && cp < 0x800) || (k == 3 && cp < 0x10000)) return false;
+    if (cp > 0x10ffff || (cp >= 0xd800 && cp <= 0xdfff)) return false;
+    i += (uint64_t)k + 1;
+  }
+  return true;
+}
+
+struct KxnPFrame {      // an open message (its fields) or map entry (fields 1 / 2) (32 B)
+  uint8_t kind;         // 0 message, 1 map entry
+  uint8_t seen;         // map entry: key / value read (bits 0 / 1)
+  int16_t id;           // message: struct instance; entry: the map node
+  int16_t close;        // root whose instance ends when the frame does (-1)
+  int16_t pad;
+  uint64_t end;         // where its bytes end
+  uint64_t c0[2];       // map entry: cursor of a string key / value at its first occurrence
+};
+
+// one value of node X (wire type matched) into the open instance of its level; a message value pushes a
+// frame (close: the root to end with it), a scalar / string value ends `close` at once
+template <bool W>
+KXN_HD int kxn_pb_value(const KxnProgram& P, const KxnCols& C, const uint8_t* b, uint64_t end, uint64_t* q, int X,
+                        uint64_t* cur, KxnState& S, KxnPFrame* stk, int* sp, int close) {
+  const KxnNode& N = P.node[X];
+  switch (N.kind) {
+    case KN_SCALAR: {
+      uint64_t v;
+      const int rc = kxn_pb_scalar(N, b, end, q, &v);
+      if (rc) return rc;
+      if (W && S.live[N.level]) kxn_put_val(C, N.col, N.width, S.idx[N.level], v);
+      break;
+    }
+    case KN_STRING: case KN_RAW: {   // string / bytes; a recursive message keeps its bytes (they merge)
+      uint64_t l;
+      const int rc = kxn_uvarint(b, end, q, &l);
+      if (rc) return rc;
+      if (l > end - *q) return KX_ERR_EOF;
+      if (N.kind == KN_STRING && N.pbk != KX_PB_BYTES && !kxn_utf8(b + *q, l)) return KX_ERR_INVALID_DATA;
+      if (W) {
+        uint8_t* dst = (uint8_t*)C.data[N.col] + cur[N.cur];
+        const uint64_t room = S.lim[N.cur] > cur[N.cur] ? S.lim[N.cur] - cur[N.cur] : 0;
+        const uint64_t m = l < room ? l : room;
+        for (uint64_t j = 0; j < m; j++) dst[j] = b[*q + j];
+      }
+      cur[N.cur] += l;
+      *q += l;
+      break;
+    }
+    case KN_STRUCT: {
+      uint64_t l;
+      const int rc = kxn_uvarint(b, end, q, &l);
+      if (rc) return rc;
+      if (l > end - *q) return KX_ERR_EOF;
+      if (*sp >= KXN_STACK) return KX_ERR_DEPTH_LIMIT;
+      stk[*sp] = KxnPFrame{0, 0, N.a, (int16_t)close, 0, *q + l, {0, 0}};
+      (*sp)++;
+      return KX_OK;
+    }
+    default:
+      return KX_ERR_INTERNAL;   // containers are opened by the field loop
+  }
+  if (close >= 0) kxn_inst_end<W>(P, C, close, cur, S);
+  return KX_OK;
+}
+
+// proto.Unmarshal of record r = b[0 .. len): same cursors / snapshots / clipping as kxn_read_record
+template <bool W>
+KXN_HD int kxn_pb_read_record(const KxnProgram& P, const KxnCols& C, const uint8_t* b, uint64_t len, uint64_t r,
+                              uint64_t* cur, uint64_t* snap, uint64_t* used, const uint64_t* lim = nullptr) {
+  KxnPFrame stk[KXN_STACK];
+  KxnState S;
+  S.lim = lim;
+  S.live[0] = S.live[1] = S.live[2] = true;
+  S.idx[0] = S.idx[1] = S.idx[2] = 0;
+  S.seen[0] = S.seen[1] = S.seen[2] = 0;
+  S.pres[0] = S.pres[1] = S.pres[2] = 0;
+  int sp = 0;
+  uint64_t q = 0;
+  int rc = KX_OK;
+  kxn_inst_start<W>(P, C, 0, r, cur, S);
+  stk[sp++] = KxnPFrame{0, 0, P.node[P.rec_node].a, -1, 0, len, {0, 0}};
+  while (sp > 0) {
+    KxnPFrame& F = stk[sp - 1];
+    if (q >= F.end) {
+      const int cl = F.close;
+      sp--;
+      if (cl >= 0) kxn_inst_end<W>(P, C, cl, cur, S);
+      continue;
+    }
+    uint64_t tag;
+    if ((rc = kxn_uvarint(b, F.end, &q, &tag))) break;
+    const uint64_t num = tag >> 3;
+    const uint32_t wt = (uint32_t)(tag & 7);
+    if (num == 0 || num > 536870911ull) { rc = KX_ERR_INVALID_DATA; break; }   // protowire.MaxValidNumber
+    if (F.kind == 1) {                                  // map entry: key = 1, value = 2
+      const KxnNode& M = P.node[F.id];
+      const int X = num == 1 ? M.a : num == 2 ? M.b : -1;
+      if (X < 0 || wt != kxn_pb_wt(P.node[X])) {
+        if ((rc = kxn_pb_skip(b, F.end, &q, wt))) break;
+        continue;
+      }
+      const KxnNode& V = P.node[X];
+      const int k = num == 1 ? 0 : 1;
+      if (V.kind == KN_STRING || V.kind == KN_RAW) {    // a repeated key / value string: the last one wins
+        if (F.seen & (1 << k)) cur[V.cur] = F.c0[k];
+        else F.c0[k] = cur[V.cur];
+      }
+      F.seen |= (uint8_t)(1 << k);
+      const uint64_t fe = F.end;
+      if ((rc = kxn_pb_value<W>(P, C, b, fe, &q, X, cur, S, stk, &sp, -1))) break;
+      continue;
+    }
+    const KxnStruct& T = P.st[F.id];
+    const int L = T.level;
+    int fi = -1;
+    for (int k = 0; k < T.nfields; k++)
+      if (P.f[T.first + k].id == (int64_t)num) { fi = T.first + k; break; }
+    if (fi < 0) {                                       // unknown field
+      if ((rc = kxn_pb_skip(b, F.end, &q, wt))) break;
+      continue;
+    }
+    const KxnField& G = P.f[fi];
+    const KxnNode& N = P.node[G.node];
+    const uint64_t bit = 1ull << G.sbit;
+    const uint64_t fend = F.end;
+    if (N.kind == KN_LIST) {                            // repeated: append
+      const KxnNode& E = P.node[N.a];
+      const uint32_t ewt = kxn_pb_wt(E);
+      if (wt == ewt) {
+        S.seen[L] |= bit;
+        if (G.pbit >= 0) S.pres[L] |= 1ull << G.pbit;
+        const uint64_t e = cur[N.cur]++;
+        kxn_inst_start<W>(P, C, N.root, e, cur, S);
+        if ((rc = kxn_pb_value<W>(P, C, b, fend, &q, N.a, cur, S, stk, &sp, N.root))) break;
+      } else if (wt == 2 && E.kind == KN_SCALAR) {      // a packed run
+        uint64_t l;
+        if ((rc = kxn_uvarint(b, fend, &q, &l))) break;
+        if (l > fend - q) { rc = KX_ERR_EOF; break; }
+        S.seen[L] |= bit;
+        if (G.pbit >= 0) S.pres[L] |= 1ull << G.pbit;
+        const uint64_t pend = q + l;
+        while (q < pend) {
+          const uint64_t e = cur[N.cur]++;
+          kxn_inst_start<W>(P, C, N.root, e, cur, S);
+          uint64_t v;
+          if ((rc = kxn_pb_scalar(E, b, pend, &q, &v))) break;
+          if (W && S.live[E.level]) kxn_put_val(C, E.col, E.width, S.idx[E.level], v);
+          kxn_inst_end<W>(P, C, N.root, cur, S);
+        }
+        if (rc) break;
+      } else if ((rc = kxn_pb_skip(b, fend, &q, wt))) {
+        break;
+      }
+      continue;
+    }
+    if (N.kind == KN_MAP) {                             // one entry per occurrence
+      if (wt != 2) {
+        if ((rc = kxn_pb_skip(b, fend, &q, wt))) break;
+        continue;
+      }
+      uint64_t l;
+      if ((rc = kxn_uvarint(b, fend, &q, &l))) break;
+      if (l > fend - q) { rc = KX_ERR_EOF; break; }
+      if (sp >= KXN_STACK) { rc = KX_ERR_DEPTH_LIMIT; break; }
+      S.seen[L] |= bit;
+      if (G.pbit >= 0) S.pres[L] |= 1ull << G.pbit;
+      const uint64_t e = cur[N.cur]++;
+      kxn_inst_start<W>(P, C, N.root, e, cur, S);
+      stk[sp++] = KxnPFrame{1, 0, G.node, N.root, 0, q + l, {0, 0}};
+      continue;
+    }
+    if (wt != kxn_pb_wt(N)) {                           // another wire type: unknown
+      if ((rc = kxn_pb_skip(b, fend, &q, wt))) break;
+      continue;
+    }
+    if (N.kind == KN_STRING && G.snap >= 0) {           // singular string: the last occurrence wins
+      if (S.seen[L] & bit) cur[N.cur] = snap[G.snap];
+      else snap[G.snap] = cur[N.cur];
+    }
+    S.seen[L] |= bit;
+    if (G.pbit >= 0) S.pres[L] |= 1ull << G.pbit;
+    if ((rc = kxn_pb_value<W>(P, C, b, fend, &q, G.node, cur, S, stk, &sp, -1))) break;   // a message merges
+  }
+  if (rc) return rc;
+  kxn_inst_end<W>(P, C, 0, cur, S);
+  *used = q;
+  return KX_OK;
+}
+
+// ---- proto.Marshal from the columns ----
+template <bool W>
+KXN_HD void kxn_pb_put_uv(uint8_t* out, uint64_t* pos, uint64_t v) {
+  while (v >= 0x80) {
+    if (W) out[*pos] = (uint8_t)(v | 0x80);
+    (*pos)++;
+    v >>= 7;
+  }
+  if (W) out[*pos] = (uint8_t)v;
+  (*pos)++;
+}
+
+// the scalar of node N at instance e: *wire = its varint value, or its fixed bytes (*fixed = 4 / 8)
+KXN_HD uint64_t kxn_pb_wire_scalar(const KxnProgram& P, const KxnCols& C, const KxnNode& N, uint64_t e, int* fixed,
+                                   bool* zero) {
+  (void)P;
+  const uint64_t v = kxn_get_val(C, N.col, N.width, e);
+  const uint32_t wt = kxn_pb_wt(N);
+  *zero = (N.ttype == KX_T_BOOL ? (v & 0xff) : v) == 0;
+  if (wt != 0) {
+    *fixed = wt == 1 ? 8 : 4;
+    return v;
+  }
+  *fixed = 0;
+  if (N.ttype == KX_T_BOOL) return (v & 0xff) ? 1 : 0;
+  if (N.ttype == KX_T_I32) {
+    const uint32_t x = (uint32_t)v;
+    if (N.pbk == KX_PB_SINT) return (uint64_t)((x << 1) ^ (uint32_t)((int32_t)x >> 31));
+    if (N.pbk == KX_PB_UINT) return (uint64_t)x;
+    return (uint64_t)(int64_t)(int32_t)x;   // int32 / enum: sign-extended
+  }
+  return N.pbk == KX_PB_SINT ? ((v << 1) ^ (uint64_t)((int64_t)v >> 63)) : v;
+}
+
+template <bool W>
+KXN_HD void kxn_pb_put_scalar(uint8_t* out, uint64_t* pos, uint64_t v, int fixed) {
+  if (fixed) {
+    if (W)
+      for (int k = 0; k < fixed; k++) out[*pos + k] = (uint8_t)(v >> (8 * k));
+    *pos += (uint64_t)fixed;
+  } else {
+    kxn_pb_put_uv<W>(out, pos, v);
+  }
+}
+
+struct KxnPEFrame {     // encode: a message's fields, a repeated message's elements, a map's entries (48 B)
+  uint8_t kind;         // 0 message, 1 repeated message elements, 2 map entries, 3 one map entry
+  uint8_t phase;        // map entry: 0 key + value, 1 (message value) done
+  int16_t id;           // message: struct; elements / entries / entry: the container node
+  int16_t f;            // message: next field (field-number order)
+  int16_t root;         // message: its instance root (presence word)
+  uint32_t tagsz;       // size mode: the tag bytes of this value in its parent (0: not length-delimited)
+  uint32_t fnum;        // elements / entries: the field number
+  uint64_t e;           // message / entry: its instance index; elements / entries: next index
+  uint64_t end;         // elements / entries: end index
+  uint64_t acc;         // size mode: bytes so far
+};
+
+// Size (W = false: returns the body size of the frame it starts with, post-order over nested messages)
+// or write (W = true: message bodies' sizes from the size walk) of a message / entry. start: the first frame.
+template <bool W>
+KXN_HD uint64_t kxn_pb_walk(const KxnProgram& P, const KxnCols& C, KxnPEFrame start, uint8_t* out, uint64_t pos0);
+
+template <bool W>
+KXN_HD uint64_t kxn_pb_walk(const KxnProgram& P, const KxnCols& C, KxnPEFrame start, uint8_t* out, uint64_t pos0) {
+  KxnPEFrame stk[KXN_STACK];
+  int sp = 0;
+  stk[sp++] = start;
+  uint64_t pos = pos0;      // W: where the next byte goes
+  uint64_t result = 0;
+  // a length-delimited child: size mode pushes it (its size returns through acc); write mode writes
+  // tag + length (from a size walk of the child) and pushes it
+  while (sp > 0) {
+    KxnPEFrame& F = stk[sp - 1];
+    uint64_t sz = 0;            // size mode: bytes this step adds to F.acc
+    if (F.kind == 0) {          // message fields, field-number order
+      if (F.f < 0) {            // done
+        const KxnPEFrame D = F;
+        sp--;
+        if (!W) {
+          if (sp == 0) result = D.acc;
+          else stk[sp - 1].acc += D.tagsz ? D.tagsz + kxn_uvlen(D.acc) + D.acc : D.acc;
+        }
+        continue;
+      }
+      const KxnField& G = P.f[F.f];
+      F.f = G.enc_next;
+      const KxnNode& N = P.node[G.node];
+      const uint64_t e = F.e;
+      uint64_t pres = 0;
+      bool isset = false;
+      if (G.pbit >= 0) {
+        pres = kxn_pres_word(P, C, F.root, e);
+        isset = (pres >> G.pbit) & 1;
+      }
+      const bool optional = G.req == KX_REQ_OPTIONAL;
+      if (N.kind == KN_SCALAR) {
+        int fixed;
+        bool zero;
+        const uint64_t v = kxn_pb_wire_scalar(P, C, N, e, &fixed, &zero);
+        if (optional ? !isset : zero) continue;       // proto3: zero omitted; `optional`: when present
+        const uint64_t tag = ((uint64_t)(uint16_t)G.id << 3) | kxn_pb_wt(N);
+        if (W) {
+          kxn_pb_put_uv<W>(out, &pos, tag);
+          kxn_pb_put_scalar<W>(out, &pos, v, fixed);
+        } else {
+          sz = kxn_uvlen(tag) + (fixed ? (uint64_t)fixed : kxn_uvlen(v));
+        }
+      } else if (N.kind == KN_STRING || N.kind == KN_RAW) {
+        const uint64_t a = kxn_get_arr(C, N.col, N.level, e), z = kxn_get_arr(C, N.col, N.level, e + 1);
+        const uint64_t l = z - a;
+        if (N.kind == KN_RAW ? !isset : (optional ? !isset : l == 0)) continue;
+        const uint64_t tag = ((uint64_t)(uint16_t)G.id << 3) | 2u;
+        if (W) {
+          kxn_pb_put_uv<W>(out, &pos, tag);
+          kxn_pb_put_uv<W>(out, &pos, l);
+          for (uint64_t j = 0; j < l; j++) out[pos + j] = ((const uint8_t*)C.data[N.col])[a + j];
+          pos += l;
+        } else {
+          sz = kxn_uvlen(tag) + kxn_uvlen(l) + l;
+        }
+      } else if (N.kind == KN_STRUCT) {
+        if (!isset) continue;                          // a nil message is not written
+        const uint64_t tag = ((uint64_t)(uint16_t)G.id << 3) | 2u;
+        if (sp >= KXN_STACK) break;
+        const KxnPEFrame Cf{0, 0, N.a, P.st[N.a].enc_first, F.root, (uint32_t)kxn_uvlen(tag), 0, e, 0, 0};
+        if (W) {
+          kxn_pb_put_uv<W>(out, &pos, tag);
+          kxn_pb_put_uv<W>(out, &pos, kxn_pb_walk<false>(P, C, KxnPEFrame{0, 0, N.a, P.st[N.a].enc_first, F.root,
+                                                                          0, 0, e, 0, 0}, nullptr, 0));
+        }
+        stk[sp++] = Cf;
+        continue;
+      } else {                                         // repeated / map
+        const uint64_t a = kxn_get_arr(C, N.rep_col, N.level, e), z = kxn_get_arr(C, N.rep_col, N.level, e + 1);
+        if (a == z) continue;
+        const KxnNode& E = P.node[N.a];
+        if (N.kind == KN_LIST && E.kind == KN_SCALAR) {  // packed
+          uint64_t body = 0;
+          for (uint64_t j = a; j < z; j++) {
+            int fixed;
+            bool zero;
+            const uint64_t v = kxn_pb_wire_scalar(P, C, E, j, &fixed, &zero);
+            body += fixed ? (uint64_t)fixed : kxn_uvlen(v);
+          }
+          const uint64_t tag = ((uint64_t)(uint16_t)G.id << 3) | 2u;
+          if (W) {
+            kxn_pb_put_uv<W>(out, &pos, tag);
+            kxn_pb_put_uv<W>(out, &pos, body);
+            for (uint64_t j = a; j < z; j++) {
+              int fixed;
+              bool zero;
+              const uint64_t v = kxn_pb_wire_scalar(P, C, E, j, &fixed, &zero);
+              kxn_pb_put_scalar<W>(out, &pos, v, fixed);
+            }
+          } else {
+            sz = kxn_uvlen(tag) + kxn_uvlen(body) + body;
+          }
+        } else if (N.kind == KN_LIST && (E.kind == KN_STRING || E.kind == KN_RAW)) {
+          const uint64_t tag = ((uint64_t)(uint16_t)G.id << 3) | 2u;
+          for (uint64_t j = a; j < z; j++) {
+            const uint64_t sa = kxn_get_arr(C, E.col, E.level, j), sb = kxn_get_arr(C, E.col, E.level, j + 1);
+            const uint64_t l = sb - sa;
+            if (W) {
+              kxn_pb_put_uv<W>(out, &pos, tag);
+              kxn_pb_put_uv<W>(out, &pos, l);
+              for (uint64_t k = 0; k < l; k++) out[pos + k] = ((const uint8_t*)C.data[E.col])[sa + k];
+              pos += l;
+            } else {
+              sz += kxn_uvlen(tag) + kxn_uvlen(l) + l;
+            }
+          }
+        } else {                                       // repeated messages / map entries: a frame
+          if (sp >= KXN_STACK) break;
+          const uint64_t tag = ((uint64_t)(uint16_t)G.id << 3) | 2u;
+          stk[sp++] = KxnPEFrame{(uint8_t)(N.kind == KN_LIST ? 1 : 2), 0, G.node, 0, 0, (uint32_t)kxn_uvlen(tag),
+                                 (uint32_t)G.id, a, z, 0};
+          continue;
+        }
+      }
+      if (!W) F.acc += sz;
+      continue;
+    }
+    if (F.kind == 1 || F.kind == 2) {   // the next element / entry
+      if (F.e >= F.end) {
+        const KxnPEFrame D = F;
+        sp--;
+        if (!W) {
+          if (sp == 0) result = D.acc;
+          else stk[sp - 1].acc += D.acc;   // each element / entry already carries its own tag + length
+        }
+        continue;
+      }
+      const uint64_t j = F.e++;
+      const KxnNode& N = P.node[F.id];
+      const uint64_t tag = ((uint64_t)F.fnum << 3) | 2u;
+      if (sp >= KXN_STACK) break;
+      KxnPEFrame Cf;
+      if (F.kind == 1) {
+        const KxnNode& E = P.node[N.a];
+        Cf = KxnPEFrame{0, 0, E.a, P.st[E.a].enc_first, N.root, F.tagsz, 0, j, 0, 0};
+      } else {
+        Cf = KxnPEFrame{3, 0, F.id, 0, N.root, F.tagsz, 0, j, 0, 0};
+      }
+      if (W) {
+        kxn_pb_put_uv<W>(out, &pos, tag);
+        KxnPEFrame Sf = Cf;
+        Sf.tagsz = 0;
+        kxn_pb_put_uv<W>(out, &pos, kxn_pb_walk<false>(P, C, Sf, nullptr, 0));
+      }
+      stk[sp++] = Cf;
+      continue;
+    }
+    // one map entry: key (field 1) and value (field 2), both always written
+    const KxnNode& M = P.node[F.id];
+    if (F.phase == 1) {
+      const KxnPEFrame D = F;
+      sp--;
+      if (!W) {
+        if (sp == 0) result = D.acc;
+        else stk[sp - 1].acc += D.tagsz ? D.tagsz + kxn_uvlen(D.acc) + D.acc : D.acc;
+      }
+      continue;
+    }
+    F.phase = 1;
+    for (int k = 0; k < 2; k++) {
+      const KxnNode& V = P.node[k == 0 ? M.a : M.b];
+      const uint64_t tag = ((uint64_t)(k + 1) << 3) | kxn_pb_wt(V);
+      if (V.kind == KN_SCALAR) {
+        int fixed;
+        bool zero;
+        const uint64_t v = kxn_pb_wire_scalar(P, C, V, F.e, &fixed, &zero);
+        if (W) {
+          kxn_pb_put_uv<W>(out, &pos, tag);
+          kxn_pb_put_scalar<W>(out, &pos, v, fixed);
+        } else {
+          F.acc += kxn_uvlen(tag) + (fixed ? (uint64_t)fixed : kxn_uvlen(v));
+        }
+      } else if (V.kind == KN_STRING || V.kind == KN_RAW) {
+        const uint64_t a = kxn_get_arr(C, V.col, V.level, F.e), z = kxn_get_arr(C, V.col, V.level, F.e + 1);
+        const uint64_t l = z - a;
+        if (W) {
+          kxn_pb_put_uv<W>(out, &pos, tag);
+          kxn_pb_put_uv<W>(out, &pos, l);
+          for (uint64_t j = 0; j < l; j++) out[pos + j] = ((const uint8_t*)C.data[V.col])[a + j];
+          pos += l;
+        } else {
+          F.acc += kxn_uvlen(tag) + kxn_uvlen(l) + l;
+        }
+      } else {                                          // a message value: a child frame (the entry's instance)
+        const KxnPEFrame Cf{0, 0, V.a, P.st[V.a].enc_first, M.root, (uint32_t)kxn_uvlen(tag), 0, F.e, 0, 0};
+        if (W) {
+          kxn_pb_put_uv<W>(out, &pos, tag);
+          KxnPEFrame Sf = Cf;
+          Sf.tagsz = 0;
+          kxn_pb_put_uv<W>(out, &pos, kxn_pb_walk<false>(P, C, Sf, nullptr, 0));
+        }
+        if (sp < KXN_STACK) stk[sp++] = Cf;
+      }
+    }
+  }
+  return W ? pos - pos0 : result;
+}
+
+// record r as a Batch frame: 0x0A, uvarint(body), body
+KXN_HD uint64_t kxn_pb_frame_size(const KxnProgram& P, const KxnCols& C, uint64_t r) {
+  const int si = P.node[P.rec_node].a;
+  const uint64_t body = kxn_pb_walk<false>(P, C, KxnPEFrame{0, 0, (int16_t)si, P.st[si].enc_first, 0, 0, 0, r, 0, 0},
+                                           nullptr, 0);
+  return 1 + kxn_uvlen(body) + body;
+}
+
+KXN_HD void kxn_pb_write_frame(const KxnProgram& P, const KxnCols& C, uint64_t r, uint8_t* out, uint64_t pos,
+                               uint64_t frame_size) {
+  const int si = P.node[P.rec_node].a;
+  // body = frame_size - 1 - uvlen(body): the uvarint length that fits
+  uint64_t body = 0;
+  for (uint32_t u = 1; u <= 10; u++) {
+    if (frame_size < 1 + (uint64_t)u) break;
+    body = frame_size - 1 - u;
+    if (kxn_uvlen(body) == u) break;
+  }
+  out[pos] = 0x0A;
+  uint64_t p = pos + 1;
+  kxn_pb_put_uv<true>(out, &p, body);
+  (void)kxn_pb_walk<true>(P, C, KxnPEFrame{0, 0, (int16_t)si, P.st[si].enc_first, 0, 0, 0, r, 0, 0}, out, p);
 }

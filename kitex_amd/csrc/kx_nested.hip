@@ -34,6 +34,8 @@ struct NParams {
   uint64_t n;
   bool concat;
   const kx_status* skip_st;   // concat: the skip pass's status (records delimited)
+  const uint64_t* bstart;     // concat, Kitex-PB: the Batch frames' body extents (the frame pass)
+  const uint64_t* bend;
   uint32_t* counts;           // [ncur][n]
   uint64_t* bsum;             // [ncur][nblk]
   uint64_t* totals;           // [ncur]
@@ -52,6 +54,11 @@ __device__ __forceinline__ int extent(const NParams& p, uint64_t r, uint64_t* a,
   if (p.concat) {
     const uint64_t ok = p.skip_st->code ? p.skip_st->n_records : p.n;
     if (r > ok || (r == ok && !p.skip_st->code)) return -1;
+    if (p.bstart) {   // Kitex-PB: the body of frame r; a frame that could not be delimited reads as empty
+      *a = r < ok ? p.bstart[r] : 0;
+      *b = r < ok ? p.bend[r] : 0;
+      return 0;
+    }
     *a = p.offsets[r];
     *b = r < ok ? p.offsets[r + 1] : p.in_len;   // the failing record: FastRead finds its error
     return 0;
@@ -73,7 +80,8 @@ __global__ void __launch_bounds__(NT) measure_kernel(NParams p) {
     rc = 0;  // not decoded: empty
     p.rcode[r] = 0xff;
   } else {
-    if (!rc) rc = kxn_read_record<false>(P, *p.C, p.in + a, b - a, r, cur, snap, &used);
+    if (!rc) rc = P.pb ? kxn_pb_read_record<false>(P, *p.C, p.in + a, b - a, r, cur, snap, &used)
+                       : kxn_read_record<false>(P, *p.C, p.in + a, b - a, r, cur, snap, &used);
     if (!rc && p.concat && r < p.n && p.skip_st->code && r == p.skip_st->n_records) rc = p.skip_st->code;
     p.rcode[r] = (uint8_t)rc;
     if (rc) atomicMin(p.errkey, (unsigned long long)((r << 8) | (uint64_t)(rc & 0xff)));
@@ -182,7 +190,8 @@ __global__ void __launch_bounds__(NT) write_kernel(NParams p) {
     const uint8_t rc = p.rcode[r];
     uint64_t a = 0, e = 0, used = 0;
     if (rc == 0 && extent(p, r, &a, &e) == 0) {
-      (void)kxn_read_record<true>(P, *p.C, p.in + a, e - a, r, cur, snap, &used, lim);
+      if (P.pb) (void)kxn_pb_read_record<true>(P, *p.C, p.in + a, e - a, r, cur, snap, &used, lim);
+      else (void)kxn_read_record<true>(P, *p.C, p.in + a, e - a, r, cur, snap, &used, lim);
     } else {
       kxn_failed_record(P, *p.C, r, cur);
     }
@@ -243,8 +252,8 @@ __global__ void __launch_bounds__(NT) esize_kernel(EParams p) {
   uint64_t acc = 0;
   for (int j = 0; j < RB / NT; j++) {
     const uint64_t r = b * RB + (uint64_t)j * NT + threadIdx.x;
-    if (r < p.n) {
-      const uint64_t sz = kxn_write_record<false>(*p.P, *p.C, r, nullptr, 0);
+    if (r < p.n) {   // Kitex-PB: the record's Batch frame (0x0A, uvarint body length, body)
+      const uint64_t sz = p.P->pb ? kxn_pb_frame_size(*p.P, *p.C, r) : kxn_write_record<false>(*p.P, *p.C, r, nullptr, 0);
       p.sizes[r] = sz;
       acc += sz;
     }
@@ -288,7 +297,8 @@ __global__ void __launch_bounds__(NT) ewrite_kernel(EParams p) {
     uint64_t tot;
     const uint64_t pre = wg_excl(sz, &tot, sh);
     if (r < p.n) {
-      (void)kxn_write_record<true>(*p.P, *p.C, r, p.out, base + pre);
+      if (p.P->pb) kxn_pb_write_frame(*p.P, *p.C, r, p.out, base + pre, sz);
+      else (void)kxn_write_record<true>(*p.P, *p.C, r, p.out, base + pre);
       if (p.offsets_out) p.offsets_out[r] = base + pre;
     }
     base += tot;
@@ -303,6 +313,7 @@ size_t kx_nested_ws_bytes(const KxnProgram& P, uint64_t n, bool concat) {
   const uint64_t nblk = (n + RB - 1) / RB;
   size_t s = 64 + ((n + 63) & ~63ull) + (size_t)P.ncur * n * 4 + 64 + (size_t)P.ncur * nblk * 8 + P.ncur * 8 + 64;
   if (concat) s += (n + 1) * 8 + 64 + sizeof(kx_status) + 64;
+  if (concat && P.pb) s += 2 * ((n * 8 + 63) & ~63ull);   // Batch frame body extents
   return s + 4096;
 }
 
@@ -316,6 +327,8 @@ struct NwsLayout {
   uint64_t* totals;
   uint64_t* starts;
   kx_status* skip_st;
+  uint64_t* bstart;
+  uint64_t* bend;
 };
 NwsLayout layout(void* ws, const KxnProgram& P, uint64_t n) {
   NwsLayout L;
@@ -335,6 +348,10 @@ NwsLayout layout(void* ws, const KxnProgram& P, uint64_t n) {
   L.starts = (uint64_t*)p;
   p += ((n + 1) * 8 + 63) & ~63ull;
   L.skip_st = (kx_status*)p;
+  p += (sizeof(kx_status) + 63) & ~(size_t)63;
+  L.bstart = (uint64_t*)p;
+  p += (n * 8 + 63) & ~63ull;
+  L.bend = (uint64_t*)p;
   return L;
 }
 }  // namespace
@@ -372,7 +389,16 @@ int kx_launch_nested_decode(const KxnProgram* dprog, const KxnProgram& hprog, co
   KX_HIP_CHECK(hipMemsetAsync(status, 0, sizeof(kx_status), stream));
   KX_HIP_CHECK(hipMemsetAsync(L.errkey, 0xff, 8, stream));
   KX_HIP_CHECK(hipMemsetAsync(L.flag, 0, 4, stream));
-  if (concat) {
+  if (concat && hprog.pb) {
+    // Kitex-PB Batch body: the frames (0x0A, uvarint length) on the frame pipeline of kx_decode.hip
+    int rc = kx_launch_pb_frames(in, in_len, n, L.starts, L.bstart, L.bend, L.skip_st, skip_ws, skip_ws_size,
+                                 skip_epoch, stream);
+    if (rc) return rc;
+    p.offsets = L.starts;
+    p.skip_st = L.skip_st;
+    p.bstart = L.bstart;
+    p.bend = L.bend;
+  } else if (concat) {
     // record boundaries: the skip decoder (codec_apache.go:166-172) on the pipeline of kx_decode.hip
     int rc = kx_launch_skip(in, in_len, n, L.starts, L.skip_st, skip_ws, skip_ws_size, skip_epoch, stream);
     if (rc) return rc;

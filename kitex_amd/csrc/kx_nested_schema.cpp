@@ -38,6 +38,7 @@ struct TypeRef {  // a value type: wire type + the descriptor parts that refine 
   uint8_t ttype;
   uint8_t elem;   // LIST/SET: element type; MAP: key | value << 4
   int16_t child;  // struct index (STRUCT, list<STRUCT>, map<K, STRUCT>) or element-type struct
+  uint16_t pbk;   // Kitex-Protobuf: proto kind of the value (elements / key) | map value kind << 8
 };
 
 struct RootB {    // an instance root under construction
@@ -60,6 +61,7 @@ struct NB {
   int16_t path[8] = {0};
   int depth = 0;                     // path length - 1
   int16_t top_field_ttype = 0;       // the record field on the current path
+  bool pb = false;                   // Kitex-Protobuf: proto3 messages (kinds in default_bits, no defaults)
   int rc = KX_OK;
 
   int fail(int code) {
@@ -124,6 +126,7 @@ struct NB {
       return true;
     }
     if (is_container(t)) {  // described by field 0 of the one-field struct `child`
+      if (pb) return false;   // proto3 has no containers of containers
       if (child < 0 || (uint32_t)child >= nstructs) return false;
       const kx_struct_desc& d = structs[child];
       if (d.nfields != 1 || !d.fields || d.fields[0].ttype != t) return false;
@@ -147,19 +150,22 @@ struct NB {
       N.cur_lo = (uint16_t)P.ncur;
     }
     if (tsize(T.ttype) > 0) {
+      if (pb && (T.ttype == KX_T_BYTE || T.ttype == KX_T_I16)) return fail(KX_ERR_NOT_IMPLEMENTED);  // no proto type
+      if (pb && (T.pbk & 0xff) > KX_PB_UINT) return fail(KX_ERR_INVALID_ARG);
       const int c = new_col(level, false, -1, T.ttype, elem_flags, fid, pbit);
       if (c < 0) return -1;
       KxnNode& N = P.node[X];
       N.kind = KN_SCALAR;
       N.width = (uint8_t)tsize(T.ttype);
       N.col = (int16_t)c;
-      if (fd) {  // a field: its default
+      N.pbk = (uint8_t)(T.pbk & 0xff);
+      if (fd || (pb && pb_entry)) {  // a field: its default (proto3: zero; a map entry's key / value too)
         RootB& RB = roots[R];
         KxnDflt d;
         memset(&d, 0, sizeof d);
         d.col = (int16_t)c;
         d.width = (uint8_t)tsize(T.ttype);
-        d.v = fd->default_bits;
+        d.v = pb ? 0 : fd->default_bits;
         RB.dfl.push_back(d);
       }
     } else if (T.ttype == KX_T_STRING || (T.ttype == KX_T_STRUCT && recursive(T.child))) {
@@ -172,7 +178,9 @@ struct NB {
       N.kind = raw ? KN_RAW : KN_STRING;
       N.col = (int16_t)c;
       N.cur = (int16_t)bc;
-      if (fd && !raw && (fd->reserved0 & KX_FIELD_STRING_DEFAULT) && fd->default_bits) {
+      N.pbk = (uint8_t)(T.pbk & 0xff);
+      if (pb && fd && (fd->reserved0 & KX_FIELD_BINARY)) N.pbk = KX_PB_BYTES;
+      if (!pb && fd && !raw && (fd->reserved0 & KX_FIELD_STRING_DEFAULT) && fd->default_bits) {
         const char* dv = (const char*)(intptr_t)fd->default_bits;
         const size_t len = strlen(dv);
         if (len) {
@@ -214,13 +222,19 @@ struct NB {
       if (map) {
         const uint8_t kt = T.elem & 15, vt = (uint8_t)(T.elem >> 4);
         if (tsize(kt) == 0 && kt != KX_T_STRING) return fail(KX_ERR_NOT_IMPLEMENTED);  // struct / container keys
-        K = TypeRef{kt, 0, -1};
+        K = TypeRef{kt, 0, -1, (uint16_t)(T.pbk & 0xff)};
         if (!elem_type(vt, T.child, &V)) return fail(KX_ERR_NOT_IMPLEMENTED);
+        V.pbk = (uint16_t)(T.pbk >> 8);
+        if (pb && (kt == KX_T_DOUBLE || (kt == KX_T_STRING && (K.pbk & 0xff) == KX_PB_BYTES)))
+          return fail(KX_ERR_INVALID_ARG);   // proto map keys: integral, bool or string
         elem_flags = 0;
+        const bool saved_entry = pb_entry;
+        pb_entry = true;
         const int kn = value(K, level + 1, ER, fid, pbit, nullptr);
         if (kn < 0) return -1;
         elem_flags = KX_ELEM_MAP_VALUE;
         const int vn = value(V, level + 1, ER, fid, pbit, nullptr);
+        pb_entry = saved_entry;
         if (vn < 0) return -1;
         P.node[X].a = (int16_t)kn;
         P.node[X].b = (int16_t)vn;
@@ -228,8 +242,12 @@ struct NB {
         P.node[X].vtype = vt;
       } else {
         if (!elem_type(T.elem, T.child, &V)) return fail(KX_ERR_NOT_IMPLEMENTED);
+        V.pbk = (uint16_t)(T.pbk & 0xff);
         elem_flags = 0;
+        const bool saved_entry = pb_entry;
+        pb_entry = false;
         const int en = value(V, level + 1, ER, fid, pbit, nullptr);
+        pb_entry = saved_entry;
         if (en < 0) return -1;
         P.node[X].a = (int16_t)en;
         P.node[X].etype = T.elem;
@@ -254,6 +272,7 @@ struct NB {
   }
 
   uint8_t elem_flags = 0;    // flags of the element columns being built (KX_ELEM_MAP_VALUE / STRUCT_FIELD)
+  bool pb_entry = false;     // building a map entry's key / value (proto3: zero defaults when absent)
   int pending_sdef = -1;     // a string default just added (its seen bit is set by the field)
 
   bool recursive(int16_t child) {
@@ -347,7 +366,8 @@ struct NB {
       if (depth == 0) top_field_ttype = fd.ttype;
       const uint8_t saved_flags = elem_flags;
       if (level > 0) elem_flags = (uint8_t)(elem_flags | KX_ELEM_STRUCT_FIELD);
-      TypeRef T{fd.ttype, fd.elem_ttype, fd.child};
+      TypeRef T{fd.ttype, fd.elem_ttype, fd.child, (uint16_t)(pb ? (fd.default_bits & 0xffff) : 0)};
+      if (pb && fd.req == KX_REQ_REQUIRED) return fail(KX_ERR_INVALID_ARG);   // proto3 has no required fields
       if (fd.ttype == KX_T_STRUCT && (fd.child < 0 || (uint32_t)fd.child >= nstructs)) return fail(KX_ERR_INVALID_ARG);
       if ((fd.ttype == KX_T_LIST || fd.ttype == KX_T_SET) && (fd.elem_ttype == KX_T_STRUCT || is_container(fd.elem_ttype)) &&
           (fd.child < 0 || (uint32_t)fd.child >= nstructs))
@@ -375,9 +395,26 @@ struct NB {
     }
     stack.pop_back();
     P.st[si].dfl_hi = (uint16_t)roots[R].dfl.size();
-    // encoder order: fixed-length fields first (patcher.go:503-522), IDL order inside each group
+    // encoder order: fixed-length fields first (patcher.go:503-522), IDL order inside each group;
+    // Kitex-Protobuf: field-number order (proto.Marshal)
     int prev = -1;
     P.st[si].enc_first = -1;
+    if (pb) {
+      int last = -1 << 20;
+      for (int k = 0; k < P.st[si].nfields; k++) {
+        int best = -1;
+        for (int j = 0; j < P.st[si].nfields; j++) {
+          const int fj = P.st[si].first + j;
+          if (P.f[fj].id > last && (best < 0 || P.f[fj].id < P.f[best].id)) best = fj;
+        }
+        if (best < 0) break;
+        last = P.f[best].id;
+        if (prev < 0) P.st[si].enc_first = (int16_t)best;
+        else P.f[prev].enc_next = (int16_t)best;
+        prev = best;
+      }
+      return si;
+    }
     for (int pass = 0; pass < 2; pass++)
       for (int k = 0; k < P.st[si].nfields; k++) {
         const int fi = P.st[si].first + k;
@@ -420,6 +457,8 @@ int kx_build_nested(const kx_struct_desc* structs, uint32_t nstructs, kx_schema*
   s->ncols = 0;
   s->npres = 0;
   NB b{structs, nstructs, s, *P, {}, {}};
+  b.pb = (structs[0].reserved0 & KX_STRUCT_PROTOBUF) != 0;
+  P->pb = b.pb ? 1 : 0;
   const int R0 = b.new_root(0);
   b.roots[R0].c_lo = 0;
   b.depth = -1;  // the record's fields are at depth 0

@@ -30,6 +30,9 @@ class Field:
     child: Optional["Struct"] = None    # STRUCT fields; the struct of list<S> / set<S> / map<K, S>
     default: object = 0                 # scalar default (two's complement / IEEE bits) or a string default
     binary: bool = False                # protobuf `bytes` (no UTF-8 check); thrift: same wire as string
+    pb: int = 0                         # Kitex-Protobuf schemas: proto kind (A.PB_*) of the field / its
+                                        # elements / a map's key
+    pbv: int = 0                        # ... of a map's value
 
 
 @dataclass
@@ -41,8 +44,9 @@ class Struct:
 class Schema:
     """A root struct and every struct reachable from it, lowered to kx_struct_desc[]."""
 
-    def __init__(self, root: Struct):
+    def __init__(self, root: Struct, protobuf: bool = False):
         self.root = root
+        self.protobuf = protobuf   # KX_STRUCT_PROTOBUF: proto3 messages, kinds in default_bits
         self.structs: List[Struct] = []
         self._index = {}
         self._elem_struct = {}     # id(field) -> the one-field struct describing its container element
@@ -70,11 +74,14 @@ class Schema:
                     self._strings.append(buf)
                     arr[j].default_bits = C.addressof(buf) if b else 0
                     arr[j].reserved0 |= A.FIELD_STRING_DEFAULT if b else 0
+                elif protobuf:   # proto3: no defaults; the proto scalar kinds instead
+                    arr[j].default_bits = (f.pb & 0xff) | ((f.pbv & 0xff) << 8)
                 else:
                     arr[j].default_bits = _signed64(f.default)
             self._field_arrays.append(arr)
             self._table[i].fields = C.cast(arr, C.POINTER(A.FieldDesc))
             self._table[i].nfields = len(s.fields)
+            self._table[i].reserved0 = A.STRUCT_PROTOBUF if protobuf and i == 0 else 0
 
     def _collect(self, s: Struct):
         if id(s) in self._index:

@@ -762,7 +762,22 @@ static int plan_build(plan_t* p, const kx_struct_desc* structs, uint32_t nstruct
   return KX_OK;
 }
 
+/* a Kitex-Protobuf schema the flat proto path does not read (the layout rule of include/kxcodec.h,
+ * KX_STRUCT_PROTOBUF): anything but one flat message of natural-kind scalars and strings */
+static int pb_nested(const kx_struct_desc* structs, uint32_t nstructs) {
+  if (!structs || nstructs == 0 || !(structs[0].reserved0 & KX_STRUCT_PROTOBUF)) return 0;
+  if (nstructs != 1) return 1;
+  for (uint32_t i = 0; i < structs[0].nfields; i++) {
+    const kx_field_desc* f = &structs[0].fields[i];
+    const int t = f->ttype;
+    if (!(t == KX_T_BOOL || t == KX_T_I32 || t == KX_T_I64 || t == KX_T_DOUBLE || t == KX_T_STRING)) return 1;
+    if ((f->default_bits & 0xffff) != 0 || f->req == KX_REQ_REQUIRED) return 1;
+  }
+  return 0;
+}
+
 int kxo_is_nested(const kx_struct_desc* structs, uint32_t nstructs) {
+  if (pb_nested(structs, nstructs)) return 1;
   plan_t* p = (plan_t*)malloc(sizeof(plan_t));
   const int rc = plan_build(p, structs, nstructs);
   free(p);
@@ -771,6 +786,7 @@ int kxo_is_nested(const kx_struct_desc* structs, uint32_t nstructs) {
 
 int kxo_flatten(const kx_struct_desc* structs, uint32_t nstructs, kx_column_info* cols,
                 uint32_t* ncols, uint32_t* npresence) {
+  if (pb_nested(structs, nstructs)) return kxo_nflatten(structs, nstructs, cols, ncols, npresence);
   plan_t* p = (plan_t*)malloc(sizeof(plan_t));
   int rc = plan_build(p, structs, nstructs);
   if (!rc) {
@@ -1711,6 +1727,8 @@ static int pb_batch_offsets(const uint8_t* in, uint64_t in_len, uint64_t n, uint
 int kxo_pb_decode(const kx_struct_desc* structs, uint32_t nstructs, const uint8_t* in,
                   uint64_t in_len, const uint64_t* offsets, uint64_t n, const kx_columns* out,
                   uint8_t* record_status, kx_status* st) {
+  if (pb_nested(structs, nstructs))
+    return kxo_npb_decode(structs, nstructs, in, in_len, offsets, n, out, record_status, st);
   int rc = pb_check_schema(structs, nstructs);
   if (rc) return rc;
   if (offsets) return decode_common(structs, nstructs, pb_reader, 1, in, in_len, offsets, n, out, record_status, st);
@@ -1756,6 +1774,8 @@ int kxo_pb_decode(const kx_struct_desc* structs, uint32_t nstructs, const uint8_
 int kxo_pb_decode_mt(const kx_struct_desc* structs, uint32_t nstructs, const uint8_t* in,
                      uint64_t in_len, const uint64_t* offsets, uint64_t n, const kx_columns* out,
                      kx_status* st, int threads) {
+  if (pb_nested(structs, nstructs))
+    return kxo_npb_decode(structs, nstructs, in, in_len, offsets, n, out, NULL, st);
   int rc = pb_check_schema(structs, nstructs);
   if (rc) return rc;
   return decode_mt(structs, nstructs, pb_reader, 1, in, in_len, offsets, n, out, st, threads);
@@ -1813,6 +1833,7 @@ static uint64_t pb_write_record(const plan_t* p, const kx_columns* in, uint64_t 
 
 int kxo_pb_encode(const kx_struct_desc* structs, uint32_t nstructs, const kx_columns* in,
                   uint64_t n, uint8_t* out, uint64_t cap, uint64_t* offsets_out, uint64_t* total) {
+  if (pb_nested(structs, nstructs)) return kxo_npb_encode(structs, nstructs, in, n, out, cap, offsets_out, total);
   int rc = pb_check_schema(structs, nstructs);
   if (rc) return rc;
   plan_t* p = (plan_t*)malloc(sizeof(plan_t));

@@ -121,6 +121,12 @@ int kxo_nthrift_decode(const kx_struct_desc* structs, uint32_t nstructs, const u
 int kxo_nthrift_encode(const kx_struct_desc* structs, uint32_t nstructs, const kx_columns* in, uint64_t n,
                        uint8_t* out, uint64_t cap, uint64_t* sizes, uint64_t* offsets_out, uint64_t* total);
 int kxo_is_nested(const kx_struct_desc* structs, uint32_t nstructs);
+/* Kitex-Protobuf nested messages (KX_STRUCT_PROTOBUF; kx_oracle_nested.c): proto.Unmarshal / proto.Marshal */
+int kxo_npb_decode(const kx_struct_desc* structs, uint32_t nstructs, const uint8_t* in, uint64_t in_len,
+                   const uint64_t* offsets, uint64_t n, const kx_columns* out, uint8_t* record_status,
+                   kx_status* st);
+int kxo_npb_encode(const kx_struct_desc* structs, uint32_t nstructs, const kx_columns* in, uint64_t n,
+                   uint8_t* out, uint64_t cap, uint64_t* offsets_out, uint64_t* total);
 
 #ifdef __cplusplus
 }

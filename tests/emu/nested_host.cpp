@@ -11,6 +11,7 @@
 #include "kx_nested.h"
 
 static int build(const kx_struct_desc* structs, uint32_t ns, kx_schema* s) {
+  if (ns && (structs[0].reserved0 & KX_STRUCT_PROTOBUF)) return kx_build_nested(structs, ns, s);  // proto mode
   int rc = kx_build_program(structs, ns, s);
   if (rc == KX_OK) return KX_ERR_INVALID_ARG;  // a flat schema: not this path
   if (rc != KX_ERR_NOT_IMPLEMENTED) return rc;
@@ -47,8 +48,22 @@ extern "C" int emu_nested_decode(const kx_struct_desc* structs, uint32_t ns, con
   std::vector<uint64_t> a(n), b(n);
   uint64_t nok = n;
   int skip_rc = 0;
+  std::vector<uint64_t> fstart(n + 1, 0);   // proto: Batch frame starts (status offsets)
   if (offsets) {
     for (uint64_t r = 0; r < n; r++) { a[r] = offsets[r]; b[r] = offsets[r + 1]; }
+  } else if (P.pb) {   // Kitex-PB Batch frames: 0x0A, uvarint length, body
+    uint64_t pos = 0;
+    for (uint64_t r = 0; r < n; r++) {
+      fstart[r] = pos;
+      uint64_t q = pos + 1, l = 0;
+      skip_rc = pos >= in_len ? KX_ERR_EOF : in[pos] != 0x0A ? KX_ERR_INVALID_DATA : kxn_uvarint(in, in_len, &q, &l);
+      if (!skip_rc && l > in_len - q) skip_rc = KX_ERR_EOF;
+      if (skip_rc) { nok = r; a[r] = b[r] = 0; break; }
+      a[r] = q;
+      b[r] = q + l;
+      pos = q + l;
+    }
+    fstart[nok < n ? nok : n] = pos;
   } else {
     uint64_t pos = 0;
     for (uint64_t r = 0; r < n; r++) {
@@ -70,8 +85,8 @@ extern "C" int emu_nested_decode(const kx_struct_desc* structs, uint32_t ns, con
     for (uint32_t k = 0; k < P.ncur; k++) cur[k] = 0;
     uint64_t used = 0;
     int e = (a[r] > b[r] || b[r] > in_len) ? KX_ERR_INVALID_ARG
-                                           : kxn_read_record<false>(P, C, in + a[r], b[r] - a[r], r, cur.data(),
-                                                                     snap.data(), &used);
+            : P.pb ? kxn_pb_read_record<false>(P, C, in + a[r], b[r] - a[r], r, cur.data(), snap.data(), &used)
+                   : kxn_read_record<false>(P, C, in + a[r], b[r] - a[r], r, cur.data(), snap.data(), &used);
     if (!e && !offsets && skip_rc && r == nok) e = skip_rc;
     code[r] = (uint8_t)e;
     if (e) { if (r < first) first = r; continue; }
@@ -97,7 +112,9 @@ extern "C" int emu_nested_decode(const kx_struct_desc* structs, uint32_t ns, con
       lim[k] = cur[k] + cnt[(size_t)k * n + r];
     }
     uint64_t used = 0;
-    if (code[r] == 0)
+    if (code[r] == 0 && P.pb)
+      (void)kxn_pb_read_record<true>(P, C, in + a[r], b[r] - a[r], r, cur.data(), snap.data(), &used, lim.data());
+    else if (code[r] == 0)
       (void)kxn_read_record<true>(P, C, in + a[r], b[r] - a[r], r, cur.data(), snap.data(), &used, lim.data());
     else kxn_failed_record(P, C, r, cur.data());
     if (rstat && offsets) rstat[r] = code[r] == 0xff ? 0 : code[r];
@@ -108,11 +125,12 @@ extern "C" int emu_nested_decode(const kx_struct_desc* structs, uint32_t ns, con
   }
   st->n_records = n;
   st->consumed = n ? b[n - 1] : 0;
+  if (!offsets && P.pb) st->consumed = n ? b[n - 1] : 0;
   if (first < n) {
     st->code = code[first];
     st->record = first;
-    st->offset = a[first];
-    if (!offsets) { st->n_records = first; st->consumed = a[first]; }
+    st->offset = !offsets && P.pb ? fstart[first] : a[first];
+    if (!offsets) { st->n_records = first; st->consumed = st->offset; }
   }
   return st->code;
 }
@@ -125,13 +143,20 @@ extern "C" int emu_nested_encode(const kx_struct_desc* structs, uint32_t ns, con
   KxnCols C;
   cols_of(s, in, &C);
   uint64_t pos = 0;
-  for (uint64_t r = 0; r < n; r++) pos += kxn_write_record<false>(*s.nprog, C, r, nullptr, 0);
+  const KxnProgram& P = *s.nprog;
+  for (uint64_t r = 0; r < n; r++) pos += P.pb ? kxn_pb_frame_size(P, C, r) : kxn_write_record<false>(P, C, r, nullptr, 0);
   *total = pos;
   if (pos > cap) return KX_ERR_SIZE_LIMIT;
   pos = 0;
   for (uint64_t r = 0; r < n; r++) {
     if (offsets_out) offsets_out[r] = pos;
-    pos += kxn_write_record<true>(*s.nprog, C, r, out, pos);
+    if (P.pb) {
+      const uint64_t fs = kxn_pb_frame_size(P, C, r);
+      kxn_pb_write_frame(P, C, r, out, pos, fs);
+      pos += fs;
+    } else {
+      pos += kxn_write_record<true>(P, C, r, out, pos);
+    }
   }
   if (offsets_out) offsets_out[n] = pos;
   return KX_OK;
