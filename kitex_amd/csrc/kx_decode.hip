@@ -38,7 +38,10 @@ namespace {
 
 constexpr int NT = 256;                  // threads per workgroup (4 independent waves)
 constexpr int WAVES = NT / 64;
-constexpr int SEG = 128;                 // bytes per lane segment
+#ifndef KX_SEG
+#define KX_SEG 128
+#endif
+constexpr int SEG = KX_SEG;              // bytes per lane segment
 constexpr int TILE = 64 * SEG;           // 8 KiB of input per wave
 constexpr int HALO = 512;                // default halo: the record straddling the tile end is read from LDS
 constexpr int HALO_MAX = 1536;           // up to here (the halo grows with the batch's mean record size)
@@ -73,8 +76,9 @@ enum { G_ENT = 0, G_EXIT, G_CNT, G_ERRC, G_ERRP, G_VAR, G_BCNT = G_VAR + KXP_NV_
 enum Mode { M_THRIFT = 0, M_SKIP = 1, M_PB = 2, M_FRAME = 3, M_THRIFT_LS = 4 };
 __host__ __device__ constexpr bool is_thrift(int m) { return m == M_THRIFT || m == M_THRIFT_LS; }
 
-// diagnostics (KX_DIAG & 64): shader-clock cycles per index-pass phase, summed over tiles (lane 0)
-__device__ unsigned long long g_phase[8];
+// diagnostics (KX_DIAG & 64): shader-clock cycles per index-pass phase, summed over tiles (lane 0), in a
+// device buffer every decode part shares (DecParams::phase; a __device__ array would be one per part)
+
 
 struct DecParams {
   const uint8_t* in;
@@ -106,7 +110,11 @@ struct DecParams {
   unsigned long long* errkey;  // offsets mode: min((record << 8) | code)
   uint32_t* overflow;        // an arena capacity was exceeded
   uint64_t* nstop;           // records to emit (chain pass)
+  uint64_t* nstop_ring;      // chunked pipeline: nstop of chunk k at [k % KX_PIPE_EV] (chain runs ahead of emit)
+  uint32_t* redo_n;          // fast index kernel: tiles it could not index (count, then their ids)
+  uint32_t* redo;
   uint64_t var_base[KXP_NV_MAX];  // arena positions start here (a chunk of a larger batch)
+  KxpFast fp;                // the canonical plan in segment form (fast_record_fp), fp.ok = 0: none
   uint64_t ntiles, ngroups, slotcap;
   // chunked pipeline (launch_t): this launch covers tiles [t_lo, t_hi) and groups [g_lo, g_hi); the
   // chain pass carries its state between chunks in `carry`
@@ -121,6 +129,7 @@ struct DecParams {
   int fast;                  // concatenated Thrift with a canonical plan: fast_tile before walk_tile
   int all_view;              // every var column is a zero-copy view (no arena to lay out)
   int nolds;                 // diagnostics (KX_NOLDS=1): read every byte from global memory
+  unsigned long long* phase; // diagnostics (KX_DIAG & 64): the phase-cycle accumulators
   int diag;                  // diagnostics (KX_DIAG bits, timing experiments only; output is wrong):
                              // 1 no walk, 2 no group arrival, 4 no tile words, 256 index pass only
 };
@@ -159,14 +168,22 @@ __device__ __forceinline__ int32_t wofs(const Src& w, uint64_t p, uint32_t need)
   return (q >= 0 && q + (int64_t)need <= (int64_t)w.wlen) ? (int32_t)q : -1;
 }
 
+// the aligned input dword at A, which holds an input byte below `end`: an aligned dword never crosses a
+// page, so its bytes past the input are readable (and ignored by every caller). The CPU emulation
+// (tests/emu/build_emu.sh) replaces the read with one of the input bytes alone, the rest poisoned.
+__device__ __forceinline__ uint32_t gdword(uint64_t A, uint64_t end) {
+  (void)end;
+  return *(const GLB uint32_t*)A;  // input tail dword
+}
+
 // 4 bytes at p from global memory; never reads past the dword holding the last input byte
 __device__ __forceinline__ uint32_t gld4(const Src& w, uint64_t p) {
   uint64_t a = (uint64_t)w.in + p;
   uint64_t A = a & ~3ull;
   uint32_t sh = (uint32_t)(a & 3);
   uint64_t end = (uint64_t)w.in + w.len;
-  uint32_t x0 = A < end ? *(const GLB uint32_t*)A : 0u;
-  uint32_t x1 = A + 4 < end ? *(const GLB uint32_t*)(A + 4) : 0u;
+  uint32_t x0 = A < end ? gdword(A, end) : 0u;
+  uint32_t x1 = A + 4 < end ? gdword(A + 4, end) : 0u;
   return __builtin_amdgcn_alignbyte(x1, x0, sh);
 }
 
@@ -1725,6 +1742,12 @@ __device__ __forceinline__ uint32_t data_sig(KParams& dp) {
   return __builtin_amdgcn_readfirstlane((uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16));
 }
 
+// data_sig by one scalar load (uniform; inputs of 4 bytes and more, whose buffer holds the dword)
+__device__ __forceinline__ uint32_t data_sig_s(KParams& dp) {
+  if (dp.in_len < 4 || dp.offsets) return data_sig(dp);
+  return *(const KAS uint32_t*)dp.in & 0xffffffu;
+}
+
 // The lane's speculation: its segment's boundary signature, and the first signature hit. A hit is
 // a guess; a guess whose own walk fails is replaced by the next hit (walk_tile), so payload bytes
 // that contain the signature (binary strings saturated with it, strings holding serialized records)
@@ -1885,7 +1908,7 @@ __device__ Agg walk_tile(KParams& dp, const Src& w, uint64_t tlo, uint64_t thi, 
   auto phase = [&](int k) {
     if (dp.diag & 64) {
       const uint64_t now = __builtin_amdgcn_s_memtime();
-      if (lane == 0) atomicAdd(&g_phase[k], (unsigned long long)(now - tp));
+      if (lane == 0) atomicAdd(&dp.phase[k], (unsigned long long)(now - tp));
       tp = now;
     }
   };
@@ -2042,23 +2065,89 @@ __device__ __forceinline__ uint32_t win_ld(const Src& w, uint32_t q) {  // 4 byt
   return __builtin_amdgcn_alignbyte(w.win[(q >> 2) + 1], w.win[q >> 2], q & 3);
 }
 
+// one canonical record at window offset q from the segment plan: the header checks of a segment are
+// independent LDS reads, so a record costs one LDS round trip per var field (its length moves the next
+// segment) instead of a scalar-load chain per step
+template <int NV>
+__device__ __forceinline__ bool fast_record_fp(KParams& dp, const Src& w, uint32_t& q, uint64_t* vl) {
+  const uint32_t wl = (uint32_t)w.wlen;
+  bool ok = true;
+  // the plan is re-read per record (a handful of independent scalar loads): hoisted out of the walk it
+  // would hold ~100 SGPRs for the whole kernel
+  uint32_t z;
+  asm volatile("s_mov_b32 %0, 0" : "=s"(z));   // an opaque 0: the loads below stay in the loop
+  const KAS KxpFast* fp = (const KAS KxpFast*)((const KAS char*)&dp.fp + z);
+  const uint32_t nseg = fp->nseg;
+#pragma unroll
+  for (int s = 0; s < KXF_SEG; s++) {
+    if (s >= (int)nseg) break;
+    const KAS KxpFastSeg& G = fp->seg[s];
+    ok &= q + G.flen + 16 <= wl;            // the run, the var header and length stay in the window
+    const uint32_t qq = ok ? q : 0u;
+    const uint32_t ng = G.nchk;
+#pragma unroll
+    for (int g = 0; g < KXF_CHK; g += 4) {  // groups of 4 independent checks: one LDS round trip each group
+      if (g >= (int)ng) break;
+#pragma unroll
+      for (int c = g; c < g + 4; c++) {
+        const uint32_t cv = G.chval[c];
+        const uint32_t m = (cv >> 31) ? 0xffu : ((cv >> 30) & 1u) ? 0u : 0xffffffu;
+        ok &= ((win_ld(w, qq + G.choff[c]) ^ cv) & m) == 0;
+      }
+    }
+    uint32_t q2 = qq + G.flen;
+    if (G.vkind) {
+      const bool list = G.vkind == 2;
+      ok &= ((win_ld(w, q2) ^ G.vhdr) & 0xffffffu) == 0;
+      const uint32_t l = __builtin_bswap32(win_ld(w, q2 + (list ? 4u : 3u)));
+      const uint64_t b = (uint64_t)l * (list ? G.vwidth : 1u);
+      ok &= l <= wl && b <= wl;             // also rejects a negative length (the generic path reports it)
+#pragma unroll
+      for (int v = 0; v < NV; v++)
+        if ((uint32_t)v == G.vslot) vl[v] += ok ? l : 0u;
+      q2 += (list ? 8u : 7u) + (ok ? (uint32_t)b : 0u);
+    }
+    q = q2;
+  }
+  return ok;
+}
+
 // one canonical record at window offset q (measure: headers, lengths, STOP); var lengths added to vl
 template <int NV>
-__device__ __forceinline__ bool fast_record(const Src& w, uint32_t& q, uint64_t* vl) {
+__device__ __forceinline__ bool fast_record(KParams& dp, const Src& w, uint32_t& q, uint64_t* vl) {
+#ifdef KX_FASTPLAN
+  if (dp.fp.ok) return fast_record_fp<NV>(dp, w, q, vl);
+#endif
   const KAS KxpStep* __restrict__ steps = w.steps;
   const uint32_t wl = (uint32_t)w.wlen;
   bool ok = true;
   uint32_t k = 0;
   while (k < w.nsteps) {
     k = __builtin_amdgcn_readfirstlane(k);
+    // steps k .. k + 3 in one scalar load (the table has room past the plan's end): a FIXED run's
+    // headers do not wait for a second load that depends on the run length
+#ifdef KX_STEP4
+    struct Q4 { KxpStep s[4]; };
+    const Q4 st4 = ldk((const KAS Q4*)&steps[k < KXP_MAX_STEPS - 3 ? k : KXP_MAX_STEPS - 4]);
+    const uint32_t kb = k < KXP_MAX_STEPS - 3 ? 0u : k - (KXP_MAX_STEPS - 4);
+    const KxpStep st = st4.s[kb];
+#else
     const KxpStep st = ldk(&steps[k]);
+#endif
     ok &= q + 64 <= wl;             // a step reads < 64 bytes from q
     const uint32_t qq = ok ? q : 0u;
     if (st.kind == KXP_S_FIXED) {
       const uint32_t m = min(st.hdr >> 24, 4u);
+#ifdef KX_STEP4
+      // a run of m > 1 FIXED steps starts at k <= nsteps - m, so kb == 0 whenever s1.. are used
+      const KxpStep s1 = st4.s[m > 1 ? 1 : 0];
+      const KxpStep s2 = st4.s[m > 2 ? 2 : 0];
+      const KxpStep s3 = st4.s[m > 3 ? 3 : 0];
+#else
       const KxpStep s1 = ldk(&steps[k + (m > 1 ? 1 : 0)]);
       const KxpStep s2 = ldk(&steps[k + (m > 2 ? 2 : 0)]);
       const KxpStep s3 = ldk(&steps[k + (m > 3 ? 3 : 0)]);
+#endif
       const uint32_t o1 = 3 + st.width, o2 = o1 + 3 + s1.width, o3 = o2 + 3 + s2.width;
       const uint32_t len = m == 1 ? o1 : m == 2 ? o2 : m == 3 ? o3 : o3 + 3 + s3.width;
       ok &= ((win_ld(w, qq) ^ st.hdr) & 0xffffffu) == 0;
@@ -2107,13 +2196,19 @@ __device__ __forceinline__ bool fast_tile(KParams& dp, const Src& w, uint64_t tl
   auto phase = [&](int k) {   // diagnostics (KX_DIAG & 64): cycles per phase, summed over tiles
     if (dp.diag & 64) {
       const uint64_t now = __builtin_amdgcn_s_memtime();
-      if (lane == 0) atomicAdd(&g_phase[k], (unsigned long long)(now - tp));
+      if (lane == 0) atomicAdd(&dp.phase[k], (unsigned long long)(now - tp));
       tp = now;
     }
   };
   uint32_t hm = 0;
   fast_scan<0>(w, D0, b0, b1, b2, lane, (uint32_t)lane >> 1, 32u * ((uint32_t)lane & 1u), hm);
   phase(1);
+  // diagnostics (timing only, output wrong): stop after a phase, keeping its result live
+  auto stop_here = [&](uint64_t live) {
+    a.ent = tlo; a.ex = thi; a.cnt = __ballot(live != 0) & 1; a.errc = T_CANON; a.errp = 0;
+    for (int v = 0; v < NV; v++) a.var[v] = 0;
+  };
+  if (dp.diag & 1024) { stop_here(hm); return true; }
   const uint32_t sq = 4 * D0 + 128u * (uint32_t)lane;   // window offset of the segment's first dword
   const uint64_t seg_lo = lane == 0 ? tlo : w.wpos + sq;
   const uint64_t seg_hi = lane == 63 ? thi : kmin64(w.wpos + sq + 128, thi);
@@ -2146,6 +2241,7 @@ __device__ __forceinline__ bool fast_tile(KParams& dp, const Src& w, uint64_t tl
     }
   }
   phase(2);
+  if (dp.diag & 2048) { stop_here(c1 ^ c2 ^ c3); return true; }
   // ---- walk: records of the segment from c1, else c2, else c3: a candidate whose walk fails anywhere
   //      (not canonical, or a record nested in a payload: it parses, but the bytes after it do not) is
   //      replaced by the next; the consistency check below accepts only an unbroken chain ----
@@ -2165,7 +2261,7 @@ __device__ __forceinline__ bool fast_tile(KParams& dp, const Src& w, uint64_t tl
       bool ok = true;
       while (ok && w.wpos + q < seg_hi) {
         const uint64_t start = w.wpos + q;
-        ok = fast_record<NV>(w, q, acc);
+        ok = fast_record<NV>(dp, w, q, acc);
         if (!ok) break;
         st0 = c == 0 ? start : st0; st1 = c == 1 ? start : st1;
         st2 = c == 2 ? start : st2; st3 = c == 3 ? start : st3;
@@ -2189,6 +2285,7 @@ __device__ __forceinline__ bool fast_tile(KParams& dp, const Src& w, uint64_t tl
     if (!__ballot(again)) break;
   }
   phase(3);
+  if (dp.diag & 4096) { stop_here(ex ^ cnt ^ st0 ^ st1 ^ vsum[0]); return true; }
   if (__ballot(bad)) return false;
   // ---- consistency: every walking lane starts where the chain of the walking lane below it exits ----
   const uint64_t hmk = __ballot(ent != X_NONE);
@@ -2235,7 +2332,7 @@ __device__ __forceinline__ Agg measure_records(KParams& dp, const Src& w, uint64
 #pragma unroll
         for (int v = 0; v < (NV > 0 ? NV : 1); v++) vl[v] = 0;
         uint32_t q = (uint32_t)(a - w.wpos);
-        if (fast_record<NV>(w, q, vl) && w.wpos + q <= b) {
+        if (fast_record<NV>(dp, w, q, vl) && w.wpos + q <= b) {
 #pragma unroll
           for (int v = 0; v < NV; v++) vs.len[v] = (uint32_t)vl[v];
           done = true;
@@ -2281,9 +2378,16 @@ __device__ Agg tile_agg(KParams& dp, LDS uint32_t* win, uint64_t t, uint64_t see
     return measure_records<NV, MODE>(dp, w, lo, hi, lane);
   }
   const uint64_t t0 = (dp.diag & 64) ? __builtin_amdgcn_s_memtime() : 0;
-  const Src w = load_window(dp, win, lo, lane, is_thrift(MODE));
-  if ((dp.diag & 64) && lane == 0) atomicAdd(&g_phase[0], (unsigned long long)(__builtin_amdgcn_s_memtime() - t0));
+  // the window DMA is issued first and the batch signature's load behind it, so both round trips overlap
+#ifndef KX_DSIG_OLD
+  const Src w = load_window(dp, win, lo, lane, is_thrift(MODE), false);
   const uint32_t dsig = data_sig(dp);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#else
+  const Src w = load_window(dp, win, lo, lane, is_thrift(MODE));
+  const uint32_t dsig = data_sig(dp);
+#endif
+  if ((dp.diag & 64) && lane == 0) atomicAdd(&dp.phase[0], (unsigned long long)(__builtin_amdgcn_s_memtime() - t0));
   if constexpr (MODE == M_THRIFT) {
     if (dp.fast && !dp.offsets && dsig == dp.prog->sig && w.wlen >= TILE + 64) {
       Agg a;
@@ -2429,7 +2533,7 @@ __device__ __forceinline__ void index_tile(KParams& dp, LDS uint32_t* win, uint6
     a = tile_agg<NV, MODE>(dp, win, t, t == 0 ? 0ull : X_NONE, lane);
   }
   if (lane == 0 && !(dp.diag & 4)) put_tile(dp, t, a, NV);
-  if ((dp.diag & 64) && lane == 0) atomicAdd(&g_phase[5], (unsigned long long)(__builtin_amdgcn_s_memtime() - t_start));
+  if ((dp.diag & 64) && lane == 0) atomicAdd(&dp.phase[5], (unsigned long long)(__builtin_amdgcn_s_memtime() - t_start));
 }
 
 template <int NV, int MODE>
@@ -2442,6 +2546,67 @@ __global__ void __launch_bounds__(NT, 4) index_kernel(DecParams dp_) {  // 4 wav
   const uint64_t t = dp.t_lo + (uint64_t)blockIdx.x * WAVES + wv;
   if (t >= dp.t_hi) return;
   index_tile<NV, MODE>(dp, (LDS uint32_t*)WIN[wv], t, lane);
+}
+
+// ---- kernel 1, fast form (concatenated Thrift with a canonical plan): the fast index path alone, in a
+// kernel of its own so that its registers are not those of the general walk; a tile the fast path
+// cannot index (a non-canonical record, a false-hit chain, a batch that starts with another signature,
+// the last partial tile) is queued for redo_kernel, which walks it with the general field loop ----
+template <int NV>
+__global__ void __launch_bounds__(NT, 4) index_fast_kernel(DecParams dp_) {
+  KParams& dp = KX_PARAMS();
+  (void)dp_;
+  __shared__ __attribute__((aligned(16))) uint32_t WIN[WAVES][WINW];
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const uint64_t t = dp.t_lo + (uint64_t)blockIdx.x * WAVES + wv;
+  if (t >= dp.t_hi) return;
+  // a batch whose first record does not start with the canonical signature is left to redo_kernel whole
+  // (no DMA here): the batch signature is one scalar load, a scalar-cache hit for all but a CU's first wave
+  if (data_sig_s(dp) != dp.prog->sig) return;
+  uint64_t lo, hi;
+  tile_range(dp, t, lo, hi);
+  const Src w = load_window(dp, (LDS uint32_t*)WIN[wv], lo, lane, true, true);
+  Agg a;
+  if (w.wlen >= TILE + 64 &&
+      fast_tile<NV>(dp, w, lo, hi, t == 0 ? 0ull : X_NONE, lane, dp.starts + t * dp.slotcap, a)) {
+    if (lane == 0 && !(dp.diag & 4)) put_tile(dp, t, a, NV);
+  } else if (lane == 0) {
+    dp.redo[atomicAdd(dp.redo_n, 1u)] = (uint32_t)t;
+  }
+}
+
+// one queued tile (an out-of-line call from uniform control flow: the persistent loop around it keeps the
+// general walk's register allocation of a one-tile kernel)
+template <int NV, int MODE>
+__device__ __noinline__ void redo_tile(KParams& dp, LDS uint32_t* win, uint32_t t, int lane) {
+  uint64_t lo, hi;
+  tile_range(dp, t, lo, hi);
+  const Src w = load_window(dp, win, lo, lane, is_thrift(MODE), false);
+  const uint32_t dsig = data_sig(dp);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (lane == 0 && dsig == dp.prog->sig) atomicAdd((unsigned long long*)&dp.status->diag[2], 1ull);
+  const Agg a = walk_tile<NV, MODE>(dp, w, lo, hi, t == 0 ? 0ull : X_NONE, lane, dp.starts + (uint64_t)t * dp.slotcap, dsig);
+  if (lane == 0) put_tile(dp, t, a, NV);
+}
+
+// ---- kernel 1, redo: the queued tiles, general walk (one persistent grid; exits at once when none) ----
+template <int NV, int MODE>
+__global__ void __launch_bounds__(NT, 4) redo_kernel(DecParams dp_) {
+  KParams& dp = KX_PARAMS();
+  (void)dp_;
+  __shared__ __attribute__((aligned(16))) uint32_t WIN[WAVES][WINW];
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const uint32_t W = gridDim.x * WAVES;
+  if (data_sig_s(dp) != dp.prog->sig) {   // index_fast_kernel left the whole batch: every tile
+    for (uint64_t t = dp.t_lo + blockIdx.x * WAVES + wv; t < dp.t_hi; t += W)
+      redo_tile<NV, MODE>(dp, (LDS uint32_t*)WIN[wv], (uint32_t)t, lane);
+    return;
+  }
+  const uint32_t n = __builtin_amdgcn_readfirstlane(*(volatile uint32_t*)dp.redo_n);
+  for (uint32_t i = blockIdx.x * WAVES + wv; i < n; i += W)
+    redo_tile<NV, MODE>(dp, (LDS uint32_t*)WIN[wv], __builtin_amdgcn_readfirstlane(dp.redo[i]), lane);
 }
 
 // ---- kernel 1 (persistent variant, concatenated mode): each wave walks tiles t, t + W, t + 2W ...
@@ -3116,8 +3281,9 @@ __global__ void __launch_bounds__(NT, 4) combo_kernel(ComboParams cp_) {
 
 // Completes a call and re-arms the workspace for the next one (error key, overflow, nstop).
 __global__ void finalize_kernel(kx_status* st, unsigned long long* errkey, uint32_t* overflow, uint64_t* nstop,
-                                const uint64_t* offsets, uint64_t n) {
+                                const uint64_t* offsets, uint64_t n, uint32_t* redo_n) {
   if (threadIdx.x != 0) return;
+  *redo_n = 0;
   unsigned long long k = *errkey;
   if (k != ~0ull && st->code == 0) {
     st->code = (int32_t)(k & 0xff);
@@ -3137,7 +3303,7 @@ constexpr size_t WS_HDR = 256;
 
 struct WsLayout {
   uint64_t ntiles, ngroups, slotcap;
-  size_t tdesc, gdesc, starts, total;
+  size_t tdesc, gdesc, starts, redo, total;
 };
 
 uint32_t krec_for(uint64_t in_len, uint64_t n) {
@@ -3185,6 +3351,7 @@ WsLayout ws_layout(uint64_t min_rec, uint64_t in_len, const uint64_t* offsets, u
   L.tdesc = o; o += (size_t)L.ntiles * T_NF * 8;
   L.gdesc = o; o += (size_t)L.ngroups * G_NF * 8;
   L.starts = o; o += ((size_t)L.ntiles * L.slotcap * 2 + 255) & ~(size_t)255;
+  L.redo = o; o += offsets ? 0 : ((size_t)L.ntiles * 4 + 255) & ~(size_t)255;   // fast index: redo queue
   L.total = o;
   return L;
 }
@@ -3223,6 +3390,30 @@ void launch_combo(unsigned grid, hipStream_t stream, const ComboParams& cp, uint
   hipLaunchKernelGGL((combo_kernel<NV, MODE, false>), dim3(grid), dim3(NT), 0, stream, cp);
 }
 
+// the split fast index pass (index_fast_kernel + redo_kernel) when it applies: 1 launched, 0 not, -1 error
+template <int NV, int MODE>
+int launch_fast_index(const DecParams& dp, unsigned grid, hipStream_t stream) {
+  if constexpr (MODE != M_THRIFT) {
+    return 0;
+  } else {
+    static int split_env = -1, ncu = -1;
+    if (split_env < 0) { const char* e = getenv("KX_FAST_SPLIT"); split_env = e ? atoi(e) : 1; }
+    if (!split_env || !dp.fast || dp.offsets || (dp.diag & ~(64 | 256 | 1024 | 2048 | 4096))) return 0;
+    if (ncu < 0) {
+      int dev = 0;
+      if (hipGetDevice(&dev) != hipSuccess ||
+          hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        ncu = 0;
+    }
+    hipLaunchKernelGGL((index_fast_kernel<NV>), dim3(grid), dim3(NT), 0, stream, dp);
+    if (hipGetLastError() != hipSuccess) return -1;
+    // the queued tiles: one resident grid's worth of waves at most (4 workgroups per CU)
+    const unsigned rgrid = (unsigned)kmin64(grid, (uint64_t)(ncu > 0 ? ncu : 64) * 4);
+    hipLaunchKernelGGL((redo_kernel<NV, MODE>), dim3(rgrid), dim3(NT), 0, stream, dp);
+    return hipGetLastError() != hipSuccess ? -1 : 1;
+  }
+}
+
 template <int NV, int MODE>
 int launch_t(const DecParams& dp0, const WsLayout& L, void* ws, hipStream_t stream, const KxPipe* pp) {
   DecParams dp = dp0;
@@ -3230,6 +3421,9 @@ int launch_t(const DecParams& dp0, const WsLayout& L, void* ws, hipStream_t stre
   dp.errkey = (unsigned long long*)(base + 8);
   dp.overflow = (uint32_t*)(base + 16);
   dp.nstop = (uint64_t*)(base + 24);
+  dp.nstop_ring = (uint64_t*)(base + 160);  // KX_PIPE_EV words, inside WS_HDR
+  dp.redo_n = (uint32_t*)(base + 232);      // inside WS_HDR; reset by finalize_kernel
+  dp.redo = (uint32_t*)(base + L.redo);
   dp.carry = (uint64_t*)(base + 64);  // 12 words, inside WS_HDR
   dp.tdesc = (uint64_t*)(base + L.tdesc);
   dp.gdesc = (uint64_t*)(base + L.gdesc);
@@ -3244,7 +3438,9 @@ int launch_t(const DecParams& dp0, const WsLayout& L, void* ws, hipStream_t stre
   const unsigned grid = (unsigned)((dp.ntiles + WAVES - 1) / WAVES);
   const unsigned ggrid = (unsigned)((dp.ngroups + WAVES - 1) / WAVES);
   if (dp.diag & 256) {
-    hipLaunchKernelGGL((index_kernel<NV, MODE>), dim3(grid), dim3(NT), 0, stream, dp);
+    const int lr = launch_fast_index<NV, MODE>(dp, grid, stream);
+    if (lr < 0) return KX_ERR_HIP;
+    if (lr == 0) hipLaunchKernelGGL((index_kernel<NV, MODE>), dim3(grid), dim3(NT), 0, stream, dp);
     return KX_OK;
   }
   const uint64_t cbt = pp ? pp->combo_tiles : 0;
@@ -3275,13 +3471,16 @@ int launch_t(const DecParams& dp0, const WsLayout& L, void* ws, hipStream_t stre
       }
     }
     hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(64), 0, stream, dp.status, dp.errkey, dp.overflow, dp.nstop,
-                       dp.offsets, dp.n);
+                       dp.offsets, dp.n, dp.redo_n);
     KX_HIP_CHECK(hipGetLastError());
     return KX_OK;
   }
   const uint64_t cht = pp && pp->aux ? pp->chunk_tiles : 0;
   if (!dp.direct && cht && dp.ntiles >= 2 * cht) {
-    // chunked pipeline: aux stream index + group(k) | caller's stream chain + emit(k - ahead)
+    // chunked pipeline: aux stream index + group + chain(k) | caller's stream emit(k - ahead). The chain
+    // pass of chunk k runs on the aux stream right after its group pass (it carries its state from chunk
+    // k - 1 there) and leaves the chunk's nstop in its own ring slot, so the caller's stream runs nothing
+    // but emit passes, each behind the event of its chunk's chain
     const uint64_t nch = (dp.ntiles + cht - 1) / cht;
     const uint64_t D = (uint64_t)(pp->ahead < 0 ? 0 : pp->ahead > KX_PIPE_EV - 2 ? KX_PIPE_EV - 2 : pp->ahead);
     KX_HIP_CHECK(hipEventRecord(pp->fork, stream));
@@ -3289,31 +3488,34 @@ int launch_t(const DecParams& dp0, const WsLayout& L, void* ws, hipStream_t stre
     for (uint64_t s = 0; s < nch + D; s++) {
       if (s < nch) {
         const uint64_t k = s;
-        // the index pass runs at most `ahead` chunks in front of emit (Infinity-Cache residency)
+        // the index pass runs at most `ahead` chunks in front of emit (Infinity-Cache residency; the
+        // nstop ring slot k % KX_PIPE_EV is free again once emit(k - D - 1) has read it)
         if (k >= D + 1) KX_HIP_CHECK(hipStreamWaitEvent(pp->aux, pp->ev_emit[(k - D - 1) % KX_PIPE_EV], 0));
-        const DecParams c = chunk_params(dp, k, nch, cht);
+        DecParams c = chunk_params(dp, k, nch, cht);
+        c.nstop = dp.nstop_ring + k % KX_PIPE_EV;
         const unsigned cg = (unsigned)((c.t_hi - c.t_lo + WAVES - 1) / WAVES);
         const unsigned gg = (unsigned)((c.g_hi - c.g_lo + WAVES - 1) / WAVES);
         hipLaunchKernelGGL((index_kernel<NV, MODE>), dim3(cg), dim3(NT), 0, pp->aux, c);
         KX_HIP_CHECK(hipGetLastError());
         hipLaunchKernelGGL((group_kernel<NV, MODE>), dim3(gg), dim3(NT), 0, pp->aux, c);
         KX_HIP_CHECK(hipGetLastError());
+        hipLaunchKernelGGL((chain_kernel<NV, MODE>), dim3(1), dim3(CT), 0, pp->aux, c);
+        KX_HIP_CHECK(hipGetLastError());
         KX_HIP_CHECK(hipEventRecord(pp->ev_idx[k % KX_PIPE_EV], pp->aux));
       }
       if (s >= D) {
         const uint64_t k = s - D;
-        const DecParams c = chunk_params(dp, k, nch, cht);
+        DecParams c = chunk_params(dp, k, nch, cht);
+        c.nstop = dp.nstop_ring + k % KX_PIPE_EV;
         const unsigned cg = (unsigned)((c.t_hi - c.t_lo + WAVES - 1) / WAVES);
         KX_HIP_CHECK(hipStreamWaitEvent(stream, pp->ev_idx[k % KX_PIPE_EV], 0));
-        hipLaunchKernelGGL((chain_kernel<NV, MODE>), dim3(1), dim3(CT), 0, stream, c);
-        KX_HIP_CHECK(hipGetLastError());
         launch_emit<NV, MODE>(dim3(cg), stream, c);
         KX_HIP_CHECK(hipGetLastError());
         KX_HIP_CHECK(hipEventRecord(pp->ev_emit[k % KX_PIPE_EV], stream));
       }
     }
     hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(64), 0, stream, dp.status, dp.errkey, dp.overflow, dp.nstop,
-                       dp.offsets, dp.n);
+                       dp.offsets, dp.n, dp.redo_n);
     KX_HIP_CHECK(hipGetLastError());
     return KX_OK;
   }
@@ -3327,6 +3529,9 @@ int launch_t(const DecParams& dp0, const WsLayout& L, void* ws, hipStream_t stre
           hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
         ncu = 0;
     }
+    int lr = launch_fast_index<NV, MODE>(dp, grid, stream);
+    if (lr < 0) return KX_ERR_HIP;
+    if (lr > 0) goto indexed;
     if (pf > 0 && !dp.offsets && ncu > 0 && !dp.diag) {
       const unsigned pgrid = (unsigned)kmin64(grid, (uint64_t)ncu * (uint64_t)pf);
       hipLaunchKernelGGL((index_kernel_pf<NV, MODE>), dim3(pgrid), dim3(NT), 0, stream, dp);
@@ -3334,6 +3539,7 @@ int launch_t(const DecParams& dp0, const WsLayout& L, void* ws, hipStream_t stre
       hipLaunchKernelGGL((index_kernel<NV, MODE>), dim3(grid), dim3(NT), 0, stream, dp);
     }
     KX_HIP_CHECK(hipGetLastError());
+  indexed:
     hipLaunchKernelGGL((group_kernel<NV, MODE>), dim3(ggrid), dim3(NT), 0, stream, dp);
     KX_HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL((chain_kernel<NV, MODE>), dim3(1), dim3(CT), 0, stream, dp);
@@ -3342,17 +3548,21 @@ int launch_t(const DecParams& dp0, const WsLayout& L, void* ws, hipStream_t stre
   launch_emit<NV, MODE>(dim3(grid), stream, dp);
   KX_HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(64), 0, stream, dp.status, dp.errkey, dp.overflow, dp.nstop,
-                     dp.offsets, dp.n);
+                     dp.offsets, dp.n, dp.redo_n);
   KX_HIP_CHECK(hipGetLastError());
   return KX_OK;
 }
 
+}  // namespace
+unsigned long long* kx_phase_buf(int diag);
+namespace {
 void fill_diag_flags(DecParams& dp) {
   static int nolds = -1, diag = -1;
   if (nolds < 0) { const char* e = getenv("KX_NOLDS"); nolds = e && e[0] == '1'; }
   if (diag < 0) { const char* e = getenv("KX_DIAG"); diag = e ? atoi(e) : 0; }
   dp.nolds = nolds;
   dp.diag = diag;
+  dp.phase = kx_phase_buf(diag);
 }
 
 }  // namespace
@@ -3436,11 +3646,21 @@ size_t kx_decode_ws_bytes(const KxProgram& hprog, uint64_t in_len, const uint64_
 }
 
 // diagnostics (not part of the public ABI): read and reset the phase-timing accumulators
+unsigned long long* kx_phase_buf(int diag) {
+  static unsigned long long* buf = nullptr;
+  if (!buf && (diag & 64)) {
+    if (hipMalloc((void**)&buf, 8 * sizeof(unsigned long long)) != hipSuccess) return nullptr;
+    if (hipMemset(buf, 0, 8 * sizeof(unsigned long long)) != hipSuccess) return nullptr;
+  }
+  return buf;
+}
+
 extern "C" int kx_debug_phase_cycles(unsigned long long* out, int n) {
   if (n > 8) n = 8;
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase), sizeof(unsigned long long) * n) != hipSuccess) return KX_ERR_HIP;
-  unsigned long long z[8] = {0};
-  if (hipMemcpyToSymbol(HIP_SYMBOL(g_phase), z, sizeof z) != hipSuccess) return KX_ERR_HIP;
+  unsigned long long* b = kx_phase_buf(64);
+  if (!b) return KX_ERR_HIP;
+  if (hipMemcpy(out, b, sizeof(unsigned long long) * n, hipMemcpyDeviceToHost) != hipSuccess) return KX_ERR_HIP;
+  if (hipMemset(b, 0, 8 * sizeof(unsigned long long)) != hipSuccess) return KX_ERR_HIP;
   return KX_OK;
 }
 
@@ -3475,6 +3695,9 @@ int kx_launch_decode(const KxProgram* dprog, const KxProgram& hprog, const uint8
     if (fast_env < 0) { const char* e = getenv("KX_FAST"); fast_env = e ? atoi(e) : 1; }
     // concatenated: the fast index path; known offsets: the fast record measure (index) pass
     dp.fast = fast_env && !pb && hprog.nsteps && (offsets || hprog.sig_len == 3);
+    static int fp_env = -1;
+    if (fp_env < 0) { const char* e = getenv("KX_FASTPLAN"); fp_env = e ? atoi(e) : 1; }
+    if (dp.fast && fp_env) kxp_fast_plan(hprog, dp.fp);
   }
   for (uint32_t c = 0; c < hprog.ncols; c++) {
     const KxpCol& K = hprog.col[c];

@@ -400,7 +400,7 @@ struct NB {
     int prev = -1;
     P.st[si].enc_first = -1;
     if (pb) {
-      int last = -1 << 20;
+      int last = INT32_MIN;
       for (int k = 0; k < P.st[si].nfields; k++) {
         int best = -1;
         for (int j = 0; j < P.st[si].nfields; j++) {

@@ -117,6 +117,75 @@ struct KxProgram {
   uint64_t canon_fixed;
 };
 
+// The canonical plan as the index pass walks it (a kernel parameter: uniform, loaded into SGPRs once per
+// wave): the record is a chain of segments, each a fixed-size run (field headers with their values, struct
+// headers, STOPs) whose header bytes are checked at known offsets, then at most one var field (string or
+// numeric list) whose length moves the next segment. R2: [8 i64 fields] s9 | [] s10 | [STOP].
+#define KXF_SEG 4
+#define KXF_CHK 12
+struct KxpFastSeg {
+  uint16_t flen;              // bytes of the fixed run
+  uint8_t nchk;               // header checks in it
+  uint8_t vkind;              // 0: no var field (the record ends), 1: string / binary, 2: numeric list
+  uint8_t vslot;              // var slot
+  uint8_t vwidth;             // list element width
+  uint16_t pad;
+  uint32_t vhdr;              // the var field's header (3 bytes)
+  uint16_t choff[KXF_CHK];    // check offsets in the run, in groups of 4 (ngrp groups; padding checks pass)
+  uint32_t chval[KXF_CHK];    // expected bytes: a 3-byte header, (bit 31) a 1-byte STOP, (bit 30) padding
+};
+struct KxpFast {
+  uint32_t nseg;
+  uint32_t ok;                // 0: the plan does not fit (the step interpreter runs instead)
+  KxpFastSeg seg[KXF_SEG];
+};
+
+// host: the segment form of a program's canonical plan
+static inline void kxp_fast_plan(const KxProgram& P, KxpFast& F) {
+  F = KxpFast{};
+  if (!P.nsteps) return;
+  uint32_t off = 0;
+  bool ok = true;
+  KxpFastSeg* G = &F.seg[0];
+  F.nseg = 1;
+  auto check = [&](uint32_t v) {
+    if (G->nchk >= KXF_CHK || off > 0xffff) { ok = false; return; }
+    G->choff[G->nchk] = (uint16_t)off;
+    G->chval[G->nchk++] = v;
+  };
+  auto pad_groups = [&]() {   // checks come in groups of 4: fill the last group with passing checks
+    while (G->nchk % 4) {
+      if (G->nchk >= KXF_CHK) { ok = false; return; }
+      G->choff[G->nchk] = 0;
+      G->chval[G->nchk++] = 0x40000000u;
+    }
+  };
+  for (uint32_t k = 0; k < P.nsteps && ok; k++) {
+    const KxpStep& st = P.steps[k];
+    switch (st.kind) {
+      case KXP_S_FIXED: check(st.hdr & 0xffffffu); off += 3u + st.width; break;
+      case KXP_S_STRUCT: check(st.hdr & 0xffffffu); off += 3u; break;
+      case KXP_S_END: check(0x80000000u); off += 1u; break;
+      case KXP_S_BYTES: case KXP_S_LIST:
+        if (off > 0xffff || F.nseg >= KXF_SEG) { ok = false; break; }
+        pad_groups();
+        G->flen = (uint16_t)off;
+        G->vkind = st.kind == KXP_S_BYTES ? 1 : 2;
+        G->vslot = st.vslot;
+        G->vwidth = st.width;
+        G->vhdr = st.hdr & 0xffffffu;
+        G = &F.seg[F.nseg++];
+        off = 0;
+        break;
+      default: ok = false;
+    }
+  }
+  if (off > 0xffff) ok = false;
+  pad_groups();
+  G->flen = (uint16_t)off;
+  F.ok = ok ? 1u : 0u;
+}
+
 static_assert(sizeof(KxpField) == 16, "KxpField layout");
 static_assert(sizeof(KxpInst) == 32, "KxpInst layout");
 static_assert(sizeof(KxpCol) == 16, "KxpCol layout");

@@ -18,13 +18,15 @@ from kitex_amd.schema import Schema
 from kitex_amd.synth import ColumnSet
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libkxoracle.so")
+# KX_ORACLE_SAN=1: the ASan + UBSan build of the same sources (make asan; tests/test_sanitizers.py)
+SAN = os.environ.get("KX_ORACLE_SAN") == "1"
+LIB_PATH = os.path.join(HERE, "lib", "libkxoracle_asan.so" if SAN else "libkxoracle.so")
 
 _lib = None
 
 
 def build(quiet: bool = True) -> str:
-    subprocess.run(["make", "-C", HERE, "-s"], check=True,
+    subprocess.run(["make", "-C", HERE, "-s"] + (["asan"] if SAN else []), check=True,
                    stdout=subprocess.DEVNULL if quiet else None)
     return LIB_PATH
 
@@ -32,7 +34,7 @@ def build(quiet: bool = True) -> str:
 def lib():
     global _lib
     if _lib is None:
-        if not os.path.exists(LIB_PATH):
+        if SAN or not os.path.exists(LIB_PATH):
             build()
         L = C.CDLL(LIB_PATH)
         u8p, u64p = C.POINTER(C.c_uint8), C.POINTER(C.c_uint64)

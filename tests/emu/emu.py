@@ -9,12 +9,20 @@ from kitex_amd import _abi as A
 from kitex_amd.columns import alloc_host, to_kx_columns
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB = os.path.join(HERE, "_build", "libkxemu.so")
+# KX_EMU_SAN=1: a host AddressSanitizer + UndefinedBehaviorSanitizer build (tests/test_sanitizers.py runs the
+# emulator suites in a child process with the ASan runtime preloaded)
+SAN = os.environ.get("KX_EMU_SAN") == "1"
+SAN_FLAGS = "-fsanitize=address,undefined -fno-sanitize-recover=undefined -fno-omit-frame-pointer -shared-libasan"
+OUT = "_build_san" if SAN else "_build"
+LIB = os.path.join(HERE, OUT, "libkxemu.so")
 _lib = None
 
 
 def build():
-    subprocess.run([os.path.join(HERE, "build_emu.sh")], check=True, stdout=subprocess.DEVNULL)
+    env = dict(os.environ, EMU_OUT=OUT)
+    if SAN:
+        env["EMU_EXTRA"] = SAN_FLAGS
+    subprocess.run([os.path.join(HERE, "build_emu.sh")], check=True, stdout=subprocess.DEVNULL, env=env)
 
 
 def lib():

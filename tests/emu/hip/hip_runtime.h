@@ -56,6 +56,13 @@ uint64_t emu_clock_ns();
 #define gridDim (emu_grid_dim())
 #define blockDim (EmuTid{256, 1, 1})
 inline void __syncthreads() { emu_sync_wg(); }
+// an input dword holding the last input bytes: those bytes only (as ASan sees the input allocation), the
+// rest 0xA5 (garbage on the device: no caller may depend on it)
+inline uint32_t emu_gdword(uint64_t A, uint64_t end) {
+  uint32_t x = 0xA5A5A5A5u;
+  memcpy(&x, (const void*)A, end - A < 4 ? (size_t)(end - A) : 4);
+  return x;
+}
 inline void __builtin_amdgcn_fence(int, const char*) {}
 
 inline uint64_t __ballot(int pred) {
@@ -217,6 +224,18 @@ template <typename F>
 inline hipError_t hipOccupancyMaxActiveBlocksPerMultiprocessor(int* n, F, int, size_t) { *n = 1; return hipSuccess; }
 inline hipError_t hipMemcpyFromSymbol(void* dst, const void* sym, size_t n) {
   memcpy(dst, sym, n);
+  return hipSuccess;
+}
+inline hipError_t hipMalloc(void** p, size_t n) {
+  *p = calloc(1, n ? n : 1);
+  return *p ? hipSuccess : (hipError_t)1;
+}
+inline hipError_t hipMemset(void* p, int v, size_t n) {
+  memset(p, v, n);
+  return hipSuccess;
+}
+inline hipError_t hipMemcpy(void* d, const void* s, size_t n, hipMemcpyKind) {
+  memcpy(d, s, n);
   return hipSuccess;
 }
 inline hipError_t hipMemcpyToSymbol(const void* sym, const void* src, size_t n) {
