@@ -345,10 +345,12 @@ def run_c5(args, world, rank, dev, local):
 
     from kitex_amd.shard import shard_range
     totals = {"r2": int(C5_R2 * args.c5_scale), "r3": int(C5_R3 * args.c5_scale)}
-    batches = []
+    batches, split = [], {}
     for cfg, tot in totals.items():
         s0, cnt = shard_range(tot, world, rank)
-        batches.append(Batch(cfg, cnt, dev, s0, args.mode, local))
+        b = Batch(cfg, cnt, dev, s0, args.mode, local)
+        split[cfg] = split_and_scatter(b, cfg, tot, world, rank, dev)
+        batches.append(b)
     torch.cuda.synchronize()
 
     def step():
@@ -385,11 +387,75 @@ def run_c5(args, world, rank, dev, local):
         "cpu_baseline": None,
         "lib_sha256": lib_sha256()[:16],
     }
+    result["split"] = split
     if concat is not None:
         result["concat"] = concat
     if rank == 0 and world == 1 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline("r2", args.cpu_records)
     return result
+
+
+def split_and_scatter(b, cfg, tot, world, rank, dev):
+    """Config 5's input as it arrives: ONE concatenated batch of `tot` records per schema on rank 0. Rank 0
+    finds the world + 1 split points on the device (kx_thrift_split_points: the index and chain passes of a
+    decode, no emit; SURVEY.md §8e pass A), then sends shard k's bytes to rank k (RCCL point-to-point). Each
+    rank checks the bytes it got against its own encoding of the same record range (the generator is
+    per-record) and decodes them in the timed steps. Split-pass time and scatter time are reported, not
+    in `value`."""
+    import torch
+    import torch.distributed as dist
+
+    from kitex_amd import synth
+    from kitex_amd.shard import shard_range
+    pts = torch.zeros(world + 1, dtype=torch.int64, device=dev)
+    info = {}
+    full = None
+    if rank == 0:
+        cdc = b.cdc
+        src = synth.TORCH_GENERATORS[cfg](tot, dev, start=0)
+        full = cdc.Marshal(src)[0]
+        del src
+        torch.cuda.synchronize()
+        cdc.SplitPoints(full, tot, world)              # warm
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        reps = 5
+        ev[0].record()
+        for _ in range(reps):
+            pts = cdc.SplitPoints(full, tot, world)
+        ev[1].record()
+        torch.cuda.synchronize()
+        info = {"split_points_ms": ev[0].elapsed_time(ev[1]) / reps, "batch_bytes": int(full.numel())}
+    if world > 1:
+        dist.broadcast(pts, 0)
+    p = [int(x) for x in pts.tolist()]
+    ok = all(p[k + 1] - p[k] >= 0 for k in range(world)) and p[0] == 0
+    s0, cnt = shard_range(tot, world, rank)
+    ok &= s0 == (rank * tot) // world and cnt == ((rank + 1) * tot) // world - s0
+    t0 = time.perf_counter()
+    if world > 1:
+        if rank == 0:
+            ops = [dist.P2POp(dist.isend, full[p[k]:p[k + 1]].contiguous(), k) for k in range(1, world)]
+            mine = full[p[0]:p[1]]
+        else:
+            mine = torch.empty(p[rank + 1] - p[rank], dtype=torch.uint8, device=dev)
+            ops = [dist.P2POp(dist.irecv, mine, 0)]
+        for r in dist.batch_isend_irecv(ops):
+            r.wait()
+        torch.cuda.synchronize()
+        dist.barrier()
+    else:
+        mine = full[p[0]:p[1]]
+    ok &= mine.numel() == b.wire.numel() and bool(torch.equal(mine, b.wire))
+    if world > 1:
+        okt = torch.tensor([1 if ok else 0], device=dev)
+        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+        ok = bool(okt.item())
+    b.wire = mine.clone() if rank == 0 else mine      # the timed decode reads the shard it was sent
+    b.in_bytes = b.wire.numel()
+    del full
+    info.update({"parts": world, "shard_equals_local_encoding": ok,
+                 "scatter_ms": (time.perf_counter() - t0) * 1e3 if world > 1 else 0.0})
+    return info
 
 
 def concat_shards(batches, world, rank, dev):

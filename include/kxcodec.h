@@ -17,6 +17,9 @@
  *                                 records are concatenated (offsets == NULL)
  *   kx_thrift_skip_batch ........ the skip decoder netpollSkipDecoder.SkipStruct/skipType
  *                                 (pkg/remote/codec/thrift/codec_apache.go:166-293) over N records
+ *   kx_thrift_split_points ...... the same skip over one concatenated batch, keeping only the G + 1
+ *                                 record boundaries that cut it into G shards of equal record counts
+ *                                 (SURVEY.md §8e pass A; the reference's caller-side partition)
  *   kx_thrift_encoded_size_batch  thrift.FastCodec.BLength (k-mock.go:201-210; struct_tpl.go:266-391)
  *   kx_thrift_encode_batch ...... thrift.FastCodec.FastWriteNocopy (k-mock.go:190-199; struct_tpl.go:225-264,
  *                                 field reorder pkg tool/.../thriftgo/patcher.go:503-522)
@@ -323,6 +326,17 @@ int kx_thrift_decode_sizes_extents(kx_ctx* c, const kx_schema* s, const uint8_t*
 /* Skip decoder over n concatenated records: writes record start offsets (n+1 entries, device u64). */
 int kx_thrift_skip_batch(kx_ctx* c, const uint8_t* in, uint64_t in_len, uint64_t n,
                          uint64_t* offsets_out, kx_status* status, void* stream);
+
+/* Split points of n concatenated records of schema s for `parts` shards (1 <= parts <= 65536):
+ * points_out[k] (parts + 1 entries, device u64) = the start of record floor(k * n / parts), and
+ * points_out[parts] = the end of record n - 1 (= status->consumed). Shard k is then the batch
+ * in[points_out[k] .. points_out[k + 1]) of floor((k+1)n/parts) - floor(kn/parts) records. Runs the decode's
+ * index pass (with the schema's fast path) and its chain, never the emit pass. A flat schema's
+ * records are walked by its program (field types checked as in decode); a nested schema's by the skip
+ * decoder (kx_thrift_skip_batch). On a decode error or EOF before n records the status is the
+ * decode's and points_out is left unwritten. n == 0: every point is 0. */
+int kx_thrift_split_points(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len, uint64_t n,
+                           uint32_t parts, uint64_t* points_out, kx_status* status, void* stream);
 
 /* ---- Thrift binary: batched BLength / FastWriteNocopy ---- */
 int kx_thrift_encoded_size_batch(kx_ctx* c, const kx_schema* s, const kx_columns* in, uint64_t n,

@@ -19,7 +19,7 @@ _lib = None
 EXPORTS = [
     "kx_abi_version", "kx_strerror", "kx_schema_create", "kx_schema_destroy", "kx_schema_num_columns",
     "kx_schema_column_info", "kx_schema_presence_bits", "kx_schema_min_record_size", "kx_ctx_create",
-    "kx_ctx_destroy", "kx_thrift_decode_batch", "kx_thrift_skip_batch", "kx_thrift_encoded_size_batch",
+    "kx_ctx_destroy", "kx_thrift_decode_batch", "kx_thrift_skip_batch", "kx_thrift_split_points", "kx_thrift_encoded_size_batch",
     "kx_thrift_encode_batch", "kx_pb_decode_batch", "kx_pb_encoded_size_batch",
     "kx_pb_encode_batch", "kx_host_decode_batch", "kx_host_pb_decode_batch",
     "kx_thrift_message_begin_length", "kx_thrift_write_message_begin", "kx_thrift_read_message_begin",
@@ -84,6 +84,7 @@ def lib():
     L.kx_decode_workspace_bytes.argtypes = [vp, u64, C.c_int, u64]
     L.kx_decode_workspace_bytes.restype = u64
     L.kx_thrift_skip_batch.argtypes = [vp, vp, u64, u64, vp, vp, vp]
+    L.kx_thrift_split_points.argtypes = [vp, vp, vp, u64, u64, C.c_uint32, vp, vp, vp]
     L.kx_thrift_encoded_size_batch.argtypes = [vp, vp, C.POINTER(A.Columns), u64, vp, vp]
     L.kx_thrift_encode_batch.argtypes = [vp, vp, C.POINTER(A.Columns), u64, vp, u64, vp, vp, vp]
     L.kx_pb_encoded_size_batch.argtypes = L.kx_thrift_encoded_size_batch.argtypes

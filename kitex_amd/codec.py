@@ -626,8 +626,26 @@ class ThriftCodec:
             raise ProtocolError(s.code, "skipThriftStruct", s.record, s.offset)
         return offs
 
+    @on_call_stream
+    def SplitPoints(self, buf, n: int, parts: int, stream=None):
+        """kx_thrift_split_points: the parts + 1 record boundaries that cut n concatenated records into
+        `parts` shards of equal record counts (shard k holds floor((k+1)n/parts) - floor(kn/parts) records)
+        -> int64[parts + 1]. The index and chain passes of a decode, no emit (SURVEY.md §8e pass A)."""
+        import torch
+        pts = torch.empty(parts + 1, dtype=torch.int64, device=self.device)
+        st = status_tensor(self.device)
+        ss = _stream(stream)
+        rc = lib().kx_thrift_split_points(self._ctx(ss).handle, self.dschema.handle, _ptr(buf), buf.numel(), n,
+                                          parts, _ptr(pts), _ptr(st), int(ss.cuda_stream))
+        check(rc, "kx_thrift_split_points")
+        s = read_status(st, ss)
+        if s.code:
+            raise ProtocolError(s.code, "split points", s.record, s.offset)
+        return pts
+
     # lower-case aliases
     name, unmarshal, marshal, blength, skip = Name, Unmarshal, Marshal, BLength, Skip
+    split_points = SplitPoints
 
 
 class ProtobufCodec(ThriftCodec):

@@ -527,6 +527,27 @@ int kx_thrift_skip_batch(kx_ctx* c, const uint8_t* in, uint64_t in_len, uint64_t
   return kx_launch_skip(in, in_len, n, offsets_out, status, c->ws, c->ws_size, epoch, st);
 }
 
+int kx_thrift_split_points(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len, uint64_t n,
+                           uint32_t parts, uint64_t* points_out, kx_status* status, void* stream) {
+  if (!c || !s || !status || !points_out || (!in && in_len) || parts == 0 || parts > 65536)
+    return KX_ERR_INVALID_ARG;
+  if (s->nprog && s->nprog->pb) return KX_ERR_NOT_IMPLEMENTED;   // Kitex-Protobuf: Batch frames, not records
+  int rc = set_device(c);
+  if (rc) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  if (n == 0) {
+    KX_HIP_CHECK(hipMemsetAsync(status, 0, sizeof(kx_status), st));
+    KX_HIP_CHECK(hipMemsetAsync(points_out, 0, 8ull * (parts + 1), st));
+    return KX_OK;
+  }
+  KxProgram* dp = nullptr;
+  if (!s->nprog && (rc = prog_on_device(const_cast<kx_schema*>(s), c->device, &dp))) return rc;
+  uint64_t epoch = 0;
+  if ((rc = ensure_ws(c, kx_skip_ws_bytes(in_len, n), st, &epoch))) return rc;
+  return kx_launch_split(dp, s->nprog ? nullptr : &s->prog, in, in_len, n, parts, points_out, status, c->ws,
+                         c->ws_size, epoch, st);
+}
+
 int kx_thrift_encoded_size_batch(kx_ctx* c, const kx_schema* s, const kx_columns* in, uint64_t n,
                                  uint64_t* sizes_out, void* stream) {
   if (!c || !s || !sizes_out) return KX_ERR_INVALID_ARG;

@@ -113,6 +113,8 @@ struct DecParams {
   uint64_t* nstop_ring;      // chunked pipeline: nstop of chunk k at [k % KX_PIPE_EV] (chain runs ahead of emit)
   uint32_t* redo_n;          // fast index kernel: tiles it could not index (count, then their ids)
   uint32_t* redo;
+  uint64_t* split_out;       // kx_thrift_split_points: nsplit + 1 record starts (no emit pass)
+  uint32_t nsplit;
   uint64_t var_base[KXP_NV_MAX];  // arena positions start here (a chunk of a larger batch)
   KxpFast fp;                // the canonical plan in segment form (fast_record_fp), fp.ok = 0: none
   uint64_t ntiles, ngroups, slotcap;
@@ -3240,6 +3242,58 @@ __device__ __forceinline__ void emit_tile(KParams& dp, LDS uint32_t* win, uint64
   }
 }
 
+// Split points of a concatenated batch (kx_thrift_split_points; SURVEY.md §8e "pass A emits G split
+// points", the partition the reference leaves to its caller, codec_apache.go:166-172): lane k of the grid
+// finds the start of record floor(k·n/G) from what the index, group and chain passes left (the tile's
+// global record base = group base + tile prefix, then the tile's record-start slot; past the slots the
+// records are skipped one by one from the last slot), and lane G the end of record n − 1. Nothing else
+// is read: no emit pass. A chain that ended early (decode error, EOF) leaves its status and no points.
+template <int NV, int MODE>
+__global__ void __launch_bounds__(64) split_kernel(DecParams dp_) {
+  KParams& dp = KX_PARAMS();
+  (void)dp_;
+  const uint64_t k = (uint64_t)blockIdx.x * 64 + threadIdx.x;
+  const uint64_t G = dp.nsplit, n = dp.n;
+  if (k > G || *(volatile uint64_t*)dp.nstop < n) return;
+  const bool last = k == G;
+  // floor(k·n / G) without a 128-bit product (G <= 2^16)
+  const uint64_t i = last ? n - 1 : (n / G) * k + ((n % G) * k) / G;
+  const uint64_t nt = dp.ntiles, ng = dp.ngroups;
+  auto tbase = [&](uint64_t t) -> uint64_t {   // first record of tile t (tiles past the chain: none)
+    const uint64_t gb = dp.gdesc[(uint64_t)G_BCNT * ng + t / GT] & V48;
+    return gb == X_DONE ? ~0ull : gb + (dp.tdesc[(uint64_t)T_PCNT * nt + t] & V48);
+  };
+  uint64_t lo = 0, hi = nt;                    // tbase(lo) <= i < tbase(hi)
+  while (hi - lo > 1) {
+    const uint64_t mid = lo + (hi - lo) / 2;
+    if (tbase(mid) <= i) lo = mid;
+    else hi = mid;
+  }
+  const uint64_t t = lo, j = i - tbase(t), sc = dp.slotcap;
+  const uint16_t* st = dp.starts + t * sc;
+  const Src w{dp.in, dp.in_len, 0, 0, nullptr, nullptr, 0u, 0ull};   // global reads only
+  auto skip = [&](uint64_t p, uint64_t r) -> uint64_t {
+    VarState<NV> vs;
+    uint64_t end = p, pres = 0;
+    parse_record<NV, MODE>(dp, w, p, dp.in_len, r, false, &end, vs, pres);
+    return end;
+  };
+  const uint64_t t0 = t * (uint64_t)TILE;
+  uint64_t pos;
+  if (j < sc) {
+    pos = t0 + st[j];
+  } else {
+    pos = t0 + st[sc - 1];
+    for (uint64_t m = sc - 1; m < j; m++) pos = skip(pos, i - j + m);
+  }
+  if (last) {
+    pos = skip(pos, i);
+    dp.status->n_records = n;
+    dp.status->consumed = pos;
+  }
+  dp.split_out[k] = pos;
+}
+
 template <int NV, int MODE, bool COOP = false>
 __global__ void __launch_bounds__(NT, 4) emit_kernel(DecParams dp_) {  // 4 waves per SIMD: <= 128 VGPRs
   KParams& dp = KX_PARAMS();
@@ -3545,8 +3599,16 @@ int launch_t(const DecParams& dp0, const WsLayout& L, void* ws, hipStream_t stre
     hipLaunchKernelGGL((chain_kernel<NV, MODE>), dim3(1), dim3(CT), 0, stream, dp);
     KX_HIP_CHECK(hipGetLastError());
   }
+  if constexpr (is_thrift(MODE) || MODE == M_SKIP) {
+    if (dp.split_out) {   // split points: the chain pass's tile bases and slots, no emit
+      hipLaunchKernelGGL((split_kernel<NV, MODE>), dim3((dp.nsplit + 64) / 64), dim3(64), 0, stream, dp);
+      KX_HIP_CHECK(hipGetLastError());
+      goto done;
+    }
+  }
   launch_emit<NV, MODE>(dim3(grid), stream, dp);
   KX_HIP_CHECK(hipGetLastError());
+done:
   hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(64), 0, stream, dp.status, dp.errkey, dp.overflow, dp.nstop,
                      dp.offsets, dp.n, dp.redo_n);
   KX_HIP_CHECK(hipGetLastError());
@@ -3710,6 +3772,34 @@ int kx_launch_decode(const KxProgram* dprog, const KxProgram& hprog, const uint8
   return pb ? launch_nv<M_PB>(dp, L, ws, stream, hprog.nvar, pipe)
             : ls ? launch_nv<M_THRIFT_LS>(dp, L, ws, stream, hprog.nvar, pipe)
                  : launch_nv<M_THRIFT>(dp, L, ws, stream, hprog.nvar, pipe);
+}
+
+// split points: a flat Thrift schema's own index pass (its fast path included), or the schema-free skip
+// walker (dprog null: nested schemas); every column a view, so no pass writes a column
+int kx_launch_split(const KxProgram* dprog, const KxProgram* hprog, const uint8_t* in, uint64_t in_len, uint64_t n,
+                    uint32_t parts, uint64_t* points, kx_status* status, void* ws, size_t ws_size, uint64_t epoch,
+                    hipStream_t stream) {
+  DecParams dp{};
+  fill_diag_flags(dp);
+  dp.in = in; dp.in_len = in_len; dp.n = n; dp.status = status; dp.epoch = epoch;
+  dp.split_out = points; dp.nsplit = parts;
+  dp.krec = 64;
+  dp.cols.view = ~0u;
+  const WsLayout L = ws_layout(1, in_len, nullptr, n);
+  if (ws_size < L.total) return KX_ERR_INVALID_ARG;
+  if (!dprog) {
+    dp.winb = TILE + HALO + 16;
+    return kx_dec_launch<0, M_SKIP>(&dp, &L, ws, stream, nullptr);
+  }
+  dp.prog = (const KAS KxProgram*)dprog;
+  dp.winb = win_bytes(in_len, n);
+  static int fast_env = -1;
+  if (fast_env < 0) { const char* e = getenv("KX_FAST"); fast_env = e ? atoi(e) : 1; }
+  dp.fast = fast_env && hprog->nsteps && hprog->sig_len == 3;
+  bool ls = false;
+  for (uint32_t f = 0; f < hprog->nfields; f++) ls |= hprog->f[f].kind == KXP_K_LSTRUCT;
+  return ls ? launch_nv<M_THRIFT_LS>(dp, L, ws, stream, hprog->nvar, nullptr)
+            : launch_nv<M_THRIFT>(dp, L, ws, stream, hprog->nvar, nullptr);
 }
 
 int kx_launch_skip(const uint8_t* in, uint64_t in_len, uint64_t n, uint64_t* offsets_out, kx_status* status,

@@ -125,6 +125,10 @@ size_t kx_decode_ws_bytes(const KxProgram& hprog, uint64_t in_len, const uint64_
 int kx_launch_skip(const uint8_t* in, uint64_t in_len, uint64_t n, uint64_t* offsets_out,
                    kx_status* status, void* ws, size_t ws_size, uint64_t epoch, hipStream_t stream);
 size_t kx_skip_ws_bytes(uint64_t in_len, uint64_t n);
+// split points of n concatenated records for `parts` shards (parts + 1 starts; dprog null: skip walker)
+int kx_launch_split(const KxProgram* dprog, const KxProgram* hprog, const uint8_t* in, uint64_t in_len, uint64_t n,
+                    uint32_t parts, uint64_t* points, kx_status* status, void* ws, size_t ws_size, uint64_t epoch,
+                    hipStream_t stream);
 // Kitex-PB Batch frames (0x0A, uvarint length, body): frame starts (n + 1) and body extents
 int kx_launch_pb_frames(const uint8_t* in, uint64_t in_len, uint64_t n, uint64_t* frame_offsets, uint64_t* body_start,
                         uint64_t* body_end, kx_status* status, void* ws, size_t ws_size, uint64_t epoch,

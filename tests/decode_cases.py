@@ -242,6 +242,73 @@ def case_skip(skipper, oracle):
     assert np.array_equal(to_np(got).astype(np.uint64), offs)
 
 
+# ---- split points (kx_thrift_split_points: SURVEY.md §8e pass A) ------------------------------------
+def expected_points(offs, n, parts):
+    return np.array([int(offs[(k * n) // parts]) if k < parts else int(offs[n]) for k in range(parts + 1)],
+                    dtype=np.uint64)
+
+
+SPLIT_CASES = ["r2", "r3", "r1", "noncanonical", "slot_overflow", "ragged", "tiny"]
+
+
+def split_input(oracle, case):
+    """(schema, wire, offs) of one split-point case"""
+    if case in ("r2", "r3", "r1"):
+        sch = S.SCHEMAS[case]()
+        n = {"r2": 20000, "r3": 3000, "r1": 30000}[case]
+        cs = synth.GENERATORS[case](n)
+        rc, wire, offs = oracle.encode(sch, cs)
+        return sch, wire, offs
+    if case == "tiny":
+        sch = S.schema_r2()
+        rc, wire, offs = oracle.encode(sch, synth.gen_r2(5))
+        return sch, wire, offs
+    rng = np.random.default_rng(11)
+    if case == "noncanonical":       # every 3rd record reordered: the walk path, not the fast path
+        recs = [r2_record(oracle, rng, order=list(rng.permutation(10)) if i % 3 == 0 else None)
+                for i in range(4000)]
+        return (S.schema_r2(),) + concat(recs)
+    if case == "ragged":             # records larger than a tile between small ones
+        recs = [r2_record(oracle, rng, strlens=((20000 if i % 97 == 0 else int(rng.integers(0, 64))), 3))
+                for i in range(2000)]
+        return (S.schema_r2(),) + concat(recs)
+    sch = S.Schema(S.Struct("D", [S.Field(1, A.T_I64, default=42), S.Field(2, A.T_I32, default=-7),
+                                  S.Field(3, A.T_BOOL), S.Field(4, A.T_STRING)]))
+    recs = [rec_bytes(oracle, [(A.T_I64, 1, i64(oracle, i)), (A.T_STRING, 4, sbytes(oracle, b"x" * 30000))])
+            for i in range(24)]
+    recs += [b"\x00"] * 30000          # tiles of 1-byte records: past the record-start slots
+    recs += [rec_bytes(oracle, [(A.T_STRING, 4, sbytes(oracle, b"y" * 100))]) for i in range(24)]
+    return (sch,) + concat(recs)
+
+
+def case_split(splitter, oracle, case, parts_list=(1, 2, 3, 8, 64)):
+    """splitter(schema, wire, n, parts) -> (points, status): record floor(k n / parts)'s start per k, the
+    batch end last, and the status of a clean pass"""
+    sch, wire, offs = split_input(oracle, case)
+    n = len(offs) - 1
+    for parts in parts_list:
+        pts, st = splitter(sch, wire, n, parts)
+        assert st.code == 0 and st.n_records == n and st.consumed == wire.size, (parts, st.code)
+        assert np.array_equal(to_np(pts).astype(np.uint64), expected_points(offs, n, parts)), parts
+
+
+def case_split_errors(splitter, oracle):
+    """a decode error or EOF before n records: the decode's status; n == 0: zero points"""
+    sch = S.schema_r2()
+    rng = np.random.default_rng(4)
+    recs = [r2_record(oracle, rng) for _ in range(900)]
+    wire, offs = concat(recs)
+    for data, n in ((wire[:-7], 900), (wire, 905)):
+        rc, exp, est, _ = oracle.decode(sch, data, n)
+        pts, st = splitter(sch, data, n, 4)
+        assert est.code != 0 and (st.code, st.record, st.offset) == (est.code, est.record, est.offset)
+    recs[400] = rec_bytes(oracle, [(A.T_STRING, 9, bytes.fromhex("fffffff0"))])
+    wire2, _ = concat(recs)
+    rc, exp, est, _ = oracle.decode(sch, wire2, 900)
+    pts, st = splitter(sch, wire2, 900, 4)
+    assert est.code != 0 and (st.code, st.record, st.offset) == (est.code, est.record, est.offset)
+
+
 # ---- containers beyond list<scalar>: list<string>, set<string>, map<K,V> (FieldFastReadList/Map,
 #      struct_tpl.go:466-625) -------------------------------------------------------------------
 CONTAINER_SCHEMAS = {"cx1": (S.schema_cx1, synth.gen_cx1), "cx2": (S.schema_cx2, synth.gen_cx2)}

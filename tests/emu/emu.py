@@ -45,6 +45,9 @@ def lib():
         _lib.emu_nested_encode.restype = C.c_int
         _lib.emu_nested_encode.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64,
                                            C.c_void_p, C.c_void_p]
+        _lib.emu_split.restype = C.c_int
+        _lib.emu_split.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint32,
+                                   C.c_void_p, C.c_void_p, C.c_int]
         _lib.emu_crc.restype = C.c_int
         _lib.emu_crc.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_int, C.c_void_p, C.c_void_p,
                                  C.c_void_p]
@@ -96,6 +99,17 @@ def skip(data: np.ndarray, n: int, threads: int = 8):
     rc = lib().emu_decode(None, 0, data.ctypes.data, data.size, None, n, None, None, C.addressof(st), 1,
                           offs.ctypes.data)
     return rc, offs, st
+
+
+def split_points(schema, data: np.ndarray, n: int, parts: int, threads: int = 8):
+    """kx_launch_split under the emulator: rc, points (parts + 1), status; schema None: the skip walker"""
+    os.environ["KX_EMU_THREADS"] = str(threads)
+    pts = np.full(parts + 1, 0xDEAD, dtype=np.uint64)
+    st = A.Status()
+    tab, ns = schema.struct_table() if schema is not None else (None, 0)
+    rc = lib().emu_split(C.cast(tab, C.c_void_p) if tab is not None else None, ns, data.ctypes.data, data.size, n,
+                         parts, pts.ctypes.data, C.addressof(st), 1 if schema is None else 0)
+    return rc, pts, st
 
 
 def frames(data: np.ndarray, n: int, max_payload: int = 0, threads: int = 8, grpc: bool = False):

@@ -63,6 +63,32 @@ extern "C" int emu_decode(const kx_struct_desc* structs, uint32_t nstructs, cons
   return rc;
 }
 
+// split points (kx_launch_split) under the emulator: skip = 1 uses the schema-free skip walker
+extern "C" int emu_split(const kx_struct_desc* structs, uint32_t nstructs, const uint8_t* in, uint64_t in_len,
+                         uint64_t n, uint32_t parts, uint64_t* points, kx_status* status, int skip) {
+  static kx_schema s;
+  int rc = skip ? KX_OK : kx_build_program(structs, nstructs, &s);
+  if (rc) return rc;
+  const size_t ws_size = kx_skip_ws_bytes(in_len, n);
+  static char* ws = nullptr;
+  static size_t ws_cap = 0;
+  static uint64_t epoch = 0xffff;
+  if (ws_cap < ws_size) {
+    free(ws);
+    ws_cap = ws_size + ws_size / 4;
+    ws = (char*)malloc(ws_cap);
+    epoch = 0xffff;
+  }
+  if (++epoch > 0xffff) {
+    memset(ws, 0, ws_cap);
+    memset(ws + 8, 0xff, 8);
+    epoch = 1;
+  }
+  memset(status, 0, sizeof *status);
+  return kx_launch_split(skip ? nullptr : &s.prog, skip ? nullptr : &s.prog, in, in_len, n, parts, points, status, ws,
+                         ws_cap, epoch, nullptr);
+}
+
 // framing sniff (kx_launch_frames) under the emulator, workspace shared with emu_decode's
 extern "C" int emu_frames(const uint8_t* in, uint64_t in_len, uint64_t n, uint64_t max_payload, uint64_t* fo,
                           uint64_t* ps, uint64_t* pe, uint8_t* kinds, kx_status* status, int grpc) {

@@ -106,6 +106,27 @@ def test_emu_skip(edec, oracle):
     DC.case_skip(lambda wire, n: emu.skip(wire, n)[1], oracle)
 
 
+def _emu_split(sch, wire, n, parts, skip=False):
+    rc, pts, st = emu.split_points(None if skip else sch, wire, n, parts)
+    assert rc == 0
+    return pts, st
+
+
+@pytest.mark.parametrize("case", DC.SPLIT_CASES)
+def test_emu_split_points(edec, oracle, case):
+    DC.case_split(_emu_split, oracle, case)
+
+
+@pytest.mark.parametrize("case", ["r3", "noncanonical", "slot_overflow"])
+def test_emu_split_points_skip_walker(edec, oracle, case):
+    """the schema-free walker (nested schemas' split points)"""
+    DC.case_split(lambda sch, w, n, p: _emu_split(sch, w, n, p, skip=True), oracle, case, parts_list=(3, 8))
+
+
+def test_emu_split_points_errors(edec, oracle):
+    DC.case_split_errors(_emu_split, oracle)
+
+
 @pytest.mark.parametrize("name,n", [("r2", 75000), ("r3", 20000), ("r1", 60000)])
 def test_emu_deep_lookback(oracle, name, n):
     """64 co-resident workgroups, one super-tile each: look-back windows that reach past their

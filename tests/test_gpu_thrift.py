@@ -10,7 +10,7 @@ from kitex_amd import _abi as A
 from kitex_amd import schema as S
 from kitex_amd import synth
 from tests import decode_cases as DC
-from tests.helpers import to_np
+from tests.helpers import assert_columns_equal, to_np
 
 pytestmark = pytest.mark.gpu
 
@@ -191,6 +191,54 @@ def test_encode_optional_and_nil(torch, dev, oracle):
 def test_skip_batch_matches_oracle(torch, dev, oracle):
     sch, cdc = codec("r3")
     DC.case_skip(lambda wire, n: cdc.Skip(torch.from_numpy(wire).to(dev), n), oracle)
+
+
+def _gpu_split(torch, dev):
+    from kitex_amd.codec import ThriftCodec, read_status, status_tensor
+    from kitex_amd._lib import lib
+    from kitex_amd.codec import _ptr
+
+    def split(sch, wire, n, parts):
+        cdc = ThriftCodec(sch)
+        buf = torch.from_numpy(wire.copy()).to(dev) if wire.size else torch.empty(0, dtype=torch.uint8, device=dev)
+        pts = torch.full((parts + 1,), 0xDEAD, dtype=torch.int64, device=dev)
+        st = status_tensor(dev)
+        ss = torch.cuda.current_stream(dev)
+        rc = lib().kx_thrift_split_points(cdc._ctx(ss).handle, cdc.dschema.handle, _ptr(buf), buf.numel(), n, parts,
+                                          _ptr(pts), _ptr(st), int(ss.cuda_stream))
+        assert rc == 0
+        return pts, read_status(st, ss)
+    return split
+
+
+@pytest.mark.parametrize("case", DC.SPLIT_CASES)
+def test_split_points_match_oracle(torch, dev, oracle, case):
+    """kx_thrift_split_points: record floor(k n / G)'s start for every k (the oracle's record offsets)"""
+    DC.case_split(_gpu_split(torch, dev), oracle, case)
+
+
+def test_split_points_errors(torch, dev, oracle):
+    DC.case_split_errors(_gpu_split(torch, dev), oracle)
+
+
+def test_split_points_codec_method_shards_decode(torch, dev, oracle):
+    """ThriftCodec.SplitPoints cuts one concatenated batch into shards that decode on their own to the
+    whole batch's columns (the c5 bench's sharding)"""
+    from kitex_amd.codec import ThriftCodec
+    sch = S.schema_r2()
+    n = 50000
+    cs = synth.gen_r2(n)
+    rc, wire, offs = oracle.encode(sch, cs)
+    buf = torch.from_numpy(wire).to(dev)
+    cdc = ThriftCodec(sch)
+    pts = to_np(cdc.SplitPoints(buf, n, 4))
+    assert np.array_equal(pts.astype(np.uint64), DC.expected_points(offs, n, 4))
+    _, infos, _ = oracle.flatten(sch)
+    for k in range(4):
+        r0, r1 = (k * n) // 4, ((k + 1) * n) // 4
+        res = cdc.Unmarshal(buf[int(pts[k]):int(pts[k + 1])], r1 - r0)
+        rc, exp, est, _ = oracle.decode(sch, wire[int(offs[r0]):int(offs[r1])], r1 - r0)
+        assert_columns_equal(res.columns, exp, infos, r1 - r0)
 
 
 def test_decode_beyond_2gib(torch, dev):
