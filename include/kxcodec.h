@@ -58,7 +58,7 @@
 extern "C" {
 #endif
 
-#define KX_ABI_VERSION 4
+#define KX_ABI_VERSION 5  /* 5: kx_status.var_total holds 16 var slots; kx_thrift_split_points */
 
 /* ---- Thrift TType ids (gopkg protocol/thrift; pinned by pkg/protocol/bthrift/binary_test.go) ---- */
 enum {
@@ -251,7 +251,7 @@ typedef struct kx_columns {
   uint64_t* presence;   /* n words (bit per presence-tracked field), required iff the schema has any */
 } kx_columns;
 
-/* Per-call status, written by the device (caller-owned DEVICE memory, 128 bytes, 8-aligned). */
+/* Per-call status, written by the device (caller-owned DEVICE memory, 192 bytes, 8-aligned). */
 typedef struct kx_status {
   int32_t code;         /* first error (lowest record index), 0 = OK */
   int32_t reserved0;
@@ -259,7 +259,7 @@ typedef struct kx_status {
   uint64_t offset;      /* byte offset of the failing record's start in the input */
   uint64_t n_records;   /* records decoded */
   uint64_t consumed;    /* input bytes consumed (concatenated mode) */
-  uint64_t var_total[8];  /* required arena size (arena units) of the first 8 var columns */
+  uint64_t var_total[16]; /* required arena size (arena units) per var slot (ABI 5: 16 slots, was 8) */
   uint64_t diag[3];       /* decode diagnostics: [0] tiles re-walked from their true entry,
                              [1] groups of 64 tiles re-scanned by the chain pass, [2] reserved */
 } kx_status;

@@ -6,7 +6,7 @@ layout is checked by tests/test_abi.py against the compiled library.
 """
 import ctypes as C
 
-KX_ABI_VERSION = 4
+KX_ABI_VERSION = 5
 
 # Thrift TType ids (gopkg protocol/thrift; pinned by pkg/protocol/bthrift/binary_test.go)
 T_STOP, T_VOID, T_BOOL, T_BYTE, T_DOUBLE = 0, 1, 2, 3, 4
@@ -109,7 +109,7 @@ class Status(C.Structure):
         ("offset", C.c_uint64),
         ("n_records", C.c_uint64),
         ("consumed", C.c_uint64),
-        ("var_total", C.c_uint64 * 8),
+        ("var_total", C.c_uint64 * 16),
         ("diag", C.c_uint64 * 3),
     ]
 
@@ -124,7 +124,7 @@ TTS_META, TTS_HEADER, TTS_DATA, TTS_TRAILER, TTS_RST = 1, 2, 3, 4, 5
 
 assert C.sizeof(TTStreamKeys) == 48
 assert C.sizeof(FieldDesc) == 16
-assert C.sizeof(Status) == 128
+assert C.sizeof(Status) == 192
 assert C.sizeof(Column) == 64
 assert C.sizeof(Columns) == MAX_COLUMNS * 64 + 16
 assert C.sizeof(ColumnInfo) == 40

@@ -30,7 +30,7 @@ def _stale() -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-DECODE_PARTS = 6   # kx_decode.hip is compiled once per part (-DKX_DEC_PART=k): its kernels in parallel
+DECODE_PARTS = 8   # kx_decode.hip is compiled once per part (-DKX_DEC_PART=k): its kernels in parallel
 
 
 def _units(libdir=LIBDIR):

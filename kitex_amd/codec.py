@@ -247,7 +247,7 @@ def ttstream_frame_scan(buf, n: int, keys: Optional[A.TTStreamKeys] = None, devi
 
 def status_tensor(device):
     import torch
-    return torch.zeros(16, dtype=torch.int64, device=device)
+    return torch.zeros(24, dtype=torch.int64, device=device)   # kx_status: 192 bytes
 
 
 def read_status(t, stream=None) -> A.Status:

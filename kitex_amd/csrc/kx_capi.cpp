@@ -322,13 +322,15 @@ const char* kx_strerror(int code) {
 // bytes. Everything else (other kinds, messages, repeated, maps) goes to the nested walker.
 static bool pb_flat_ok(const kx_struct_desc* structs, uint32_t nstructs) {
   if (!structs || nstructs != 1 || (structs[0].nfields && !structs[0].fields)) return false;
+  uint32_t nstr = 0;
   for (uint32_t i = 0; i < structs[0].nfields; i++) {
     const kx_field_desc& f = structs[0].fields[i];
     const bool ok_t = f.ttype == KX_T_BOOL || f.ttype == KX_T_I32 || f.ttype == KX_T_I64 ||
                       f.ttype == KX_T_DOUBLE || f.ttype == KX_T_STRING;
     if (!ok_t || (f.default_bits & 0xffff) != 0 || f.req == KX_REQ_REQUIRED) return false;
+    nstr += f.ttype == KX_T_STRING;
   }
-  return true;
+  return nstr <= 8;   // the flat proto walker's instantiations stop at 8 var slots (kx_decode.hip launch_nv)
 }
 
 int kx_schema_create(const kx_struct_desc* structs, uint32_t nstructs, kx_schema** out) {

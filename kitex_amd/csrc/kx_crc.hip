@@ -302,7 +302,7 @@ __global__ void crc_final_kernel(kx_status* st, const uint64_t* offs, uint64_t n
   const unsigned long long k = *errkey;
   *errkey = ~0ull;
   for (int j = 0; j < 3; j++) st->diag[j] = 0;
-  for (int j = 0; j < 8; j++) st->var_total[j] = 0;
+  for (int j = 0; j < 16; j++) st->var_total[j] = 0;
   if (k != ~0ull) {
     st->code = (int32_t)(k & 0xff);
     st->record = k >> 8;

@@ -55,6 +55,7 @@ constexpr int GT = 64;                   // tiles per group (one group-scan lane
 constexpr int CT = KX_CT, CW = CT / 64;  // chain pass: one workgroup, lane = group (1024 measured: the launch fails on the MI355X)
 
 constexpr uint64_t V48 = (1ull << 48) - 1;
+constexpr int KX_STATUS_VT = 16;         // kx_status.var_total slots
 constexpr uint64_t X_ERR = V48;          // chain terminated by a decode error
 constexpr uint64_t X_DONE = V48 - 1;     // chain already ended (no records to emit)
 constexpr uint64_t X_NONE = V48 - 2;     // no candidate in this tile / lane
@@ -70,6 +71,8 @@ constexpr uint64_t T_CANON = 0x100;
 // group words: group aggregate, then the global exclusive base written by the chain pass
 enum { G_ENT = 0, G_EXIT, G_CNT, G_ERRC, G_ERRP, G_VAR, G_BCNT = G_VAR + KXP_NV_MAX, G_BVAR,
        G_NF = G_BVAR + KXP_NV_MAX };
+// chain carry between chunks: E, record count, var units per slot, nstop, error | done << 1
+enum { CY_E = 0, CY_CNT, CY_VAR, CY_NSTOP = CY_VAR + KXP_NV_MAX, CY_FLAGS, CY_WORDS };
 
 // M_FRAME: framing sniff; M_THRIFT_LS: Thrift with list<struct> fields (its own instantiation, so that the
 // element loop does not change the register allocation of every other schema's kernels)
@@ -2699,7 +2702,7 @@ __global__ void __launch_bounds__(CT) chain_kernel(DecParams dp_) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const uint64_t ep = dp.epoch, ng = dp.ngroups;
   const bool chain = !dp.offsets;
-  uint64_t* const cy = dp.carry;  // chain state between chunks: E, cnt, var[8], nstop, err | done << 1
+  uint64_t* const cy = dp.carry;  // chain state between chunks (CY_*)
   if (tid == 0) {
     if (dp.chunk_first) {
       s_E = 0;  // the chain enters group 0 at offset 0
@@ -2709,12 +2712,12 @@ __global__ void __launch_bounds__(CT) chain_kernel(DecParams dp_) {
       s_err = 0;
       s_done = 0;
     } else {
-      s_E = cy[0];
-      s_cnt = cy[1];
-      for (int v = 0; v < KXP_NV_MAX; v++) s_var[v] = cy[2 + v];
-      s_nstop = cy[10];
-      s_err = (int)(cy[11] & 1);
-      s_done = (int)(cy[11] >> 1);
+      s_E = cy[CY_E];
+      s_cnt = cy[CY_CNT];
+      for (int v = 0; v < KXP_NV_MAX; v++) s_var[v] = cy[CY_VAR + v];
+      s_nstop = cy[CY_NSTOP];
+      s_err = (int)(cy[CY_FLAGS] & 1);
+      s_done = (int)(cy[CY_FLAGS] >> 1);
     }
   }
   __syncthreads();
@@ -2912,7 +2915,7 @@ __global__ void __launch_bounds__(CT) chain_kernel(DecParams dp_) {
 #pragma unroll
         for (int v = 0; v < NV; v++) {
           tot[v] = vbase[v] + var[v];
-          if (v < (int)dp.prog->nvar) st->var_total[v] = tot[v];
+          if (v < (int)dp.prog->nvar && v < KX_STATUS_VT) st->var_total[v] = tot[v];
         }
         close_slots<NV>(dp.prog, dp.cols, dp.overflow, rec, tot);
         if (MODE == M_SKIP || MODE == M_FRAME) dp.skip_out[rec] = errp;
@@ -2943,7 +2946,7 @@ __global__ void __launch_bounds__(CT) chain_kernel(DecParams dp_) {
       uint64_t vt[NV > 0 ? NV : 1];
       for (int v = 0; v < NV; v++) {
         vt[v] = s_var[v];
-        if (v < (int)dp.prog->nvar) st->var_total[v] = s_var[v];
+        if (v < (int)dp.prog->nvar && v < KX_STATUS_VT) st->var_total[v] = s_var[v];
       }
       close_slots<NV>(dp.prog, dp.cols, dp.overflow, tot, vt);
       if (MODE == M_SKIP || MODE == M_FRAME) dp.skip_out[tot] = dp.in_len;
@@ -2952,11 +2955,11 @@ __global__ void __launch_bounds__(CT) chain_kernel(DecParams dp_) {
     // emit of this chunk bounds itself by nstop: final once the chain has ended, else unbounded
     *dp.nstop = (dp.chunk_last || s_err || s_done) ? s_nstop : ~0ull;
     if (!dp.chunk_last) {
-      cy[0] = s_E;
-      cy[1] = s_cnt;
-      for (int v = 0; v < KXP_NV_MAX; v++) cy[2 + v] = s_var[v];
-      cy[10] = s_nstop;
-      cy[11] = (uint64_t)(s_err != 0) | (uint64_t)(s_done != 0) << 1;
+      cy[CY_E] = s_E;
+      cy[CY_CNT] = s_cnt;
+      for (int v = 0; v < KXP_NV_MAX; v++) cy[CY_VAR + v] = s_var[v];
+      cy[CY_NSTOP] = s_nstop;
+      cy[CY_FLAGS] = (uint64_t)(s_err != 0) | (uint64_t)(s_done != 0) << 1;
     }
   }
 }
@@ -3228,7 +3231,7 @@ __device__ __forceinline__ void emit_tile(KParams& dp, LDS uint32_t* win, uint64
 #pragma unroll
       for (int v = 0; v < NV; v++) {
         tot[v] = (v < (int)P->nvar) ? atv[v] + vs.len[v] : 0;
-        if (v < (int)P->nvar) dp.status->var_total[v] = tot[v];
+        if (v < (int)P->nvar && v < KX_STATUS_VT) dp.status->var_total[v] = tot[v];
       }
       close_slots<NV>(P, dp.cols, dp.overflow, dp.n, tot);
     }
@@ -3353,7 +3356,12 @@ __global__ void finalize_kernel(kx_status* st, unsigned long long* errkey, uint3
 
 // ---- workspace: [8] errkey u64, [16] overflow u32, [24] nstop u64, then tile words, group words,
 //      record-start slots ----
-constexpr size_t WS_HDR = 256;
+constexpr size_t WS_HDR = 512;
+// header words: [8] errkey, [16] overflow, [24] nstop, [64..) chain carry (CY_WORDS), [256..) nstop ring
+// (KX_PIPE_EV words), [448] redo count
+constexpr size_t WS_CARRY = 64, WS_RING = 256, WS_REDO = 448;
+static_assert(WS_CARRY + 8 * CY_WORDS <= WS_RING && WS_RING + 8 * KX_PIPE_EV <= WS_REDO && WS_REDO + 8 <= WS_HDR,
+              "workspace header layout");
 
 struct WsLayout {
   uint64_t ntiles, ngroups, slotcap;
@@ -3475,10 +3483,10 @@ int launch_t(const DecParams& dp0, const WsLayout& L, void* ws, hipStream_t stre
   dp.errkey = (unsigned long long*)(base + 8);
   dp.overflow = (uint32_t*)(base + 16);
   dp.nstop = (uint64_t*)(base + 24);
-  dp.nstop_ring = (uint64_t*)(base + 160);  // KX_PIPE_EV words, inside WS_HDR
-  dp.redo_n = (uint32_t*)(base + 232);      // inside WS_HDR; reset by finalize_kernel
+  dp.nstop_ring = (uint64_t*)(base + WS_RING);
+  dp.redo_n = (uint32_t*)(base + WS_REDO);  // reset by finalize_kernel
   dp.redo = (uint32_t*)(base + L.redo);
-  dp.carry = (uint64_t*)(base + 64);  // 12 words, inside WS_HDR
+  dp.carry = (uint64_t*)(base + WS_CARRY);
   dp.tdesc = (uint64_t*)(base + L.tdesc);
   dp.gdesc = (uint64_t*)(base + L.gdesc);
   dp.starts = (uint16_t*)(base + L.starts);
@@ -3629,7 +3637,7 @@ void fill_diag_flags(DecParams& dp) {
 
 }  // namespace
 
-// Split compilation: build.py compiles this file once per part (-DKX_DEC_PART=k, k = 0..5); each
+// Split compilation: build.py compiles this file once per part (-DKX_DEC_PART=k, k = 0..7); each
 // part instantiates its share of the decode kernels, part 0 also holds the host entry points.
 // Without KX_DEC_PART (one translation unit: the emulator build) everything is instantiated here.
 #ifndef KX_DEC_PART
@@ -3670,6 +3678,16 @@ KX_DEF(8, M_THRIFT_LS)
 #else
 KX_EXT(8, M_THRIFT_LS)
 #endif
+#if KX_OWNS(6)
+KX_DEF(16, M_THRIFT)
+#else
+KX_EXT(16, M_THRIFT)
+#endif
+#if KX_OWNS(7)
+KX_DEF(16, M_THRIFT_LS)
+#else
+KX_EXT(16, M_THRIFT_LS)
+#endif
 #if KX_OWNS(4)
 KX_DEF(0, M_PB) KX_DEF(1, M_PB) KX_DEF(2, M_PB)
 #else
@@ -3690,7 +3708,8 @@ static int launch_nv(const DecParams& dp, const WsLayout& L, void* ws, hipStream
       case 0: case 1: return kx_dec_launch<1, M_THRIFT_LS>(&dp, &L, ws, stream, pp);
       case 2: return kx_dec_launch<2, M_THRIFT_LS>(&dp, &L, ws, stream, pp);
       case 3: case 4: return kx_dec_launch<4, M_THRIFT_LS>(&dp, &L, ws, stream, pp);
-      default: return kx_dec_launch<8, M_THRIFT_LS>(&dp, &L, ws, stream, pp);
+      case 5: case 6: case 7: case 8: return kx_dec_launch<8, M_THRIFT_LS>(&dp, &L, ws, stream, pp);
+      default: return kx_dec_launch<16, M_THRIFT_LS>(&dp, &L, ws, stream, pp);
     }
   } else {
     switch (nvar) {
@@ -3698,7 +3717,10 @@ static int launch_nv(const DecParams& dp, const WsLayout& L, void* ws, hipStream
       case 1: return kx_dec_launch<1, MODE>(&dp, &L, ws, stream, pp);
       case 2: return kx_dec_launch<2, MODE>(&dp, &L, ws, stream, pp);
       case 3: case 4: return kx_dec_launch<4, MODE>(&dp, &L, ws, stream, pp);
-      default: return kx_dec_launch<8, MODE>(&dp, &L, ws, stream, pp);
+      case 5: case 6: case 7: case 8: return kx_dec_launch<8, MODE>(&dp, &L, ws, stream, pp);
+      default:   // 9..16 var slots: Thrift only (Kitex-Protobuf flat schemas keep <= 8, kx_capi.cpp pb_flat_ok)
+        if constexpr (MODE == M_THRIFT) return kx_dec_launch<16, MODE>(&dp, &L, ws, stream, pp);
+        else return KX_ERR_NOT_IMPLEMENTED;
     }
   }
 }

@@ -228,7 +228,7 @@ __global__ void finalize_kernel(NParams p) {
       st->consumed = p.offsets[r];
     }
   }
-  for (int v = 0; v < 8; v++) st->var_total[v] = v < (int)p.ncur ? p.totals[v] : 0;
+  for (int v = 0; v < 16; v++) st->var_total[v] = v < (int)p.ncur ? p.totals[v] : 0;
   *p.errkey = ~0ull;
 }
 

@@ -17,7 +17,7 @@
 #define KXP_MAX_FIELDS 64
 #define KXP_MAX_INST 16
 #define KXP_MAX_COLS 32
-#define KXP_NV_MAX 8  // var (BYTES / LIST) columns per schema handled by the device kernels
+#define KXP_NV_MAX 16  // var slots (BYTES / LIST columns; a LIST_BYTES column takes 2) per flat schema
 
 enum : uint8_t { KXP_K_FIXED = 1, KXP_K_BYTES = 2, KXP_K_LIST = 3, KXP_K_STRUCT = 4,
                  KXP_K_LISTB = 5,   // list/set<string>: column LIST_BYTES, slots vslot (elements) + vslot2 (bytes)

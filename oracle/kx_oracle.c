@@ -758,7 +758,7 @@ static int plan_build(plan_t* p, const kx_struct_desc* structs, uint32_t nstruct
     p->varidx[c] = p->cols[c].kind == KX_COL_FIXED ? -1 : p->nvar++;
     p->varidx2[c] = p->cols[c].kind == KX_COL_LIST_BYTES ? p->nvar++ : -1;
   }
-  if (p->nvar > 8) return KX_ERR_NOT_IMPLEMENTED;
+  if (p->nvar > 16) return KX_ERR_NOT_IMPLEMENTED;   /* KXP_NV_MAX */
   return KX_OK;
 }
 
@@ -767,13 +767,15 @@ static int plan_build(plan_t* p, const kx_struct_desc* structs, uint32_t nstruct
 static int pb_nested(const kx_struct_desc* structs, uint32_t nstructs) {
   if (!structs || nstructs == 0 || !(structs[0].reserved0 & KX_STRUCT_PROTOBUF)) return 0;
   if (nstructs != 1) return 1;
+  int nstr = 0;
   for (uint32_t i = 0; i < structs[0].nfields; i++) {
     const kx_field_desc* f = &structs[0].fields[i];
     const int t = f->ttype;
     if (!(t == KX_T_BOOL || t == KX_T_I32 || t == KX_T_I64 || t == KX_T_DOUBLE || t == KX_T_STRING)) return 1;
     if ((f->default_bits & 0xffff) != 0 || f->req == KX_REQ_REQUIRED) return 1;
+    nstr += t == KX_T_STRING;
   }
-  return 0;
+  return nstr > 8;   /* the library's flat proto path stops at 8 strings (kx_capi.cpp pb_flat_ok) */
 }
 
 int kxo_is_nested(const kx_struct_desc* structs, uint32_t nstructs) {
@@ -1208,8 +1210,8 @@ static void finish_status(const plan_t* p, const kx_columns* out, kx_status* st,
       if (cursor[vs] <= elem_lim(col) && cursor[vs2] <= arena_lim(col)) eoff_set(col, cursor[vs], cursor[vs2]);
       else overflow = 1;
     }
-    if (k < 8) st->var_total[k++] = cursor[vs];
-    if (vs2 >= 0 && k < 8) st->var_total[k++] = cursor[vs2];
+    if (k < 16) st->var_total[k++] = cursor[vs];
+    if (vs2 >= 0 && k < 16) st->var_total[k++] = cursor[vs2];
   }
   if (overflow && st->code == 0) st->code = KX_ERR_SIZE_LIMIT;
 }

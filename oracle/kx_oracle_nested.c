@@ -593,7 +593,7 @@ int kxo_nthrift_decode(const kx_struct_desc* structs, uint32_t nstructs, const u
   st->consumed = offsets ? (n ? offsets[n] : 0) : pos;
   flat_close(F, offsets ? n : r);
   if (F->overflow && st->code == 0) st->code = KX_ERR_SIZE_LIMIT;
-  for (int k = 0; k < 8; k++) st->var_total[k] = 0;
+  for (int k = 0; k < 16; k++) st->var_total[k] = 0;
   rc = st->code;
   free(F);
   free(p);

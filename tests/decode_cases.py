@@ -242,6 +242,54 @@ def case_skip(skipper, oracle):
     assert np.array_equal(to_np(got).astype(np.uint64), offs)
 
 
+# ---- R2 + base.Base (pkg/generic/json_test/idl/base.thrift:10-17): 11 var slots on the flat pipeline ----
+R2BASE_IDL = """include "base.thrift"
+struct R2Base {
+  1: i64 a1, 2: i64 a2, 3: i64 a3, 4: i64 a4, 5: i64 a5, 6: i64 a6, 7: i64 a7, 8: i64 a8,
+  9: string s9, 10: string s10,
+  255: base.Base Base,
+}
+"""
+
+
+def schema_r2_base():
+    import os
+
+    from kitex_amd import idl
+    d = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "idl")
+    return idl.to_schema(idl.parse_idl(R2BASE_IDL, include_dirs=[d]).struct("R2Base"))
+
+
+def r2_base_record(oracle, rng, i):
+    P = oracle.prim
+    fields = [(A.T_I64, f, i64(oracle, int(rng.integers(-2**63, 2**63 - 1)))) for f in range(1, 9)]
+    fields += [(A.T_STRING, f, sbytes(oracle, bytes(rng.integers(97, 123, size=int(rng.integers(0, 40)),
+                                                                 dtype=np.uint8)))) for f in (9, 10)]
+    base = [(A.T_STRING, 1, sbytes(oracle, b"log-%d" % i)), (A.T_STRING, 2, sbytes(oracle, b"caller.svc")),
+            (A.T_STRING, 3, sbytes(oracle, b"10.0.%d.%d:8888" % (i % 256, i % 7))),
+            (A.T_STRING, 4, sbytes(oracle, b"" if i % 3 else b"client"))]
+    if i % 2:
+        base.append((A.T_STRUCT, 5, rec_bytes(oracle, [(A.T_BOOL, 1, P("kxo_write_bool", i % 4 == 1)),
+                                                       (A.T_STRING, 2, sbytes(oracle, b"env%d" % (i % 5)))])))
+    k = i % 4
+    if k:
+        m = P("kxo_write_map_begin", A.T_STRING, A.T_STRING, k)
+        for j in range(k):
+            m += sbytes(oracle, b"k%d" % j) + sbytes(oracle, b"v%d-%d" % (i, j))
+        base.append((A.T_MAP, 6, m))
+    if i % 5 == 0:
+        base = base[::-1]                     # some records off the canonical order: the walk path
+    fields.append((A.T_STRUCT, 255, rec_bytes(oracle, base)))
+    return rec_bytes(oracle, fields)
+
+
+def case_r2_base(dec, oracle, mode, n=3000):
+    sch = schema_r2_base()
+    rng = np.random.default_rng(8)
+    wire, offs = concat([r2_base_record(oracle, rng, i) for i in range(n)])
+    check_decode(dec, oracle, sch, wire, n, offsets=offs if mode == "offsets" else None)
+
+
 # ---- split points (kx_thrift_split_points: SURVEY.md §8e pass A) ------------------------------------
 def expected_points(offs, n, parts):
     return np.array([int(offs[(k * n) // parts]) if k < parts else int(offs[n]) for k in range(parts + 1)],

@@ -106,6 +106,14 @@ def test_emu_skip(edec, oracle):
     DC.case_skip(lambda wire, n: emu.skip(wire, n)[1], oracle)
 
 
+@pytest.mark.parametrize("mode", ["concat", "offsets"])
+def test_emu_r2_base_flat(edec, oracle, mode):
+    """R2 + base.Base: 11 var slots on the flat pipeline (the 16-slot instantiation)"""
+    from kitex_amd.codec import DeviceSchema
+    assert not DeviceSchema(DC.schema_r2_base()).nested
+    DC.case_r2_base(edec, oracle, mode, n=1500)
+
+
 def _emu_split(sch, wire, n, parts, skip=False):
     rc, pts, st = emu.split_points(None if skip else sch, wire, n, parts)
     assert rc == 0

@@ -193,6 +193,15 @@ def test_skip_batch_matches_oracle(torch, dev, oracle):
     DC.case_skip(lambda wire, n: cdc.Skip(torch.from_numpy(wire).to(dev), n), oracle)
 
 
+@pytest.mark.parametrize("mode", ["concat", "offsets"])
+def test_r2_base_flat_path(torch, dev, oracle, mode):
+    """R2 + base.Base (base.thrift:10-17): 11 var slots stay on the flat tile pipeline (kx_schema_is_nested
+    == 0) and decode like the oracle"""
+    from kitex_amd.codec import DeviceSchema
+    assert not DeviceSchema(DC.schema_r2_base()).nested
+    DC.case_r2_base(GpuDecoder(torch, dev), oracle, mode, n=20000)
+
+
 def _gpu_split(torch, dev):
     from kitex_amd.codec import ThriftCodec, read_status, status_tensor
     from kitex_amd._lib import lib
