@@ -551,6 +551,69 @@ def extras(args, r2, dev, local):
         return {"ranges": b.n, "ranges_per_s": b.n * steps / t, "ms_per_step": t / steps * 1e3, "sample_ok": ok,
                 "roofline": roofline(alg, avg, "crc32c")}
 
+    def nested_entry(n=1 << 20, k=4096):
+        """config-3-style nested records: baseline.thrift's Nesting (NestingMethod's request: list<Simple>,
+        map<string,Simple>, map<i32,i64>, list<string>, ...; tests/golden/idl/baseline.thrift) on the nested
+        walker (lane = record), decode + encode. k distinct host-written records tiled to n on the device."""
+        import numpy as np
+
+        from kitex_amd import idl, synth
+        from kitex_amd.codec import ThriftCodec, read_status
+        from kitex_amd.columns import alloc_device
+        doc = idl.parse_idl(os.path.join(os.path.dirname(os.path.abspath(__file__)), "tests", "golden", "idl",
+                                         "baseline.thrift"))
+        sch = idl.to_schema(doc.struct("Nesting"))
+        cdc = ThriftCodec(sch, device=local)
+        ds = cdc.dschema
+        one = np.frombuffer(b"".join(synth.thrift_records(sch, k, seed=7)), dtype=np.uint8).copy()
+        wire = torch.from_numpy(one).to(dev).repeat(n // k)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        ev[0].record()
+        units = cdc.DecodeSizes(wire, n)
+        ev[1].record()
+        torch.cuda.synchronize()
+        sizes_ms = ev[0].elapsed_time(ev[1])
+        vc, ec, sc = units[0::3], units[1::3], units[2::3]
+        outc = alloc_device(ds.infos, n, vc, ds.npresence, dev, elem_caps=ec, sub_caps=sc)
+        st = status_tensor(dev)
+
+        def dec():
+            cdc.Unmarshal(wire, n, out=outc, var_caps=vc, raise_on_error=False, status=st)
+        t, per = time_steps(dec, steps, warm, 1, dev)
+        s = read_status(st)
+        ok = s.code == 0 and s.n_records == n and s.consumed == wire.numel()
+
+        def tensors(cs):
+            for c in cs.cols:
+                yield from (c if isinstance(c, tuple) else (c,))
+            if cs.presence is not None:
+                yield cs.presence
+        out_bytes = sum(x.numel() * x.element_size() for x in tensors(outc))
+        avg = sum(per) / len(per) / 1e3
+        res = {"records": n, "distinct_records": k, "wire_bytes_per_record": wire.numel() / n,
+               "decode": {"records_per_s": n * steps / t, "ms_per_step": t / steps * 1e3, "verified": ok,
+                          "sizes_pass_ms": sizes_ms,
+                          "roofline": roofline(wire.numel() + out_bytes, avg, "nested decode (measure + write)")}}
+        w2, _ = cdc.Marshal(outc)
+        buf = torch.empty_like(w2)
+        st2 = status_tensor(dev)
+
+        def enc():
+            cdc.Marshal(outc, with_offsets=False, out=buf, status=st2, check_status=False)
+        t, per = time_steps(enc, steps, warm, 1, dev)
+        avg = sum(per) / len(per) / 1e3
+        back = cdc.Unmarshal(buf, n, raise_on_error=False)
+        eq = all(bool(torch.equal(a, b)) for a, b in zip(tensors(outc), tensors(back.columns)))
+        res["encode"] = {"records_per_s": n * steps / t, "ms_per_step": t / steps * 1e3,
+                         "round_trip_equal": eq and bool(torch.equal(buf, w2)),
+                         "roofline": roofline(out_bytes + buf.numel(), avg, "nested encode (size + write)")}
+        return res
+
+    try:
+        out["nested_decode_encode"] = nested_entry()
+        torch.cuda.empty_cache()
+    except Exception as e:
+        out["nested_decode_encode"] = {"error": repr(e)}
     try:
         if r2 is not None:
             out["r2_encode"] = {"records": r2.n, **encode_entry(r2)}
@@ -570,6 +633,17 @@ def extras(args, r2, dev, local):
                                      "decode (known offsets)")
             out["r2_decode_offsets"] = {"records": bo.n, **e}
             del bo
+            torch.cuda.empty_cache()
+            # known offsets + string views: no arena to lay out, the emit pass runs alone
+            bov = Batch("r2", r2.n, dev, 0, "offsets", local, views=True)
+            e = decode_entry(bov)
+            avg = e["roofline"]["avg_launch_ms"] / 1e3
+            e["roofline"] = roofline(bov.in_bytes + 8 * (bov.n + 1) + bov.out_bytes_per_record() * bov.n, avg,
+                                     "decode (known offsets, views: emit pass alone)")
+            e["roofline"]["read_only_frac"] = bov.in_bytes / avg / 1e9 / HBM_PEAK_GBS
+            out["r2_decode_offsets_views"] = {"records": bov.n, "out_bytes_per_record": bov.out_bytes_per_record(),
+                                              **e}
+            del bov
             torch.cuda.empty_cache()
         b3 = Batch("r3", 4 << 20, dev, 0, "concat", local)
         out["r3_decode"] = {"records": b3.n, "wire_bytes_per_record": b3.in_bytes / b3.n, **decode_entry(b3)}

@@ -398,3 +398,71 @@ def gen_r3_torch(n: int, device, start: int = 0, maxlist: int = 128, maxtag: int
 
 
 TORCH_GENERATORS = {"r1": gen_r1_torch, "r2": gen_r2_torch, "r3": gen_r3_torch, "pf": gen_pf_torch}
+
+
+# ---------------------------------------------------------------------------------------------
+# Any schema: k distinct Thrift-binary records written on the host (the nested-path bench input, tiled
+# on the device). Fields in IDL order, every field present; containers of 0..maxn entries, strings of
+# 0..maxs bytes. numpy's PCG64 stream seeded with `seed`.
+# ---------------------------------------------------------------------------------------------
+def _tw_value(out: bytearray, t: int, node, child, rng, maxn: int, maxs: int, depth: int):
+    import struct
+    if t == A.T_BOOL:
+        out.append(int(rng.integers(0, 2)))
+    elif t == A.T_BYTE:
+        out += struct.pack(">b", int(rng.integers(-128, 128)))
+    elif t == A.T_I16:
+        out += struct.pack(">h", int(rng.integers(-2**15, 2**15)))
+    elif t == A.T_I32:
+        out += struct.pack(">i", int(rng.integers(-2**31, 2**31)))
+    elif t == A.T_I64:
+        out += struct.pack(">q", int(rng.integers(-2**63, 2**63 - 1)))
+    elif t == A.T_DOUBLE:
+        out += struct.pack(">d", float(rng.standard_normal()))
+    elif t == A.T_STRING:
+        s = rng.integers(97, 123, size=int(rng.integers(0, maxs + 1)), dtype=np.uint8).tobytes()
+        out += struct.pack(">I", len(s)) + s
+    elif t == A.T_STRUCT:
+        _tw_struct(out, child, rng, maxn, maxs, depth + 1)
+    elif t in (A.T_LIST, A.T_SET):
+        et, enode, echild = _tw_sub(node.elem, node.child)
+        k = int(rng.integers(0, maxn + 1)) if depth < 3 else 0
+        out += struct.pack(">bi", et, k)
+        for _ in range(k):
+            _tw_value(out, et, enode, echild, rng, maxn, maxs, depth)
+    elif t == A.T_MAP:
+        kt, knode, kchild = _tw_sub(node.elem, None)
+        vt, vnode, vchild = _tw_sub(node.val, node.child)
+        k = int(rng.integers(0, maxn + 1)) if depth < 3 else 0
+        out += struct.pack(">bbi", kt, vt, k)
+        for _ in range(k):
+            _tw_value(out, kt, knode, kchild, rng, maxn, maxs, depth)
+            _tw_value(out, vt, vnode, vchild, rng, maxn, maxs, depth)
+    else:
+        raise ValueError(f"type {t}")
+
+
+def _tw_sub(sub, child):
+    """(ttype, container node, struct) of a container's element / key / value"""
+    from .schema import Field
+    if isinstance(sub, Field):
+        return sub.ttype, sub, sub.child
+    return sub, None, child
+
+
+def _tw_struct(out: bytearray, st, rng, maxn: int, maxs: int, depth: int):
+    import struct
+    for f in st.fields:
+        out += struct.pack(">bh", f.ttype, f.id)
+        _tw_value(out, f.ttype, f, f.child, rng, maxn, maxs, depth)
+    out.append(A.T_STOP)
+
+
+def thrift_records(schema, k: int, seed: int = 1, maxn: int = 4, maxs: int = 24) -> List[bytes]:
+    rng = np.random.default_rng(seed)
+    recs = []
+    for _ in range(k):
+        out = bytearray()
+        _tw_struct(out, schema.root, rng, maxn, maxs, 0)
+        recs.append(bytes(out))
+    return recs
