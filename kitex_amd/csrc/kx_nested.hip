@@ -46,6 +46,7 @@ struct NParams {
   kx_status* status;
   uint64_t nblk;
   uint32_t ncur;
+  uint32_t lstride, wstride;  // LDS-cursor kernels: words per lane (measure: ncur + nsnap; write: 2 ncur + nsnap)
   bool sizes_only;            // kx_thrift_decode_sizes: no column is written
 };
 
@@ -68,11 +69,8 @@ __device__ __forceinline__ int extent(const NParams& p, uint64_t r, uint64_t* a,
   return (*a > *b || *b > p.in_len) ? KX_ERR_INVALID_ARG : 0;
 }
 
-__global__ void __launch_bounds__(NT) measure_kernel(NParams p) {
-  const uint64_t r = (uint64_t)blockIdx.x * NT + threadIdx.x;
-  if (r >= p.n) return;
+__device__ __forceinline__ void measure_record(const NParams& p, uint64_t r, uint64_t* cur, uint64_t* snap) {
   const KxnProgram& P = *p.P;
-  uint64_t cur[CUR], snap[SNAP];
   for (uint32_t k = 0; k < p.ncur; k++) cur[k] = 0;
   uint64_t a = 0, b = 0, used = 0;
   int rc = extent(p, r, &a, &b);
@@ -87,6 +85,26 @@ __global__ void __launch_bounds__(NT) measure_kernel(NParams p) {
     if (rc) atomicMin(p.errkey, (unsigned long long)((r << 8) | (uint64_t)(rc & 0xff)));
   }
   for (uint32_t k = 0; k < p.ncur; k++) p.counts[(uint64_t)k * p.n + r] = rc ? 0u : (uint32_t)cur[k];
+}
+
+// cursors and snapshots in per-lane private (scratch) arrays
+__global__ void __launch_bounds__(NT) measure_kernel(NParams p) {
+  const uint64_t r = (uint64_t)blockIdx.x * NT + threadIdx.x;
+  if (r >= p.n) return;
+  uint64_t cur[CUR], snap[SNAP];
+  measure_record(p, r, cur, snap);
+}
+
+// Cursors and snapshots in LDS (one wave per workgroup, p.lstride words per lane): the scratch arrays of
+// every resident lane (ncur + nsnap words, touched at data-dependent indices) overflow L2 at full
+// occupancy, so every cursor access of the walk went to the Infinity Cache; LDS keeps them on the CU.
+constexpr int NL = 64;
+__global__ void __launch_bounds__(NL) measure_lds_kernel(NParams p) {
+  extern __shared__ uint64_t lds_words[];
+  const uint64_t r = (uint64_t)blockIdx.x * NL + threadIdx.x;
+  if (r >= p.n) return;
+  uint64_t* cur = lds_words + (size_t)threadIdx.x * p.lstride;
+  measure_record(p, r, cur, cur + p.ncur);
 }
 
 __device__ __forceinline__ uint64_t wave_incl(uint64_t v, int lane) {
@@ -167,17 +185,17 @@ __global__ void check_kernel(NParams p) {
   *p.flag = over ? 1u : 0u;
 }
 
-__global__ void __launch_bounds__(NT) write_kernel(NParams p) {
-  __shared__ uint64_t sh[NT / 64];
-  if (*p.flag) return;
+// one block of RB records: per record the workgroup scan of every cursor's counts gives the lane's
+// bases; carry: the block's running base per cursor (uniform)
+template <int T>
+__device__ __forceinline__ void write_block(const NParams& p, uint64_t* carry, uint64_t* cur, uint64_t* lim,
+                                            uint64_t* snap, uint64_t* sh) {
   const KxnProgram& P = *p.P;
   const uint64_t b = blockIdx.x;
-  uint64_t carry[CUR];
   for (uint32_t k = 0; k < p.ncur; k++) carry[k] = p.bsum[(uint64_t)k * p.nblk + b];
-  for (int j = 0; j < RB / NT; j++) {
-    const uint64_t r = b * RB + (uint64_t)j * NT + threadIdx.x;
+  for (int j = 0; j < RB / T; j++) {
+    const uint64_t r = b * RB + (uint64_t)j * T + threadIdx.x;
     const bool act = r < p.n;
-    uint64_t cur[CUR], lim[CUR], snap[SNAP];
     for (uint32_t k = 0; k < p.ncur; k++) {
       const uint64_t x = act ? p.counts[(uint64_t)k * p.n + r] : 0;
       uint64_t tot;
@@ -197,6 +215,24 @@ __global__ void __launch_bounds__(NT) write_kernel(NParams p) {
     }
     if (p.record_status && !p.concat) p.record_status[r] = rc == 0xff ? 0 : rc;
   }
+}
+
+__global__ void __launch_bounds__(NT) write_kernel(NParams p) {
+  __shared__ uint64_t sh[NT / 64];
+  if (*p.flag) return;
+  uint64_t carry[CUR], cur[CUR], lim[CUR], snap[SNAP];
+  write_block<NT>(p, carry, cur, lim, snap, sh);
+}
+
+// LDS per lane: cur[ncur], lim[ncur], snap[nsnap] (p.wstride words); the block carry stays private (its
+// index is uniform: coalesced)
+__global__ void __launch_bounds__(NL) write_lds_kernel(NParams p) {
+  __shared__ uint64_t sh[1];
+  extern __shared__ uint64_t lds_words[];
+  if (*p.flag) return;
+  uint64_t carry[CUR];
+  uint64_t* lane = lds_words + (size_t)threadIdx.x * p.wstride;
+  write_block<NL>(p, carry, lane, lane + p.ncur, lane + 2 * p.ncur, sh);
 }
 
 __global__ void finalize_kernel(NParams p) {
@@ -407,8 +443,26 @@ int kx_launch_nested_decode(const KxnProgram* dprog, const KxnProgram& hprog, co
   } else {
     p.offsets = offsets;
   }
-  const unsigned gm = (unsigned)((n + NT - 1) / NT);
-  hipLaunchKernelGGL(measure_kernel, dim3(gm), dim3(NT), 0, stream, p);
+  // cursors in LDS unless KX_NESTED_LDS=0 (or a lane's words exceed what one wave may hold)
+  static int lds_env = -1;
+  if (lds_env < 0) { const char* e = getenv("KX_NESTED_LDS"); lds_env = e ? atoi(e) : 1; }
+  p.lstride = (hprog.ncur + hprog.nsnap) | 1u;          // odd: lanes spread over the LDS banks
+  p.wstride = (2 * hprog.ncur + hprog.nsnap) | 1u;
+  const size_t lm = (size_t)NL * p.lstride * 8, lw = (size_t)NL * p.wstride * 8;
+  const bool use_lds = lds_env && lw <= 120 * 1024;
+  if (use_lds) {
+    static bool attr = false;
+    if (!attr) {
+      KX_HIP_CHECK(hipFuncSetAttribute((const void*)measure_lds_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       120 * 1024));
+      KX_HIP_CHECK(hipFuncSetAttribute((const void*)write_lds_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       120 * 1024));
+      attr = true;
+    }
+    hipLaunchKernelGGL(measure_lds_kernel, dim3((unsigned)((n + NL - 1) / NL)), dim3(NL), lm, stream, p);
+  } else {
+    hipLaunchKernelGGL(measure_kernel, dim3((unsigned)((n + NT - 1) / NT)), dim3(NT), 0, stream, p);
+  }
   KX_HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(bsum_kernel, dim3((unsigned)p.nblk, hprog.ncur), dim3(NT), 0, stream, p);
   KX_HIP_CHECK(hipGetLastError());
@@ -423,7 +477,8 @@ int kx_launch_nested_decode(const KxnProgram* dprog, const KxnProgram& hprog, co
   }
   hipLaunchKernelGGL(check_kernel, dim3(1), dim3(64), 0, stream, p);
   KX_HIP_CHECK(hipGetLastError());
-  hipLaunchKernelGGL(write_kernel, dim3((unsigned)p.nblk), dim3(NT), 0, stream, p);
+  if (use_lds) hipLaunchKernelGGL(write_lds_kernel, dim3((unsigned)p.nblk), dim3(NL), lw, stream, p);
+  else hipLaunchKernelGGL(write_kernel, dim3((unsigned)p.nblk), dim3(NT), 0, stream, p);
   KX_HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(64), 0, stream, p);
   KX_HIP_CHECK(hipGetLastError());
