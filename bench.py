@@ -609,6 +609,60 @@ def extras(args, r2, dev, local):
                          "roofline": roofline(out_bytes + buf.numel(), avg, "nested encode (size + write)")}
         return res
 
+    def frames_entry(n=16 << 20):
+        """kx_thrift_decode_frames over a socket buffer of n TTHeader frames (R1 request messages) whose
+        str-info carries "crc32c" (default_codec.go:205-209, validate.go:183-217), CRC32Check off and on.
+        With the check fused into the frame scan's emit pass the payloads are not read a second time."""
+        from kitex_amd import schema as S
+        from kitex_amd import synth
+        from kitex_amd.codec import CRC32PayloadValidator, ThriftCodec
+        cdc = ThriftCodec(S.schema_r1(), device=local)
+        src = synth.TORCH_GENERATORS["r1"](n, dev)
+        msgs, moffs = cdc.MarshalMessages(src, "Echo", torch.zeros(n, dtype=torch.int32, device=dev))
+        M = msgs.numel() // n
+        assert M * n == msgs.numel()
+        crc = CRC32PayloadValidator(local).Generate(msgs, moffs)
+        # TTHeader: length, magic 0x1000 + flags, seqid, header size / 4; protocol 0 (binary), no transforms,
+        # one string KV "crc32c" -> 8 lowercase hex digits, zero padding to a multiple of 4
+        info = bytes([0, 0, 1, 0, 1, 0, 6]) + b"crc32c" + bytes([0, 8]) + b"0" * 8
+        info += bytes(-len(info) % 4)
+        H = 14 + len(info)
+        hdr = (H + M - 4).to_bytes(4, "big") + bytes([0x10, 0, 0, 0]) + bytes(4) + (len(info) // 4).to_bytes(2, "big")
+        tmpl = torch.tensor(list(hdr + info), dtype=torch.uint8, device=dev)
+        fr = torch.empty((n, H + M), dtype=torch.uint8, device=dev)
+        fr[:, :H] = tmpl
+        nib = (crc[:, None] >> torch.arange(28, -4, -4, device=dev)) & 0xF
+        fr[:, H - len(info) + 15:H - len(info) + 23] = torch.where(nib < 10, nib + 48, nib + 87).to(torch.uint8)
+        fr[:, H:] = msgs.view(n, M)
+        wire = fr.view(-1)
+        del fr, msgs, nib
+        res = {"frames": n, "frame_bytes": H + M}
+        for chk in (False, True):
+            last = {}
+
+            def dec():
+                last["r"] = cdc.UnmarshalFrames(wire, n, raise_on_error=False, crc32_check=chk)
+            t, per = time_steps(dec, steps, warm, 1, dev)
+            r = last["r"]
+            s = r.read_status()
+            ok = s.code == 0 and s.n_records == n and bool(torch.equal(r.columns.cols[0], src.cols[0]))
+            res["crc32_check_on" if chk else "crc32_check_off"] = {
+                "ms_per_step": t / steps * 1e3, "frames_per_s": n * steps / t, "verified": ok,
+                "roofline": roofline(wire.numel() + 8 * 8 * n, sum(per) / len(per) / 1e3,
+                                     "frame scan + message decode" + (" + fused CRC32C check" if chk else ""))}
+        res["check_overhead"] = res["crc32_check_on"]["ms_per_step"] / res["crc32_check_off"]["ms_per_step"] - 1
+        bad = wire.clone()
+        bad[(n // 2) * (H + M) + H + M - 3] ^= 1   # one payload byte of frame n/2
+        rb = cdc.UnmarshalFrames(bad, n, raise_on_error=False, crc32_check=True)
+        sb = rb.read_status()
+        res["tamper_detected"] = sb.code == 11 and sb.record == n // 2
+        return res
+
+    try:
+        out["frames_crc32c"] = frames_entry()
+        torch.cuda.empty_cache()
+    except Exception as e:
+        out["frames_crc32c"] = {"error": repr(e)}
     try:
         out["nested_decode_encode"] = nested_entry()
         torch.cuda.empty_cache()

@@ -744,9 +744,9 @@ static int ensure_fws(kx_ctx* c, size_t bytes, hipStream_t stream) {
   return KX_OK;
 }
 
-int kx_frame_scan(kx_ctx* c, const uint8_t* in, uint64_t in_len, uint64_t n, uint64_t max_payload,
-                  uint64_t* frame_offsets, uint64_t* payload_start, uint64_t* payload_end, uint8_t* kinds,
-                  kx_status* status, void* stream) {
+static int frame_scan(kx_ctx* c, const uint8_t* in, uint64_t in_len, uint64_t n, uint64_t max_payload,
+                      uint64_t* frame_offsets, uint64_t* payload_start, uint64_t* payload_end, uint8_t* kinds,
+                      kx_status* status, void* stream, uint8_t* crc_codes) {
   if (!c || !status || !frame_offsets || (n && (!payload_start || !payload_end)) || (!in && in_len))
     return KX_ERR_INVALID_ARG;
   int rc = set_device(c);
@@ -760,7 +760,14 @@ int kx_frame_scan(kx_ctx* c, const uint8_t* in, uint64_t in_len, uint64_t n, uin
   uint64_t epoch = 0;
   if ((rc = ensure_ws(c, kx_skip_ws_bytes(in_len, n), st, &epoch))) return rc;
   return kx_launch_frames(in, in_len, n, max_payload, frame_offsets, payload_start, payload_end, kinds, status, c->ws,
-                          c->ws_size, epoch, st);
+                          c->ws_size, epoch, st, false, nullptr, nullptr, nullptr, nullptr, crc_codes);
+}
+
+int kx_frame_scan(kx_ctx* c, const uint8_t* in, uint64_t in_len, uint64_t n, uint64_t max_payload,
+                  uint64_t* frame_offsets, uint64_t* payload_start, uint64_t* payload_end, uint8_t* kinds,
+                  kx_status* status, void* stream) {
+  return frame_scan(c, in, in_len, n, max_payload, frame_offsets, payload_start, payload_end, kinds, status, stream,
+                    nullptr);
 }
 
 // CRC32C scratch: the launcher's error key (8 bytes, ~0 = none; its final kernel re-arms it)
@@ -821,11 +828,17 @@ static int decode_frames(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint6
   uint64_t* fo = frame_offsets ? frame_offsets : (uint64_t*)(f + fo_at);
   uint64_t* ps = (uint64_t*)(f + ps_at);
   uint64_t* pe = (uint64_t*)(f + pe_at);
-  if ((rc = kx_frame_scan(c, in, in_len, n, max_payload, fo, ps, pe, kinds, pre, stream))) return rc;
-  uint8_t* vrc = nullptr;
-  if (c->crc32c_check) {  // DecodeMeta's payloadChecksumValidate (default_codec.go:205-209)
+  // DecodeMeta's payloadChecksumValidate (default_codec.go:205-209): fused into the frame scan's emit pass
+  // (the payload is checked from the LDS window the scan already holds); KX_CRC_FUSED=0 runs the separate
+  // checksum kernel after the scan instead
+  static int fused_env = -1;
+  if (fused_env < 0) { const char* e = getenv("KX_CRC_FUSED"); fused_env = e ? atoi(e) : 1; }
+  uint8_t* vrc = c->crc32c_check ? (uint8_t*)(f + vr_at) : nullptr;
+  const bool fused = vrc && fused_env;
+  if ((rc = frame_scan(c, in, in_len, n, max_payload, fo, ps, pe, kinds, pre, stream, fused ? vrc : nullptr)))
+    return rc;
+  if (vrc && !fused) {
     if ((rc = ensure_cws(c, st))) return rc;
-    vrc = (uint8_t*)(f + vr_at);
     if ((rc = kx_launch_crc32c(in, in_len, fo, n, true, pre, nullptr, vrc, (kx_status*)(f + 128), c->cws, st)))
       return rc;
   }

@@ -23,10 +23,10 @@
 #include <hip/hip_runtime.h>
 
 #include "kx_internal.h"
+#include "kx_crc.h"
 
 namespace {
 
-constexpr uint32_t POLY = 0x82F63B78u;  // Castagnoli, reflected
 constexpr int CT = 256;                  // threads per workgroup
 constexpr uint64_t CHUNK = 4096;         // per-lane chunk of a wave-cooperative range
 constexpr uint64_t LARGE = 2048;         // longer ranges are folded by the whole wave
@@ -59,7 +59,7 @@ __device__ __forceinline__ uint32_t multmodp(uint32_t a, uint32_t b) {
       if ((a & (m - 1)) == 0) break;
     }
     m >>= 1;
-    b = b & 1 ? (b >> 1) ^ POLY : b >> 1;
+    b = b & 1 ? (b >> 1) ^ KX_CRC_POLY : b >> 1;
   }
   return p;
 }
@@ -78,7 +78,7 @@ __device__ __forceinline__ uint32_t x2nmodp(const Tabs& T, uint64_t n, unsigned 
 __device__ void build_tabs(Tabs& T) {
   const int t = threadIdx.x;
   uint32_t c = (uint32_t)t;
-  for (int k = 0; k < 8; k++) c = c & 1 ? (c >> 1) ^ POLY : c >> 1;
+  for (int k = 0; k < 8; k++) c = c & 1 ? (c >> 1) ^ KX_CRC_POLY : c >> 1;
   T.t[0][t] = c;
   if (t == 0) {
     uint32_t p = 1u << 30;  // x^1
@@ -93,20 +93,6 @@ __device__ void build_tabs(Tabs& T) {
   const uint32_t K = x2nmodp(T, CHUNK, 3);
   for (int j = 0; j < 4; j++) T.s[j][t] = multmodp(K, (uint32_t)t << (8 * j));
   __syncthreads();
-}
-
-// c after feeding the k (0..8) low bytes of d (little-endian; bytes >= k of d must be zero): the
-// slicing-by-k form of the byte-at-a-time update, k table lookups, no dependent chain between them
-__device__ __forceinline__ uint32_t upd_k(const Tabs& T, uint32_t c, uint64_t d, uint32_t k) {
-  const uint32_t xl = c ^ (uint32_t)d, xh = (uint32_t)(d >> 32);
-  uint32_t r = k == 0 ? c : k < 4 ? xl >> (8 * k) : 0u;
-#pragma unroll
-  for (uint32_t j = 0; j < 4; j++)
-    if (j < k) r ^= T.t[k - 1 - j][(xl >> (8 * j)) & 0xff];
-#pragma unroll
-  for (uint32_t j = 0; j < 4; j++)
-    if (j + 4 < k) r ^= T.t[k - 5 - j][(xh >> (8 * j)) & 0xff];
-  return r;
 }
 
 __device__ __forceinline__ uint64_t low_bytes(uint64_t v, uint32_t k) { return k >= 8 ? v : v & ((1ull << (8 * k)) - 1); }
@@ -134,8 +120,8 @@ __device__ __forceinline__ uint32_t crc_run(const Tabs& T, const uint8_t* in, ui
     if (s >= 64) { q0 = q1 >> (s - 64); q1 = 0; }
     else if (s) { q0 = (q0 >> s) | (q1 << (64 - s)); q1 >>= s; }
     const uint32_t k = hi - lo, k1 = k < 8 ? k : 8u, k2 = k - k1;
-    c = upd_k(T, c, low_bytes(q0, k1), k1);
-    c = upd_k(T, c, low_bytes(q1, k2), k2);
+    c = kx_crc_upd_k(T.t, c, low_bytes(q0, k1), k1);
+    c = kx_crc_upd_k(T.t, c, low_bytes(q1, k2), k2);
     g += 16;
     if (g >= pb) break;
     v0 = v1;
@@ -148,87 +134,11 @@ __device__ __forceinline__ uint32_t shift_chunk(const Tabs& T, uint32_t c) {
   return T.s[0][c & 0xff] ^ T.s[1][(c >> 8) & 0xff] ^ T.s[2][(c >> 16) & 0xff] ^ T.s[3][c >> 24];
 }
 
-__device__ __forceinline__ uint32_t be32g(const uint8_t* p) {
-  return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
-}
-__device__ __forceinline__ uint32_t be16g(const uint8_t* p) { return ((uint32_t)p[0] << 8) | p[1]; }
-
-__device__ __forceinline__ int hexval(uint32_t ch) {
-  return ch >= '0' && ch <= '9' ? (int)(ch - '0') : ch >= 'a' && ch <= 'f' ? (int)(ch - 'a' + 10) : -1;
-}
-
-// Expected value of frame f (TTHeader at [f, in_len)): want = 0 no check (not a TTHeader frame, no
-// "crc32c" key, or an empty value), 1 compare with exp, 2 a value that no lowercase 8-digit hex CRC can
-// equal (always fails). Payload range [*a, *b). Header layout as kx_decode.hip frame_one / the oracle.
-__device__ int frame_expect(const uint8_t* in, uint64_t in_len, uint64_t f, uint64_t* a, uint64_t* b, int* want,
-                            uint32_t* exp) {
-  *want = 0;
-  *a = *b = f;
-  if (f > in_len || in_len - f < 14) return KX_OK;  // too short for a TTHeader: not one (the scan decides)
-  const uint8_t* h = in + f;
-  if ((be32g(h + 4) >> 16) != 0x1000u) return KX_OK;  // IsTTHeader
-  const uint64_t len = (uint64_t)be32g(h) + 4, hs = (uint64_t)be16g(h + 12) * 4;
-  if (hs < 2 || 14 + hs > len || len > in_len - f) return KX_ERR_UNKNOWN_PROTOCOL;
-  *a = f + 14 + hs;
-  *b = f + len;
-  const uint8_t* info = h + 14;
-  uint64_t i = 2 + (uint64_t)info[1];
-  if (i > hs) return KX_ERR_UNKNOWN_PROTOCOL;
-  while (i < hs) {
-    const uint32_t id = info[i++];
-    if (id == 0x00) continue;
-    if (id == 0x01) {  // string KVs: the last "crc32c" wins (a map assignment per pair)
-      if (i + 2 > hs) return KX_ERR_UNKNOWN_PROTOCOL;
-      const uint32_t k = be16g(info + i);
-      i += 2;
-      for (uint32_t j = 0; j < k; j++) {
-        if (i + 2 > hs) return KX_ERR_UNKNOWN_PROTOCOL;
-        const uint64_t kl = be16g(info + i);
-        if (i + 2 + kl + 2 > hs) return KX_ERR_UNKNOWN_PROTOCOL;
-        const uint8_t* key = info + i + 2;
-        i += 2 + kl;
-        const uint64_t vl = be16g(info + i);
-        if (i + 2 + vl > hs) return KX_ERR_UNKNOWN_PROTOCOL;
-        const uint8_t* v = info + i + 2;
-        i += 2 + vl;
-        if (kl == 6 && key[0] == 'c' && key[1] == 'r' && key[2] == 'c' && key[3] == '3' && key[4] == '2' &&
-            key[5] == 'c') {
-          if (vl == 0) {
-            *want = 0;
-          } else {
-            uint32_t x = 0;
-            bool ok = vl == 8;
-            for (int q = 0; ok && q < 8; q++) {
-              const int d = hexval(v[q]);
-              ok = d >= 0;
-              x = (x << 4) | (uint32_t)(d & 15);
-            }
-            *want = ok ? 1 : 2;
-            *exp = x;
-          }
-        }
-      }
-    } else if (id == 0x10) {  // int KVs: (u16 key, u16-length string)
-      if (i + 2 > hs) return KX_ERR_UNKNOWN_PROTOCOL;
-      const uint32_t k = be16g(info + i);
-      i += 2;
-      for (uint32_t j = 0; j < k; j++) {
-        if (i + 4 > hs) return KX_ERR_UNKNOWN_PROTOCOL;
-        const uint64_t l = be16g(info + i + 2);
-        if (i + 4 + l > hs) return KX_ERR_UNKNOWN_PROTOCOL;
-        i += 4 + l;
-      }
-    } else if (id == 0x11) {  // ACL token
-      if (i + 2 > hs) return KX_ERR_UNKNOWN_PROTOCOL;
-      const uint64_t l = be16g(info + i);
-      if (i + 2 + l > hs) return KX_ERR_UNKNOWN_PROTOCOL;
-      i += 2 + l;
-    } else {
-      return KX_ERR_UNKNOWN_PROTOCOL;
-    }
-  }
-  return KX_OK;
-}
+// the frame's bytes straight from global memory
+struct GlobalBytes {
+  const uint8_t* in;
+  __device__ __forceinline__ uint32_t operator()(uint64_t p) const { return in[p]; }
+};
 
 __device__ __forceinline__ void crc_block(const CrcParams& cp, const Tabs& T, uint64_t i);
 
@@ -250,7 +160,7 @@ __device__ __forceinline__ void crc_block(const CrcParams& cp, const Tabs& T, ui
   if (live && cp.val && cp.pre && cp.pre->code && i >= (uint64_t)cp.pre->record) live = false;  // not delimited
   if (live) {
     if (cp.val) {
-      rc = frame_expect(cp.in, cp.in_len, cp.offs[i], &a, &b, &want, &exp);
+      rc = kx_frame_expect(GlobalBytes{cp.in}, cp.in_len, cp.offs[i], &a, &b, &want, &exp);
       if (rc) a = b = 0;
     } else {
       a = cp.offs[i];

@@ -29,6 +29,7 @@
 #include <stdlib.h>
 
 #include "kx_internal.h"
+#include "kx_crc.h"
 
 #define LDS __attribute__((address_space(3)))
 #define GLB __attribute__((address_space(1)))
@@ -107,6 +108,7 @@ struct DecParams {
   uint32_t tts_flag;         // ttstream: HeaderFlagsStreaming
   uint64_t tts_name[5];      // ttstream: frame-type values (little-endian packed, NUL-padded)
   uint32_t tts_nlen[5];
+  uint8_t* fr_crc;           // M_FRAME with CRC32Check: per-frame code of the fused payload checksum
   uint64_t* tdesc;           // tile words
   uint64_t* gdesc;           // group words
   uint16_t* starts;          // concatenated mode: record starts per tile (slotcap slots each)
@@ -3074,6 +3076,37 @@ __device__ __forceinline__ void emit_container(const Src& w, const KAS KxProgram
   }
 }
 
+// ---- CRC32Check fused into the frame walk: the frame pipeline's emit pass checks each
+// TTHeader frame's "crc32c" (crcPayloadValidator.Validate, validate.go:183-201) while the frame is in the
+// LDS window, instead of a second kernel re-reading every payload from HBM (kx_crc.hip) ----
+__shared__ uint32_t g_crct[8][256];   // slicing-by-8 tables, built by the frame emit kernel
+
+struct SrcBytes {
+  const Src& w;
+  __device__ __forceinline__ uint32_t operator()(uint64_t p) const { return ld1(w, p); }
+};
+
+// the payload check of frame f: 0, KX_ERR_PAYLOAD_VALIDATION, or the header's UNKNOWN_PROTOCOL
+__device__ __noinline__ uint8_t frame_crc_check(const Src w, uint64_t in_len, uint64_t f) {
+  uint64_t a, b;
+  int want;
+  uint32_t exp = 0;
+  const int rc = kx_frame_expect(SrcBytes{w}, in_len, f, &a, &b, &want, &exp);
+  if (rc) return (uint8_t)rc;
+  if (want != 1) return want == 2 ? (uint8_t)KX_ERR_PAYLOAD_VALIDATION : 0;
+  uint32_t c = ~0u;
+  uint64_t p = a;
+  for (; p + 8 <= b; p += 8)
+    c = kx_crc_upd_k(g_crct, c, (uint64_t)ld4(w, p) | ((uint64_t)ld4(w, p + 4) << 32), 8);
+  if (p < b) {
+    const uint32_t k = (uint32_t)(b - p);
+    uint64_t d = (uint64_t)ld4(w, p) | ((uint64_t)(k > 4 ? ld4(w, p + 4) : 0u) << 32);
+    d &= (1ull << (8 * k)) - 1;
+    c = kx_crc_upd_k(g_crct, c, d, k);
+  }
+  return ~c == exp ? 0 : (uint8_t)KX_ERR_PAYLOAD_VALIDATION;
+}
+
 // ---- kernel 3: emit pass (one wave per tile, lane = record) ----
 // COOP: numeric list columns are copied by the whole wave (its own instantiation, so that schemas
 // without such a column keep the record-by-record kernel's code)
@@ -3147,6 +3180,9 @@ __device__ __forceinline__ void emit_tile(KParams& dp, LDS uint32_t* win, uint64
         if (MODE != M_SKIP && MODE != M_FRAME) emit_defaults(P, dp.cols, r);
       }
       if (MODE == M_SKIP || MODE == M_FRAME) dp.skip_out[r] = pos;
+      if constexpr (MODE == M_FRAME) {
+        if (dp.fr_crc) dp.fr_crc[r] = rc ? 0 : frame_crc_check(w, dp.in_len, pos);
+      }
       if (MODE != M_SKIP && MODE != M_FRAME && dp.cols.presence) dp.cols.presence[r] = pres;
       if (known) {
         if (rc) atomicMin(dp.errkey, (unsigned long long)((r << 8) | (uint64_t)(rc & 0xff)));
@@ -3304,6 +3340,14 @@ __global__ void __launch_bounds__(NT, 4) emit_kernel(DecParams dp_) {  // 4 wave
   __shared__ __attribute__((aligned(16))) uint32_t WIN[WAVES][WINW];
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
+  if constexpr (MODE == M_FRAME) {
+    if (dp.fr_crc) {   // the CRC-32C slicing tables, one column per thread (NT = 256)
+      const uint32_t c0 = kx_crc_t0(g_crct, (int)threadIdx.x);
+      __syncthreads();
+      kx_crc_tk(g_crct, (int)threadIdx.x, c0);
+      __syncthreads();
+    }
+  }
   const uint64_t t = dp.t_lo + (uint64_t)blockIdx.x * WAVES + wv;
   if (t >= dp.t_hi) return;
   emit_tile<NV, MODE, COOP>(dp, (LDS uint32_t*)WIN[wv], t, lane);
@@ -3855,8 +3899,9 @@ int kx_launch_pb_frames(const uint8_t* in, uint64_t in_len, uint64_t n, uint64_t
 int kx_launch_frames(const uint8_t* in, uint64_t in_len, uint64_t n, uint64_t max_payload, uint64_t* frame_offsets,
                      uint64_t* pay_start, uint64_t* pay_end, uint8_t* kinds, kx_status* status, void* ws,
                      size_t ws_size, uint64_t epoch, hipStream_t stream, bool grpc, const kx_ttstream_keys* tts,
-                     int32_t* sids, uint64_t* mpos, uint32_t* mlen) {
+                     int32_t* sids, uint64_t* mpos, uint32_t* mlen, uint8_t* crc_codes) {
   DecParams dp{};
+  dp.fr_crc = crc_codes;
   fill_diag_flags(dp);
   dp.in = in; dp.in_len = in_len; dp.offsets = nullptr; dp.n = n; dp.prog = nullptr;
   dp.status = status; dp.skip_out = frame_offsets; dp.epoch = epoch;

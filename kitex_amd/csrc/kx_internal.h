@@ -137,7 +137,7 @@ int kx_launch_frames(const uint8_t* in, uint64_t in_len, uint64_t n, uint64_t ma
                      uint64_t* pay_start, uint64_t* pay_end, uint8_t* kinds, kx_status* status, void* ws,
                      size_t ws_size, uint64_t epoch, hipStream_t stream, bool grpc = false,
                      const kx_ttstream_keys* tts = nullptr, int32_t* sids = nullptr, uint64_t* mpos = nullptr,
-                     uint32_t* mlen = nullptr);
+                     uint32_t* mlen = nullptr, uint8_t* crc_codes = nullptr);
 
 int kx_launch_encode(const KxProgram* dprog, const KxProgram& hprog, const KxLaunchCols& cols,
                      uint64_t n, uint8_t* out, uint64_t out_cap, uint64_t* sizes_out,

@@ -52,7 +52,8 @@ def lib():
         _lib.emu_crc.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_int, C.c_void_p, C.c_void_p,
                                  C.c_void_p]
         _lib.emu_frames.restype = C.c_int
-        _lib.emu_frames.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint64] + [C.c_void_p] * 5 + [C.c_int]
+        _lib.emu_frames.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint64] + [C.c_void_p] * 5 + [C.c_int,
+                                                                                                  C.c_void_p]
         _lib.emu_tts_frames.restype = C.c_int
         _lib.emu_tts_frames.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.POINTER(A.TTStreamKeys)] + \
             [C.c_void_p] * 8
@@ -112,15 +113,20 @@ def split_points(schema, data: np.ndarray, n: int, parts: int, threads: int = 8)
     return rc, pts, st
 
 
-def frames(data: np.ndarray, n: int, max_payload: int = 0, threads: int = 8, grpc: bool = False):
+def frames(data: np.ndarray, n: int, max_payload: int = 0, threads: int = 8, grpc: bool = False, crc: bool = False):
+    """the frame scan of the kernel source; crc=True also returns the fused CRC32Check codes per frame"""
     os.environ["KX_EMU_THREADS"] = str(threads)
     fo = np.zeros(n + 1, dtype=np.uint64)
     ps = np.zeros(max(1, n), dtype=np.uint64)
     pe = np.zeros(max(1, n), dtype=np.uint64)
     kd = np.zeros(max(1, n), dtype=np.uint8)
+    cc = np.full(max(1, n), 0xEE, dtype=np.uint8)
     st = A.Status()
     rc = lib().emu_frames(data.ctypes.data, data.size, n, max_payload, fo.ctypes.data, ps.ctypes.data,
-                          pe.ctypes.data, kd.ctypes.data, C.addressof(st), 1 if grpc else 0)
+                          pe.ctypes.data, kd.ctypes.data, C.addressof(st), 1 if grpc else 0,
+                          cc.ctypes.data if crc else None)
+    if crc:
+        return rc, fo, ps[:n], pe[:n], kd[:n], st, cc[:n]
     return rc, fo, ps[:n], pe[:n], kd[:n], st
 
 

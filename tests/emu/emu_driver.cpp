@@ -91,7 +91,7 @@ extern "C" int emu_split(const kx_struct_desc* structs, uint32_t nstructs, const
 
 // framing sniff (kx_launch_frames) under the emulator, workspace shared with emu_decode's
 extern "C" int emu_frames(const uint8_t* in, uint64_t in_len, uint64_t n, uint64_t max_payload, uint64_t* fo,
-                          uint64_t* ps, uint64_t* pe, uint8_t* kinds, kx_status* status, int grpc) {
+                          uint64_t* ps, uint64_t* pe, uint8_t* kinds, kx_status* status, int grpc, uint8_t* crc_codes) {
   const size_t ws_size = kx_skip_ws_bytes(in_len, n);
   static char* ws = nullptr;
   static size_t ws_cap = 0;
@@ -108,7 +108,8 @@ extern "C" int emu_frames(const uint8_t* in, uint64_t in_len, uint64_t n, uint64
     epoch = 1;
   }
   status->diag[0] = status->diag[1] = 0;
-  return kx_launch_frames(in, in_len, n, max_payload, fo, ps, pe, kinds, status, ws, ws_cap, epoch, nullptr, grpc != 0);
+  return kx_launch_frames(in, in_len, n, max_payload, fo, ps, pe, kinds, status, ws, ws_cap, epoch, nullptr, grpc != 0,
+                          nullptr, nullptr, nullptr, nullptr, crc_codes);
 }
 
 // ttstream frame scan (kx_launch_frames with keys) under the emulator

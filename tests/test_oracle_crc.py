@@ -90,3 +90,15 @@ def test_emu_validate_frames(oracle):
     crc, rs, st = emu.crc32c(wire, fo, n, True)
     assert np.array_equal(rs, ers) and np.array_equal(crc, ecrc)
     assert st.code == rc == 11 and st.record == first
+
+
+@pytest.mark.parametrize("n", [1, 200, 3000])
+def test_emu_fused_frame_check(oracle, n):
+    """CRC32Check fused into the frame scan's emit pass (kx_decode.hip frame_crc_check): the per-frame codes
+    equal the oracle's validator and the checksum kernel's"""
+    from tests.emu import emu
+    sch, recs, frames, wire, fo, exp = CC.crc_batch(n, CC.MODES_PASS + CC.MODES_FAIL)
+    rc, ecrc, ers, first = oracle.frame_crc32c_validate(wire, fo, n)
+    src, sfo, ps, pe, kd, st, codes = emu.frames(wire, n, crc=True)
+    assert src == 0 and st.code == 0 and np.array_equal(sfo[:n + 1], fo[:n + 1])
+    assert np.array_equal(codes, ers)
