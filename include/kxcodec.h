@@ -261,7 +261,9 @@ typedef struct kx_status {
   uint64_t consumed;    /* input bytes consumed (concatenated mode) */
   uint64_t var_total[16]; /* required arena size (arena units) per var slot (ABI 5: 16 slots, was 8) */
   uint64_t diag[3];       /* decode diagnostics: [0] tiles re-walked from their true entry,
-                             [1] groups of 64 tiles re-scanned by the chain pass, [2] reserved */
+                             [1] groups of 64 tiles re-scanned by the chain pass, [2] concatenated:
+                             tiles the fast index path left to the field loop; known offsets: 2 when
+                             the length gather ran, 3 when its extents needed the repair pass */
 } kx_status;
 
 typedef struct kx_ctx kx_ctx; /* opaque; one per host thread / stream */

@@ -118,6 +118,9 @@ struct DecParams {
   uint64_t* nstop_ring;      // chunked pipeline: nstop of chunk k at [k % KX_PIPE_EV] (chain runs ahead of emit)
   uint32_t* redo_n;          // fast index kernel: tiles it could not index (count, then their ids)
   uint32_t* redo;
+  uint32_t* gate;            // known offsets, length gather: these kernels run only when *gate != 0 (repair)
+  uint32_t* gcheck;          // ... the checking emit pass: a tile whose decoded var units differ from the
+                             // gathered ones sets *gcheck (the repair pass then runs)
   uint64_t* split_out;       // kx_thrift_split_points: nsplit + 1 record starts (no emit pass)
   uint32_t nsplit;
   uint64_t var_base[KXP_NV_MAX];  // arena positions start here (a chunk of a larger batch)
@@ -1900,7 +1903,6 @@ __device__ __forceinline__ uint64_t next_hit(KParams& dp, const Src& w, const Ca
 template <int NV, int MODE>
 __device__ Agg walk_tile(KParams& dp, const Src& w, uint64_t tlo, uint64_t thi, uint64_t seed, int lane,
                          uint16_t* starts, uint32_t dsig) {
-  const KAS KxProgram* P = dp.prog;
   const uint64_t seg_lo = tlo + (uint64_t)lane * SEG;
   const uint64_t seg_hi = kmin64(seg_lo + SEG, thi);
   const Cand cd = lane_candidate<NV, MODE>(dp, w, seg_lo, seg_hi, lane, dsig);
@@ -2364,6 +2366,42 @@ __device__ __forceinline__ Agg measure_records(KParams& dp, const Src& w, uint64
   return g;
 }
 
+// Known offsets, length gather (the index pass without the window): a canonical record's var extents
+// follow from the plan's segments (KxpFast) and one big-endian length word per var field but the last,
+// whose length is what the record's end leaves (R2: s9's length at offsets[r] + 91, s10's =
+// end - start - 103 - len9). Nothing is checked here: the emit pass compares every tile's decoded
+// extents with these and, on any difference, the gated repair pass redoes index -> emit (launch_t).
+// False: the record is off the plan's shape (its extents count as empty, which the emit pass then finds
+// to differ unless the record failed).
+template <int NV>
+__device__ __forceinline__ bool gather_lengths(KParams& dp, uint64_t a, uint64_t b, uint64_t* len) {
+  if (a > b || b > dp.in_len) return false;
+  const Src g{dp.in, dp.in_len, 0, 0, nullptr, nullptr, 0u, 0ull};
+  const uint32_t ns = dp.fp.nseg;
+  uint64_t pos = a;
+  for (uint32_t j = 0; j + 1 < ns; j++) {
+    const uint32_t flen = dp.fp.seg[j].flen, vk = dp.fp.seg[j].vkind, vs = dp.fp.seg[j].vslot;
+    const uint64_t w = vk == 2 ? dp.fp.seg[j].vwidth : 1u;
+    const uint64_t hl = vk == 2 ? 8u : 7u;   // field header (3), list element type (1), length (4)
+    pos += flen;
+    if (pos + hl > b) return false;
+    uint64_t L;
+    if (j + 2 == ns) {   // the last var field: the record's end fixes it
+      const uint64_t rest = b - pos - hl, tail = dp.fp.seg[j + 1].flen;
+      if (rest < tail || (rest - tail) % w) return false;
+      L = (rest - tail) / w;
+    } else {
+      L = __builtin_bswap32(gld4(g, pos + hl - 4));
+    }
+#pragma unroll
+    for (int v = 0; v < NV; v++)
+      if ((uint32_t)v == vs) len[v] = L;
+    pos += hl + L * w;
+    if (pos > b) return false;
+  }
+  return true;
+}
+
 // tile geometry
 __device__ __forceinline__ void tile_range(KParams& dp, uint64_t t, uint64_t& lo, uint64_t& hi) {
   if (dp.offsets) {
@@ -2413,6 +2451,35 @@ __device__ __forceinline__ void put_tile(KParams& dp, uint64_t t, const Agg& a, 
   put_word(dp.tdesc, nt, T_ERRC, t, ep, a.errc);
   put_word(dp.tdesc, nt, T_ERRP, t, ep, a.errp);
   for (int v = 0; v < nv; v++) put_word(dp.tdesc, nt, T_VAR + v, t, ep, a.var[v]);
+}
+
+template <int NV>
+__global__ void __launch_bounds__(NT) gather_kernel(DecParams dp_) {
+  KParams& dp = KX_PARAMS();
+  (void)dp_;
+  const int lane = threadIdx.x & 63;
+  const uint64_t t = (uint64_t)blockIdx.x * WAVES + (threadIdx.x >> 6);
+  if (t >= dp.ntiles) return;
+  const uint64_t r0 = t * dp.krec, r1 = kmin64(r0 + dp.krec, dp.n), r = r0 + lane;
+  uint64_t len[NV > 0 ? NV : 1];
+#pragma unroll
+  for (int v = 0; v < (NV > 0 ? NV : 1); v++) len[v] = 0;
+  if (r < r1 && !gather_lengths<NV>(dp, dp.offsets[r], rec_end(dp, r), len)) {
+#pragma unroll
+    for (int v = 0; v < (NV > 0 ? NV : 1); v++) len[v] = 0;
+  }
+  Agg g;
+  g.ent = X_NONE; g.ex = X_NONE; g.errc = 0; g.errp = 0;
+  g.cnt = r1 - r0;
+#pragma unroll
+  for (int v = 0; v < NV; v++) g.var[v] = wave_sum(len[v]);
+  put_tile(dp, t, g, NV);
+  if (t == 0 && lane == 0) atomicOr(dp.gcheck, 2u);   // diagnostics: the gather ran (kx_status.diag[2])
+}
+
+// the repair pass re-arms what the checking emit pass may have set from the gathered extents
+__global__ void gate_rearm_kernel(const uint32_t* gate, uint32_t* overflow) {
+  if (threadIdx.x == 0 && (*(volatile const uint32_t*)gate & 1u)) *overflow = 0;
 }
 
 // Does a chain arriving at `E` agree with an item whose speculative entry is `ent`? (An item with no
@@ -2551,7 +2618,7 @@ __global__ void __launch_bounds__(NT, 4) index_kernel(DecParams dp_) {  // 4 wav
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
   const uint64_t t = dp.t_lo + (uint64_t)blockIdx.x * WAVES + wv;
-  if (t >= dp.t_hi) return;
+  if (t >= dp.t_hi || (dp.gate && !(*(volatile uint32_t*)dp.gate & 1u))) return;
   index_tile<NV, MODE>(dp, (LDS uint32_t*)WIN[wv], t, lane);
 }
 
@@ -2666,7 +2733,7 @@ __global__ void __launch_bounds__(NT) group_kernel(DecParams dp_) {
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
   const uint64_t g = dp.g_lo + (uint64_t)blockIdx.x * WAVES + wv;
-  if (g >= dp.g_hi) return;
+  if (g >= dp.g_hi || (dp.gate && !(*(volatile uint32_t*)dp.gate & 1u))) return;
   group_scan<NV, MODE, false>(dp, (LDS uint32_t*)WIN[wv], g, g == 0 && !dp.offsets ? 0ull : X_NONE, lane);
 }
 
@@ -2695,6 +2762,7 @@ template <int NV, int MODE>
 __global__ void __launch_bounds__(CT) chain_kernel(DecParams dp_) {
   KParams& dp = KX_PARAMS();
   (void)dp_;
+  if (dp.gate && !(*(volatile uint32_t*)dp.gate & 1u)) return;
   __shared__ __attribute__((aligned(16))) uint32_t WIN0[WINW];
   __shared__ uint64_t s_wcnt[CW], s_wvar[CW][KXP_NV_MAX], s_wlast[CW];
   __shared__ int s_werr[CW];
@@ -3138,6 +3206,9 @@ __device__ __forceinline__ void emit_tile(KParams& dp, LDS uint32_t* win, uint64
     for (int v = 0; v < NV; v++)
       run[v] = (gd[(uint64_t)(G_BVAR + v) * dp.ngroups + g] & V48) + (td[(uint64_t)(T_PVAR + v) * dp.ntiles + t] & V48);
   }
+  uint64_t run0[NV > 0 ? NV : 1];
+#pragma unroll
+  for (int v = 0; v < (NV > 0 ? NV : 1); v++) run0[v] = run[v];
   // a tile the fast index path validated: records are read with the plan alone
   const bool canon = is_thrift(MODE) && !known && !dp.direct && MODE != M_THRIFT_LS &&
                      ((dp.tdesc[(uint64_t)T_ERRC * dp.ntiles + t] & V48) == T_CANON);
@@ -3279,6 +3350,13 @@ __device__ __forceinline__ void emit_tile(KParams& dp, LDS uint32_t* win, uint64
     }
     if (!known) chain = rl64(end, (int)(kmin64(step, cnt - j0) - 1));   // the round's last record ends here
   }
+  if (dp.gcheck) {   // the gathered extents of this tile against the decoded ones (uniform)
+    bool same = true;
+#pragma unroll
+    for (int v = 0; v < NV; v++)
+      same &= run[v] - run0[v] == (dp.tdesc[(uint64_t)(T_VAR + v) * dp.ntiles + t] & V48);
+    if (!same && lane == 0) atomicOr(dp.gcheck, 1u);
+  }
 }
 
 // Split points of a concatenated batch (kx_thrift_split_points; SURVEY.md §8e "pass A emits G split
@@ -3349,7 +3427,7 @@ __global__ void __launch_bounds__(NT, 4) emit_kernel(DecParams dp_) {  // 4 wave
     }
   }
   const uint64_t t = dp.t_lo + (uint64_t)blockIdx.x * WAVES + wv;
-  if (t >= dp.t_hi) return;
+  if (t >= dp.t_hi || (dp.gate && !(*(volatile uint32_t*)dp.gate & 1u))) return;
   emit_tile<NV, MODE, COOP>(dp, (LDS uint32_t*)WIN[wv], t, lane);
 }
 
@@ -3384,7 +3462,9 @@ __global__ void __launch_bounds__(NT, 4) combo_kernel(ComboParams cp_) {
 __global__ void finalize_kernel(kx_status* st, unsigned long long* errkey, uint32_t* overflow, uint64_t* nstop,
                                 const uint64_t* offsets, uint64_t n, uint32_t* redo_n) {
   if (threadIdx.x != 0) return;
-  *redo_n = 0;
+  redo_n[0] = 0;
+  if (offsets) st->diag[2] = redo_n[1];   // known offsets: 2 the length gather ran, 3 and was repaired
+  redo_n[1] = 0;   // the length-gather check flag (launch_t)
   unsigned long long k = *errkey;
   if (k != ~0ull && st->code == 0) {
     st->code = (int32_t)(k & 0xff);
@@ -3402,7 +3482,7 @@ __global__ void finalize_kernel(kx_status* st, unsigned long long* errkey, uint3
 //      record-start slots ----
 constexpr size_t WS_HDR = 512;
 // header words: [8] errkey, [16] overflow, [24] nstop, [64..) chain carry (CY_WORDS), [256..) nstop ring
-// (KX_PIPE_EV words), [448] redo count
+// (KX_PIPE_EV words), [448] redo count (u32), [452] length-gather check flag (u32)
 constexpr size_t WS_CARRY = 64, WS_RING = 256, WS_REDO = 448;
 static_assert(WS_CARRY + 8 * CY_WORDS <= WS_RING && WS_RING + 8 * KX_PIPE_EV <= WS_REDO && WS_REDO + 8 <= WS_HDR,
               "workspace header layout");
@@ -3624,6 +3704,40 @@ int launch_t(const DecParams& dp0, const WsLayout& L, void* ws, hipStream_t stre
                        dp.offsets, dp.n, dp.redo_n);
     KX_HIP_CHECK(hipGetLastError());
     return KX_OK;
+  }
+  if constexpr (MODE == M_THRIFT && NV > 0) {
+    // known offsets, canonical plan: the length gather instead of the index pass's window, checked by the
+    // emit pass; on any difference the gated repair pass (index -> group -> chain -> emit) runs
+    static int gather_env = -1;
+    if (gather_env < 0) { const char* e = getenv("KX_GATHER"); gather_env = e ? atoi(e) : 1; }
+    if (gather_env && !dp.direct && dp.offsets && dp.fast && dp.fp.ok && !dp.diag) {
+      DecParams c = dp;
+      c.gcheck = dp.redo_n + 1;
+      hipLaunchKernelGGL((gather_kernel<NV>), dim3(grid), dim3(NT), 0, stream, c);
+      KX_HIP_CHECK(hipGetLastError());
+      hipLaunchKernelGGL((group_kernel<NV, MODE>), dim3(ggrid), dim3(NT), 0, stream, c);
+      KX_HIP_CHECK(hipGetLastError());
+      hipLaunchKernelGGL((chain_kernel<NV, MODE>), dim3(1), dim3(CT), 0, stream, c);
+      KX_HIP_CHECK(hipGetLastError());
+      launch_emit<NV, MODE>(dim3(grid), stream, c);
+      KX_HIP_CHECK(hipGetLastError());
+      DecParams rp = dp;
+      rp.gate = dp.redo_n + 1;
+      hipLaunchKernelGGL(gate_rearm_kernel, dim3(1), dim3(64), 0, stream, rp.gate, dp.overflow);
+      KX_HIP_CHECK(hipGetLastError());
+      hipLaunchKernelGGL((index_kernel<NV, MODE>), dim3(grid), dim3(NT), 0, stream, rp);
+      KX_HIP_CHECK(hipGetLastError());
+      hipLaunchKernelGGL((group_kernel<NV, MODE>), dim3(ggrid), dim3(NT), 0, stream, rp);
+      KX_HIP_CHECK(hipGetLastError());
+      hipLaunchKernelGGL((chain_kernel<NV, MODE>), dim3(1), dim3(CT), 0, stream, rp);
+      KX_HIP_CHECK(hipGetLastError());
+      launch_emit<NV, MODE>(dim3(grid), stream, rp);
+      KX_HIP_CHECK(hipGetLastError());
+      hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(64), 0, stream, dp.status, dp.errkey, dp.overflow, dp.nstop,
+                         dp.offsets, dp.n, dp.redo_n);
+      KX_HIP_CHECK(hipGetLastError());
+      return KX_OK;
+    }
   }
   if (!dp.direct) {
     static int ncu = -1;

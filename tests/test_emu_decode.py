@@ -7,6 +7,7 @@ import pytest
 
 from kitex_amd import schema as S
 from kitex_amd import synth
+from kitex_amd import _abi as A
 from tests import decode_cases as DC
 from tests import frame_cases as FC
 from tests import pb_cases as PC
@@ -248,3 +249,8 @@ def test_emu_fast_index_path_taken(edec, oracle, name, n):
     assert st.diag[2] <= 2, (st.diag[2], tiles)
     rc, exp, est, _ = oracle.decode(sch, wire, n)
     assert_columns_equal(cols, exp, infos, n)
+
+
+@pytest.mark.parametrize("case", DC.GATHER_CASES)
+def test_emu_offsets_length_gather(edec, oracle, case):
+    DC.case_offsets_gather(edec, oracle, case)

@@ -193,6 +193,11 @@ def test_skip_batch_matches_oracle(torch, dev, oracle):
     DC.case_skip(lambda wire, n: cdc.Skip(torch.from_numpy(wire).to(dev), n), oracle)
 
 
+@pytest.mark.parametrize("case", DC.GATHER_CASES)
+def test_offsets_length_gather(torch, dev, oracle, case):
+    DC.case_offsets_gather(GpuDecoder(torch, dev), oracle, case, n=20000)
+
+
 @pytest.mark.parametrize("mode", ["concat", "offsets"])
 def test_r2_base_flat_path(torch, dev, oracle, mode):
     """R2 + base.Base (base.thrift:10-17): 11 var slots stay on the flat tile pipeline (kx_schema_is_nested
