@@ -557,4 +557,4 @@ def case_offsets_gather(dec, oracle, case, n=3000):
             recs[n // 3] = rec_bytes(oracle, [(A.T_STRING, 9, bytes.fromhex("fffffff0"))])
         wire, offs = concat(recs)
     cols, st = check_decode(dec, oracle, sch, wire, n, offsets=offs)
-    assert st.diag[2] == (3 if case == "noncanonical" else 2)
+    assert st.diag[2] == (3 if case == "noncanonical" else 2), (case, st.diag[0], st.diag[1], st.diag[2])
