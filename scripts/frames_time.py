@@ -38,3 +38,13 @@ for chk in (False, True):
     torch.cuda.synchronize()
     s = r.read_status()
     print(f"frames n={n} crc={chk}: {(time.perf_counter() - t0) / 3 * 1e3:.2f} ms code={s.code}", flush=True)
+from kitex_amd.codec import frame_scan, read_status  # noqa: E402
+for _ in range(2):
+    res = frame_scan(wire, n)
+torch.cuda.synchronize()
+t0 = time.perf_counter()
+for _ in range(3):
+    res = frame_scan(wire, n)
+torch.cuda.synchronize()
+st = read_status(res[-1])
+print(f"frame_scan n={n}: {(time.perf_counter() - t0) / 3 * 1e3:.2f} ms code={st.code} diag={list(st.diag)}", flush=True)
