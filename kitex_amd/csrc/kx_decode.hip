@@ -1814,6 +1814,10 @@ __device__ __forceinline__ uint64_t frame_scan_segment(KParams& dp, const Src& w
     if (cls == 0) {
       const uint32_t c = be32(w, p + 4);
       if ((c >> 16) != m0 || (uint64_t)a + 4 > dp.in_len - p) continue;
+      // the frame it would be must be followed by another of its class (or end the buffer): two magic
+      // words a length apart, where one alone occurs in payload bytes every 64 Ki positions
+      const uint64_t nx = p + 4 + (uint64_t)a;
+      if (nx != dp.in_len && (nx + 8 > dp.in_len || (be32(w, nx + 4) >> 16) != m0)) continue;
     } else if ((a >> 16) != m0) {
       continue;
     }
