@@ -1809,20 +1809,52 @@ __device__ __forceinline__ uint64_t frame_scan_segment(KParams& dp, const Src& w
   const uint32_t cls = (c0 >> 16) == 0x1000u ? 0u : (a0 >> 16) == 0xFFAFu ? 1u : (a0 >> 16) == 0x8001u ? 2u : 0u;
   const uint32_t m0 = cls == 0 ? (c0 >> 16) : (a0 >> 16);
   const uint64_t plim = kmin64(hi, dp.in_len - 7);
-  for (uint64_t p = lo; p < plim; p++) {
+  // a candidate at p: its magic word; class 0 also needs a length that fits and the frame it would be
+  // followed by another of its class (or the buffer's end): two magic words a length apart, where one
+  // alone occurs in payload bytes every 64 Ki positions
+  auto cand = [&](uint64_t p) -> bool {
     const uint32_t a = be32(w, p);
-    if (cls == 0) {
-      const uint32_t c = be32(w, p + 4);
-      if ((c >> 16) != m0 || (uint64_t)a + 4 > dp.in_len - p) continue;
-      // the frame it would be must be followed by another of its class (or end the buffer): two magic
-      // words a length apart, where one alone occurs in payload bytes every 64 Ki positions
-      const uint64_t nx = p + 4 + (uint64_t)a;
-      if (nx != dp.in_len && (nx + 8 > dp.in_len || (be32(w, nx + 4) >> 16) != m0)) continue;
-    } else if ((a >> 16) != m0) {
-      continue;
+    if (cls != 0) return (a >> 16) == m0;
+    if ((be32(w, p + 4) >> 16) != m0 || (uint64_t)a + 4 > dp.in_len - p) return false;
+    const uint64_t nx = p + 4 + (uint64_t)a;
+    return nx == dp.in_len || (nx + 8 <= dp.in_len && (be32(w, nx + 4) >> 16) == m0);
+  };
+  const uint32_t mo = cls == 0 ? 4u : 0u;   // the magic's offset in a frame
+  const int32_t q0 = hi - lo == SEG ? wofs(w, lo + mo, SEG + 8) : -1;
+  if (q0 >= 0) {
+    // the rotated, conflict-free 33-dword pass of scan_segment2 with the 2-byte magic: one bit per
+    // dword holding a match, then the matches in order, each tested in full
+    const LDS uint32_t* s = w.win + (q0 >> 2);
+    const uint32_t sh0 = q0 & 3;
+    const uint32_t B0 = (m0 >> 8) * 0x01010101u, B1 = (m0 & 0xffu) * 0x01010101u;
+    const int lane = (int)(threadIdx.x & 63);
+    uint64_t hb = 0;
+    int idx = lane % 33;
+    for (int i = 0; i < 33; i++) {
+      const uint32_t x0 = s[idx], x1 = s[idx + 1];
+      const uint32_t m = zero_bytes((x0 ^ B0) | (__builtin_amdgcn_alignbyte(x1, x0, 1) ^ B1));
+      hb |= (uint64_t)(m != 0) << idx;
+      idx = idx == 32 ? 0 : idx + 1;
     }
-    return p;
+    while (hb) {
+      const int d = __ffsll((long long)hb) - 1;
+      hb &= hb - 1;
+      const uint32_t x0 = s[d], x1 = s[d + 1];
+      uint32_t m = zero_bytes((x0 ^ B0) | (__builtin_amdgcn_alignbyte(x1, x0, 1) ^ B1));
+      while (m) {
+        const uint32_t j = first_hit(m);
+        m &= m - 1;
+        const uint32_t off = 4u * (uint32_t)d + j;
+        if (off < sh0 || off - sh0 >= (uint32_t)SEG) continue;
+        const uint64_t p = lo + (off - sh0);
+        if (p >= plim) return X_NONE;
+        if (cand(p)) return p;
+      }
+    }
+    return X_NONE;
   }
+  for (uint64_t p = lo; p < plim; p++)
+    if (cand(p)) return p;
   return X_NONE;
 }
 
