@@ -3200,6 +3200,17 @@ __device__ __noinline__ uint8_t frame_crc_check(const Src w, uint64_t in_len, ui
   if (want != 1) return want == 2 ? (uint8_t)KX_ERR_PAYLOAD_VALIDATION : 0;
   uint32_t c = ~0u;
   uint64_t p = a;
+  const int32_t q = b - a <= (uint64_t)WINB ? wofs(w, a, (uint32_t)(b - a) + 8) : -1;
+  if (q >= 0 && b - a >= 8) {
+    // inside the window: the head up to a dword boundary, then two aligned dwords per step
+    const uint32_t h = (4u - ((uint32_t)q & 3u)) & 3u;
+    if (h) {
+      c = kx_crc_upd_k(g_crct, c, ld4(w, p) & ((1u << (8 * h)) - 1), h);
+      p += h;
+    }
+    const LDS uint32_t* s = w.win + ((uint32_t)q + h) / 4;
+    for (; p + 8 <= b; p += 8, s += 2) c = kx_crc_upd_k(g_crct, c, (uint64_t)s[0] | ((uint64_t)s[1] << 32), 8);
+  }
   for (; p + 8 <= b; p += 8)
     c = kx_crc_upd_k(g_crct, c, (uint64_t)ld4(w, p) | ((uint64_t)ld4(w, p + 4) << 32), 8);
   if (p < b) {
