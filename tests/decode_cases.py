@@ -539,6 +539,15 @@ GATHER_CASES = ["r2", "r3", "noncanonical", "error"]
 
 
 def case_offsets_gather(dec, oracle, case, n=3000):
+    import os
+    os.environ["KX_GATHER"] = "1"   # opt-in, read per call
+    try:
+        _case_offsets_gather(dec, oracle, case, n)
+    finally:
+        del os.environ["KX_GATHER"]
+
+
+def _case_offsets_gather(dec, oracle, case, n):
     """known offsets on a canonical plan: the length gather replaces the index window (kx_status.diag[2] = 2);
     records off the plan make the checking emit pass run the gated repair (diag[2] = 3); parity either way.
     A failing record counts as empty both ways, so it needs no repair."""
