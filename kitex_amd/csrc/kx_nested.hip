@@ -7,8 +7,8 @@
 //   2. block sums per (1024-record block, cursor), then one workgroup per cursor scans the block sums
 //      into block bases and the cursor's total; a one-thread check compares the totals with the
 //      columns' capacities (SIZE_LIMIT: nothing is written);
-//   3. write: a workgroup per block re-scans its records' counts (one workgroup scan per cursor) into
-//      per-lane cursor bases and re-walks each record writing values, offsets entries and presence;
+//   3. write: each lane reads its record's cursor bases (block base + the in-block prefix the block-sum
+//      pass left in place of the counts) and re-walks the record writing values, offsets and presence;
 //   4. finalize: the last entry of every offsets array, the call status.
 // Encode: size pass (lane = record, BLength) -> block scan -> write pass (FastWriteNocopy at the
 // record's offset); struct_tpl.go:225-391.
@@ -122,17 +122,31 @@ __device__ uint64_t wg_excl(uint64_t v, uint64_t* tot, uint64_t* sh) {
   return base + inc - v;
 }
 
-// grid (nblk, ncur): block sums
+// grid (nblk, ncur): block sums, and each count replaced by its exclusive prefix inside the block (u32:
+// a block's units of one cursor stay below 2^32, kx_launch_nested_decode), so that the write pass reads
+// every record's cursor bases instead of scanning for them. Thread t owns RB / NT consecutive records.
+constexpr int RPT = RB / NT;
 __global__ void __launch_bounds__(NT) bsum_kernel(NParams p) {
   __shared__ uint64_t sh[NT / 64];
   const uint64_t b = blockIdx.x, k = blockIdx.y;
+  const uint64_t r0 = b * RB + (uint64_t)threadIdx.x * RPT;
+  uint32_t* c = p.counts + k * p.n;
+  uint32_t x[RPT];
   uint64_t acc = 0;
-  for (int j = 0; j < RB / NT; j++) {
-    const uint64_t r = b * RB + (uint64_t)j * NT + threadIdx.x;
-    if (r < p.n) acc += p.counts[k * p.n + r];
+#pragma unroll
+  for (int j = 0; j < RPT; j++) {
+    x[j] = r0 + j < p.n ? c[r0 + j] : 0u;
+    acc += x[j];
   }
   uint64_t tot;
-  (void)wg_excl(acc, &tot, sh);
+  uint64_t pre = wg_excl(acc, &tot, sh);
+  if (!p.sizes_only) {
+#pragma unroll
+    for (int j = 0; j < RPT; j++) {
+      if (r0 + j < p.n) c[r0 + j] = (uint32_t)pre;
+      pre += x[j];
+    }
+  }
   if (threadIdx.x == 0) p.bsum[k * p.nblk + b] = tot;
 }
 
@@ -144,7 +158,12 @@ __global__ void __launch_bounds__(1024) bscan_kernel(NParams p) {
   const uint64_t per = (nb + 1023) / 1024;
   const uint64_t lo = threadIdx.x * per, hi = kmin64(lo + per, nb);
   uint64_t acc = 0;
-  for (uint64_t i = lo; i < hi; i++) acc += s[i];
+  bool big = false;   // a block holding 2^32 units of one cursor: its u32 in-block prefixes would wrap
+  for (uint64_t i = lo; i < hi; i++) {
+    acc += s[i];
+    big |= s[i] >> 32 != 0;
+  }
+  if (big) atomicOr(p.flag, 1u);   // SIZE_LIMIT: nothing is written
   uint64_t tot;
   uint64_t run = wg_excl(acc, &tot, sh);
   for (uint64_t i = lo; i < hi; i++) {
@@ -171,29 +190,29 @@ __global__ void check_kernel(NParams p) {
     for (int k = 1; k < K.narr; k++)
       if (parent_size(p, K, k) > p.C->cap[c][1 + k]) over = true;
   }
-  *p.flag = over ? 1u : 0u;
+  if (over) *p.flag = 1u;
 }
 
-// one block of RB records: per record the workgroup scan of every cursor's counts gives the lane's
-// bases; carry: the block's running base per cursor (uniform)
+// one block of RB records, lane = record
 template <int T>
 __device__ __forceinline__ void write_block(const NParams& p, uint64_t* carry, uint64_t* cur, uint64_t* lim,
                                             uint64_t* snap, uint64_t* sh) {
   const KxnProgram& P = *p.P;
   const uint64_t b = blockIdx.x;
-  for (uint32_t k = 0; k < p.ncur; k++) carry[k] = p.bsum[(uint64_t)k * p.nblk + b];
+  (void)carry;
+  (void)sh;
+  const uint64_t rb1 = kmin64((b + 1) * RB, p.n);   // the block's end
   for (int j = 0; j < RB / T; j++) {
     const uint64_t r = b * RB + (uint64_t)j * T + threadIdx.x;
-    const bool act = r < p.n;
+    if (r >= p.n) continue;
+    // the record's cursor bases: the block base + the in-block prefix (bsum_kernel); its extent ends
+    // at the next record's prefix, or at the next block's base
     for (uint32_t k = 0; k < p.ncur; k++) {
-      const uint64_t x = act ? p.counts[(uint64_t)k * p.n + r] : 0;
-      uint64_t tot;
-      const uint64_t pre = wg_excl(x, &tot, sh);
-      cur[k] = carry[k] + pre;
-      lim[k] = cur[k] + x;
-      carry[k] += tot;
+      const uint64_t base = p.bsum[(uint64_t)k * p.nblk + b];
+      const uint32_t* c = p.counts + (uint64_t)k * p.n;
+      cur[k] = base + c[r];
+      lim[k] = r + 1 < rb1 ? base + c[r + 1] : (b + 1 < p.nblk ? p.bsum[(uint64_t)k * p.nblk + b + 1] : p.totals[k]);
     }
-    if (!act) continue;
     const uint8_t rc = p.rcode[r];
     uint64_t a = 0, e = 0, used = 0;
     if (rc == 0 && extent(p, r, &a, &e) == 0) {
