@@ -341,6 +341,21 @@ KXN_HD uint64_t kxn_scalar(uint32_t t, const uint8_t* p) {  // host order; BOOL 
   }
 }
 
+// byte copy in blocks of 16: a block's loads are all issued before its stores (the compiler may not
+// reorder them itself: source and destination could alias), so a lane waits once per 16 bytes rather
+// than once per byte
+KXN_HD void kxn_copy(uint8_t* dst, const uint8_t* src, uint64_t m) {
+  uint64_t j = 0;
+  for (; j + 16 <= m; j += 16) {
+    uint8_t t[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) t[k] = src[j + k];
+#pragma unroll
+    for (int k = 0; k < 16; k++) dst[j + k] = t[k];
+  }
+  for (; j < m; j++) dst[j] = src[j];
+}
+
 // ---------------------------------------------------------------------------------------------
 // decode walker
 struct KxnFrame {
@@ -426,7 +441,7 @@ KXN_HD int kxn_value(const KxnProgram& P, const KxnCols& C, const uint8_t* b, ui
         uint8_t* dst = (uint8_t*)C.data[N.col] + cur[N.cur];
         const uint64_t room = S.lim[N.cur] > cur[N.cur] ? S.lim[N.cur] - cur[N.cur] : 0;
         const uint64_t m = (uint64_t)l < room ? (uint64_t)l : room;
-        for (uint64_t j = 0; j < m; j++) dst[j] = b[*q + 4 + j];
+        kxn_copy(dst, b + *q + 4, m);
       }
       cur[N.cur] += (uint64_t)l;
       *q += 4 + (uint64_t)l;
@@ -440,7 +455,7 @@ KXN_HD int kxn_value(const KxnProgram& P, const KxnCols& C, const uint8_t* b, ui
         uint8_t* dst = (uint8_t*)C.data[N.col] + cur[N.cur];
         const uint64_t room = S.lim[N.cur] > cur[N.cur] ? S.lim[N.cur] - cur[N.cur] : 0;
         const uint64_t m = e - *q < room ? e - *q : room;
-        for (uint64_t j = 0; j < m; j++) dst[j] = b[*q + j];
+        kxn_copy(dst, b + *q, m);
       }
       cur[N.cur] += e - *q;
       *q = e;
@@ -626,7 +641,7 @@ KXN_HD void kxn_wvalue(const KxnProgram& P, const KxnCols& C, int X, uint64_t e,
       if (N.kind == KN_STRING) kxn_out<W>(out, pos, l, 4);
       else if (l == 0) { kxn_out<W>(out, pos, KX_T_STOP, 1); return; }  // an empty raw struct: STOP
       if (W)
-        for (uint64_t j = 0; j < l; j++) out[*pos + j] = ((const uint8_t*)C.data[N.col])[a + j];
+        kxn_copy(out + *pos, (const uint8_t*)C.data[N.col] + a, l);
       *pos += l;
       return;
     }
@@ -847,7 +862,7 @@ KXN_HD int kxn_pb_value(const KxnProgram& P, const KxnCols& C, const uint8_t* b,
         uint8_t* dst = (uint8_t*)C.data[N.col] + cur[N.cur];
         const uint64_t room = S.lim[N.cur] > cur[N.cur] ? S.lim[N.cur] - cur[N.cur] : 0;
         const uint64_t m = l < room ? l : room;
-        for (uint64_t j = 0; j < m; j++) dst[j] = b[*q + j];
+        kxn_copy(dst, b + *q, m);
       }
       cur[N.cur] += l;
       *q += l;
@@ -1110,7 +1125,7 @@ KXN_HD uint64_t kxn_pb_walk(const KxnProgram& P, const KxnCols& C, KxnPEFrame st
         if (W) {
           kxn_pb_put_uv<W>(out, &pos, tag);
           kxn_pb_put_uv<W>(out, &pos, l);
-          for (uint64_t j = 0; j < l; j++) out[pos + j] = ((const uint8_t*)C.data[N.col])[a + j];
+          kxn_copy(out + pos, (const uint8_t*)C.data[N.col] + a, l);
           pos += l;
         } else {
           sz = kxn_uvlen(tag) + kxn_uvlen(l) + l;
@@ -1238,7 +1253,7 @@ KXN_HD uint64_t kxn_pb_walk(const KxnProgram& P, const KxnCols& C, KxnPEFrame st
         if (W) {
           kxn_pb_put_uv<W>(out, &pos, tag);
           kxn_pb_put_uv<W>(out, &pos, l);
-          for (uint64_t j = 0; j < l; j++) out[pos + j] = ((const uint8_t*)C.data[V.col])[a + j];
+          kxn_copy(out + pos, (const uint8_t*)C.data[V.col] + a, l);
           pos += l;
         } else {
           F.acc += kxn_uvlen(tag) + kxn_uvlen(l) + l;
