@@ -12,7 +12,7 @@ import os
 import sys
 from collections import defaultdict
 
-DECODE = ("index_kernel", "group_kernel", "chain_kernel", "emit_kernel", "finalize_kernel")
+DECODE = ("index_kernel", "index_fast_kernel", "redo_kernel", "group_kernel", "chain_kernel", "emit_kernel", "finalize_kernel")
 ENCODE = ("size_kernel", "scan_kernel", "write_kernel")
 KERNELS = DECODE
 
