@@ -68,8 +68,9 @@ def main():
            "note": "FETCH_SIZE x2 (gfx950 wide-read correction) + WRITE_SIZE, KiB -> bytes, summed over the "
                    "kernels of one call; Infinity-Cache hits are counted by these counters; bench.py "
                    "uses it only when lib_sha256 matches the library it times"}
-    out = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles",
-                       f"pmc_{cfg}_{mode}.json")
+    odir = os.environ.get("PMC_OUT") or os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                                     "profiles")
+    out = os.path.join(odir, f"pmc_{cfg}_{mode}.json")
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1)
     print(json.dumps(res, indent=1))
