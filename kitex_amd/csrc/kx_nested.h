@@ -163,11 +163,14 @@ struct KxnCols {
 
 // ---------------------------------------------------------------------------------------------
 // byte reads (big-endian wire)
-KXN_HD uint32_t kxn_be16(const uint8_t* p) { return ((uint32_t)p[0] << 8) | p[1]; }
-KXN_HD uint32_t kxn_be32(const uint8_t* p) {
+template <class B>
+KXN_HD uint32_t kxn_be16(B p) { return ((uint32_t)p[0] << 8) | p[1]; }
+template <class B>
+KXN_HD uint32_t kxn_be32(B p) {
   return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
 }
-KXN_HD uint64_t kxn_be64(const uint8_t* p) { return ((uint64_t)kxn_be32(p) << 32) | kxn_be32(p + 4); }
+template <class B>
+KXN_HD uint64_t kxn_be64(B p) { return ((uint64_t)kxn_be32(p) << 32) | kxn_be32(p + 4); }
 
 KXN_HD int kxn_tsize(uint32_t t) {
   switch (t) {
@@ -189,7 +192,8 @@ struct KxnSkipFrame {
 };
 
 // visit one value of type t with depth d at b[*n]: skip it or push its frame
-KXN_HD int kxn_skip_visit(const uint8_t* b, uint64_t len, uint64_t* n, uint32_t t, int d, KxnSkipFrame* st,
+template <class B>
+KXN_HD int kxn_skip_visit(B b, uint64_t len, uint64_t* n, uint32_t t, int d, KxnSkipFrame* st,
                           int* sp) {
   if (d == 0) return KX_ERR_DEPTH_LIMIT;                     // :192-194
   const int sz = kxn_tsize(t);
@@ -252,7 +256,8 @@ KXN_HD int kxn_skip_visit(const uint8_t* b, uint64_t len, uint64_t* n, uint32_t 
 }
 
 // skip one value of wire type t at b[*n] (len: the readable extent)
-KXN_HD int kxn_skip(const uint8_t* b, uint64_t len, uint64_t* n, uint32_t t, int maxdepth) {
+template <class B>
+KXN_HD int kxn_skip(B b, uint64_t len, uint64_t* n, uint32_t t, int maxdepth) {
   KxnSkipFrame st[KXN_SKIP_DEPTH + 1];
   int sp = 0;
   int rc = kxn_skip_visit(b, len, n, t, maxdepth, st, &sp);
@@ -331,7 +336,8 @@ KXN_HD uint64_t kxn_get_val(const KxnCols& C, int c, uint32_t w, uint64_t i) {
   }
 }
 
-KXN_HD uint64_t kxn_scalar(uint32_t t, const uint8_t* p) {  // host order; BOOL is `b == 1` (parity unpinned)
+template <class B>
+KXN_HD uint64_t kxn_scalar(uint32_t t, B p) {  // host order; BOOL is `b == 1` (parity unpinned)
   switch (t) {
     case KX_T_BOOL: return p[0] == 1;
     case KX_T_BYTE: return p[0];
@@ -344,7 +350,8 @@ KXN_HD uint64_t kxn_scalar(uint32_t t, const uint8_t* p) {  // host order; BOOL 
 // byte copy in blocks of 16: a block's loads are all issued before its stores (the compiler may not
 // reorder them itself: source and destination could alias), so a lane waits once per 16 bytes rather
 // than once per byte
-KXN_HD void kxn_copy(uint8_t* dst, const uint8_t* src, uint64_t m) {
+template <class S>
+KXN_HD void kxn_copy(uint8_t* dst, S src, uint64_t m) {
   uint64_t j = 0;
   for (; j + 16 <= m; j += 16) {
     uint8_t t[16];
@@ -421,8 +428,8 @@ KXN_HD void kxn_inst_end(const KxnProgram& P, const KxnCols& C, int R, uint64_t*
 
 // read one value of node X at b[*q] (scalars, strings, raw structs directly; structs / containers push a
 // frame). Element instances of containers are opened by the caller.
-template <bool W>
-KXN_HD int kxn_value(const KxnProgram& P, const KxnCols& C, const uint8_t* b, uint64_t len, uint64_t* q, int X,
+template <bool W, class B>
+KXN_HD int kxn_value(const KxnProgram& P, const KxnCols& C, B b, uint64_t len, uint64_t* q, int X,
                      uint64_t* cur, KxnState& S, KxnFrame* stk, int* sp) {
   const KxnNode& N = P.node[X];
   switch (N.kind) {
@@ -491,8 +498,8 @@ KXN_HD int kxn_value(const KxnProgram& P, const KxnCols& C, const uint8_t* b, ui
 
 // FastRead of record r = b[0 .. len). cur: cursors (measure: from 0, write: at the record's bases);
 // lim (write): the ends of the record's extents; snap: KXN_MAX_SNAP slots. *used = bytes of the struct.
-template <bool W>
-KXN_HD int kxn_read_record(const KxnProgram& P, const KxnCols& C, const uint8_t* b, uint64_t len, uint64_t r,
+template <bool W, class B>
+KXN_HD int kxn_read_record(const KxnProgram& P, const KxnCols& C, B b, uint64_t len, uint64_t r,
                            uint64_t* cur, uint64_t* snap, uint64_t* used, const uint64_t* lim = nullptr) {
   KxnFrame stk[KXN_STACK];
   KxnState S;
@@ -723,7 +730,8 @@ KXN_HD uint64_t kxn_write_record(const KxnProgram& P, const KxnCols& C, uint64_t
 // as packed runs), a map appends one entry per occurrence (its key and value default to zero); unknown
 // numbers and known numbers with another wire type are skipped.
 
-KXN_HD int kxn_uvarint(const uint8_t* b, uint64_t end, uint64_t* q, uint64_t* v) {  // protowire.ConsumeVarint
+template <class B>
+KXN_HD int kxn_uvarint(B b, uint64_t end, uint64_t* q, uint64_t* v) {  // protowire.ConsumeVarint
   uint64_t x = 0;
   for (int i = 0; i < 10; i++) {
     if (*q + (uint64_t)i >= end) return KX_ERR_EOF;
@@ -753,7 +761,8 @@ KXN_HD uint32_t kxn_pb_wt(const KxnNode& N) {
   return 0;
 }
 
-KXN_HD int kxn_pb_skip(const uint8_t* b, uint64_t end, uint64_t* q, uint32_t wt) {
+template <class B>
+KXN_HD int kxn_pb_skip(B b, uint64_t end, uint64_t* q, uint32_t wt) {
   uint64_t v;
   switch (wt) {
     case 0: return kxn_uvarint(b, end, q, &v);
@@ -770,14 +779,16 @@ KXN_HD int kxn_pb_skip(const uint8_t* b, uint64_t end, uint64_t* q, uint32_t wt)
   }
 }
 
-KXN_HD uint64_t kxn_le(const uint8_t* p, int n) {
+template <class B>
+KXN_HD uint64_t kxn_le(B p, int n) {
   uint64_t v = 0;
   for (int k = n - 1; k >= 0; k--) v = (v << 8) | p[k];
   return v;
 }
 
 // one scalar of node N at b[*q] (its wire type already matched), in the column's host form
-KXN_HD int kxn_pb_scalar(const KxnNode& N, const uint8_t* b, uint64_t end, uint64_t* q, uint64_t* out) {
+template <class B>
+KXN_HD int kxn_pb_scalar(const KxnNode& N, B b, uint64_t end, uint64_t* q, uint64_t* out) {
   const uint32_t wt = kxn_pb_wt(N);
   uint64_t v;
   if (wt == 0) {
@@ -804,7 +815,8 @@ KXN_HD int kxn_pb_scalar(const KxnNode& N, const uint8_t* b, uint64_t end, uint6
 }
 
 // utf8.Valid, as protobuf-go checks proto3 `string` fields
-KXN_HD bool kxn_utf8(const uint8_t* s, uint64_t n) {
+template <class B>
+KXN_HD bool kxn_utf8(B s, uint64_t n) {
   uint64_t i = 0;
   while (i < n) {
     const uint32_t c = s[i];
@@ -840,8 +852,8 @@ struct KxnPFrame {      // an open message (its fields) or map entry (fields 1 /
 
 // one value of node X (wire type matched) into the open instance of its level; a message value pushes a
 // frame (close: the root to end with it), a scalar / string value ends `close` at once
-template <bool W>
-KXN_HD int kxn_pb_value(const KxnProgram& P, const KxnCols& C, const uint8_t* b, uint64_t end, uint64_t* q, int X,
+template <bool W, class B>
+KXN_HD int kxn_pb_value(const KxnProgram& P, const KxnCols& C, B b, uint64_t end, uint64_t* q, int X,
                         uint64_t* cur, KxnState& S, KxnPFrame* stk, int* sp, int close) {
   const KxnNode& N = P.node[X];
   switch (N.kind) {
@@ -886,8 +898,8 @@ KXN_HD int kxn_pb_value(const KxnProgram& P, const KxnCols& C, const uint8_t* b,
 }
 
 // proto.Unmarshal of record r = b[0 .. len): same cursors / snapshots / clipping as kxn_read_record
-template <bool W>
-KXN_HD int kxn_pb_read_record(const KxnProgram& P, const KxnCols& C, const uint8_t* b, uint64_t len, uint64_t r,
+template <bool W, class B>
+KXN_HD int kxn_pb_read_record(const KxnProgram& P, const KxnCols& C, B b, uint64_t len, uint64_t r,
                               uint64_t* cur, uint64_t* snap, uint64_t* used, const uint64_t* lim = nullptr) {
   KxnPFrame stk[KXN_STACK];
   KxnState S;
