@@ -41,11 +41,6 @@ constexpr int RB = 1024;             // records per block
 #endif
 constexpr int WT = KX_ENC_WT;        // write pass: threads per workgroup (records per round)
 constexpr int OUTB = KX_ENC_OUTB;    // LDS image bytes per round
-// the image path's list payloads are copied by the workgroup from a queue at the image's tail
-// (KX_ENC_IQ=0: each lane copies its own, in blocks of 4 elements)
-#ifndef KX_ENC_IQ
-#define KX_ENC_IQ 1
-#endif
 
 struct EncParams {
   const KxProgram* prog;
@@ -226,7 +221,6 @@ __device__ __forceinline__ void put_bytes(SK& s, const uint8_t* src, uint32_t le
 // instead of one dword in each of 64 records. Edge dwords shared with the record's own bytes are written
 // byte by byte, so no store ever covers a byte another store writes.
 constexpr int QCAP = 128;            // queued payloads per wave (a full queue: the lane copies inline)
-constexpr uint32_t IQ = 256;         // image path: queued list payloads per round and workgroup
 constexpr uint32_t DEFER_MIN = 32;   // strings shorter than this stay in the lane's sink
 
 struct PayItem {
@@ -236,12 +230,9 @@ struct PayItem {
   uint32_t w;        // element width (1: raw bytes, 2 / 4 / 8: big-endian scalars)
 };
 
-constexpr int IQ_BYTES = KX_ENC_IQ ? (int)(IQ * sizeof(PayItem)) : 0;   // carved from the image's tail
-
 struct PayQueue {
-  PayItem* q;        // this wave's LDS queue (QCAP items), or the workgroup's image-path queue
+  PayItem* q;        // this wave's LDS queue (QCAP items)
   uint32_t* cnt;     // LDS counter
-  uint32_t cap = QCAP;
 };
 
 // the aligned source dword i of a payload's big-endian byte stream (i < ceil(n * w / 4))
@@ -294,38 +285,11 @@ __device__ __forceinline__ void wave_copy(const PayItem& it, int lane) {
   }
 }
 
-// the same copy into the write pass's LDS image (it.dst = image offset)
-__device__ __forceinline__ void lds_copy(const PayItem& it, LDSB* img, int lane) {
-  const uint64_t total = (uint64_t)it.n * it.w;
-  if (!total) return;
-  const uint64_t d0 = it.dst, d1 = it.dst + total;
-  const uint64_t A0 = d0 & ~3ull;
-  const uint64_t nd = ((d1 + 3) & ~3ull) - A0 >> 2;
-  const uint32_t sh = (uint32_t)(d0 & 3);
-  for (uint64_t k = (uint64_t)lane; k < nd; k += 64) {
-    uint32_t v;
-    if (sh == 0) {
-      v = be_stream_dword(it, k);
-    } else {
-      const uint32_t lo = k ? be_stream_dword(it, k - 1) : 0u;
-      const uint32_t hi = be_stream_dword(it, k);
-      v = __builtin_amdgcn_alignbyte(hi, lo, 4 - sh);
-    }
-    const uint64_t a = A0 + 4 * k;
-    if (a >= d0 && a + 4 <= d1) {
-      *(__attribute__((address_space(3))) uint32_t*)(img + a) = v;
-    } else {
-      for (int j = 0; j < 4; j++)
-        if (a + j >= d0 && a + j < d1) img[a + j] = (uint8_t)(v >> (8 * j));
-    }
-  }
-}
-
 // queue a payload (false: the queue is full, the caller copies inline)
 __device__ __forceinline__ bool defer(const PayQueue& pq, uint64_t dst, const void* src, uint32_t n, uint32_t w) {
   if (!pq.q) return false;
   const uint32_t slot = atomicAdd(pq.cnt, 1u);
-  if (slot >= pq.cap) return false;
+  if (slot >= QCAP) return false;
   pq.q[slot] = PayItem{dst, (uint64_t)src, n, w};
   return true;
 }
@@ -583,8 +547,7 @@ __device__ __forceinline__ void any_write(const EncParams& ep, const KxProgram& 
 // nil-free structs): a run of fixed-width fields loads all its values before the first is written (one
 // memory round trip per run), strings and lists follow their headers. Same bytes as write_record.
 template <class SK>
-__device__ __forceinline__ void write_canon(const KxProgram& P, const KxLaunchCols& C, uint64_t r, SK& s,
-                                            const PayQueue& pq = PayQueue{nullptr, nullptr}) {
+__device__ __forceinline__ void write_canon(const KxProgram& P, const KxLaunchCols& C, uint64_t r, SK& s) {
   const uint32_t ns = P.nsteps;
   for (uint32_t k = 0; k < ns;) {
     const KxpStep st = P.steps[k];
@@ -623,18 +586,6 @@ __device__ __forceinline__ void write_canon(const KxProgram& P, const KxLaunchCo
     s.put(K.elem, 1);
     put_be(s, len, 4);
     const void* src = C.data[st.col];
-    if constexpr (std::is_same<SK, LSink>::value) {
-      // the image path: the payload is left to the workgroup (lds_copy: coalesced column loads, aligned
-      // image dwords); the sink flushes before it and restarts after it, so no byte is written twice
-      if (pq.q && len >= 4 && K.width > 1 && K.elem != KX_T_BOOL) {
-        const uint64_t at = s.pos();
-        if (defer(pq, at, (const uint8_t*)src + o * K.width, len, K.width)) {
-          s.flush();
-          s = SK(s.base, at + (uint64_t)len * K.width);
-          continue;
-        }
-      }
-    }
     for (uint32_t i0 = 0; i0 < len; i0 += 4) {
       uint64_t V[4];
 #pragma unroll
@@ -753,7 +704,7 @@ __global__ void __launch_bounds__(WT, KX_ENC_LB) write_kernel(EncParams ep) {
     uint64_t pre = block_excl_scan(sz, &tot, scratch);
     const uint32_t skew = (uint32_t)(((uint64_t)ep.out + gpos) & 15);
     // records that fit entirely into this round's image (at least one)
-    bool fits = my < rend && skew + pre + sz <= (uint64_t)(OUTB - IQ_BYTES);
+    bool fits = my < rend && skew + pre + sz <= OUTB;
     if (threadIdx.x == 0) { s_take = 0; s_round_bytes = 0; }
     __syncthreads();
     if (fits) {
@@ -786,24 +737,15 @@ __global__ void __launch_bounds__(WT, KX_ENC_LB) write_kernel(EncParams ep) {
       r += cnt;
       continue;
     }
-    if (threadIdx.x == 0) qcnt[0] = 0;
-    __syncthreads();
-    PayItem* iq = (PayItem*)(smem_raw + OUTB - IQ_BYTES);   // the image path's payload queue
     if (threadIdx.x < take) {
       LSink s((LDSB*)img, skew + pre);
       if (CANON && is_canon(P, ep.cols, my))
-        write_canon(P, ep.cols, my, s, PayQueue{KX_ENC_IQ ? iq : nullptr, &qcnt[0], IQ});
+        write_canon(P, ep.cols, my, s);
       else
         any_write<LS>(ep, P, my, s);
       if (ep.offsets_out) ep.offsets_out[my] = gpos + pre;
     }
     __syncthreads();
-    if (KX_ENC_IQ) {   // the queued list payloads, one item per wave at a time
-      const uint32_t nq = min(qcnt[0], IQ);
-      const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-      for (uint32_t i = (uint32_t)wv; i < nq; i += WT / 64) lds_copy(iq[i], (LDSB*)img, lane);
-      __syncthreads();
-    }
     // stream the image [skew, skew + bytes) to out[gpos ...): the image is congruent mod 16
     const uint64_t bytes = s_round_bytes;
     const uint64_t gstart = (uint64_t)ep.out + gpos;
