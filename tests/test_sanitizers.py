@@ -17,14 +17,13 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CLANG = "/opt/rocm/lib/llvm/bin/clang++"
 
-# the emulator and host-walker suites and the oracle suites; the emulator's long-running cases (large
-# persistent-loop, slot-overflow and look-back batches, the chunked / combined experiments) are left to the
-# full sanitizer runs recorded in profiles/r4_sanitizers_*.log (about 5x slower under ASan)
-SUITES = ["tests/test_emu_decode.py", "tests/test_nested.py", "tests/test_pbn.py", "tests/test_shard.py",
-          "tests/test_oracle_list_struct.py", "tests/test_oracle_crc.py", "tests/test_oracle_grpc.py",
-          "tests/test_oracle_ttstream.py", "tests/test_oracle_frames.py", "tests/test_oracle_kat.py"]
-SLOW = ("persistent_loop", "slot_overflow", "slotcap_64", "deep_lookback", "25000", "chunked", "combo",
-        "index_prefetch")
+# the emulator and host-walker suites and the oracle suites closest to them; the emulator's long-running
+# cases (large persistent-loop and look-back batches, the chunked / combined experiments, the 25 000-frame
+# batch) and the gloo shard suite are left to the full sanitizer runs recorded in
+# profiles/r4_sanitizers_*.log (about 5x slower under ASan)
+SUITES = ["tests/test_emu_decode.py", "tests/test_nested.py", "tests/test_pbn.py", "tests/test_oracle_list_struct.py",
+          "tests/test_oracle_crc.py", "tests/test_oracle_kat.py"]
+SLOW = ("persistent_loop", "slotcap_64", "deep_lookback", "25000", "chunked", "combo", "index_prefetch", "many")
 
 
 def _asan_runtime():
