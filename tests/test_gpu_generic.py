@@ -87,3 +87,25 @@ def test_idl_schema_decode_matches_oracle(torch, oracle, idl_file, struct):
     for o in (torch.from_numpy(offs.astype(np.int64)).to("cuda:0"), None):
         res = cdc.Unmarshal(buf, n, offsets=o)
         assert_columns_equal(res.columns, exp, infos, n)
+
+
+@pytest.mark.parametrize("f", ["testservice.thrift", "http_binary_echo.thrift", "http_annotation.thrift",
+                               "http_baseline.thrift", "grpcjson_api.thrift"])
+def test_reference_fixture_methods_decode_encode_on_gpu(torch, oracle, f):
+    """every method's Args / Result of the reference's other IDL fixtures: concatenated decode on the GPU
+    equals the oracle's, and the GPU's encode of those columns equals the oracle's bytes"""
+    from kitex_amd import synth
+    from kitex_amd.codec import ThriftCodec
+    from tests.helpers import assert_columns_equal, to_np
+    from tests.test_idl import fixture_schemas
+    for name, sch in fixture_schemas(f):
+        n = 3000
+        wire = np.frombuffer(b"".join(synth.thrift_records(sch, n, seed=13)), dtype=np.uint8).copy()
+        rc, exp, est, _ = oracle.decode(sch, wire, n)
+        _, infos, _ = oracle.flatten(sch)
+        cdc = ThriftCodec(sch)
+        res = cdc.Unmarshal(torch.from_numpy(wire).to("cuda:0"), n)
+        assert_columns_equal(res.columns, exp, infos, n)
+        rc, ow, _ = oracle.encode(sch, exp)
+        got, _ = cdc.Marshal(res.columns)
+        assert np.array_equal(to_np(got), ow), name

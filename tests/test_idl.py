@@ -129,3 +129,51 @@ def test_list_of_fixed_structs_compiles():
         service S { void put(1: LS1 r) }
     """)
     assert _table_bytes(idl.request_schema(doc, "put")) == _table_bytes(S.schema_ls1())
+
+
+# the reference's other IDL fixtures (internal/mocks/thrift/testservice.thrift,
+# pkg/generic/http_test/idl/{binary_echo,http_annotation,baseline}.thrift, pkg/generic/grpcjson_test/idl/api.thrift,
+# copied as test data): streaming-mode and api.* annotations, i8, set<string>, map<i64, struct>, a string default
+REF_FIXTURES = ["testservice.thrift", "http_binary_echo.thrift", "http_annotation.thrift", "http_baseline.thrift",
+                "grpcjson_api.thrift"]
+
+
+def fixture_schemas(f):
+    doc = idl.parse_idl(os.path.join(IDL, f))
+    svc = doc.service()
+    out = []
+    for m in sorted(svc.functions):
+        fn = svc.functions[m]
+        out.append((m + ".req", idl.request_schema(doc, m)))
+        if fn.response.struct.fields:
+            out.append((m + ".resp", idl.to_schema(fn.response.struct)))
+    return out
+
+
+@pytest.mark.parametrize("f", REF_FIXTURES)
+def test_reference_fixture_methods_compile_and_decode(oracle, f):
+    """every method's Args and Result of the fixture compiles (kx_schema_create) and decodes on the kernel
+    source (the SIMT emulator for flat schemas, the host walker for nested ones) like the oracle; the
+    oracle's re-encode decodes back to the same columns"""
+    from kitex_amd import synth
+    from kitex_amd.codec import DeviceSchema
+    from tests.emu import emu
+    from tests.helpers import assert_columns_equal
+    for name, sch in fixture_schemas(f):
+        ds = DeviceSchema(sch)
+        rc, infos, npres = oracle.flatten(sch)
+        assert rc == 0 and ds.ncols == len(infos), name
+        n = 300
+        wire = np.frombuffer(b"".join(synth.thrift_records(sch, n, seed=9)), dtype=np.uint8).copy()
+        rc, exp, est, _ = oracle.decode(sch, wire, n)
+        assert rc == 0 and est.code == 0 and est.consumed == wire.size, name
+        if ds.nested:
+            rc2, got, gst, _ = emu.nested_decode(sch, infos, npres, wire, n)
+        else:
+            rc2, got, gst, _ = emu.decode(sch, infos, npres, wire, n)
+        assert gst.code == 0 and gst.n_records == n, name
+        assert_columns_equal(got, exp, infos, n)
+        rc, wire2, _ = oracle.encode(sch, exp)
+        rc, back, bst, _ = oracle.decode(sch, wire2, n)
+        assert bst.code == 0
+        assert_columns_equal(back, exp, infos, n)
