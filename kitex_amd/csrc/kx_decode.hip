@@ -1396,8 +1396,10 @@ __device__ __forceinline__ uint64_t pb_scan_segment(const Src& w, uint64_t seg_l
 // < 16 bytes of the input are read from global memory. The descriptor is built from wave-uniform
 // values (SGPRs); a chunk past num_records still writes its LDS slot (zeros), so the issue loop masks
 // the lanes past the window's end.
+template <int WB = WINB>
 __device__ __forceinline__ Src load_window(KParams& dp, LDS uint32_t* win, uint64_t lo, int lane, bool thrift,
                                            bool wait = true) {
+  constexpr int WL = (WB / 16 + 63) / 64;
   const uint64_t abs_in = (uint64_t)dp.in;
   const uint64_t wbase = (abs_in + kmin64(lo, dp.in_len)) & ~15ull;
   const uint64_t end = abs_in + dp.in_len;
@@ -1407,8 +1409,8 @@ __device__ __forceinline__ Src load_window(KParams& dp, LDS uint32_t* win, uint6
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(((uint64_t)bhi << 32) | blo), (short)0, __builtin_amdgcn_readfirstlane(wlen), 0x00020000);
 #pragma unroll
-  for (int k = 0; k < WIN_LOADS; k++)
-    if ((k + 1) * 64 <= WINB / 16 || k * 64 + lane < WINB / 16)
+  for (int k = 0; k < WL; k++)
+    if ((k + 1) * 64 <= WB / 16 || k * 64 + lane < WB / 16)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (LDS void*)(win + k * 256), 16, lane * 16, k * 1024, 0, 0);
   if (wait) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const KAS KxProgram* P = dp.prog;
@@ -2665,21 +2667,25 @@ __global__ void __launch_bounds__(NT, 4) index_kernel(DecParams dp_) {  // 4 wav
 // kernel of its own so that its registers are not those of the general walk; a tile the fast path
 // cannot index (a non-canonical record, a false-hit chain, a batch that starts with another signature,
 // the last partial tile) is queued for redo_kernel, which walks it with the general field loop ----
-template <int NV>
-__global__ void __launch_bounds__(NT, 4) index_fast_kernel(DecParams dp_) {
+// NARROW: batches whose halo is the default (dp.winb <= FWINB) take a window sized for it and 2-wave
+// workgroups, so that 18 waves fit a CU's LDS instead of 16
+constexpr int FWINB = TILE + HALO + 16, FWINW = FWINB / 4 + 4, FNT = 128, FWAVES = FNT / 64;
+template <int NV, bool NARROW>
+__global__ void __launch_bounds__(NARROW ? FNT : NT) index_fast_kernel(DecParams dp_) {
   KParams& dp = KX_PARAMS();
   (void)dp_;
-  __shared__ __attribute__((aligned(16))) uint32_t WIN[WAVES][WINW];
+  constexpr int WV = NARROW ? FWAVES : WAVES, WW = NARROW ? FWINW : WINW;
+  __shared__ __attribute__((aligned(16))) uint32_t WIN[WV][WW];
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
-  const uint64_t t = dp.t_lo + (uint64_t)blockIdx.x * WAVES + wv;
+  const uint64_t t = dp.t_lo + (uint64_t)blockIdx.x * WV + wv;
   if (t >= dp.t_hi) return;
   // a batch whose first record does not start with the canonical signature is left to redo_kernel whole
   // (no DMA here): the batch signature is one scalar load, a scalar-cache hit for all but a CU's first wave
   if (data_sig_s(dp) != dp.prog->sig) return;
   uint64_t lo, hi;
   tile_range(dp, t, lo, hi);
-  const Src w = load_window(dp, (LDS uint32_t*)WIN[wv], lo, lane, true, true);
+  const Src w = load_window<NARROW ? FWINB : WINB>(dp, (LDS uint32_t*)WIN[wv], lo, lane, true, true);
   Agg a;
   if (w.wlen >= TILE + 64 &&
       fast_tile<NV>(dp, w, lo, hi, t == 0 ? 0ull : X_NONE, lane, dp.starts + t * dp.slotcap, a)) {
@@ -3641,7 +3647,14 @@ int launch_fast_index(const DecParams& dp, unsigned grid, hipStream_t stream) {
           hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
         ncu = 0;
     }
-    hipLaunchKernelGGL((index_fast_kernel<NV>), dim3(grid), dim3(NT), 0, stream, dp);
+    static int narrow_env = -1;
+    if (narrow_env < 0) { const char* e = getenv("KX_FAST_NARROW"); narrow_env = e ? atoi(e) : 1; }
+    if (narrow_env && dp.winb <= (uint32_t)FWINB) {
+      const unsigned fgrid = (unsigned)((dp.ntiles + FWAVES - 1) / FWAVES);
+      hipLaunchKernelGGL((index_fast_kernel<NV, true>), dim3(fgrid), dim3(FNT), 0, stream, dp);
+    } else {
+      hipLaunchKernelGGL((index_fast_kernel<NV, false>), dim3(grid), dim3(NT), 0, stream, dp);
+    }
     if (hipGetLastError() != hipSuccess) return -1;
     // the queued tiles: one resident grid's worth of waves at most (4 workgroups per CU)
     const unsigned rgrid = (unsigned)kmin64(grid, (uint64_t)(ncu > 0 ? ncu : 64) * 4);
