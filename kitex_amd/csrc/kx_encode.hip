@@ -28,6 +28,11 @@ constexpr int RB = 1024;             // records per block
 #endif
 // tuning switches (A/B builds): list elements loaded in blocks of 4 (on: R3 encode 9.35 -> 6.35 ms on the
 // MI355X, R2 unchanged) / min waves per SIMD of the write pass (4 spills registers: no gain)
+// list<scalar> elements per block in the canonical writer (loads of a block all issued before the first
+// element is written)
+#ifndef KX_ENC_LISTB
+#define KX_ENC_LISTB 4
+#endif
 #ifndef KX_ENC_LISTPF
 #define KX_ENC_LISTPF 1
 #endif
@@ -55,6 +60,7 @@ struct EncParams {
   uint64_t nblocks;
   bool pb;               // Kitex-Protobuf records (Batch framing) instead of Thrift binary
   int direct;            // tuning (KX_ENC_DIRECT=1): every round writes straight to HBM
+  int wcu;               // tuning (KX_ENC_WCU): output dwords per lane in flight in the queue copy (1: per item)
 };
 
 // record offsets are 4 or 8 bytes wide (kx_column.offset_bytes)
@@ -263,7 +269,7 @@ __device__ __forceinline__ void wave_copy(const PayItem& it, int lane) {
   if (!total) return;
   const uint64_t d0 = it.dst, d1 = it.dst + total;
   const uint64_t A0 = d0 & ~3ull;
-  const uint64_t nd = ((d1 + 3) & ~3ull) - A0 >> 2;            // output dwords touched
+  const uint64_t nd = (((d1 + 3) & ~3ull) - A0) >> 2;          // output dwords touched
   const uint32_t sh = (uint32_t)(d0 & 3);                       // stream byte p sits at output A0 + sh + p
   for (uint64_t k = (uint64_t)lane; k < nd; k += 64) {
     // output dword k = stream bytes [4k - sh, 4k - sh + 4)
@@ -281,6 +287,77 @@ __device__ __forceinline__ void wave_copy(const PayItem& it, int lane) {
     } else {
       for (int j = 0; j < 4; j++)
         if (a + j >= d0 && a + j < d1) *(uint8_t*)(a + j) = (uint8_t)(v >> (8 * j));
+    }
+  }
+}
+
+// output dwords a payload touches
+__device__ __forceinline__ uint64_t item_dwords(const PayItem& it) {
+  const uint64_t total = (uint64_t)it.n * it.w;
+  if (!total) return 0;
+  const uint64_t d0 = it.dst, d1 = it.dst + total;
+  return (((d1 + 3) & ~3ull) - (d0 & ~3ull)) >> 2;
+}
+
+// every queued payload of the wave as one stream of output dwords (the payloads one after another):
+// lane l takes dwords base + 64u + l, u < U, all U loads issued before the first store, so a wave has U
+// (2U when unaligned) loads in flight instead of one per payload (wave_copy's loop waits on each load
+// before its store: a chain of about 2 memory round trips per list). pre: this wave's LDS array of
+// QCAP + 1 payload starts (in dwords).
+template <int U>
+__device__ __forceinline__ void wave_copy_queue(const PayItem* q, uint32_t nq, int lane, uint64_t* pre) {
+  const uint64_t n0 = (uint32_t)lane < nq ? item_dwords(q[lane]) : 0;
+  const uint64_t n1 = (uint32_t)lane + 64 < nq ? item_dwords(q[lane + 64]) : 0;
+  uint64_t i0 = n0, i1 = n1;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t o0 = __shfl_up(i0, d, 64), o1 = __shfl_up(i1, d, 64);
+    if (lane >= d) { i0 += o0; i1 += o1; }
+  }
+  const uint64_t t0 = __shfl(i0, 63, 64);
+  i1 += t0;
+  const uint64_t total = __shfl(i1, 63, 64);
+  if (lane == 0) pre[0] = 0;
+  pre[lane + 1] = i0;
+  pre[lane + 65] = i1;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  uint32_t it = 0;
+  for (uint64_t base = 0; base < total; base += 64 * U) {
+    uint32_t v[U], m[U];
+    uint64_t a[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint64_t j = base + 64 * u + (uint64_t)lane;
+      m[u] = 0;
+      v[u] = 0;
+      a[u] = 0;
+      if (j < total) {
+        while (pre[it + 1] <= j) it++;
+        const PayItem im = q[it];
+        const uint64_t k = j - pre[it];
+        const uint64_t d0 = im.dst, d1 = im.dst + (uint64_t)im.n * im.w;
+        const uint32_t sh = (uint32_t)(d0 & 3);
+        if (sh == 0) {
+          v[u] = be_stream_dword(im, k);
+        } else {
+          const uint32_t lo = k ? be_stream_dword(im, k - 1) : 0u;
+          v[u] = __builtin_amdgcn_alignbyte(be_stream_dword(im, k), lo, 4 - sh);
+        }
+        a[u] = (d0 & ~3ull) + 4 * k;
+#pragma unroll
+        for (int b = 0; b < 4; b++) m[u] |= (a[u] + b >= d0 && a[u] + b < d1) ? 1u << b : 0u;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      if (m[u] == 15u) {
+        *(uint32_t*)a[u] = v[u];
+      } else if (m[u]) {
+        for (int b = 0; b < 4; b++)
+          if ((m[u] >> b) & 1) *(uint8_t*)(a[u] + b) = (uint8_t)(v[u] >> (8 * b));
+      }
     }
   }
 }
@@ -586,12 +663,12 @@ __device__ __forceinline__ void write_canon(const KxProgram& P, const KxLaunchCo
     s.put(K.elem, 1);
     put_be(s, len, 4);
     const void* src = C.data[st.col];
-    for (uint32_t i0 = 0; i0 < len; i0 += 4) {
-      uint64_t V[4];
+    for (uint32_t i0 = 0; i0 < len; i0 += KX_ENC_LISTB) {
+      uint64_t V[KX_ENC_LISTB];
 #pragma unroll
-      for (int u = 0; u < 4; u++) V[u] = i0 + u < len ? load_fixed(src, K.width, o + i0 + u) : 0;
+      for (int u = 0; u < KX_ENC_LISTB; u++) V[u] = i0 + u < len ? load_fixed(src, K.width, o + i0 + u) : 0;
 #pragma unroll
-      for (int u = 0; u < 4; u++) {
+      for (int u = 0; u < KX_ENC_LISTB; u++) {
         if (i0 + u >= len) break;
         uint64_t x = V[u];
         if (K.elem == KX_T_BOOL) x = (x & 0xff) ? 1 : 0;
@@ -688,7 +765,7 @@ __global__ void __launch_bounds__(WT, KX_ENC_LB) write_kernel(EncParams ep) {
   __shared__ uint32_t qcnt[WT / 64];
   // the direct path's payload queues live in the (then unused) LDS image
   PayItem* qbase = (PayItem*)smem_raw;
-  static_assert((WT / 64) * QCAP * sizeof(PayItem) <= OUTB, "payload queues fit the image");
+  static_assert((WT / 64) * (QCAP * sizeof(PayItem) + (QCAP + 1) * 8) <= OUTB, "payload queues fit the image");
   if (ep.status->code != 0) return;                         // size limit: write nothing
   for (int i = threadIdx.x; i < (int)(sizeof(KxProgram) / 4); i += WT) progw[i] = ((const uint32_t*)ep.prog)[i];
   __syncthreads();
@@ -731,7 +808,11 @@ __global__ void __launch_bounds__(WT, KX_ENC_LB) write_kernel(EncParams ep) {
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
       const uint32_t nq = min(qcnt[wv], (uint32_t)QCAP);
-      for (uint32_t i = 0; i < nq; i++) wave_copy(qbase[wv * QCAP + i], lane);
+      uint64_t* pre = (uint64_t*)(smem_raw + (WT / 64) * QCAP * sizeof(PayItem)) + wv * (QCAP + 1);
+      if (ep.wcu == 0) {}  // diagnostics only (output incomplete): no payload copy
+      else if (ep.wcu == 8) wave_copy_queue<8>(qbase + wv * QCAP, nq, lane, pre);
+      else if (ep.wcu == 4) wave_copy_queue<4>(qbase + wv * QCAP, nq, lane, pre);
+      else for (uint32_t i = 0; i < nq; i++) wave_copy(qbase[wv * QCAP + i], lane);
       __syncthreads();
       gpos += tot;
       r += cnt;
@@ -786,6 +867,8 @@ int kx_launch_encode(const KxProgram* dprog, const KxProgram& hprog, const KxLau
   {
     const char* e = getenv("KX_ENC_DIRECT");
     ep.direct = e ? atoi(e) : 0;
+    const char* w = getenv("KX_ENC_WCU");
+    ep.wcu = w ? atoi(w) : 8;
   }
   if (ws_size < kx_encode_ws_bytes(n)) return KX_ERR_INVALID_ARG;
   ep.block_tot = (uint64_t*)ws;
