@@ -26,6 +26,7 @@
 
 #include "kx_internal.h"
 #include "kx_crc.h"
+#include "kx_mem.h"
 
 namespace {
 
@@ -100,7 +101,7 @@ __device__ void build_tabs(Tabs& T) {
 __device__ __forceinline__ uint64_t low_bytes(uint64_t v, uint32_t k) { return k >= 8 ? v : v & ((1ull << (8 * k)) - 1); }
 
 // the 16-byte aligned granule at p: it holds a byte of the range, so it lies inside mapped memory
-__device__ __forceinline__ uint4 ld_granule(const uint8_t* p) { return *(const uint4*)p; }
+__device__ __forceinline__ uint4 ld_granule(const uint8_t* p) { return kx_ld16(p); }
 
 // standard CRC-32C of in[a, b): 16-byte aligned granules (absolute addresses), two loads in flight
 // ahead of the fold; the bytes of a granule outside [a, b) are shifted / masked away, so every granule

@@ -18,6 +18,7 @@
 #include <type_traits>
 
 #include "kx_internal.h"
+#include "kx_mem.h"
 
 namespace {
 
@@ -28,6 +29,10 @@ constexpr int RB = 1024;             // records per block
 #endif
 // tuning switches (A/B builds): list elements loaded in blocks of 4 (on: R3 encode 9.35 -> 6.35 ms on the
 // MI355X, R2 unchanged) / min waves per SIMD of the write pass (4 spills registers: no gain)
+// output dwords per lane in flight in the direct path's payload copy
+#ifndef KX_ENC_WCU
+#define KX_ENC_WCU 4
+#endif
 // list<scalar> elements per block in the canonical writer (loads of a block all issued before the first
 // element is written)
 #ifndef KX_ENC_LISTB
@@ -37,9 +42,11 @@ constexpr int RB = 1024;             // records per block
 #define KX_ENC_LISTPF 1
 #endif
 // the write pass stages a round through the LDS image when at least cnt >> KX_ENC_MINTAKE of its records fit
-// (2: a quarter; measured R3 encode 5.91 -> 5.34 ms on the MI355X with the LDS sink, R2 unchanged)
+// (round 3, 2 = a quarter: R3 encode 5.91 -> 5.34 ms while the direct path copied one payload at a time;
+// round 4, 1 = half: with the streamed payload copy the direct path takes R3 in 3.22 ms against the
+// image's 5.30, R2 (303-byte records) stays on the image, 2.30 ms against 6.60 direct)
 #ifndef KX_ENC_MINTAKE
-#define KX_ENC_MINTAKE 2
+#define KX_ENC_MINTAKE 1
 #endif
 #ifndef KX_ENC_OUTB
 #define KX_ENC_OUTB (48 * 1024)
@@ -65,7 +72,7 @@ struct EncParams {
 
 // record offsets are 4 or 8 bytes wide (kx_column.offset_bytes)
 __device__ __forceinline__ uint64_t off_at(const KxLaunchCols& C, int col, uint64_t r) {
-  return ((C.owide >> col) & 1) ? ((const uint64_t*)C.offs[col])[r] : (uint64_t)((const uint32_t*)C.offs[col])[r];
+  return ((C.owide >> col) & 1) ? kx_ld((const uint64_t*)C.offs[col] + r) : (uint64_t)kx_ld((const uint32_t*)C.offs[col] + r);
 }
 
 __device__ __forceinline__ uint64_t var_len(const KxLaunchCols& C, int col, uint64_t r) {
@@ -74,7 +81,7 @@ __device__ __forceinline__ uint64_t var_len(const KxLaunchCols& C, int col, uint
 
 // LIST_BYTES columns: element byte offsets (same width as the record offsets)
 __device__ __forceinline__ uint64_t eoff_at(const KxLaunchCols& C, int col, uint64_t i) {
-  return ((C.owide >> col) & 1) ? ((const uint64_t*)C.eoffs[col])[i] : (uint64_t)((const uint32_t*)C.eoffs[col])[i];
+  return ((C.owide >> col) & 1) ? kx_ld((const uint64_t*)C.eoffs[col] + i) : (uint64_t)kx_ld((const uint32_t*)C.eoffs[col] + i);
 }
 
 // encoded bytes of elements [E, E + cnt) of a container column side: fixed width or strings
@@ -90,7 +97,7 @@ __device__ __forceinline__ uint64_t side_bytes(const KxProgram& P, const KxLaunc
 // register allocation of the write pass, which ran 2.4x slower for every schema with it compiled in)
 template <bool LS>
 __device__ __forceinline__ uint64_t record_size(const KxProgram& P, const KxLaunchCols& C, uint64_t r) {
-  uint64_t pres = C.presence ? C.presence[r] : 0;
+  uint64_t pres = C.presence ? kx_ld(C.presence + r) : 0;
   int inst = 0;
   int f = P.inst[0].enc_first;
   uint64_t sz = 0;
@@ -153,7 +160,7 @@ struct SinkT {
       head = 0;
     } else {
       *(typename std::conditional<std::is_same<B, LDSB>::value, __attribute__((address_space(3))) uint32_t,
-                                  uint32_t>::type*)(base + off) = v;
+                                  KX_GLOBAL uint32_t>::type*)(base + off) = v;
     }
     off += 4; acc >>= 32; n -= 4;
   }
@@ -170,7 +177,8 @@ struct SinkT {
   // the position of the next byte
   __device__ __forceinline__ uint64_t pos() const { return off + n; }
 };
-using Sink = SinkT<uint8_t>;   // global (the direct path)
+typedef KX_GLOBAL uint8_t GB;   // global output (global_store, not flat)
+using Sink = SinkT<GB>;        // global (the direct path)
 using LSink = SinkT<LDSB>;     // the LDS image
 
 template <class SK>
@@ -188,10 +196,10 @@ __device__ __forceinline__ void put_be(SK& s, uint64_t v, uint32_t w) {
 
 __device__ __forceinline__ uint64_t load_fixed(const void* base, uint32_t w, uint64_t i) {
   switch (w) {
-    case 1: return ((const uint8_t*)base)[i];
-    case 2: return ((const uint16_t*)base)[i];
-    case 4: return ((const uint32_t*)base)[i];
-    default: return ((const uint64_t*)base)[i];
+    case 1: return kx_ld((const uint8_t*)base + i);
+    case 2: return kx_ld((const uint16_t*)base + i);
+    case 4: return kx_ld((const uint32_t*)base + i);
+    default: return kx_ld((const uint64_t*)base + i);
   }
 }
 
@@ -208,7 +216,7 @@ __device__ __forceinline__ void put_bytes(SK& s, const uint8_t* src, uint32_t le
     const uint32_t units = min((len - done) >> 2, 16u);
     uint32_t W[17];
 #pragma unroll
-    for (int j = 0; j < 17; j++) W[j] = ((uint32_t)j <= units && A + 4 * j < se) ? *(const uint32_t*)(A + 4 * j) : 0u;
+    for (int j = 0; j < 17; j++) W[j] = ((uint32_t)j <= units && A + 4 * j < se) ? kx_ld((const uint32_t*)(A + 4 * j)) : 0u;
 #pragma unroll
     for (int u = 0; u < 16; u++)
       if ((uint32_t)u < units) s.put(sh ? __builtin_amdgcn_alignbyte(W[u + 1], W[u], sh) : W[u], 4);
@@ -247,20 +255,20 @@ __device__ __forceinline__ uint32_t be_stream_dword(const PayItem& it, uint64_t 
   const uint64_t b = 4 * i;
   if (b >= total) return 0u;
   if (it.w == 8) {
-    const uint64_t v = ((const uint64_t*)it.src)[i >> 1];
+    const uint64_t v = kx_ld<uint64_t>(it.src + 8 * (i >> 1));
     return __builtin_bswap32((i & 1) ? (uint32_t)v : (uint32_t)(v >> 32));
   }
-  if (it.w == 4) return __builtin_bswap32(((const uint32_t*)it.src)[i]);
+  if (it.w == 4) return __builtin_bswap32(kx_ld<uint32_t>(it.src + 4 * i));
   if (it.w == 2) {
-    const uint32_t lo = ((const uint16_t*)it.src)[2 * i];
-    const uint32_t hi = b + 2 < total ? ((const uint16_t*)it.src)[2 * i + 1] : 0u;
+    const uint32_t lo = kx_ld<uint16_t>(it.src + 4 * i);
+    const uint32_t hi = b + 2 < total ? kx_ld<uint16_t>(it.src + 4 * i + 2) : 0u;
     return ((lo >> 8) | ((lo & 0xff) << 8)) | (((hi >> 8) | ((hi & 0xff) << 8)) << 16);
   }
   // raw bytes: the source may be unaligned; never read past its last byte's dword
   const uint64_t a = it.src + b;
   const uint64_t A = a & ~3ull, end = it.src + total;
-  const uint32_t x0 = *(const uint32_t*)A;
-  const uint32_t x1 = A + 4 < end ? *(const uint32_t*)(A + 4) : 0u;
+  const uint32_t x0 = kx_ld<uint32_t>(A);
+  const uint32_t x1 = A + 4 < end ? kx_ld<uint32_t>(A + 4) : 0u;
   return __builtin_amdgcn_alignbyte(x1, x0, (uint32_t)(a & 3));
 }
 
@@ -283,10 +291,10 @@ __device__ __forceinline__ void wave_copy(const PayItem& it, int lane) {
     }
     const uint64_t a = A0 + 4 * k;
     if (a >= d0 && a + 4 <= d1) {
-      *(uint32_t*)a = v;
+      kx_st<uint32_t>(a, v);
     } else {
       for (int j = 0; j < 4; j++)
-        if (a + j >= d0 && a + j < d1) *(uint8_t*)(a + j) = (uint8_t)(v >> (8 * j));
+        if (a + j >= d0 && a + j < d1) kx_st<uint8_t>(a + j, (uint8_t)(v >> (8 * j)));
     }
   }
 }
@@ -323,43 +331,75 @@ __device__ __forceinline__ void wave_copy_queue(const PayItem* q, uint32_t nq, i
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  // Each output dword is two aligned source dwords, loaded unconditionally (addresses clamped into the
+  // payload) after the address arithmetic, and assembled only after all 2U loads are out: a load inside
+  // a data-dependent branch (be_stream_dword's width switch) is waited for inside that branch, which left
+  // one load in flight. i64 / i32 payloads: stream dword s is source dword s ^ 1 / s, byte-swapped;
+  // bytes: two aligned dwords around the stream position. i16 payloads (rare) are copied per payload
+  // after the stream.
   uint32_t it = 0;
   for (uint64_t base = 0; base < total; base += 64 * U) {
-    uint32_t v[U], m[U];
+    uint32_t d0[U], d1[U], m[U], mode[U];
+    int32_t r[U];
     uint64_t a[U];
 #pragma unroll
     for (int u = 0; u < U; u++) {
       const uint64_t j = base + 64 * u + (uint64_t)lane;
-      m[u] = 0;
-      v[u] = 0;
-      a[u] = 0;
-      if (j < total) {
-        while (pre[it + 1] <= j) it++;
-        const PayItem im = q[it];
-        const uint64_t k = j - pre[it];
-        const uint64_t d0 = im.dst, d1 = im.dst + (uint64_t)im.n * im.w;
-        const uint32_t sh = (uint32_t)(d0 & 3);
-        if (sh == 0) {
-          v[u] = be_stream_dword(im, k);
-        } else {
-          const uint32_t lo = k ? be_stream_dword(im, k - 1) : 0u;
-          v[u] = __builtin_amdgcn_alignbyte(be_stream_dword(im, k), lo, 4 - sh);
-        }
-        a[u] = (d0 & ~3ull) + 4 * k;
-#pragma unroll
-        for (int b = 0; b < 4; b++) m[u] |= (a[u] + b >= d0 && a[u] + b < d1) ? 1u << b : 0u;
+      const uint64_t jj = j < total ? j : total - 1;
+      while (pre[it + 1] <= jj) it++;
+      const PayItem im = q[it];
+      const uint64_t k = jj - pre[it];
+      const uint64_t tb = (uint64_t)im.n * im.w;              // >= 1: an empty payload owns no dword
+      const uint64_t o0 = im.dst, o1 = o0 + tb;
+      const int64_t qs = (int64_t)(4 * k) - (int64_t)(o0 & 3);  // stream byte under output byte 0
+      uint64_t x0, x1;
+      if (im.w <= 2) {
+        const uint64_t sp = im.src + (uint64_t)(qs > 0 ? qs : 0);
+        const uint64_t last = (im.src + tb - 1) & ~3ull;
+        x0 = sp & ~3ull;
+        x1 = x0 + 4 <= last ? x0 + 4 : last;
+        r[u] = (int32_t)((int64_t)(im.src + (uint64_t)qs) - (int64_t)x0);  // < 0 only at k = 0
+        mode[u] = 1;
+      } else {
+        const int64_t s0 = qs >= 0 ? qs >> 2 : -1;              // stream dwords s0, s0 + 1
+        const uint64_t nd = tb >> 2;                             // source dwords (tb % 4 == 0)
+        const uint64_t c0 = s0 < 0 ? 0 : (uint64_t)s0 < nd ? (uint64_t)s0 : nd - 1;
+        const uint64_t c1 = (uint64_t)(s0 + 1) < nd ? (uint64_t)(s0 + 1) : nd - 1;
+        const uint64_t f = im.w == 8 ? 1u : 0u;
+        x0 = im.src + 4 * (c0 ^ f);
+        x1 = im.src + 4 * (c1 ^ f);
+        r[u] = (int32_t)(qs - 4 * s0);
+        mode[u] = s0 < 0 ? 2u : 0u;                              // 2: stream dword s0 precedes the payload
       }
+      a[u] = (o0 & ~3ull) + 4 * k;
+      uint32_t mm = 0;
+#pragma unroll
+      for (int b = 0; b < 4; b++) mm |= (a[u] + b >= o0 && a[u] + b < o1) ? 1u << b : 0u;
+      m[u] = (j < total && im.w != 2) ? mm : 0u;
+      d0[u] = kx_ld<uint32_t>(x0);
+      d1[u] = kx_ld<uint32_t>(x1);
     }
 #pragma unroll
     for (int u = 0; u < U; u++) {
+      uint32_t v;
+      if (mode[u] == 1) {
+        const uint64_t W = (uint64_t)d0[u] | ((uint64_t)d1[u] << 32);
+        v = r[u] < 0 ? (uint32_t)(W << (-8 * r[u])) : (uint32_t)(W >> (8 * r[u]));
+      } else {
+        const uint64_t W = (uint64_t)(mode[u] == 2 ? 0u : __builtin_bswap32(d0[u])) |
+                           ((uint64_t)__builtin_bswap32(d1[u]) << 32);
+        v = (uint32_t)(W >> (8 * r[u]));
+      }
       if (m[u] == 15u) {
-        *(uint32_t*)a[u] = v[u];
+        kx_st<uint32_t>(a[u], v);
       } else if (m[u]) {
         for (int b = 0; b < 4; b++)
-          if ((m[u] >> b) & 1) *(uint8_t*)(a[u] + b) = (uint8_t)(v[u] >> (8 * b));
+          if ((m[u] >> b) & 1) kx_st<uint8_t>(a[u] + b, (uint8_t)(v >> (8 * b)));
       }
     }
   }
+  for (uint32_t i = 0; i < nq; i++)
+    if (q[i].w == 2) wave_copy(q[i], lane);
 }
 
 // queue a payload (false: the queue is full, the caller copies inline)
@@ -376,7 +416,7 @@ template <bool LS, class SK>
 __device__ __forceinline__ void write_record(const KxProgram& P, const KxLaunchCols& C, uint64_t r, SK& s,
                                              const PayQueue& pq) {
   constexpr bool GL = std::is_same<SK, Sink>::value;   // payload queueing: the global (direct) path only
-  uint64_t pres = C.presence ? C.presence[r] : 0;
+  uint64_t pres = C.presence ? kx_ld(C.presence + r) : 0;
   int inst = 0;
   int f = P.inst[0].enc_first;
   for (;;) {
@@ -535,7 +575,7 @@ __device__ __forceinline__ uint64_t pb_value(const KxpField& F, const KxLaunchCo
 }
 
 __device__ __forceinline__ uint64_t pb_body_size(const KxProgram& P, const KxLaunchCols& C, uint64_t r) {
-  const uint64_t pres = C.presence ? C.presence[r] : 0;
+  const uint64_t pres = C.presence ? kx_ld(C.presence + r) : 0;
   uint64_t sz = 0;
   for (int f = P.pb_first; f >= 0; f = P.f[f].pb_next) {
     const KxpField F = P.f[f];
@@ -564,7 +604,7 @@ template <class SK>
 __device__ __forceinline__ void pb_write_record(const KxProgram& P, const KxLaunchCols& C, uint64_t r, SK& s) {
   s.put(0x0Au, 1);
   put_uvarint(s, pb_body_size(P, C, r));
-  const uint64_t pres = C.presence ? C.presence[r] : 0;
+  const uint64_t pres = C.presence ? kx_ld(C.presence + r) : 0;
   for (int f = P.pb_first; f >= 0; f = P.f[f].pb_next) {
     const KxpField F = P.f[f];
     const bool expl = F.req == KX_REQ_OPTIONAL;
@@ -604,7 +644,7 @@ __device__ __forceinline__ uint64_t canon_size(const KxProgram& P, const KxLaunc
 }
 
 __device__ __forceinline__ bool is_canon(const KxProgram& P, const KxLaunchCols& C, uint64_t r) {
-  return !C.presence || (C.presence[r] & P.canon_pres) == P.canon_pres;
+  return !C.presence || (kx_ld(C.presence + r) & P.canon_pres) == P.canon_pres;
 }
 
 template <bool LS, bool CANON = false>
@@ -800,7 +840,7 @@ __global__ void __launch_bounds__(WT, KX_ENC_LB) write_kernel(EncParams ep) {
       __builtin_amdgcn_wave_barrier();
       const PayQueue pq{qbase + wv * QCAP, &qcnt[wv]};
       if (my < rend) {
-        Sink s(ep.out, gpos + pre);
+        Sink s((GB*)ep.out, gpos + pre);
         any_write<LS>(ep, P, my, s, ep.pb ? PayQueue{nullptr, nullptr} : pq);
         if (ep.offsets_out) ep.offsets_out[my] = gpos + pre;
       }
@@ -810,8 +850,7 @@ __global__ void __launch_bounds__(WT, KX_ENC_LB) write_kernel(EncParams ep) {
       const uint32_t nq = min(qcnt[wv], (uint32_t)QCAP);
       uint64_t* pre = (uint64_t*)(smem_raw + (WT / 64) * QCAP * sizeof(PayItem)) + wv * (QCAP + 1);
       if (ep.wcu == 0) {}  // diagnostics only (output incomplete): no payload copy
-      else if (ep.wcu == 8) wave_copy_queue<8>(qbase + wv * QCAP, nq, lane, pre);
-      else if (ep.wcu == 4) wave_copy_queue<4>(qbase + wv * QCAP, nq, lane, pre);
+      else if (ep.wcu >= 4) wave_copy_queue<KX_ENC_WCU>(qbase + wv * QCAP, nq, lane, pre);
       else for (uint32_t i = 0; i < nq; i++) wave_copy(qbase[wv * QCAP + i], lane);
       __syncthreads();
       gpos += tot;
@@ -836,11 +875,11 @@ __global__ void __launch_bounds__(WT, KX_ENC_LB) write_kernel(EncParams ep) {
     for (uint64_t c = threadIdx.x; c < nch; c += WT) {
       uint64_t ca = a0 + c * 16;
       if (ca >= gstart && ca + 16 <= gend) {
-        *(uint4*)ca = *(const uint4*)(img + c * 16);
+        kx_st16(ca, *(const uint4*)(img + c * 16));
       } else {
         for (int k = 0; k < 16; k++) {
           uint64_t x = ca + k;
-          if (x >= gstart && x < gend) *(uint8_t*)x = img[c * 16 + k];
+          if (x >= gstart && x < gend) kx_st<uint8_t>(x, img[c * 16 + k]);
         }
       }
     }
@@ -868,7 +907,7 @@ int kx_launch_encode(const KxProgram* dprog, const KxProgram& hprog, const KxLau
     const char* e = getenv("KX_ENC_DIRECT");
     ep.direct = e ? atoi(e) : 0;
     const char* w = getenv("KX_ENC_WCU");
-    ep.wcu = w ? atoi(w) : 8;
+    ep.wcu = w ? atoi(w) : 4;
   }
   if (ws_size < kx_encode_ws_bytes(n)) return KX_ERR_INVALID_ARG;
   ep.block_tot = (uint64_t*)ws;
