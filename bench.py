@@ -548,8 +548,9 @@ def extras(args, r2, dev, local):
         offs = b.offs.cpu()
         ok = all(crc32c_py(bytes(b.wire[int(offs[i]):int(offs[i + 1])].cpu().numpy())) == int(crc[i]) for i in pick)
         alg = b.in_bytes + 12 * b.n  # payload bytes + u64 offsets in + u32 CRC out
+        traffic, tnote = pmc_traffic("r2_crc")
         return {"ranges": b.n, "ranges_per_s": b.n * steps / t, "ms_per_step": t / steps * 1e3, "sample_ok": ok,
-                "roofline": roofline(alg, avg, "crc32c")}
+                "roofline": roofline(alg, avg, "crc32c", traffic, tnote)}
 
     def nested_entry(n=1 << 20, k=4096):
         """config-3-style nested records: baseline.thrift's Nesting (NestingMethod's request: list<Simple>,

@@ -31,6 +31,14 @@
 #else
 #define KXN_HD static inline
 #endif
+// global memory through address-space-1 pointers on the device pass (column arrays, the input and the
+// output are all global): the column pointers come out of the KxnCols struct in device memory, which the
+// compiler cannot prove global, and flat accesses also count on the LDS counter (kx_mem.h)
+#if defined(__HIP_DEVICE_COMPILE__)
+#define KXN_G(T) __attribute__((address_space(1))) T
+#else
+#define KXN_G(T) T
+#endif
 
 #define KXN_MAX_NODES 256
 #define KXN_MAX_FIELDS 192
@@ -313,26 +321,26 @@ KXN_HD int kxn_skip(B b, uint64_t len, uint64_t* n, uint32_t t, int maxdepth) {
 // ---------------------------------------------------------------------------------------------
 // column stores
 KXN_HD void kxn_put_arr(const KxnCols& C, int c, int k, uint64_t i, uint64_t v) {
-  if ((C.owide >> c) & 1) ((uint64_t*)C.arr[c][k])[i] = v;
-  else ((uint32_t*)C.arr[c][k])[i] = (uint32_t)v;
+  if ((C.owide >> c) & 1) ((KXN_G(uint64_t)*)C.arr[c][k])[i] = v;
+  else ((KXN_G(uint32_t)*)C.arr[c][k])[i] = (uint32_t)v;
 }
 KXN_HD uint64_t kxn_get_arr(const KxnCols& C, int c, int k, uint64_t i) {
-  return ((C.owide >> c) & 1) ? ((const uint64_t*)C.arr[c][k])[i] : (uint64_t)((const uint32_t*)C.arr[c][k])[i];
+  return ((C.owide >> c) & 1) ? ((const KXN_G(uint64_t)*)C.arr[c][k])[i] : (uint64_t)((const KXN_G(uint32_t)*)C.arr[c][k])[i];
 }
 KXN_HD void kxn_put_val(const KxnCols& C, int c, uint32_t w, uint64_t i, uint64_t v) {
   switch (w) {
-    case 1: ((uint8_t*)C.data[c])[i] = (uint8_t)v; break;
-    case 2: ((uint16_t*)C.data[c])[i] = (uint16_t)v; break;
-    case 4: ((uint32_t*)C.data[c])[i] = (uint32_t)v; break;
-    default: ((uint64_t*)C.data[c])[i] = v; break;
+    case 1: ((KXN_G(uint8_t)*)C.data[c])[i] = (uint8_t)v; break;
+    case 2: ((KXN_G(uint16_t)*)C.data[c])[i] = (uint16_t)v; break;
+    case 4: ((KXN_G(uint32_t)*)C.data[c])[i] = (uint32_t)v; break;
+    default: ((KXN_G(uint64_t)*)C.data[c])[i] = v; break;
   }
 }
 KXN_HD uint64_t kxn_get_val(const KxnCols& C, int c, uint32_t w, uint64_t i) {
   switch (w) {
-    case 1: return ((const uint8_t*)C.data[c])[i];
-    case 2: return ((const uint16_t*)C.data[c])[i];
-    case 4: return ((const uint32_t*)C.data[c])[i];
-    default: return ((const uint64_t*)C.data[c])[i];
+    case 1: return ((const KXN_G(uint8_t)*)C.data[c])[i];
+    case 2: return ((const KXN_G(uint16_t)*)C.data[c])[i];
+    case 4: return ((const KXN_G(uint32_t)*)C.data[c])[i];
+    default: return ((const KXN_G(uint64_t)*)C.data[c])[i];
   }
 }
 
@@ -351,16 +359,21 @@ KXN_HD uint64_t kxn_scalar(uint32_t t, B p) {  // host order; BOOL is `b == 1` (
 // reorder them itself: source and destination could alias), so a lane waits once per 16 bytes rather
 // than once per byte
 template <class S>
-KXN_HD void kxn_copy(uint8_t* dst, S src, uint64_t m) {
+KXN_HD uint8_t kxn_ld8(S s, uint64_t i) { return s[i]; }
+KXN_HD uint8_t kxn_ld8(const uint8_t* s, uint64_t i) { return ((const KXN_G(uint8_t)*)s)[i]; }
+
+template <class S>
+KXN_HD void kxn_copy(uint8_t* dst_, S src, uint64_t m) {
+  KXN_G(uint8_t)* dst = (KXN_G(uint8_t)*)dst_;
   uint64_t j = 0;
   for (; j + 16 <= m; j += 16) {
     uint8_t t[16];
 #pragma unroll
-    for (int k = 0; k < 16; k++) t[k] = src[j + k];
+    for (int k = 0; k < 16; k++) t[k] = kxn_ld8(src, j + k);
 #pragma unroll
     for (int k = 0; k < 16; k++) dst[j + k] = t[k];
   }
-  for (; j < m; j++) dst[j] = src[j];
+  for (; j < m; j++) dst[j] = kxn_ld8(src, j);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -415,14 +428,14 @@ KXN_HD void kxn_inst_end(const KxnProgram& P, const KxnCols& C, int R, uint64_t*
     if ((S.seen[L] >> D.sbit) & 1) continue;
     if (W)
       for (uint32_t j = 0; j < D.len; j++)
-        if (cur[D.cur] + j < S.lim[D.cur]) ((uint8_t*)C.data[D.col])[cur[D.cur] + j] = P.defb[D.off + j];
+        if (cur[D.cur] + j < S.lim[D.cur]) ((KXN_G(uint8_t)*)C.data[D.col])[cur[D.cur] + j] = P.defb[D.off + j];
     cur[D.cur] += D.len;
   }
   if (!W || !S.live[L]) return;
   if (L == 0) {
     if (C.presence) C.presence[S.idx[0]] = S.pres[0];
   } else if (RT.pres_col >= 0) {
-    ((uint64_t*)C.data[RT.pres_col])[S.idx[L]] = S.pres[L];
+    ((KXN_G(uint64_t)*)C.data[RT.pres_col])[S.idx[L]] = S.pres[L];
   }
 }
 
@@ -620,14 +633,14 @@ struct KxnEFrame {
 template <bool W>
 KXN_HD void kxn_out(uint8_t* out, uint64_t* pos, uint64_t v, int nbytes) {  // big-endian
   if (W)
-    for (int k = 0; k < nbytes; k++) out[*pos + k] = (uint8_t)(v >> (8 * (nbytes - 1 - k)));
+    for (int k = 0; k < nbytes; k++) ((KXN_G(uint8_t)*)out)[*pos + k] = (uint8_t)(v >> (8 * (nbytes - 1 - k)));
   *pos += (uint64_t)nbytes;
 }
 
 KXN_HD uint64_t kxn_pres_word(const KxnProgram& P, const KxnCols& C, int R, uint64_t e) {
   const KxnRoot& RT = P.root[R];
   if (RT.level == 0) return C.presence ? C.presence[e] : 0;
-  return RT.pres_col >= 0 ? ((const uint64_t*)C.data[RT.pres_col])[e] : 0;
+  return RT.pres_col >= 0 ? ((const KXN_G(uint64_t)*)C.data[RT.pres_col])[e] : 0;
 }
 
 // one value of node X at instance index e (level X.level); structs / containers push a frame
@@ -1025,11 +1038,11 @@ KXN_HD int kxn_pb_read_record(const KxnProgram& P, const KxnCols& C, B b, uint64
 template <bool W>
 KXN_HD void kxn_pb_put_uv(uint8_t* out, uint64_t* pos, uint64_t v) {
   while (v >= 0x80) {
-    if (W) out[*pos] = (uint8_t)(v | 0x80);
+    if (W) ((KXN_G(uint8_t)*)out)[*pos] = (uint8_t)(v | 0x80);
     (*pos)++;
     v >>= 7;
   }
-  if (W) out[*pos] = (uint8_t)v;
+  if (W) ((KXN_G(uint8_t)*)out)[*pos] = (uint8_t)v;
   (*pos)++;
 }
 
@@ -1059,7 +1072,7 @@ template <bool W>
 KXN_HD void kxn_pb_put_scalar(uint8_t* out, uint64_t* pos, uint64_t v, int fixed) {
   if (fixed) {
     if (W)
-      for (int k = 0; k < fixed; k++) out[*pos + k] = (uint8_t)(v >> (8 * k));
+      for (int k = 0; k < fixed; k++) ((KXN_G(uint8_t)*)out)[*pos + k] = (uint8_t)(v >> (8 * k));
     *pos += (uint64_t)fixed;
   } else {
     kxn_pb_put_uv<W>(out, pos, v);
@@ -1187,7 +1200,7 @@ KXN_HD uint64_t kxn_pb_walk(const KxnProgram& P, const KxnCols& C, KxnPEFrame st
             if (W) {
               kxn_pb_put_uv<W>(out, &pos, tag);
               kxn_pb_put_uv<W>(out, &pos, l);
-              for (uint64_t k = 0; k < l; k++) out[pos + k] = ((const uint8_t*)C.data[E.col])[sa + k];
+              for (uint64_t k = 0; k < l; k++) ((KXN_G(uint8_t)*)out)[pos + k] = ((const KXN_G(uint8_t)*)C.data[E.col])[sa + k];
               pos += l;
             } else {
               sz += kxn_uvlen(tag) + kxn_uvlen(l) + l;
@@ -1303,7 +1316,7 @@ KXN_HD void kxn_pb_write_frame(const KxnProgram& P, const KxnCols& C, uint64_t r
     body = frame_size - 1 - u;
     if (kxn_uvlen(body) == u) break;
   }
-  out[pos] = 0x0A;
+  ((KXN_G(uint8_t)*)out)[pos] = 0x0A;
   uint64_t p = pos + 1;
   kxn_pb_put_uv<true>(out, &p, body);
   (void)kxn_pb_walk<true>(P, C, KxnPEFrame{0, 0, (int16_t)si, P.st[si].enc_first, 0, 0, 0, r, 0, 0}, out, p);

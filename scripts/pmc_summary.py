@@ -4,6 +4,7 @@ WRITE_SIZE are in KiB; gfx950 FETCH_SIZE counts half of a wide streaming read ->
 
   python scripts/pmc_summary.py <gpurun_out/prof_TAG> <cfg> <mode>  -> profiles/pmc_<cfg>_<mode>.json
   mode "encode": the encode kernels (size pass, scan, write pass) of scripts/run_encode.py instead
+  mode "crc": the CRC32C Generate kernels of scripts/run_crc.py
 """
 import csv
 import glob
@@ -14,6 +15,7 @@ from collections import defaultdict
 
 DECODE = ("index_kernel", "index_fast_kernel", "redo_kernel", "group_kernel", "chain_kernel", "emit_kernel", "finalize_kernel")
 ENCODE = ("size_kernel", "scan_kernel", "write_kernel")
+CRC = ("crc_kernel", "crc_final_kernel")
 KERNELS = DECODE
 
 
@@ -38,8 +40,8 @@ def counter_sums(path, counter):
 def main():
     global KERNELS
     d, cfg, mode = sys.argv[1], sys.argv[2], sys.argv[3]
-    KERNELS = ENCODE if mode == "encode" else DECODE
-    last = "write_kernel" if mode == "encode" else "emit_kernel"
+    KERNELS = ENCODE if mode == "encode" else CRC if mode == "crc" else DECODE
+    last = "write_kernel" if mode == "encode" else "crc_kernel" if mode == "crc" else "emit_kernel"
     fetch = counter_sums(os.path.join(d, "fetch"), "FETCH_SIZE")
     write = counter_sums(os.path.join(d, "write"), "WRITE_SIZE")
     calls = len(fetch.get(last, [])) or 1
@@ -61,7 +63,7 @@ def main():
             sha = fh.read().strip()
     except OSError:
         pass
-    res = {"workload": f"{cfg}_encode" if mode == "encode" else f"{cfg}_decode_{mode}", "calls": calls, "lib_sha256": sha,
+    res = {"workload": f"{cfg}_{mode}" if mode in ("encode", "crc") else f"{cfg}_decode_{mode}", "calls": calls, "lib_sha256": sha,
            "hbm_bytes_per_launch": fetch_b + write_b, "fetch_bytes_per_call": fetch_b,
            "write_bytes_per_call": write_b, "per_kernel": per_kernel,
            "avg_ms": {k: sum(v) / len(v) for k, v in dur.items() if v},

@@ -18,6 +18,7 @@ for w in $WL; do
     r3_concat) CMD="bench.py --config r3 --records 4194304 --steps 5 --warmup 2 --no-cpu --no-host --no-extra";;
     r2_encode) CMD="scripts/run_encode.py r2 16777216 5";;
     r3_encode) CMD="scripts/run_encode.py r3 4194304 5";;
+    r2_crc) CMD="scripts/run_crc.py r2 16777216 5";;
     *) echo "unknown workload $w"; exit 2;;
   esac
   for pass in stats fetch write; do
