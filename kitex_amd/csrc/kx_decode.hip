@@ -845,6 +845,22 @@ __device__ __forceinline__ int pb_varint_f(const Fetch& f, uint64_t rem, uint64_
   return KX_OK;
 }
 
+// the same checks as pb_varint_f, the length alone (the index pass measures records: values unused)
+__device__ __forceinline__ int pb_varint_len_f(const Fetch& f, uint64_t rem, uint32_t& used) {
+  const uint64_t lo = (uint64_t)f.w0 | ((uint64_t)f.w1 << 32);
+  const uint64_t stop = ~lo & 0x8080808080808080ull;
+  const uint32_t b8 = f.w2 & 0xffu, b9 = (f.w2 >> 8) & 0xffu;
+  const uint32_t k = stop ? (uint32_t)__builtin_ctzll(stop) >> 3 : b8 < 0x80 ? 8u : b9 < 0x80 ? 9u : 10u;
+  if (k >= 9) {
+    if (rem <= 9) return KX_ERR_EOF;
+    if (b9 > 1) return KX_ERR_INVALID_DATA;
+  } else if ((uint64_t)k >= rem) {
+    return KX_ERR_EOF;
+  }
+  used = k + 1;
+  return KX_OK;
+}
+
 __device__ __forceinline__ int pb_varint(const Src& w, uint64_t p, uint64_t rem, uint64_t& v, uint32_t& used) {
   return pb_varint_f(fetch12(w, p), rem, v, used);
 }
@@ -891,12 +907,17 @@ __device__ __forceinline__ bool pb_utf8_ok(const Src& w, uint64_t p, uint64_t n)
     const int sh = q & 3;
     const int nd = (sh + (int)n + 3) >> 2;
     const int tail = (sh + (int)n) & 3;
-    uint32_t acc = 0;
-    for (int i = 0; i < nd; i++) {
-      uint32_t m = 0xffffffffu;
-      if (i == 0) m &= 0xffffffffu << (8 * sh);
-      if (i == nd - 1 && tail) m &= 0xffffffffu >> (8 * (4 - tail));
-      acc |= s[i] & m;
+    const uint32_t lm = tail ? 0xffffffffu >> (8 * (4 - tail)) : 0xffffffffu;
+    const uint32_t first = s[0] & (0xffffffffu << (8 * sh));
+    uint32_t acc;
+    if (nd == 1) {
+      acc = first & lm;
+    } else {  // the masked edge dwords, then the ones between with four independent ORs
+      uint32_t a0 = first, a1 = s[nd - 1] & lm, a2 = 0, a3 = 0;
+      int i = 1;
+      for (; i + 4 <= nd - 1; i += 4) { a0 |= s[i]; a1 |= s[i + 1]; a2 |= s[i + 2]; a3 |= s[i + 3]; }
+      for (; i < nd - 1; i++) a0 |= s[i];
+      acc = a0 | a1 | a2 | a3;
     }
     if (!(acc & 0x80808080u)) return true;
   }
@@ -1014,9 +1035,13 @@ __device__ __forceinline__ bool pb_canon(const Src& w, const KAS KxProgram* P, c
         uint64_t v;
         uint32_t u;
         if (S.kind == KXP_S_PB_VARINT) {
-          if (pb_varint_f(fv, rem, v, u)) return false;
-          if ((S.hdr >> 24) & 1u) v = v != 0;
-          if (emit) store_col(cols.data[S.col], S.width, rec, v);  // int32: low 32 bits
+          if (!emit) {  // measuring: the value is not needed
+            if (pb_varint_len_f(fv, rem, u)) return false;
+          } else {
+            if (pb_varint_f(fv, rem, v, u)) return false;
+            if ((S.hdr >> 24) & 1u) v = v != 0;
+            store_col(cols.data[S.col], S.width, rec, v);  // int32: low 32 bits
+          }
           pos += tl + u;
         } else if (S.kind == KXP_S_PB_FIXED64) {
           if (rem < 8) return false;

@@ -11,14 +11,14 @@ import torch  # noqa: E402
 from kitex_amd import _abi as A  # noqa: E402
 from kitex_amd import schema as S, synth  # noqa: E402
 from kitex_amd._lib import lib  # noqa: E402
-from kitex_amd.codec import ThriftCodec, status_tensor  # noqa: E402
+from kitex_amd.codec import ProtobufCodec, ThriftCodec, status_tensor  # noqa: E402
 from kitex_amd.columns import alloc_device  # noqa: E402
 
 cfg = sys.argv[1] if len(sys.argv) > 1 else "r2"
 n = int(sys.argv[2]) if len(sys.argv) > 2 else 16 << 20
 mode = sys.argv[3] if len(sys.argv) > 3 else "concat"
 dev = torch.device("cuda", 0)
-cdc = ThriftCodec(S.SCHEMAS[cfg]())
+cdc = ProtobufCodec(S.SCHEMAS[cfg]()) if cfg == "pf" else ThriftCodec(S.SCHEMAS[cfg]())  # pf: Kitex-Protobuf, as bench.py
 src = synth.TORCH_GENERATORS[cfg](n, dev)
 wire, offs = cdc.Marshal(src, with_offsets=True)
 infos = cdc.dschema.infos
