@@ -162,6 +162,7 @@ inline void emu_dma_lds16(uint32_t __attribute__((ext_vector_type(4))) rs, void*
   __builtin_amdgcn_raw_ptr_buffer_load_lds(emu_rsrc{base, (int32_t)rs.z}, dst, 16, (int)voff, (int)soff, 0, 0);
 }
 struct uint4 { uint32_t x, y, z, w; };
+inline uint4 make_uint4(uint32_t x, uint32_t y, uint32_t z, uint32_t w) { return uint4{x, y, z, w}; }
 inline int __ffsll(long long x) { return __builtin_ffsll(x); }
 inline int __clzll(long long x) { return x ? __builtin_clzll((unsigned long long)x) : 64; }
 
