@@ -33,6 +33,10 @@ constexpr int RB = 1024;             // records per block
 #ifndef KX_ENC_WCU
 #define KX_ENC_WCU 4
 #endif
+// 16-byte output chunks per lane in flight in the chunked payload copy (KX_ENC_WCU=16)
+#ifndef KX_ENC_WCU16
+#define KX_ENC_WCU16 4
+#endif
 // list<scalar> elements per block in the canonical writer (loads of a block all issued before the first
 // element is written)
 #ifndef KX_ENC_LISTB
@@ -67,7 +71,7 @@ struct EncParams {
   uint64_t nblocks;
   bool pb;               // Kitex-Protobuf records (Batch framing) instead of Thrift binary
   int direct;            // tuning (KX_ENC_DIRECT=1): every round writes straight to HBM
-  int wcu;               // tuning (KX_ENC_WCU): output dwords per lane in flight in the queue copy (1: per item)
+  int wcu;               // tuning (KX_ENC_WCU): the queue copy: 16 (default) 16-byte chunks, 4 dwords, 1 per item
 };
 
 // record offsets are 4 or 8 bytes wide (kx_column.offset_bytes)
@@ -395,6 +399,112 @@ __device__ __forceinline__ void wave_copy_queue(const PayItem* q, uint32_t nq, i
       } else if (m[u]) {
         for (int b = 0; b < 4; b++)
           if ((m[u] >> b) & 1) kx_st<uint8_t>(a[u] + b, (uint8_t)(v >> (8 * b)));
+      }
+    }
+  }
+  for (uint32_t i = 0; i < nq; i++)
+    if (q[i].w == 2) wave_copy(q[i], lane);
+}
+
+// 16-byte aligned output chunks a payload touches
+__device__ __forceinline__ uint64_t item_chunks(const PayItem& it) {
+  const uint64_t total = (uint64_t)it.n * it.w;
+  if (!total) return 0;
+  const uint64_t d0 = it.dst, d1 = it.dst + total;
+  return (((d1 + 15) & ~15ull) - (d0 & ~15ull)) >> 4;
+}
+
+// wave_copy_queue with 16-byte output units: lane l takes aligned chunks base + 64u + l, each assembled
+// from 5 aligned source dwords (i64 / i32: stream dword s = source dword s ^ 1 / s, byte-swapped; bytes:
+// the dwords around the chunk's first source byte) and stored with one 16-byte store when the chunk is
+// inside the payload (the chunks at a payload's two ends are stored dword / byte by byte).
+template <int U>
+__device__ __forceinline__ void wave_copy_queue16(const PayItem* q, uint32_t nq, int lane, uint64_t* pre) {
+  const uint64_t n0 = (uint32_t)lane < nq ? item_chunks(q[lane]) : 0;
+  const uint64_t n1 = (uint32_t)lane + 64 < nq ? item_chunks(q[lane + 64]) : 0;
+  uint64_t i0 = n0, i1 = n1;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t o0 = __shfl_up(i0, d, 64), o1 = __shfl_up(i1, d, 64);
+    if (lane >= d) { i0 += o0; i1 += o1; }
+  }
+  const uint64_t t0 = __shfl(i0, 63, 64);
+  i1 += t0;
+  const uint64_t total = __shfl(i1, 63, 64);
+  if (lane == 0) pre[0] = 0;
+  pre[lane + 1] = i0;
+  pre[lane + 65] = i1;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  uint32_t it = 0;
+  for (uint64_t base = 0; base < total; base += 64 * U) {
+    uint32_t x[U][5], bsw[U], r[U], lo[U], hi[U];
+    uint64_t a[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint64_t j = base + 64 * u + (uint64_t)lane;
+      const uint64_t jj = j < total ? j : total - 1;
+      while (pre[it + 1] <= jj) it++;
+      const PayItem im = q[it];
+      const uint64_t k = jj - pre[it];
+      const uint64_t tb = (uint64_t)im.n * im.w;
+      const uint64_t o0 = im.dst, o1 = o0 + tb;
+      a[u] = (o0 & ~15ull) + 16 * k;
+      const int64_t qs = (int64_t)(a[u] - o0);                 // stream byte under the chunk's byte 0
+      // chunk bytes [lo, hi) belong to the payload
+      lo[u] = qs < 0 ? (uint32_t)(-qs) : 0u;
+      const uint64_t endb = o1 - a[u];
+      hi[u] = (j < total && im.w != 2) ? (endb < 16 ? (uint32_t)endb : 16u) : 0u;
+      uint64_t ad[5];
+      if (im.w <= 2) {
+        const uint64_t sb = im.src + (uint64_t)qs;               // source byte under chunk byte 0
+        const uint64_t d0 = sb & ~3ull, first = im.src & ~3ull, last = (im.src + tb - 1) & ~3ull;
+#pragma unroll
+        for (int i = 0; i < 5; i++) {
+          const uint64_t d = d0 + 4 * (uint64_t)i;
+          ad[i] = (int64_t)(d - first) < 0 ? first : d > last ? last : d;
+        }
+        r[u] = (uint32_t)(sb & 3);
+        bsw[u] = 0;
+      } else {
+        const int64_t s0 = qs >= 0 ? qs >> 2 : -((-qs + 3) >> 2);  // floor(qs / 4)
+        const int64_t nd = (int64_t)(tb >> 2);
+        const uint64_t f = im.w == 8 ? 1u : 0u;
+#pragma unroll
+        for (int i = 0; i < 5; i++) {
+          const int64_t si = s0 + i;
+          const uint64_t c = si < 0 ? 0 : si >= nd ? (uint64_t)(nd - 1) : (uint64_t)si;
+          ad[i] = im.src + 4 * (c ^ f);
+        }
+        r[u] = (uint32_t)(qs - 4 * s0);
+        bsw[u] = 1;
+      }
+#pragma unroll
+      for (int i = 0; i < 5; i++) x[u][i] = kx_ld<uint32_t>(ad[i]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      if (lo[u] >= hi[u]) continue;
+      uint32_t y[5];
+#pragma unroll
+      for (int i = 0; i < 5; i++) y[i] = bsw[u] ? __builtin_bswap32(x[u][i]) : x[u][i];
+      uint32_t v[4];
+#pragma unroll
+      for (int i = 0; i < 4; i++) v[i] = __builtin_amdgcn_alignbyte(y[i + 1], y[i], r[u]);
+      if (lo[u] == 0 && hi[u] == 16) {
+        kx_st16(a[u], make_uint4(v[0], v[1], v[2], v[3]));
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          const uint32_t b0 = 4 * i;
+          if (b0 >= lo[u] && b0 + 4 <= hi[u]) {
+            kx_st<uint32_t>(a[u] + b0, v[i]);
+          } else {
+            for (uint32_t b = 0; b < 4; b++)
+              if (b0 + b >= lo[u] && b0 + b < hi[u]) kx_st<uint8_t>(a[u] + b0 + b, (uint8_t)(v[i] >> (8 * b)));
+          }
+        }
       }
     }
   }
@@ -850,6 +960,7 @@ __global__ void __launch_bounds__(WT, KX_ENC_LB) write_kernel(EncParams ep) {
       const uint32_t nq = min(qcnt[wv], (uint32_t)QCAP);
       uint64_t* pre = (uint64_t*)(smem_raw + (WT / 64) * QCAP * sizeof(PayItem)) + wv * (QCAP + 1);
       if (ep.wcu == 0) {}  // diagnostics only (output incomplete): no payload copy
+      else if (ep.wcu == 16) wave_copy_queue16<KX_ENC_WCU16>(qbase + wv * QCAP, nq, lane, pre);
       else if (ep.wcu >= 4) wave_copy_queue<KX_ENC_WCU>(qbase + wv * QCAP, nq, lane, pre);
       else for (uint32_t i = 0; i < nq; i++) wave_copy(qbase[wv * QCAP + i], lane);
       __syncthreads();
@@ -907,7 +1018,7 @@ int kx_launch_encode(const KxProgram* dprog, const KxProgram& hprog, const KxLau
     const char* e = getenv("KX_ENC_DIRECT");
     ep.direct = e ? atoi(e) : 0;
     const char* w = getenv("KX_ENC_WCU");
-    ep.wcu = w ? atoi(w) : 4;
+    ep.wcu = w ? atoi(w) : 16;
   }
   if (ws_size < kx_encode_ws_bytes(n)) return KX_ERR_INVALID_ARG;
   ep.block_tot = (uint64_t*)ws;
