@@ -52,9 +52,22 @@ struct Frame {
   uint32_t left;
 };
 
+// The innermost open frame lives in registers (`top`); only the frames below it go to the stack array,
+// which is private (scratch) memory: a record nested one level deep never touches it (with every frame
+// in the array, each field re-read its frame from scratch, a memory round trip per field).
 __device__ __forceinline__ int skip_value(const uint8_t* in, uint64_t& pos, uint64_t end, uint32_t t) {
   Frame st[MAXDEPTH];
-  int sp = 0;
+  Frame top = Frame{0, 0, 0, 0, 0};
+  int sp = 0;  // open frames: st[0 .. sp - 2], then top
+  auto push = [&](const Frame& f) {
+    if (sp > 0) st[sp - 1] = top;
+    top = f;
+    sp++;
+  };
+  auto pop = [&]() {
+    sp--;
+    if (sp > 0) top = st[sp - 1];
+  };
   uint32_t cur = t;
   for (;;) {
     const int w = fixed_size(cur);
@@ -69,7 +82,7 @@ __device__ __forceinline__ int skip_value(const uint8_t* in, uint64_t& pos, uint
       pos += 4 + (uint64_t)l;
     } else if (cur == KX_T_STRUCT) {
       if (sp == MAXDEPTH) return KX_ERR_DEPTH_LIMIT;
-      st[sp++] = Frame{0, 0, 0, 0, 0};
+      push(Frame{0, 0, 0, 0, 0});
     } else if (cur == KX_T_LIST || cur == KX_T_SET) {
       if (end - pos < 5) return KX_ERR_EOF;
       const uint32_t et = in[pos];
@@ -82,7 +95,7 @@ __device__ __forceinline__ int skip_value(const uint8_t* in, uint64_t& pos, uint
         pos += (uint64_t)sz * ew;
       } else if (sz) {
         if (sp == MAXDEPTH) return KX_ERR_DEPTH_LIMIT;
-        st[sp++] = Frame{1, (uint8_t)et, 0, 0, (uint32_t)sz};
+        push(Frame{1, (uint8_t)et, 0, 0, (uint32_t)sz});
       }
     } else if (cur == KX_T_MAP) {
       if (end - pos < 6) return KX_ERR_EOF;
@@ -96,7 +109,7 @@ __device__ __forceinline__ int skip_value(const uint8_t* in, uint64_t& pos, uint
         pos += (uint64_t)sz * (kw + vw);
       } else if (sz) {
         if (sp == MAXDEPTH) return KX_ERR_DEPTH_LIMIT;
-        st[sp++] = Frame{2, (uint8_t)kt, (uint8_t)vt, 0, (uint32_t)sz};
+        push(Frame{2, (uint8_t)kt, (uint8_t)vt, 0, (uint32_t)sz});
       }
     } else {
       return KX_ERR_INVALID_DATA;  // unknown data type
@@ -104,27 +117,26 @@ __device__ __forceinline__ int skip_value(const uint8_t* in, uint64_t& pos, uint
     // the next value to skip, from the innermost open frame
     for (;;) {
       if (sp == 0) return KX_OK;
-      Frame& f = st[sp - 1];
-      if (f.kind == 0) {
+      if (top.kind == 0) {
         if (pos >= end) return KX_ERR_EOF;
         const uint32_t ft = in[pos];
-        if (ft == KX_T_STOP) { pos++; sp--; continue; }
+        if (ft == KX_T_STOP) { pos++; pop(); continue; }
         if (end - pos < 3) return KX_ERR_EOF;
         pos += 3;
         cur = ft;
         break;
       }
-      if (f.left == 0) { sp--; continue; }
-      if (f.kind == 1) {
-        f.left--;
-        cur = f.t1;
-      } else if (f.phase == 0) {
-        f.phase = 1;
-        cur = f.t1;
+      if (top.left == 0) { pop(); continue; }
+      if (top.kind == 1) {
+        top.left--;
+        cur = top.t1;
+      } else if (top.phase == 0) {
+        top.phase = 1;
+        cur = top.t1;
       } else {
-        f.phase = 0;
-        f.left--;
-        cur = f.t2;
+        top.phase = 0;
+        top.left--;
+        cur = top.t2;
       }
       break;
     }
