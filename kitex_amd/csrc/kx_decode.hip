@@ -1024,7 +1024,6 @@ __device__ __forceinline__ bool pb_canon(const Src& w, const KAS KxProgram* P, c
   for (uint32_t k = 0; k < ns; k++) {
     const KxpStep S = ldk(&P->pbsteps[k]);
     const uint32_t tl = (S.hdr >> 16) & 3u;
-    const KxpCol K = ld_col(P, S.col);
     bool present = false;
     if (pos < limit) {
       const Fetch f = fetch12(w, pos);
@@ -1054,13 +1053,12 @@ __device__ __forceinline__ bool pb_canon(const Src& w, const KAS KxProgram* P, c
           vset<NV>(vs, S.vslot, b, (uint32_t)v);
           pos = b + v;
         }
-        if (K.field >= 0) {
-          const int8_t pb = ld_field(P, K.field).pbit;
-          if (pb >= 0) pres |= 1ull << pb;
-        }
+        const int pb = (int)(S.kind == KXP_S_PB_LEN ? S.width : S.vslot) - 1;  // kx_schema.cpp
+        if (pb >= 0) pres |= 1ull << pb;
       }
     }
-    if (!present && emit && S.kind != KXP_S_PB_LEN) store_col(cols.data[S.col], S.width, rec, (uint64_t)K.defv);
+    if (!present && emit && S.kind != KXP_S_PB_LEN)
+      store_col(cols.data[S.col], S.width, rec, (uint64_t)ld_col(P, S.col).defv);
   }
   if (pos != limit) return false;
   pres_out = pres;

@@ -338,9 +338,11 @@ int kx_build_program(const kx_struct_desc* structs, uint32_t nstructs, kx_schema
       T.hdr = tb | ((tag < 0x80 ? 1u : 2u) << 16) | ((F.ttype == KX_T_BOOL ? 1u : 0u) << 24) |
               ((F.flags & 1u) << 25);
       T.kind = F.pb_wt == 0 ? KXP_S_PB_VARINT : F.pb_wt == 1 ? KXP_S_PB_FIXED64 : KXP_S_PB_LEN;
-      T.width = F.width;
+      // the field's presence bit + 1 rides in the byte the step's kind leaves unused (LEN: width;
+      // VARINT / FIXED64: vslot), so a present field costs the decoder one descriptor load
+      T.width = T.kind == KXP_S_PB_LEN ? (uint8_t)(F.pbit + 1) : F.width;
       T.col = F.col;
-      T.vslot = F.vslot;
+      T.vslot = T.kind == KXP_S_PB_LEN ? F.vslot : (uint8_t)(F.pbit + 1);
     }
     if (ok) P.npbsteps = (uint32_t)ord.size();
   }
