@@ -1,4 +1,4 @@
-"""Summarise a scripts/profile_gpu.sh run into profiles/: per-kernel average duration (kernel trace)
+"""Summarise a scripts/profile_all.sh run into profiles/: per-kernel average duration (kernel trace)
 and HBM bytes per decode call from the PMC passes (MI355X_MICROARCH.md HBM section: FETCH_SIZE and
 WRITE_SIZE are in KiB; gfx950 FETCH_SIZE counts half of a wide streaming read -> x2).
 
