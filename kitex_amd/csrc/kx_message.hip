@@ -24,6 +24,7 @@
 #include <hip/hip_runtime.h>
 
 #include "kx_internal.h"
+#include "kx_mem.h"
 
 namespace {
 
@@ -52,10 +53,46 @@ struct Frame {
   uint32_t left;
 };
 
+// The header walk's bytes through a 16-byte aligned block held in registers: a field's type byte, ids and
+// lengths mostly lie in the block the previous field's read loaded, so the walk's chain of dependent global
+// byte loads (one per field) becomes one 16-byte load per block crossed. A read that straddles the block's
+// end is made byte by byte (and leaves the block as it is). An aligned 16-byte block never crosses a page,
+// so its bytes past the input are readable (and never used).
+struct HWin {
+  const uint8_t* in;
+  uint64_t base;        // absolute address of the block (16-aligned), ~0 before the first read
+  uint32_t d0, d1, d2, d3;
+  __device__ __forceinline__ uint32_t dw(uint32_t i) const { return i == 0 ? d0 : i == 1 ? d1 : i == 2 ? d2 : d3; }
+  __device__ __forceinline__ void fill(uint64_t a) {
+    base = a & ~15ull;
+    const uint4 v = kx_ld16((const void*)base);
+    d0 = v.x; d1 = v.y; d2 = v.z; d3 = v.w;
+  }
+  __device__ __forceinline__ uint32_t b(uint64_t p) {
+    const uint64_t a = (uint64_t)in + p;
+    if (a - base >= 16) fill(a);
+    const uint32_t o = (uint32_t)(a - base);
+    return (dw(o >> 2) >> (8 * (o & 3))) & 0xffu;
+  }
+  // 4 bytes at p, big-endian
+  __device__ __forceinline__ uint32_t be32(uint64_t p) {
+    const uint64_t a = (uint64_t)in + p;
+    if (a - base >= 16) fill(a);
+    const uint32_t o = (uint32_t)(a - base);
+    if (o + 4 <= 16) {
+      const uint32_t i = o >> 2;
+      const uint32_t lo = dw(i), hi = i < 3 ? dw(i + 1) : 0u;
+      return __builtin_bswap32(__builtin_amdgcn_alignbyte(hi, lo, o & 3));
+    }
+    const uint8_t* q = in + p;
+    return ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | q[3];
+  }
+};
+
 // The innermost open frame lives in registers (`top`); only the frames below it go to the stack array,
 // which is private (scratch) memory: a record nested one level deep never touches it (with every frame
 // in the array, each field re-read its frame from scratch, a memory round trip per field).
-__device__ __forceinline__ int skip_value(const uint8_t* in, uint64_t& pos, uint64_t end, uint32_t t) {
+__device__ __forceinline__ int skip_value(HWin& in, uint64_t& pos, uint64_t end, uint32_t t) {
   Frame st[MAXDEPTH];
   Frame top = Frame{0, 0, 0, 0, 0};
   int sp = 0;  // open frames: st[0 .. sp - 2], then top
@@ -76,7 +113,7 @@ __device__ __forceinline__ int skip_value(const uint8_t* in, uint64_t& pos, uint
       pos += w;
     } else if (cur == KX_T_STRING) {
       if (end - pos < 4) return KX_ERR_EOF;
-      const int32_t l = (int32_t)be32(in + pos);
+      const int32_t l = (int32_t)in.be32(pos);
       if (l < 0) return KX_ERR_NEGATIVE_SIZE;
       if (end - pos - 4 < (uint64_t)l) return KX_ERR_EOF;
       pos += 4 + (uint64_t)l;
@@ -85,8 +122,8 @@ __device__ __forceinline__ int skip_value(const uint8_t* in, uint64_t& pos, uint
       push(Frame{0, 0, 0, 0, 0});
     } else if (cur == KX_T_LIST || cur == KX_T_SET) {
       if (end - pos < 5) return KX_ERR_EOF;
-      const uint32_t et = in[pos];
-      const int32_t sz = (int32_t)be32(in + pos + 1);
+      const uint32_t et = in.b(pos);
+      const int32_t sz = (int32_t)in.be32(pos + 1);
       pos += 5;
       if (sz < 0) return KX_ERR_NEGATIVE_SIZE;
       const int ew = fixed_size(et);
@@ -99,8 +136,8 @@ __device__ __forceinline__ int skip_value(const uint8_t* in, uint64_t& pos, uint
       }
     } else if (cur == KX_T_MAP) {
       if (end - pos < 6) return KX_ERR_EOF;
-      const uint32_t kt = in[pos], vt = in[pos + 1];
-      const int32_t sz = (int32_t)be32(in + pos + 2);
+      const uint32_t kt = in.b(pos), vt = in.b(pos + 1);
+      const int32_t sz = (int32_t)in.be32(pos + 2);
       pos += 6;
       if (sz < 0) return KX_ERR_NEGATIVE_SIZE;
       const int kw = fixed_size(kt), vw = fixed_size(vt);
@@ -119,7 +156,7 @@ __device__ __forceinline__ int skip_value(const uint8_t* in, uint64_t& pos, uint
       if (sp == 0) return KX_OK;
       if (top.kind == 0) {
         if (pos >= end) return KX_ERR_EOF;
-        const uint32_t ft = in[pos];
+        const uint32_t ft = in.b(pos);
         if (ft == KX_T_STOP) { pos++; pop(); continue; }
         if (end - pos < 3) return KX_ERR_EOF;
         pos += 3;
@@ -240,18 +277,19 @@ __global__ void __launch_bounds__(MT) header_kernel(MsgParams mp) {
   } else if (!rc) {  // the Args / Result struct: fields until STOP, the record field kept, the rest skipped
     uint64_t pos = p + 12 + (uint64_t)nl;
     bool have = false;
+    HWin hw{in, ~0ull, 0u, 0u, 0u, 0u};
     for (;;) {
       if (pos >= e) { rc = KX_ERR_EOF; break; }
-      const uint32_t t = in[pos];
+      const uint32_t t = hw.b(pos);
       if (t == KX_T_STOP) {
         if (!have) { rs = pos; re = pos + 1; }  // no record field: an empty struct (the STOP byte)
         break;
       }
       if (e - pos < 3) { rc = KX_ERR_EOF; break; }
-      const int32_t id = (int16_t)(((uint32_t)in[pos + 1] << 8) | in[pos + 2]);
+      const int32_t id = (int16_t)((hw.b(pos + 1) << 8) | hw.b(pos + 2));
       pos += 3;
       const uint64_t s0 = pos;
-      rc = skip_value(in, pos, e, t);
+      rc = skip_value(hw, pos, e, t);
       if (rc) break;
       if (id == mp.body_field && t == KX_T_STRUCT) { rs = s0; re = pos; have = true; }
     }
