@@ -241,6 +241,14 @@ def roofline(alg_bytes, avg_launch_s, kernel, traffic=None, note=None):
     return r
 
 
+_T0 = time.perf_counter()
+
+
+def note(msg: str):
+    """progress on stderr (the JSON line alone goes to stdout): long runs stay visibly alive"""
+    print(f"[bench {time.perf_counter() - _T0:7.1f}s] {msg}", file=sys.stderr, flush=True)
+
+
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -281,7 +289,9 @@ def run_single(args, world, rank, dev, local):
     st = b.status()
     assert st.code == 0 and st.n_records == n, f"decode failed: code={st.code} n={st.n_records}"
 
+    note(f"{cfg} {args.mode}: {n} records ready, timing")
     t_rank, per = time_steps(b.step, args.steps, args.warmup, world, dev)
+    note(f"headline: {t_rank / args.steps * 1e3:.3f} ms per step")
     st = b.status()
     ok = b.verify()
     if world > 1:
@@ -328,10 +338,12 @@ def run_single(args, world, rank, dev, local):
     if concat is not None:
         result["concat"] = concat
     if rank == 0 and world == 1 and not args.no_host and cfg != "pf":
+        note("host-inclusive paths")
         result["host_inclusive"] = host_inclusive(b, dev)
     if world == 1 and not args.no_extra:
         result["extra"] = extras(args, b if cfg == "r2" else None, dev, local)
     if rank == 0 and world == 1 and not args.no_cpu:
+        note("cpu baseline")
         result["cpu_baseline"] = cpu_baseline(cfg, args.cpu_records)
         if result["cpu_baseline"].get("value"):
             result["cpu_baseline"]["gpu_speedup"] = value / result["cpu_baseline"]["value"]
@@ -552,21 +564,36 @@ def extras(args, r2, dev, local):
         return {"ranges": b.n, "ranges_per_s": b.n * steps / t, "ms_per_step": t / steps * 1e3, "sample_ok": ok,
                 "roofline": roofline(alg, avg, "crc32c", traffic, tnote)}
 
-    def nested_entry(n=1 << 20, k=4096):
-        """config-3-style nested records: baseline.thrift's Nesting (NestingMethod's request: list<Simple>,
-        map<string,Simple>, map<i32,i64>, list<string>, ...; tests/golden/idl/baseline.thrift) on the nested
-        walker (lane = record), decode + encode. k distinct host-written records tiled to n on the device."""
+    def nested_entry(n=1 << 20, k=4096, pb=False):
+        """config-3-style nested records on the nested walker (lane = record), decode + encode; k distinct
+        host-written records tiled to n on the device. Thrift: baseline.thrift's Nesting (NestingMethod's
+        request: list<Simple>, map<string,Simple>, map<i32,i64>, list<string>, ...; tests/golden/idl/
+        baseline.thrift). pb: the nested Kitex-Protobuf test message PN (tests/pbn_cases.py: zig-zag, fixed,
+        packed repeated, nested and repeated messages, maps with message values), Batch-framed. Beside it the
+        oracle's nested FastRead / proto.Unmarshal on the host's threads (nested_cpu_baseline)."""
         import numpy as np
 
         from kitex_amd import idl, synth
-        from kitex_amd.codec import ThriftCodec, read_status
+        from kitex_amd.codec import ProtobufCodec, ThriftCodec, read_status
         from kitex_amd.columns import alloc_device
-        doc = idl.parse_idl(os.path.join(os.path.dirname(os.path.abspath(__file__)), "tests", "golden", "idl",
-                                         "baseline.thrift"))
-        sch = idl.to_schema(doc.struct("Nesting"))
-        cdc = ThriftCodec(sch, device=local)
+        if pb:
+            from tests import pbn_cases as PB
+            sch = PB.schema_pn()
+            cdc = ProtobufCodec(sch, device=local)
+            _, bodies_np, boffs = PB.batch(k, seed=7, name="PN")
+            lens = np.diff(boffs).astype(np.int64)
+            framed = [b"\x0a" + PB.uvarint(int(x)) for x in lens]
+            recs = [framed[i] + bodies_np[int(boffs[i]):int(boffs[i + 1])].tobytes() for i in range(k)]
+            cpu_recs = [bodies_np[int(boffs[i]):int(boffs[i + 1])].tobytes() for i in range(k)]   # bare bodies
+        else:
+            doc = idl.parse_idl(os.path.join(os.path.dirname(os.path.abspath(__file__)), "tests", "golden", "idl",
+                                             "baseline.thrift"))
+            sch = idl.to_schema(doc.struct("Nesting"))
+            cdc = ThriftCodec(sch, device=local)
+            recs = synth.thrift_records(sch, k, seed=7)
+            cpu_recs = recs
         ds = cdc.dschema
-        one = np.frombuffer(b"".join(synth.thrift_records(sch, k, seed=7)), dtype=np.uint8).copy()
+        one = np.frombuffer(b"".join(recs), dtype=np.uint8).copy()
         wire = torch.from_numpy(one).to(dev).repeat(n // k)
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
         ev[0].record()
@@ -592,6 +619,7 @@ def extras(args, r2, dev, local):
         out_bytes = sum(x.numel() * x.element_size() for x in tensors(outc))
         avg = sum(per) / len(per) / 1e3
         res = {"records": n, "distinct_records": k, "wire_bytes_per_record": wire.numel() / n,
+               "schema": "PN (tests/pbn_cases.py), Batch-framed" if pb else "Nesting (baseline.thrift)",
                "decode": {"records_per_s": n * steps / t, "ms_per_step": t / steps * 1e3, "verified": ok,
                           "sizes_pass_ms": sizes_ms,
                           "roofline": roofline(wire.numel() + out_bytes, avg, "nested decode (measure + write)")}}
@@ -608,6 +636,11 @@ def extras(args, r2, dev, local):
         res["encode"] = {"records_per_s": n * steps / t, "ms_per_step": t / steps * 1e3,
                          "round_trip_equal": eq and bool(torch.equal(buf, w2)),
                          "roofline": roofline(out_bytes + buf.numel(), avg, "nested encode (size + write)")}
+        if not args.no_cpu:
+            cb = nested_cpu_baseline(sch, cpu_recs, n, pb)
+            if cb.get("value"):
+                cb["gpu_speedup"] = res["decode"]["records_per_s"] / cb["value"]
+            res["cpu_baseline"] = cb
         return res
 
     def frames_entry(n=16 << 20):
@@ -660,17 +693,26 @@ def extras(args, r2, dev, local):
         return res
 
     try:
+        note("extra: frames")
         out["frames_crc32c"] = frames_entry()
         torch.cuda.empty_cache()
     except Exception as e:
         out["frames_crc32c"] = {"error": repr(e)}
     try:
+        note("extra: nested")
         out["nested_decode_encode"] = nested_entry()
         torch.cuda.empty_cache()
     except Exception as e:
         out["nested_decode_encode"] = {"error": repr(e)}
     try:
+        note("extra: nested Kitex-Protobuf")
+        out["pb_nested"] = nested_entry(pb=True)
+        torch.cuda.empty_cache()
+    except Exception as e:
+        out["pb_nested"] = {"error": repr(e)}
+    try:
         if r2 is not None:
+            note("extra: r2 encode, crc, views, offsets")
             out["r2_encode"] = {"records": r2.n, **encode_entry(r2)}
             out["crc32c_generate"] = crc_entry(r2)
             bv = Batch("r2", r2.n, dev, 0, "concat", local, views=True)
@@ -700,6 +742,7 @@ def extras(args, r2, dev, local):
                                               **e}
             del bov
             torch.cuda.empty_cache()
+        note("extra: r3, pf")
         b3 = Batch("r3", 4 << 20, dev, 0, "concat", local)
         out["r3_decode"] = {"records": b3.n, "wire_bytes_per_record": b3.in_bytes / b3.n, **decode_entry(b3)}
         out["r3_encode"] = {"records": b3.n, **encode_entry(b3)}
@@ -712,6 +755,64 @@ def extras(args, r2, dev, local):
     except Exception as e:  # the extras must never break the headline line
         out["error"] = repr(e)
     return out
+
+
+def nested_cpu_baseline(sch, recs, n, pb):
+    """The oracle's nested decode (oracle/kx_oracle_nested.c: FastRead / proto.Unmarshal into a value tree,
+    then flattened) over n records (the k distinct ones tiled) with message offsets known, split into one
+    record range per host thread, each decoded into its own preallocated columns (ctypes releases the GIL:
+    the threads run in parallel); the concatenation of the ranges is not timed, as the GPU's is not."""
+    try:
+        import ctypes as C
+        from concurrent.futures import ThreadPoolExecutor
+
+        import numpy as np
+
+        from kitex_amd import _abi as A
+        from kitex_amd.columns import alloc_host, to_kx_columns
+        from oracle import oracle
+        oracle.build()
+        L = oracle.lib()
+        threads = max(1, min(len(os.sched_getaffinity(0)), 256))
+        k = len(recs)
+        lens = np.array([len(r) for r in recs], dtype=np.uint64)
+        one = np.frombuffer(b"".join(recs), dtype=np.uint8)
+        reps = n // k
+        wire = np.tile(one, reps)
+        offs = np.zeros(n + 1, dtype=np.uint64)
+        offs[1:] = np.cumsum(np.tile(lens, reps))
+        rc, infos, npres = oracle.flatten(sch)
+        tab, ns = sch.struct_table()
+        fn = L.kxo_pb_decode if pb else L.kxo_thrift_decode
+        jobs = []
+        for t in range(threads):
+            a, b = n * t // threads, n * (t + 1) // threads
+            if a == b:
+                continue
+            base = int(offs[a])
+            so = (offs[a:b + 1] - offs[a]).astype(np.uint64)
+            nb = int(offs[b]) - base
+            caps = [0 if ci.kind == A.COL_FIXED else max(1, nb) for ci in infos]
+            out = alloc_host(infos, b - a, caps, npres, elem_caps=caps, sub_caps=caps)
+            kc = to_kx_columns(out, infos, caps)
+            jobs.append((wire.ctypes.data + base, nb, so, b - a, kc, A.Status(), np.zeros(b - a, dtype=np.uint8), out))
+
+        def run(j):
+            d, nb, so, m, kc, st, rs, _ = j
+            return fn(tab, ns, d, nb, so.ctypes.data, m, C.byref(kc), rs.ctypes.data, C.byref(st)), st.code
+        best = 1e30
+        with ThreadPoolExecutor(max_workers=threads) as ex:
+            for _ in range(2):
+                t0 = time.perf_counter()
+                got = list(ex.map(run, jobs))
+                best = min(best, time.perf_counter() - t0)
+        ok = all(r == 0 and c == 0 for r, c in got)
+        return {"value": n / best, "unit": "records/s", "cores": threads, "kind": "port", "verified": ok,
+                "sample": f"{n} records ({k} distinct, tiled), nested {'proto.Unmarshal' if pb else 'FastRead'} "
+                          f"restatement (oracle/kx_oracle_nested.c) with message offsets known, one record range "
+                          f"per thread, best of 2, {threads} threads"}
+    except Exception as e:  # never break the bench line
+        return {"error": repr(e)}
 
 
 def crc32c_py(data: bytes) -> int:
@@ -790,6 +891,39 @@ def host_inclusive(b, dev):
         sbest = min(sbest, time.perf_counter() - t0)
     res["serial_concat"] = {"records_per_s": n / sbest, "ms": sbest * 1e3,
                             "note": "concatenated batch (no offsets): pinned H2D, decode, D2H serial on one stream"}
+    # latency of a 64 Ki-record batch (16 chunks of 4096 records): decode k + 1 queued before the host reads
+    # chunk k's status (default) vs queued after it (KX_HOST_SERIAL=1, the round-4 schedule)
+    k64 = min(n, 1 << 16)
+    sub_off = np.ascontiguousarray(off_np[:k64 + 1])
+    sub_in = wire_np[:int(sub_off[k64])]
+    lat = {}
+    for mode, env in (("pipelined", "0"), ("serial_host_sync", "1")):
+        os.environ["KX_HOST_SERIAL"] = env
+        ts = []
+        for _ in range(30):
+            t0 = time.perf_counter()
+            b.cdc.UnmarshalHost(sub_in, k64, offsets=sub_off, var_caps=b.var_caps, out=hout, raise_on_error=False)
+            ts.append(time.perf_counter() - t0)
+        lat[mode] = {"median_ms": sorted(ts)[len(ts) // 2] * 1e3, "min_ms": min(ts) * 1e3}
+    os.environ.pop("KX_HOST_SERIAL", None)
+    res["latency_64k"] = dict(lat, records=k64)
+    # the reply path: kx_host_encode_batch from the pinned host columns just decoded back to a pinned wire
+    h_wire = pinned(b.wire.numel(), torch.uint8).numpy()
+    h_eoff = pinned(n + 1, torch.int64).numpy().view(np.uint64)
+    ebest = 1e30
+    for _ in range(4):
+        t0 = time.perf_counter()
+        w, _, est = b.cdc.MarshalHost(hout, out=h_wire, with_offsets=False, raise_on_error=False)
+        ebest = min(ebest, time.perf_counter() - t0)
+    eok = est.code == 0 and est.consumed == b.wire.numel()
+    eok &= bool(np.array_equal(h_wire, wire_np[:b.wire.numel()]))
+    del h_eoff
+    res["encode"] = {"records_per_s": n / ebest, "ms": ebest * 1e3, "h2d_bytes": out_bytes,
+                     "d2h_bytes": b.wire.numel(), "pcie_gb_s": (b.wire.numel() + out_bytes) / ebest / 1e9,
+                     "verified": eok,
+                     "note": "kx_host_encode_batch: pinned host columns -> pinned host wire, 16-chunk pipeline "
+                             "(H2D of the columns / encode / D2H of the wire overlap; each chunk's output placed "
+                             "by the previous chunk's device status)"}
     return res
 
 

@@ -31,6 +31,12 @@
  *   kx_host_decode_batch ........ fastUnmarshal end to end from host (netpoll) memory: pinned H2D ->
  *                                 decode -> D2H (codec_fast.go:60-82 with the Next(dataLen) slice);
  *                                 kx_host_pb_decode_batch the same for protobufCodec.Unmarshal bodies
+ *   kx_host_encode_batch ........ fastMarshal end to end to host memory: H2D of the columns -> encode ->
+ *                                 D2H of the wire (codec_fast.go:40-58; thrift.go:106-160); kx_host_pb_
+ *                                 encode_batch the same for protobufCodec.Marshal (protobuf.go:64-134)
+ *   kx_shard_meta / kx_concat_plan / kx_concat_rebase: the concatenation of record-range shards decoded
+ *                                 on several GPUs into one (the reference has no
+ *                                 multi-device path, its caller partitions: pkg/remote/payload_codec.go:29-33)
  *   kx_thrift_encode_messages ... fastMarshal (codec_fast.go:40-58) over N messages: MessageBegin + Args wrapper
  *                                 + record + STOP on the device
  *   kx_thrift_decode_messages ... thriftCodec.Unmarshal over N framed messages (thrift.go:180-225):
@@ -58,7 +64,8 @@
 extern "C" {
 #endif
 
-#define KX_ABI_VERSION 5  /* 5: kx_status.var_total holds 16 var slots; kx_thrift_split_points */
+#define KX_ABI_VERSION 6  /* 6: shard concatenation (kx_shard_meta, kx_concat_plan, kx_concat_rebase);
+                             5: kx_status.var_total holds 16 var slots; kx_thrift_split_points */
 
 /* ---- Thrift TType ids (gopkg protocol/thrift; pinned by pkg/protocol/bthrift/binary_test.go) ---- */
 enum {
@@ -340,6 +347,61 @@ int kx_thrift_skip_batch(kx_ctx* c, const uint8_t* in, uint64_t in_len, uint64_t
 int kx_thrift_split_points(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len, uint64_t n,
                            uint32_t parts, uint64_t* points_out, kx_status* status, void* stream);
 
+/* ---- multi-GPU record-range shards: concatenation of decoded shards into one rank ----
+ * The reference has no multi-device path (its caller partitions; pkg/remote/payload_codec.go:29-33 is the
+ * per-message surface); this is the exchange a host runs after every rank decoded its record range:
+ *   1. kx_shard_meta on every rank: its exchange header (device u64[kx_shard_meta_words(...)]);
+ *   2. all-gather of the headers (ncclAllGather), copied to host on the root as metas[world][words];
+ *   3. kx_concat_plan on the root: the pieces every rank sends (in piece order) and where they land,
+ *      and the root's array sizes; the root allocates its output columns (8-byte offsets, 8-byte views);
+ *   4. ncclGroupStart; per piece ncclSend on its rank / ncclRecv on the root; ncclGroupEnd. A piece of
+ *      an offsets array (array < 3, or a view column's pairs) lands in the root's STAGING column
+ *      (senders' offset width), every other piece in the output column;
+ *   5. kx_concat_rebase on the root: staging offsets + the rank's rebase -> output, closing entries.
+ * Header layout: [n, in_len, then per non-FIXED column in column order, per level j of its offsets chain
+ * (depth 1 for BYTES / LIST, 2 for LIST_BYTES / LIST2, 3 for LIST2_BYTES) the first entry f_j and the units
+ * u_j it spans: f_0 = offsets[0], u_0 = offsets[n] - f_0, f_{j+1} = next[f_j], u_{j+1} = next[f_j + u_j] -
+ * f_{j+1}] (a view column's words are 0). Every rank must give its columns the same offset_bytes / flags. */
+#define KX_PIECE_OFFSETS 0u       /* kx_column.offsets (a view column: its (offset, length) pairs) */
+#define KX_PIECE_ELEM_OFFSETS 1u  /* kx_column.elem_offsets */
+#define KX_PIECE_SUB_OFFSETS 2u   /* kx_column.sub_offsets */
+#define KX_PIECE_DATA 3u          /* kx_column.data (FIXED values, arenas); presence words: column == KX_MAX_COLUMNS */
+typedef struct kx_concat_piece {
+  uint32_t rank;        /* sender */
+  uint32_t column;      /* schema column, or KX_MAX_COLUMNS for the presence words */
+  uint32_t array;       /* KX_PIECE_* */
+  uint32_t elem_bytes;  /* bytes per element of the piece (the sender's width) */
+  uint64_t src_first;   /* first element in the sender's array */
+  uint64_t count;       /* elements */
+  uint64_t dst_first;   /* first element in the root's array (staging for offsets / view pieces) */
+  int64_t rebase;       /* offsets: added to every entry; views: input bytes before this rank (added to a
+                           non-empty view's offset); 0 otherwise */
+} kx_concat_piece;
+typedef struct kx_concat_sizes {
+  uint64_t n;                          /* records of the concatenation */
+  uint64_t in_len;                     /* input bytes of all ranks (views point into their concatenation) */
+  uint64_t units[KX_MAX_COLUMNS][4];   /* per column and KX_PIECE_* array: entries before the closing one
+                                          (offsets arrays hold units + 1 entries; data: its elements) */
+} kx_concat_sizes;
+/* infos / ncols: kx_schema_column_info of every column of the schema (host memory), which is all the
+ * concatenation needs to know of it. */
+uint32_t kx_shard_meta_words(const kx_column_info* infos, uint32_t ncols);
+/* cols: this rank's decoded columns (device); writes the header to meta (device u64[kx_shard_meta_words]). */
+int kx_shard_meta(kx_ctx* c, const kx_column_info* infos, uint32_t ncols, const kx_columns* cols, uint64_t n,
+                  uint64_t in_len, uint64_t* meta, void* stream);
+/* Host only (no device access). layout: any rank's columns (offset_bytes and flags are read, pointers
+ * are not; presence != NULL when the records carry presence words). metas: host u64[world][words].
+ * pieces: capacity *npieces on entry, the count on return (KX_ERR_SIZE_LIMIT, with the needed count,
+ * when too small). Pieces are ordered by rank, then column, then array; empty pieces are listed. */
+int kx_concat_plan(const kx_column_info* infos, uint32_t ncols, const kx_columns* layout, const uint64_t* metas,
+                   uint32_t world, kx_concat_piece* pieces, uint32_t* npieces, kx_concat_sizes* sizes);
+/* staging: the root's received offset arrays (offset_bytes = the senders'); out: the concatenated columns
+ * (8-byte offsets and view pairs). Adds each offsets / view piece's rebase on the device and writes the
+ * closing entry of every offsets array. pieces: host memory, as kx_concat_plan returned them. */
+int kx_concat_rebase(kx_ctx* c, const kx_column_info* infos, uint32_t ncols, const kx_concat_piece* pieces,
+                     uint32_t npieces, const kx_columns* staging, const kx_columns* out, const kx_concat_sizes* sizes,
+                     void* stream);
+
 /* ---- Thrift binary: batched BLength / FastWriteNocopy ---- */
 int kx_thrift_encoded_size_batch(kx_ctx* c, const kx_schema* s, const kx_columns* in, uint64_t n,
                                  uint64_t* sizes_out, void* stream);
@@ -393,6 +455,17 @@ int kx_host_decode_batch(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint6
 int kx_host_pb_decode_batch(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len,
                             const uint64_t* offsets, uint64_t n, const kx_columns* out,
                             kx_status* status);
+/* fastMarshal from host memory (codec_fast.go:40-58 / thrift.go:106-160, the reply path): n records'
+ * columns (HOST memory, pinned for full PCIe rate; FIXED / BYTES / LIST / LIST_BYTES columns of a flat
+ * schema, no views) -> out[0 ..) (host) the records back to back, as kx_thrift_encode_batch writes
+ * them; offsets_out (host, n + 1, optional) each record's start; status (host) consumed = total bytes,
+ * SIZE_LIMIT when out_cap is too small (out then holds no complete batch). Synchronous. With n >= 64 Ki
+ * a pipeline of 16 record-range chunks: the H2D of the columns, the encode and the D2H of the wire of
+ * different chunks overlap. kx_host_pb_encode_batch: the Kitex-Protobuf Batch body (kx_pb_encode_batch). */
+int kx_host_encode_batch(kx_ctx* c, const kx_schema* s, const kx_columns* in, uint64_t n, uint8_t* out,
+                         uint64_t out_cap, uint64_t* offsets_out, kx_status* status);
+int kx_host_pb_encode_batch(kx_ctx* c, const kx_schema* s, const kx_columns* in, uint64_t n, uint8_t* out,
+                            uint64_t out_cap, uint64_t* offsets_out, kx_status* status);
 
 /* ---- message level: N framed RPC messages (framing already removed by the transport) ----
  * message i = in[offsets[i] .. offsets[i+1]) (u64, n+1 entries, device).

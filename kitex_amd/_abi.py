@@ -6,7 +6,7 @@ layout is checked by tests/test_abi.py against the compiled library.
 """
 import ctypes as C
 
-KX_ABI_VERSION = 5
+KX_ABI_VERSION = 6
 
 # Thrift TType ids (gopkg protocol/thrift; pinned by pkg/protocol/bthrift/binary_test.go)
 T_STOP, T_VOID, T_BOOL, T_BYTE, T_DOUBLE = 0, 1, 2, 3, 4
@@ -122,12 +122,25 @@ class TTStreamKeys(C.Structure):
 
 TTS_META, TTS_HEADER, TTS_DATA, TTS_TRAILER, TTS_RST = 1, 2, 3, 4, 5
 
+# shard concatenation (kx_concat_plan): the arrays of a column a piece belongs to
+PIECE_OFFSETS, PIECE_ELEM_OFFSETS, PIECE_SUB_OFFSETS, PIECE_DATA = 0, 1, 2, 3
+
+
+class ConcatPiece(C.Structure):
+    _fields_ = [("rank", C.c_uint32), ("column", C.c_uint32), ("array", C.c_uint32), ("elem_bytes", C.c_uint32),
+                ("src_first", C.c_uint64), ("count", C.c_uint64), ("dst_first", C.c_uint64), ("rebase", C.c_int64)]
+
+
+class ConcatSizes(C.Structure):
+    _fields_ = [("n", C.c_uint64), ("in_len", C.c_uint64), ("units", (C.c_uint64 * 4) * MAX_COLUMNS)]
+
 assert C.sizeof(TTStreamKeys) == 48
 assert C.sizeof(FieldDesc) == 16
 assert C.sizeof(Status) == 192
 assert C.sizeof(Column) == 64
 assert C.sizeof(Columns) == MAX_COLUMNS * 64 + 16
 assert C.sizeof(ColumnInfo) == 40
+assert C.sizeof(ConcatPiece) == 48
 
 
 def n_arrays(ci) -> int:

@@ -29,7 +29,8 @@ EXPORTS = [
     "kx_grpc_frame_scan", "kx_thrift_decode_grpc", "kx_pb_decode_grpc", "kx_thrift_raw_messages",
     "kx_thrift_set_seqids", "kx_thrift_encode_messages", "kx_ttstream_default_keys", "kx_ttstream_frame_scan",
     "kx_thrift_decode_extents", "kx_pb_decode_extents", "kx_schema_is_nested", "kx_thrift_decode_sizes",
-    "kx_decode_workspace_bytes", "kx_thrift_decode_sizes_extents",
+    "kx_decode_workspace_bytes", "kx_thrift_decode_sizes_extents", "kx_shard_meta_words", "kx_shard_meta",
+    "kx_concat_plan", "kx_concat_rebase", "kx_host_encode_batch", "kx_host_pb_encode_batch",
 ]
 
 
@@ -91,6 +92,8 @@ def lib():
     L.kx_pb_encode_batch.argtypes = L.kx_thrift_encode_batch.argtypes
     L.kx_host_decode_batch.argtypes = [vp, vp, vp, u64, vp, u64, C.POINTER(A.Columns), C.POINTER(A.Status)]
     L.kx_host_pb_decode_batch.argtypes = L.kx_host_decode_batch.argtypes
+    L.kx_host_encode_batch.argtypes = [vp, vp, C.POINTER(A.Columns), u64, vp, u64, vp, C.POINTER(A.Status)]
+    L.kx_host_pb_encode_batch.argtypes = L.kx_host_encode_batch.argtypes
     L.kx_thrift_message_begin_length.argtypes = [u32]
     L.kx_thrift_message_begin_length.restype = u64
     L.kx_thrift_write_message_begin.argtypes = [vp, u64, C.c_char_p, u32, i32, i32, C.POINTER(u64)]
@@ -121,6 +124,14 @@ def lib():
                                             u64, vp, u64, vp, vp, vp]
     L.kx_thrift_decode_grpc.argtypes = [vp, vp, vp, u64, u64, u64, vp, C.POINTER(A.Columns), vp, vp, vp]
     L.kx_pb_decode_grpc.argtypes = L.kx_thrift_decode_grpc.argtypes
+    ci = C.POINTER(A.ColumnInfo)
+    L.kx_shard_meta_words.argtypes = [ci, u32]
+    L.kx_shard_meta_words.restype = u32
+    L.kx_shard_meta.argtypes = [vp, ci, u32, C.POINTER(A.Columns), u64, u64, vp, vp]
+    L.kx_concat_plan.argtypes = [ci, u32, C.POINTER(A.Columns), C.POINTER(u64), u32, C.POINTER(A.ConcatPiece),
+                                 C.POINTER(u32), C.POINTER(A.ConcatSizes)]
+    L.kx_concat_rebase.argtypes = [vp, ci, u32, C.POINTER(A.ConcatPiece), u32, C.POINTER(A.Columns),
+                                   C.POINTER(A.Columns), C.POINTER(A.ConcatSizes), vp]
     L.kx_pb_meta_length.argtypes = [u32]
     L.kx_pb_meta_length.restype = u64
     L.kx_pb_write_meta.argtypes = L.kx_thrift_write_message_begin.argtypes

@@ -55,7 +55,15 @@ def build(force: bool = False, verbose: bool = False, extra=(), variant: str = "
     hdrs = glob.glob(os.path.join(CSRC, "*.h")) + [os.path.join(HERE, "..", "include", "kxcodec.h")]
     newest_hdr = max(os.path.getmtime(h) for h in hdrs)
     jobs = []
+    # KX_VARIANT_PARTS=1,3: a variant recompiles only these decode parts with its flags and links the default
+    # build's other objects (a kernel-tuning experiment that touches one instantiation builds in one unit)
+    only = os.environ.get("KX_VARIANT_PARTS") if variant else None
+    only_objs = {f"kx_decode.hip.{k}.o" for k in only.split(",")} if only else None
     for src, obj, flags in _units(libdir):
+        if only_objs is not None and os.path.basename(obj) not in only_objs:
+            import shutil
+            shutil.copy2(os.path.join(LIBDIR, os.path.basename(obj)), obj)
+            continue
         fresh = (not force and not extra and not variant and os.path.exists(obj)
                  and os.path.getmtime(obj) > max(os.path.getmtime(src), newest_hdr))
         if fresh:

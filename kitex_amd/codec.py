@@ -372,6 +372,30 @@ class ThriftCodec:
             raise ProtocolError(st.code, self._WHAT, st.record, st.offset)
         return out, st
 
+    _HOST_ENCODE = "kx_host_encode_batch"
+
+    def MarshalHost(self, cols: ColumnSet, out=None, with_offsets: bool = True, raise_on_error: bool = True):
+        """fastMarshal to host memory (the reply path, codec_fast.go:40-58): host ColumnSet (numpy; pinned
+        buffers reach full PCIe rate) -> (wire uint8 numpy, offsets uint64[n+1] or None, status) via
+        kx_host_encode_batch (H2D of the columns, device encode, D2H of the wire; with n >= 64 Ki a chunked
+        pipeline whose copies overlap the encode). `out`: a preallocated uint8 buffer (default: an upper
+        bound from the column sizes)."""
+        import numpy as np
+        ds = self.dschema
+        n = cols.n
+        kc = to_kx_columns(cols, ds.infos)
+        if out is None:
+            out = np.empty(max(1, _host_encode_bound(cols, ds.infos, n, self._HOST_ENCODE != "kx_host_encode_batch")),
+                           dtype=np.uint8)
+        offs = np.empty(n + 1, dtype=np.uint64) if with_offsets else None
+        st = A.Status()
+        rc = getattr(lib(), self._HOST_ENCODE)(self.ctx.handle, ds.handle, C.byref(kc), n, out.ctypes.data, out.size,
+                                               offs.ctypes.data if offs is not None else None, C.byref(st))
+        check(rc, self._HOST_ENCODE)
+        if raise_on_error and st.code:
+            raise ProtocolError(st.code, self._HOST_ENCODE)
+        return out[:st.consumed], offs, st
+
     _MESSAGES = "kx_thrift_decode_messages"
     _FRAMES = "kx_thrift_decode_frames"
     _GRPC = "kx_thrift_decode_grpc"
@@ -393,21 +417,24 @@ class ThriftCodec:
     @on_call_stream
     def UnmarshalFrames(self, buf, n: int, body_field: int = 1, max_payload: int = 0, out: ColumnSet = None,
                         var_caps: Sequence[int] = None, name_cap: int = None, stream=None,
-                        raise_on_error: bool = True, crc32_check: bool = False) -> "MessageBatch":
+                        raise_on_error: bool = True, crc32_check: bool = False,
+                        frame_offsets: bool = True) -> "MessageBatch":
         """A socket buffer of n frames (TTHeader / Mesh / Framed / PurePayload, default_codec.go:189-221)
         straight to columns: framing sniff on the device, then UnmarshalMessages on the payloads.
         The batch also carries frame_offsets (int64[n+1]) and kinds (uint8[n], transport.Protocol |
         FRAME_PB | FRAME_MESH). crc32_check: CodecConfig{CRC32Check: true} (default_codec.go:70-92), every
-        TTHeader frame's "crc32c" header is checked against its payload (ERR_PAYLOAD_VALIDATION)."""
+        TTHeader frame's "crc32c" header is checked against its payload (ERR_PAYLOAD_VALIDATION).
+        frame_offsets=False passes NULL for them (the library keeps them in its scratch) and the batch
+        carries none."""
         import torch
         s = _stream(stream)
         check(lib().kx_ctx_set_crc32c_check(self._ctx(s).handle, 1 if crc32_check else 0), "set crc32c check")
-        fo = torch.zeros(n + 1, dtype=torch.int64, device=self.device)
+        fo = torch.zeros(n + 1, dtype=torch.int64, device=self.device) if frame_offsets else None
         kinds = torch.zeros(max(1, n), dtype=torch.uint8, device=self.device)
         args = [self._ctx(s).handle, self.dschema.handle, _ptr(buf), buf.numel(), n]
         if self._FRAMES == "kx_thrift_decode_frames":
             args.append(body_field)
-        args += [max_payload, _ptr(fo), _ptr(kinds)]
+        args += [max_payload, _ptr(fo) if fo is not None else None, _ptr(kinds)]
         res = self._messages(self._FRAMES, args, buf, n, out, var_caps, name_cap, s, raise_on_error)
         res.frame_offsets, res.kinds = fo, kinds[:n]
         return res
@@ -648,6 +675,26 @@ class ThriftCodec:
     split_points = SplitPoints
 
 
+def _host_encode_bound(cols: ColumnSet, infos, n: int, pb: bool) -> int:
+    """an upper bound of the encoded size of host columns: per record 16 bytes per column (header, length,
+    list header, STOP / frame) plus 16 per fixed value, plus every var column's payload bytes (elements at
+    up to 10 bytes as proto varints)"""
+    import numpy as np
+    total = n * (16 * (len(infos) + 2) + 16)
+    for c, ci in enumerate(infos):
+        if ci.kind == A.COL_FIXED:
+            total += n * 16
+            continue
+        parts = cols.cols[c]
+        if ci.kind == A.COL_LIST_BYTES:
+            ne = int(np.asarray(parts[0])[n])
+            total += int(np.asarray(parts[1])[ne]) + 8 * ne
+        else:
+            units = int(np.asarray(parts[0])[n])
+            total += units * (max(ci.width, 10 if pb else ci.width) if ci.kind == A.COL_LIST else 1)
+    return total
+
+
 class ProtobufCodec(ThriftCodec):
     """Batch Kitex-Protobuf payload codec (pkg/remote/codec/protobuf/protobuf.go:49-61).
 
@@ -657,6 +704,7 @@ class ProtobufCodec(ThriftCodec):
 
     _DECODE = "kx_pb_decode_batch"
     _HOST = "kx_host_pb_decode_batch"
+    _HOST_ENCODE = "kx_host_pb_encode_batch"
     _MESSAGES = "kx_pb_decode_messages"
     _FRAMES = "kx_pb_decode_frames"
     _GRPC = "kx_pb_decode_grpc"
@@ -676,7 +724,13 @@ class ProtobufCodec(ThriftCodec):
     def Skip(self, buf, n: int, stream=None):
         raise KxError(A.ERR_NOT_IMPLEMENTED, "protobuf has no skip decoder")
 
-    name, skip = Name, Skip
+    @on_call_stream
+    def SplitPoints(self, buf, n: int, parts: int, stream=None):
+        """kx_thrift_split_points walks Thrift records; a flat proto3 schema carries no wire-format mark the
+        library could refuse it by (its calls choose the format), so the codec refuses it here"""
+        raise KxError(A.ERR_NOT_IMPLEMENTED, "split points: Thrift records only")
+
+    name, skip, split_points = Name, Skip, SplitPoints
 
 
 def write_message_begin(name: str, msg_type: int, seqid: int) -> bytes:

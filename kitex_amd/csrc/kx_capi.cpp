@@ -345,6 +345,7 @@ int kx_schema_create(const kx_struct_desc* structs, uint32_t nstructs, kx_schema
     delete s;
     return rc;
   }
+  if (!s->nprog) s->prog.is_pb = pb ? 1u : 0u;   // the flat program remembers its wire format (split points)
   *out = s;
   return KX_OK;
 }
@@ -422,6 +423,12 @@ void kx_ctx_destroy(kx_ctx* c) {
   }
   if (c->h2d_stream) (void)hipStreamDestroy(c->h2d_stream);
   if (c->d2h_stream) (void)hipStreamDestroy(c->d2h_stream);
+  for (int k = 0; k < KX_HOST_CH; k++) {
+    if (c->hev_in[k]) (void)hipEventDestroy(c->hev_in[k]);
+    if (c->hev_run[k]) (void)hipEventDestroy(c->hev_run[k]);
+    if (c->hev_st[k]) (void)hipEventDestroy(c->hev_st[k]);
+  }
+  if (c->hst) (void)hipHostFree(c->hst);
   delete c;
 }
 
@@ -533,7 +540,8 @@ int kx_thrift_split_points(kx_ctx* c, const kx_schema* s, const uint8_t* in, uin
                            uint32_t parts, uint64_t* points_out, kx_status* status, void* stream) {
   if (!c || !s || !status || !points_out || (!in && in_len) || parts == 0 || parts > 65536)
     return KX_ERR_INVALID_ARG;
-  if (s->nprog && s->nprog->pb) return KX_ERR_NOT_IMPLEMENTED;   // Kitex-Protobuf: Batch frames, not records
+  // Kitex-Protobuf (nested or flat): Batch frames, not Thrift records
+  if ((s->nprog && s->nprog->pb) || (!s->nprog && s->prog.is_pb)) return KX_ERR_NOT_IMPLEMENTED;
   int rc = set_device(c);
   if (rc) return rc;
   hipStream_t st = (hipStream_t)stream;
@@ -805,6 +813,11 @@ int kx_ctx_set_crc32c_check(kx_ctx* c, int enable) {
   return KX_OK;
 }
 
+// a kx_status inside a scratch layout takes a slot of this many bytes (the status grew to 192 B
+// and the CRC status used to overlap the frame offsets)
+#define KX_STATUS_SLOT 256
+static_assert(sizeof(kx_status) <= KX_STATUS_SLOT, "scratch status slot");
+
 // a socket buffer of n frames -> frame scan -> message headers -> record bodies
 static int decode_frames(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len, uint64_t n,
                          int32_t body_field, bool pb, uint64_t max_payload, uint64_t* frame_offsets, uint8_t* kinds,
@@ -819,9 +832,10 @@ static int decode_frames(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint6
     uint64_t z = 0;
     return decode_messages(c, s, in, in_len, &z, 0, body_field, pb, msg_cols, out, record_status, status, stream);
   }
-  // scratch: [scan status 128 B][crc status 128 B][frame offsets n + 1][payload starts n + 1]
-  //          [payload ends n][crc codes n]
-  const size_t fo_at = 256, ps_at = fo_at + (n + 1) * 8, pe_at = ps_at + (n + 1) * 8, vr_at = pe_at + n * 8;
+  // scratch: [scan status][crc status][frame offsets n + 1][payload starts n + 1][payload ends n][crc codes n],
+  // each status in its own KX_STATUS_SLOT-byte slot
+  const size_t cs_at = KX_STATUS_SLOT, fo_at = 2 * KX_STATUS_SLOT, ps_at = fo_at + (n + 1) * 8,
+               pe_at = ps_at + (n + 1) * 8, vr_at = pe_at + n * 8;
   if ((rc = ensure_fws(c, vr_at + n, st))) return rc;
   char* f = (char*)c->fws;
   kx_status* pre = (kx_status*)f;
@@ -831,15 +845,16 @@ static int decode_frames(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint6
   // DecodeMeta's payloadChecksumValidate (default_codec.go:205-209): fused into the frame scan's emit pass
   // (the payload is checked from the LDS window the scan already holds); KX_CRC_FUSED=0 runs the separate
   // checksum kernel after the scan instead
-  static int fused_env = -1;
-  if (fused_env < 0) { const char* e = getenv("KX_CRC_FUSED"); fused_env = e ? atoi(e) : 1; }
+  // (read per call, so an A/B run or a test can switch forms within one process)
+  const char* fe = getenv("KX_CRC_FUSED");
+  const int fused_env = fe ? atoi(fe) : 1;
   uint8_t* vrc = c->crc32c_check ? (uint8_t*)(f + vr_at) : nullptr;
   const bool fused = vrc && fused_env;
   if ((rc = frame_scan(c, in, in_len, n, max_payload, fo, ps, pe, kinds, pre, stream, fused ? vrc : nullptr)))
     return rc;
   if (vrc && !fused) {
     if ((rc = ensure_cws(c, st))) return rc;
-    if ((rc = kx_launch_crc32c(in, in_len, fo, n, true, pre, nullptr, vrc, (kx_status*)(f + 128), c->cws, st)))
+    if ((rc = kx_launch_crc32c(in, in_len, fo, n, true, pre, nullptr, vrc, (kx_status*)(f + cs_at), c->cws, st)))
       return rc;
   }
   return decode_messages(c, s, in, in_len, ps, n, body_field, pb, msg_cols, out, record_status, status, stream, pe,
@@ -878,8 +893,8 @@ static int decode_grpc(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_
     uint64_t z = 0;
     return decode_messages(c, s, in, in_len, &z, 0, 0, pb, nullptr, out, record_status, status, stream);
   }
-  // scratch: [scan status 256 B][frame offsets n + 1][payload starts n + 1][payload ends n][flags n]
-  const size_t fo_at = 256, ps_at = fo_at + (n + 1) * 8, pe_at = ps_at + (n + 1) * 8, fl_at = pe_at + n * 8;
+  // scratch: [scan status][frame offsets n + 1][payload starts n + 1][payload ends n][flags n]
+  const size_t fo_at = KX_STATUS_SLOT, ps_at = fo_at + (n + 1) * 8, pe_at = ps_at + (n + 1) * 8, fl_at = pe_at + n * 8;
   if ((rc = ensure_fws(c, fl_at + n, st))) return rc;
   char* f = (char*)c->fws;
   kx_status* pre = (kx_status*)f;
@@ -1106,7 +1121,7 @@ int kx_pb_encode_batch(kx_ctx* c, const kx_schema* s, const kx_columns* in, uint
 // device decode of one batch (thrift or protobuf body), arena positions starting at var_base
 static int decode_device(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len, const uint64_t* offsets,
                          uint64_t n, const kx_columns* out, kx_status* status, hipStream_t st, bool pb,
-                         const uint64_t* var_base) {
+                         const uint64_t* var_base, const uint64_t* var_base_dev = nullptr) {
   KxLaunchCols lc;
   int rc = to_launch_cols(s, out, &lc);
   if (rc) return rc;
@@ -1117,7 +1132,24 @@ static int decode_device(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint6
   if ((rc = ensure_ws(c, kx_decode_ws_bytes(s->prog, in_len, offsets, n), st, &epoch))) return rc;
   if ((rc = ensure_pipe(c))) return rc;
   return kx_launch_decode(dp, s->prog, in, in_len, offsets, n, lc, nullptr, status, c->ws, c->ws_size, epoch, st, pb,
-                          nullptr, var_base, &c->pipe);
+                          nullptr, var_base, &c->pipe, var_base_dev);
+}
+
+// the host pipelines' events (a ring of KX_HOST_CH per kind) and pinned status staging, created once per ctx
+static int ensure_host_events(kx_ctx* c) {
+  if (c->hst) return KX_OK;
+  for (int k = 0; k < KX_HOST_CH; k++) {
+    KX_HIP_CHECK(hipEventCreateWithFlags(&c->hev_in[k], hipEventDisableTiming));
+    KX_HIP_CHECK(hipEventCreateWithFlags(&c->hev_run[k], hipEventDisableTiming));
+    KX_HIP_CHECK(hipEventCreateWithFlags(&c->hev_st[k], hipEventDisableTiming));
+  }
+  KX_HIP_CHECK(hipHostMalloc((void**)&c->hst, KX_HOST_CH * sizeof(kx_status), hipHostMallocDefault));
+  return KX_OK;
+}
+
+// entry i of a host offsets array (4 or 8 bytes)
+static inline uint64_t host_off(const void* p, uint32_t ob, uint64_t i) {
+  return ob == 8 ? ((const uint64_t*)p)[i] : ((const uint32_t*)p)[i];
 }
 
 // fastUnmarshal end to end from host (netpoll) memory. With message offsets (the RPC case: framing
@@ -1137,7 +1169,7 @@ static int host_decode(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_
   if (!c->h2d_stream) KX_HIP_CHECK(hipStreamCreateWithFlags(&c->h2d_stream, hipStreamNonBlocking));
   if (!c->d2h_stream) KX_HIP_CHECK(hipStreamCreateWithFlags(&c->d2h_stream, hipStreamNonBlocking));
   hipStream_t st = c->own_stream, sh = c->h2d_stream, sd = c->d2h_stream;
-  const uint32_t K = offsets && n >= (1u << 16) ? 16u : 1u;  // chunks
+  const uint32_t K = offsets && n >= (1u << 16) ? (uint32_t)KX_HOST_CH : 1u;  // chunks
   auto al = [](uint64_t x) { return (x + 255) & ~255ull; };
   // staging layout: K statuses | input | offsets | columns (fixed data, var offsets + arenas) | presence
   uint64_t need = al(K * sizeof(kx_status)) + al(in_len) + (offsets ? al((n + 1) * 8) : 0);
@@ -1211,26 +1243,24 @@ static int host_decode(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_
   }
 
   // ---- chunked pipeline (offsets known) ----
-  uint64_t r[17];
+  // H2D of every chunk is queued on the copy-in stream at once; decode k waits for its chunk's input and
+  // takes its arena base from chunk k - 1's status ON THE DEVICE (var_base_dev), so decode k + 1 is queued
+  // before the host reads chunk k's status: the decode stream never waits for a host round trip. The host
+  // reads each chunk's status (pinned, behind its decode on the copy-out stream) only to size the D2H of
+  // that chunk's arena range; fixed columns, offsets and presence go out behind the decode with no wait.
+  if ((rc = ensure_host_events(c))) return rc;
+  uint64_t r[KX_HOST_CH + 1];
   for (uint32_t k = 0; k <= K; k++) r[k] = n * k / K;
   for (uint32_t k = 0; k < K; k++)
     if (offsets[r[k + 1]] < offsets[r[k]] || offsets[r[k + 1]] > in_len) return KX_ERR_INVALID_ARG;
-  hipEvent_t ev_in[16], ev_dec[16];
-  for (uint32_t k = 0; k < K; k++) {
-    KX_HIP_CHECK(hipEventCreateWithFlags(&ev_in[k], hipEventDisableTiming));
-    KX_HIP_CHECK(hipEventCreateWithFlags(&ev_dec[k], hipEventDisableTiming));
-  }
   // every chunk's input lands at its own offsets: the caller's offsets work unchanged on the device
   KX_HIP_CHECK(hipMemcpyAsync(d_off, offsets, (n + 1) * 8, hipMemcpyHostToDevice, sh));
   for (uint32_t k = 0; k < K; k++) {
     const uint64_t a = offsets[r[k]], b = offsets[r[k + 1]];
     if (b > a) KX_HIP_CHECK(hipMemcpyAsync(d_in + a, in + a, b - a, hipMemcpyHostToDevice, sh));
-    KX_HIP_CHECK(hipEventRecord(ev_in[k], sh));
+    KX_HIP_CHECK(hipEventRecord(c->hev_in[k], sh));
   }
-  uint64_t base[KXP_NV_MAX] = {0};
-  kx_status first{};
-  bool failed = false;
-  for (uint32_t k = 0; k < K; k++) {
+  auto launch_chunk = [&](uint32_t k) -> int {
     const uint64_t r0 = r[k], nk = r[k + 1] - r[k];
     kx_columns ck = dc;  // this chunk's window of the output columns
     for (uint32_t j = 0; j < s->ncols; j++) {
@@ -1239,19 +1269,15 @@ static int host_decode(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_
       else ck.cols[j].offsets = (char*)dc.cols[j].offsets + r0 * dc.cols[j].offset_bytes;
     }
     if (dc.presence) ck.presence = dc.presence + r0;
-    KX_HIP_CHECK(hipStreamWaitEvent(st, ev_in[k], 0));
-    if ((rc = decode_device(c, s, d_in, in_len, d_off + r0, nk, &ck, d_st + k, st, pb, base))) return rc;
-    KX_HIP_CHECK(hipEventRecord(ev_dec[k], st));
-    kx_status sk;
-    KX_HIP_CHECK(hipMemcpyAsync(&sk, d_st + k, sizeof sk, hipMemcpyDeviceToHost, st));
-    KX_HIP_CHECK(hipStreamSynchronize(st));  // the next chunk's arena starts where this one ends
-    if (sk.code && !failed) {
-      failed = true;
-      first = sk;
-      first.record += r0;
-    }
-    // D2H of this chunk behind its decode, while the next chunk decodes
-    KX_HIP_CHECK(hipStreamWaitEvent(sd, ev_dec[k], 0));
+    KX_HIP_CHECK(hipStreamWaitEvent(st, c->hev_in[k], 0));
+    int e = decode_device(c, s, d_in, in_len, d_off + r0, nk, &ck, d_st + k, st, pb, nullptr,
+                          k ? d_st[k - 1].var_total : nullptr);
+    if (e) return e;
+    KX_HIP_CHECK(hipEventRecord(c->hev_run[k], st));
+    // behind the decode on the copy-out stream: the status (pinned), then the fixed columns / offsets
+    KX_HIP_CHECK(hipStreamWaitEvent(sd, c->hev_run[k], 0));
+    KX_HIP_CHECK(hipMemcpyAsync(&c->hst[k], d_st + k, sizeof(kx_status), hipMemcpyDeviceToHost, sd));
+    KX_HIP_CHECK(hipEventRecord(c->hev_st[k], sd));
     for (uint32_t j = 0; j < s->ncols; j++) {
       const kx_column_info& ci = s->info[j];
       if (ci.kind == KX_COL_FIXED) {
@@ -1265,6 +1291,27 @@ static int host_decode(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_
     }
     if (s->npres)
       KX_HIP_CHECK(hipMemcpyAsync(out->presence + r0, dc.presence + r0, nk * 8, hipMemcpyDeviceToHost, sd));
+    return KX_OK;
+  };
+  uint64_t base[KXP_NV_MAX] = {0};
+  kx_status first{};
+  bool failed = false;
+  // KX_HOST_SERIAL=1 (A/B, read per call): decode k + 1 is queued only after the host has read chunk k's
+  // status, the round-4 schedule
+  const char* ser = getenv("KX_HOST_SERIAL");
+  const bool serial = ser && atoi(ser);
+  if ((rc = launch_chunk(0))) return rc;
+  for (uint32_t k = 0; k < K; k++) {
+    if (!serial && k + 1 < K && (rc = launch_chunk(k + 1))) return rc;   // queued before chunk k's status is read
+    KX_HIP_CHECK(hipEventSynchronize(c->hev_st[k]));
+    if (serial && k + 1 < K && (rc = launch_chunk(k + 1))) return rc;
+    const kx_status sk = c->hst[k];
+    if (sk.code && !failed) {
+      failed = true;
+      first = sk;
+      first.record += r[k];
+    }
+    // chunk k's arena range, known now: after its fixed columns on the copy-out stream
     for (uint32_t v = 0; v < s->prog.nvar && v < KXP_NV_MAX; v++) {
       const uint32_t j = s->prog.var_col[v];
       const uint64_t cap = out->cols[j].capacity;
@@ -1282,11 +1329,207 @@ static int host_decode(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_
     }
   }
   KX_HIP_CHECK(hipStreamSynchronize(sd));
+  return KX_OK;
+}
+
+// fastMarshal from host (netpoll-bound) memory: the columns go up, the wire comes back. The records are
+// cut into KX_HOST_CH chunks (n >= 64 Ki): H2D of every chunk's column slices is queued at once (fixed
+// rows, offsets rows, and the arena ranges those offsets span, all at their own positions, so the
+// caller's offsets work unchanged on the device); encode k waits for its slices and starts writing where
+// chunk k - 1 ended, which it reads from chunk k - 1's status on the device (kx_launch_encode out_base),
+// so it is queued before the host learns chunk k - 1's size; the host reads each chunk's status (pinned,
+// behind its encode) to copy that chunk's wire bytes out, while the next chunk encodes.
+static int host_encode(kx_ctx* c, const kx_schema* s, const kx_columns* in, uint64_t n, uint8_t* out,
+                       uint64_t out_cap, uint64_t* offsets_out, kx_status* status, bool pb) {
+  if (!c || !s || !in || !status || (!out && out_cap)) return KX_ERR_INVALID_ARG;
+  if (s->nprog) return KX_ERR_NOT_IMPLEMENTED;   // nested schemas: the device entry points
+  if (in->ncols != s->ncols || (s->npres && !in->presence)) return KX_ERR_INVALID_ARG;
+  if (pb) {
+    int e = pb_schema_ok(s);
+    if (e) return e;
+  }
+  for (uint32_t k = 0; k < s->ncols; k++) {
+    const kx_column_info& ci = s->info[k];
+    const kx_column& col = in->cols[k];
+    if (col.flags) return KX_ERR_INVALID_ARG;   // views: device-resident inputs only
+    if (ci.kind == KX_COL_FIXED ? !col.data : !col.offsets || !offset_width(col)) return KX_ERR_INVALID_ARG;
+    if (ci.kind == KX_COL_LIST2 || ci.kind == KX_COL_LIST2_BYTES) return KX_ERR_NOT_IMPLEMENTED;
+    if (ci.kind == KX_COL_LIST_BYTES && !col.elem_offsets) return KX_ERR_INVALID_ARG;
+  }
+  int rc = set_device(c);
+  if (rc) return rc;
+  if (!c->own_stream) KX_HIP_CHECK(hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking));
+  if (!c->h2d_stream) KX_HIP_CHECK(hipStreamCreateWithFlags(&c->h2d_stream, hipStreamNonBlocking));
+  if (!c->d2h_stream) KX_HIP_CHECK(hipStreamCreateWithFlags(&c->d2h_stream, hipStreamNonBlocking));
+  if ((rc = ensure_host_events(c))) return rc;
+  hipStream_t st = c->own_stream, sh = c->h2d_stream, sd = c->d2h_stream;
+  if (n == 0) {
+    memset(status, 0, sizeof *status);
+    if (offsets_out) offsets_out[0] = 0;
+    return KX_OK;
+  }
+  const uint32_t K = n >= (1u << 16) ? (uint32_t)KX_HOST_CH : 1u;
+  auto al = [](uint64_t x) { return (x + 255) & ~255ull; };
+  auto unit = [&](uint32_t k) -> uint64_t {
+    const kx_column_info& ci = s->info[k];
+    return ci.kind == KX_COL_LIST ? ci.width : 1;
+  };
+  // staging: K statuses | out | offsets_out (n + 1) | columns (fixed, offsets + arenas, elem offsets) | presence
+  uint64_t need = al(K * sizeof(kx_status)) + al(out_cap) + al((n + 1) * 8);
+  uint64_t units[KX_MAX_COLUMNS] = {0}, elems[KX_MAX_COLUMNS] = {0};
+  for (uint32_t k = 0; k < s->ncols; k++) {
+    const kx_column_info& ci = s->info[k];
+    const kx_column& col = in->cols[k];
+    if (ci.kind == KX_COL_FIXED) {
+      need += al(n * ci.width);
+      continue;
+    }
+    const uint32_t ob = (uint32_t)offset_width(col);
+    need += al((n + 1) * ob);
+    if (ci.kind == KX_COL_LIST_BYTES) {
+      elems[k] = host_off(col.offsets, ob, n);
+      units[k] = host_off(col.elem_offsets, ob, elems[k]);
+      need += al((elems[k] + 1) * ob);
+    } else {
+      units[k] = host_off(col.offsets, ob, n);
+    }
+    need += al(units[k] * unit(k));
+  }
+  if (s->npres) need += al(n * 8);
+  if (c->dstage_size < need) {
+    if (c->dstage) KX_HIP_CHECK(hipFree(c->dstage));
+    c->dstage = nullptr;
+    c->dstage_size = 0;
+    KX_HIP_CHECK(hipMalloc(&c->dstage, need));
+    c->dstage_size = need;
+  }
+  char* p = (char*)c->dstage;
+  kx_status* d_st = (kx_status*)p; p += al(K * sizeof(kx_status));
+  uint8_t* d_out = (uint8_t*)p; p += al(out_cap);
+  uint64_t* d_offs = (uint64_t*)p; p += al((n + 1) * 8);
+  kx_columns dc;
+  memset(&dc, 0, sizeof dc);
+  dc.ncols = s->ncols;
+  for (uint32_t k = 0; k < s->ncols; k++) {
+    const kx_column_info& ci = s->info[k];
+    if (ci.kind == KX_COL_FIXED) {
+      dc.cols[k].data = p; p += al(n * ci.width);
+      continue;
+    }
+    const uint32_t ob = (uint32_t)offset_width(in->cols[k]);
+    dc.cols[k].offset_bytes = ob;
+    dc.cols[k].offsets = p; p += al((n + 1) * ob);
+    if (ci.kind == KX_COL_LIST_BYTES) {
+      dc.cols[k].elem_offsets = p; p += al((elems[k] + 1) * ob);
+      dc.cols[k].elem_capacity = elems[k];
+    }
+    dc.cols[k].data = p; p += al(units[k] * unit(k));
+    dc.cols[k].capacity = units[k];
+  }
+  if (s->npres) { dc.presence = (uint64_t*)p; p += al(n * 8); }
+  KxProgram* dprog = nullptr;
+  if ((rc = prog_on_device(const_cast<kx_schema*>(s), c->device, &dprog))) return rc;
+  uint64_t r[KX_HOST_CH + 1];
+  for (uint32_t k = 0; k <= K; k++) r[k] = n * k / K;
+  if ((rc = ensure_ews(c, kx_encode_ws_bytes(r[1] - r[0] + 1), st))) return rc;
+  // H2D of every chunk's slices, queued at once
   for (uint32_t k = 0; k < K; k++) {
-    (void)hipEventDestroy(ev_in[k]);
-    (void)hipEventDestroy(ev_dec[k]);
+    const uint64_t r0 = r[k], r1 = r[k + 1];
+    auto h2d = [&](void* d, const void* h, uint64_t bytes) -> int {
+      if (bytes) KX_HIP_CHECK(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, sh));
+      return KX_OK;
+    };
+    for (uint32_t j = 0; j < s->ncols; j++) {
+      const kx_column_info& ci = s->info[j];
+      const kx_column& col = in->cols[j];
+      if (ci.kind == KX_COL_FIXED) {
+        if ((rc = h2d((char*)dc.cols[j].data + r0 * ci.width, (const char*)col.data + r0 * ci.width,
+                      (r1 - r0) * ci.width)))
+          return rc;
+        continue;
+      }
+      const uint32_t ob = dc.cols[j].offset_bytes;
+      if ((rc = h2d((char*)dc.cols[j].offsets + r0 * ob, (const char*)col.offsets + r0 * ob, (r1 - r0 + 1) * ob)))
+        return rc;
+      uint64_t a = host_off(col.offsets, ob, r0), b = host_off(col.offsets, ob, r1);
+      if (b < a || b > (ci.kind == KX_COL_LIST_BYTES ? elems[j] : units[j])) return KX_ERR_INVALID_ARG;
+      if (ci.kind == KX_COL_LIST_BYTES) {
+        if ((rc = h2d((char*)dc.cols[j].elem_offsets + a * ob, (const char*)col.elem_offsets + a * ob,
+                      (b - a + 1) * ob)))
+          return rc;
+        const uint64_t ea = host_off(col.elem_offsets, ob, a), eb = host_off(col.elem_offsets, ob, b);
+        if (eb < ea || eb > units[j]) return KX_ERR_INVALID_ARG;
+        a = ea;
+        b = eb;
+      }
+      if ((rc = h2d((char*)dc.cols[j].data + a * unit(j), (const char*)col.data + a * unit(j), (b - a) * unit(j))))
+        return rc;
+    }
+    if (s->npres && (rc = h2d(dc.presence + r0, in->presence + r0, (r1 - r0) * 8))) return rc;
+    KX_HIP_CHECK(hipEventRecord(c->hev_in[k], sh));
+  }
+  auto launch_chunk = [&](uint32_t k) -> int {
+    const uint64_t r0 = r[k], nk = r[k + 1] - r[k];
+    kx_columns ck = dc;   // this chunk's rows; arenas indexed by the (absolute) offsets as they are
+    for (uint32_t j = 0; j < s->ncols; j++) {
+      const kx_column_info& ci = s->info[j];
+      if (ci.kind == KX_COL_FIXED) ck.cols[j].data = (char*)dc.cols[j].data + r0 * ci.width;
+      else ck.cols[j].offsets = (char*)dc.cols[j].offsets + r0 * dc.cols[j].offset_bytes;
+    }
+    if (dc.presence) ck.presence = dc.presence + r0;
+    KxLaunchCols lc;
+    int e = to_launch_cols(s, &ck, &lc);
+    if (e) return e;
+    KX_HIP_CHECK(hipStreamWaitEvent(st, c->hev_in[k], 0));
+    if ((e = kx_launch_encode(dprog, s->prog, lc, nk, d_out, out_cap, nullptr, d_offs + r0, d_st + k, c->ews,
+                              c->ews_size, st, false, pb, k ? &d_st[k - 1].consumed : nullptr)))
+      return e;
+    KX_HIP_CHECK(hipEventRecord(c->hev_run[k], st));
+    KX_HIP_CHECK(hipStreamWaitEvent(sd, c->hev_run[k], 0));
+    KX_HIP_CHECK(hipMemcpyAsync(&c->hst[k], d_st + k, sizeof(kx_status), hipMemcpyDeviceToHost, sd));
+    KX_HIP_CHECK(hipEventRecord(c->hev_st[k], sd));
+    if (offsets_out)
+      KX_HIP_CHECK(hipMemcpyAsync(offsets_out + r0, d_offs + r0, (nk + (k == K - 1 ? 1 : 0)) * 8,
+                                  hipMemcpyDeviceToHost, sd));
+    return KX_OK;
+  };
+  if ((rc = launch_chunk(0))) return rc;
+  uint64_t pos = 0;
+  kx_status first{};
+  bool failed = false;
+  for (uint32_t k = 0; k < K; k++) {
+    if (k + 1 < K && (rc = launch_chunk(k + 1))) return rc;   // queued before chunk k's size is known
+    KX_HIP_CHECK(hipEventSynchronize(c->hev_st[k]));
+    const kx_status sk = c->hst[k];
+    if (sk.code && !failed) {
+      failed = true;
+      first = sk;
+    }
+    if (!failed && sk.consumed > pos) {
+      KX_HIP_CHECK(hipMemcpyAsync(out + pos, d_out + pos, sk.consumed - pos, hipMemcpyDeviceToHost, sd));
+      pos = sk.consumed;
+    }
+  }
+  KX_HIP_CHECK(hipStreamSynchronize(sd));
+  KX_HIP_CHECK(hipStreamSynchronize(st));
+  if (failed) {
+    *status = first;
+  } else {
+    memset(status, 0, sizeof *status);
+    status->n_records = n;
+    status->consumed = pos;
   }
   return KX_OK;
+}
+
+int kx_host_encode_batch(kx_ctx* c, const kx_schema* s, const kx_columns* in, uint64_t n, uint8_t* out,
+                         uint64_t out_cap, uint64_t* offsets_out, kx_status* status) {
+  return host_encode(c, s, in, n, out, out_cap, offsets_out, status, false);
+}
+
+int kx_host_pb_encode_batch(kx_ctx* c, const kx_schema* s, const kx_columns* in, uint64_t n, uint8_t* out,
+                            uint64_t out_cap, uint64_t* offsets_out, kx_status* status) {
+  return host_encode(c, s, in, n, out, out_cap, offsets_out, status, true);
 }
 
 int kx_host_decode_batch(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len,

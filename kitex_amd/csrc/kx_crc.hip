@@ -291,15 +291,19 @@ __global__ void crc_final_kernel(kx_status* st, const uint64_t* offs, uint64_t n
 // partly occupied round of workgroups behind the first)
 template <int G>
 void launch_crc(const CrcParams& cp, uint64_t nblk, hipStream_t stream) {
-  static int resident = -1;
-  if (resident < 0) {
-    int dev = 0, ncu = 0, per = 0;
-    if (hipGetDevice(&dev) == hipSuccess &&
-        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, crc_kernel<G>, CT, 0) == hipSuccess && ncu > 0 && per > 0)
-      resident = ncu * per;
-    else
-      resident = (int)MAX_WG;
+  static int resident_dev[64];   // per device ordinal (0: not yet asked): devices may differ
+  int dev = 0, resident = (int)MAX_WG;
+  if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64) {
+    if (!resident_dev[dev]) {
+      int ncu = 0, per = 0;
+      resident_dev[dev] =
+          hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+                  hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, crc_kernel<G>, CT, 0) == hipSuccess &&
+                  ncu > 0 && per > 0
+              ? ncu * per
+              : (int)MAX_WG;
+    }
+    resident = resident_dev[dev];
   }
   const unsigned grid = (unsigned)kmin64(nblk, (uint64_t)resident);
   hipLaunchKernelGGL(crc_kernel<G>, dim3(grid), dim3(CT), 0, stream, cp);

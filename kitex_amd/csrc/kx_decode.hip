@@ -44,6 +44,7 @@ constexpr int WAVES = NT / 64;
 #endif
 constexpr int SEG = KX_SEG;              // bytes per lane segment
 constexpr int TILE = 64 * SEG;           // 8 KiB of input per wave
+static_assert(TILE <= 65536, "record starts are uint16 offsets from the tile start");
 constexpr int HALO = 512;                // default halo: the record straddling the tile end is read from LDS
 constexpr int HALO_MAX = 1536;           // up to here (the halo grows with the batch's mean record size)
 constexpr int WINB = TILE + HALO_MAX + 16;  // LDS window bytes allocated (+16 for the aligned-down start)
@@ -118,13 +119,16 @@ struct DecParams {
   uint64_t* nstop_ring;      // chunked pipeline: nstop of chunk k at [k % KX_PIPE_EV] (chain runs ahead of emit)
   uint32_t* redo_n;          // fast index kernel: tiles it could not index (count, then their ids)
   uint32_t* redo;
+  int gate_reset;            // chain_kernel zeroes *gate when it ends (its gate is chain_fast_kernel's fallback flag)
   uint32_t* gate;            // known offsets, length gather: these kernels run only when *gate != 0 (repair)
   uint32_t* gcheck;          // ... the checking emit pass: a tile whose decoded var units differ from the
                              // gathered ones sets *gcheck (the repair pass then runs)
   uint64_t* split_out;       // kx_thrift_split_points: nsplit + 1 record starts (no emit pass)
   uint32_t nsplit;
   uint64_t var_base[KXP_NV_MAX];  // arena positions start here (a chunk of a larger batch)
+  const uint64_t* var_base_dev;   // ... plus these device words (the previous chunk's status->var_total)
   KxpFast fp;                // the canonical plan in segment form (fast_record_fp), fp.ok = 0: none
+  KxpEmit ep;                // ... in emit form (emit_fast_kernel), ep.ok = 0: none
   uint64_t ntiles, ngroups, slotcap;
   // chunked pipeline (launch_t): this launch covers tiles [t_lo, t_hi) and groups [g_lo, g_hi); the
   // chain pass carries its state between chunks in `carry`
@@ -1419,6 +1423,12 @@ __device__ __forceinline__ uint64_t pb_scan_segment(const Src& w, uint64_t seg_l
 // < 16 bytes of the input are read from global memory. The descriptor is built from wave-uniform
 // values (SGPRs); a chunk past num_records still writes its LDS slot (zeros), so the issue loop masks
 // the lanes past the window's end.
+#ifndef KX_EXP_EMIT
+#define KX_EXP_EMIT 0   // timing experiments on the emit pass (bits: 1 DMA only, 2 no payload copy, 4 no fixed stores)
+#endif
+#ifndef KX_DMA_AUX
+#define KX_DMA_AUX 0   // cache policy of the window DMA (2: nt, MI355X_MICROARCH.md "nt-weights"); A/B knob
+#endif
 template <int WB = WINB>
 __device__ __forceinline__ Src load_window(KParams& dp, LDS uint32_t* win, uint64_t lo, int lane, bool thrift,
                                            bool wait = true) {
@@ -1434,7 +1444,8 @@ __device__ __forceinline__ Src load_window(KParams& dp, LDS uint32_t* win, uint6
 #pragma unroll
   for (int k = 0; k < WL; k++)
     if ((k + 1) * 64 <= WB / 16 || k * 64 + lane < WB / 16)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (LDS void*)(win + k * 256), 16, lane * 16, k * 1024, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (LDS void*)(win + k * 256), 16, lane * 16, k * 1024, 0,
+                                               KX_DMA_AUX);
   if (wait) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const KAS KxProgram* P = dp.prog;
   return Src{dp.in, dp.in_len, wbase - abs_in, wlen, win, thrift ? P->steps : nullptr, thrift ? P->nsteps : 0u,
@@ -2845,7 +2856,8 @@ __global__ void __launch_bounds__(CT) chain_kernel(DecParams dp_) {
     if (dp.chunk_first) {
       s_E = 0;  // the chain enters group 0 at offset 0
       s_cnt = 0;
-      for (int v = 0; v < KXP_NV_MAX; v++) s_var[v] = dp.var_base[v];  // arena units before this call
+      for (int v = 0; v < KXP_NV_MAX; v++)   // arena units before this call
+        s_var[v] = dp.var_base[v] + (dp.var_base_dev ? dp.var_base_dev[v] : 0);
       s_nstop = dp.n;
       s_err = 0;
       s_done = 0;
@@ -2860,12 +2872,13 @@ __global__ void __launch_bounds__(CT) chain_kernel(DecParams dp_) {
   }
   __syncthreads();
   const uint64_t gend = dp.g_hi;
-  // Fast path (one un-chunked call): when every group has a record start, no group ended in an error and
-  // each group's entry is where the group below it exits (known offsets: always), the pass is a plain scan
-  // of the group totals: a thread takes a contiguous run of groups, checks and sums it, one block scan
-  // gives every run its base. Anything else, and every chunked call, takes the batch loop below.
+  // Fast path: when every group of the call (or chunk) has a record start, no group ended in an error and
+  // each group's entry is where the group below it exits (the first one: where the chain carried in from
+  // the previous chunk, offset 0 for the first), the pass is a plain scan of the group totals: a thread
+  // takes a contiguous run of groups, checks and sums it, one block scan gives every run its base, the
+  // carry moves on. Anything else (and a chain that already ended) takes the batch loop below.
   if (tid == 0) {
-    s_fast = dp.chunk_first && dp.chunk_last;
+    s_fast = !s_err && !s_done;
     s_fok = 1;
   }
   __syncthreads();
@@ -2874,14 +2887,15 @@ __global__ void __launch_bounds__(CT) chain_kernel(DecParams dp_) {
     // the group words were written by the group kernel (an earlier launch): plain loads, issued four
     // groups at a time so that their latencies overlap
     const uint64_t* gw = dp.gdesc;
-    const uint64_t per = (ng + CT - 1) / CT;
-    const uint64_t lo = kmin64((uint64_t)tid * per, ng), hi = kmin64(lo + per, ng);
+    const uint64_t gl = dp.g_lo, gn = dp.g_hi - dp.g_lo;
+    const uint64_t per = (gn + CT - 1) / CT;
+    const uint64_t lo = gl + kmin64((uint64_t)tid * per, gn), hi = kmin64(lo + per, dp.g_hi);
     bool ok = true;
     uint64_t c = 0, vs[NV > 0 ? NV : 1];
 #pragma unroll
     for (int v = 0; v < NV; v++) vs[v] = 0;
-    uint64_t E = 0;   // the chain enters group 0 at offset 0
-    if (lo > 0 && lo < hi) {
+    uint64_t E = s_E;   // the chain enters the call's first group where the previous chunk left it
+    if (lo > gl && lo < hi) {
       const uint64_t x = gw[(uint64_t)G_EXIT * ng + lo - 1];
       ok &= (x >> 48) == ep;
       E = x & V48;
@@ -2923,9 +2937,9 @@ __global__ void __launch_bounds__(CT) chain_kernel(DecParams dp_) {
     if (fast) {
       uint64_t vb[NV > 0 ? NV : 1], vt[NV > 0 ? NV : 1];
 #pragma unroll
-      for (int v = 0; v < NV; v++) vb[v] = s_var[v];   // arena units before this call
+      for (int v = 0; v < NV; v++) vb[v] = s_var[v];   // arena units before this call (or chunk)
       uint64_t tot;
-      uint64_t base = block_scan_u64(c, &tot, s_scan, tid);
+      uint64_t base = s_cnt + block_scan_u64(c, &tot, s_scan, tid);
 #pragma unroll
       for (int v = 0; v < NV; v++) vb[v] += block_scan_u64(vs[v], &vt[v], s_scan, tid);
       for (uint64_t g0 = lo; g0 < hi; g0 += U) {
@@ -2951,10 +2965,11 @@ __global__ void __launch_bounds__(CT) chain_kernel(DecParams dp_) {
         }
       }
       if (tid == 0) {
-        s_cnt = tot;
+        s_cnt += tot;
 #pragma unroll
         for (int v = 0; v < NV; v++) s_var[v] += vt[v];
-        s_done = tot >= dp.n;
+        s_done = s_cnt >= dp.n;
+        if (chain && dp.g_hi > dp.g_lo) s_E = gw[(uint64_t)G_EXIT * ng + dp.g_hi - 1] & V48;   // the carry
       }
       __syncthreads();
     }
@@ -3092,12 +3107,150 @@ __global__ void __launch_bounds__(CT) chain_kernel(DecParams dp_) {
     }
     // emit of this chunk bounds itself by nstop: final once the chain has ended, else unbounded
     *dp.nstop = (dp.chunk_last || s_err || s_done) ? s_nstop : ~0ull;
+    if (dp.gate_reset) *(volatile uint32_t*)dp.gate = 0u;   // re-armed for the next call (chain_fast_kernel)
     if (!dp.chunk_last) {
       cy[CY_E] = s_E;
       cy[CY_CNT] = s_cnt;
       for (int v = 0; v < KXP_NV_MAX; v++) cy[CY_VAR + v] = s_var[v];
       cy[CY_NSTOP] = s_nstop;
       cy[CY_FLAGS] = (uint64_t)(s_err != 0) | (uint64_t)(s_done != 0) << 1;
+    }
+  }
+}
+
+// ---- kernel 2, fast form: the chain pass's fast path alone (round 5). The general chain kernel holds the
+// serial repair loop and the group re-scan (268 VGPRs, scratch, one 256-thread workgroup: ~65 us for 16 M
+// R2 records, most of it the latency of each thread's run of 21 groups). This kernel has 1024 threads and
+// no repair: when every group of the call (chunk) chains, it writes the bases, the nstop and the carry;
+// otherwise it raises *dp.gate and chain_kernel (launched right behind it, gated) does the whole pass.
+constexpr int CFT = 1024, CFW = CFT / 64;
+__device__ __forceinline__ uint64_t block_scan_cf(uint64_t v, uint64_t* tot, uint64_t* sc, int tid) {
+  const int lane = tid & 63, wv = tid >> 6;
+  const uint64_t inc = wave_incl_scan(v, lane);
+  if (lane == 63) sc[wv] = inc;
+  __syncthreads();
+  uint64_t before = 0, all = 0;
+#pragma unroll
+  for (int k = 0; k < CFW; k++) {
+    const uint64_t x = sc[k];
+    before += k < wv ? x : 0;
+    all += x;
+  }
+  __syncthreads();
+  *tot = all;
+  return before + inc - v;
+}
+
+template <int NV, int MODE>
+__global__ void __launch_bounds__(CFT) chain_fast_kernel(DecParams dp_) {
+  KParams& dp = KX_PARAMS();
+  (void)dp_;
+  __shared__ uint64_t s_E, s_cnt, s_var[KXP_NV_MAX], s_nstop;
+  __shared__ int s_err, s_done, s_fok;
+  __shared__ uint64_t s_scan[CFW];
+  const int tid = threadIdx.x;
+  const uint64_t ep = dp.epoch, ng = dp.ngroups;
+  const bool chain = !dp.offsets;
+  uint64_t* const cy = dp.carry;
+  if (tid == 0) {
+    if (dp.chunk_first) {
+      s_E = 0;
+      s_cnt = 0;
+      for (int v = 0; v < KXP_NV_MAX; v++) s_var[v] = dp.var_base[v] + (dp.var_base_dev ? dp.var_base_dev[v] : 0);
+      s_nstop = dp.n;
+      s_err = 0;
+      s_done = 0;
+    } else {
+      s_E = cy[CY_E];
+      s_cnt = cy[CY_CNT];
+      for (int v = 0; v < KXP_NV_MAX; v++) s_var[v] = cy[CY_VAR + v];
+      s_nstop = cy[CY_NSTOP];
+      s_err = (int)(cy[CY_FLAGS] & 1);
+      s_done = (int)(cy[CY_FLAGS] >> 1);
+    }
+    s_fok = 1;
+  }
+  __syncthreads();
+  if (s_err || s_done) {   // the chain already ended in an earlier chunk: the general pass marks the groups
+    if (tid == 0) *(volatile uint32_t*)dp.gate = 1u;
+    return;
+  }
+  const uint64_t* gw = dp.gdesc;
+  const uint64_t gl = dp.g_lo, gn = dp.g_hi - dp.g_lo;
+  const uint64_t per = (gn + CFT - 1) / CFT;
+  const uint64_t lo = gl + kmin64((uint64_t)tid * per, gn), hi = kmin64(lo + per, dp.g_hi);
+  bool ok = true;
+  uint64_t c = 0, vs[NV > 0 ? NV : 1];
+#pragma unroll
+  for (int v = 0; v < NV; v++) vs[v] = 0;
+  uint64_t E = s_E;
+  if (lo > gl && lo < hi) {
+    const uint64_t x = gw[(uint64_t)G_EXIT * ng + lo - 1];
+    ok &= (x >> 48) == ep;
+    E = x & V48;
+  }
+  for (uint64_t g = lo; g < hi; g++) {
+    const uint64_t xe = gw[(uint64_t)G_ENT * ng + g], xx = gw[(uint64_t)G_EXIT * ng + g];
+    const uint64_t xc = gw[(uint64_t)G_CNT * ng + g];
+    ok &= (xe >> 48) == ep && (xx >> 48) == ep && (xc >> 48) == ep;
+    const uint64_t gent = xe & V48, gex = xx & V48;
+    if (chain) {
+      ok &= gent != X_NONE && gent != X_BAD && gex != X_ERR;
+      ok &= chain_ok(E, gent, kmin64((g + 1) * (uint64_t)GT * TILE, dp.in_len));
+    }
+    E = gex;
+    c += xc & V48;
+#pragma unroll
+    for (int v = 0; v < NV; v++) {
+      const uint64_t xv = gw[(uint64_t)(G_VAR + v) * ng + g];
+      ok &= (xv >> 48) == ep;
+      vs[v] += xv & V48;
+    }
+  }
+  if (!ok) s_fok = 0;
+  __syncthreads();
+  if (!s_fok) {
+    if (tid == 0) *(volatile uint32_t*)dp.gate = 1u;
+    return;
+  }
+  uint64_t tot, vt[NV > 0 ? NV : 1], vb[NV > 0 ? NV : 1];
+  uint64_t base = s_cnt + block_scan_cf(c, &tot, s_scan, tid);
+#pragma unroll
+  for (int v = 0; v < NV; v++) vb[v] = s_var[v] + block_scan_cf(vs[v], &vt[v], s_scan, tid);
+  for (uint64_t g = lo; g < hi; g++) {
+    put_word(dp.gdesc, ng, G_BCNT, g, ep, base);
+    base += gw[(uint64_t)G_CNT * ng + g] & V48;
+#pragma unroll
+    for (int v = 0; v < NV; v++) {
+      put_word(dp.gdesc, ng, G_BVAR + v, g, ep, vb[v]);
+      vb[v] += gw[(uint64_t)(G_VAR + v) * ng + g] & V48;
+    }
+  }
+  if (tid == 0) {
+    const uint64_t cnt = s_cnt + tot;
+    uint64_t var[NV > 0 ? NV : 1];
+#pragma unroll
+    for (int v = 0; v < NV; v++) var[v] = s_var[v] + vt[v];
+    const bool done = cnt >= dp.n;
+    const uint64_t ex = chain && gn ? gw[(uint64_t)G_EXIT * ng + dp.g_hi - 1] & V48 : s_E;
+    uint64_t nstop = s_nstop;
+    if (dp.chunk_last && chain && cnt < dp.n) {   // the chain ran out of input before n records: EOF
+      kx_status* st = dp.status;
+      st->code = KX_ERR_EOF; st->record = cnt; st->offset = dp.in_len;
+      st->n_records = cnt; st->consumed = dp.in_len;
+      for (int v = 0; v < NV; v++)
+        if (v < (int)dp.prog->nvar && v < KX_STATUS_VT) st->var_total[v] = var[v];
+      close_slots<NV>(dp.prog, dp.cols, dp.overflow, cnt, var);
+      if (MODE == M_SKIP || MODE == M_FRAME) dp.skip_out[cnt] = dp.in_len;
+      nstop = cnt;
+    }
+    *dp.nstop = (dp.chunk_last || done) ? nstop : ~0ull;
+    if (!dp.chunk_last) {
+      cy[CY_E] = ex;
+      cy[CY_CNT] = cnt;
+      for (int v = 0; v < KXP_NV_MAX; v++) cy[CY_VAR + v] = v < NV ? var[v] : s_var[v];
+      cy[CY_NSTOP] = nstop;
+      cy[CY_FLAGS] = (uint64_t)(done ? 1 : 0) << 1;
     }
   }
 }
@@ -3125,7 +3278,12 @@ __device__ __forceinline__ uint64_t emit_canon(const Src& w, const KAS KxLaunchC
         f.w0 = __builtin_amdgcn_alignbyte(s0[1], s0[0], sh);
         f.w1 = __builtin_amdgcn_alignbyte(s0[2], s0[1], sh);
         f.w2 = __builtin_amdgcn_alignbyte(s0[3], s0[2], sh);
+#if KX_EXP_EMIT & 4   // timing experiment: fixed values computed, not stored
+        const uint64_t xv = fixed_after_header(f, sj.hdr & 0xff);
+        if (xv == 0x0123456789abcdefull) store_col(cols.data[sj.col], sj.width, r, xv);
+#else
         store_col(cols.data[sj.col], sj.width, r, fixed_after_header(f, sj.hdr & 0xff));
+#endif
         q += 3 + sj.width;
       }
       k += m;
@@ -3293,6 +3451,10 @@ __device__ __forceinline__ void emit_tile(KParams& dp, LDS uint32_t* win, uint64
                      ((dp.tdesc[(uint64_t)T_ERRC * dp.ntiles + t] & V48) == T_CANON);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (cnt == 0 || base >= nstop) return;
+#if KX_EXP_EMIT & 1   // timing experiment: the window DMA and the tile's bases only
+  if (w.win[lane] == 0xdeadbeefu && base == 12345) dp.status->diag[2] = cnt;
+  return;
+#endif
   cnt = kmin64(cnt, nstop - base);
   // records past the tile's slots (slotcap, a multiple of 64; ws_layout) are emitted one per round,
   // each starting where the previous one ended
@@ -3406,7 +3568,12 @@ __device__ __forceinline__ void emit_tile(KParams& dp, LDS uint32_t* win, uint64
         const uint32_t nn = vs.len[v];
         if (at + nn <= arena_lim(dp.cols, cc)) {
           put_off(dp.cols, cc, r, at);
-          if (nn) copy_var(w, K, vs.pos[v], nn, (uint8_t*)dp.cols.data[cc] + at * K.width);
+#if KX_EXP_EMIT & 2   // timing experiment: no payload copy
+          if (nn == 0x7fffffff)
+#else
+          if (nn)
+#endif
+            copy_var(w, K, vs.pos[v], nn, (uint8_t*)dp.cols.data[cc] + at * K.width);
         } else {
           atomicOr(dp.overflow, 1u);
         }
@@ -3510,6 +3677,209 @@ __global__ void __launch_bounds__(NT, 4) emit_kernel(DecParams dp_) {  // 4 wave
   emit_tile<NV, MODE, COOP>(dp, (LDS uint32_t*)WIN[wv], t, lane);
 }
 
+// ---- kernel 3, fast form ----
+// Inclusive scan of 32-bit values over the wave with DPP moves (row shifts, then the row broadcasts): no
+// LDS traffic, unlike the bpermute-based wave_incl_scan
+__device__ __forceinline__ uint32_t wave_incl_scan32(uint32_t v) {
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
+  return v;
+}
+
+// n string bytes at window offset x -> dst (global): head bytes up to a dword-aligned destination, then
+// 16-byte stores assembled from 5 window dwords, then a dword / byte tail. The bytes lie in the window (a
+// T_CANON record).
+__device__ __forceinline__ void copy_str_win(const Src& w, uint32_t x, uint32_t n, uint8_t* dst_) {
+  GLB uint8_t* dst = (GLB uint8_t*)dst_;
+  const LDS uint8_t* wb = (const LDS uint8_t*)w.win;
+  uint32_t i = 0;
+  const uint32_t h = min((4u - ((uint32_t)(uintptr_t)dst_ & 3u)) & 3u, n);
+#pragma clang loop vectorize(disable) unroll(disable)
+  for (; i < h; i++) dst[i] = wb[x + i];
+  for (; i + 16 <= n; i += 16) {
+    const uint32_t q = x + i;
+    const LDS uint32_t* s = w.win + (q >> 2);
+    const uint32_t sh = q & 3;
+    const uint32_t x0 = s[0], x1 = s[1], x2 = s[2], x3 = s[3], x4 = s[4];
+    const v4u_a4 o = {__builtin_amdgcn_alignbyte(x1, x0, sh), __builtin_amdgcn_alignbyte(x2, x1, sh),
+                      __builtin_amdgcn_alignbyte(x3, x2, sh), __builtin_amdgcn_alignbyte(x4, x3, sh)};
+    *(GLB v4u_a4*)(dst + i) = o;
+  }
+  for (; i + 4 <= n; i += 4) *(GLB uint32_t*)(dst + i) = win_ld(w, x + i);
+#pragma clang loop vectorize(disable) unroll(disable)
+  for (; i < n; i++) dst[i] = wb[x + i];   // < 4 bytes
+}
+
+// the fixed value of wire type t at window offset x (big-endian) -> column c, record r
+__device__ __forceinline__ void emit_fixed_at(const Src& w, const KAS KxLaunchCols& cols, uint32_t t, uint32_t c,
+                                              uint32_t x, uint64_t r) {
+  const LDS uint32_t* s0 = w.win + (x >> 2);
+  const uint32_t sh = x & 3;
+  const uint32_t lo4 = __builtin_amdgcn_alignbyte(s0[1], s0[0], sh);
+  void* colp = cols.data[c];
+  switch (t) {
+    case KX_T_I64: case KX_T_DOUBLE: {
+      const uint32_t hi4 = __builtin_amdgcn_alignbyte(s0[2], s0[1], sh);
+      ((GLB uint64_t*)colp)[r] = ((uint64_t)__builtin_bswap32(lo4) << 32) | __builtin_bswap32(hi4);
+      break;
+    }
+    case KX_T_I32: ((GLB uint32_t*)colp)[r] = __builtin_bswap32(lo4); break;
+    case KX_T_I16: ((GLB uint16_t*)colp)[r] = (uint16_t)(__builtin_bswap32(lo4) >> 16); break;
+    case KX_T_BOOL: ((GLB uint8_t*)colp)[r] = (lo4 & 0xffu) == 1u ? 1 : 0; break;
+    default: ((GLB uint8_t*)colp)[r] = (uint8_t)lo4; break;   // BYTE
+  }
+}
+
+// One T_CANON tile, lane = record: the segment bases first (only the string lengths chain them), then every
+// fixed value at its constant offset in its segment, then the arena positions (a DPP scan per var slot) and
+// the string copies. Same stores as emit_tile's emit_canon path.
+template <int NV>
+__device__ __forceinline__ void emit_fast_tile(KParams& dp, const Src& w, uint64_t lo, uint64_t base, uint64_t cnt,
+                                               uint64_t nstop, uint64_t* run, const uint16_t* starts, int lane) {
+  const KAS KxProgram* P = dp.prog;
+  const uint32_t q0 = (uint32_t)(lo - w.wpos);
+  const uint32_t nseg = dp.ep.nseg, nvar = P->nvar;
+  for (uint64_t j0 = 0; j0 < cnt; j0 += 64) {
+    const uint64_t j = j0 + lane;
+    const bool act = j < cnt;
+    const uint64_t r = base + j;
+    const uint32_t q = q0 + starts[act ? j : j0];   // an idle lane parses the round's first record (no stores)
+    uint32_t sb[KXE_SEG];
+    uint32_t vp[NV > 0 ? NV : 1], vl[NV > 0 ? NV : 1];
+#pragma unroll
+    for (int v = 0; v < (NV > 0 ? NV : 1); v++) { vp[v] = 0; vl[v] = 0; }
+    uint32_t qs = q;
+#pragma unroll
+    for (int s = 0; s < KXE_SEG; s++) {
+      sb[s] = qs;
+      if (s >= (int)nseg) continue;
+      const uint32_t fl = dp.ep.seg[s].flen;
+      if (dp.ep.seg[s].vkind) {
+        const uint32_t x = qs + fl;
+        const uint32_t l = __builtin_bswap32(win_ld(w, x + 3));
+        const uint32_t slot = dp.ep.seg[s].vslot;
+#pragma unroll
+        for (int v = 0; v < NV; v++)
+          if ((uint32_t)v == slot) { vp[v] = x + 7; vl[v] = l; }
+        qs = x + 7 + l;
+      } else {
+        qs += fl;
+      }
+    }
+    if (act) {
+#pragma unroll
+      for (int s = 0; s < KXE_SEG; s++) {
+        if (s >= (int)nseg) break;
+        const uint32_t nf = dp.ep.seg[s].nfix;
+#pragma unroll
+        for (int f = 0; f < KXE_FIX; f++) {
+          if (f >= (int)nf) break;
+          const KxpEmitFix F = ldk(&dp.ep.seg[s].fix[f]);
+          emit_fixed_at(w, dp.cols, F.ttype, F.col, sb[s] + F.off, r);
+        }
+      }
+      if (dp.cols.presence) dp.cols.presence[r] = w.canon_pres;
+    }
+    uint64_t atv[NV > 0 ? NV : 1];
+#pragma unroll
+    for (int v = 0; v < NV; v++) {
+      if (v >= (int)nvar) break;
+      const uint32_t x0 = act ? vl[v] : 0u;
+      const uint32_t inc = wave_incl_scan32(x0);
+      const uint64_t at = run[v] + (inc - x0);
+      atv[v] = at;
+      run[v] += (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+      const uint32_t cc = P->var_col[v];
+      if (act) {
+        if ((dp.cols.view >> cc) & 1) {
+          put_view(dp.cols, cc, r, w.wpos + vp[v], vl[v]);
+        } else if (at + vl[v] <= arena_lim(dp.cols, cc)) {
+          put_off(dp.cols, cc, r, at);
+          if (vl[v]) copy_str_win(w, vp[v], vl[v], (uint8_t*)dp.cols.data[cc] + at);
+        } else {
+          atomicOr(dp.overflow, 1u);
+        }
+      }
+    }
+    if (act && r == nstop - 1 && nstop == dp.n) {   // the batch's last record closes the var columns
+      uint64_t tot[NV > 0 ? NV : 1];
+#pragma unroll
+      for (int v = 0; v < NV; v++) {
+        tot[v] = v < (int)nvar ? atv[v] + vl[v] : 0;
+        if (v < (int)nvar && v < KX_STATUS_VT) dp.status->var_total[v] = tot[v];
+      }
+      close_slots<NV>(P, dp.cols, dp.overflow, dp.n, tot);
+      dp.status->n_records = dp.n;
+      dp.status->consumed = w.wpos + qs;
+    }
+  }
+}
+
+// T_CANON tiles of a concatenated Thrift batch whose canonical plan has an emit form (dp.ep.ok): a kernel of
+// its own, so its registers are not those of the general field loop; any other tile (walked by the redo
+// index pass, or more records than record-start slots) is queued for emit_redo_kernel. NARROW as
+// index_fast_kernel (the same window the index pass validated the records in).
+template <int NV, bool NARROW>
+__global__ void __launch_bounds__(NARROW ? FNT : NT) emit_fast_kernel(DecParams dp_) {
+  KParams& dp = KX_PARAMS();
+  (void)dp_;
+  constexpr int WV = NARROW ? FWAVES : WAVES, WW = NARROW ? FWINW : WINW;
+  __shared__ __attribute__((aligned(16))) uint32_t WIN[WV][WW];
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const uint64_t t = dp.t_lo + (uint64_t)blockIdx.x * WV + wv;
+  if (t >= dp.t_hi) return;
+  // a batch the fast index path left whole (its first record is not canonical: no tile is T_CANON) goes to
+  // emit_redo_kernel whole, with no DMA here (one scalar load, as index_fast_kernel)
+  if (data_sig_s(dp) != dp.prog->sig) return;
+  uint64_t lo, hi;
+  tile_range(dp, t, lo, hi);
+  const Src w = load_window<NARROW ? FWINB : WINB>(dp, (LDS uint32_t*)WIN[wv], lo, lane, true, false);
+  const uint64_t nstop = *(volatile uint64_t*)dp.nstop;
+  const uint64_t g = t / GT;
+  const uint64_t* gd = dp.gdesc;
+  const uint64_t* td = dp.tdesc;
+  const uint64_t gb = gd[(uint64_t)G_BCNT * dp.ngroups + g] & V48;
+  const uint64_t base = gb + (td[(uint64_t)T_PCNT * dp.ntiles + t] & V48);
+  uint64_t cnt = gb == X_DONE ? 0 : td[(uint64_t)T_CNT * dp.ntiles + t] & V48;
+  const bool canon = (td[(uint64_t)T_ERRC * dp.ntiles + t] & V48) == T_CANON;
+  uint64_t run[NV > 0 ? NV : 1];
+#pragma unroll
+  for (int v = 0; v < (NV > 0 ? NV : 1); v++)
+    run[v] = NV > 0 ? (gd[(uint64_t)(G_BVAR + v) * dp.ngroups + g] & V48) + (td[(uint64_t)(T_PVAR + v) * dp.ntiles + t] & V48)
+                    : 0;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (cnt == 0 || base >= nstop) return;
+  if (!canon || cnt > dp.slotcap) {   // the general emit pass takes it
+    if (lane == 0) dp.redo[atomicAdd(dp.redo_n + 2, 1u)] = (uint32_t)t;
+    return;
+  }
+  emit_fast_tile<NV>(dp, w, lo, base, kmin64(cnt, nstop - base), nstop, run, dp.starts + t * dp.slotcap, lane);
+}
+
+// the tiles emit_fast_kernel queued, with the general emit pass (one resident grid; exits at once when none)
+template <int NV, int MODE, bool COOP = false>
+__global__ void __launch_bounds__(NT, 4) emit_redo_kernel(DecParams dp_) {
+  KParams& dp = KX_PARAMS();
+  (void)dp_;
+  __shared__ __attribute__((aligned(16))) uint32_t WIN[WAVES][WINW];
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const uint32_t W = gridDim.x * WAVES;
+  if (data_sig_s(dp) != dp.prog->sig) {   // emit_fast_kernel left the whole batch: every tile
+    for (uint64_t t = dp.t_lo + blockIdx.x * WAVES + wv; t < dp.t_hi; t += W)
+      emit_tile<NV, MODE, COOP>(dp, (LDS uint32_t*)WIN[wv], t, lane);
+    return;
+  }
+  const uint32_t n = __builtin_amdgcn_readfirstlane(*(volatile uint32_t*)(dp.redo_n + 2));
+  for (uint32_t i = blockIdx.x * WAVES + wv; i < n; i += W)
+    emit_tile<NV, MODE, COOP>(dp, (LDS uint32_t*)WIN[wv], __builtin_amdgcn_readfirstlane(dp.redo[i]), lane);
+}
+
 // ---- index of chunk k and emit of chunk k - 1 in one launch (KX_COMBO_MB): the first `nib` workgroups
 // index, the rest emit, so the index pass's VALU-bound waves and the emit pass's memory-bound waves share
 // every CU instead of running one after the other ----
@@ -3542,6 +3912,7 @@ __global__ void finalize_kernel(kx_status* st, unsigned long long* errkey, uint3
                                 const uint64_t* offsets, uint64_t n, uint32_t* redo_n) {
   if (threadIdx.x != 0) return;
   redo_n[0] = 0;
+  redo_n[2] = 0;   // the emit queue (emit_fast_kernel -> emit_redo_kernel)
   if (offsets) st->diag[2] = redo_n[1];   // known offsets: 2 the length gather ran, 3 and was repaired
   redo_n[1] = 0;   // the length-gather check flag (launch_t)
   unsigned long long k = *errkey;
@@ -3561,14 +3932,15 @@ __global__ void finalize_kernel(kx_status* st, unsigned long long* errkey, uint3
 //      record-start slots ----
 constexpr size_t WS_HDR = 512;
 // header words: [8] errkey, [16] overflow, [24] nstop, [64..) chain carry (CY_WORDS), [256..) nstop ring
-// (KX_PIPE_EV words), [448] redo count (u32), [452] length-gather check flag (u32)
+// (KX_PIPE_EV words), [448] redo count (u32), [452] length-gather check flag (u32), [456] emit queue count (u32),
+// [460] chain fallback flag (u32)
 constexpr size_t WS_CARRY = 64, WS_RING = 256, WS_REDO = 448;
-static_assert(WS_CARRY + 8 * CY_WORDS <= WS_RING && WS_RING + 8 * KX_PIPE_EV <= WS_REDO && WS_REDO + 8 <= WS_HDR,
+static_assert(WS_CARRY + 8 * CY_WORDS <= WS_RING && WS_RING + 8 * KX_PIPE_EV <= WS_REDO && WS_REDO + 16 <= WS_HDR,
               "workspace header layout");
 
 struct WsLayout {
   uint64_t ntiles, ngroups, slotcap;
-  size_t tdesc, gdesc, starts, redo, total;
+  size_t tdesc, gdesc, starts, redo, qcnt, total;
 };
 
 uint32_t krec_for(uint64_t in_len, uint64_t n) {
@@ -3617,6 +3989,8 @@ WsLayout ws_layout(uint64_t min_rec, uint64_t in_len, const uint64_t* offsets, u
   L.gdesc = o; o += (size_t)L.ngroups * G_NF * 8;
   L.starts = o; o += ((size_t)L.ntiles * L.slotcap * 2 + 255) & ~(size_t)255;
   L.redo = o; o += offsets ? 0 : ((size_t)L.ntiles * 4 + 255) & ~(size_t)255;   // fast index: redo queue
+  // chunked pipeline: per chunk the index and emit queue counts (u32 [0] and [2] of a 16-byte block)
+  L.qcnt = o; o += offsets ? 0 : ((size_t)L.ngroups * 16 + 255) & ~(size_t)255;
   L.total = o;
   return L;
 }
@@ -3655,6 +4029,60 @@ void launch_combo(unsigned grid, hipStream_t stream, const ComboParams& cp, uint
   hipLaunchKernelGGL((combo_kernel<NV, MODE, false>), dim3(grid), dim3(NT), 0, stream, cp);
 }
 
+// the chain pass: chain_fast_kernel, then chain_kernel gated on its fallback flag (ws header word
+// redo_n[3]); KX_CHAIN_FAST=0 (read per call) launches chain_kernel alone
+template <int NV, int MODE>
+int launch_chain(const DecParams& dp, hipStream_t stream) {
+  const char* e = getenv("KX_CHAIN_FAST");
+  if (dp.gate || (e && !atoi(e))) {
+    hipLaunchKernelGGL((chain_kernel<NV, MODE>), dim3(1), dim3(CT), 0, stream, dp);
+    return hipGetLastError() != hipSuccess ? KX_ERR_HIP : KX_OK;
+  }
+  DecParams f = dp;
+  f.gate = dp.redo_n + 3;
+  hipLaunchKernelGGL((chain_fast_kernel<NV, MODE>), dim3(1), dim3(CFT), 0, stream, f);
+  KX_HIP_CHECK(hipGetLastError());
+  f.gate_reset = 1;
+  hipLaunchKernelGGL((chain_kernel<NV, MODE>), dim3(1), dim3(CT), 0, stream, f);
+  return hipGetLastError() != hipSuccess ? KX_ERR_HIP : KX_OK;
+}
+
+// the split fast emit pass (emit_fast_kernel + emit_redo_kernel) when it applies: 1 launched, 0 not, -1 error.
+// It needs the fast index pass's T_CANON tiles (concatenated Thrift with a canonical plan) and a plan in emit
+// form (strings and fixed scalars only); KX_EMIT_FAST=0 keeps the general emit pass (A/B, read per call)
+template <int NV, int MODE>
+int launch_fast_emit(const DecParams& dp, unsigned grid, hipStream_t stream) {
+  if constexpr (MODE != M_THRIFT) {
+    return 0;
+  } else {
+    const char* e = getenv("KX_EMIT_FAST");
+    if ((e && !atoi(e)) || !dp.fast || dp.offsets || !dp.ep.ok || dp.diag || dp.split_out) return 0;
+    static int ncu_dev[64];
+    int dev = 0, ncu = 64;
+    if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64) {
+      int v = 0;
+      if (!ncu_dev[dev] && hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
+        ncu_dev[dev] = v + 1;
+      if (ncu_dev[dev] > 1) ncu = ncu_dev[dev] - 1;
+    }
+    const char* ne = getenv("KX_FAST_NARROW");
+    const bool narrow = (!ne || atoi(ne)) && dp.winb <= (uint32_t)FWINB;
+    const unsigned tiles = (unsigned)(dp.t_hi - dp.t_lo);
+    if (narrow)
+      hipLaunchKernelGGL((emit_fast_kernel<NV, true>), dim3((tiles + FWAVES - 1) / FWAVES), dim3(FNT), 0, stream, dp);
+    else
+      hipLaunchKernelGGL((emit_fast_kernel<NV, false>), dim3((tiles + WAVES - 1) / WAVES), dim3(NT), 0, stream, dp);
+    if (hipGetLastError() != hipSuccess) return -1;
+    const char* rg = getenv("KX_REDO_WG");   // workgroups per CU of the queue kernels (A/B; default 4)
+    const unsigned rgrid = (unsigned)kmin64(grid, (uint64_t)ncu * (rg ? (uint64_t)kmax64(1, atoi(rg)) : 4));
+    if (KX_EMIT_COOP && dp.nlist)
+      hipLaunchKernelGGL((emit_redo_kernel<NV, MODE, true>), dim3(rgrid), dim3(NT), 0, stream, dp);
+    else
+      hipLaunchKernelGGL((emit_redo_kernel<NV, MODE, false>), dim3(rgrid), dim3(NT), 0, stream, dp);
+    return hipGetLastError() != hipSuccess ? -1 : 1;
+  }
+}
+
 // the split fast index pass (index_fast_kernel + redo_kernel) when it applies: 1 launched, 0 not, -1 error
 template <int NV, int MODE>
 int launch_fast_index(const DecParams& dp, unsigned grid, hipStream_t stream) {
@@ -3672,15 +4100,18 @@ int launch_fast_index(const DecParams& dp, unsigned grid, hipStream_t stream) {
     }
     static int narrow_env = -1;
     if (narrow_env < 0) { const char* e = getenv("KX_FAST_NARROW"); narrow_env = e ? atoi(e) : 1; }
+    const uint64_t tiles = dp.t_hi - dp.t_lo;
     if (narrow_env && dp.winb <= (uint32_t)FWINB) {
-      const unsigned fgrid = (unsigned)((dp.ntiles + FWAVES - 1) / FWAVES);
+      const unsigned fgrid = (unsigned)((tiles + FWAVES - 1) / FWAVES);
       hipLaunchKernelGGL((index_fast_kernel<NV, true>), dim3(fgrid), dim3(FNT), 0, stream, dp);
     } else {
-      hipLaunchKernelGGL((index_fast_kernel<NV, false>), dim3(grid), dim3(NT), 0, stream, dp);
+      hipLaunchKernelGGL((index_fast_kernel<NV, false>), dim3((unsigned)((tiles + WAVES - 1) / WAVES)), dim3(NT), 0,
+                         stream, dp);
     }
     if (hipGetLastError() != hipSuccess) return -1;
     // the queued tiles: one resident grid's worth of waves at most (4 workgroups per CU)
-    const unsigned rgrid = (unsigned)kmin64(grid, (uint64_t)(ncu > 0 ? ncu : 64) * 4);
+    const char* rg = getenv("KX_REDO_WG");   // workgroups per CU of the queue kernels (A/B; default 4)
+    const unsigned rgrid = (unsigned)kmin64(grid, (uint64_t)(ncu > 0 ? ncu : 64) * (rg ? (uint64_t)kmax64(1, atoi(rg)) : 4));
     hipLaunchKernelGGL((redo_kernel<NV, MODE>), dim3(rgrid), dim3(NT), 0, stream, dp);
     return hipGetLastError() != hipSuccess ? -1 : 1;
   }
@@ -3755,6 +4186,18 @@ int launch_t(const DecParams& dp0, const WsLayout& L, void* ws, hipStream_t stre
     // but emit passes, each behind the event of its chunk's chain
     const uint64_t nch = (dp.ntiles + cht - 1) / cht;
     const uint64_t D = (uint64_t)(pp->ahead < 0 ? 0 : pp->ahead > KX_PIPE_EV - 2 ? KX_PIPE_EV - 2 : pp->ahead);
+    // each chunk queues the tiles its fast index / emit kernels leave in its own part of the redo list,
+    // counted in its own block (zeroed here)
+    uint32_t* const qcnt = (uint32_t*)(base + L.qcnt);
+    uint32_t* const qlist = dp.redo;
+    KX_HIP_CHECK(hipMemsetAsync(qcnt, 0, (size_t)nch * 16, stream));
+    auto chunk = [&](uint64_t k) {
+      DecParams c = chunk_params(dp, k, nch, cht);
+      c.nstop = dp.nstop_ring + k % KX_PIPE_EV;
+      c.redo = qlist + c.t_lo;
+      c.redo_n = qcnt + 4 * k;
+      return c;
+    };
     KX_HIP_CHECK(hipEventRecord(pp->fork, stream));
     KX_HIP_CHECK(hipStreamWaitEvent(pp->aux, pp->fork, 0));
     for (uint64_t s = 0; s < nch + D; s++) {
@@ -3763,25 +4206,26 @@ int launch_t(const DecParams& dp0, const WsLayout& L, void* ws, hipStream_t stre
         // the index pass runs at most `ahead` chunks in front of emit (Infinity-Cache residency; the
         // nstop ring slot k % KX_PIPE_EV is free again once emit(k - D - 1) has read it)
         if (k >= D + 1) KX_HIP_CHECK(hipStreamWaitEvent(pp->aux, pp->ev_emit[(k - D - 1) % KX_PIPE_EV], 0));
-        DecParams c = chunk_params(dp, k, nch, cht);
-        c.nstop = dp.nstop_ring + k % KX_PIPE_EV;
+        const DecParams c = chunk(k);
         const unsigned cg = (unsigned)((c.t_hi - c.t_lo + WAVES - 1) / WAVES);
         const unsigned gg = (unsigned)((c.g_hi - c.g_lo + WAVES - 1) / WAVES);
-        hipLaunchKernelGGL((index_kernel<NV, MODE>), dim3(cg), dim3(NT), 0, pp->aux, c);
+        const int lr = launch_fast_index<NV, MODE>(c, cg, pp->aux);
+        if (lr < 0) return KX_ERR_HIP;
+        if (lr == 0) hipLaunchKernelGGL((index_kernel<NV, MODE>), dim3(cg), dim3(NT), 0, pp->aux, c);
         KX_HIP_CHECK(hipGetLastError());
         hipLaunchKernelGGL((group_kernel<NV, MODE>), dim3(gg), dim3(NT), 0, pp->aux, c);
         KX_HIP_CHECK(hipGetLastError());
-        hipLaunchKernelGGL((chain_kernel<NV, MODE>), dim3(1), dim3(CT), 0, pp->aux, c);
-        KX_HIP_CHECK(hipGetLastError());
+        if (int rc = launch_chain<NV, MODE>(c, pp->aux)) return rc;
         KX_HIP_CHECK(hipEventRecord(pp->ev_idx[k % KX_PIPE_EV], pp->aux));
       }
       if (s >= D) {
         const uint64_t k = s - D;
-        DecParams c = chunk_params(dp, k, nch, cht);
-        c.nstop = dp.nstop_ring + k % KX_PIPE_EV;
+        const DecParams c = chunk(k);
         const unsigned cg = (unsigned)((c.t_hi - c.t_lo + WAVES - 1) / WAVES);
         KX_HIP_CHECK(hipStreamWaitEvent(stream, pp->ev_idx[k % KX_PIPE_EV], 0));
-        launch_emit<NV, MODE>(dim3(cg), stream, c);
+        const int fe = launch_fast_emit<NV, MODE>(c, cg, stream);
+        if (fe < 0) return KX_ERR_HIP;
+        if (fe == 0) launch_emit<NV, MODE>(dim3(cg), stream, c);
         KX_HIP_CHECK(hipGetLastError());
         KX_HIP_CHECK(hipEventRecord(pp->ev_emit[k % KX_PIPE_EV], stream));
       }
@@ -3828,14 +4272,17 @@ int launch_t(const DecParams& dp0, const WsLayout& L, void* ws, hipStream_t stre
     }
   }
   if (!dp.direct) {
-    static int ncu = -1;
+    static int ncu_dev[64];   // CU count + 1 per device ordinal (0: not yet asked)
     const char* e = getenv("KX_INDEX_PF");
     const int pf = e ? atoi(e) : 0;
-    if (pf > 0 && ncu < 0) {
-      int dev = 0;
-      if (hipGetDevice(&dev) != hipSuccess ||
-          hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-        ncu = 0;
+    int ncu = 0;
+    if (pf > 0) {
+      int dev = 0, v = 0;
+      if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64) {
+        if (!ncu_dev[dev] && hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
+          ncu_dev[dev] = v + 1;
+        ncu = ncu_dev[dev] ? ncu_dev[dev] - 1 : 0;
+      }
     }
     int lr = launch_fast_index<NV, MODE>(dp, grid, stream);
     if (lr < 0) return KX_ERR_HIP;
@@ -3850,8 +4297,7 @@ int launch_t(const DecParams& dp0, const WsLayout& L, void* ws, hipStream_t stre
   indexed:
     hipLaunchKernelGGL((group_kernel<NV, MODE>), dim3(ggrid), dim3(NT), 0, stream, dp);
     KX_HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL((chain_kernel<NV, MODE>), dim3(1), dim3(CT), 0, stream, dp);
-    KX_HIP_CHECK(hipGetLastError());
+    if (int rc = launch_chain<NV, MODE>(dp, stream)) return rc;
   }
   if constexpr (is_thrift(MODE) || MODE == M_SKIP) {
     if (dp.split_out) {   // split points: the chain pass's tile bases and slots, no emit
@@ -3860,7 +4306,11 @@ int launch_t(const DecParams& dp0, const WsLayout& L, void* ws, hipStream_t stre
       goto done;
     }
   }
-  launch_emit<NV, MODE>(dim3(grid), stream, dp);
+  {
+    const int fe = launch_fast_emit<NV, MODE>(dp, grid, stream);
+    if (fe < 0) return KX_ERR_HIP;
+    if (fe == 0) launch_emit<NV, MODE>(dim3(grid), stream, dp);
+  }
   KX_HIP_CHECK(hipGetLastError());
 done:
   hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(64), 0, stream, dp.status, dp.errkey, dp.overflow, dp.nstop,
@@ -4008,11 +4458,13 @@ static uint32_t win_bytes(uint64_t in_len, uint64_t n) {
 int kx_launch_decode(const KxProgram* dprog, const KxProgram& hprog, const uint8_t* in, uint64_t in_len,
                      const uint64_t* offsets, uint64_t n, const KxLaunchCols& cols, uint8_t* record_status,
                      kx_status* status, void* ws, size_t ws_size, uint64_t epoch, hipStream_t stream, bool pb,
-                     const uint64_t* ends, const uint64_t* var_base, const KxPipe* pipe) {
+                     const uint64_t* ends, const uint64_t* var_base, const KxPipe* pipe,
+                     const uint64_t* var_base_dev) {
   DecParams dp{};
   fill_diag_flags(dp);
   if (var_base)
     for (int v = 0; v < KXP_NV_MAX; v++) dp.var_base[v] = var_base[v];
+  dp.var_base_dev = var_base_dev;
   dp.in = in; dp.in_len = in_len; dp.offsets = offsets; dp.ends = offsets ? ends : nullptr; dp.n = n;
   dp.prog = (const KAS KxProgram*)dprog;
   dp.cols = cols; dp.rstat = record_status; dp.status = status; dp.epoch = epoch;
@@ -4028,6 +4480,15 @@ int kx_launch_decode(const KxProgram* dprog, const KxProgram& hprog, const uint8
     static int fp_env = -1;
     if (fp_env < 0) { const char* e = getenv("KX_FASTPLAN"); fp_env = e ? atoi(e) : 1; }
     if (dp.fast && fp_env) kxp_fast_plan(hprog, dp.fp);
+    if (dp.fast && !pb && !offsets) {
+      kxp_emit_plan(hprog, dp.ep);
+      // every var slot is a string, or a numeric list absent from the plan (its records hold none): the
+      // fast emit pass writes each slot's record offsets with no container logic
+      for (uint32_t v = 0; v < hprog.nvar && dp.ep.ok; v++) {
+        const KxpCol& K = hprog.col[hprog.var_col[v]];
+        if (!(K.kind == KXP_K_BYTES || (K.kind == KXP_K_LIST && !K.mside))) dp.ep.ok = 0;
+      }
+    }
   }
   for (uint32_t c = 0; c < hprog.ncols; c++) {
     const KxpCol& K = hprog.col[c];

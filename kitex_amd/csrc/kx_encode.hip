@@ -68,6 +68,8 @@ struct EncParams {
   uint64_t* offsets_out;
   kx_status* status;
   uint64_t* block_tot;   // workspace: per-block total size, then (after scan) block base
+  const uint64_t* out_base;  // device: where this call's first record goes in `out` (a chunk of a larger
+                             // batch: the previous chunk's status->consumed), null = 0
   uint64_t nblocks;
   bool pb;               // Kitex-Protobuf records (Batch framing) instead of Thrift binary
   int direct;            // tuning (KX_ENC_DIRECT=1): every round writes straight to HBM
@@ -885,7 +887,8 @@ __global__ void __launch_bounds__(1024) scan_kernel(EncParams ep) {
   uint64_t s = 0;
   for (uint64_t i = lo; i < hi; i++) s += ep.block_tot[i];
   uint64_t tot;
-  uint64_t run = block_excl_scan(s, &tot, scratch);
+  const uint64_t b0 = ep.out_base ? *ep.out_base : 0;
+  uint64_t run = b0 + block_excl_scan(s, &tot, scratch);
   for (uint64_t i = lo; i < hi; i++) {
     uint64_t v = ep.block_tot[i];
     ep.block_tot[i] = run;
@@ -894,9 +897,9 @@ __global__ void __launch_bounds__(1024) scan_kernel(EncParams ep) {
   if (threadIdx.x == 0) {
     kx_status* st = ep.status;
     st->n_records = ep.n;
-    st->consumed = tot;
-    st->code = tot > ep.out_cap ? KX_ERR_SIZE_LIMIT : 0;
-    if (ep.offsets_out && tot <= ep.out_cap) ep.offsets_out[ep.n] = tot;
+    st->consumed = b0 + tot;
+    st->code = b0 + tot > ep.out_cap ? KX_ERR_SIZE_LIMIT : 0;
+    if (ep.offsets_out && b0 + tot <= ep.out_cap) ep.offsets_out[ep.n] = b0 + tot;
   }
 }
 
@@ -1007,10 +1010,11 @@ size_t kx_encode_ws_bytes(uint64_t n) { return ((n + RB - 1) / RB) * 8 + 256; }
 int kx_launch_encode(const KxProgram* dprog, const KxProgram& hprog, const KxLaunchCols& cols, uint64_t n,
                      uint8_t* out, uint64_t out_cap, uint64_t* sizes_out, uint64_t* offsets_out,
                      kx_status* status, void* ws, size_t ws_size, hipStream_t stream, bool sizes_only,
-                     bool pb) {
+                     bool pb, const uint64_t* out_base) {
   (void)hprog;
   EncParams ep{};
   ep.pb = pb;
+  ep.out_base = out_base;
   ep.prog = dprog; ep.cols = cols; ep.n = n; ep.out = out; ep.out_cap = out_cap;
   ep.sizes_out = sizes_out; ep.offsets_out = offsets_out; ep.status = status;
   ep.nblocks = (n + RB - 1) / RB;

@@ -44,6 +44,8 @@ struct KxPipe {
   uint64_t combo_tiles = 0;             // one-stream schedule: index(k) + emit(k - 1) per launch (0: off)
 };
 
+#define KX_HOST_CH 16   // record-range chunks of the kx_host_* pipelines
+
 struct kx_ctx {
   int device = 0;
   KxPipe pipe;                         // created lazily (ensure_pipe)
@@ -81,6 +83,9 @@ struct kx_ctx {
   // grow-only device staging for kx_host_decode_batch (input, offsets, columns, status)
   void* dstage = nullptr;
   size_t dstage_size = 0;
+  // kx_host_* pipelines: per chunk, input landed / kernel done / status copied out; pinned status staging
+  hipEvent_t hev_in[KX_HOST_CH] = {}, hev_run[KX_HOST_CH] = {}, hev_st[KX_HOST_CH] = {};
+  kx_status* hst = nullptr;
 };
 
 // kx_schema.cpp / kx_nested_schema.cpp
@@ -119,7 +124,7 @@ int kx_launch_decode(const KxProgram* dprog, const KxProgram& hprog, const uint8
                      const KxLaunchCols& cols, uint8_t* record_status, kx_status* status,
                      void* ws, size_t ws_size, uint64_t epoch, hipStream_t stream, bool pb,
                      const uint64_t* ends = nullptr, const uint64_t* var_base = nullptr,
-                     const KxPipe* pipe = nullptr);
+                     const KxPipe* pipe = nullptr, const uint64_t* var_base_dev = nullptr);
 size_t kx_decode_ws_bytes(const KxProgram& hprog, uint64_t in_len, const uint64_t* offsets, uint64_t n);
 
 int kx_launch_skip(const uint8_t* in, uint64_t in_len, uint64_t n, uint64_t* offsets_out,
@@ -142,7 +147,7 @@ int kx_launch_frames(const uint8_t* in, uint64_t in_len, uint64_t n, uint64_t ma
 int kx_launch_encode(const KxProgram* dprog, const KxProgram& hprog, const KxLaunchCols& cols,
                      uint64_t n, uint8_t* out, uint64_t out_cap, uint64_t* sizes_out,
                      uint64_t* offsets_out, kx_status* status, void* ws, size_t ws_size,
-                     hipStream_t stream, bool sizes_only, bool pb = false);
+                     hipStream_t stream, bool sizes_only, bool pb = false, const uint64_t* out_base = nullptr);
 size_t kx_encode_ws_bytes(uint64_t n);
 
 // kx_message.hip: MessageBegin + Args{1: Req} headers of n framed messages (lane = message)

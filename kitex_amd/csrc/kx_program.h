@@ -53,8 +53,7 @@ struct KxpInst {       // 32 B
   int8_t parent;          // parent instance, -1 for the root
   int8_t ret_pred;        // predictor to resume with in the parent after this struct's STOP
   int8_t self_field;      // flat field (in the parent) holding this instance
-  uint8_t vslot_mask;     // var slots inside this instance's subtree
-  int8_t pad;
+  uint16_t vslot_mask;    // var slots inside this instance's subtree (KXP_NV_MAX = 16 bits)
 };
 
 struct KxpCol {        // 16 B
@@ -186,6 +185,72 @@ static inline void kxp_fast_plan(const KxProgram& P, KxpFast& F) {
   F.ok = ok ? 1u : 0u;
 }
 
+// The canonical plan as the fast emit pass executes it (emit_fast_kernel, T_CANON tiles): per segment the
+// fixed fields of its run (value offset after the 3-byte header, wire type, column) and at most one string
+// field after the run. Every offset inside a segment is a constant, so a record's fixed values are read
+// with no dependence on each other; only the string lengths chain the segments. Schemas whose canonical
+// plan holds a numeric list, more than KXE_SEG - 1 strings or more than KXE_FIX fixed fields in one run
+// take the general emit pass (ok = 0).
+#define KXE_SEG 4
+#define KXE_FIX 16
+struct KxpEmitFix {           // 4 B
+  uint16_t off;               // value offset in the segment (past the field header)
+  uint8_t ttype;              // wire type (BOOL: b == 1; BYTE / I16 / I32 / I64 / DOUBLE: big-endian)
+  uint8_t col;                // FIXED column
+};
+struct KxpEmitSeg {           // 72 B
+  uint16_t flen;              // bytes of the fixed run (headers, values, struct headers, STOPs)
+  uint8_t nfix;
+  uint8_t vkind;              // 0: the record ends with this run, 1: a string / binary field follows
+  uint8_t vslot;              // its var slot
+  uint8_t vcol;               // and column
+  uint16_t pad;
+  KxpEmitFix fix[KXE_FIX];
+};
+struct KxpEmit {
+  uint32_t ok, nseg;
+  KxpEmitSeg seg[KXE_SEG];
+};
+
+// host: the emit form of a program's canonical plan
+static inline void kxp_emit_plan(const KxProgram& P, KxpEmit& E) {
+  E = KxpEmit{};
+  if (!P.nsteps || P.is_pb) return;
+  uint32_t off = 0;
+  bool ok = true;
+  KxpEmitSeg* G = &E.seg[0];
+  E.nseg = 1;
+  for (uint32_t k = 0; k < P.nsteps && ok; k++) {
+    const KxpStep& st = P.steps[k];
+    switch (st.kind) {
+      case KXP_S_FIXED:
+        if (G->nfix >= KXE_FIX || st.col < 0 || off + 3 > 0xffff ||
+            !(st.width == 1 || st.width == 2 || st.width == 4 || st.width == 8)) { ok = false; break; }
+        G->fix[G->nfix++] = KxpEmitFix{(uint16_t)(off + 3), (uint8_t)(st.hdr & 0xff), (uint8_t)st.col};
+        off += 3u + st.width;
+        break;
+      case KXP_S_STRUCT: off += 3u; break;
+      case KXP_S_END: off += 1u; break;
+      case KXP_S_BYTES: {
+        const uint32_t c = st.vslot < KXP_NV_MAX ? P.var_col[st.vslot] : 0xffu;
+        if (E.nseg >= KXE_SEG || off > 0xffff || c >= KXP_MAX_COLS || P.col[c].kind != KXP_K_BYTES) { ok = false; break; }
+        G->flen = (uint16_t)off;
+        G->vkind = 1;
+        G->vslot = st.vslot;
+        G->vcol = (uint8_t)c;
+        G = &E.seg[E.nseg++];
+        off = 0;
+        break;
+      }
+      default: ok = false;   // numeric lists: the general emit pass (its wave-cooperative copy)
+    }
+  }
+  if (off > 0xffff) ok = false;
+  G->flen = (uint16_t)off;
+  E.ok = ok ? 1u : 0u;
+}
+
+static_assert(sizeof(KxpEmitSeg) == 72, "KxpEmitSeg layout");
 static_assert(sizeof(KxpField) == 16, "KxpField layout");
 static_assert(sizeof(KxpInst) == 32, "KxpInst layout");
 static_assert(sizeof(KxpCol) == 16, "KxpCol layout");

@@ -288,15 +288,15 @@ int kx_build_program(const kx_struct_desc* structs, uint32_t nstructs, kx_schema
   for (int i = (int)P.ninst - 1; i >= 0; i--) {
     KxpInst& I = P.inst[i];
     uint64_t m = 0, pm = 0;
-    uint8_t vm = 0;
+    uint16_t vm = 0;
     for (int k = 0; k < I.nfields; k++) {
       const KxpField& F = P.f[I.first + k];
       m |= 1ull << (I.first + k);
       if (F.pbit >= 0) pm |= 1ull << F.pbit;
       if (F.col >= 0)  // every var slot of the field's columns (map: both sides; LISTB: both slots)
         for (int cc = F.col; cc <= F.col + (F.kind == KXP_K_MAP ? 1 : F.kind == KXP_K_LSTRUCT ? F.width - 1 : 0); cc++) {
-          if (P.col[cc].vslot != 0xff) vm |= (uint8_t)(1u << P.col[cc].vslot);
-          if (P.col[cc].vslot2 != 0xff) vm |= (uint8_t)(1u << P.col[cc].vslot2);
+          if (P.col[cc].vslot != 0xff) vm |= (uint16_t)(1u << P.col[cc].vslot);
+          if (P.col[cc].vslot2 != 0xff) vm |= (uint16_t)(1u << P.col[cc].vslot2);
         }
       if (F.child >= 0) {
         m |= P.inst[F.child].subtree_mask;

@@ -18,6 +18,7 @@ BASELINE.json (112M R2 + 16M R3 records sharded across the GPUs, concatenation o
 """
 from __future__ import annotations
 
+import ctypes as C
 from typing import List, Optional, Sequence, Tuple
 
 from . import _abi as A
@@ -60,15 +61,36 @@ def _kind(col, ci):
     return k
 
 
+def _depth(ci) -> int:
+    return 0 if ci.kind == A.COL_FIXED else _DEPTH[ci.kind]
+
+
 def _meta(cols: ColumnSet, n: int, infos, in_len: int, dev):
-    """this rank's exchange header, built on the device: n, input bytes, then per var column and per
-    level j of its offsets chain the first entry f_j and the units u_j it spans (f_0 = o_0[0],
-    u_0 = o_0[n] - f_0; f_{j+1} = o_{j+1}[f_j], u_{j+1} = o_{j+1}[f_j + u_j] - f_{j+1})"""
+    """this rank's exchange header (include/kxcodec.h kx_shard_meta): n, input bytes, then per non-FIXED
+    column and per level j of its offsets chain the first entry f_j and the units u_j it spans (f_0 =
+    o_0[0], u_0 = o_0[n] - f_0; f_{j+1} = o_{j+1}[f_j], u_{j+1} = o_{j+1}[f_j + u_j] - f_{j+1}); a view
+    column's words are 0. Device columns: kx_shard_meta (one wave on the device); host tensors (the gloo
+    test harness): the same words with torch ops."""
     import torch
+    if dev.type == "cuda":
+        from .codec import _ctx_for
+        from .columns import to_kx_columns
+        from ._lib import check, lib
+        L = lib()
+        cinfos = (A.ColumnInfo * max(1, len(infos)))(*infos)
+        words = L.kx_shard_meta_words(cinfos, len(infos))
+        meta = torch.empty(words, dtype=torch.int64, device=dev)
+        kc = to_kx_columns(cols, infos)
+        s = torch.cuda.current_stream(dev)
+        check(L.kx_shard_meta(_ctx_for(dev.index or 0, s).handle, cinfos, len(infos), C.byref(kc), n, in_len,
+                              meta.data_ptr(), int(s.cuda_stream)), "kx_shard_meta")
+        return meta
     parts = [torch.tensor([n, in_len], dtype=torch.int64, device=dev)]
     for c, ci in enumerate(infos):
         k = _kind(cols.cols[c], ci)
-        if isinstance(k, int):
+        if k == "view":
+            parts.append(torch.zeros(2 * _depth(ci), dtype=torch.int64, device=dev))
+        elif isinstance(k, int):
             col = cols.cols[c]
             f, l = _unsigned(col[0][0:1]), _unsigned(col[0][n:n + 1])
             parts += [f, l - f]
@@ -79,8 +101,8 @@ def _meta(cols: ColumnSet, n: int, infos, in_len: int, dev):
 
 
 def rebase(dst, src, delta: int):
-    """dst[:] = src (uint32 values in int32, or int64) + delta, as int64, on src's device: the offset
-    rebase of the concatenation (one add per rank slice, no host round trip)"""
+    """dst[:] = src (uint32 values in int32, or int64) + delta, as int64 (host tensors; device columns
+    go through kx_concat_rebase)"""
     if dst.numel():
         dst.copy_(_unsigned(src) + delta)
 
@@ -95,126 +117,131 @@ def rebase_views(dst, src, delta: int):
     dst[:, 0] = torch.where(s[:, 1] != 0, s[:, 0] + delta, torch.zeros_like(s[:, 0]))
 
 
+def _arrays(col, k):
+    """a column's arrays by KX_PIECE_* index (offsets, elem_offsets, sub_offsets, data)"""
+    if k == "fixed":
+        return [None, None, None, col]
+    if k == "view":
+        return [col.pairs, None, None, None]
+    return list(col[:k]) + [None] * (3 - k) + [col[k]]
+
+
 class _Plan:
-    """Where every rank's slice lands in the concatenation, from the ranks' exchange headers (_meta).
-    For a column of depth k, rank r sends o_0[:n] and, for j = 1 .. k-1, the o_j entries its o_{j-1}
-    slice spans, then its data; the root rebases its o_j slice by (the units of o_{j+1} (or data) the
-    ranks before it hold) - f_{j+1}(r), and closes every level with the total."""
+    """Where every rank's slice lands in the concatenation: kx_concat_plan (libkxcodec, host code) over
+    the ranks' exchange headers. A piece of an offsets array (or a view column's pairs) lands in a
+    staging array in the sender's width, which kx_concat_rebase (device) or rebase / rebase_views (host
+    tensors) turn into the output's int64 entries plus the ranks' bases, closing every level."""
 
-    def __init__(self, metas, kinds):
-        self.kinds = kinds
-        self.world = world = len(metas)
-        self.counts = [m[0] for m in metas]
-        inl = [m[1] for m in metas]
-        self.info = []  # per rank, per var column: [(f_j, u_j) for each level j]
-        for m in metas:
-            i, d = 2, {}
-            for c, k in enumerate(kinds):
-                if isinstance(k, int):
-                    d[c] = [(m[i + 2 * j], m[i + 2 * j + 1]) for j in range(k)]
-                    i += 2 * k
-            self.info.append(d)
-        self.N = sum(self.counts)
-        self.rec0 = [sum(self.counts[:r]) for r in range(world)]
-        self.in0 = [sum(inl[:r]) for r in range(world)]
-        # base[c][j][r]: units of level j held by the ranks before r (r = world: the total)
-        self.base = {c: [[sum(self.info[q][c][j][1] for q in range(r)) for r in range(world + 1)]
-                         for j in range(k)]
-                     for c, k in enumerate(kinds) if isinstance(k, int)}
+    def __init__(self, metas, kinds, infos, like: ColumnSet):
+        import numpy as np
 
-    def _slices(self, c, k, r, n):
-        """(start, length) of rank r's piece of each array o_0 .. o_{k-1}, data, in its own column"""
-        info = self.info[r][c]
-        out = [(0, n)]
-        for j in range(1, k):
-            out.append(info[j - 1])       # o_j entries spanned by the o_{j-1} slice
-        out.append(info[k - 1])           # data units spanned by o_{k-1}
-        return out
+        from .columns import to_kx_columns
+        from ._lib import KxError, check, lib
+        self.kinds, self.infos = kinds, infos
+        self.world = len(metas)
+        self.cinfos = (A.ColumnInfo * max(1, len(infos)))(*infos)
+        L = lib()
+        m = np.ascontiguousarray(np.array(metas, dtype=np.int64).view(np.uint64))
+        if m.shape[1] != L.kx_shard_meta_words(self.cinfos, len(infos)):
+            raise KxError(A.ERR_INVALID_ARG, "concat: exchange header size")
+        layout = to_kx_columns(like, infos)
+        mp = m.ctypes.data_as(C.POINTER(C.c_uint64))
+        cnt, sizes = C.c_uint32(0), A.ConcatSizes()
+        rc = L.kx_concat_plan(self.cinfos, len(infos), C.byref(layout), mp, self.world, None, C.byref(cnt),
+                              C.byref(sizes))
+        if rc not in (0, A.ERR_SIZE_LIMIT):
+            check(rc, "kx_concat_plan")
+        self.pieces = (A.ConcatPiece * max(1, cnt.value))()
+        check(L.kx_concat_plan(self.cinfos, len(infos), C.byref(layout), mp, self.world, self.pieces,
+                               C.byref(cnt), C.byref(sizes)), "kx_concat_plan")
+        self.npieces, self.sizes = cnt.value, sizes
+        self.N = int(sizes.n)
+        self.counts = [int(x[0]) for x in metas]
+        self.rec0 = [sum(self.counts[:r]) for r in range(self.world)]
+        self.by_rank = [[self.pieces[i] for i in range(self.npieces) if self.pieces[i].rank == r]
+                        for r in range(self.world)]
+
+    def _src(self, cs: ColumnSet, p):
+        if p.column == A.MAX_COLUMNS:
+            return cs.presence
+        return _arrays(cs.cols[p.column], self.kinds[p.column])[p.array]
 
     def local_parts(self, cs: ColumnSet, r: int, n: int):
-        """what rank r contributes, in a fixed order: per column its pieces, then presence"""
-        out = []
-        for c, k in enumerate(self.kinds):
-            col = cs.cols[c]
-            if k == "fixed":
-                out.append(col[:n])
-            elif k == "view":
-                out.append(col.pairs[:n])
-            else:
-                for j, (a, u) in enumerate(self._slices(c, k, r, n)):
-                    out.append(col[j][a:a + u])
-        if cs.presence is not None:
-            out.append(cs.presence[:n])
-        return out
+        """what rank r contributes, in piece order"""
+        assert n == self.counts[r]
+        return [self._src(cs, p)[p.src_first:p.src_first + p.count] for p in self.by_rank[r]]
 
     def alloc(self, like: ColumnSet, dev):
-        """the concatenated batch (int64 offsets / views) and the staging of the ranks' offsets / views
-        (in the senders' dtypes) that the rebase reads"""
+        """the concatenated batch (int64 offsets / views) and the staging arrays of the received offsets
+        (in the senders' dtypes)"""
         import torch
 
         from .columns import Views
-        N, W = self.N, self.world
-        out_cols, self.recv = [], {}
+        N, U = self.N, self.sizes.units
+        out_cols, stage_cols = [], []
         for c, k in enumerate(self.kinds):
             col = like.cols[c]
             if k == "fixed":
                 out_cols.append(torch.empty(N, dtype=col.dtype, device=dev))
+                stage_cols.append(None)
             elif k == "view":
                 out_cols.append(Views(torch.empty((max(1, N), 2), dtype=torch.int64, device=dev)))
-                self.recv[c] = (torch.empty((max(1, N), 2), dtype=col.pairs.dtype, device=dev),)
+                stage_cols.append(Views(torch.empty((max(1, N), 2), dtype=col.pairs.dtype, device=dev)))
             else:
-                sizes = [N] + [self.base[c][j - 1][W] for j in range(1, k)]   # entries of o_j before closing
-                parts = [torch.empty(s + 1, dtype=torch.int64, device=dev) for s in sizes]
-                parts.append(torch.empty(max(1, self.base[c][k - 1][W]), dtype=col[k].dtype, device=dev))
+                parts = [torch.empty(int(U[c][j]) + 1, dtype=torch.int64, device=dev) for j in range(k)]
+                parts.append(torch.empty(max(1, int(U[c][A.PIECE_DATA])), dtype=col[k].dtype, device=dev))
                 out_cols.append(tuple(parts))
-                self.recv[c] = tuple(torch.empty(max(1, s), dtype=col[j].dtype, device=dev)
-                                     for j, s in enumerate(sizes))
+                stage_cols.append(tuple(torch.empty(max(1, int(U[c][j])), dtype=col[j].dtype, device=dev)
+                                        for j in range(k)) + (parts[k],))
         pres = torch.empty(N, dtype=like.presence.dtype, device=dev) if like.presence is not None else None
         self.out = ColumnSet(out_cols, pres, N)
+        self.stage = ColumnSet([s if s is not None else o for s, o in zip(stage_cols, out_cols)], pres, N)
         return self.out
-
-    def _dest_off(self, c, j, r):
-        """where rank r's piece of o_j (j >= 1: entries of level j - 1) or data (j = k) starts"""
-        return self.rec0[r] if j == 0 else self.base[c][j - 1][r]
 
     def dest_parts(self, r: int):
         """where rank r's pieces (local_parts order) are received"""
-        out, d = self.out, []
-        a, b = self.rec0[r], self.rec0[r] + self.counts[r]
-        for c, k in enumerate(self.kinds):
-            if k == "fixed":
-                d.append(out.cols[c][a:b])
-            elif k == "view":
-                d.append(self.recv[c][0][a:b])
+        out = []
+        for p in self.by_rank[r]:
+            if p.column == A.MAX_COLUMNS:
+                dst = self.out.presence
+            elif p.array == A.PIECE_DATA:
+                dst = _arrays(self.out.cols[p.column], self.kinds[p.column])[A.PIECE_DATA]
             else:
-                for j, (_, u) in enumerate(self._slices(c, k, r, self.counts[r])):
-                    s0 = self._dest_off(c, j, r)
-                    d.append((self.recv[c][j] if j < k else out.cols[c][k])[s0:s0 + u])
-        if out.presence is not None:
-            d.append(out.presence[a:b])
-        return d
+                dst = _arrays(self.stage.cols[p.column], self.kinds[p.column])[p.array]
+            out.append(dst[p.dst_first:p.dst_first + p.count])
+        return out
 
     def rebase_all(self):
-        """every rank's slice, on the device: level j's entries by the units of level j + 1 (or data)
-        before it, views by the input bytes before it; then the closing entry of every level"""
-        out, W = self.out, self.world
-        for c, k in enumerate(self.kinds):
-            if k == "fixed":
+        """staging offsets + each piece's base -> output, closing entries: kx_concat_rebase on the device"""
+        import torch
+        dev = _device_of(self.out)
+        if dev.type == "cuda":
+            from .codec import _ctx_for
+            from .columns import to_kx_columns
+            from ._lib import check, lib
+            s = torch.cuda.current_stream(dev)
+            ks, ko = to_kx_columns(self.stage, self.infos), to_kx_columns(self.out, self.infos)
+            check(lib().kx_concat_rebase(_ctx_for(dev.index or 0, s).handle, self.cinfos, len(self.infos),
+                                         self.pieces, self.npieces, C.byref(ks), C.byref(ko), C.byref(self.sizes),
+                                         int(s.cuda_stream)), "kx_concat_rebase")
+            return
+        # host tensors (the gloo test harness): the same arithmetic with torch ops
+        for i in range(self.npieces):
+            p = self.pieces[i]
+            if p.column == A.MAX_COLUMNS or p.array == A.PIECE_DATA:
                 continue
-            for r in range(W):
-                a, b = self.rec0[r], self.rec0[r] + self.counts[r]
-                if k == "view":
-                    rebase_views(out.cols[c].pairs[a:b], self.recv[c][0][a:b], self.in0[r])
-                    continue
-                for j, (_, u) in enumerate(self._slices(c, k, r, self.counts[r])[:k]):
-                    s0 = self._dest_off(c, j, r)
-                    f_next = self.info[r][c][j][0]
-                    rebase(out.cols[c][j][s0:s0 + u], self.recv[c][j][s0:s0 + u], self.base[c][j][r] - f_next)
+            k = self.kinds[p.column]
+            a, b = p.dst_first, p.dst_first + p.count
             if k == "view":
+                rebase_views(self.out.cols[p.column].pairs[a:b], self.stage.cols[p.column].pairs[a:b], p.rebase)
+            else:
+                rebase(self.out.cols[p.column][p.array][a:b], self.stage.cols[p.column][p.array][a:b], p.rebase)
+        for c, k in enumerate(self.kinds):
+            if not isinstance(k, int):
                 continue
             for j in range(k):
-                end = self.N if j == 0 else self.base[c][j - 1][W]
-                out.cols[c][j][end] = self.base[c][j][W]
+                nxt = self.sizes.units[c][j + 1 if j + 1 < k else A.PIECE_DATA]
+                self.out.cols[c][j][int(self.sizes.units[c][j])] = int(nxt)
 
 
 def _check_views(kinds, in_len):
@@ -252,7 +279,7 @@ def concat_to_root(cols: ColumnSet, n_local: int, infos: Sequence[A.ColumnInfo],
     meta = _meta(cols, n_local, infos, int(in_len or 0), dev)
     metas = [torch.empty_like(meta) for _ in range(world)]
     dist.all_gather(metas, meta, group=group)
-    plan = _Plan(torch.stack(metas).cpu().tolist(), kinds)
+    plan = _Plan(torch.stack(metas).cpu().tolist(), kinds, infos, cols)
     if rank != root:
         ops = [dist.P2POp(dist.isend, t.contiguous(), root, group) for t in plan.local_parts(cols, rank, n_local)
                if t.numel()]
@@ -283,7 +310,7 @@ def concat_local(shards, infos: Sequence[A.ColumnInfo]) -> ColumnSet:
     dev = _device_of(shards[0][0])
     metas = [_meta(cs, n, infos, int((rest[0] if rest else 0) or 0), dev).cpu().tolist()
              for cs, n, *rest in shards]
-    plan = _Plan(metas, kinds)
+    plan = _Plan(metas, kinds, infos, shards[0][0])
     plan.alloc(shards[0][0], dev)
     for r, (cs, n, *_) in enumerate(shards):
         for d, s_ in zip(plan.dest_parts(r), plan.local_parts(cs, r, n)):

@@ -260,7 +260,7 @@ def schema_r2_base():
     return idl.to_schema(idl.parse_idl(R2BASE_IDL, include_dirs=[d]).struct("R2Base"))
 
 
-def r2_base_record(oracle, rng, i):
+def r2_base_record(oracle, rng, i, repeat=False):
     P = oracle.prim
     fields = [(A.T_I64, f, i64(oracle, int(rng.integers(-2**63, 2**63 - 1)))) for f in range(1, 9)]
     fields += [(A.T_STRING, f, sbytes(oracle, bytes(rng.integers(97, 123, size=int(rng.integers(0, 40)),
@@ -280,13 +280,17 @@ def r2_base_record(oracle, rng, i):
     if i % 5 == 0:
         base = base[::-1]                     # some records off the canonical order: the walk path
     fields.append((A.T_STRUCT, 255, rec_bytes(oracle, base)))
+    if repeat and i % 3 == 1:
+        # 255:Base again without its Extra map: the struct is replaced wholesale (NewX() + FastRead,
+        # struct_tpl.go:79-101), so the first copy's Extra entries (var slots 7..10) must not survive
+        fields.append((A.T_STRUCT, 255, rec_bytes(oracle, [(A.T_STRING, 1, sbytes(oracle, b"again-%d" % i))])))
     return rec_bytes(oracle, fields)
 
 
-def case_r2_base(dec, oracle, mode, n=3000):
+def case_r2_base(dec, oracle, mode, n=3000, repeat=False):
     sch = schema_r2_base()
     rng = np.random.default_rng(8)
-    wire, offs = concat([r2_base_record(oracle, rng, i) for i in range(n)])
+    wire, offs = concat([r2_base_record(oracle, rng, i, repeat) for i in range(n)])
     check_decode(dec, oracle, sch, wire, n, offsets=offs if mode == "offsets" else None)
 
 

@@ -118,6 +118,28 @@ inline int __builtin_amdgcn_readfirstlane(int v) { return v; }
 // src and l are wave-uniform where the kernels use it
 inline int emu_writelane(int old, int src, int l) { return emu_lane() == (l & 63) ? src : old; }
 
+// DPP moves the kernels use: row_shr:1..15 (0x111..0x11f), row_bcast:15 (0x142), row_bcast:31 (0x143); a lane of
+// a row outside row_mask, or whose source lies outside its row, keeps `old` (bound_ctrl: 0)
+inline int __builtin_amdgcn_update_dpp(int old, int src, int ctrl, int row_mask, int bank_mask, bool bound_ctrl) {
+  (void)bank_mask;
+  uint64_t all[64];
+  emu_wave_xchg((uint32_t)src, all);
+  const int l = emu_lane(), row = l >> 4;
+  if (!((row_mask >> row) & 1)) return old;
+  int sl = -1;
+  if (ctrl >= 0x111 && ctrl <= 0x11f) {
+    const int d = ctrl - 0x110;
+    if ((l & 15) >= d) sl = l - d;
+  } else if (ctrl == 0x142) {
+    if (row >= 1) sl = (l & ~15) - 1;
+  } else if (ctrl == 0x143) {
+    if (row >= 2) sl = 31;
+  } else {
+    abort();
+  }
+  if (sl < 0) return bound_ctrl ? 0 : old;
+  return (int)(uint32_t)all[sl];
+}
 inline uint32_t __builtin_amdgcn_alignbyte(uint32_t hi, uint32_t lo, uint32_t s) {
   return (uint32_t)((((uint64_t)hi << 32) | lo) >> ((s & 3) * 8));
 }

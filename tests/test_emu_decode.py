@@ -115,6 +115,13 @@ def test_emu_r2_base_flat(edec, oracle, mode):
     DC.case_r2_base(edec, oracle, mode, n=1500)
 
 
+@pytest.mark.parametrize("mode", ["concat", "offsets"])
+def test_emu_r2_base_repeated_struct(edec, oracle, mode):
+    """a second 255:Base without Extra replaces the first wholesale: var slots 8..15 are reset too
+    (vslot_mask is 16 bits)"""
+    DC.case_r2_base(edec, oracle, mode, n=600, repeat=True)
+
+
 def _emu_split(sch, wire, n, parts, skip=False):
     rc, pts, st = emu.split_points(None if skip else sch, wire, n, parts)
     assert rc == 0

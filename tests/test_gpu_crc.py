@@ -94,15 +94,23 @@ def test_validate_reference_tamper_case(torch, oracle):
     assert np.array_equal(_u32(crc), ecrc)
 
 
-def test_decode_frames_with_crc32_check(torch, oracle):
+@pytest.mark.parametrize("form", ["fused", "separate_no_fo"])
+def test_decode_frames_with_crc32_check(torch, oracle, form, monkeypatch):
     """UnmarshalFrames(crc32_check=True): failing frames carry ERR_PAYLOAD_VALIDATION, every other
-    message decodes exactly as the oracle decodes its record; without the check all decode"""
+    message decodes exactly as the oracle decodes its record; without the check all decode.
+    separate_no_fo: the separate checksum kernel (KX_CRC_FUSED=0) with frame_offsets NULL, so the frame
+    offsets live in the library's scratch next to the CRC status (the status used to overlap
+    them); the first failing frame is frame 5"""
     from kitex_amd.codec import ThriftCodec
     n = 6000
     sch, recs, frames, wire, fo, exp = CC.crc_batch(n, CC.MODES_PASS + CC.MODES_FAIL)
+    assert int(np.nonzero(exp)[0][0]) < 8
+    if form == "separate_no_fo":
+        monkeypatch.setenv("KX_CRC_FUSED", "0")
     cdc = ThriftCodec(sch)
     buf = torch.from_numpy(wire).to("cuda:0")
-    res = cdc.UnmarshalFrames(buf, n, raise_on_error=False, crc32_check=True)
+    res = cdc.UnmarshalFrames(buf, n, raise_on_error=False, crc32_check=True,
+                              frame_offsets=form == "fused")
     st = res.read_status()
     rs = to_np(res.record_status)[:n]
     assert np.array_equal(rs, exp)

@@ -131,3 +131,18 @@ def test_pb_golden_fixture_on_gpu(torch, oracle):
     assert st.code == 0 and st.n_records == 64 and st.consumed == golden.size
     _, infos, _ = oracle.flatten(sch)
     assert_columns_equal(res.columns, synth.gen_pf(64), infos, 64)
+
+
+def test_pb_split_points_refused(torch):
+    """SplitPoints on a flat Kitex-Protobuf codec: NOT_IMPLEMENTED, never a Thrift walk over protobuf Batch
+    bytes (a nested proto3 schema is refused by kx_thrift_split_points itself)"""
+    from kitex_amd.codec import ProtobufCodec
+    sch = S.schema_pf()
+    cdc = ProtobufCodec(sch)
+    assert not cdc.dschema.nested
+    buf = torch.zeros(64, dtype=torch.uint8, device="cuda:0")
+    from kitex_amd import _abi as A
+    from kitex_amd._lib import KxError
+    with pytest.raises(KxError) as ei:
+        cdc.SplitPoints(buf, 4, 2)
+    assert ei.value.code == A.ERR_NOT_IMPLEMENTED

@@ -207,6 +207,13 @@ def test_r2_base_flat_path(torch, dev, oracle, mode):
     DC.case_r2_base(GpuDecoder(torch, dev), oracle, mode, n=20000)
 
 
+@pytest.mark.parametrize("mode", ["concat", "offsets"])
+def test_r2_base_repeated_struct(torch, dev, oracle, mode):
+    """a repeated 255:Base whose second copy omits Extra: the struct is replaced wholesale, so the
+    first copy's Extra (var slots past 8) is dropped, as the oracle does"""
+    DC.case_r2_base(GpuDecoder(torch, dev), oracle, mode, n=20000, repeat=True)
+
+
 def _gpu_split(torch, dev):
     from kitex_amd.codec import ThriftCodec, read_status, status_tensor
     from kitex_amd._lib import lib
@@ -446,6 +453,35 @@ def test_host_decode_chunked_pipeline(torch, oracle, name):
         out, st = cdc.UnmarshalHost(bad, n, offsets=offs, raise_on_error=False)
         _, _, est, _ = oracle.decode(sch, bad, n, offsets=offs)
         assert (st.code, st.record, st.offset) == (est.code, est.record, est.offset) and st.record == k
+
+
+@pytest.mark.parametrize("n", [20_000, 100_000])
+@pytest.mark.parametrize("name", ["r2", "r3", "pf", "cx1", "cx2"])
+def test_host_encode_bit_exact(torch, oracle, name, n):
+    """kx_host_encode_batch / kx_host_pb_encode_batch (fastMarshal from host columns to host wire, the
+    16-chunk pipeline at 100 000 records with each chunk's output placed by the previous chunk's device
+    status): bytes and record offsets identical to the oracle's encoder"""
+    from kitex_amd.codec import ProtobufCodec, ThriftCodec
+    if name in DC.CONTAINER_SCHEMAS:   # list<string>, set<string>, maps: LIST_BYTES columns
+        mk, gen = DC.CONTAINER_SCHEMAS[name]
+        sch, cs = mk(), gen(n, start=23)
+    else:
+        sch, cs = S.SCHEMAS[name](), synth.GENERATORS[name](n, start=23)
+    pb = name == "pf"
+    cdc = ProtobufCodec(sch) if pb else ThriftCodec(sch)
+    rc, exp, eoffs = oracle.encode(sch, cs, pb=pb)
+    assert rc == 0
+    wire, offs, st = cdc.MarshalHost(cs)
+    assert st.code == 0 and st.consumed == exp.size
+    assert np.array_equal(wire, exp)
+    if pb:   # kx_pb_encode_batch's offsets are the Batch frame starts (the oracle's: the bodies)
+        from tests import pb_cases as PC
+        _, eoffs = PC.join(PC.split_frames(exp), framed=True)
+    assert np.array_equal(offs.astype(np.uint64), eoffs.astype(np.uint64))
+    # too small an output: SIZE_LIMIT, reported, never a partial overrun
+    small = np.zeros(exp.size // 2, dtype=np.uint8)
+    _, _, st2 = cdc.MarshalHost(cs, out=small, raise_on_error=False)
+    assert st2.code == A.ERR_SIZE_LIMIT
 
 
 @pytest.mark.parametrize("name", ["cx1", "cx2"])

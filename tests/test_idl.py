@@ -177,3 +177,42 @@ def test_reference_fixture_methods_compile_and_decode(oracle, f):
         rc, back, bst, _ = oracle.decode(sch, wire2, n)
         assert bst.code == 0
         assert_columns_equal(back, exp, infos, n)
+
+
+def test_enum_and_typedef_write_order_pinned(oracle):
+    """Parity-unpinned choice, pinned here so it cannot drift: an enum field (i32 on the wire,
+    kitex_amd/idl.py) and a typedef of a scalar count as fixed-length in the encoder's reorder
+    (reorderStructFields, patcher.go:503-522), so both are written before the string. Whether thriftgo's
+    golang.IsFixedLengthType counts Category_Enum is not visible in the reference (un-vendored thriftgo), and
+    no generated struct in the reference has an enum field."""
+    doc = idl.parse_idl("""
+        enum Color { RED = 1, BLUE = 7 }
+        typedef i64 Stamp
+        struct ES { 1: string name; 2: Color color; 3: Stamp at; 4: list<i32> xs; 5: bool ok }
+    """)
+    sch = idl.to_schema(doc.struct("ES"))
+    from tests.helpers import random_columns
+    rc, infos, npres = oracle.flatten(sch)
+    assert rc == 0
+    cs = random_columns(infos, npres, 3, seed=5)
+    rc, wire, offs = oracle.encode(sch, cs)
+    assert rc == 0
+    rec = bytes(wire[int(offs[0]):int(offs[1])])
+    order, p = [], 0
+    while rec[p] != A.T_STOP:
+        t, fid = rec[p], int.from_bytes(rec[p + 1:p + 3], "big")
+        order.append((fid, t))
+        p += 3
+        if t in (A.T_I32,):
+            p += 4
+        elif t in (A.T_I64,):
+            p += 8
+        elif t == A.T_BOOL:
+            p += 1
+        elif t == A.T_STRING:
+            p += 4 + int.from_bytes(rec[p:p + 4], "big")
+        elif t == A.T_LIST:
+            p += 5 + 4 * int.from_bytes(rec[p + 1:p + 5], "big")
+        else:
+            raise AssertionError(t)
+    assert order == [(2, A.T_I32), (3, A.T_I64), (5, A.T_BOOL), (1, A.T_STRING), (4, A.T_LIST)]
