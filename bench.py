@@ -593,6 +593,7 @@ def extras(args, r2, dev, local):
             recs = synth.thrift_records(sch, k, seed=7)
             cpu_recs = recs
         ds = cdc.dschema
+        note(f"  nested {'pb' if pb else 'thrift'}: {k} records generated")
         one = np.frombuffer(b"".join(recs), dtype=np.uint8).copy()
         wire = torch.from_numpy(one).to(dev).repeat(n // k)
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
@@ -608,6 +609,7 @@ def extras(args, r2, dev, local):
         def dec():
             cdc.Unmarshal(wire, n, out=outc, var_caps=vc, raise_on_error=False, status=st)
         t, per = time_steps(dec, steps, warm, 1, dev)
+        note(f"  nested decode timed: {t / steps * 1e3:.2f} ms")
         s = read_status(st)
         ok = s.code == 0 and s.n_records == n and s.consumed == wire.numel()
 
@@ -636,8 +638,10 @@ def extras(args, r2, dev, local):
         res["encode"] = {"records_per_s": n * steps / t, "ms_per_step": t / steps * 1e3,
                          "round_trip_equal": eq and bool(torch.equal(buf, w2)),
                          "roofline": roofline(out_bytes + buf.numel(), avg, "nested encode (size + write)")}
+        note("  nested encode timed; cpu baseline")
         if not args.no_cpu:
             cb = nested_cpu_baseline(sch, cpu_recs, n, pb)
+            note("  nested cpu baseline done")
             if cb.get("value"):
                 cb["gpu_speedup"] = res["decode"]["records_per_s"] / cb["value"]
             res["cpu_baseline"] = cb

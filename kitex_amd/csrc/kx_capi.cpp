@@ -1273,11 +1273,14 @@ static int host_decode(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_
     int e = decode_device(c, s, d_in, in_len, d_off + r0, nk, &ck, d_st + k, st, pb, nullptr,
                           k ? d_st[k - 1].var_total : nullptr);
     if (e) return e;
-    KX_HIP_CHECK(hipEventRecord(c->hev_run[k], st));
-    // behind the decode on the copy-out stream: the status (pinned), then the fixed columns / offsets
-    KX_HIP_CHECK(hipStreamWaitEvent(sd, c->hev_run[k], 0));
-    KX_HIP_CHECK(hipMemcpyAsync(&c->hst[k], d_st + k, sizeof(kx_status), hipMemcpyDeviceToHost, sd));
-    KX_HIP_CHECK(hipEventRecord(c->hev_st[k], sd));
+    // the status (pinned) right behind the decode, on the decode stream: nothing is queued on the copy-out
+    // stream before it can run (streams share hardware queues: a queued wait would hold back what follows)
+    KX_HIP_CHECK(hipMemcpyAsync(&c->hst[k], d_st + k, sizeof(kx_status), hipMemcpyDeviceToHost, st));
+    KX_HIP_CHECK(hipEventRecord(c->hev_st[k], st));
+    return KX_OK;
+  };
+  auto copy_out = [&](uint32_t k) -> int {   // chunk k has been decoded: its fixed columns, offsets, presence
+    const uint64_t r0 = r[k], nk = r[k + 1] - r[k];
     for (uint32_t j = 0; j < s->ncols; j++) {
       const kx_column_info& ci = s->info[j];
       if (ci.kind == KX_COL_FIXED) {
@@ -1305,6 +1308,7 @@ static int host_decode(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_
     if (!serial && k + 1 < K && (rc = launch_chunk(k + 1))) return rc;   // queued before chunk k's status is read
     KX_HIP_CHECK(hipEventSynchronize(c->hev_st[k]));
     if (serial && k + 1 < K && (rc = launch_chunk(k + 1))) return rc;
+    if ((rc = copy_out(k))) return rc;
     const kx_status sk = c->hst[k];
     if (sk.code && !failed) {
       failed = true;
@@ -1484,13 +1488,9 @@ static int host_encode(kx_ctx* c, const kx_schema* s, const kx_columns* in, uint
     if ((e = kx_launch_encode(dprog, s->prog, lc, nk, d_out, out_cap, nullptr, d_offs + r0, d_st + k, c->ews,
                               c->ews_size, st, false, pb, k ? &d_st[k - 1].consumed : nullptr)))
       return e;
-    KX_HIP_CHECK(hipEventRecord(c->hev_run[k], st));
-    KX_HIP_CHECK(hipStreamWaitEvent(sd, c->hev_run[k], 0));
-    KX_HIP_CHECK(hipMemcpyAsync(&c->hst[k], d_st + k, sizeof(kx_status), hipMemcpyDeviceToHost, sd));
-    KX_HIP_CHECK(hipEventRecord(c->hev_st[k], sd));
-    if (offsets_out)
-      KX_HIP_CHECK(hipMemcpyAsync(offsets_out + r0, d_offs + r0, (nk + (k == K - 1 ? 1 : 0)) * 8,
-                                  hipMemcpyDeviceToHost, sd));
+    // the status (pinned) right behind the encode on its stream (see host_decode)
+    KX_HIP_CHECK(hipMemcpyAsync(&c->hst[k], d_st + k, sizeof(kx_status), hipMemcpyDeviceToHost, st));
+    KX_HIP_CHECK(hipEventRecord(c->hev_st[k], st));
     return KX_OK;
   };
   if ((rc = launch_chunk(0))) return rc;
@@ -1501,6 +1501,11 @@ static int host_encode(kx_ctx* c, const kx_schema* s, const kx_columns* in, uint
     if (k + 1 < K && (rc = launch_chunk(k + 1))) return rc;   // queued before chunk k's size is known
     KX_HIP_CHECK(hipEventSynchronize(c->hev_st[k]));
     const kx_status sk = c->hst[k];
+    if (offsets_out) {
+      const uint64_t r0 = r[k], nk = r[k + 1] - r[k];
+      KX_HIP_CHECK(hipMemcpyAsync(offsets_out + r0, d_offs + r0, (nk + (k == K - 1 ? 1 : 0)) * 8,
+                                  hipMemcpyDeviceToHost, sd));
+    }
     if (sk.code && !failed) {
       failed = true;
       first = sk;

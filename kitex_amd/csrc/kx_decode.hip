@@ -1198,6 +1198,55 @@ __device__ __forceinline__ uint64_t shfl64(uint64_t v, int l) {
   return ((uint64_t)hi << 32) | lo;
 }
 
+// ---- long strings: copied by the whole wave (bimodal record sizes) ----
+// A string of KX_WAVE_COPY bytes or more costs one lane n/16 dependent 16-byte round trips; a batch with 1 %
+// of its records at 64 KiB spent 11x the canonical time per byte in them. Lanes holding one defer it, and
+// the wave copies the deferred strings one after another, lane k taking 16-byte pieces k, k + 64, ... of
+// the 16-byte-aligned destination body (four pieces in flight per lane). For strings of this size the wave
+// form never needs more rounds than the lanes would (n/1024 per string, 64 strings: n/16).
+#define KX_WAVE_COPY 1024u
+__device__ __forceinline__ void wave_copy_one(const Src& w, uint64_t src, uint32_t n, GLB uint8_t* dst,
+                                              int lane, bool inwin) {
+  const uint32_t h = min((uint32_t)((16u - ((uint32_t)(uintptr_t)dst & 15u)) & 15u), n);
+  const bool body_ok = inwin || src + n + 20 <= w.len;   // ld16's global form reads 4 bytes past the piece
+  if (!body_ok) {
+    for (uint32_t i = lane; i < n; i += 64) dst[i] = (uint8_t)ld1(w, src + i);
+    return;
+  }
+  if ((uint32_t)lane < h) dst[lane] = (uint8_t)ld1(w, src + lane);
+  const uint32_t nb = (n - h) & ~15u;
+  GLB uint8_t* d = dst + h;
+  const uint64_t s = src + h;
+  uint32_t i = (uint32_t)lane * 16u;
+  for (; i + 3 * 1024 + 16 <= nb; i += 4 * 1024) {
+    const Q16 a = ld16(w, s + i, inwin), b = ld16(w, s + i + 1024, inwin);
+    const Q16 c = ld16(w, s + i + 2048, inwin), e = ld16(w, s + i + 3072, inwin);
+    *(GLB v4u*)(d + i) = v4u{a.a0, a.a1, a.a2, a.a3};
+    *(GLB v4u*)(d + i + 1024) = v4u{b.a0, b.a1, b.a2, b.a3};
+    *(GLB v4u*)(d + i + 2048) = v4u{c.a0, c.a1, c.a2, c.a3};
+    *(GLB v4u*)(d + i + 3072) = v4u{e.a0, e.a1, e.a2, e.a3};
+  }
+  for (; i < nb; i += 1024) {
+    const Q16 a = ld16(w, s + i, inwin);
+    *(GLB v4u*)(d + i) = v4u{a.a0, a.a1, a.a2, a.a3};
+  }
+  const uint32_t tl = n - h - nb;   // < 16
+  if ((uint32_t)lane < tl) d[nb + lane] = (uint8_t)ld1(w, s + nb + lane);
+}
+// every lane with big set hands its string (src, n -> dst) to the wave; uniform control flow
+__device__ __forceinline__ void wave_copy_deferred(const Src& w, bool big, uint64_t src, uint32_t n, uint8_t* dst,
+                                                   int lane, bool inwin) {
+  uint64_t m = __ballot(big);
+  while (m) {
+    const int l = __builtin_ctzll(m);
+    m &= m - 1;
+    const uint64_t s = rl64(src, l);
+    const uint32_t nn = __builtin_amdgcn_readlane(n, l);
+    GLB uint8_t* d = (GLB uint8_t*)rl64((uint64_t)(uintptr_t)dst, l);
+    wave_copy_one(w, s, nn, d, lane, inwin);
+  }
+}
+
 // emit: numeric list columns copied by the whole wave, one element per lane (1), or record by record (0)
 #ifndef KX_EMIT_COOP
 #define KX_EMIT_COOP 1
@@ -3525,8 +3574,8 @@ __device__ __forceinline__ void emit_tile(KParams& dp, LDS uint32_t* win, uint64
             if ((uint32_t)u == K.vslot2) { B = atv[u]; nb = vs.len[u]; }
           emit_container<MODE == M_THRIFT_LS>(w, P, dp.cols, cc, K, vs.pos[v], vs.len[v], at, B, nb, r, dp.overflow);
         }
-      } else if (act && ((dp.cols.view >> cc) & 1)) {
-        put_view(dp.cols, cc, r, vs.pos[v], vs.len[v]);
+      } else if ((dp.cols.view >> cc) & 1) {
+        if (act) put_view(dp.cols, cc, r, vs.pos[v], vs.len[v]);
       } else if (COOP && K.kind == KXP_K_LIST && K.width > 1 && !((dp.cols.view >> cc) & 1)) {
         // wave-cooperative list copy: the wave's elements are one contiguous arena run [at0, at0 + T);
         // lane e copies element e of it, finding its record by a binary search over the lanes' starts
@@ -3564,19 +3613,25 @@ __device__ __forceinline__ void emit_tile(KParams& dp, LDS uint32_t* win, uint64
             }
           }
         }
-      } else if (act) {
-        const uint32_t nn = vs.len[v];
-        if (at + nn <= arena_lim(dp.cols, cc)) {
-          put_off(dp.cols, cc, r, at);
+      } else {
+        const uint32_t nn = act ? vs.len[v] : 0u;
+        uint8_t* dst = (uint8_t*)dp.cols.data[cc] + at * K.width;
+        bool big = false;
+        if (act) {
+          if (at + nn <= arena_lim(dp.cols, cc)) {
+            put_off(dp.cols, cc, r, at);
+            big = K.kind == KXP_K_BYTES && nn >= KX_WAVE_COPY;
 #if KX_EXP_EMIT & 2   // timing experiment: no payload copy
-          if (nn == 0x7fffffff)
+            if (nn == 0x7fffffff)
 #else
-          if (nn)
+            if (nn && !big)
 #endif
-            copy_var(w, K, vs.pos[v], nn, (uint8_t*)dp.cols.data[cc] + at * K.width);
-        } else {
-          atomicOr(dp.overflow, 1u);
+              copy_var(w, K, vs.pos[v], nn, dst);
+          } else {
+            atomicOr(dp.overflow, 1u);
+          }
         }
+        wave_copy_deferred(w, big, vs.pos[v], nn, dst, lane, false);
       }
     }
     if (act && r == nstop - 1 && nstop == dp.n) {
@@ -3794,15 +3849,21 @@ __device__ __forceinline__ void emit_fast_tile(KParams& dp, const Src& w, uint64
       atv[v] = at;
       run[v] += (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
       const uint32_t cc = P->var_col[v];
-      if (act) {
-        if ((dp.cols.view >> cc) & 1) {
-          put_view(dp.cols, cc, r, w.wpos + vp[v], vl[v]);
-        } else if (at + vl[v] <= arena_lim(dp.cols, cc)) {
-          put_off(dp.cols, cc, r, at);
-          if (vl[v]) copy_str_win(w, vp[v], vl[v], (uint8_t*)dp.cols.data[cc] + at);
-        } else {
-          atomicOr(dp.overflow, 1u);
+      if ((dp.cols.view >> cc) & 1) {
+        if (act) put_view(dp.cols, cc, r, w.wpos + vp[v], vl[v]);
+      } else {
+        uint8_t* dst = (uint8_t*)dp.cols.data[cc] + at;
+        bool big = false;
+        if (act) {
+          if (at + vl[v] <= arena_lim(dp.cols, cc)) {
+            put_off(dp.cols, cc, r, at);
+            big = vl[v] >= KX_WAVE_COPY;
+            if (vl[v] && !big) copy_str_win(w, vp[v], vl[v], dst);
+          } else {
+            atomicOr(dp.overflow, 1u);
+          }
         }
+        wave_copy_deferred(w, big, w.wpos + vp[v], act ? vl[v] : 0u, dst, lane, true);
       }
     }
     if (act && r == nstop - 1 && nstop == dp.n) {   // the batch's last record closes the var columns

@@ -167,6 +167,27 @@ def case_slot_overflow(dec, oracle):
     check_decode(dec, oracle, sch, wire, len(recs), offsets=offs)
 
 
+def case_long_strings(dec, oracle, n=400, seed=3):
+    """strings at and past the wave-copy threshold (1024 B, kx_decode.hip wave_copy_one) among short ones,
+    random bytes at every destination alignment: the ones inside a tile's window (the fast emit form copies
+    from LDS) and the ones that leave it (the general form copies from global memory)"""
+    rng = np.random.default_rng(seed)
+    sch = S.Schema(S.Struct("L", [S.Field(1, A.T_I64), S.Field(2, A.T_STRING), S.Field(3, A.T_STRING, binary=True)]))
+    kinds = rng.integers(0, 6, size=n)
+    recs = []
+    for i in range(n):
+        k = kinds[i]
+        ln = [int(rng.integers(0, 40)), 1023, 1024, int(rng.integers(1025, 3000)),
+              int(rng.integers(3000, 40000)), int(rng.integers(0, 8))][k]
+        s = rng.integers(0, 256, size=ln, dtype=np.uint8).tobytes()
+        b = rng.integers(0, 256, size=int(rng.integers(0, 1200 if i % 7 == 0 else 20)), dtype=np.uint8).tobytes()
+        recs.append(rec_bytes(oracle, [(A.T_I64, 1, i64(oracle, i * 7919)), (A.T_STRING, 2, sbytes(oracle, s)),
+                                       (A.T_STRING, 3, sbytes(oracle, b))]))
+    wire, offs = concat(recs)
+    check_decode(dec, oracle, sch, wire, n)
+    check_decode(dec, oracle, sch, wire, n, offsets=offs)
+
+
 def case_nested(dec, oracle):
     inner = S.Struct("In", [S.Field(1, A.T_I64, req=A.REQ_REQUIRED), S.Field(2, A.T_STRING, req=A.REQ_OPTIONAL),
                             S.Field(3, A.T_I16, default=9)])

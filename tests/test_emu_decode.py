@@ -261,3 +261,8 @@ def test_emu_fast_index_path_taken(edec, oracle, name, n):
 @pytest.mark.parametrize("case", DC.GATHER_CASES)
 def test_emu_offsets_length_gather(edec, oracle, case):
     DC.case_offsets_gather(edec, oracle, case)
+
+
+def test_emu_long_strings(edec, oracle):
+    """strings past the wave-copy threshold, inside and outside the tile window"""
+    DC.case_long_strings(edec, oracle)

@@ -110,6 +110,12 @@ def test_slot_overflow(gdec, oracle):
     DC.case_slot_overflow(gdec, oracle)
 
 
+@pytest.mark.parametrize("seed", [3, 4])
+def test_long_strings(gdec, oracle, seed):
+    """strings at and past the wave-copy threshold, inside and outside the tile window"""
+    DC.case_long_strings(gdec, oracle, n=3000, seed=seed)
+
+
 @pytest.mark.parametrize("name", ["r2", "r3", "cx1"])
 def test_slotcap_64(gdec, oracle, name, monkeypatch):
     """64 record-start slots per tile (KX_SLOTCAP): records past them are emitted from the chain"""
