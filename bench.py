@@ -626,19 +626,23 @@ def extras(args, r2, dev, local):
                           "sizes_pass_ms": sizes_ms,
                           "roofline": roofline(wire.numel() + out_bytes, avg, "nested decode (measure + write)")}}
         w2, _ = cdc.Marshal(outc)
+        note("  nested encode: first Marshal done")
         buf = torch.empty_like(w2)
         st2 = status_tensor(dev)
 
         def enc():
             cdc.Marshal(outc, with_offsets=False, out=buf, status=st2, check_status=False)
         t, per = time_steps(enc, steps, warm, 1, dev)
+        note(f"  nested encode timed: {t / steps * 1e3:.2f} ms")
         avg = sum(per) / len(per) / 1e3
         back = cdc.Unmarshal(buf, n, raise_on_error=False)
+        torch.cuda.synchronize()
+        note("  nested encode: round-trip decode done")
         eq = all(bool(torch.equal(a, b)) for a, b in zip(tensors(outc), tensors(back.columns)))
         res["encode"] = {"records_per_s": n * steps / t, "ms_per_step": t / steps * 1e3,
                          "round_trip_equal": eq and bool(torch.equal(buf, w2)),
                          "roofline": roofline(out_bytes + buf.numel(), avg, "nested encode (size + write)")}
-        note("  nested encode timed; cpu baseline")
+        note("  nested round trip compared; cpu baseline")
         if not args.no_cpu:
             cb = nested_cpu_baseline(sch, cpu_recs, n, pb)
             note("  nested cpu baseline done")

@@ -2242,6 +2242,32 @@ __device__ __forceinline__ bool fast_record_fp(KParams& dp, const Src& w, uint32
   return ok;
 }
 
+// After fast_record failed on the record at window offset q: did it fail only because the record runs on
+// past the window (every header up to there matches the plan)? A canonical record longer than the window
+// (a 64 KiB string) is then a record start the fast path cannot walk, not a false signature hit: its tile
+// takes the general walk instead of reading as one with no record start (such a tile
+// used to send its whole group to the chain pass's repair). Off the hot path: failing lanes only.
+__device__ __noinline__ bool record_leaves_window(const Src& w, uint32_t q) {
+  const KAS KxpStep* __restrict__ steps = w.steps;
+  const uint32_t wl = (uint32_t)w.wlen;
+  for (uint32_t k = 0; k < w.nsteps; k++) {
+    const KxpStep st = ldk(&steps[k]);
+    if (q + 64 > wl) return true;
+    const uint32_t h = win_ld(w, q);
+    if (st.kind == KXP_S_END) return false;
+    if ((h ^ st.hdr) & 0xffffffu) return false;
+    if (st.kind == KXP_S_FIXED) { q += 3 + st.width; continue; }
+    if (st.kind == KXP_S_STRUCT) { q += 3; continue; }
+    const bool list = st.kind == KXP_S_LIST;
+    const uint32_t l = __builtin_bswap32(win_ld(w, q + (list ? 4u : 3u)));
+    if (l > 0x7fffffffu) return false;
+    const uint64_t b = (uint64_t)l * (list ? st.width : 1u);
+    if ((uint64_t)q + (list ? 8u : 7u) + b + 64 > wl) return true;
+    q += (list ? 8u : 7u) + (uint32_t)b;
+  }
+  return false;
+}
+
 // one canonical record at window offset q (measure: headers, lengths, STOP); var lengths added to vl
 template <int NV>
 __device__ __forceinline__ bool fast_record(KParams& dp, const Src& w, uint32_t& q, uint64_t* vl) {
@@ -2379,7 +2405,7 @@ __device__ __forceinline__ bool fast_tile(KParams& dp, const Src& w, uint64_t tl
   uint64_t vsum[NV > 0 ? NV : 1];
 #pragma unroll
   for (int v = 0; v < (NV > 0 ? NV : 1); v++) vsum[v] = 0;
-  bool bad = false;
+  bool bad = false, wf = false;   // wf: a walk met a record that runs on past the window
   for (int attempt = 0; attempt < 3; attempt++) {
     bool again = false;
     if (ent != X_NONE) {
@@ -2392,7 +2418,10 @@ __device__ __forceinline__ bool fast_tile(KParams& dp, const Src& w, uint64_t tl
       while (ok && w.wpos + q < seg_hi) {
         const uint64_t start = w.wpos + q;
         ok = fast_record<NV>(dp, w, q, acc);
-        if (!ok) break;
+        if (!ok) {
+          wf |= record_leaves_window(w, (uint32_t)(start - w.wpos));
+          break;
+        }
         st0 = c == 0 ? start : st0; st1 = c == 1 ? start : st1;
         st2 = c == 2 ? start : st2; st3 = c == 3 ? start : st3;
         c++;
@@ -2416,7 +2445,7 @@ __device__ __forceinline__ bool fast_tile(KParams& dp, const Src& w, uint64_t tl
   }
   phase(3);
   if (dp.diag & 4096) { stop_here(ex ^ cnt ^ st0 ^ st1 ^ vsum[0]); return true; }
-  if (__ballot(bad)) return false;
+  if (__ballot(bad || wf)) return false;
   // ---- consistency: every walking lane starts where the chain of the walking lane below it exits ----
   const uint64_t hmk = __ballot(ent != X_NONE);
   const uint64_t below = hmk & ((1ull << lane) - 1);
@@ -3531,6 +3560,10 @@ __device__ __forceinline__ void emit_tile(KParams& dp, LDS uint32_t* win, uint64
       if (canon) {
         end = emit_canon<NV>(w, dp.cols, pos, r, vs);
         pres = w.canon_pres;
+      } else if (MODE == M_SKIP && !known && !past && r != nstop - 1 && !(j + 1 == dp.slotcap && cnt > dp.slotcap)) {
+        // the skip decoder's boundaries: the index pass walked every record before nstop and left its start
+        // in the slots, which is all this pass writes (the end is read only where the chain goes on from it:
+        // the last slotted record of a tile with more, and the batch's last record)
       } else if (!rc) {
         rc = parse_record<NV, MODE>(dp, w, pos, lim, r, MODE != M_SKIP, &end, vs, pres);
       }

@@ -179,6 +179,23 @@ KXN_HD uint32_t kxn_be32(B p) {
 }
 template <class B>
 KXN_HD uint64_t kxn_be64(B p) { return ((uint64_t)kxn_be32(p) << 32) | kxn_be32(p + 4); }
+// the input itself: one unaligned load per value (global_load_dword / dwordx2 at any byte address on the
+// device) instead of a load per byte, which left every lane's walk a chain of byte round trips
+KXN_HD uint32_t kxn_be16(const uint8_t* p) {
+  uint16_t x;
+  __builtin_memcpy(&x, p, 2);
+  return (uint32_t)(uint16_t)((x << 8) | (x >> 8));
+}
+KXN_HD uint32_t kxn_be32(const uint8_t* p) {
+  uint32_t x;
+  __builtin_memcpy(&x, p, 4);
+  return __builtin_bswap32(x);
+}
+KXN_HD uint64_t kxn_be64(const uint8_t* p) {
+  uint64_t x;
+  __builtin_memcpy(&x, p, 8);
+  return __builtin_bswap64(x);
+}
 
 KXN_HD int kxn_tsize(uint32_t t) {
   switch (t) {
@@ -375,6 +392,16 @@ KXN_HD void kxn_copy(uint8_t* dst_, S src, uint64_t m) {
   }
   for (; j < m; j++) dst[j] = kxn_ld8(src, j);
 }
+// from the input: 16-byte unaligned loads and stores
+KXN_HD void kxn_copy(uint8_t* dst, const uint8_t* src, uint64_t m) {
+  uint64_t j = 0;
+  for (; j + 16 <= m; j += 16) {
+    uint64_t t[2];
+    __builtin_memcpy(t, src + j, 16);
+    __builtin_memcpy(dst + j, t, 16);
+  }
+  for (; j < m; j++) ((KXN_G(uint8_t)*)dst)[j] = ((const KXN_G(uint8_t)*)src)[j];
+}
 
 // ---------------------------------------------------------------------------------------------
 // decode walker
@@ -530,7 +557,10 @@ KXN_HD int kxn_read_record(const KxnProgram& P, const KxnCols& C, B b, uint64_t 
     if (F.kind == KN_STRUCT) {
       const KxnStruct& T = P.st[F.id];
       if (q + 1 > len) { rc = KX_ERR_EOF; break; }             // ReadFieldBegin
-      const uint32_t t = b[q];
+      // type and id in one load where 4 bytes remain (all but a record's final STOP)
+      const bool h4 = q + 4 <= len;
+      const uint32_t hw = h4 ? kxn_be32(b + q) : 0u;
+      const uint32_t t = h4 ? hw >> 24 : (uint32_t)b[q];
       const int L = T.level;
       if (t == KX_T_STOP) {
         q += 1;
@@ -539,7 +569,7 @@ KXN_HD int kxn_read_record(const KxnProgram& P, const KxnCols& C, B b, uint64_t 
         continue;
       }
       if (q + 3 > len) { rc = KX_ERR_EOF; break; }
-      const int16_t id = (int16_t)kxn_be16(b + q + 1);
+      const int16_t id = h4 ? (int16_t)(uint16_t)(hw >> 8) : (int16_t)kxn_be16(b + q + 1);
       q += 3;
       int fi = -1;
       for (int k = 0; k < T.nfields; k++)

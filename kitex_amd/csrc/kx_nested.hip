@@ -195,43 +195,38 @@ __global__ void check_kernel(NParams p) {
   if (over) *p.flag = 1u;
 }
 
-// one block of RB records, lane = record
-template <int T>
-__device__ __forceinline__ void write_block(const NParams& p, uint64_t* carry, uint64_t* cur, uint64_t* lim,
-                                            uint64_t* snap, uint64_t* sh) {
+// record r (of block b), lane = record
+__device__ __forceinline__ void write_record(const NParams& p, uint64_t b, uint64_t r, uint64_t* cur, uint64_t* lim,
+                                             uint64_t* snap) {
   const KxnProgram& P = *p.P;
-  const uint64_t b = blockIdx.x;
-  (void)carry;
-  (void)sh;
   const uint64_t rb1 = kmin64((b + 1) * RB, p.n);   // the block's end
-  for (int j = 0; j < RB / T; j++) {
-    const uint64_t r = b * RB + (uint64_t)j * T + threadIdx.x;
-    if (r >= p.n) continue;
-    // the record's cursor bases: the block base + the in-block prefix (bsum_kernel); its extent ends
-    // at the next record's prefix, or at the next block's base
-    for (uint32_t k = 0; k < p.ncur; k++) {
-      const uint64_t base = p.bsum[(uint64_t)k * p.nblk + b];
-      const uint32_t* c = p.counts + (uint64_t)k * p.n;
-      cur[k] = base + c[r];
-      lim[k] = r + 1 < rb1 ? base + c[r + 1] : (b + 1 < p.nblk ? p.bsum[(uint64_t)k * p.nblk + b + 1] : p.totals[k]);
-    }
-    const uint8_t rc = p.rcode[r];
-    uint64_t a = 0, e = 0, used = 0;
-    if (rc == 0 && extent(p, r, &a, &e) == 0) {
-      if (P.pb) (void)kxn_pb_read_record<true>(P, *p.C, p.in + a, e - a, r, cur, snap, &used, lim);
-      else (void)kxn_read_record<true>(P, *p.C, p.in + a, e - a, r, cur, snap, &used, lim);
-    } else {
-      kxn_failed_record(P, *p.C, r, cur);
-    }
-    if (p.record_status && !p.concat) p.record_status[r] = rc == 0xff ? 0 : rc;
+  // the record's cursor bases: the block base + the in-block prefix (bsum_kernel); its extent ends at the
+  // next record's prefix, or at the next block's base
+  for (uint32_t k = 0; k < p.ncur; k++) {
+    const uint64_t base = p.bsum[(uint64_t)k * p.nblk + b];
+    const uint32_t* c = p.counts + (uint64_t)k * p.n;
+    cur[k] = base + c[r];
+    lim[k] = r + 1 < rb1 ? base + c[r + 1] : (b + 1 < p.nblk ? p.bsum[(uint64_t)k * p.nblk + b + 1] : p.totals[k]);
   }
+  const uint8_t rc = p.rcode[r];
+  uint64_t a = 0, e = 0, used = 0;
+  if (rc == 0 && extent(p, r, &a, &e) == 0) {
+    if (P.pb) (void)kxn_pb_read_record<true>(P, *p.C, p.in + a, e - a, r, cur, snap, &used, lim);
+    else (void)kxn_read_record<true>(P, *p.C, p.in + a, e - a, r, cur, snap, &used, lim);
+  } else {
+    kxn_failed_record(P, *p.C, r, cur);
+  }
+  if (p.record_status && !p.concat) p.record_status[r] = rc == 0xff ? 0 : rc;
 }
 
+// one record per thread: workgroup w holds records [w·NT, (w + 1)·NT) of block w / (RB / NT) (a workgroup
+// per block looping over its 4 quarters left 4 waves per SIMD: DESIGN §3.10)
 __global__ void __launch_bounds__(NT) write_kernel(NParams p) {
-  __shared__ uint64_t sh[NT / 64];
   if (*p.flag) return;
-  uint64_t carry[CUR], cur[CUR], lim[CUR], snap[SNAP];
-  write_block<NT>(p, carry, cur, lim, snap, sh);
+  const uint64_t r = (uint64_t)blockIdx.x * NT + threadIdx.x;
+  if (r >= p.n) return;
+  uint64_t cur[CUR], lim[CUR], snap[SNAP];
+  write_record(p, blockIdx.x / (RB / NT), r, cur, lim, snap);
 }
 
 
@@ -282,21 +277,20 @@ struct EParams {
   uint64_t nblk;
 };
 
+// encode blocks: ERB = NT records, one per thread (a workgroup per 1024 records looping over its quarters
+// left 4 waves per SIMD)
+constexpr int ERB = NT;
 __global__ void __launch_bounds__(NT) esize_kernel(EParams p) {
   __shared__ uint64_t sh[NT / 64];
-  const uint64_t b = blockIdx.x;
-  uint64_t acc = 0;
-  for (int j = 0; j < RB / NT; j++) {
-    const uint64_t r = b * RB + (uint64_t)j * NT + threadIdx.x;
-    if (r < p.n) {   // Kitex-PB: the record's Batch frame (0x0A, uvarint body length, body)
-      const uint64_t sz = p.P->pb ? kxn_pb_frame_size(*p.P, *p.C, r) : kxn_write_record<false>(*p.P, *p.C, r, nullptr, 0);
-      p.sizes[r] = sz;
-      acc += sz;
-    }
+  const uint64_t r = (uint64_t)blockIdx.x * ERB + threadIdx.x;
+  uint64_t sz = 0;
+  if (r < p.n) {   // Kitex-PB: the record's Batch frame (0x0A, uvarint body length, body)
+    sz = p.P->pb ? kxn_pb_frame_size(*p.P, *p.C, r) : kxn_write_record<false>(*p.P, *p.C, r, nullptr, 0);
+    p.sizes[r] = sz;
   }
   uint64_t tot;
-  (void)wg_excl(acc, &tot, sh);
-  if (threadIdx.x == 0 && p.bsum) p.bsum[b] = tot;
+  (void)wg_excl(sz, &tot, sh);
+  if (threadIdx.x == 0 && p.bsum) p.bsum[blockIdx.x] = tot;
 }
 
 __global__ void __launch_bounds__(1024) escan_kernel(EParams p) {
@@ -325,19 +319,14 @@ __global__ void __launch_bounds__(1024) escan_kernel(EParams p) {
 __global__ void __launch_bounds__(NT) ewrite_kernel(EParams p) {
   __shared__ uint64_t sh[NT / 64];
   if (p.status->code != 0) return;
-  const uint64_t b = blockIdx.x;
-  uint64_t base = p.bsum[b];
-  for (int j = 0; j < RB / NT; j++) {
-    const uint64_t r = b * RB + (uint64_t)j * NT + threadIdx.x;
-    const uint64_t sz = r < p.n ? p.sizes[r] : 0;
-    uint64_t tot;
-    const uint64_t pre = wg_excl(sz, &tot, sh);
-    if (r < p.n) {
-      if (p.P->pb) kxn_pb_write_frame(*p.P, *p.C, r, p.out, base + pre, sz);
-      else (void)kxn_write_record<true>(*p.P, *p.C, r, p.out, base + pre);
-      if (p.offsets_out) p.offsets_out[r] = base + pre;
-    }
-    base += tot;
+  const uint64_t r = (uint64_t)blockIdx.x * ERB + threadIdx.x;
+  const uint64_t sz = r < p.n ? p.sizes[r] : 0;
+  uint64_t tot;
+  const uint64_t at = p.bsum[blockIdx.x] + wg_excl(sz, &tot, sh);
+  if (r < p.n) {
+    if (p.P->pb) kxn_pb_write_frame(*p.P, *p.C, r, p.out, at, sz);
+    else (void)kxn_write_record<true>(*p.P, *p.C, r, p.out, at);
+    if (p.offsets_out) p.offsets_out[r] = at;
   }
 }
 
@@ -458,14 +447,14 @@ int kx_launch_nested_decode(const KxnProgram* dprog, const KxnProgram& hprog, co
   }
   hipLaunchKernelGGL(check_kernel, dim3(1), dim3(64), 0, stream, p);
   KX_HIP_CHECK(hipGetLastError());
-  hipLaunchKernelGGL(write_kernel, dim3((unsigned)p.nblk), dim3(NT), 0, stream, p);
+  hipLaunchKernelGGL(write_kernel, dim3((unsigned)((n + NT - 1) / NT)), dim3(NT), 0, stream, p);
   KX_HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(64), 0, stream, p);
   KX_HIP_CHECK(hipGetLastError());
   return KX_OK;
 }
 
-size_t kx_nested_enc_ws_bytes(uint64_t n) { return (n + 64) * 8 + ((n + RB - 1) / RB) * 8 + 256; }
+size_t kx_nested_enc_ws_bytes(uint64_t n) { return (n + 64) * 8 + ((n + ERB - 1) / ERB) * 8 + 256; }
 
 int kx_launch_nested_encode(const KxnProgram* dprog, const KxnProgram& hprog, const KxnCols* dcols, uint64_t n,
                             uint8_t* out, uint64_t out_cap, uint64_t* sizes_out, uint64_t* offsets_out,
@@ -478,7 +467,7 @@ int kx_launch_nested_encode(const KxnProgram* dprog, const KxnProgram& hprog, co
   p.n = n;
   p.out = out;
   p.out_cap = out_cap;
-  p.nblk = (n + RB - 1) / RB;
+  p.nblk = (n + ERB - 1) / ERB;
   p.bsum = (uint64_t*)ws;
   p.sizes = sizes_out ? sizes_out : (uint64_t*)ws + ((p.nblk + 63) & ~63ull);
   p.offsets_out = offsets_out;

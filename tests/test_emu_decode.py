@@ -266,3 +266,14 @@ def test_emu_offsets_length_gather(edec, oracle, case):
 def test_emu_long_strings(edec, oracle):
     """strings past the wave-copy threshold, inside and outside the tile window"""
     DC.case_long_strings(edec, oracle)
+
+
+def test_emu_bimodal_no_chain_repair(edec, oracle):
+    """1 % of the records at 64 KiB (tests/test_gpu_adversarial.py's batch, 20 000 records): decoded as the
+    oracle does, and no group needs the chain pass's repair (a tile holding the start of a record longer
+    than its window leaves the fast index path instead of reading as a tile with no record start)"""
+    from tests.test_gpu_adversarial import _bimodal_batch
+    sch = S.Schema(S.Struct("Bi", [S.Field(1, A.T_I64, "id"), S.Field(2, A.T_STRING, "s")]))
+    _, _, _, wire = _bimodal_batch(20000)
+    _, st = DC.check_decode(edec, oracle, sch, wire, 20000)
+    assert st.code == 0 and (st.diag[0], st.diag[1]) == (0, 0), list(st.diag)
