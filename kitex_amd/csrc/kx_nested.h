@@ -53,6 +53,7 @@
 #define KXN_MAX_DEFB 4096
 #define KXN_STACK 32          // walker frames (struct nesting + containers)
 #define KXN_SKIP_DEPTH 64     // codec_apache.go:167
+#define KXN_FMAP 32           // field ids 0 .. 31: direct lookup per struct (KxnProgram.fmap)
 
 enum : uint8_t { KN_SCALAR = 1, KN_STRING = 2, KN_RAW = 3, KN_STRUCT = 4, KN_LIST = 5, KN_MAP = 6 };
 
@@ -158,7 +159,19 @@ struct KxnProgram {
   KxnSdef sdf[KXN_MAX_SDF];
   KxnCol col[KX_MAX_COLUMNS];
   uint8_t defb[KXN_MAX_DEFB];
+  uint8_t fmap[KXN_MAX_STRUCTS][KXN_FMAP];   // struct s, field id i < KXN_FMAP: its field's index - st[s].first, 0xff none
 };
+
+// the field of struct T (index si) with id `id`, or -1: one table read for ids below KXN_FMAP, else a scan
+KXN_HD int kxn_field(const KxnProgram& P, int si, const KxnStruct& T, int64_t id) {
+  if (id >= 0 && id < KXN_FMAP) {
+    const uint32_t m = P.fmap[si][id];
+    return m == 0xff ? -1 : T.first + (int)m;
+  }
+  for (int k = 0; k < T.nfields; k++)
+    if (P.f[T.first + k].id == id) return T.first + k;
+  return -1;
+}
 
 // the column buffers of one call (device memory, uploaded per call)
 struct KxnCols {
@@ -551,8 +564,19 @@ KXN_HD int kxn_read_record(const KxnProgram& P, const KxnCols& C, B b, uint64_t 
   int sp = 0;
   uint64_t q = 0;
   kxn_inst_start<W>(P, C, 0, r, cur, S);
-  int rc = kxn_value<W>(P, C, b, len, &q, P.rec_node, cur, S, stk, &sp);
-  while (!rc && sp > 0) {
+  // One value read per iteration, at a single call site: the frame logic only chooses the node X to read
+  // (a struct's next field, a container's next element / key / value), so lanes of a wave at different
+  // frame kinds meet again at the read (lane = record: 3.4x between 4 096 distinct Nesting records and
+  // one record tiled, DESIGN §3.10, most of it divergence)
+  int rc = KX_OK;
+  int X = P.rec_node;
+  for (;;) {
+    if (X >= 0) {
+      rc = kxn_value<W>(P, C, b, len, &q, X, cur, S, stk, &sp);
+      X = -1;
+      if (rc) break;
+    }
+    if (sp == 0) break;
     KxnFrame& F = stk[sp - 1];
     if (F.kind == KN_STRUCT) {
       const KxnStruct& T = P.st[F.id];
@@ -571,31 +595,23 @@ KXN_HD int kxn_read_record(const KxnProgram& P, const KxnCols& C, B b, uint64_t 
       if (q + 3 > len) { rc = KX_ERR_EOF; break; }
       const int16_t id = h4 ? (int16_t)(uint16_t)(hw >> 8) : (int16_t)kxn_be16(b + q + 1);
       q += 3;
-      int fi = -1;
-      for (int k = 0; k < T.nfields; k++)
-        if (P.f[T.first + k].id == id) { fi = T.first + k; break; }
+      const int fi = kxn_field(P, F.id, T, id);
       if (fi < 0 || P.f[fi].ttype != t) {                       // default: / mismatched type -> Skip
-        rc = kxn_skip(b, len, &q, t, KXN_SKIP_DEPTH);
+        if ((rc = kxn_skip(b, len, &q, t, KXN_SKIP_DEPTH))) break;
         continue;
       }
       const KxnField& G = P.f[fi];
       const KxnNode& N = P.node[G.node];
       const uint64_t bit = 1ull << G.sbit;
+      const bool again = (S.seen[L] & bit) != 0;
       if (G.snap >= 0) {
-        if (S.seen[L] & bit) {                                  // repeated: keep only this occurrence
+        if (again) {                                            // repeated: keep only this occurrence
           for (int k = N.cur_lo; k < N.cur_hi; k++) cur[k] = snap[G.snap + k - N.cur_lo];
-          if (N.kind == KN_STRUCT) {                            // a fresh NewX()
-            const KxnStruct& U = P.st[N.a];
-            if (W && S.live[L])
-              for (int k = U.dfl_lo; k < U.dfl_hi; k++)
-                kxn_put_val(C, P.dfl[k].col, P.dfl[k].width, S.idx[L], (uint64_t)P.dfl[k].v);
-            S.seen[L] &= ~U.sub_mask;
-            S.pres[L] &= ~U.pres_mask;
-          }
         } else {
           for (int k = N.cur_lo; k < N.cur_hi; k++) snap[G.snap + k - N.cur_lo] = cur[k];
         }
-      } else if (N.kind == KN_STRUCT && (S.seen[L] & bit)) {  // repeated struct without var fields
+      }
+      if (again && N.kind == KN_STRUCT) {                       // a fresh NewX()
         const KxnStruct& U = P.st[N.a];
         if (W && S.live[L])
           for (int k = U.dfl_lo; k < U.dfl_hi; k++)
@@ -605,7 +621,7 @@ KXN_HD int kxn_read_record(const KxnProgram& P, const KxnCols& C, B b, uint64_t 
       }
       S.seen[L] |= bit;
       if (G.pbit >= 0) S.pres[L] |= 1ull << G.pbit;
-      rc = kxn_value<W>(P, C, b, len, &q, G.node, cur, S, stk, &sp);
+      X = G.node;
       continue;
     }
     // LIST / MAP: close the open element, then open the next one
@@ -614,24 +630,17 @@ KXN_HD int kxn_read_record(const KxnProgram& P, const KxnCols& C, B b, uint64_t 
       kxn_inst_end<W>(P, C, N.root, cur, S);
       F.open = 0;
     }
-    if (N.kind == KN_LIST) {
+    if (N.kind == KN_LIST || F.phase == 0) {
       if (F.rem == 0) { sp--; continue; }
       F.rem--;
       const uint64_t e = cur[N.cur]++;
       kxn_inst_start<W>(P, C, N.root, e, cur, S);
       F.open = 1;
-      rc = kxn_value<W>(P, C, b, len, &q, N.a, cur, S, stk, &sp);
-    } else if (F.phase == 0) {
-      if (F.rem == 0) { sp--; continue; }
-      F.rem--;
-      const uint64_t e = cur[N.cur]++;
-      kxn_inst_start<W>(P, C, N.root, e, cur, S);
-      F.open = 1;
-      F.phase = 1;
-      rc = kxn_value<W>(P, C, b, len, &q, N.a, cur, S, stk, &sp);
+      if (N.kind == KN_MAP) F.phase = 1;
+      X = N.a;
     } else {
       F.phase = 0;
-      rc = kxn_value<W>(P, C, b, len, &q, N.b, cur, S, stk, &sp);
+      X = N.b;
     }
   }
   if (rc) return rc;
@@ -956,7 +965,17 @@ KXN_HD int kxn_pb_read_record(const KxnProgram& P, const KxnCols& C, B b, uint64
   int rc = KX_OK;
   kxn_inst_start<W>(P, C, 0, r, cur, S);
   stk[sp++] = KxnPFrame{0, 0, P.node[P.rec_node].a, -1, 0, len, {0, 0}};
-  while (sp > 0) {
+  // one value read per iteration at a single call site (as kxn_read_record): X, its frame's end and the
+  // root its instance closes are chosen by the field logic below
+  int X = -1, xclose = -1;
+  uint64_t xend = 0;
+  for (;;) {
+    if (X >= 0) {
+      rc = kxn_pb_value<W>(P, C, b, xend, &q, X, cur, S, stk, &sp, xclose);
+      X = -1;
+      if (rc) break;
+    }
+    if (sp == 0) break;
     KxnPFrame& F = stk[sp - 1];
     if (q >= F.end) {
       const int cl = F.close;
@@ -971,27 +990,26 @@ KXN_HD int kxn_pb_read_record(const KxnProgram& P, const KxnCols& C, B b, uint64
     if (num == 0 || num > 536870911ull) { rc = KX_ERR_INVALID_DATA; break; }   // protowire.MaxValidNumber
     if (F.kind == 1) {                                  // map entry: key = 1, value = 2
       const KxnNode& M = P.node[F.id];
-      const int X = num == 1 ? M.a : num == 2 ? M.b : -1;
-      if (X < 0 || wt != kxn_pb_wt(P.node[X])) {
+      const int Xm = num == 1 ? M.a : num == 2 ? M.b : -1;
+      if (Xm < 0 || wt != kxn_pb_wt(P.node[Xm])) {
         if ((rc = kxn_pb_skip(b, F.end, &q, wt))) break;
         continue;
       }
-      const KxnNode& V = P.node[X];
+      const KxnNode& V = P.node[Xm];
       const int k = num == 1 ? 0 : 1;
       if (V.kind == KN_STRING || V.kind == KN_RAW) {    // a repeated key / value string: the last one wins
         if (F.seen & (1 << k)) cur[V.cur] = F.c0[k];
         else F.c0[k] = cur[V.cur];
       }
       F.seen |= (uint8_t)(1 << k);
-      const uint64_t fe = F.end;
-      if ((rc = kxn_pb_value<W>(P, C, b, fe, &q, X, cur, S, stk, &sp, -1))) break;
+      xend = F.end;
+      xclose = -1;
+      X = Xm;
       continue;
     }
     const KxnStruct& T = P.st[F.id];
     const int L = T.level;
-    int fi = -1;
-    for (int k = 0; k < T.nfields; k++)
-      if (P.f[T.first + k].id == (int64_t)num) { fi = T.first + k; break; }
+    const int fi = kxn_field(P, F.id, T, (int64_t)num);
     if (fi < 0) {                                       // unknown field
       if ((rc = kxn_pb_skip(b, F.end, &q, wt))) break;
       continue;
@@ -1008,7 +1026,9 @@ KXN_HD int kxn_pb_read_record(const KxnProgram& P, const KxnCols& C, B b, uint64
         if (G.pbit >= 0) S.pres[L] |= 1ull << G.pbit;
         const uint64_t e = cur[N.cur]++;
         kxn_inst_start<W>(P, C, N.root, e, cur, S);
-        if ((rc = kxn_pb_value<W>(P, C, b, fend, &q, N.a, cur, S, stk, &sp, N.root))) break;
+        xend = fend;
+        xclose = N.root;
+        X = N.a;
       } else if (wt == 2 && E.kind == KN_SCALAR) {      // a packed run
         uint64_t l;
         if ((rc = kxn_uvarint(b, fend, &q, &l))) break;
@@ -1056,7 +1076,9 @@ KXN_HD int kxn_pb_read_record(const KxnProgram& P, const KxnCols& C, B b, uint64
     }
     S.seen[L] |= bit;
     if (G.pbit >= 0) S.pres[L] |= 1ull << G.pbit;
-    if ((rc = kxn_pb_value<W>(P, C, b, fend, &q, G.node, cur, S, stk, &sp, -1))) break;   // a message merges
+    xend = fend;   // a message merges
+    xclose = -1;
+    X = G.node;
   }
   if (rc) return rc;
   kxn_inst_end<W>(P, C, 0, cur, S);

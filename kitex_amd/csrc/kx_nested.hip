@@ -13,6 +13,7 @@
 // Encode: size pass (lane = record, BLength) -> block scan -> write pass (FastWriteNocopy at the
 // record's offset); struct_tpl.go:225-391.
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 
 #include "kx_internal.h"
 #include "kx_nested.h"
@@ -68,19 +69,28 @@ __device__ __forceinline__ int extent(const NParams& p, uint64_t r, uint64_t* a,
   return (*a > *b || *b > p.in_len) ? KX_ERR_INVALID_ARG : 0;
 }
 
-__device__ __forceinline__ void measure_record(const NParams& p, uint64_t r, uint64_t* cur, uint64_t* snap) {
-  const KxnProgram& P = *p.P;
+// the walk of record [a, b) (a per-lane LDS window over the record's bytes, refilled 32 bytes at a time,
+// measured slower: 7.8 / 21.0 ms for the measure / write passes against 7.2 / 15.6 ms)
+template <bool W>
+__device__ __forceinline__ int walk(const NParams& p, const KxnProgram& P, uint64_t a, uint64_t b, uint64_t r,
+                                   uint64_t* cur, uint64_t* snap, uint64_t* lim) {
+  uint64_t used = 0;
+  return P.pb ? kxn_pb_read_record<W>(P, *p.C, p.in + a, b - a, r, cur, snap, &used, lim)
+              : kxn_read_record<W>(P, *p.C, p.in + a, b - a, r, cur, snap, &used, lim);
+}
+
+__device__ __forceinline__ void measure_record(const NParams& p, const KxnProgram& P, uint64_t r, uint64_t* cur,
+                                               uint64_t* snap) {
   for (uint32_t k = 0; k < p.ncur; k++) cur[k] = 0;
-  uint64_t a = 0, b = 0, used = 0;
+  uint64_t a = 0, b = 0;
   int rc = extent(p, r, &a, &b);
   if (rc < 0) {
     rc = 0;  // not decoded: empty
     p.rcode[r] = 0xff;
   } else {
-    // (a per-lane 16-byte read-ahead block in place of the byte loads measured slower: 55.7 vs 41.7 ms
-    // for 1 M Nesting records, divergent refills and 164 VGPRs in the write pass)
-    if (!rc) rc = P.pb ? kxn_pb_read_record<false>(P, *p.C, p.in + a, b - a, r, cur, snap, &used)
-                       : kxn_read_record<false>(P, *p.C, p.in + a, b - a, r, cur, snap, &used);
+    // (a per-lane 16-byte read-ahead block in registers measured slower: 55.7 vs 41.7 ms for 1 M Nesting
+    // records, divergent refills and 164 VGPRs in the write pass)
+    if (!rc) rc = walk<false>(p, P, a, b, r, cur, snap, nullptr);
     if (!rc && p.concat && r < p.n && p.skip_st->code && r == p.skip_st->n_records) rc = p.skip_st->code;
     p.rcode[r] = (uint8_t)rc;
     if (rc) atomicMin(p.errkey, (unsigned long long)((r << 8) | (uint64_t)(rc & 0xff)));
@@ -90,11 +100,26 @@ __device__ __forceinline__ void measure_record(const NParams& p, uint64_t r, uin
 
 // cursors and snapshots in per-lane private (scratch) arrays (an LDS-resident variant, one wave per
 // workgroup, measured slower on the MI355X: 62.8 vs 43.7 ms for 1 M Nesting records)
-__global__ void __launch_bounds__(NT) measure_kernel(NParams p) {
-  const uint64_t r = (uint64_t)blockIdx.x * NT + threadIdx.x;
+// The program in LDS: the walk's table reads (nodes, fields, structs, roots, entries, defaults: a dozen
+// dependent reads per field) at LDS latency instead of through the vector L1 / L2. One copy per 512-thread
+// workgroup (31 KB: 5 workgroups fit a CU's LDS, more than the registers allow).
+constexpr int NTD = 512;
+__device__ __forceinline__ const KxnProgram& lds_program(const KxnProgram* g, KxnProgram* s) {
+  static_assert(sizeof(KxnProgram) % 4 == 0, "dword copy");
+  const uint32_t* src = (const uint32_t*)g;
+  uint32_t* dst = (uint32_t*)s;
+  for (uint32_t i = threadIdx.x; i < sizeof(KxnProgram) / 4; i += blockDim.x) dst[i] = src[i];
+  __syncthreads();
+  return *s;
+}
+
+__global__ void __launch_bounds__(NTD) measure_kernel(NParams p) {
+  __shared__ KxnProgram sP;
+  const KxnProgram& P = lds_program(p.P, &sP);
+  const uint64_t r = (uint64_t)blockIdx.x * NTD + threadIdx.x;
   if (r >= p.n) return;
   uint64_t cur[CUR], snap[SNAP];
-  measure_record(p, r, cur, snap);
+  measure_record(p, P, r, cur, snap);
 }
 
 
@@ -196,9 +221,8 @@ __global__ void check_kernel(NParams p) {
 }
 
 // record r (of block b), lane = record
-__device__ __forceinline__ void write_record(const NParams& p, uint64_t b, uint64_t r, uint64_t* cur, uint64_t* lim,
-                                             uint64_t* snap) {
-  const KxnProgram& P = *p.P;
+__device__ __forceinline__ void write_record(const NParams& p, const KxnProgram& P, uint64_t b, uint64_t r,
+                                             uint64_t* cur, uint64_t* lim, uint64_t* snap) {
   const uint64_t rb1 = kmin64((b + 1) * RB, p.n);   // the block's end
   // the record's cursor bases: the block base + the in-block prefix (bsum_kernel); its extent ends at the
   // next record's prefix, or at the next block's base
@@ -209,24 +233,25 @@ __device__ __forceinline__ void write_record(const NParams& p, uint64_t b, uint6
     lim[k] = r + 1 < rb1 ? base + c[r + 1] : (b + 1 < p.nblk ? p.bsum[(uint64_t)k * p.nblk + b + 1] : p.totals[k]);
   }
   const uint8_t rc = p.rcode[r];
-  uint64_t a = 0, e = 0, used = 0;
+  uint64_t a = 0, e = 0;
   if (rc == 0 && extent(p, r, &a, &e) == 0) {
-    if (P.pb) (void)kxn_pb_read_record<true>(P, *p.C, p.in + a, e - a, r, cur, snap, &used, lim);
-    else (void)kxn_read_record<true>(P, *p.C, p.in + a, e - a, r, cur, snap, &used, lim);
+    (void)walk<true>(p, P, a, e, r, cur, snap, lim);
   } else {
     kxn_failed_record(P, *p.C, r, cur);
   }
   if (p.record_status && !p.concat) p.record_status[r] = rc == 0xff ? 0 : rc;
 }
 
-// one record per thread: workgroup w holds records [w·NT, (w + 1)·NT) of block w / (RB / NT) (a workgroup
-// per block looping over its 4 quarters left 4 waves per SIMD: DESIGN §3.10)
-__global__ void __launch_bounds__(NT) write_kernel(NParams p) {
+// one record per thread: workgroup w holds records [w·NTD, (w + 1)·NTD) of block w / (RB / NTD) (a workgroup
+// per block looping over its quarters left 4 waves per SIMD: DESIGN §3.10)
+__global__ void __launch_bounds__(NTD) write_kernel(NParams p) {
   if (*p.flag) return;
-  const uint64_t r = (uint64_t)blockIdx.x * NT + threadIdx.x;
+  __shared__ KxnProgram sP;
+  const KxnProgram& P = lds_program(p.P, &sP);
+  const uint64_t r = (uint64_t)blockIdx.x * NTD + threadIdx.x;
   if (r >= p.n) return;
   uint64_t cur[CUR], lim[CUR], snap[SNAP];
-  write_record(p, blockIdx.x / (RB / NT), r, cur, lim, snap);
+  write_record(p, P, blockIdx.x / (RB / NTD), r, cur, lim, snap);
 }
 
 
@@ -432,7 +457,7 @@ int kx_launch_nested_decode(const KxnProgram* dprog, const KxnProgram& hprog, co
   } else {
     p.offsets = offsets;
   }
-  hipLaunchKernelGGL(measure_kernel, dim3((unsigned)((n + NT - 1) / NT)), dim3(NT), 0, stream, p);
+  hipLaunchKernelGGL(measure_kernel, dim3((unsigned)((n + NTD - 1) / NTD)), dim3(NTD), 0, stream, p);
   KX_HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(bsum_kernel, dim3((unsigned)p.nblk, hprog.ncur), dim3(NT), 0, stream, p);
   KX_HIP_CHECK(hipGetLastError());
@@ -447,7 +472,7 @@ int kx_launch_nested_decode(const KxnProgram* dprog, const KxnProgram& hprog, co
   }
   hipLaunchKernelGGL(check_kernel, dim3(1), dim3(64), 0, stream, p);
   KX_HIP_CHECK(hipGetLastError());
-  hipLaunchKernelGGL(write_kernel, dim3((unsigned)((n + NT - 1) / NT)), dim3(NT), 0, stream, p);
+  hipLaunchKernelGGL(write_kernel, dim3((unsigned)((n + NTD - 1) / NTD)), dim3(NTD), 0, stream, p);
   KX_HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(64), 0, stream, p);
   KX_HIP_CHECK(hipGetLastError());

@@ -394,6 +394,9 @@ struct NB {
       }
     }
     stack.pop_back();
+    memset(P.fmap[si], 0xff, KXN_FMAP);
+    for (uint32_t i = 0; i < sd.nfields; i++)
+      if (sd.fields[i].id >= 0 && sd.fields[i].id < KXN_FMAP) P.fmap[si][sd.fields[i].id] = (uint8_t)i;
     P.st[si].dfl_hi = (uint16_t)roots[R].dfl.size();
     // encoder order: fixed-length fields first (patcher.go:503-522), IDL order inside each group;
     // Kitex-Protobuf: field-number order (proto.Marshal)

@@ -12,7 +12,7 @@ from kitex_amd.codec import ThriftCodec, read_status, status_tensor  # noqa: E40
 from kitex_amd.columns import alloc_device  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 20
-k = 4096
+k = int(sys.argv[2]) if len(sys.argv) > 2 else 4096   # distinct records (1: every lane walks the same shape)
 dev = torch.device("cuda", 0)
 doc = idl.parse_idl(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden",
                                  "idl", "baseline.thrift"))
@@ -37,7 +37,7 @@ for mode in ("concat", "offsets"):
         cdc.Unmarshal(wire, n, offsets=offs, out=out, var_caps=vc, raise_on_error=False, status=st)
     torch.cuda.synchronize()
     s = read_status(st)
-    print(f"KX_NESTED_LDS={os.environ.get('KX_NESTED_LDS', '1')} decode {mode} n={n}: "
+    print(f"k={k} decode {mode} n={n}: "
           f"{(time.perf_counter() - t0) / 5 * 1e3:.2f} ms code={s.code} n_records={s.n_records}", flush=True)
 w2, _ = cdc.Marshal(out)
 torch.cuda.synchronize()
