@@ -485,68 +485,52 @@ template <bool W, class B>
 KXN_HD int kxn_value(const KxnProgram& P, const KxnCols& C, B b, uint64_t len, uint64_t* q, int X,
                      uint64_t* cur, KxnState& S, KxnFrame* stk, int* sp) {
   const KxnNode& N = P.node[X];
-  switch (N.kind) {
-    case KN_SCALAR: {
-      if (*q + N.width > len) return KX_ERR_EOF;
-      if (W && S.live[N.level]) kxn_put_val(C, N.col, N.width, S.idx[N.level], kxn_scalar(N.ttype, b + *q));
-      *q += N.width;
-      return KX_OK;
+  const uint32_t kind = N.kind;
+  if (kind == KN_RAW) {                                      // a recursive struct: its encoded bytes
+    uint64_t e = *q;
+    const int rc = kxn_skip(b, len, &e, KX_T_STRUCT, KXN_SKIP_DEPTH);
+    if (rc) return rc;
+    if (W) {
+      uint8_t* dst = (uint8_t*)C.data[N.col] + cur[N.cur];
+      const uint64_t room = S.lim[N.cur] > cur[N.cur] ? S.lim[N.cur] - cur[N.cur] : 0;
+      const uint64_t m = e - *q < room ? e - *q : room;
+      kxn_copy(dst, b + *q, m);
     }
-    case KN_STRING: {                                        // ReadString: a copy
-      if (*q + 4 > len) return KX_ERR_EOF;
-      const int32_t l = (int32_t)kxn_be32(b + *q);
-      if (l < 0) return KX_ERR_NEGATIVE_SIZE;
-      if (*q + 4 + (uint64_t)l > len) return KX_ERR_EOF;
-      if (W) {
-        uint8_t* dst = (uint8_t*)C.data[N.col] + cur[N.cur];
-        const uint64_t room = S.lim[N.cur] > cur[N.cur] ? S.lim[N.cur] - cur[N.cur] : 0;
-        const uint64_t m = (uint64_t)l < room ? (uint64_t)l : room;
-        kxn_copy(dst, b + *q + 4, m);
-      }
-      cur[N.cur] += (uint64_t)l;
-      *q += 4 + (uint64_t)l;
-      return KX_OK;
-    }
-    case KN_RAW: {                                           // a recursive struct: its encoded bytes
-      uint64_t e = *q;
-      const int rc = kxn_skip(b, len, &e, KX_T_STRUCT, KXN_SKIP_DEPTH);
-      if (rc) return rc;
-      if (W) {
-        uint8_t* dst = (uint8_t*)C.data[N.col] + cur[N.cur];
-        const uint64_t room = S.lim[N.cur] > cur[N.cur] ? S.lim[N.cur] - cur[N.cur] : 0;
-        const uint64_t m = e - *q < room ? e - *q : room;
-        kxn_copy(dst, b + *q, m);
-      }
-      cur[N.cur] += e - *q;
-      *q = e;
-      return KX_OK;
-    }
-    case KN_STRUCT:
-      if (*sp >= KXN_STACK) return KX_ERR_DEPTH_LIMIT;
-      stk[*sp] = KxnFrame{KN_STRUCT, 0, 0, 0, N.a, 0, 0};
-      (*sp)++;
-      return KX_OK;
-    case KN_LIST: {                                          // ReadListBegin / ReadSetBegin (:537-625)
-      if (*q + 5 > len) return KX_ERR_EOF;
-      const int32_t c = (int32_t)kxn_be32(b + *q + 1);
-      if (c < 0) return KX_ERR_NEGATIVE_SIZE;
-      *q += 5;
-      if (*sp >= KXN_STACK) return KX_ERR_DEPTH_LIMIT;
-      stk[*sp] = KxnFrame{KN_LIST, 0, 0, 0, (int16_t)X, 0, (int64_t)c};
-      (*sp)++;
-      return KX_OK;
-    }
-    default: {                                               // ReadMapBegin (:466-533)
-      if (*q + 6 > len) return KX_ERR_EOF;
-      const int32_t c = (int32_t)kxn_be32(b + *q + 2);
-      if (c < 0) return KX_ERR_NEGATIVE_SIZE;
-      *q += 6;
-      if (*sp >= KXN_STACK) return KX_ERR_DEPTH_LIMIT;
-      stk[*sp] = KxnFrame{KN_MAP, 0, 0, 0, (int16_t)X, 0, (int64_t)c};
-      (*sp)++;
-      return KX_OK;
-    }
+    cur[N.cur] += e - *q;
+    *q = e;
+    return KX_OK;
   }
+  // Every other kind in one straight line (lanes of a wave reading different kinds stay together): the
+  // bytes it starts with (a scalar's value, a string's length, ReadListBegin's type + count, ReadMapBegin's
+  // two types + count: struct_tpl.go:425-625) and, for strings and containers, the one length word
+  const uint32_t hl = kind == KN_SCALAR ? N.width : kind == KN_STRING ? 4u : kind == KN_LIST ? 5u : kind == KN_MAP ? 6u : 0u;
+  if (*q + hl > len) return KX_ERR_EOF;
+  const bool word = kind == KN_STRING || kind == KN_LIST || kind == KN_MAP;
+  const int32_t c = word ? (int32_t)kxn_be32(b + *q + (kind == KN_LIST ? 1u : kind == KN_MAP ? 2u : 0u)) : 0;
+  if (c < 0) return KX_ERR_NEGATIVE_SIZE;
+  if (kind == KN_SCALAR) {
+    if (W && S.live[N.level]) kxn_put_val(C, N.col, N.width, S.idx[N.level], kxn_scalar(N.ttype, b + *q));
+    *q += hl;
+    return KX_OK;
+  }
+  if (kind == KN_STRING) {                                   // ReadString: a copy
+    const uint64_t l = (uint64_t)c;
+    if (*q + 4 + l > len) return KX_ERR_EOF;
+    if (W) {
+      uint8_t* dst = (uint8_t*)C.data[N.col] + cur[N.cur];
+      const uint64_t room = S.lim[N.cur] > cur[N.cur] ? S.lim[N.cur] - cur[N.cur] : 0;
+      kxn_copy(dst, b + *q + 4, l < room ? l : room);
+    }
+    cur[N.cur] += l;
+    *q += 4 + l;
+    return KX_OK;
+  }
+  // STRUCT / LIST / SET / MAP: a frame (a struct's fields, a container's elements)
+  if (*sp >= KXN_STACK) return KX_ERR_DEPTH_LIMIT;
+  stk[*sp] = KxnFrame{(uint8_t)kind, 0, 0, 0, (int16_t)(kind == KN_STRUCT ? N.a : X), 0, (int64_t)c};
+  (*sp)++;
+  *q += hl;
+  return KX_OK;
 }
 
 // FastRead of record r = b[0 .. len). cur: cursors (measure: from 0, write: at the record's bases);
