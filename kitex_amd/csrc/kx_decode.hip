@@ -1843,6 +1843,32 @@ __device__ __forceinline__ uint32_t data_sig_s(KParams& dp) {
   return *(const KAS uint32_t*)dp.in & 0xffffffu;
 }
 
+// A second data-derived signature for batches without the schema's own one (the skip decoder; producers
+// whose records start with another field): the header that follows the batch's first record's leading
+// fixed-size fields (up to three), at its offset. Records that start alike share it; a nested struct
+// whose first fields coincide with the record's usually does not (Kitex's encoder writes a Nesting
+// record's double, i32 and i64 first, the way its Simple elements start: before this, every Simple
+// element was a candidate record start, and 1 M re-encoded Nesting records sent the chain pass into
+// serial repair for minutes). s2o = 0: none.
+__device__ __forceinline__ void data_sig2(KParams& dp, uint32_t& s2o, uint32_t& s2) {
+  s2o = 0;
+  s2 = 0;
+  if (dp.offsets) return;
+  const GLB uint8_t* p = (const GLB uint8_t*)dp.in;
+  uint64_t pos = 0;
+  for (int k = 0; k < 3; k++) {
+    if (pos + 3 > dp.in_len) break;
+    const int sz = tsize(p[pos]);
+    if (sz <= 0) break;
+    pos += 3 + (uint64_t)sz;
+    if (pos + 3 > dp.in_len || p[pos] == KX_T_STOP || pos > 256) break;
+    s2o = (uint32_t)pos;
+    s2 = (uint32_t)p[pos] | ((uint32_t)p[pos + 1] << 8) | ((uint32_t)p[pos + 2] << 16);
+  }
+  s2o = __builtin_amdgcn_readfirstlane(s2o);
+  s2 = __builtin_amdgcn_readfirstlane(s2);
+}
+
 // The lane's speculation: its segment's boundary signature, and the first signature hit. A hit is
 // a guess; a guess whose own walk fails is replaced by the next hit (walk_tile), so payload bytes
 // that contain the signature (binary strings saturated with it, strings holding serialized records)
@@ -1943,6 +1969,8 @@ __device__ __forceinline__ uint64_t frame_scan_segment(KParams& dp, const Src& w
   return X_NONE;
 }
 
+__device__ __forceinline__ uint64_t next_hit(KParams& dp, const Src& w, const Cand& cd, uint64_t p);
+
 template <int NV, int MODE>
 __device__ __forceinline__ Cand lane_candidate(KParams& dp, const Src& w, uint64_t seg_lo, uint64_t seg_hi, int lane,
                                                uint32_t dsig) {
@@ -2001,6 +2029,12 @@ __device__ __forceinline__ Cand lane_candidate(KParams& dp, const Src& w, uint64
   } else {
     for (uint64_t p = seg_lo; p < plim; p++)
       if ((ld4(w, p) & cd.smask) == sig) { cd.ent = p; break; }
+  }
+  if (!own && slen == 3) {   // a data-derived signature: its second header too (data_sig2)
+    data_sig2(dp, cd.s2o, cd.s2);
+    if (cd.s2o && cd.ent != X_NONE &&
+        (cd.ent + cd.s2o + 3 > dp.in_len || (ld4(w, cd.ent + cd.s2o) & 0xffffffu) != cd.s2))
+      cd.ent = next_hit(dp, w, cd, cd.ent);
   }
   return cd;
 }

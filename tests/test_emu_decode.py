@@ -277,3 +277,24 @@ def test_emu_bimodal_no_chain_repair(edec, oracle):
     _, _, _, wire = _bimodal_batch(20000)
     _, st = DC.check_decode(edec, oracle, sch, wire, 20000)
     assert st.code == 0 and (st.diag[0], st.diag[1]) == (0, 0), list(st.diag)
+
+
+def test_emu_skip_encoder_order_nesting(oracle):
+    """baseline.thrift Nesting records as Kitex's encoder writes them (fixed-length fields first: double,
+    i32, i64, byte — the way its Simple elements start too): the skip decoder delimits them as the oracle
+    does with no tile re-walk and no group re-scan (data_sig2)"""
+    import os
+    from kitex_amd import idl
+    doc = idl.parse_idl(os.path.join(os.path.dirname(__file__), "golden", "idl", "baseline.thrift"))
+    sch = idl.to_schema(doc.struct("Nesting"))
+    recs = synth.thrift_records(sch, 1500, seed=7)
+    wire = np.frombuffer(b"".join(recs), dtype=np.uint8).copy()
+    _, infos, npres = oracle.flatten(sch)
+    rc, out, st, _ = emu.nested_decode(sch, infos, npres, wire, 1500)
+    assert rc == 0 and st.code == 0
+    rc, w2, offs = emu.nested_encode(sch, infos, out)
+    assert rc == 0 and w2[0] == A.T_DOUBLE          # encoder order: the double first
+    rc, got, st = emu.skip(w2, 1500)
+    assert rc == 0 and st.code == 0 and st.n_records == 1500
+    assert np.array_equal(got, offs)
+    assert (st.diag[0], st.diag[1]) == (0, 0), list(st.diag)
