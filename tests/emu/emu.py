@@ -51,6 +51,8 @@ def lib():
         _lib.emu_crc.restype = C.c_int
         _lib.emu_crc.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_int, C.c_void_p, C.c_void_p,
                                  C.c_void_p]
+        _lib.emu_pb_frames.restype = C.c_int
+        _lib.emu_pb_frames.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64] + [C.c_void_p] * 4
         _lib.emu_frames.restype = C.c_int
         _lib.emu_frames.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint64] + [C.c_void_p] * 5 + [C.c_int,
                                                                                                   C.c_void_p]
@@ -111,6 +113,19 @@ def split_points(schema, data: np.ndarray, n: int, parts: int, threads: int = 8)
     rc = lib().emu_split(C.cast(tab, C.c_void_p) if tab is not None else None, ns, data.ctypes.data, data.size, n,
                          parts, pts.ctypes.data, C.addressof(st), 1 if schema is None else 0)
     return rc, pts, st
+
+
+def pb_frames(data: np.ndarray, n: int, threads: int = 8):
+    """the Kitex-PB Batch frame pass of the kernel source: rc, frame offsets (n + 1), body starts, body ends,
+    status"""
+    os.environ["KX_EMU_THREADS"] = str(threads)
+    fo = np.zeros(n + 1, dtype=np.uint64)
+    bs = np.zeros(max(1, n), dtype=np.uint64)
+    be = np.zeros(max(1, n), dtype=np.uint64)
+    st = A.Status()
+    rc = lib().emu_pb_frames(data.ctypes.data, data.size, n, fo.ctypes.data, bs.ctypes.data, be.ctypes.data,
+                             C.addressof(st))
+    return rc, fo, bs[:n], be[:n], st
 
 
 def frames(data: np.ndarray, n: int, max_payload: int = 0, threads: int = 8, grpc: bool = False, crc: bool = False):

@@ -112,6 +112,28 @@ extern "C" int emu_frames(const uint8_t* in, uint64_t in_len, uint64_t n, uint64
                           nullptr, nullptr, nullptr, nullptr, crc_codes);
 }
 
+// Kitex-PB Batch frames (kx_launch_pb_frames: the nested proto path's record delimiter) under the emulator
+extern "C" int emu_pb_frames(const uint8_t* in, uint64_t in_len, uint64_t n, uint64_t* fo, uint64_t* bs, uint64_t* be,
+                             kx_status* status) {
+  const size_t ws_size = kx_skip_ws_bytes(in_len, n);
+  static char* ws = nullptr;
+  static size_t ws_cap = 0;
+  static uint64_t epoch = 0xffff;
+  if (ws_cap < ws_size) {
+    free(ws);
+    ws_cap = ws_size + ws_size / 4;
+    ws = (char*)malloc(ws_cap);
+    epoch = 0xffff;
+  }
+  if (++epoch > 0xffff) {
+    memset(ws, 0, ws_cap);
+    memset(ws + 8, 0xff, 8);
+    epoch = 1;
+  }
+  status->diag[0] = status->diag[1] = status->diag[2] = 0;
+  return kx_launch_pb_frames(in, in_len, n, fo, bs, be, status, ws, ws_cap, epoch, nullptr);
+}
+
 // ttstream frame scan (kx_launch_frames with keys) under the emulator
 extern "C" int emu_tts_frames(const uint8_t* in, uint64_t in_len, uint64_t n, const kx_ttstream_keys* keys,
                               uint64_t* fo, uint64_t* ps, uint64_t* pe, uint8_t* ft, int32_t* sid, uint64_t* mp,

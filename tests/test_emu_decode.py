@@ -298,3 +298,22 @@ def test_emu_skip_encoder_order_nesting(oracle):
     assert rc == 0 and st.code == 0 and st.n_records == 1500
     assert np.array_equal(got, offs)
     assert (st.diag[0], st.diag[1]) == (0, 0), list(st.diag)
+
+
+def test_emu_pb_frames_nested_no_repair():
+    """Kitex-PB Batch frames of nested PN records (tests/pbn_cases.py: maps with string keys and repeated
+    messages put 0x0A bytes inside every record): delimited exactly, and no group needs the chain pass's
+    re-scan (a candidate frame must be followed by another; a lane tries its segment's later 0x0A bytes)"""
+    from tests import pbn_cases as PB
+    k = 4000
+    _, bodies, boffs = PB.batch(k, seed=7, name="PN")
+    lens = np.diff(boffs).astype(np.int64)
+    recs = [b"\x0a" + PB.uvarint(int(lens[i])) + bodies[int(boffs[i]):int(boffs[i + 1])].tobytes() for i in range(k)]
+    wire = np.frombuffer(b"".join(recs), dtype=np.uint8).copy()
+    rc, fo, bs, be, st = emu.pb_frames(wire, k)
+    exp = np.zeros(k + 1, dtype=np.uint64)
+    exp[1:] = np.cumsum([len(r) for r in recs])
+    assert rc == 0 and st.code == 0 and st.n_records == k
+    assert np.array_equal(fo, exp)
+    assert np.array_equal(be - bs, lens.astype(np.uint64))
+    assert (st.diag[0], st.diag[1]) == (0, 0), list(st.diag)
