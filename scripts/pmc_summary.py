@@ -13,7 +13,8 @@ import os
 import sys
 from collections import defaultdict
 
-DECODE = ("index_kernel", "index_fast_kernel", "redo_kernel", "group_kernel", "chain_kernel", "emit_kernel", "finalize_kernel")
+DECODE = ("index_kernel", "index_fast_kernel", "redo_kernel", "group_kernel", "chain_kernel", "chain_fast_kernel", "emit_kernel",
+          "emit_fast_kernel", "emit_redo_kernel", "finalize_kernel")
 ENCODE = ("size_kernel", "scan_kernel", "write_kernel")
 CRC = ("crc_kernel", "crc_final_kernel")
 KERNELS = DECODE

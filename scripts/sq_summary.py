@@ -7,7 +7,8 @@ import sys
 from collections import defaultdict
 
 d = sys.argv[1]
-KS = ("index_kernel<", "index_fast_kernel<", "redo_kernel<", "group_kernel<", "chain_kernel<", "emit_kernel<", "combo_kernel<", "write_kernel<", "size_kernel<",
+KS = ("index_kernel<", "index_fast_kernel<", "redo_kernel<", "group_kernel<", "chain_kernel<", "chain_fast_kernel<",
+      "emit_kernel<", "emit_fast_kernel<", "emit_redo_kernel<", "combo_kernel<", "write_kernel<", "size_kernel<",
       "crc_kernel(")
 agg = defaultdict(lambda: defaultdict(list))
 for p in ("p1", "p2"):
