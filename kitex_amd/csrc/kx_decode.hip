@@ -1477,6 +1477,20 @@ __device__ __forceinline__ uint64_t pb_scan_segment(const Src& w, uint64_t seg_l
   // both lowest were false (0x0A bytes in the previous record's tail): the segment's later 0x0A bytes in
   // order, so the tile's first frame is still its entry (a later one would send the group to the chain
   // pass's serial re-scan)
+  if (q0 >= 0 && n == SEG) {   // dword by dword from the window: only the 0x0A bytes are probed
+    const LDS uint32_t* s = w.win + (q0 >> 2);
+    const uint32_t sh0 = q0 & 3;
+    for (uint32_t d = (c2 + 1 + sh0) >> 2; d < 33; d++) {
+      uint32_t m = zero_bytes(s[d] ^ 0x0A0A0A0Au);
+      while (m) {
+        const uint32_t rel = 4 * d + first_hit(m) - sh0;
+        m &= m - 1;
+        if (rel <= c2 || rel >= n) continue;
+        if (pb_frame_ok(w, seg_lo + rel, len)) return seg_lo + rel;
+      }
+    }
+    return X_NONE;
+  }
   for (uint32_t rel = c2 + 1; rel < n; rel++)
     if (ld1(w, seg_lo + rel) == 0x0Au && pb_frame_ok(w, seg_lo + rel, len)) return seg_lo + rel;
   return X_NONE;

@@ -307,10 +307,12 @@ struct EParams {
 constexpr int ERB = NT;
 __global__ void __launch_bounds__(NT) esize_kernel(EParams p) {
   __shared__ uint64_t sh[NT / 64];
+  __shared__ KxnProgram sP;
+  const KxnProgram& P = lds_program(p.P, &sP);   // the walk's table reads at LDS latency (as decode)
   const uint64_t r = (uint64_t)blockIdx.x * ERB + threadIdx.x;
   uint64_t sz = 0;
   if (r < p.n) {   // Kitex-PB: the record's Batch frame (0x0A, uvarint body length, body)
-    sz = p.P->pb ? kxn_pb_frame_size(*p.P, *p.C, r) : kxn_write_record<false>(*p.P, *p.C, r, nullptr, 0);
+    sz = P.pb ? kxn_pb_frame_size(P, *p.C, r) : kxn_write_record<false>(P, *p.C, r, nullptr, 0);
     p.sizes[r] = sz;
   }
   uint64_t tot;
@@ -343,14 +345,16 @@ __global__ void __launch_bounds__(1024) escan_kernel(EParams p) {
 
 __global__ void __launch_bounds__(NT) ewrite_kernel(EParams p) {
   __shared__ uint64_t sh[NT / 64];
+  __shared__ KxnProgram sP;
   if (p.status->code != 0) return;
+  const KxnProgram& P = lds_program(p.P, &sP);
   const uint64_t r = (uint64_t)blockIdx.x * ERB + threadIdx.x;
   const uint64_t sz = r < p.n ? p.sizes[r] : 0;
   uint64_t tot;
   const uint64_t at = p.bsum[blockIdx.x] + wg_excl(sz, &tot, sh);
   if (r < p.n) {
-    if (p.P->pb) kxn_pb_write_frame(*p.P, *p.C, r, p.out, at, sz);
-    else (void)kxn_write_record<true>(*p.P, *p.C, r, p.out, at);
+    if (P.pb) kxn_pb_write_frame(P, *p.C, r, p.out, at, sz);
+    else (void)kxn_write_record<true>(P, *p.C, r, p.out, at);
     if (p.offsets_out) p.offsets_out[r] = at;
   }
 }
