@@ -2313,7 +2313,7 @@ __device__ __forceinline__ bool fast_record_fp(KParams& dp, const Src& w, uint32
 // (a 64 KiB string) is then a record start the fast path cannot walk, not a false signature hit: its tile
 // takes the general walk instead of reading as one with no record start (such a tile
 // used to send its whole group to the chain pass's repair). Off the hot path: failing lanes only.
-__device__ __noinline__ bool record_leaves_window(const Src& w, uint32_t q) {
+__device__ __forceinline__ bool record_leaves_window(const Src& w, uint32_t q) {
   const KAS KxpStep* __restrict__ steps = w.steps;
   const uint32_t wl = (uint32_t)w.wlen;
   for (uint32_t k = 0; k < w.nsteps; k++) {
