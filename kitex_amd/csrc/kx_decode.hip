@@ -623,6 +623,7 @@ __device__ __forceinline__ int generic_record(const Src& w, const KAS KxProgram*
   uint64_t pos = start;
   int inst = 0;
   int pred = P->inst[0].enc_first;
+  int ipred = -1;   // IDL-order guess: the field after the last one read
   uint64_t seen = 0;
   // inside a list<S> field (S of fixed scalars): its elements are read by this same loop (one skip
   // decoder instance per kernel: a second inlined copy doubled the index pass's scratch and halved it)
@@ -678,9 +679,15 @@ __device__ __forceinline__ int generic_record(const Src& w, const KAS KxProgram*
     } else if (pred >= 0 && F.id == id) {
       fi = pred;
     } else {
+      // the encoder-order guess missed: the field after the last one in IDL order (a producer writing IDL
+      // order, e.g. Apache Thrift), else a scan of the instance's fields
       const KxpInst I = ld_inst(P, inst);
-      for (int k = 0; k < I.nfields; k++)
-        if (P->f[I.first + k].id == id) { fi = I.first + k; break; }
+      if (ipred >= I.first && ipred < I.first + I.nfields && P->f[ipred].id == id) {
+        fi = ipred;
+      } else {
+        for (int k = 0; k < I.nfields; k++)
+          if (P->f[I.first + k].id == id) { fi = I.first + k; break; }
+      }
       if (fi >= 0) F = ld_field(P, fi);
     }
     const uint64_t vp = pos + 3;
@@ -691,6 +698,7 @@ __device__ __forceinline__ int generic_record(const Src& w, const KAS KxProgram*
       continue;
     }
     pred = F.enc_next;
+    ipred = fi + 1;
     if (F.kind == KXP_K_FIXED) {
       const uint32_t wd = F.width;
       if (limit - vp < wd) return KX_ERR_EOF;
@@ -2062,7 +2070,9 @@ __device__ __forceinline__ Cand lane_candidate(KParams& dp, const Src& w, uint64
     for (uint64_t p = seg_lo; p < plim; p++)
       if ((ld4(w, p) & cd.smask) == sig) { cd.ent = p; break; }
   }
-  if (!own && slen == 3) {   // a data-derived signature: its second header too (data_sig2)
+  // a data-derived signature of a batch that can nest structs (the skip decoder, list<S> schemas): its
+  // second header too (data_sig2); a flat schema's typed walk rejects a nested struct's fields itself
+  if ((MODE == M_SKIP || MODE == M_THRIFT_LS) && !own && slen == 3) {
     data_sig2(dp, cd.s2o, cd.s2);
     if (cd.s2o && cd.ent != X_NONE &&
         (cd.ent + cd.s2o + 3 > dp.in_len || (ld4(w, cd.ent + cd.s2o) & 0xffffffu) != cd.s2))
@@ -2088,8 +2098,13 @@ __device__ __forceinline__ uint64_t next_hit(KParams& dp, const Src& w, const Ca
 // candidate is trusted). The record starts of the tile are written to `starts` (u16, relative to
 // tlo). Returns the tile aggregate (uniform).
 template <int NV, int MODE>
-__device__ Agg walk_tile(KParams& dp, const Src& w, uint64_t tlo, uint64_t thi, uint64_t seed, int lane,
+__device__ Agg walk_tile(KParams& dp, const Src& w_, uint64_t tlo, uint64_t thi, uint64_t seed, int lane,
                          uint16_t* starts, uint32_t dsig) {
+  // a batch whose first record does not start with the plan's signature (an IDL-order producer, an unset
+  // first field) is walked with the generic field loop alone: trying the plan first failed on every
+  // record, one wasted LDS round trip each
+  Src w = w_;
+  if (is_thrift(MODE) && dsig && dsig != dp.prog->sig) w.nsteps = 0;
   const uint64_t seg_lo = tlo + (uint64_t)lane * SEG;
   const uint64_t seg_hi = kmin64(seg_lo + SEG, thi);
   const Cand cd = lane_candidate<NV, MODE>(dp, w, seg_lo, seg_hi, lane, dsig);
@@ -3560,7 +3575,7 @@ __device__ __noinline__ uint8_t frame_crc_check(const Src w, uint64_t in_len, ui
 // COOP: numeric list columns are copied by the whole wave (its own instantiation, so that schemas
 // without such a column keep the record-by-record kernel's code)
 template <int NV, int MODE, bool COOP>
-__device__ __forceinline__ void emit_tile(KParams& dp, LDS uint32_t* win, uint64_t t, int lane) {
+__device__ __forceinline__ void emit_tile(KParams& dp, LDS uint32_t* win, uint64_t t, int lane, bool plan = true) {
   const KAS KxProgram* P = dp.prog;
   const bool known = dp.offsets != nullptr;
   const uint64_t nstop = known ? dp.n : *(volatile uint64_t*)dp.nstop;
@@ -3568,7 +3583,8 @@ __device__ __forceinline__ void emit_tile(KParams& dp, LDS uint32_t* win, uint64
   tile_range(dp, t, lo, hi);
   // the window DMA is issued first; the tile's bases are read while it is in flight
   const uint16_t* starts = dp.starts + t * dp.slotcap;
-  const Src w = load_window(dp, win, known ? dp.offsets[lo] : lo, lane, is_thrift(MODE), false);
+  Src w = load_window(dp, win, known ? dp.offsets[lo] : lo, lane, is_thrift(MODE), false);
+  if (!plan) w.nsteps = 0;   // records known not to start on the plan (walk_tile): the generic loop alone
   uint64_t base = 0, cnt = 0, run[NV > 0 ? NV : 1];
 #pragma unroll
   for (int v = 0; v < (NV > 0 ? NV : 1); v++) run[v] = 0;
@@ -4032,7 +4048,7 @@ __global__ void __launch_bounds__(NT, 4) emit_redo_kernel(DecParams dp_) {
   const uint32_t W = gridDim.x * WAVES;
   if (data_sig_s(dp) != dp.prog->sig) {   // emit_fast_kernel left the whole batch: every tile
     for (uint64_t t = dp.t_lo + blockIdx.x * WAVES + wv; t < dp.t_hi; t += W)
-      emit_tile<NV, MODE, COOP>(dp, (LDS uint32_t*)WIN[wv], t, lane);
+      emit_tile<NV, MODE, COOP>(dp, (LDS uint32_t*)WIN[wv], t, lane, false);
     return;
   }
   const uint32_t n = __builtin_amdgcn_readfirstlane(*(volatile uint32_t*)(dp.redo_n + 2));

@@ -29,7 +29,7 @@ def torch():
     return t
 
 
-def _time_decode(torch, cdc, wire, n, reps=3):
+def _time_decode(torch, cdc, wire, n, reps=5):
     """decoded ColumnSet, status, and the best per-call time (s) over `reps` timed calls"""
     res = cdc.Unmarshal(wire, n, raise_on_error=False)
     torch.cuda.synchronize()
