@@ -2098,13 +2098,10 @@ __device__ __forceinline__ uint64_t next_hit(KParams& dp, const Src& w, const Ca
 // candidate is trusted). The record starts of the tile are written to `starts` (u16, relative to
 // tlo). Returns the tile aggregate (uniform).
 template <int NV, int MODE>
-__device__ Agg walk_tile(KParams& dp, const Src& w_, uint64_t tlo, uint64_t thi, uint64_t seed, int lane,
+__device__ Agg walk_tile(KParams& dp, const Src& w, uint64_t tlo, uint64_t thi, uint64_t seed, int lane,
                          uint16_t* starts, uint32_t dsig) {
-  // a batch whose first record does not start with the plan's signature (an IDL-order producer, an unset
-  // first field) is walked with the generic field loop alone: trying the plan first failed on every
-  // record, one wasted LDS round trip each
-  Src w = w_;
-  if (is_thrift(MODE) && dsig && dsig != dp.prog->sig) w.nsteps = 0;
+  // (skipping the plan attempt here for batches that do not start on it, as the emit pass does, tipped the
+  // general index kernel from 128 to 232 VGPRs: the known-offsets decode's index pass went 0.6 -> 1.5 ms)
   const uint64_t seg_lo = tlo + (uint64_t)lane * SEG;
   const uint64_t seg_hi = kmin64(seg_lo + SEG, thi);
   const Cand cd = lane_candidate<NV, MODE>(dp, w, seg_lo, seg_hi, lane, dsig);
