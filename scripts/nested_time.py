@@ -19,8 +19,12 @@ doc = idl.parse_idl(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath
 sch = idl.to_schema(doc.struct("Nesting"))
 cdc = ThriftCodec(sch)
 ds = cdc.dschema
-one = np.frombuffer(b"".join(synth.thrift_records(sch, k, seed=7)), dtype=np.uint8).copy()
-wire = torch.from_numpy(one).to(dev).repeat(n // k)
+if os.environ.get("NEST_FILE"):   # n distinct records from a file (scripts/r5sort_gpu.sh)
+    wire = torch.from_numpy(np.fromfile(os.environ["NEST_FILE"], dtype=np.uint8)).to(dev)
+    k = n
+else:
+    one = np.frombuffer(b"".join(synth.thrift_records(sch, k, seed=7)), dtype=np.uint8).copy()
+    wire = torch.from_numpy(one).to(dev).repeat(n // k)
 offs = None
 units = cdc.DecodeSizes(wire, n)
 vc, ec, sc = units[0::3], units[1::3], units[2::3]
