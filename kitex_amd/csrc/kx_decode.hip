@@ -3824,8 +3824,11 @@ __global__ void __launch_bounds__(64) split_kernel(DecParams dp_) {
   dp.split_out[k] = pos;
 }
 
+#ifndef KX_EMIT_WPS
+#define KX_EMIT_WPS 4   // A/B knob: emit_kernel waves per SIMD (4: <= 128 VGPRs)
+#endif
 template <int NV, int MODE, bool COOP = false>
-__global__ void __launch_bounds__(NT, 4) emit_kernel(DecParams dp_) {  // 4 waves per SIMD: <= 128 VGPRs
+__global__ void __launch_bounds__(NT, KX_EMIT_WPS) emit_kernel(DecParams dp_) {
   KParams& dp = KX_PARAMS();
   (void)dp_;
   __shared__ __attribute__((aligned(16))) uint32_t WIN[WAVES][WINW];
