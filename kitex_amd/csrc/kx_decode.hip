@@ -828,8 +828,9 @@ __device__ __forceinline__ void emit_defaults(const KAS KxProgram* P, const KAS 
 // protowire.ConsumeVarint of the varint starting at byte 0 of f: at most 10 bytes, the 10th <= 1;
 // `rem` bytes are available. Branch-free SWAR: the terminator is the first byte with bit 7 clear,
 // the 7-bit groups of the first 8 bytes are compacted in three shift/mask steps.
+template <bool EARLY = true>
 __device__ __forceinline__ int pb_varint_f(const Fetch& f, uint64_t rem, uint64_t& v, uint32_t& used) {
-  if (!(f.w0 & 0x80u)) {  // one byte: tags, lengths < 128, small values (usually wave-uniform)
+  if (EARLY && !(f.w0 & 0x80u)) {  // one byte: tags, lengths < 128, small values (usually wave-uniform)
     if (rem < 1) return KX_ERR_EOF;
     v = f.w0 & 0x7fu;
     used = 1;
@@ -1027,10 +1028,82 @@ __device__ __forceinline__ int pb_body(const Src& w, const KAS KxProgram* P, con
 // False when the record has anything else left at the end (unknown or out-of-order fields, a
 // repeated field, a malformed value): the generic field loop then decodes it from the start and
 // reports the error.
+#ifndef KX_PB_NOEARLY
+#define KX_PB_NOEARLY 1   // A/B knob: plan varint values decoded without the one-byte early exit
+#endif
+// The same plan over a record that lies in the LDS window with 16 bytes to spare (the usual case): positions
+// are 32-bit window offsets, every fetch is four LDS reads with no window test and no global-memory branch.
+template <int NV>
+__device__ __forceinline__ bool pb_canon_lds(const Src& w, const KAS KxProgram* P, const KAS KxLaunchCols& cols,
+                                             uint64_t start, uint32_t q0, uint32_t qlim, uint64_t rec, bool emit,
+                                             bool utf8, VarState<NV>& vs, uint64_t& pres_out) {
+  uint32_t q = q0;
+  uint64_t pres = 0;
+  const uint32_t ns = P->npbsteps;
+  for (uint32_t k = 0; k < ns; k++) {
+    const KxpStep S = ldk(&P->pbsteps[k]);
+    const uint32_t tl = (S.hdr >> 16) & 3u;
+    bool present = false;
+    if (q < qlim) {
+      const LDS uint32_t* sw = w.win + (q >> 2);
+      const uint32_t sh = q & 3;
+      const uint32_t x0 = sw[0], x1 = sw[1], x2 = sw[2], x3 = sw[3];
+      Fetch f;
+      f.w0 = __builtin_amdgcn_alignbyte(x1, x0, sh);
+      f.w1 = __builtin_amdgcn_alignbyte(x2, x1, sh);
+      f.w2 = __builtin_amdgcn_alignbyte(x3, x2, sh);
+      present = (f.w0 & (tl == 1 ? 0xffu : 0xffffu)) == (S.hdr & 0xffffu) && qlim - q > tl;
+      if (present) {
+        const uint32_t rem = qlim - q - tl;
+        const Fetch fv = fetch_skip(f, tl);
+        uint64_t v;
+        uint32_t u;
+        if (S.kind == KXP_S_PB_VARINT) {
+          if (!emit) {
+            if (pb_varint_len_f(fv, rem, u)) return false;
+          } else {
+            // values of any length: the one-byte early exit would split the wave (both paths run)
+            if (pb_varint_f<!KX_PB_NOEARLY>(fv, rem, v, u)) return false;
+            if ((S.hdr >> 24) & 1u) v = v != 0;
+            store_col(cols.data[S.col], S.width, rec, v);
+          }
+          q += tl + u;
+        } else if (S.kind == KXP_S_PB_FIXED64) {
+          if (rem < 8) return false;
+          if (emit) store_col(cols.data[S.col], S.width, rec, (uint64_t)fv.w0 | ((uint64_t)fv.w1 << 32));
+          q += tl + 8;
+        } else {
+          if (pb_varint_f(fv, rem, v, u) || v > rem - u) return false;
+          const uint32_t b = q + tl + u;
+          const uint64_t pb = start + (b - q0);
+          if (utf8 && !((S.hdr >> 25) & 1u) && !pb_utf8_ok(w, pb, v)) return false;
+          vset<NV>(vs, S.vslot, pb, (uint32_t)v);
+          q = b + (uint32_t)v;
+        }
+        const int pbit = (int)(S.kind == KXP_S_PB_LEN ? S.width : S.vslot) - 1;  // kx_schema.cpp
+        if (pbit >= 0) pres |= 1ull << pbit;
+      }
+    }
+    if (!present && emit && S.kind != KXP_S_PB_LEN)
+      store_col(cols.data[S.col], S.width, rec, (uint64_t)ld_col(P, S.col).defv);
+  }
+  if (q != qlim) return false;
+  pres_out = pres;
+  return true;
+}
+
 template <int NV>
 __device__ __forceinline__ bool pb_canon(const Src& w, const KAS KxProgram* P, const KAS KxLaunchCols& cols,
                                          uint64_t start, uint64_t limit, uint64_t rec, bool emit, bool utf8,
                                          VarState<NV>& vs, uint64_t& pres_out) {
+#ifndef KX_PB_LDS
+#define KX_PB_LDS 1   // A/B knob: the window-offset walk above
+#endif
+  if (KX_PB_LDS && limit >= start && limit - start <= 65536) {
+    const int32_t q0 = wofs(w, start, (uint32_t)(limit - start) + 16);
+    if (q0 >= 0) return pb_canon_lds<NV>(w, P, cols, start, (uint32_t)q0, (uint32_t)q0 + (uint32_t)(limit - start),
+                                         rec, emit, utf8, vs, pres_out);
+  }
   uint64_t pos = start, pres = 0;
   const uint32_t ns = P->npbsteps;
   for (uint32_t k = 0; k < ns; k++) {
