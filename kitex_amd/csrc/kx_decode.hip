@@ -1252,6 +1252,21 @@ __device__ __forceinline__ void copy_var(const Src& w, const KxpCol& K, uint64_t
 // ---------------------------------------------------------------------------------------------
 // wave helpers
 // ---------------------------------------------------------------------------------------------
+#ifndef KX_SCAN32
+#define KX_SCAN32 1   // A/B knob: emit_tile's arena scan with DPP moves when the wave's lengths allow
+#endif
+// Inclusive scan of 32-bit values over the wave with DPP moves (row shifts, then the row broadcasts): no
+// LDS traffic, unlike the bpermute-based wave_incl_scan
+__device__ __forceinline__ uint32_t wave_incl_scan32(uint32_t v) {
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
+  return v;
+}
+
 __device__ __forceinline__ uint64_t wave_incl_scan(uint64_t v, int lane) {
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
@@ -3741,7 +3756,9 @@ __device__ __forceinline__ void emit_tile(KParams& dp, LDS uint32_t* win, uint64
     for (int v = 0; v < NV; v++) {
       if (v >= (int)P->nvar) break;
       const uint64_t x0 = act ? vs.len[v] : 0;
-      const uint64_t xi = wave_incl_scan(x0, lane);
+      uint64_t xi;
+      if (KX_SCAN32 && !__ballot(x0 >= (1u << 26))) xi = wave_incl_scan32((uint32_t)x0);   // 64 lengths < 2^26: the sum fits
+      else xi = wave_incl_scan(x0, lane);
       atv[v] = run[v] + xi - x0;
       run[v] += rl64(xi, 63);
     }
@@ -3921,17 +3938,6 @@ __global__ void __launch_bounds__(NT, KX_EMIT_WPS) emit_kernel(DecParams dp_) {
 }
 
 // ---- kernel 3, fast form ----
-// Inclusive scan of 32-bit values over the wave with DPP moves (row shifts, then the row broadcasts): no
-// LDS traffic, unlike the bpermute-based wave_incl_scan
-__device__ __forceinline__ uint32_t wave_incl_scan32(uint32_t v) {
-  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
-  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
-  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
-  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
-  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
-  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
-  return v;
-}
 
 // n string bytes at window offset x -> dst (global): head bytes up to a dword-aligned destination, then
 // 16-byte stores assembled from 5 window dwords, then a dword / byte tail. The bytes lie in the window (a

@@ -33,8 +33,13 @@ def lib():
                                                 "kx_schema.cpp", "kx_internal.h")] + \
             [os.path.join(HERE, f) for f in ("emu_driver.cpp", "emu_rt.cpp", "nested_host.cpp",
                                              os.path.join("hip", "hip_runtime.h"))]
-        if not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(f) for f in srcs):
-            build()
+        import fcntl
+        os.makedirs(os.path.join(HERE, OUT), exist_ok=True)
+        # one build at a time (pytest -n workers share the build directory); the check is repeated under the lock
+        with open(os.path.join(HERE, OUT, ".lock"), "w") as lk:
+            fcntl.flock(lk, fcntl.LOCK_EX)
+            if not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(f) for f in srcs):
+                build()
         _lib = C.CDLL(LIB)
         _lib.emu_decode.restype = C.c_int
         _lib.emu_decode.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64,
