@@ -64,7 +64,8 @@
 extern "C" {
 #endif
 
-#define KX_ABI_VERSION 6  /* 6: shard concatenation (kx_shard_meta, kx_concat_plan, kx_concat_rebase);
+#define KX_ABI_VERSION 7  /* 7: the kx_host_* entries take every schema and report per-record codes
+                             (record_status); 6: shard concatenation (kx_shard_meta, kx_concat_plan, kx_concat_rebase);
                              5: kx_status.var_total holds 16 var slots; kx_thrift_split_points */
 
 /* ---- Thrift TType ids (gopkg protocol/thrift; pinned by pkg/protocol/bthrift/binary_test.go) ---- */
@@ -443,29 +444,42 @@ int kx_pb_encode_batch(kx_ctx* c, const kx_schema* s, const kx_columns* in, uint
                        uint8_t* out, uint64_t out_cap, uint64_t* offsets_out,
                        kx_status* status, void* stream);
 
-/* ---- host-memory entry point (the netpoll buffer side) ----
- * in / out columns / status are HOST memory (pinned for full PCIe rate, or pageable). Synchronous.
- * With offsets (each message's length known from its framing) the batch is a pipeline of 16
- * record-range chunks over three streams of the ctx: H2D, decode and D2H of different chunks
- * overlap. Without offsets: H2D, decode, D2H in sequence. */
+/* ---- host-memory entry points (the netpoll buffer side) ----
+ * in / out columns / record_status / status are HOST memory (pinned for full PCIe rate, or pageable).
+ * Synchronous: every copy has completed when the call returns, on success and on error.
+ * Every schema the device entry points take: flat columns of every kind (FIXED, BYTES, LIST, LIST_BYTES:
+ * MockReq's map<string,string> and list<string>, k-mock.go:39-114; base.Base's Extra map), nested Thrift
+ * schemas and nested Kitex-Protobuf messages (the record walker; LIST2 / LIST2_BYTES columns). A column's
+ * capacities (capacity, elem_capacity, sub_capacity) are the units its host arrays hold; the device decides
+ * the arena positions and only the units the records fill are copied back (status->var_total, a nested
+ * schema's cursor totals); an arena too small is KX_ERR_SIZE_LIMIT.
+ * With offsets (each message's length known from its framing) and n >= 64 Ki the batch is a pipeline of
+ * 16 record-range chunks over three streams of the ctx: the H2D, the decode and the D2H of different chunks
+ * overlap, each chunk continuing the previous one's arenas on the device. Without offsets: H2D, decode, D2H.
+ * record_status (optional, n bytes): each record's code. With offsets every record is decoded on its own
+ * (fastUnmarshal, codec_fast.go:62-71: a failing message fails alone, the others decode), so a caller can
+ * fall back per message; status is the first failing record's (record = its index). Without offsets the
+ * records from the failing one on carry its code. */
 int kx_host_decode_batch(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len,
-                         const uint64_t* offsets, uint64_t n, const kx_columns* out,
+                         const uint64_t* offsets, uint64_t n, const kx_columns* out, uint8_t* record_status,
                          kx_status* status);
 /* The same for Kitex-Protobuf bodies (offsets semantics as kx_pb_decode_batch). */
 int kx_host_pb_decode_batch(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len,
-                            const uint64_t* offsets, uint64_t n, const kx_columns* out,
+                            const uint64_t* offsets, uint64_t n, const kx_columns* out, uint8_t* record_status,
                             kx_status* status);
 /* fastMarshal from host memory (codec_fast.go:40-58 / thrift.go:106-160, the reply path): n records'
- * columns (HOST memory, pinned for full PCIe rate; FIXED / BYTES / LIST / LIST_BYTES columns of a flat
- * schema, no views) -> out[0 ..) (host) the records back to back, as kx_thrift_encode_batch writes
- * them; offsets_out (host, n + 1, optional) each record's start; status (host) consumed = total bytes,
- * SIZE_LIMIT when out_cap is too small (out then holds no complete batch). Synchronous. With n >= 64 Ki
- * a pipeline of 16 record-range chunks: the H2D of the columns, the encode and the D2H of the wire of
- * different chunks overlap. kx_host_pb_encode_batch: the Kitex-Protobuf Batch body (kx_pb_encode_batch). */
+ * columns (HOST memory, pinned for full PCIe rate; flat or nested schemas, no views; elem_capacity /
+ * sub_capacity = the entries - 1 their arrays hold) -> out[0 ..) (host) the records back to back, as
+ * kx_thrift_encode_batch writes them; offsets_out (host, n + 1, optional) each record's start; status (host):
+ * consumed = total bytes. SIZE_LIMIT when out_cap is too small: consumed is then the size the whole batch
+ * needs, and out holds the records of the chunks that fitted (record_status 0 for them, SIZE_LIMIT for the
+ * rest; optional, n bytes). With n >= 64 Ki a pipeline of 16 record-range chunks: the H2D of the columns,
+ * the encode and the D2H of the wire of different chunks overlap. kx_host_pb_encode_batch: the
+ * Kitex-Protobuf Batch body (kx_pb_encode_batch). */
 int kx_host_encode_batch(kx_ctx* c, const kx_schema* s, const kx_columns* in, uint64_t n, uint8_t* out,
-                         uint64_t out_cap, uint64_t* offsets_out, kx_status* status);
+                         uint64_t out_cap, uint64_t* offsets_out, uint8_t* record_status, kx_status* status);
 int kx_host_pb_encode_batch(kx_ctx* c, const kx_schema* s, const kx_columns* in, uint64_t n, uint8_t* out,
-                            uint64_t out_cap, uint64_t* offsets_out, kx_status* status);
+                            uint64_t out_cap, uint64_t* offsets_out, uint8_t* record_status, kx_status* status);
 
 /* ---- message level: N framed RPC messages (framing already removed by the transport) ----
  * message i = in[offsets[i] .. offsets[i+1]) (u64, n+1 entries, device).

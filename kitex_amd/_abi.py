@@ -6,7 +6,7 @@ layout is checked by tests/test_abi.py against the compiled library.
 """
 import ctypes as C
 
-KX_ABI_VERSION = 6
+KX_ABI_VERSION = 7
 
 # Thrift TType ids (gopkg protocol/thrift; pinned by pkg/protocol/bthrift/binary_test.go)
 T_STOP, T_VOID, T_BOOL, T_BYTE, T_DOUBLE = 0, 1, 2, 3, 4

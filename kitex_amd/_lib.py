@@ -90,9 +90,9 @@ def lib():
     L.kx_thrift_encode_batch.argtypes = [vp, vp, C.POINTER(A.Columns), u64, vp, u64, vp, vp, vp]
     L.kx_pb_encoded_size_batch.argtypes = L.kx_thrift_encoded_size_batch.argtypes
     L.kx_pb_encode_batch.argtypes = L.kx_thrift_encode_batch.argtypes
-    L.kx_host_decode_batch.argtypes = [vp, vp, vp, u64, vp, u64, C.POINTER(A.Columns), C.POINTER(A.Status)]
+    L.kx_host_decode_batch.argtypes = [vp, vp, vp, u64, vp, u64, C.POINTER(A.Columns), vp, C.POINTER(A.Status)]
     L.kx_host_pb_decode_batch.argtypes = L.kx_host_decode_batch.argtypes
-    L.kx_host_encode_batch.argtypes = [vp, vp, C.POINTER(A.Columns), u64, vp, u64, vp, C.POINTER(A.Status)]
+    L.kx_host_encode_batch.argtypes = [vp, vp, C.POINTER(A.Columns), u64, vp, u64, vp, vp, C.POINTER(A.Status)]
     L.kx_host_pb_encode_batch.argtypes = L.kx_host_encode_batch.argtypes
     L.kx_thrift_message_begin_length.argtypes = [u32]
     L.kx_thrift_message_begin_length.restype = u64

@@ -348,16 +348,20 @@ class ThriftCodec:
         return [int(units[i]) for i in range(3 * ds.ncols)]
 
     def UnmarshalHost(self, wire, n: int, offsets=None, var_caps: Sequence[int] = None,
-                      raise_on_error: bool = True, out: ColumnSet = None):
+                      raise_on_error: bool = True, out: ColumnSet = None, elem_caps: Sequence[int] = None,
+                      sub_caps: Sequence[int] = None, record_status: bool = False):
         """fastUnmarshal from host memory (netpoll buffers): numpy uint8 wire (+ uint64 offsets[n+1])
         -> host ColumnSet + status, via kx_host_decode_batch (H2D, device decode, D2H; with offsets
-        a chunked pipeline whose copies overlap the decode). Pinned buffers reach full PCIe rate."""
+        a chunked pipeline whose copies overlap the decode). Pinned buffers reach full PCIe rate.
+        Every schema: flat columns of every kind and nested schemas (var_caps / elem_caps / sub_caps: the
+        units each column's arrays hold; default: the wire size, a bound for every column kind).
+        record_status=True: returns (out, status, codes uint8[n]) with each record's own code."""
         import numpy as np
         ds = self.dschema
         if var_caps is None:
             var_caps = [0 if ci.kind == A.COL_FIXED else max(1, wire.size) for ci in ds.infos]
         if out is None:
-            out = alloc_host(ds.infos, n, var_caps, ds.npresence)
+            out = alloc_host(ds.infos, n, var_caps, ds.npresence, elem_caps=elem_caps, sub_caps=sub_caps)
         kc = to_kx_columns(out, ds.infos, var_caps)
         st = A.Status()
         wire = np.ascontiguousarray(wire, dtype=np.uint8)
@@ -365,21 +369,24 @@ class ThriftCodec:
         if offsets is not None:
             offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
             offp = offsets.ctypes.data
+        rs = np.zeros(max(1, n), dtype=np.uint8) if record_status else None
         rc = getattr(lib(), self._HOST)(self.ctx.handle, ds.handle, wire.ctypes.data if wire.size else None,
-                                        wire.size, offp, n, C.byref(kc), C.byref(st))
+                                        wire.size, offp, n, C.byref(kc), rs.ctypes.data if rs is not None else None,
+                                        C.byref(st))
         check(rc, self._HOST)
         if raise_on_error and st.code:
             raise ProtocolError(st.code, self._WHAT, st.record, st.offset)
-        return out, st
+        return (out, st, rs[:n]) if record_status else (out, st)
 
     _HOST_ENCODE = "kx_host_encode_batch"
 
-    def MarshalHost(self, cols: ColumnSet, out=None, with_offsets: bool = True, raise_on_error: bool = True):
+    def MarshalHost(self, cols: ColumnSet, out=None, with_offsets: bool = True, raise_on_error: bool = True,
+                    record_status: bool = False):
         """fastMarshal to host memory (the reply path, codec_fast.go:40-58): host ColumnSet (numpy; pinned
-        buffers reach full PCIe rate) -> (wire uint8 numpy, offsets uint64[n+1] or None, status) via
-        kx_host_encode_batch (H2D of the columns, device encode, D2H of the wire; with n >= 64 Ki a chunked
-        pipeline whose copies overlap the encode). `out`: a preallocated uint8 buffer (default: an upper
-        bound from the column sizes)."""
+        buffers reach full PCIe rate; flat or nested schemas) -> (wire uint8 numpy, offsets uint64[n+1] or
+        None, status) via kx_host_encode_batch (H2D of the columns, device encode, D2H of the wire; with
+        n >= 64 Ki a chunked pipeline whose copies overlap the encode). `out`: a preallocated uint8 buffer
+        (default: an upper bound from the column sizes). record_status=True appends each record's code."""
         import numpy as np
         ds = self.dschema
         n = cols.n
@@ -388,13 +395,16 @@ class ThriftCodec:
             out = np.empty(max(1, _host_encode_bound(cols, ds.infos, n, self._HOST_ENCODE != "kx_host_encode_batch")),
                            dtype=np.uint8)
         offs = np.empty(n + 1, dtype=np.uint64) if with_offsets else None
+        rs = np.zeros(max(1, n), dtype=np.uint8) if record_status else None
         st = A.Status()
         rc = getattr(lib(), self._HOST_ENCODE)(self.ctx.handle, ds.handle, C.byref(kc), n, out.ctypes.data, out.size,
-                                               offs.ctypes.data if offs is not None else None, C.byref(st))
+                                               offs.ctypes.data if offs is not None else None,
+                                               rs.ctypes.data if rs is not None else None, C.byref(st))
         check(rc, self._HOST_ENCODE)
         if raise_on_error and st.code:
             raise ProtocolError(st.code, self._HOST_ENCODE)
-        return out[:st.consumed], offs, st
+        wire = out[:min(st.consumed, out.size)]
+        return (wire, offs, st, rs[:n]) if record_status else (wire, offs, st)
 
     _MESSAGES = "kx_thrift_decode_messages"
     _FRAMES = "kx_thrift_decode_frames"
@@ -677,8 +687,9 @@ class ThriftCodec:
 
 def _host_encode_bound(cols: ColumnSet, infos, n: int, pb: bool) -> int:
     """an upper bound of the encoded size of host columns: per record 16 bytes per column (header, length,
-    list header, STOP / frame) plus 16 per fixed value, plus every var column's payload bytes (elements at
-    up to 10 bytes as proto varints)"""
+    list header, STOP / frame) plus 16 per fixed value, plus per var column its payload bytes and 16 bytes
+    per element of every level (headers, lengths, element STOPs; elements at up to 10 bytes as proto
+    varints)"""
     import numpy as np
     total = n * (16 * (len(infos) + 2) + 16)
     for c, ci in enumerate(infos):
@@ -686,12 +697,12 @@ def _host_encode_bound(cols: ColumnSet, infos, n: int, pb: bool) -> int:
             total += n * 16
             continue
         parts = cols.cols[c]
-        if ci.kind == A.COL_LIST_BYTES:
-            ne = int(np.asarray(parts[0])[n])
-            total += int(np.asarray(parts[1])[ne]) + 8 * ne
-        else:
-            units = int(np.asarray(parts[0])[n])
-            total += units * (max(ci.width, 10 if pb else ci.width) if ci.kind == A.COL_LIST else 1)
+        hi = n
+        for arr in parts[:-1]:            # walk the offsets chain: the units of every level
+            hi = int(np.asarray(arr)[hi])
+            total += 16 * hi
+        width = 1 if ci.kind in (A.COL_BYTES, A.COL_LIST_BYTES, A.COL_LIST2_BYTES) else ci.width
+        total += hi * (max(width, 10) if pb and width > 1 else width)
     return total
 
 

@@ -189,19 +189,10 @@ int ensure_nws(kx_ctx* c, size_t bytes, hipStream_t stream) {
   return KX_OK;
 }
 
-// the call's column table: checked on the host, staged in pinned memory, copied on the stream (the
-// staging buffer is reused once the previous copy has executed)
-int nested_cols(kx_ctx* c, const kx_schema* s, const kx_columns* cols, bool decode, hipStream_t st, KxnCols** out) {
+// the call's column table (checked on the host) in the walker's form
+int fill_ncols(const kx_schema* s, const kx_columns* cols, bool decode, KxnCols& K) {
   if (!cols || cols->ncols != s->ncols) return KX_ERR_INVALID_ARG;
   if (s->npres && !cols->presence) return KX_ERR_INVALID_ARG;
-  if (!c->ncols_dev) {
-    KX_HIP_CHECK(hipMalloc(&c->ncols_dev, sizeof(KxnCols)));
-    KX_HIP_CHECK(hipHostMalloc(&c->ncols_host, sizeof(KxnCols), hipHostMallocDefault));
-    KX_HIP_CHECK(hipEventCreateWithFlags(&c->ncols_ev, hipEventDisableTiming));
-  } else {
-    KX_HIP_CHECK(hipEventSynchronize(c->ncols_ev));
-  }
-  KxnCols& K = *(KxnCols*)c->ncols_host;
   memset(&K, 0, sizeof K);
   const KxnProgram& P = *s->nprog;
   for (uint32_t i = 0; i < s->ncols; i++) {
@@ -230,6 +221,23 @@ int nested_cols(kx_ctx* c, const kx_schema* s, const kx_columns* cols, bool deco
     K.data[i] = k.data;
   }
   K.presence = cols->presence;
+  return KX_OK;
+}
+
+// the call's column table: checked on the host, staged in pinned memory, copied on the stream (the
+// staging buffer is reused once the previous copy has executed)
+int nested_cols(kx_ctx* c, const kx_schema* s, const kx_columns* cols, bool decode, hipStream_t st, KxnCols** out) {
+  if (!cols || cols->ncols != s->ncols) return KX_ERR_INVALID_ARG;
+  if (!c->ncols_dev) {
+    KX_HIP_CHECK(hipMalloc(&c->ncols_dev, sizeof(KxnCols)));
+    KX_HIP_CHECK(hipHostMalloc(&c->ncols_host, sizeof(KxnCols), hipHostMallocDefault));
+    KX_HIP_CHECK(hipEventCreateWithFlags(&c->ncols_ev, hipEventDisableTiming));
+  } else {
+    KX_HIP_CHECK(hipEventSynchronize(c->ncols_ev));
+  }
+  KxnCols& K = *(KxnCols*)c->ncols_host;
+  int rc = fill_ncols(s, cols, decode, K);
+  if (rc) return rc;
   KX_HIP_CHECK(hipMemcpyAsync(c->ncols_dev, &K, sizeof K, hipMemcpyHostToDevice, st));
   KX_HIP_CHECK(hipEventRecord(c->ncols_ev, st));
   *out = (KxnCols*)c->ncols_dev;
@@ -237,10 +245,13 @@ int nested_cols(kx_ctx* c, const kx_schema* s, const kx_columns* cols, bool deco
 }
 
 // decode of a nested schema (offsets / ends as kx_launch_decode; offsets == NULL: concatenated).
-// totals: sizes only (host, ncur entries; synchronous)
+// totals: sizes only (host, ncur entries; synchronous). dcols_in: a column table already on the device
+// (the host pipelines upload one per chunk); cur_base / totals_dev: a record-range chunk continues the
+// arenas of the previous one (device, ncur entries each)
 int nested_decode(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len, const uint64_t* offsets,
                   const uint64_t* ends, uint64_t n, const kx_columns* out, uint8_t* record_status, kx_status* status,
-                  hipStream_t st, uint64_t* totals) {
+                  hipStream_t st, uint64_t* totals, const KxnCols* dcols_in = nullptr,
+                  const uint64_t* cur_base = nullptr, uint64_t* totals_dev = nullptr) {
   int rc;
   KxnCols* dcols = nullptr;
   if (n == 0) {  // no record: empty offsets arrays (a single 0 entry each)
@@ -265,6 +276,8 @@ int nested_decode(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_
       KX_HIP_CHECK(hipMemsetAsync(c->ncols_dev, 0, sizeof(KxnCols), st));
     }
     dcols = (KxnCols*)c->ncols_dev;
+  } else if (dcols_in) {
+    dcols = const_cast<KxnCols*>(dcols_in);
   } else if ((rc = nested_cols(c, s, out, true, st, &dcols))) {
     return rc;
   }
@@ -274,20 +287,21 @@ int nested_decode(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_
   uint64_t epoch = 0;
   if (!offsets && (rc = ensure_ws(c, kx_skip_ws_bytes(in_len, n), st, &epoch))) return rc;
   return kx_launch_nested_decode(dp, *s->nprog, in, in_len, offsets, ends, n, dcols, record_status, status, c->nws,
-                                 c->nws_size, c->ws, c->ws_size, epoch, st, totals);
+                                 c->nws_size, c->ws, c->ws_size, epoch, st, totals, cur_base, totals_dev);
 }
 
 int nested_encode(kx_ctx* c, const kx_schema* s, const kx_columns* in, uint64_t n, uint8_t* out, uint64_t out_cap,
-                  uint64_t* sizes_out, uint64_t* offsets_out, kx_status* status, hipStream_t st, bool sizes_only) {
+                  uint64_t* sizes_out, uint64_t* offsets_out, kx_status* status, hipStream_t st, bool sizes_only,
+                  const KxnCols* dcols_in = nullptr, const uint64_t* out_base = nullptr) {
   int rc;
-  KxnCols* dcols = nullptr;
-  if ((rc = nested_cols(c, s, in, false, st, &dcols))) return rc;
+  KxnCols* dcols = const_cast<KxnCols*>(dcols_in);
+  if (!dcols && (rc = nested_cols(c, s, in, false, st, &dcols))) return rc;
   if (n == 0) return KX_OK;
   KxnProgram* dp = nullptr;
   if ((rc = nprog_on_device(const_cast<kx_schema*>(s), c->device, &dp))) return rc;
   if ((rc = ensure_ews(c, kx_nested_enc_ws_bytes(n), st))) return rc;
   return kx_launch_nested_encode(dp, *s->nprog, dcols, n, out, out_cap, sizes_out, offsets_out, status, c->ews,
-                                 c->ews_size, st, sizes_only);
+                                 c->ews_size, st, sizes_only, out_base);
 }
 
 }  // namespace
@@ -429,6 +443,8 @@ void kx_ctx_destroy(kx_ctx* c) {
     if (c->hev_st[k]) (void)hipEventDestroy(c->hev_st[k]);
   }
   if (c->hst) (void)hipHostFree(c->hst);
+  if (c->htot) (void)hipHostFree(c->htot);
+  if (c->hcols) (void)hipHostFree(c->hcols);
   delete c;
 }
 
@@ -1115,13 +1131,10 @@ int kx_pb_encode_batch(kx_ctx* c, const kx_schema* s, const kx_columns* in, uint
                           st, false, true);
 }
 
-// fastUnmarshal from host (netpoll) memory: H2D of the wire bytes (+ offsets) into a grow-only
-// device staging area, the device decode, then D2H of exactly the decoded bytes (fixed columns,
-// var offsets, var payloads up to their totals, presence) and the status. One stream, synchronous.
-// device decode of one batch (thrift or protobuf body), arena positions starting at var_base
+// device decode of one batch (thrift or protobuf body, flat schema), arena positions starting at var_base
 static int decode_device(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len, const uint64_t* offsets,
-                         uint64_t n, const kx_columns* out, kx_status* status, hipStream_t st, bool pb,
-                         const uint64_t* var_base, const uint64_t* var_base_dev = nullptr) {
+                         uint64_t n, const kx_columns* out, uint8_t* record_status, kx_status* status, hipStream_t st,
+                         bool pb, const uint64_t* var_base_dev) {
   KxLaunchCols lc;
   int rc = to_launch_cols(s, out, &lc);
   if (rc) return rc;
@@ -1131,18 +1144,24 @@ static int decode_device(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint6
   uint64_t epoch = 0;
   if ((rc = ensure_ws(c, kx_decode_ws_bytes(s->prog, in_len, offsets, n), st, &epoch))) return rc;
   if ((rc = ensure_pipe(c))) return rc;
-  return kx_launch_decode(dp, s->prog, in, in_len, offsets, n, lc, nullptr, status, c->ws, c->ws_size, epoch, st, pb,
-                          nullptr, var_base, &c->pipe, var_base_dev);
+  return kx_launch_decode(dp, s->prog, in, in_len, offsets, n, lc, record_status, status, c->ws, c->ws_size, epoch, st,
+                          pb, nullptr, nullptr, &c->pipe, var_base_dev);
 }
 
-// the host pipelines' events (a ring of KX_HOST_CH per kind) and pinned status staging, created once per ctx
-static int ensure_host_events(kx_ctx* c) {
+// the host pipelines' streams, events (a ring of KX_HOST_CH per kind) and pinned staging (per-chunk status,
+// per-chunk unit totals, per-chunk nested column tables), created once per ctx
+static int ensure_host(kx_ctx* c) {
+  if (!c->own_stream) KX_HIP_CHECK(hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking));
+  if (!c->h2d_stream) KX_HIP_CHECK(hipStreamCreateWithFlags(&c->h2d_stream, hipStreamNonBlocking));
+  if (!c->d2h_stream) KX_HIP_CHECK(hipStreamCreateWithFlags(&c->d2h_stream, hipStreamNonBlocking));
   if (c->hst) return KX_OK;
   for (int k = 0; k < KX_HOST_CH; k++) {
     KX_HIP_CHECK(hipEventCreateWithFlags(&c->hev_in[k], hipEventDisableTiming));
     KX_HIP_CHECK(hipEventCreateWithFlags(&c->hev_run[k], hipEventDisableTiming));
     KX_HIP_CHECK(hipEventCreateWithFlags(&c->hev_st[k], hipEventDisableTiming));
   }
+  KX_HIP_CHECK(hipHostMalloc((void**)&c->htot, KX_HOST_CH * KXN_MAX_CUR * sizeof(uint64_t), hipHostMallocDefault));
+  KX_HIP_CHECK(hipHostMalloc((void**)&c->hcols, KX_HOST_CH * sizeof(KxnCols), hipHostMallocDefault));
   KX_HIP_CHECK(hipHostMalloc((void**)&c->hst, KX_HOST_CH * sizeof(kx_status), hipHostMallocDefault));
   return KX_OK;
 }
@@ -1152,290 +1171,402 @@ static inline uint64_t host_off(const void* p, uint32_t ob, uint64_t i) {
   return ob == 8 ? ((const uint64_t*)p)[i] : ((const uint32_t*)p)[i];
 }
 
-// fastUnmarshal end to end from host (netpoll) memory. With message offsets (the RPC case: framing
-// gives every message's length) the batch runs as a pipeline of record-range chunks over three
-// streams: H2D of chunk k+1, decode of chunk k and D2H of chunk k-1 overlap (PCIe is full duplex).
-// The input lands at its own offsets in one device buffer, so a chunk decodes with the caller's
-// offsets as they are; each chunk's arena continues where the previous one ended (var_base), which
-// the host learns from the previous chunk's status before launching the next decode. Without
-// offsets the record boundaries are only known after the decode: H2D, decode, D2H in sequence.
-static int host_decode(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len, const uint64_t* offsets,
-                       uint64_t n, const kx_columns* out, kx_status* status, bool pb) {
-  if (!c || !s || !status || !out || (!in && in_len)) return KX_ERR_INVALID_ARG;
-  if (out->ncols != s->ncols) return KX_ERR_INVALID_ARG;
-  int rc = set_device(c);
-  if (rc) return rc;
-  if (!c->own_stream) KX_HIP_CHECK(hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking));
-  if (!c->h2d_stream) KX_HIP_CHECK(hipStreamCreateWithFlags(&c->h2d_stream, hipStreamNonBlocking));
-  if (!c->d2h_stream) KX_HIP_CHECK(hipStreamCreateWithFlags(&c->d2h_stream, hipStreamNonBlocking));
-  hipStream_t st = c->own_stream, sh = c->h2d_stream, sd = c->d2h_stream;
-  const uint32_t K = offsets && n >= (1u << 16) ? (uint32_t)KX_HOST_CH : 1u;  // chunks
+// What the host pipelines copy of one column: its offsets arrays (array 0 = record offsets, n + 1
+// entries; array j >= 1 indexed by the element domain array j - 1 points into) and its data units. key[j]
+// names the running total (a flat schema's var slot, a nested schema's cursor) that counts array j's
+// entries past the first, dkey the one that counts data units (-1: one value per record).
+struct HostCol {
+  uint32_t narr;   // offsets arrays (0: FIXED)
+  uint32_t unit;   // bytes per data unit
+  int key[3];
+  int dkey;
+};
+
+static void host_plan(const kx_schema* s, HostCol* hc) {
+  for (uint32_t c = 0; c < s->ncols; c++) {
+    HostCol& h = hc[c];
+    h.key[0] = h.key[1] = h.key[2] = -1;
+    if (s->nprog) {
+      const KxnCol& K = s->nprog->col[c];
+      h.narr = K.narr;
+      h.unit = K.width ? K.width : 1;
+      for (int j = 1; j < K.narr && j < 3; j++) h.key[j] = K.acur[j - 1];
+      h.dkey = K.dcur;
+      continue;
+    }
+    const KxpCol& K = s->prog.col[c];
+    const uint32_t kind = s->info[c].kind;
+    h.unit = kind == KX_COL_BYTES || kind == KX_COL_LIST_BYTES ? 1u : s->info[c].width;
+    h.narr = kind == KX_COL_FIXED ? 0u : kind == KX_COL_LIST_BYTES ? 2u : 1u;
+    h.dkey = kind == KX_COL_FIXED ? -1 : kind == KX_COL_LIST_BYTES ? (int)K.vslot2 : (int)K.vslot;
+    if (kind == KX_COL_LIST_BYTES) h.key[1] = K.vslot;
+  }
+}
+
+static inline void* host_arr(const kx_column& k, int j) {
+  return j == 0 ? k.offsets : j == 1 ? k.elem_offsets : k.sub_offsets;
+}
+static inline uint64_t host_arr_cap(const kx_column& k, int j, uint64_t n) {   // entries - 1
+  return j == 0 ? n : j == 1 ? k.elem_capacity : k.sub_capacity;
+}
+static inline void set_arr(kx_column& k, int j, void* p, uint64_t cap) {
+  if (j == 0) k.offsets = p;
+  else if (j == 1) { k.elem_offsets = p; k.elem_capacity = cap; }
+  else { k.sub_offsets = p; k.sub_capacity = cap; }
+}
+
+// the host columns of a host pipeline: no views, every array its column kind needs
+static int check_host_cols(const kx_schema* s, const HostCol* hc, const kx_columns* cols) {
+  if (cols->ncols != s->ncols || (s->npres && !cols->presence)) return KX_ERR_INVALID_ARG;
+  for (uint32_t k = 0; k < s->ncols; k++) {
+    const kx_column& col = cols->cols[k];
+    if (col.flags) return KX_ERR_INVALID_ARG;   // views: device-resident inputs only
+    if (!hc[k].narr) {
+      if (!col.data) return KX_ERR_INVALID_ARG;
+      continue;
+    }
+    if (!offset_width(col) || (!col.data && col.capacity)) return KX_ERR_INVALID_ARG;
+    for (uint32_t j = 0; j < hc[k].narr; j++)
+      if (!host_arr(col, (int)j)) return KX_ERR_INVALID_ARG;
+  }
+  return KX_OK;
+}
+
+// Column staging in the device area at p (advanced): the same shape as the host columns, arrays sized
+// to their capacities (decode) or to the units the host columns hold (encode: units[k][j], data at j = narr)
+static void stage_cols(const kx_schema* s, const HostCol* hc, const kx_columns* host, uint64_t n,
+                       const uint64_t (*units)[4], char** p, kx_columns* dc) {
   auto al = [](uint64_t x) { return (x + 255) & ~255ull; };
-  // staging layout: K statuses | input | offsets | columns (fixed data, var offsets + arenas) | presence
-  uint64_t need = al(K * sizeof(kx_status)) + al(in_len) + (offsets ? al((n + 1) * 8) : 0);
+  memset(dc, 0, sizeof *dc);
+  dc->ncols = s->ncols;
   for (uint32_t k = 0; k < s->ncols; k++) {
-    const kx_column_info& ci = s->info[k];
-    if (ci.kind == KX_COL_FIXED) need += al(n * ci.width);
-    else need += al((n + 1) * offset_width(out->cols[k])) +
-                 al(out->cols[k].capacity * (ci.kind == KX_COL_LIST ? ci.width : 1));
+    const kx_column& col = host->cols[k];
+    kx_column& d = dc->cols[k];
+    if (!hc[k].narr) {
+      d.data = *p;
+      *p += al(n * hc[k].unit);
+      continue;
+    }
+    const uint32_t ob = (uint32_t)offset_width(col);
+    d.offset_bytes = ob;
+    for (uint32_t j = 0; j < hc[k].narr; j++) {
+      const uint64_t cap = units ? units[k][j] : host_arr_cap(col, (int)j, n);
+      set_arr(d, (int)j, *p, cap);
+      *p += al((cap + 1) * ob);
+    }
+    d.capacity = units ? units[k][hc[k].narr] : col.capacity;
+    d.data = *p;
+    *p += al(d.capacity * hc[k].unit);
   }
-  if (s->npres) need += al(n * 8);
-  if (c->dstage_size < need) {
-    if (c->dstage) KX_HIP_CHECK(hipFree(c->dstage));
-    c->dstage = nullptr;
-    c->dstage_size = 0;
-    KX_HIP_CHECK(hipMalloc(&c->dstage, need));
-    c->dstage_size = need;
+  if (s->npres) {
+    dc->presence = (uint64_t*)*p;
+    *p += al(n * 8);
   }
-  char* p = (char*)c->dstage;
-  kx_status* d_st = (kx_status*)p; p += al(K * sizeof(kx_status));
-  uint8_t* d_in = (uint8_t*)p; p += al(in_len);
-  uint64_t* d_off = nullptr;
-  if (offsets) { d_off = (uint64_t*)p; p += al((n + 1) * 8); }
+}
+
+static uint64_t stage_bytes(const kx_schema* s, const HostCol* hc, const kx_columns* host, uint64_t n,
+                            const uint64_t (*units)[4]) {
+  char* p = nullptr;
   kx_columns dc;
-  memset(&dc, 0, sizeof dc);
-  dc.ncols = s->ncols;
-  for (uint32_t k = 0; k < s->ncols; k++) {
-    const kx_column_info& ci = s->info[k];
-    if (ci.kind == KX_COL_FIXED) {
-      dc.cols[k].data = p; p += al(n * ci.width);
-    } else {
-      dc.cols[k].offset_bytes = (uint32_t)offset_width(out->cols[k]);
-      dc.cols[k].offsets = p; p += al((n + 1) * dc.cols[k].offset_bytes);
-      dc.cols[k].data = p; p += al(out->cols[k].capacity * (ci.kind == KX_COL_LIST ? ci.width : 1));
-      dc.cols[k].capacity = out->cols[k].capacity;
-    }
-  }
-  if (s->npres) { dc.presence = (uint64_t*)p; p += al(n * 8); }
-  auto unit = [&](uint32_t k) -> uint64_t { return s->info[k].kind == KX_COL_LIST ? s->info[k].width : 1; };
+  stage_cols(s, hc, host, n, units, &p, &dc);
+  return (uint64_t)(uintptr_t)p;
+}
 
-  if (K == 1) {  // serial: H2D, decode, D2H
-    if (in_len) KX_HIP_CHECK(hipMemcpyAsync(d_in, in, in_len, hipMemcpyHostToDevice, st));
-    if (offsets) KX_HIP_CHECK(hipMemcpyAsync(d_off, offsets, (n + 1) * 8, hipMemcpyHostToDevice, st));
-    if (n == 0) {
-      KX_HIP_CHECK(hipStreamSynchronize(st));
-      memset(status, 0, sizeof *status);
-      for (uint32_t k = 0; k < s->ncols; k++)
-        if (s->info[k].kind != KX_COL_FIXED) memset(out->cols[k].offsets, 0, (size_t)offset_width(out->cols[k]));
-      return KX_OK;
-    }
-    if ((rc = decode_device(c, s, d_in, in_len, d_off, n, &dc, d_st, st, pb, nullptr))) return rc;
-    KX_HIP_CHECK(hipMemcpyAsync(status, d_st, sizeof(kx_status), hipMemcpyDeviceToHost, st));
-    for (uint32_t k = 0; k < s->ncols; k++) {
-      const kx_column_info& ci = s->info[k];
-      if (ci.kind == KX_COL_FIXED)
-        KX_HIP_CHECK(hipMemcpyAsync(out->cols[k].data, dc.cols[k].data, n * ci.width, hipMemcpyDeviceToHost, st));
-      else
-        KX_HIP_CHECK(hipMemcpyAsync(out->cols[k].offsets, dc.cols[k].offsets, (n + 1) * dc.cols[k].offset_bytes,
-                                    hipMemcpyDeviceToHost, st));
-    }
-    if (s->npres) KX_HIP_CHECK(hipMemcpyAsync(out->presence, dc.presence, n * 8, hipMemcpyDeviceToHost, st));
-    KX_HIP_CHECK(hipStreamSynchronize(st));
-    // var payloads: only the decoded units (status->var_total per var slot)
-    for (uint32_t v = 0; v < s->prog.nvar && v < KXP_NV_MAX; v++) {
-      const uint32_t k = s->prog.var_col[v];
-      const uint64_t units = status->var_total[v] < out->cols[k].capacity ? status->var_total[v] : out->cols[k].capacity;
-      if (units)
-        KX_HIP_CHECK(hipMemcpyAsync(out->cols[k].data, dc.cols[k].data, units * unit(k), hipMemcpyDeviceToHost, st));
-    }
-    KX_HIP_CHECK(hipStreamSynchronize(st));
-    return KX_OK;
+// record rows [r0, r0 + nk) of staged columns: the window a chunk's kernels see (record-indexed arrays and
+// fixed values shifted, element arrays and arenas absolute)
+static kx_columns chunk_window(const kx_schema* s, const HostCol* hc, const kx_columns& dc, uint64_t r0) {
+  kx_columns ck = dc;
+  for (uint32_t j = 0; j < s->ncols; j++) {
+    if (!hc[j].narr) ck.cols[j].data = (char*)dc.cols[j].data + r0 * hc[j].unit;
+    else ck.cols[j].offsets = (char*)dc.cols[j].offsets + r0 * dc.cols[j].offset_bytes;
   }
+  if (dc.presence) ck.presence = dc.presence + r0;
+  return ck;
+}
 
-  // ---- chunked pipeline (offsets known) ----
-  // H2D of every chunk is queued on the copy-in stream at once; decode k waits for its chunk's input and
-  // takes its arena base from chunk k - 1's status ON THE DEVICE (var_base_dev), so decode k + 1 is queued
-  // before the host reads chunk k's status: the decode stream never waits for a host round trip. The host
-  // reads each chunk's status (pinned, behind its decode on the copy-out stream) only to size the D2H of
-  // that chunk's arena range; fixed columns, offsets and presence go out behind the decode with no wait.
-  if ((rc = ensure_host_events(c))) return rc;
+static int grow_dstage(kx_ctx* c, uint64_t need) {
+  if (c->dstage_size >= need) return KX_OK;
+  if (c->dstage) KX_HIP_CHECK(hipFree(c->dstage));
+  c->dstage = nullptr;
+  c->dstage_size = 0;
+  KX_HIP_CHECK(hipMalloc(&c->dstage, need));
+  c->dstage_size = need;
+  return KX_OK;
+}
+
+// fastUnmarshal end to end from host (netpoll) memory, for every schema the device entry points take
+// (flat columns of every kind, nested Thrift and Kitex-PB schemas). With message offsets (the RPC case:
+// framing gives every message's length) and n >= 64 Ki the batch runs as a pipeline of KX_HOST_CH
+// record-range chunks over three streams: the H2D of every chunk is queued at once (each chunk's input at
+// its own offsets, so the caller's offsets work unchanged on the device); decode k waits for its chunk's
+// input and continues the arenas where chunk k - 1 ended, reading chunk k - 1's totals ON THE DEVICE (a
+// flat schema's var_total, a nested schema's cursor totals), so decode k + 1 is queued before the host
+// reads chunk k's totals; the host reads them (pinned, behind the decode on the decode stream) only to size
+// the D2H of chunk k's element and arena ranges. Without offsets: one chunk (the boundaries are found by
+// the decode). record_status (host, n bytes, optional): each record's code (known offsets: records fail
+// independently, codec_fast.go:62-71; concatenated: records from the failing one on carry its code).
+static int host_decode(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len, const uint64_t* offsets,
+                       uint64_t n, const kx_columns* out, uint8_t* record_status, kx_status* status, bool pb) {
+  if (!c || !s || !status || !out || (!in && in_len)) return KX_ERR_INVALID_ARG;
+  const bool nested = s->nprog != nullptr;
+  if (nested && (s->nprog->pb != 0) != pb) return KX_ERR_NOT_IMPLEMENTED;
+  int rc;
+  if (!nested && pb && (rc = pb_schema_ok(s))) return rc;
+  HostCol hc[KX_MAX_COLUMNS];
+  host_plan(s, hc);
+  if ((rc = check_host_cols(s, hc, out))) return rc;
+  const uint32_t K = offsets && n >= (1u << 16) ? (uint32_t)KX_HOST_CH : 1u;  // chunks
   uint64_t r[KX_HOST_CH + 1];
   for (uint32_t k = 0; k <= K; k++) r[k] = n * k / K;
-  for (uint32_t k = 0; k < K; k++)
-    if (offsets[r[k + 1]] < offsets[r[k]] || offsets[r[k + 1]] > in_len) return KX_ERR_INVALID_ARG;
-  // every chunk's input lands at its own offsets: the caller's offsets work unchanged on the device
-  KX_HIP_CHECK(hipMemcpyAsync(d_off, offsets, (n + 1) * 8, hipMemcpyHostToDevice, sh));
-  for (uint32_t k = 0; k < K; k++) {
-    const uint64_t a = offsets[r[k]], b = offsets[r[k + 1]];
-    if (b > a) KX_HIP_CHECK(hipMemcpyAsync(d_in + a, in + a, b - a, hipMemcpyHostToDevice, sh));
-    KX_HIP_CHECK(hipEventRecord(c->hev_in[k], sh));
+  if (offsets) {   // every chunk's input range, checked before anything is queued
+    if (offsets[n] > in_len || offsets[0] > offsets[n]) return KX_ERR_INVALID_ARG;
+    for (uint32_t k = 0; k < K; k++)
+      if (offsets[r[k + 1]] < offsets[r[k]]) return KX_ERR_INVALID_ARG;
+  }
+  if ((rc = set_device(c))) return rc;
+  if ((rc = ensure_host(c))) return rc;
+  hipStream_t st = c->own_stream, sh = c->h2d_stream, sd = c->d2h_stream;
+  if (n == 0) {
+    memset(status, 0, sizeof *status);
+    for (uint32_t k = 0; k < s->ncols; k++)
+      for (uint32_t j = 0; j < hc[k].narr; j++)
+        memset(host_arr(out->cols[k], (int)j), 0, (size_t)offset_width(out->cols[k]));
+    return KX_OK;
+  }
+  const uint32_t nt = nested ? s->nprog->ncur : KXP_NV_MAX;   // running totals per chunk
+  auto al = [](uint64_t x) { return (x + 255) & ~255ull; };
+  // staging: K statuses | K totals | K column tables | input | offsets | record codes | columns | presence
+  const uint64_t cols_at = al(K * sizeof(kx_status)) + al(K * KXN_MAX_CUR * 8) + (nested ? al(K * sizeof(KxnCols)) : 0);
+  const uint64_t in_at = cols_at, off_at = in_at + al(in_len), rs_at = off_at + (offsets ? al((n + 1) * 8) : 0),
+                 col_at = rs_at + al(n);
+  if ((rc = grow_dstage(c, col_at + stage_bytes(s, hc, out, n, nullptr)))) return rc;
+  char* base = (char*)c->dstage;
+  kx_status* d_st = (kx_status*)base;
+  uint64_t* d_tot = (uint64_t*)(base + al(K * sizeof(kx_status)));
+  KxnCols* d_cols = (KxnCols*)(base + al(K * sizeof(kx_status)) + al(K * KXN_MAX_CUR * 8));
+  uint8_t* d_in = (uint8_t*)(base + in_at);
+  uint64_t* d_off = offsets ? (uint64_t*)(base + off_at) : nullptr;
+  uint8_t* d_rs = (uint8_t*)(base + rs_at);
+  char* p = base + col_at;
+  kx_columns dc;
+  stage_cols(s, hc, out, n, nullptr, &p, &dc);
+  // a failure after copies are queued: drain every stream before returning (the caller may free its
+  // buffers as soon as this synchronous call returns)
+  auto fail = [&](int e) {
+    (void)hipStreamSynchronize(sh);
+    (void)hipStreamSynchronize(st);
+    (void)hipStreamSynchronize(sd);
+    return e;
+  };
+  if (nested) {   // one column table per chunk, uploaded with the input (the walker's pinned staging is per ctx)
+    KxnCols* hcols = (KxnCols*)c->hcols;
+    for (uint32_t k = 0; k < K; k++) {
+      const kx_columns ck = chunk_window(s, hc, dc, r[k]);
+      if ((rc = fill_ncols(s, &ck, true, hcols[k]))) return rc;
+    }
+    KX_HIP_CHECK(hipMemcpyAsync(d_cols, hcols, K * sizeof(KxnCols), hipMemcpyHostToDevice, sh));
+    if ((rc = ensure_nws(c, kx_nested_ws_bytes(*s->nprog, n / K + 1, offsets == nullptr), st))) return fail(rc);
+  }
+  if (offsets) {
+    KX_HIP_CHECK(hipMemcpyAsync(d_off, offsets, (n + 1) * 8, hipMemcpyHostToDevice, sh));
+    for (uint32_t k = 0; k < K; k++) {
+      const uint64_t a = offsets[r[k]], b = offsets[r[k + 1]];
+      if (b > a && hipMemcpyAsync(d_in + a, in + a, b - a, hipMemcpyHostToDevice, sh) != hipSuccess)
+        return fail(KX_ERR_HIP);
+      if (hipEventRecord(c->hev_in[k], sh) != hipSuccess) return fail(KX_ERR_HIP);
+    }
+  } else {
+    if (in_len) KX_HIP_CHECK(hipMemcpyAsync(d_in, in, in_len, hipMemcpyHostToDevice, sh));
+    KX_HIP_CHECK(hipEventRecord(c->hev_in[0], sh));
   }
   auto launch_chunk = [&](uint32_t k) -> int {
     const uint64_t r0 = r[k], nk = r[k + 1] - r[k];
-    kx_columns ck = dc;  // this chunk's window of the output columns
-    for (uint32_t j = 0; j < s->ncols; j++) {
-      const kx_column_info& ci = s->info[j];
-      if (ci.kind == KX_COL_FIXED) ck.cols[j].data = (char*)dc.cols[j].data + r0 * ci.width;
-      else ck.cols[j].offsets = (char*)dc.cols[j].offsets + r0 * dc.cols[j].offset_bytes;
-    }
-    if (dc.presence) ck.presence = dc.presence + r0;
     KX_HIP_CHECK(hipStreamWaitEvent(st, c->hev_in[k], 0));
-    int e = decode_device(c, s, d_in, in_len, d_off + r0, nk, &ck, d_st + k, st, pb, nullptr,
-                          k ? d_st[k - 1].var_total : nullptr);
+    const uint64_t* ob = offsets ? d_off + r0 : nullptr;
+    int e;
+    if (nested) {
+      e = nested_decode(c, s, d_in, in_len, ob, nullptr, nk, nullptr, d_rs + r0, d_st + k, st, nullptr, d_cols + k,
+                        k ? d_tot + (uint64_t)(k - 1) * KXN_MAX_CUR : nullptr, d_tot + (uint64_t)k * KXN_MAX_CUR);
+    } else {
+      const kx_columns ck = chunk_window(s, hc, dc, r0);
+      e = decode_device(c, s, d_in, in_len, ob, nk, &ck, offsets ? d_rs + r0 : nullptr, d_st + k, st, pb,
+                        k ? d_st[k - 1].var_total : nullptr);
+    }
     if (e) return e;
-    // the status (pinned) right behind the decode, on the decode stream: nothing is queued on the copy-out
-    // stream before it can run (streams share hardware queues: a queued wait would hold back what follows)
+    // the status and the totals (pinned) right behind the decode, on the decode stream: nothing is queued on
+    // the copy-out stream before it can run (streams share hardware queues: a queued wait would hold back
+    // what follows)
     KX_HIP_CHECK(hipMemcpyAsync(&c->hst[k], d_st + k, sizeof(kx_status), hipMemcpyDeviceToHost, st));
+    if (nested)
+      KX_HIP_CHECK(hipMemcpyAsync(c->htot + (uint64_t)k * KXN_MAX_CUR, d_tot + (uint64_t)k * KXN_MAX_CUR, nt * 8,
+                                  hipMemcpyDeviceToHost, st));
     KX_HIP_CHECK(hipEventRecord(c->hev_st[k], st));
     return KX_OK;
   };
-  auto copy_out = [&](uint32_t k) -> int {   // chunk k has been decoded: its fixed columns, offsets, presence
+  static const uint64_t zeros[KXN_MAX_CUR] = {0};
+  auto totals_of = [&](uint32_t k) -> const uint64_t* {
+    return nested ? c->htot + (uint64_t)k * KXN_MAX_CUR : c->hst[k].var_total;
+  };
+  // chunk k has been decoded: its rows of the fixed columns, record offsets, presence and record codes,
+  // and the element / arena ranges its totals span past chunk k - 1's
+  auto copy_out = [&](uint32_t k) -> int {
     const uint64_t r0 = r[k], nk = r[k + 1] - r[k];
+    const uint64_t* t0 = k ? totals_of(k - 1) : zeros;
+    const uint64_t* t1 = totals_of(k);
+    auto d2h = [&](void* h, const void* d, uint64_t bytes) -> int {
+      if (bytes) KX_HIP_CHECK(hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, sd));
+      return KX_OK;
+    };
     for (uint32_t j = 0; j < s->ncols; j++) {
-      const kx_column_info& ci = s->info[j];
-      if (ci.kind == KX_COL_FIXED) {
-        KX_HIP_CHECK(hipMemcpyAsync((char*)out->cols[j].data + r0 * ci.width, (char*)dc.cols[j].data + r0 * ci.width,
-                                    nk * ci.width, hipMemcpyDeviceToHost, sd));
-      } else {
-        const uint32_t ob = dc.cols[j].offset_bytes;
-        KX_HIP_CHECK(hipMemcpyAsync((char*)out->cols[j].offsets + r0 * ob, (char*)dc.cols[j].offsets + r0 * ob,
-                                    (nk + (k == K - 1 ? 1 : 0)) * ob, hipMemcpyDeviceToHost, sd));
+      const HostCol& h = hc[j];
+      const kx_column& o = out->cols[j];
+      const kx_column& d = dc.cols[j];
+      int e;
+      if (!h.narr) {
+        if ((e = d2h((char*)o.data + r0 * h.unit, (const char*)d.data + r0 * h.unit, nk * h.unit))) return e;
+        continue;
       }
+      const uint32_t ob = d.offset_bytes;
+      for (uint32_t a = 0; a < h.narr; a++) {   // entries [lo, hi] of array a (its closing entry included)
+        uint64_t lo = r0, hi = r0 + nk;
+        if (a) {
+          const uint64_t cap = host_arr_cap(o, (int)a, n);
+          lo = kmin64(t0[h.key[a]], cap);
+          hi = kmin64(t1[h.key[a]], cap);
+          if (hi < lo) continue;
+        }
+        if ((e = d2h((char*)host_arr(o, (int)a) + lo * ob, (const char*)host_arr(d, (int)a) + lo * ob,
+                     (hi - lo + 1) * ob)))
+          return e;
+      }
+      const uint64_t lo = kmin64(t0[h.dkey], o.capacity), hi = kmin64(t1[h.dkey], o.capacity);
+      if (hi > lo && (e = d2h((char*)o.data + lo * h.unit, (const char*)d.data + lo * h.unit, (hi - lo) * h.unit)))
+        return e;
     }
-    if (s->npres)
-      KX_HIP_CHECK(hipMemcpyAsync(out->presence + r0, dc.presence + r0, nk * 8, hipMemcpyDeviceToHost, sd));
+    if (s->npres) KX_HIP_CHECK(hipMemcpyAsync(out->presence + r0, dc.presence + r0, nk * 8, hipMemcpyDeviceToHost, sd));
+    if (record_status && offsets)
+      KX_HIP_CHECK(hipMemcpyAsync(record_status + r0, d_rs + r0, nk, hipMemcpyDeviceToHost, sd));
     return KX_OK;
   };
-  uint64_t base[KXP_NV_MAX] = {0};
   kx_status first{};
   bool failed = false;
-  // KX_HOST_SERIAL=1 (A/B, read per call): decode k + 1 is queued only after the host has read chunk k's
-  // status, the round-4 schedule
-  const char* ser = getenv("KX_HOST_SERIAL");
-  const bool serial = ser && atoi(ser);
-  if ((rc = launch_chunk(0))) return rc;
+  uint32_t fail_chunk = K;
+  if ((rc = launch_chunk(0))) return fail(rc);
   for (uint32_t k = 0; k < K; k++) {
-    if (!serial && k + 1 < K && (rc = launch_chunk(k + 1))) return rc;   // queued before chunk k's status is read
-    KX_HIP_CHECK(hipEventSynchronize(c->hev_st[k]));
-    if (serial && k + 1 < K && (rc = launch_chunk(k + 1))) return rc;
-    if ((rc = copy_out(k))) return rc;
+    if (k + 1 < K && (rc = launch_chunk(k + 1))) return fail(rc);   // queued before chunk k's status is read
+    if (hipEventSynchronize(c->hev_st[k]) != hipSuccess) return fail(KX_ERR_HIP);
+    if ((rc = copy_out(k))) return fail(rc);
     const kx_status sk = c->hst[k];
     if (sk.code && !failed) {
       failed = true;
       first = sk;
       first.record += r[k];
     }
-    // chunk k's arena range, known now: after its fixed columns on the copy-out stream
-    for (uint32_t v = 0; v < s->prog.nvar && v < KXP_NV_MAX; v++) {
-      const uint32_t j = s->prog.var_col[v];
-      const uint64_t cap = out->cols[j].capacity;
-      const uint64_t hi = sk.var_total[v] < cap ? sk.var_total[v] : cap, lo = base[v] < hi ? base[v] : hi;
-      if (hi > lo)
-        KX_HIP_CHECK(hipMemcpyAsync((char*)out->cols[j].data + lo * unit(j), (char*)dc.cols[j].data + lo * unit(j),
-                                    (hi - lo) * unit(j), hipMemcpyDeviceToHost, sd));
-      base[v] = sk.var_total[v];
-    }
-    if (k == K - 1) {
-      *status = failed ? first : sk;
-      status->n_records = n;
-      status->consumed = offsets[n];
-      for (uint32_t v = 0; v < KXP_NV_MAX; v++) status->var_total[v] = sk.var_total[v];
+    if (sk.code == KX_ERR_SIZE_LIMIT && fail_chunk == K) fail_chunk = k;
+  }
+  if (hipStreamSynchronize(sd) != hipSuccess) return fail(KX_ERR_HIP);
+  const kx_status last = c->hst[K - 1];
+  *status = failed ? first : last;
+  if (offsets) {
+    status->n_records = n;
+    status->consumed = offsets[n];
+  }
+  for (uint32_t v = 0; v < 16; v++) status->var_total[v] = last.var_total[v];
+  if (record_status) {
+    if (!offsets) {   // concatenated: the records before the failing one decoded, the rest carry its code
+      const uint64_t ok = failed ? kmin64(first.record, n) : n;
+      memset(record_status, 0, ok);
+      if (ok < n) memset(record_status + ok, first.code, n - ok);
+    } else if (fail_chunk < K) {   // an arena too small: nothing of that chunk or a later one was written
+      memset(record_status + r[fail_chunk], KX_ERR_SIZE_LIMIT, n - r[fail_chunk]);
     }
   }
-  KX_HIP_CHECK(hipStreamSynchronize(sd));
   return KX_OK;
 }
 
-// fastMarshal from host (netpoll-bound) memory: the columns go up, the wire comes back. The records are
-// cut into KX_HOST_CH chunks (n >= 64 Ki): H2D of every chunk's column slices is queued at once (fixed
-// rows, offsets rows, and the arena ranges those offsets span, all at their own positions, so the
-// caller's offsets work unchanged on the device); encode k waits for its slices and starts writing where
-// chunk k - 1 ended, which it reads from chunk k - 1's status on the device (kx_launch_encode out_base),
-// so it is queued before the host learns chunk k - 1's size; the host reads each chunk's status (pinned,
-// behind its encode) to copy that chunk's wire bytes out, while the next chunk encodes.
+// fastMarshal from host (netpoll-bound) memory: the columns go up, the wire comes back, for flat and
+// nested schemas. The records are cut into KX_HOST_CH chunks (n >= 64 Ki): H2D of every chunk's column
+// slices is queued at once (fixed rows, record offsets rows, and the element / arena ranges those offsets
+// span level by level, all at their own positions, so the caller's offsets work unchanged on the device);
+// encode k waits for its slices and starts writing where chunk k - 1 ended, which it reads from chunk k - 1's
+// status on the device (out_base), so it is queued before the host learns chunk k - 1's size; the host reads
+// each chunk's status (pinned, behind its encode) to copy that chunk's wire bytes out while the next chunk
+// encodes. Every range is checked before the first copy is queued.
 static int host_encode(kx_ctx* c, const kx_schema* s, const kx_columns* in, uint64_t n, uint8_t* out,
-                       uint64_t out_cap, uint64_t* offsets_out, kx_status* status, bool pb) {
+                       uint64_t out_cap, uint64_t* offsets_out, uint8_t* record_status, kx_status* status, bool pb) {
   if (!c || !s || !in || !status || (!out && out_cap)) return KX_ERR_INVALID_ARG;
-  if (s->nprog) return KX_ERR_NOT_IMPLEMENTED;   // nested schemas: the device entry points
-  if (in->ncols != s->ncols || (s->npres && !in->presence)) return KX_ERR_INVALID_ARG;
-  if (pb) {
-    int e = pb_schema_ok(s);
-    if (e) return e;
-  }
-  for (uint32_t k = 0; k < s->ncols; k++) {
-    const kx_column_info& ci = s->info[k];
-    const kx_column& col = in->cols[k];
-    if (col.flags) return KX_ERR_INVALID_ARG;   // views: device-resident inputs only
-    if (ci.kind == KX_COL_FIXED ? !col.data : !col.offsets || !offset_width(col)) return KX_ERR_INVALID_ARG;
-    if (ci.kind == KX_COL_LIST2 || ci.kind == KX_COL_LIST2_BYTES) return KX_ERR_NOT_IMPLEMENTED;
-    if (ci.kind == KX_COL_LIST_BYTES && !col.elem_offsets) return KX_ERR_INVALID_ARG;
-  }
-  int rc = set_device(c);
-  if (rc) return rc;
-  if (!c->own_stream) KX_HIP_CHECK(hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking));
-  if (!c->h2d_stream) KX_HIP_CHECK(hipStreamCreateWithFlags(&c->h2d_stream, hipStreamNonBlocking));
-  if (!c->d2h_stream) KX_HIP_CHECK(hipStreamCreateWithFlags(&c->d2h_stream, hipStreamNonBlocking));
-  if ((rc = ensure_host_events(c))) return rc;
-  hipStream_t st = c->own_stream, sh = c->h2d_stream, sd = c->d2h_stream;
+  const bool nested = s->nprog != nullptr;
+  if (nested && (s->nprog->pb != 0) != pb) return KX_ERR_NOT_IMPLEMENTED;
+  int rc;
+  if (!nested && pb && (rc = pb_schema_ok(s))) return rc;
+  HostCol hc[KX_MAX_COLUMNS];
+  host_plan(s, hc);
+  if ((rc = check_host_cols(s, hc, in))) return rc;
   if (n == 0) {
     memset(status, 0, sizeof *status);
     if (offsets_out) offsets_out[0] = 0;
     return KX_OK;
   }
   const uint32_t K = n >= (1u << 16) ? (uint32_t)KX_HOST_CH : 1u;
-  auto al = [](uint64_t x) { return (x + 255) & ~255ull; };
-  auto unit = [&](uint32_t k) -> uint64_t {
-    const kx_column_info& ci = s->info[k];
-    return ci.kind == KX_COL_LIST ? ci.width : 1;
-  };
-  // staging: K statuses | out | offsets_out (n + 1) | columns (fixed, offsets + arenas, elem offsets) | presence
-  uint64_t need = al(K * sizeof(kx_status)) + al(out_cap) + al((n + 1) * 8);
-  uint64_t units[KX_MAX_COLUMNS] = {0}, elems[KX_MAX_COLUMNS] = {0};
-  for (uint32_t k = 0; k < s->ncols; k++) {
-    const kx_column_info& ci = s->info[k];
-    const kx_column& col = in->cols[k];
-    if (ci.kind == KX_COL_FIXED) {
-      need += al(n * ci.width);
-      continue;
-    }
-    const uint32_t ob = (uint32_t)offset_width(col);
-    need += al((n + 1) * ob);
-    if (ci.kind == KX_COL_LIST_BYTES) {
-      elems[k] = host_off(col.offsets, ob, n);
-      units[k] = host_off(col.elem_offsets, ob, elems[k]);
-      need += al((elems[k] + 1) * ob);
-    } else {
-      units[k] = host_off(col.offsets, ob, n);
-    }
-    need += al(units[k] * unit(k));
-  }
-  if (s->npres) need += al(n * 8);
-  if (c->dstage_size < need) {
-    if (c->dstage) KX_HIP_CHECK(hipFree(c->dstage));
-    c->dstage = nullptr;
-    c->dstage_size = 0;
-    KX_HIP_CHECK(hipMalloc(&c->dstage, need));
-    c->dstage_size = need;
-  }
-  char* p = (char*)c->dstage;
-  kx_status* d_st = (kx_status*)p; p += al(K * sizeof(kx_status));
-  uint8_t* d_out = (uint8_t*)p; p += al(out_cap);
-  uint64_t* d_offs = (uint64_t*)p; p += al((n + 1) * 8);
-  kx_columns dc;
-  memset(&dc, 0, sizeof dc);
-  dc.ncols = s->ncols;
-  for (uint32_t k = 0; k < s->ncols; k++) {
-    const kx_column_info& ci = s->info[k];
-    if (ci.kind == KX_COL_FIXED) {
-      dc.cols[k].data = p; p += al(n * ci.width);
-      continue;
-    }
-    const uint32_t ob = (uint32_t)offset_width(in->cols[k]);
-    dc.cols[k].offset_bytes = ob;
-    dc.cols[k].offsets = p; p += al((n + 1) * ob);
-    if (ci.kind == KX_COL_LIST_BYTES) {
-      dc.cols[k].elem_offsets = p; p += al((elems[k] + 1) * ob);
-      dc.cols[k].elem_capacity = elems[k];
-    }
-    dc.cols[k].data = p; p += al(units[k] * unit(k));
-    dc.cols[k].capacity = units[k];
-  }
-  if (s->npres) { dc.presence = (uint64_t*)p; p += al(n * 8); }
-  KxProgram* dprog = nullptr;
-  if ((rc = prog_on_device(const_cast<kx_schema*>(s), c->device, &dprog))) return rc;
   uint64_t r[KX_HOST_CH + 1];
   for (uint32_t k = 0; k <= K; k++) r[k] = n * k / K;
-  if ((rc = ensure_ews(c, kx_encode_ws_bytes(r[1] - r[0] + 1), st))) return rc;
+  // pos[k][c][j]: where chunk boundary k falls in array j of column c (j = narr: the data units); checked
+  // monotonic and inside the arrays the host columns hold
+  static thread_local uint64_t pos[KX_HOST_CH + 1][KX_MAX_COLUMNS][4];
+  uint64_t units[KX_MAX_COLUMNS][4] = {{0}};
+  for (uint32_t j = 0; j < s->ncols; j++) {
+    const HostCol& h = hc[j];
+    const kx_column& col = in->cols[j];
+    if (!h.narr) continue;
+    const uint32_t ob = (uint32_t)offset_width(col);
+    for (uint32_t k = 0; k <= K; k++) {
+      uint64_t x = r[k];
+      pos[k][j][0] = x;
+      for (uint32_t a = 0; a < h.narr; a++) {
+        x = host_off(host_arr(col, (int)a), ob, x);
+        pos[k][j][a + 1] = x;
+        const uint64_t lim = a + 1 < h.narr ? host_arr_cap(col, (int)a + 1, n) : col.capacity;
+        if (x > lim || (k && x < pos[k - 1][j][a + 1])) return KX_ERR_INVALID_ARG;
+      }
+    }
+    units[j][0] = n;
+    for (uint32_t a = 1; a <= h.narr; a++) units[j][a] = pos[K][j][a];
+  }
+  if ((rc = set_device(c))) return rc;
+  if ((rc = ensure_host(c))) return rc;
+  hipStream_t st = c->own_stream, sh = c->h2d_stream, sd = c->d2h_stream;
+  auto al = [](uint64_t x) { return (x + 255) & ~255ull; };
+  // staging: K statuses | K column tables | out | offsets_out (n + 1) | columns | presence
+  const uint64_t tab_at = al(K * sizeof(kx_status)), out_at = tab_at + (nested ? al(K * sizeof(KxnCols)) : 0),
+                 offs_at = out_at + al(out_cap), col_at = offs_at + al((n + 1) * 8);
+  if ((rc = grow_dstage(c, col_at + stage_bytes(s, hc, in, n, units)))) return rc;
+  char* base = (char*)c->dstage;
+  kx_status* d_st = (kx_status*)base;
+  KxnCols* d_cols = (KxnCols*)(base + tab_at);
+  uint8_t* d_out = (uint8_t*)(base + out_at);
+  uint64_t* d_offs = (uint64_t*)(base + offs_at);
+  char* p = base + col_at;
+  kx_columns dc;
+  stage_cols(s, hc, in, n, units, &p, &dc);
+  auto fail = [&](int e) {
+    (void)hipStreamSynchronize(sh);
+    (void)hipStreamSynchronize(st);
+    (void)hipStreamSynchronize(sd);
+    return e;
+  };
+  KxProgram* dprog = nullptr;
+  if (!nested && (rc = prog_on_device(const_cast<kx_schema*>(s), c->device, &dprog))) return rc;
+  if (nested) {
+    KxnCols* hcols = (KxnCols*)c->hcols;
+    for (uint32_t k = 0; k < K; k++) {
+      const kx_columns ck = chunk_window(s, hc, dc, r[k]);
+      if ((rc = fill_ncols(s, &ck, false, hcols[k]))) return rc;
+    }
+    KX_HIP_CHECK(hipMemcpyAsync(d_cols, hcols, K * sizeof(KxnCols), hipMemcpyHostToDevice, sh));
+  }
+  const uint64_t chunk_max = r[1] - r[0] + 1;
+  if ((rc = ensure_ews(c, nested ? kx_nested_enc_ws_bytes(chunk_max) : kx_encode_ws_bytes(chunk_max), st)))
+    return fail(rc);
   // H2D of every chunk's slices, queued at once
   for (uint32_t k = 0; k < K; k++) {
     const uint64_t r0 = r[k], r1 = r[k + 1];
@@ -1444,107 +1575,116 @@ static int host_encode(kx_ctx* c, const kx_schema* s, const kx_columns* in, uint
       return KX_OK;
     };
     for (uint32_t j = 0; j < s->ncols; j++) {
-      const kx_column_info& ci = s->info[j];
+      const HostCol& h = hc[j];
       const kx_column& col = in->cols[j];
-      if (ci.kind == KX_COL_FIXED) {
-        if ((rc = h2d((char*)dc.cols[j].data + r0 * ci.width, (const char*)col.data + r0 * ci.width,
-                      (r1 - r0) * ci.width)))
-          return rc;
+      const kx_column& d = dc.cols[j];
+      if (!h.narr) {
+        if ((rc = h2d((char*)d.data + r0 * h.unit, (const char*)col.data + r0 * h.unit, (r1 - r0) * h.unit)))
+          return fail(rc);
         continue;
       }
-      const uint32_t ob = dc.cols[j].offset_bytes;
-      if ((rc = h2d((char*)dc.cols[j].offsets + r0 * ob, (const char*)col.offsets + r0 * ob, (r1 - r0 + 1) * ob)))
-        return rc;
-      uint64_t a = host_off(col.offsets, ob, r0), b = host_off(col.offsets, ob, r1);
-      if (b < a || b > (ci.kind == KX_COL_LIST_BYTES ? elems[j] : units[j])) return KX_ERR_INVALID_ARG;
-      if (ci.kind == KX_COL_LIST_BYTES) {
-        if ((rc = h2d((char*)dc.cols[j].elem_offsets + a * ob, (const char*)col.elem_offsets + a * ob,
-                      (b - a + 1) * ob)))
-          return rc;
-        const uint64_t ea = host_off(col.elem_offsets, ob, a), eb = host_off(col.elem_offsets, ob, b);
-        if (eb < ea || eb > units[j]) return KX_ERR_INVALID_ARG;
-        a = ea;
-        b = eb;
+      const uint32_t ob = d.offset_bytes;
+      for (uint32_t a = 0; a < h.narr; a++) {   // entries [pos_k, pos_k+1] of array a
+        const uint64_t lo = pos[k][j][a], hi = pos[k + 1][j][a];
+        if ((rc = h2d((char*)host_arr(d, (int)a) + lo * ob, (const char*)host_arr(col, (int)a) + lo * ob,
+                      (hi - lo + 1) * ob)))
+          return fail(rc);
       }
-      if ((rc = h2d((char*)dc.cols[j].data + a * unit(j), (const char*)col.data + a * unit(j), (b - a) * unit(j))))
-        return rc;
+      const uint64_t lo = pos[k][j][h.narr], hi = pos[k + 1][j][h.narr];
+      if ((rc = h2d((char*)d.data + lo * h.unit, (const char*)col.data + lo * h.unit, (hi - lo) * h.unit)))
+        return fail(rc);
     }
-    if (s->npres && (rc = h2d(dc.presence + r0, in->presence + r0, (r1 - r0) * 8))) return rc;
-    KX_HIP_CHECK(hipEventRecord(c->hev_in[k], sh));
+    if (s->npres && (rc = h2d(dc.presence + r0, in->presence + r0, (r1 - r0) * 8))) return fail(rc);
+    if (hipEventRecord(c->hev_in[k], sh) != hipSuccess) return fail(KX_ERR_HIP);
   }
   auto launch_chunk = [&](uint32_t k) -> int {
     const uint64_t r0 = r[k], nk = r[k + 1] - r[k];
-    kx_columns ck = dc;   // this chunk's rows; arenas indexed by the (absolute) offsets as they are
-    for (uint32_t j = 0; j < s->ncols; j++) {
-      const kx_column_info& ci = s->info[j];
-      if (ci.kind == KX_COL_FIXED) ck.cols[j].data = (char*)dc.cols[j].data + r0 * ci.width;
-      else ck.cols[j].offsets = (char*)dc.cols[j].offsets + r0 * dc.cols[j].offset_bytes;
-    }
-    if (dc.presence) ck.presence = dc.presence + r0;
-    KxLaunchCols lc;
-    int e = to_launch_cols(s, &ck, &lc);
-    if (e) return e;
+    const uint64_t* ob = k ? &d_st[k - 1].consumed : nullptr;
     KX_HIP_CHECK(hipStreamWaitEvent(st, c->hev_in[k], 0));
-    if ((e = kx_launch_encode(dprog, s->prog, lc, nk, d_out, out_cap, nullptr, d_offs + r0, d_st + k, c->ews,
-                              c->ews_size, st, false, pb, k ? &d_st[k - 1].consumed : nullptr)))
-      return e;
+    int e;
+    if (nested) {
+      e = nested_encode(c, s, nullptr, nk, d_out, out_cap, nullptr, d_offs + r0, d_st + k, st, false, d_cols + k, ob);
+    } else {
+      const kx_columns ck = chunk_window(s, hc, dc, r0);
+      KxLaunchCols lc;
+      if ((e = to_launch_cols(s, &ck, &lc))) return e;
+      e = kx_launch_encode(dprog, s->prog, lc, nk, d_out, out_cap, nullptr, d_offs + r0, d_st + k, c->ews, c->ews_size,
+                           st, false, pb, ob);
+    }
+    if (e) return e;
     // the status (pinned) right behind the encode on its stream (see host_decode)
     KX_HIP_CHECK(hipMemcpyAsync(&c->hst[k], d_st + k, sizeof(kx_status), hipMemcpyDeviceToHost, st));
     KX_HIP_CHECK(hipEventRecord(c->hev_st[k], st));
     return KX_OK;
   };
-  if ((rc = launch_chunk(0))) return rc;
-  uint64_t pos = 0;
+  if ((rc = launch_chunk(0))) return fail(rc);
+  uint64_t pos_out = 0;
   kx_status first{};
   bool failed = false;
+  uint32_t fail_chunk = K;
   for (uint32_t k = 0; k < K; k++) {
-    if (k + 1 < K && (rc = launch_chunk(k + 1))) return rc;   // queued before chunk k's size is known
-    KX_HIP_CHECK(hipEventSynchronize(c->hev_st[k]));
+    if (k + 1 < K && (rc = launch_chunk(k + 1))) return fail(rc);   // queued before chunk k's size is known
+    if (hipEventSynchronize(c->hev_st[k]) != hipSuccess) return fail(KX_ERR_HIP);
     const kx_status sk = c->hst[k];
-    if (offsets_out) {
-      const uint64_t r0 = r[k], nk = r[k + 1] - r[k];
-      KX_HIP_CHECK(hipMemcpyAsync(offsets_out + r0, d_offs + r0, (nk + (k == K - 1 ? 1 : 0)) * 8,
-                                  hipMemcpyDeviceToHost, sd));
-    }
     if (sk.code && !failed) {
       failed = true;
       first = sk;
+      fail_chunk = k;
     }
-    if (!failed && sk.consumed > pos) {
-      KX_HIP_CHECK(hipMemcpyAsync(out + pos, d_out + pos, sk.consumed - pos, hipMemcpyDeviceToHost, sd));
-      pos = sk.consumed;
+    if (!failed) {
+      const uint64_t r0 = r[k], nk = r[k + 1] - r[k];
+      if (offsets_out && hipMemcpyAsync(offsets_out + r0, d_offs + r0, (nk + (k == K - 1 ? 1 : 0)) * 8,
+                                        hipMemcpyDeviceToHost, sd) != hipSuccess)
+        return fail(KX_ERR_HIP);
+      if (sk.consumed > pos_out) {
+        if (hipMemcpyAsync(out + pos_out, d_out + pos_out, sk.consumed - pos_out, hipMemcpyDeviceToHost, sd) !=
+            hipSuccess)
+          return fail(KX_ERR_HIP);
+        pos_out = sk.consumed;
+      }
     }
   }
-  KX_HIP_CHECK(hipStreamSynchronize(sd));
-  KX_HIP_CHECK(hipStreamSynchronize(st));
+  if (hipStreamSynchronize(sd) != hipSuccess || hipStreamSynchronize(st) != hipSuccess) return fail(KX_ERR_HIP);
+  memset(status, 0, sizeof *status);
+  status->n_records = n;
   if (failed) {
-    *status = first;
+    // the first failing chunk's code; consumed = the size the whole batch needs (chunk bases chain on the
+    // device, so the last chunk's end is the total even past the failure), a caller retries with that
+    status->code = first.code;
+    status->record = r[fail_chunk];
+    status->offset = pos_out;
+    status->consumed = c->hst[K - 1].consumed;
   } else {
-    memset(status, 0, sizeof *status);
-    status->n_records = n;
-    status->consumed = pos;
+    status->consumed = pos_out;
+  }
+  if (record_status) {   // the records whose bytes are in `out`: 0; the rest: the failing chunk's code
+    const uint64_t ok = failed ? r[fail_chunk] : n;
+    memset(record_status, 0, ok);
+    if (ok < n) memset(record_status + ok, first.code, n - ok);
   }
   return KX_OK;
 }
 
 int kx_host_encode_batch(kx_ctx* c, const kx_schema* s, const kx_columns* in, uint64_t n, uint8_t* out,
-                         uint64_t out_cap, uint64_t* offsets_out, kx_status* status) {
-  return host_encode(c, s, in, n, out, out_cap, offsets_out, status, false);
+                         uint64_t out_cap, uint64_t* offsets_out, uint8_t* record_status, kx_status* status) {
+  return host_encode(c, s, in, n, out, out_cap, offsets_out, record_status, status, false);
 }
 
 int kx_host_pb_encode_batch(kx_ctx* c, const kx_schema* s, const kx_columns* in, uint64_t n, uint8_t* out,
-                            uint64_t out_cap, uint64_t* offsets_out, kx_status* status) {
-  return host_encode(c, s, in, n, out, out_cap, offsets_out, status, true);
+                            uint64_t out_cap, uint64_t* offsets_out, uint8_t* record_status, kx_status* status) {
+  return host_encode(c, s, in, n, out, out_cap, offsets_out, record_status, status, true);
 }
 
 int kx_host_decode_batch(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len,
-                         const uint64_t* offsets, uint64_t n, const kx_columns* out, kx_status* status) {
-  return host_decode(c, s, in, in_len, offsets, n, out, status, false);
+                         const uint64_t* offsets, uint64_t n, const kx_columns* out, uint8_t* record_status,
+                         kx_status* status) {
+  return host_decode(c, s, in, in_len, offsets, n, out, record_status, status, false);
 }
 
 int kx_host_pb_decode_batch(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint64_t in_len,
-                            const uint64_t* offsets, uint64_t n, const kx_columns* out, kx_status* status) {
-  return host_decode(c, s, in, in_len, offsets, n, out, status, true);
+                            const uint64_t* offsets, uint64_t n, const kx_columns* out, uint8_t* record_status,
+                            kx_status* status) {
+  return host_decode(c, s, in, in_len, offsets, n, out, record_status, status, true);
 }
 
 uint64_t kx_thrift_message_begin_length(uint32_t name_len) { return 12ull + name_len; }

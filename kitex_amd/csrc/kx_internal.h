@@ -86,6 +86,8 @@ struct kx_ctx {
   // kx_host_* pipelines: per chunk, input landed / kernel done / status copied out; pinned status staging
   hipEvent_t hev_in[KX_HOST_CH] = {}, hev_run[KX_HOST_CH] = {}, hev_st[KX_HOST_CH] = {};
   kx_status* hst = nullptr;
+  uint64_t* htot = nullptr;         // per chunk: the running unit totals (nested: cursor totals), pinned
+  void* hcols = nullptr;            // per chunk: the nested walker's column table (KxnCols), pinned
 };
 
 // kx_schema.cpp / kx_nested_schema.cpp
@@ -99,11 +101,13 @@ int kx_launch_nested_decode(const struct KxnProgram* dprog, const struct KxnProg
                             uint64_t in_len, const uint64_t* offsets, const uint64_t* ends, uint64_t n,
                             const KxnCols* dcols, uint8_t* record_status, kx_status* status, void* ws,
                             size_t ws_size, void* skip_ws, size_t skip_ws_size, uint64_t skip_epoch,
-                            hipStream_t stream, uint64_t* totals_out);
+                            hipStream_t stream, uint64_t* totals_out, const uint64_t* cur_base_dev = nullptr,
+                            uint64_t* totals_dev = nullptr);
 size_t kx_nested_enc_ws_bytes(uint64_t n);
 int kx_launch_nested_encode(const struct KxnProgram* dprog, const struct KxnProgram& hprog, const KxnCols* dcols,
                             uint64_t n, uint8_t* out, uint64_t out_cap, uint64_t* sizes_out, uint64_t* offsets_out,
-                            kx_status* status, void* ws, size_t ws_size, hipStream_t stream, bool sizes_only);
+                            kx_status* status, void* ws, size_t ws_size, hipStream_t stream, bool sizes_only,
+                            const uint64_t* out_base = nullptr);
 
 // device launchers (kx_decode.hip / kx_encode.hip)
 struct KxLaunchCols {            // flat schemas (<= KXP_MAX_COLS columns)

@@ -48,6 +48,9 @@ struct NParams {
   uint64_t nblk;
   uint32_t ncur;
   bool sizes_only;            // kx_thrift_decode_sizes: no column is written
+  const uint64_t* cur_base;   // (optional) every cursor starts here: a record-range chunk of a larger batch
+                              // continues the previous chunk's arenas (kx_host_* pipelines)
+  uint64_t* totals_out;       // (optional) the absolute cursor totals at the end of the call
 };
 
 // record r's extent; false when the record is not decoded at all (concat: past the failing one)
@@ -192,13 +195,14 @@ __global__ void __launch_bounds__(1024) bscan_kernel(NParams p) {
   }
   if (big) atomicOr(p.flag, 1u);   // SIZE_LIMIT: nothing is written
   uint64_t tot;
-  uint64_t run = wg_excl(acc, &tot, sh);
+  const uint64_t base = p.cur_base ? p.cur_base[k] : 0;
+  uint64_t run = base + wg_excl(acc, &tot, sh);
   for (uint64_t i = lo; i < hi; i++) {
     const uint64_t v = s[i];
     s[i] = run;
     run += v;
   }
-  if (threadIdx.x == 0) p.totals[k] = tot;
+  if (threadIdx.x == 0) p.totals[k] = base + tot;
 }
 
 // the parent domain size of column c's offsets array k
@@ -261,6 +265,9 @@ __global__ void finalize_kernel(NParams p) {
     if (threadIdx.x == 0) {
       p.status->code = KX_ERR_SIZE_LIMIT;
       p.status->n_records = 0;
+      for (int v = 0; v < 16; v++) p.status->var_total[v] = v < (int)p.ncur ? p.totals[v] : 0;
+      if (p.totals_out)   // the required sizes: a later chunk based on them fails too
+        for (uint32_t v = 0; v < p.ncur; v++) p.totals_out[v] = p.totals[v];
       *p.errkey = ~0ull;
     }
     return;
@@ -285,6 +292,8 @@ __global__ void finalize_kernel(NParams p) {
     }
   }
   for (int v = 0; v < 16; v++) st->var_total[v] = v < (int)p.ncur ? p.totals[v] : 0;
+  if (p.totals_out)
+    for (uint32_t v = 0; v < p.ncur; v++) p.totals_out[v] = p.totals[v];
   *p.errkey = ~0ull;
 }
 
@@ -300,6 +309,8 @@ struct EParams {
   uint64_t* offsets_out; // optional
   kx_status* status;
   uint64_t nblk;
+  const uint64_t* out_base;  // (optional, device) the records start here: a chunk continues the previous
+                             // chunk's output (kx_host_encode_batch pipeline, its status->consumed)
 };
 
 // encode blocks: ERB = NT records, one per thread (a workgroup per 1024 records looping over its quarters
@@ -328,7 +339,8 @@ __global__ void __launch_bounds__(1024) escan_kernel(EParams p) {
   uint64_t acc = 0;
   for (uint64_t i = lo; i < hi; i++) acc += p.bsum[i];
   uint64_t tot;
-  uint64_t run = wg_excl(acc, &tot, sh);
+  const uint64_t base = p.out_base ? *p.out_base : 0;
+  uint64_t run = base + wg_excl(acc, &tot, sh);
   for (uint64_t i = lo; i < hi; i++) {
     const uint64_t v = p.bsum[i];
     p.bsum[i] = run;
@@ -336,10 +348,11 @@ __global__ void __launch_bounds__(1024) escan_kernel(EParams p) {
   }
   if (threadIdx.x == 0) {
     kx_status* st = p.status;
+    const uint64_t end = base + tot;
     st->n_records = p.n;
-    st->consumed = tot;
-    st->code = tot > p.out_cap ? KX_ERR_SIZE_LIMIT : 0;
-    if (p.offsets_out && tot <= p.out_cap) p.offsets_out[p.n] = tot;
+    st->consumed = end;
+    st->code = end > p.out_cap ? KX_ERR_SIZE_LIMIT : 0;
+    if (p.offsets_out && end <= p.out_cap) p.offsets_out[p.n] = end;
   }
 }
 
@@ -416,7 +429,7 @@ int kx_launch_nested_decode(const KxnProgram* dprog, const KxnProgram& hprog, co
                             const uint64_t* offsets, const uint64_t* ends, uint64_t n, const KxnCols* dcols,
                             uint8_t* record_status, kx_status* status, void* ws, size_t ws_size,
                             void* skip_ws, size_t skip_ws_size, uint64_t skip_epoch, hipStream_t stream,
-                            uint64_t* totals_out) {
+                            uint64_t* totals_out, const uint64_t* cur_base_dev, uint64_t* totals_dev) {
   if (hprog.nsnap > SNAP || hprog.ncur > CUR || hprog.ncur == 0) return KX_ERR_NOT_IMPLEMENTED;
   const bool concat = offsets == nullptr;
   if (ws_size < kx_nested_ws_bytes(hprog, n, concat)) return KX_ERR_INVALID_ARG;
@@ -440,6 +453,8 @@ int kx_launch_nested_decode(const KxnProgram* dprog, const KxnProgram& hprog, co
   p.nblk = (n + RB - 1) / RB;
   p.ncur = hprog.ncur;
   p.sizes_only = totals_out != nullptr;
+  p.cur_base = cur_base_dev;
+  p.totals_out = totals_dev;
   KX_HIP_CHECK(hipMemsetAsync(status, 0, sizeof(kx_status), stream));
   KX_HIP_CHECK(hipMemsetAsync(L.errkey, 0xff, 8, stream));
   KX_HIP_CHECK(hipMemsetAsync(L.flag, 0, 4, stream));
@@ -487,7 +502,8 @@ size_t kx_nested_enc_ws_bytes(uint64_t n) { return (n + 64) * 8 + ((n + ERB - 1)
 
 int kx_launch_nested_encode(const KxnProgram* dprog, const KxnProgram& hprog, const KxnCols* dcols, uint64_t n,
                             uint8_t* out, uint64_t out_cap, uint64_t* sizes_out, uint64_t* offsets_out,
-                            kx_status* status, void* ws, size_t ws_size, hipStream_t stream, bool sizes_only) {
+                            kx_status* status, void* ws, size_t ws_size, hipStream_t stream, bool sizes_only,
+                            const uint64_t* out_base) {
   (void)hprog;
   if (ws_size < kx_nested_enc_ws_bytes(n)) return KX_ERR_INVALID_ARG;
   EParams p{};
@@ -501,6 +517,7 @@ int kx_launch_nested_encode(const KxnProgram* dprog, const KxnProgram& hprog, co
   p.sizes = sizes_out ? sizes_out : (uint64_t*)ws + ((p.nblk + 63) & ~63ull);
   p.offsets_out = offsets_out;
   p.status = status;
+  p.out_base = out_base;
   if (status) KX_HIP_CHECK(hipMemsetAsync(status, 0, sizeof(kx_status), stream));
   hipLaunchKernelGGL(esize_kernel, dim3((unsigned)p.nblk), dim3(NT), 0, stream, p);
   KX_HIP_CHECK(hipGetLastError());

@@ -487,7 +487,8 @@ def test_host_encode_bit_exact(torch, oracle, name, n):
     # too small an output: SIZE_LIMIT, reported, never a partial overrun
     small = np.zeros(exp.size // 2, dtype=np.uint8)
     _, _, st2 = cdc.MarshalHost(cs, out=small, raise_on_error=False)
-    assert st2.code == A.ERR_SIZE_LIMIT
+    # consumed = the size the whole batch needs (a caller sizes its retry from it)
+    assert st2.code == A.ERR_SIZE_LIMIT and st2.consumed == exp.size and st2.n_records == n
 
 
 @pytest.mark.parametrize("name", ["cx1", "cx2"])
