@@ -45,7 +45,7 @@ def parse():
     ap.add_argument("--no-host", action="store_true")
     ap.add_argument("--no-extra", action="store_true")
     ap.add_argument("--no-concat", action="store_true", help="N>1: skip the RCCL concatenation into rank 0")
-    ap.add_argument("--cpu-records", type=int, default=4 * 1024 * 1024)
+    ap.add_argument("--cpu-records", type=int, default=8 * 1024 * 1024)
     ap.add_argument("--dry-run", action="store_true",
                     help="launch / rendezvous check only: no GPU call, gloo between the ranks")
     return ap.parse_args()
@@ -340,6 +340,12 @@ def run_single(args, world, rank, dev, local):
     if rank == 0 and world == 1 and not args.no_host and cfg != "pf":
         note("host-inclusive paths")
         result["host_inclusive"] = host_inclusive(b, dev)
+        for shape, cnt in (("mockreq", 4 << 20), ("nesting", 1 << 20)):
+            note(f"host-inclusive {shape}")
+            try:
+                result["host_inclusive"][shape] = host_inclusive_shape(shape, cnt)
+            except Exception as e:   # never break the bench line
+                result["host_inclusive"][shape] = {"error": repr(e)}
     if world == 1 and not args.no_extra:
         result["extra"] = extras(args, b if cfg == "r2" else None, dev, local)
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -782,22 +788,72 @@ def extras(args, r2, dev, local):
     return out
 
 
+def cpu_decode_pool(sch, wire, offs, n, pb, threads, runs=5):
+    """The oracle's FastRead / proto.Unmarshal restatement (oracle/kx_oracle.c, kx_oracle_nested.c) over n
+    records with message offsets known, on a persistent pool of `threads` host threads: one record range
+    per thread, each decoded by the single-threaded restatement into its own columns, allocated once, sized
+    exactly from the range's wire bytes and pre-faulted (written once) before any timed run, so a run
+    times decode alone (no thread start, no first-touch page faults). One untimed warm-up run, then `runs`
+    timed runs. Returns (per-run seconds, all records decoded without error)."""
+    import ctypes as C
+    from concurrent.futures import ThreadPoolExecutor
+
+    import numpy as np
+
+    from kitex_amd import _abi as A
+    from kitex_amd.columns import alloc_host, to_kx_columns
+    from oracle import oracle
+    oracle.build()
+    L = oracle.lib()
+    rc, infos, npres = oracle.flatten(sch)
+    tab, ns = sch.struct_table()
+    fn = L.kxo_pb_decode if pb else L.kxo_thrift_decode
+    jobs = []
+    for t in range(threads):
+        a, b = n * t // threads, n * (t + 1) // threads
+        if a == b:
+            continue
+        base = int(offs[a])
+        so = (offs[a:b + 1] - offs[a]).astype(np.uint64)
+        nb = int(offs[b]) - base
+        caps = [0 if ci.kind == A.COL_FIXED else max(1, nb) for ci in infos]
+        out = alloc_host(infos, b - a, caps, npres, elem_caps=caps, sub_caps=caps)
+        for c in out.cols:   # pre-fault every page the decode may write
+            for x in (c if isinstance(c, tuple) else (c,)):
+                x.fill(1)
+        if out.presence is not None:
+            out.presence.fill(1)
+        kc = to_kx_columns(out, infos, caps)
+        jobs.append((wire.ctypes.data + base, nb, so, b - a, kc, A.Status(), np.ones(b - a, dtype=np.uint8), out))
+
+    def run(j):
+        d, nb, so, m, kc, st, rs, _ = j
+        return fn(tab, ns, d, nb, so.ctypes.data, m, C.byref(kc), rs.ctypes.data, C.byref(st)), st.code
+    ts = []
+    ok = True
+    with ThreadPoolExecutor(max_workers=threads) as ex:
+        list(ex.map(run, jobs))   # warm-up (pool threads started, caches and TLBs warm)
+        for _ in range(runs):
+            t0 = time.perf_counter()
+            got = list(ex.map(run, jobs))
+            ts.append(time.perf_counter() - t0)
+            ok &= all(r == 0 and c == 0 for r, c in got)
+    return ts, ok
+
+
+def spread(n, ts):
+    """records/s statistics of per-run times"""
+    rates = sorted(n / t for t in ts)
+    return {"median": rates[len(rates) // 2], "min": rates[0], "max": rates[-1], "runs": len(rates),
+            "spread": (rates[-1] - rates[0]) / rates[len(rates) // 2]}
+
+
 def nested_cpu_baseline(sch, recs, n, pb):
     """The oracle's nested decode (oracle/kx_oracle_nested.c: FastRead / proto.Unmarshal into a value tree,
-    then flattened) over n records (the k distinct ones tiled) with message offsets known, split into one
-    record range per host thread, each decoded into its own preallocated columns (ctypes releases the GIL:
-    the threads run in parallel); the concatenation of the ranges is not timed, as the GPU's is not."""
+    then flattened) over n records (the k distinct ones tiled) with message offsets known, on the persistent
+    pre-faulted pool of cpu_decode_pool; the concatenation of the ranges is not timed, as the GPU's is not."""
     try:
-        import ctypes as C
-        from concurrent.futures import ThreadPoolExecutor
-
         import numpy as np
-
-        from kitex_amd import _abi as A
-        from kitex_amd.columns import alloc_host, to_kx_columns
-        from oracle import oracle
-        oracle.build()
-        L = oracle.lib()
         threads = max(1, min(len(os.sched_getaffinity(0)), 256))
         k = len(recs)
         lens = np.array([len(r) for r in recs], dtype=np.uint64)
@@ -806,36 +862,14 @@ def nested_cpu_baseline(sch, recs, n, pb):
         wire = np.tile(one, reps)
         offs = np.zeros(n + 1, dtype=np.uint64)
         offs[1:] = np.cumsum(np.tile(lens, reps))
-        rc, infos, npres = oracle.flatten(sch)
-        tab, ns = sch.struct_table()
-        fn = L.kxo_pb_decode if pb else L.kxo_thrift_decode
-        jobs = []
-        for t in range(threads):
-            a, b = n * t // threads, n * (t + 1) // threads
-            if a == b:
-                continue
-            base = int(offs[a])
-            so = (offs[a:b + 1] - offs[a]).astype(np.uint64)
-            nb = int(offs[b]) - base
-            caps = [0 if ci.kind == A.COL_FIXED else max(1, nb) for ci in infos]
-            out = alloc_host(infos, b - a, caps, npres, elem_caps=caps, sub_caps=caps)
-            kc = to_kx_columns(out, infos, caps)
-            jobs.append((wire.ctypes.data + base, nb, so, b - a, kc, A.Status(), np.zeros(b - a, dtype=np.uint8), out))
-
-        def run(j):
-            d, nb, so, m, kc, st, rs, _ = j
-            return fn(tab, ns, d, nb, so.ctypes.data, m, C.byref(kc), rs.ctypes.data, C.byref(st)), st.code
-        best = 1e30
-        with ThreadPoolExecutor(max_workers=threads) as ex:
-            for _ in range(2):
-                t0 = time.perf_counter()
-                got = list(ex.map(run, jobs))
-                best = min(best, time.perf_counter() - t0)
-        ok = all(r == 0 and c == 0 for r, c in got)
-        return {"value": n / best, "unit": "records/s", "cores": threads, "kind": "port", "verified": ok,
+        ts, ok = cpu_decode_pool(sch, wire, offs, n, pb, threads)
+        st = spread(n, ts)
+        return {"value": st["median"], "unit": "records/s", "cores": threads, "kind": "port", "verified": ok,
+                "spread": st,
                 "sample": f"{n} records ({k} distinct, tiled), nested {'proto.Unmarshal' if pb else 'FastRead'} "
                           f"restatement (oracle/kx_oracle_nested.c) with message offsets known, one record range "
-                          f"per thread, best of 2, {threads} threads"}
+                          f"per thread of a persistent pool, pre-faulted outputs, median of {st['runs']} runs, "
+                          f"{threads} threads"}
     except Exception as e:  # never break the bench line
         return {"error": repr(e)}
 
@@ -916,22 +950,20 @@ def host_inclusive(b, dev):
         sbest = min(sbest, time.perf_counter() - t0)
     res["serial_concat"] = {"records_per_s": n / sbest, "ms": sbest * 1e3,
                             "note": "concatenated batch (no offsets): pinned H2D, decode, D2H serial on one stream"}
-    # latency of a 64 Ki-record batch (16 chunks of 4096 records): decode k + 1 queued before the host reads
-    # chunk k's status (default) vs queued after it (KX_HOST_SERIAL=1, the round-4 schedule)
-    k64 = min(n, 1 << 16)
-    sub_off = np.ascontiguousarray(off_np[:k64 + 1])
-    sub_in = wire_np[:int(sub_off[k64])]
+    # latency of a 64 Ki-record batch (16 chunks of 4096 records, decode k + 1 queued before the host reads
+    # chunk k's status) and of a 4 Ki-record batch (one chunk)
     lat = {}
-    for mode, env in (("pipelined", "0"), ("serial_host_sync", "1")):
-        os.environ["KX_HOST_SERIAL"] = env
+    for kk in (1 << 16, 1 << 12):
+        k64 = min(n, kk)
+        sub_off = np.ascontiguousarray(off_np[:k64 + 1])
+        sub_in = wire_np[:int(sub_off[k64])]
         ts = []
         for _ in range(30):
             t0 = time.perf_counter()
             b.cdc.UnmarshalHost(sub_in, k64, offsets=sub_off, var_caps=b.var_caps, out=hout, raise_on_error=False)
             ts.append(time.perf_counter() - t0)
-        lat[mode] = {"median_ms": sorted(ts)[len(ts) // 2] * 1e3, "min_ms": min(ts) * 1e3}
-    os.environ.pop("KX_HOST_SERIAL", None)
-    res["latency_64k"] = dict(lat, records=k64)
+        lat[str(k64)] = {"median_ms": sorted(ts)[len(ts) // 2] * 1e3, "min_ms": min(ts) * 1e3}
+    res["latency"] = lat
     # the reply path: kx_host_encode_batch from the pinned host columns just decoded back to a pinned wire
     h_wire = pinned(b.wire.numel(), torch.uint8).numpy()
     h_eoff = pinned(n + 1, torch.int64).numpy().view(np.uint64)
@@ -949,6 +981,108 @@ def host_inclusive(b, dev):
                      "note": "kx_host_encode_batch: pinned host columns -> pinned host wire, 16-chunk pipeline "
                              "(H2D of the columns / encode / D2H of the wire overlap; each chunk's output placed "
                              "by the previous chunk's device status)"}
+    return res
+
+
+def host_inclusive_shape(name, n, k=4096):
+    """The host path on the reference's own request shapes (ABI 7): kx_host_decode_batch with message offsets
+    known and kx_host_encode_batch, pinned buffers, k distinct records tiled to n. mockreq: MockReq{Msg,
+    map<string,string>, list<string>} (internal/mocks/thrift/mock.thrift:3-6, flat LIST_BYTES columns);
+    nesting: baseline.thrift's Nesting (the nested record walker). Arenas sized exactly (the distinct
+    records' units times the tiling); verified against a decode of the distinct records and the wire."""
+    import numpy as np
+    import torch
+
+    from kitex_amd import _abi as A
+    from kitex_amd import idl, synth
+    from kitex_amd import schema as S
+    from kitex_amd.codec import ThriftCodec
+    from kitex_amd.synth import ColumnSet
+    if name == "mockreq":
+        sch = S.schema_mockreq()
+    else:
+        doc = idl.parse_idl(os.path.join(ROOT, "tests", "golden", "idl", "baseline.thrift"))
+        sch = idl.to_schema(doc.struct("Nesting"))
+    cdc = ThriftCodec(sch)
+    ds = cdc.dschema
+    recs = synth.thrift_records(sch, k, seed=11)
+    one = np.frombuffer(b"".join(recs), dtype=np.uint8)
+    lens = np.array([len(r) for r in recs], dtype=np.uint64)
+    reps = n // k
+    n = reps * k
+
+    def pinned(cnt, dtype):
+        return torch.empty(max(1, cnt), dtype=dtype, pin_memory=True).numpy()
+    wire = pinned(one.size * reps, torch.uint8)
+    wire[:] = np.tile(one, reps)
+    offs = pinned(n + 1, torch.int64).view(np.uint64)
+    offs[0] = 0
+    offs[1:] = np.cumsum(np.tile(lens, reps))
+    ooffs = np.zeros(k + 1, dtype=np.uint64)
+    ooffs[1:] = np.cumsum(lens)
+    ref, st0 = cdc.UnmarshalHost(one.copy(), k, offsets=ooffs)   # the distinct records' columns and units
+    var, elem, sub = [], [], []
+    for c, ci in enumerate(ds.infos):
+        if ci.kind == A.COL_FIXED:
+            var.append(0), elem.append(0), sub.append(0)
+            continue
+        hi, lv = k, []
+        for arr in ref.cols[c][:-1]:
+            hi = int(arr[hi])
+            lv.append(hi * reps)
+        var.append(max(1, lv[-1]))
+        elem.append(lv[0] if len(lv) >= 2 else 0)
+        sub.append(lv[1] if len(lv) >= 3 else 0)
+    fixed = {1: np.uint8, 2: np.int16, 4: np.int32, 8: np.int64}
+    cols = []
+    for c, ci in enumerate(ds.infos):
+        if ci.kind == A.COL_FIXED:
+            cols.append(pinned(n * ci.width, torch.uint8).view(fixed[ci.width]))
+            continue
+        arrs = [pinned(n + 1, torch.int32).view(np.uint32)]
+        if ci.kind in (A.COL_LIST_BYTES, A.COL_LIST2, A.COL_LIST2_BYTES):
+            arrs.append(pinned(elem[c] + 1, torch.int32).view(np.uint32))
+        if ci.kind == A.COL_LIST2_BYTES:
+            arrs.append(pinned(sub[c] + 1, torch.int32).view(np.uint32))
+        w = 1 if ci.kind in (A.COL_BYTES, A.COL_LIST_BYTES, A.COL_LIST2_BYTES) else ci.width
+        arrs.append(pinned(var[c] * w, torch.uint8).view(fixed[w]))
+        cols.append(tuple(arrs))
+    pres = pinned(n * 8, torch.uint8).view(np.uint64) if ds.npresence else None
+    hout = ColumnSet(cols, pres, n)
+    best = 1e30
+    for _ in range(4):
+        t0 = time.perf_counter()
+        _, st, rs = cdc.UnmarshalHost(wire, n, offsets=offs, var_caps=var, elem_caps=elem, sub_caps=sub, out=hout,
+                                      raise_on_error=False, record_status=True)
+        best = min(best, time.perf_counter() - t0)
+    ok = st.code == 0 and st.n_records == n and not rs.any()
+    try:   # the first k records equal the distinct records' decode
+        from tests.helpers import assert_columns_equal
+        assert_columns_equal(hout, ref, ds.infos, k)
+    except Exception:
+        ok = False
+    out_bytes = sum(sum(x.nbytes for x in c) if isinstance(c, tuple) else c.nbytes for c in cols) + \
+        (pres.nbytes if pres is not None else 0)
+    res = {"schema": "MockReq (mock.thrift:3-6)" if name == "mockreq" else "Nesting (baseline.thrift)",
+           "records": n, "wire_bytes_per_record": wire.size / n,
+           "decode": {"records_per_s": n / best, "ms": best * 1e3, "pcie_gb_s": (wire.size + out_bytes) / best / 1e9,
+                      "verified": ok},
+           "note": "kx_host_decode_batch / kx_host_encode_batch (ABI 7) from pinned buffers, offsets known, "
+                   "16-chunk pipelines; arenas sized exactly"}
+    # the reply bytes: the encoder's bytes of the distinct records, tiled (the generator may write fields in
+    # another order than FastWriteNocopy's, so the input is not the reference)
+    one_enc, _, st1 = cdc.MarshalHost(ref)
+    h_wire = pinned(max(wire.size, one_enc.size * reps), torch.uint8)
+    ebest = 1e30
+    for _ in range(4):
+        t0 = time.perf_counter()
+        w, _, est = cdc.MarshalHost(hout, out=h_wire, with_offsets=False, raise_on_error=False)
+        ebest = min(ebest, time.perf_counter() - t0)
+    exact = est.code == 0 and st1.code == 0 and est.consumed == one_enc.size * reps and \
+        bool(np.array_equal(h_wire[:est.consumed].reshape(reps, -1), np.broadcast_to(one_enc, (reps, one_enc.size))))
+    res["encode"] = {"records_per_s": n / ebest, "ms": ebest * 1e3,
+                     "pcie_gb_s": (est.consumed + out_bytes) / ebest / 1e9,
+                     "bit_exact": bool(exact)}
     return res
 
 
@@ -995,12 +1129,9 @@ def cpu_baseline(cfg, nrec):
             wire = wire[keep]
             offs = np.zeros(nrec + 1, dtype=np.uint64)
             offs[1:] = np.cumsum(lens)
-        best = 1e30
-        for _ in range(3):
-            t0 = time.perf_counter()
-            rc, out, st, _ = oracle.decode(sch, wire, nrec, offsets=offs, threads=threads, pb=pb)
-            best = min(best, time.perf_counter() - t0)
-            assert rc == 0
+        ts, ok = cpu_decode_pool(sch, wire, offs, nrec, pb, threads)
+        st = spread(nrec, ts)
+        best = nrec / st["median"]
         one = min(nrec, 1 << 20)
         t0 = time.perf_counter()
         oracle.decode(sch, wire[:int(offs[one])], one, offsets=offs[:one + 1], threads=1, pb=pb)
@@ -1018,9 +1149,12 @@ def cpu_baseline(cfg, nrec):
                 cpu = next((l.split(":", 1)[1].strip() for l in fh if l.startswith("model name")), "")
         except Exception:
             pass
-        return {"value": nrec / best, "unit": "records/s", "cores": threads, "kind": "port",
+        return {"value": st["median"], "unit": "records/s", "cores": threads, "kind": "port", "verified": ok,
+                "spread": st,
                 "sample": f"{nrec} {cfg} records, FastRead restatement (oracle/kx_oracle.c) with message "
-                          f"offsets known, best of 3, {threads} threads (len(sched_getaffinity))",
+                          f"offsets known, one record range per thread of a persistent pool with pre-faulted "
+                          f"outputs, median of {st['runs']} runs after a warm-up, {threads} threads "
+                          f"(len(sched_getaffinity))",
                 "threads": threads, "physical_cores": phys,
                 "cores_note": "cores = worker threads used (one per logical CPU of the affinity mask); "
                               "physical_cores = distinct (package, core) pairs among them",

@@ -56,18 +56,14 @@ int ensure_ws(kx_ctx* c, size_t bytes, hipStream_t stream, uint64_t* epoch) {
 }
 
 // The chunked decode pipeline's second stream and events (KxPipe). Chunk size: KX_CHUNK_MB MiB of
-// 8 KiB tiles (0 = one chunk), KX_CHUNK_AHEAD chunks of index-pass lead.
+// 8 KiB tiles (0 = one chunk; measured slower at every size), KX_CHUNK_AHEAD chunks of
+// index-pass lead.
 static int ensure_pipe(kx_ctx* c) {
   KxPipe& p = c->pipe;
   if (p.aux) return KX_OK;
-  const char* e = getenv("KX_CHUNK_MB");
-  const uint64_t mb = e ? strtoull(e, nullptr, 10) : KX_CHUNK_MB_DEFAULT;
-  const char* a = getenv("KX_CHUNK_AHEAD");
-  p.ahead = a ? atoi(a) : 1;
+  const uint64_t mb = (uint64_t)kx_knob(KXK_CHUNK_MB);
+  p.ahead = kx_knob(KXK_CHUNK_AHEAD);
   p.chunk_tiles = (mb * 128 + 63) & ~63ull;  // 128 tiles of 8 KiB per MiB, whole groups of 64 tiles
-  const char* cb = getenv("KX_COMBO_MB");
-  const uint64_t cmb = cb ? strtoull(cb, nullptr, 10) : KX_COMBO_MB_DEFAULT;
-  p.combo_tiles = (cmb * 128 + 63) & ~63ull;
   KX_HIP_CHECK(hipEventCreateWithFlags(&p.fork, hipEventDisableTiming));
   for (int k = 0; k < KX_PIPE_EV; k++) {
     KX_HIP_CHECK(hipEventCreateWithFlags(&p.ev_idx[k], hipEventDisableTiming));
@@ -861,11 +857,8 @@ static int decode_frames(kx_ctx* c, const kx_schema* s, const uint8_t* in, uint6
   // DecodeMeta's payloadChecksumValidate (default_codec.go:205-209): fused into the frame scan's emit pass
   // (the payload is checked from the LDS window the scan already holds); KX_CRC_FUSED=0 runs the separate
   // checksum kernel after the scan instead
-  // (read per call, so an A/B run or a test can switch forms within one process)
-  const char* fe = getenv("KX_CRC_FUSED");
-  const int fused_env = fe ? atoi(fe) : 1;
   uint8_t* vrc = c->crc32c_check ? (uint8_t*)(f + vr_at) : nullptr;
-  const bool fused = vrc && fused_env;
+  const bool fused = vrc && kx_knob(KXK_CRC_FUSED);
   if ((rc = frame_scan(c, in, in_len, n, max_payload, fo, ps, pe, kinds, pre, stream, fused ? vrc : nullptr)))
     return rc;
   if (vrc && !fused) {

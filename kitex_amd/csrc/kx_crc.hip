@@ -24,6 +24,8 @@
 #include <hip/hip_runtime.h>
 #include <stdlib.h>
 
+#include <atomic>
+
 #include "kx_internal.h"
 #include "kx_crc.h"
 #include "kx_mem.h"
@@ -291,19 +293,19 @@ __global__ void crc_final_kernel(kx_status* st, const uint64_t* offs, uint64_t n
 // partly occupied round of workgroups behind the first)
 template <int G>
 void launch_crc(const CrcParams& cp, uint64_t nblk, hipStream_t stream) {
-  static int resident_dev[64];   // per device ordinal (0: not yet asked): devices may differ
+  static std::atomic<int> resident_dev[64];   // per device ordinal (0: not yet asked): devices may differ
   int dev = 0, resident = (int)MAX_WG;
   if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64) {
-    if (!resident_dev[dev]) {
+    resident = resident_dev[dev].load(std::memory_order_relaxed);
+    if (!resident) {
       int ncu = 0, per = 0;
-      resident_dev[dev] =
-          hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-                  hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, crc_kernel<G>, CT, 0) == hipSuccess &&
-                  ncu > 0 && per > 0
-              ? ncu * per
-              : (int)MAX_WG;
+      resident = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+                         hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, crc_kernel<G>, CT, 0) == hipSuccess &&
+                         ncu > 0 && per > 0
+                     ? ncu * per
+                     : (int)MAX_WG;
+      resident_dev[dev].store(resident, std::memory_order_relaxed);
     }
-    resident = resident_dev[dev];
   }
   const unsigned grid = (unsigned)kmin64(nblk, (uint64_t)resident);
   hipLaunchKernelGGL(crc_kernel<G>, dim3(grid), dim3(CT), 0, stream, cp);
@@ -320,8 +322,7 @@ int kx_launch_crc32c(const uint8_t* in, uint64_t in_len, const uint64_t* offs, u
   cp.errkey = (unsigned long long*)scratch;
   const uint64_t nblk = (n + CT - 1) / CT;
   if (nblk) {
-    const char* e = getenv("KX_CRC_BLK");
-    const int blk = e ? atoi(e) : 8;
+    const int blk = kx_knob(KXK_CRC_BLK);
     if (blk == 4) launch_crc<4>(cp, nblk, stream);
     else if (blk == 1) launch_crc<1>(cp, nblk, stream);
     else launch_crc<8>(cp, nblk, stream);

@@ -30,6 +30,7 @@
 
 #include "kx_internal.h"
 #include "kx_crc.h"
+#include "kx_knobs.h"
 
 #define LDS __attribute__((address_space(3)))
 #define GLB __attribute__((address_space(1)))
@@ -49,7 +50,6 @@ constexpr int HALO = 512;                // default halo: the record straddling 
 constexpr int HALO_MAX = 1536;           // up to here (the halo grows with the batch's mean record size)
 constexpr int WINB = TILE + HALO_MAX + 16;  // LDS window bytes allocated (+16 for the aligned-down start)
 constexpr int WINW = WINB / 4 + 4;       // window dwords (+ pad for the last aligned read pair)
-constexpr int WIN_LOADS = (WINB / 16 + 63) / 64;
 constexpr int GT = 64;                   // tiles per group (one group-scan lane per tile)
 #ifndef KX_CT
 #define KX_CT 256
@@ -78,7 +78,11 @@ enum { CY_E = 0, CY_CNT, CY_VAR, CY_NSTOP = CY_VAR + KXP_NV_MAX, CY_FLAGS, CY_WO
 
 // M_FRAME: framing sniff; M_THRIFT_LS: Thrift with list<struct> fields (its own instantiation, so that the
 // element loop does not change the register allocation of every other schema's kernels)
-enum Mode { M_THRIFT = 0, M_SKIP = 1, M_PB = 2, M_FRAME = 3, M_THRIFT_LS = 4 };
+enum Mode { M_THRIFT = 0, M_SKIP = 1, M_PB = 2, M_FRAME = 3, M_THRIFT_LS = 4, M_PBB = 5 };
+// M_PBB: Kitex-PB Batch frames (0x0A, uvarint length; the nested walker's record boundaries) on the frame
+// pipeline, an instantiation of its own: its candidate test (two frames, later 0x0A bytes) inlined into
+// the M_FRAME index kernel took it from 4 to 2 waves per SIMD (248 VGPRs), round 5's frames regression
+constexpr bool is_frame(int m) { return m == M_FRAME || m == M_PBB; }
 __host__ __device__ constexpr bool is_thrift(int m) { return m == M_THRIFT || m == M_THRIFT_LS; }
 
 // diagnostics (KX_DIAG & 64): shader-clock cycles per index-pass phase, summed over tiles (lane 0), in a
@@ -119,10 +123,8 @@ struct DecParams {
   uint64_t* nstop_ring;      // chunked pipeline: nstop of chunk k at [k % KX_PIPE_EV] (chain runs ahead of emit)
   uint32_t* redo_n;          // fast index kernel: tiles it could not index (count, then their ids)
   uint32_t* redo;
-  int gate_reset;            // chain_kernel zeroes *gate when it ends (its gate is chain_fast_kernel's fallback flag)
-  uint32_t* gate;            // known offsets, length gather: these kernels run only when *gate != 0 (repair)
-  uint32_t* gcheck;          // ... the checking emit pass: a tile whose decoded var units differ from the
-                             // gathered ones sets *gcheck (the repair pass then runs)
+  int gate_reset;            // chain_kernel zeroes *gate when it ends
+  uint32_t* gate;            // chain_kernel runs only when *gate != 0 (chain_fast_kernel's fallback flag)
   uint64_t* split_out;       // kx_thrift_split_points: nsplit + 1 record starts (no emit pass)
   uint32_t nsplit;
   uint64_t var_base[KXP_NV_MAX];  // arena positions start here (a chunk of a larger batch)
@@ -152,7 +154,6 @@ struct DecParams {
 // parameter (cols.data[c]) would otherwise make the compiler copy the whole block to scratch per lane.
 typedef const KAS DecParams KParams;
 #define KX_PARAMS() (*(KParams*)__builtin_amdgcn_kernarg_segment_ptr())
-#define KX_CPARAMS() (*(const KAS ComboParams*)__builtin_amdgcn_kernarg_segment_ptr())
 
 // known-offsets mode: where record r ends (message bodies: an explicit end per record)
 __device__ __forceinline__ uint64_t rec_end(KParams& dp, uint64_t r) {
@@ -1440,7 +1441,6 @@ __device__ __forceinline__ uint64_t scan_segment(const Src& w, int32_t q0, uint6
 // candidate checks. The 33-dword loop only records which dwords hold a hit (one bit per dword); the
 // hit positions are then recomputed for the (one or two) lowest such dwords. Positions are exact: bytes
 // of dword 0 below the segment start and bytes of dword 32 at or past its end are masked off.
-#ifndef KX_SCAN2_OLD
 __device__ __forceinline__ void scan_segment2(const Src& w, int32_t q0, uint32_t sig, int lane, uint32_t& c1,
                                               uint32_t& c2) {
   const LDS uint32_t* s = w.win + (q0 >> 2);
@@ -1480,32 +1480,6 @@ __device__ __forceinline__ void scan_segment2(const Src& w, int32_t q0, uint32_t
     if (c2 != ~0u) break;
   }
 }
-#else
-__device__ __forceinline__ void scan_segment2(const Src& w, int32_t q0, uint32_t sig, int lane, uint32_t& c1,
-                                              uint32_t& c2) {
-  const LDS uint32_t* s = w.win + (q0 >> 2);
-  const uint32_t sh0 = q0 & 3;
-  const uint32_t b0 = (sig & 0xff) * 0x01010101u, b1 = ((sig >> 8) & 0xff) * 0x01010101u;
-  const uint32_t b2 = ((sig >> 16) & 0xff) * 0x01010101u;
-  c1 = ~0u;
-  c2 = ~0u;
-  int idx = lane % 33;
-  for (int i = 0; i < 33; i++) {
-    const uint32_t x0 = s[idx], x1 = s[idx + 1];
-    uint32_t m = zero_bytes((x0 ^ b0) | (__builtin_amdgcn_alignbyte(x1, x0, 1) ^ b1) |
-                            (__builtin_amdgcn_alignbyte(x1, x0, 2) ^ b2));
-    const uint32_t base = (uint32_t)(4 * idx) - sh0;
-    const uint32_t h1 = base + first_hit(m);
-    m &= m - 1;
-    const uint32_t h2 = base + first_hit(m);
-    const uint32_t lo = min(c1, h1);
-    c2 = min(min(c2, h2), max(c1, h1));
-    c1 = lo;
-    idx = idx == 32 ? 0 : idx + 1;
-  }
-}
-
-#endif
 
 // Kitex-Protobuf record candidate at p: a Batch frame header (0x0A, uvarint length) whose body fits
 // the input, starts with a plausible tag, and is followed by the next frame's 0x0A (or the end).
@@ -1600,9 +1574,6 @@ __device__ __forceinline__ uint64_t pb_scan_segment(const Src& w, uint64_t seg_l
 // < 16 bytes of the input are read from global memory. The descriptor is built from wave-uniform
 // values (SGPRs); a chunk past num_records still writes its LDS slot (zeros), so the issue loop masks
 // the lanes past the window's end.
-#ifndef KX_EXP_EMIT
-#define KX_EXP_EMIT 0   // timing experiments on the emit pass (bits: 1 DMA only, 2 no payload copy, 4 no fixed stores)
-#endif
 #ifndef KX_DMA_AUX
 #define KX_DMA_AUX 0   // cache policy of the window DMA (2: nt, MI355X_MICROARCH.md "nt-weights"); A/B knob
 #endif
@@ -1624,34 +1595,6 @@ __device__ __forceinline__ Src load_window(KParams& dp, LDS uint32_t* win, uint6
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (LDS void*)(win + k * 256), 16, lane * 16, k * 1024, 0,
                                                KX_DMA_AUX);
   if (wait) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  const KAS KxProgram* P = dp.prog;
-  return Src{dp.in, dp.in_len, wbase - abs_in, wlen, win, thrift ? P->steps : nullptr, thrift ? P->nsteps : 0u,
-             thrift ? P->canon_pres : 0ull};
-}
-
-// The same window load with the DMA issued from inline assembly, invisible to the compiler's wait
-// insertion: its own tracking would put `s_waitcnt vmcnt(0)` in front of every LDS read (it cannot
-// tell which window a read hits), which serialises a prefetch. The caller owns the wait: exactly
-// WIN_LOADS vector-memory instructions are issued per window.
-__device__ __forceinline__ void dma_lds16(v4u rs, LDS uint32_t* dst, uint32_t voff, uint32_t soff) {
-  const uint32_t m0v = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)dst);
-  asm volatile("s_mov_b32 m0, %0\n\ts_nop 1\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds" ::"s"(m0v), "v"(voff), "s"(rs), "s"(soff) : "memory", "m0");
-}
-
-__device__ __forceinline__ Src load_window_async(KParams& dp, LDS uint32_t* win, uint64_t lo, int lane, bool thrift) {
-  const uint64_t abs_in = (uint64_t)dp.in;
-  const uint64_t wbase = (abs_in + kmin64(lo, dp.in_len)) & ~15ull;
-  const uint64_t end = abs_in + dp.in_len;
-  const int32_t wlen = dp.nolds || end < wbase + 16 ? 0 : (int32_t)kmin64((uint64_t)dp.winb, (end - wbase) & ~15ull);
-  v4u rs;
-  rs.x = __builtin_amdgcn_readfirstlane((uint32_t)wbase);
-  rs.y = __builtin_amdgcn_readfirstlane((uint32_t)(wbase >> 32)) & 0xffffu;
-  rs.z = __builtin_amdgcn_readfirstlane((uint32_t)wlen);
-  rs.w = 0x00020000u;
-  const uint32_t voff = (uint32_t)lane * 16u;
-#pragma unroll
-  for (int k = 0; k < WIN_LOADS; k++)
-    if ((k + 1) * 64 <= WINB / 16 || k * 64 + lane < WINB / 16) dma_lds16(rs, win + k * 256, voff, (uint32_t)k * 1024u);
   const KAS KxProgram* P = dp.prog;
   return Src{dp.in, dp.in_len, wbase - abs_in, wlen, win, thrift ? P->steps : nullptr, thrift ? P->nsteps : 0u,
              thrift ? P->canon_pres : 0ull};
@@ -1926,11 +1869,11 @@ __device__ __forceinline__ int parse_record(KParams& dp, const Src& w, uint64_t 
     if (dp.prog->npbsteps && pb_canon<NV>(w, dp.prog, dp.cols, b, e, r, emit, utf8, vs, pres)) return KX_OK;
     return pb_body<NV>(w, dp.prog, dp.cols, b, e, r, emit, vs, pres, utf8);
   }
-  if (MODE == M_FRAME) {
+  if (is_frame(MODE)) {
     uint64_t ps, pe, mp = 0;
     uint32_t kind, ml = 0;
     int32_t sid = 0;
-    const int rc = dp.fr_grpc == 3 ? frame_pbb(w, pos, lim, end, ps, pe, kind)
+    const int rc = MODE == M_PBB ? frame_pbb(w, pos, lim, end, ps, pe, kind)
                    : dp.fr_grpc == 2 ? frame_tts(dp, w, pos, lim, end, ps, pe, kind, sid, mp, ml)
                    : dp.fr_grpc ? frame_grpc(w, pos, lim, dp.fr_max, end, ps, pe, kind)
                                 : frame_one(w, pos, lim, dp.fr_max, end, ps, pe, kind);
@@ -2105,7 +2048,7 @@ __device__ __forceinline__ Cand lane_candidate(KParams& dp, const Src& w, uint64
   Cand cd;
   cd.ent = X_NONE; cd.plim = seg_lo; cd.sig = 0; cd.smask = 0xffu; cd.s2o = 0; cd.s2 = 0; cd.strict = false;
   if (seg_lo >= seg_hi) return cd;
-  if (MODE == M_PB || (MODE == M_FRAME && dp.fr_grpc == 3)) {   // Kitex-PB Batch frames
+  if (MODE == M_PB || MODE == M_PBB) {   // Kitex-PB Batch frames
     cd.ent = pb_scan_segment(w, seg_lo, seg_hi, dp.in_len, lane);
     return cd;
   }
@@ -2685,42 +2628,6 @@ __device__ __forceinline__ Agg measure_records(KParams& dp, const Src& w, uint64
   return g;
 }
 
-// Known offsets, length gather (the index pass without the window): a canonical record's var extents
-// follow from the plan's segments (KxpFast) and one big-endian length word per var field but the last,
-// whose length is what the record's end leaves (R2: s9's length at offsets[r] + 91, s10's =
-// end - start - 103 - len9). Nothing is checked here: the emit pass compares every tile's decoded
-// extents with these and, on any difference, the gated repair pass redoes index -> emit (launch_t).
-// False: the record is off the plan's shape (its extents count as empty, which the emit pass then finds
-// to differ unless the record failed).
-template <int NV>
-__device__ __forceinline__ bool gather_lengths(KParams& dp, uint64_t a, uint64_t b, uint64_t* len) {
-  if (a > b || b > dp.in_len) return false;
-  const Src g{dp.in, dp.in_len, 0, 0, nullptr, nullptr, 0u, 0ull};
-  const uint32_t ns = dp.fp.nseg;
-  uint64_t pos = a;
-  for (uint32_t j = 0; j + 1 < ns; j++) {
-    const uint32_t flen = dp.fp.seg[j].flen, vk = dp.fp.seg[j].vkind, vs = dp.fp.seg[j].vslot;
-    const uint64_t w = vk == 2 ? dp.fp.seg[j].vwidth : 1u;
-    const uint64_t hl = vk == 2 ? 8u : 7u;   // field header (3), list element type (1), length (4)
-    pos += flen;
-    if (pos + hl > b) return false;
-    uint64_t L;
-    if (j + 2 == ns) {   // the last var field: the record's end fixes it
-      const uint64_t rest = b - pos - hl, tail = dp.fp.seg[j + 1].flen;
-      if (rest < tail || (rest - tail) % w) return false;
-      L = (rest - tail) / w;
-    } else {
-      L = __builtin_bswap32(gld4(g, pos + hl - 4));
-    }
-#pragma unroll
-    for (int v = 0; v < NV; v++)
-      if ((uint32_t)v == vs) len[v] = L;
-    pos += hl + L * w;
-    if (pos > b) return false;
-  }
-  return true;
-}
-
 // tile geometry
 __device__ __forceinline__ void tile_range(KParams& dp, uint64_t t, uint64_t& lo, uint64_t& hi) {
   if (dp.offsets) {
@@ -2743,14 +2650,9 @@ __device__ Agg tile_agg(KParams& dp, LDS uint32_t* win, uint64_t t, uint64_t see
   }
   const uint64_t t0 = (dp.diag & 64) ? __builtin_amdgcn_s_memtime() : 0;
   // the window DMA is issued first and the batch signature's load behind it, so both round trips overlap
-#ifndef KX_DSIG_OLD
   const Src w = load_window(dp, win, lo, lane, is_thrift(MODE), false);
   const uint32_t dsig = data_sig(dp);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#else
-  const Src w = load_window(dp, win, lo, lane, is_thrift(MODE));
-  const uint32_t dsig = data_sig(dp);
-#endif
   if ((dp.diag & 64) && lane == 0) atomicAdd(&dp.phase[0], (unsigned long long)(__builtin_amdgcn_s_memtime() - t0));
   if constexpr (MODE == M_THRIFT) {
     if (dp.fast && !dp.offsets && dsig == dp.prog->sig && w.wlen >= TILE + 64) {
@@ -2770,35 +2672,6 @@ __device__ __forceinline__ void put_tile(KParams& dp, uint64_t t, const Agg& a, 
   put_word(dp.tdesc, nt, T_ERRC, t, ep, a.errc);
   put_word(dp.tdesc, nt, T_ERRP, t, ep, a.errp);
   for (int v = 0; v < nv; v++) put_word(dp.tdesc, nt, T_VAR + v, t, ep, a.var[v]);
-}
-
-template <int NV>
-__global__ void __launch_bounds__(NT) gather_kernel(DecParams dp_) {
-  KParams& dp = KX_PARAMS();
-  (void)dp_;
-  const int lane = threadIdx.x & 63;
-  const uint64_t t = (uint64_t)blockIdx.x * WAVES + (threadIdx.x >> 6);
-  if (t >= dp.ntiles) return;
-  const uint64_t r0 = t * dp.krec, r1 = kmin64(r0 + dp.krec, dp.n), r = r0 + lane;
-  uint64_t len[NV > 0 ? NV : 1];
-#pragma unroll
-  for (int v = 0; v < (NV > 0 ? NV : 1); v++) len[v] = 0;
-  if (r < r1 && !gather_lengths<NV>(dp, dp.offsets[r], rec_end(dp, r), len)) {
-#pragma unroll
-    for (int v = 0; v < (NV > 0 ? NV : 1); v++) len[v] = 0;
-  }
-  Agg g;
-  g.ent = X_NONE; g.ex = X_NONE; g.errc = 0; g.errp = 0;
-  g.cnt = r1 - r0;
-#pragma unroll
-  for (int v = 0; v < NV; v++) g.var[v] = wave_sum(len[v]);
-  put_tile(dp, t, g, NV);
-  if (t == 0 && lane == 0) atomicOr(dp.gcheck, 2u);   // diagnostics: the gather ran (kx_status.diag[2])
-}
-
-// the repair pass re-arms what the checking emit pass may have set from the gathered extents
-__global__ void gate_rearm_kernel(const uint32_t* gate, uint32_t* overflow) {
-  if (threadIdx.x == 0 && (*(volatile const uint32_t*)gate & 1u)) *overflow = 0;
 }
 
 // Does a chain arriving at `E` agree with an item whose speculative entry is `ent`? (An item with no
@@ -2937,7 +2810,7 @@ __global__ void __launch_bounds__(NT, 4) index_kernel(DecParams dp_) {  // 4 wav
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
   const uint64_t t = dp.t_lo + (uint64_t)blockIdx.x * WAVES + wv;
-  if (t >= dp.t_hi || (dp.gate && !(*(volatile uint32_t*)dp.gate & 1u))) return;
+  if (t >= dp.t_hi) return;
   index_tile<NV, MODE>(dp, (LDS uint32_t*)WIN[wv], t, lane);
 }
 
@@ -3006,47 +2879,6 @@ __global__ void __launch_bounds__(NT, 4) redo_kernel(DecParams dp_) {
     redo_tile<NV, MODE>(dp, (LDS uint32_t*)WIN[wv], __builtin_amdgcn_readfirstlane(dp.redo[i]), lane);
 }
 
-// ---- kernel 1 (persistent variant, concatenated mode): each wave walks tiles t, t + W, t + 2W ...
-// with two LDS windows: the DMA of its next tile is in flight while it walks the current one
-// (s_waitcnt vmcnt(WIN_LOADS) leaves exactly the next window's loads outstanding). Two LDS windows
-// per wave halve the occupancy (2 waves / SIMD) in exchange for a wave that never waits for its own
-// DMA after the first tile.
-template <int NV, int MODE>
-__global__ void __launch_bounds__(NT, 2) index_kernel_pf(DecParams dp_) {
-  KParams& dp = KX_PARAMS();
-  (void)dp_;
-  __shared__ __attribute__((aligned(16))) uint32_t WINA[WAVES][WINW];
-  __shared__ __attribute__((aligned(16))) uint32_t WINB_[WAVES][WINW];
-  const int lane = threadIdx.x & 63;
-  const int wv = threadIdx.x >> 6;
-  const uint64_t W = (uint64_t)gridDim.x * WAVES;
-  uint64_t t = dp.t_lo + (uint64_t)blockIdx.x * WAVES + wv;
-  if (t >= dp.t_hi) return;
-  LDS uint32_t* wa = (LDS uint32_t*)WINA[wv];
-  LDS uint32_t* wb = (LDS uint32_t*)WINB_[wv];
-  const uint32_t dsig = data_sig(dp);  // before the first DMA: its global load must not wait on one
-  uint64_t lo, hi;
-  tile_range(dp, t, lo, hi);
-  Src w = load_window_async(dp, wa, lo, lane, is_thrift(MODE));
-  bool odd = false;
-  for (;;) {
-    const uint64_t tn = t + W;
-    uint64_t lon = 0, hin = 0;
-    Src wn = w;
-    if (tn < dp.t_hi) {
-      tile_range(dp, tn, lon, hin);
-      wn = load_window_async(dp, odd ? wa : wb, lon, lane, is_thrift(MODE));
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WIN_LOADS) : "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    const Agg a = walk_tile<NV, MODE>(dp, w, lo, hi, t == 0 ? 0ull : X_NONE, lane, dp.starts + t * dp.slotcap, dsig);
-    if (lane == 0) put_tile(dp, t, a, NV);
-    if (tn >= dp.t_hi) break;
-    t = tn; lo = lon; hi = hin; w = wn; odd = !odd;
-  }
-}
-
 // ---- kernel 1b: group scan (one wave per group of 64 tiles) ----
 template <int NV, int MODE>
 __global__ void __launch_bounds__(NT) group_kernel(DecParams dp_) {
@@ -3056,7 +2888,7 @@ __global__ void __launch_bounds__(NT) group_kernel(DecParams dp_) {
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
   const uint64_t g = dp.g_lo + (uint64_t)blockIdx.x * WAVES + wv;
-  if (g >= dp.g_hi || (dp.gate && !(*(volatile uint32_t*)dp.gate & 1u))) return;
+  if (g >= dp.g_hi) return;
   group_scan<NV, MODE, false>(dp, (LDS uint32_t*)WIN[wv], g, g == 0 && !dp.offsets ? 0ull : X_NONE, lane);
 }
 
@@ -3315,7 +3147,7 @@ __global__ void __launch_bounds__(CT) chain_kernel(DecParams dp_) {
           if (v < (int)dp.prog->nvar && v < KX_STATUS_VT) st->var_total[v] = tot[v];
         }
         close_slots<NV>(dp.prog, dp.cols, dp.overflow, rec, tot);
-        if (MODE == M_SKIP || MODE == M_FRAME) dp.skip_out[rec] = errp;
+        if (MODE == M_SKIP || is_frame(MODE)) dp.skip_out[rec] = errp;
         s_nstop = rec;
       }
       s_err = 1;
@@ -3346,7 +3178,7 @@ __global__ void __launch_bounds__(CT) chain_kernel(DecParams dp_) {
         if (v < (int)dp.prog->nvar && v < KX_STATUS_VT) st->var_total[v] = s_var[v];
       }
       close_slots<NV>(dp.prog, dp.cols, dp.overflow, tot, vt);
-      if (MODE == M_SKIP || MODE == M_FRAME) dp.skip_out[tot] = dp.in_len;
+      if (MODE == M_SKIP || is_frame(MODE)) dp.skip_out[tot] = dp.in_len;
       s_nstop = tot;
     }
     // emit of this chunk bounds itself by nstop: final once the chain has ended, else unbounded
@@ -3485,7 +3317,7 @@ __global__ void __launch_bounds__(CFT) chain_fast_kernel(DecParams dp_) {
       for (int v = 0; v < NV; v++)
         if (v < (int)dp.prog->nvar && v < KX_STATUS_VT) st->var_total[v] = var[v];
       close_slots<NV>(dp.prog, dp.cols, dp.overflow, cnt, var);
-      if (MODE == M_SKIP || MODE == M_FRAME) dp.skip_out[cnt] = dp.in_len;
+      if (MODE == M_SKIP || is_frame(MODE)) dp.skip_out[cnt] = dp.in_len;
       nstop = cnt;
     }
     *dp.nstop = (dp.chunk_last || done) ? nstop : ~0ull;
@@ -3522,12 +3354,7 @@ __device__ __forceinline__ uint64_t emit_canon(const Src& w, const KAS KxLaunchC
         f.w0 = __builtin_amdgcn_alignbyte(s0[1], s0[0], sh);
         f.w1 = __builtin_amdgcn_alignbyte(s0[2], s0[1], sh);
         f.w2 = __builtin_amdgcn_alignbyte(s0[3], s0[2], sh);
-#if KX_EXP_EMIT & 4   // timing experiment: fixed values computed, not stored
-        const uint64_t xv = fixed_after_header(f, sj.hdr & 0xff);
-        if (xv == 0x0123456789abcdefull) store_col(cols.data[sj.col], sj.width, r, xv);
-#else
         store_col(cols.data[sj.col], sj.width, r, fixed_after_header(f, sj.hdr & 0xff));
-#endif
         q += 3 + sj.width;
       }
       k += m;
@@ -3688,18 +3515,11 @@ __device__ __forceinline__ void emit_tile(KParams& dp, LDS uint32_t* win, uint64
     for (int v = 0; v < NV; v++)
       run[v] = (gd[(uint64_t)(G_BVAR + v) * dp.ngroups + g] & V48) + (td[(uint64_t)(T_PVAR + v) * dp.ntiles + t] & V48);
   }
-  uint64_t run0[NV > 0 ? NV : 1];
-#pragma unroll
-  for (int v = 0; v < (NV > 0 ? NV : 1); v++) run0[v] = run[v];
   // a tile the fast index path validated: records are read with the plan alone
   const bool canon = is_thrift(MODE) && !dp.direct && MODE != M_THRIFT_LS &&
                      ((dp.tdesc[(uint64_t)T_ERRC * dp.ntiles + t] & V48) == T_CANON);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (cnt == 0 || base >= nstop) return;
-#if KX_EXP_EMIT & 1   // timing experiment: the window DMA and the tile's bases only
-  if (w.win[lane] == 0xdeadbeefu && base == 12345) dp.status->diag[2] = cnt;
-  return;
-#endif
   cnt = kmin64(cnt, nstop - base);
   // records past the tile's slots (slotcap, a multiple of 64; ws_layout) are emitted one per round,
   // each starting where the previous one ended
@@ -3738,13 +3558,13 @@ __device__ __forceinline__ void emit_tile(KParams& dp, LDS uint32_t* win, uint64
 #pragma unroll
         for (int v = 0; v < NV; v++) vs.len[v] = 0;
         pres = 0;
-        if (MODE != M_SKIP && MODE != M_FRAME) emit_defaults(P, dp.cols, r);
+        if (MODE != M_SKIP && !is_frame(MODE)) emit_defaults(P, dp.cols, r);
       }
-      if (MODE == M_SKIP || MODE == M_FRAME) dp.skip_out[r] = pos;
-      if constexpr (MODE == M_FRAME) {
+      if (MODE == M_SKIP || is_frame(MODE)) dp.skip_out[r] = pos;
+      if constexpr (is_frame(MODE)) {
         if (dp.fr_crc) dp.fr_crc[r] = rc ? 0 : frame_crc_check(w, dp.in_len, pos);
       }
-      if (MODE != M_SKIP && MODE != M_FRAME && dp.cols.presence) dp.cols.presence[r] = pres;
+      if (MODE != M_SKIP && !is_frame(MODE) && dp.cols.presence) dp.cols.presence[r] = pres;
       if (known) {
         if (rc) atomicMin(dp.errkey, (unsigned long long)((r << 8) | (uint64_t)(rc & 0xff)));
         if (dp.rstat) dp.rstat[r] = (uint8_t)rc;
@@ -3823,11 +3643,7 @@ __device__ __forceinline__ void emit_tile(KParams& dp, LDS uint32_t* win, uint64
           if (at + nn <= arena_lim(dp.cols, cc)) {
             put_off(dp.cols, cc, r, at);
             big = K.kind == KXP_K_BYTES && nn >= KX_WAVE_COPY;
-#if KX_EXP_EMIT & 2   // timing experiment: no payload copy
-            if (nn == 0x7fffffff)
-#else
             if (nn && !big)
-#endif
               copy_var(w, K, vs.pos[v], nn, dst);
           } else {
             atomicOr(dp.overflow, 1u);
@@ -3849,16 +3665,9 @@ __device__ __forceinline__ void emit_tile(KParams& dp, LDS uint32_t* win, uint64
       kx_status* st = dp.status;
       st->n_records = dp.n;
       st->consumed = known ? rec_end(dp, dp.n - 1) : end;
-      if (MODE == M_SKIP || MODE == M_FRAME) dp.skip_out[dp.n] = end;
+      if (MODE == M_SKIP || is_frame(MODE)) dp.skip_out[dp.n] = end;
     }
     if (!known) chain = rl64(end, (int)(kmin64(step, cnt - j0) - 1));   // the round's last record ends here
-  }
-  if (dp.gcheck) {   // the gathered extents of this tile against the decoded ones (uniform)
-    bool same = true;
-#pragma unroll
-    for (int v = 0; v < NV; v++)
-      same &= run[v] - run0[v] == (dp.tdesc[(uint64_t)(T_VAR + v) * dp.ntiles + t] & V48);
-    if (!same && lane == 0) atomicOr(dp.gcheck, 1u);
   }
 }
 
@@ -3914,17 +3723,14 @@ __global__ void __launch_bounds__(64) split_kernel(DecParams dp_) {
   dp.split_out[k] = pos;
 }
 
-#ifndef KX_EMIT_WPS
-#define KX_EMIT_WPS 4   // A/B knob: emit_kernel waves per SIMD (4: <= 128 VGPRs)
-#endif
 template <int NV, int MODE, bool COOP = false>
-__global__ void __launch_bounds__(NT, KX_EMIT_WPS) emit_kernel(DecParams dp_) {
+__global__ void __launch_bounds__(NT, 4) emit_kernel(DecParams dp_) {
   KParams& dp = KX_PARAMS();
   (void)dp_;
   __shared__ __attribute__((aligned(16))) uint32_t WIN[WAVES][WINW];
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
-  if constexpr (MODE == M_FRAME) {
+  if constexpr (is_frame(MODE)) {
     if (dp.fr_crc) {   // the CRC-32C slicing tables, one column per thread (NT = 256)
       const uint32_t c0 = kx_crc_t0(g_crct, (int)threadIdx.x);
       __syncthreads();
@@ -3933,7 +3739,7 @@ __global__ void __launch_bounds__(NT, KX_EMIT_WPS) emit_kernel(DecParams dp_) {
     }
   }
   const uint64_t t = dp.t_lo + (uint64_t)blockIdx.x * WAVES + wv;
-  if (t >= dp.t_hi || (dp.gate && !(*(volatile uint32_t*)dp.gate & 1u))) return;
+  if (t >= dp.t_hi) return;
   emit_tile<NV, MODE, COOP>(dp, (LDS uint32_t*)WIN[wv], t, lane);
 }
 
@@ -4135,41 +3941,12 @@ __global__ void __launch_bounds__(NT, 4) emit_redo_kernel(DecParams dp_) {
     emit_tile<NV, MODE, COOP>(dp, (LDS uint32_t*)WIN[wv], __builtin_amdgcn_readfirstlane(dp.redo[i]), lane);
 }
 
-// ---- index of chunk k and emit of chunk k - 1 in one launch (KX_COMBO_MB): the first `nib` workgroups
-// index, the rest emit, so the index pass's VALU-bound waves and the emit pass's memory-bound waves share
-// every CU instead of running one after the other ----
-struct ComboParams {
-  DecParams ix, em;
-  uint32_t nib;
-};
-
-template <int NV, int MODE, bool COOP>
-__global__ void __launch_bounds__(NT, 4) combo_kernel(ComboParams cp_) {
-  const KAS ComboParams& C = KX_CPARAMS();
-  (void)cp_;
-  __shared__ __attribute__((aligned(16))) uint32_t WIN[WAVES][WINW];
-  const int lane = threadIdx.x & 63;
-  const int wv = threadIdx.x >> 6;
-  LDS uint32_t* win = (LDS uint32_t*)WIN[wv];
-  if (blockIdx.x < C.nib) {
-    KParams& dp = C.ix;
-    const uint64_t t = dp.t_lo + (uint64_t)blockIdx.x * WAVES + wv;
-    if (t < dp.t_hi) index_tile<NV, MODE>(dp, win, t, lane);
-  } else {
-    KParams& dp = C.em;
-    const uint64_t t = dp.t_lo + (uint64_t)(blockIdx.x - C.nib) * WAVES + wv;
-    if (t < dp.t_hi) emit_tile<NV, MODE, COOP>(dp, win, t, lane);
-  }
-}
-
 // Completes a call and re-arms the workspace for the next one (error key, overflow, nstop).
 __global__ void finalize_kernel(kx_status* st, unsigned long long* errkey, uint32_t* overflow, uint64_t* nstop,
                                 const uint64_t* offsets, uint64_t n, uint32_t* redo_n) {
   if (threadIdx.x != 0) return;
   redo_n[0] = 0;
   redo_n[2] = 0;   // the emit queue (emit_fast_kernel -> emit_redo_kernel)
-  if (offsets) st->diag[2] = redo_n[1];   // known offsets: 2 the length gather ran, 3 and was repaired
-  redo_n[1] = 0;   // the length-gather check flag (launch_t)
   unsigned long long k = *errkey;
   if (k != ~0ull && st->code == 0) {
     st->code = (int32_t)(k & 0xff);
@@ -4187,7 +3964,7 @@ __global__ void finalize_kernel(kx_status* st, unsigned long long* errkey, uint3
 //      record-start slots ----
 constexpr size_t WS_HDR = 512;
 // header words: [8] errkey, [16] overflow, [24] nstop, [64..) chain carry (CY_WORDS), [256..) nstop ring
-// (KX_PIPE_EV words), [448] redo count (u32), [452] length-gather check flag (u32), [456] emit queue count (u32),
+// (KX_PIPE_EV words), [448] redo count (u32), [452] unused (u32), [456] emit queue count (u32),
 // [460] chain fallback flag (u32)
 constexpr size_t WS_CARRY = 64, WS_RING = 256, WS_REDO = 448;
 static_assert(WS_CARRY + 8 * CY_WORDS <= WS_RING && WS_RING + 8 * KX_PIPE_EV <= WS_REDO && WS_REDO + 16 <= WS_HDR,
@@ -4212,8 +3989,7 @@ uint32_t krec_for(uint64_t in_len, uint64_t n) {
 // what decodes: 16 M R2 records (2.8 GB) need 0.22 GB of slots instead of 5.6 GB at one slot per byte.
 // KX_SLOTCAP overrides it (tests force the record-by-record path with 64).
 uint64_t slot_cap(uint64_t in_len, uint64_t n) {
-  const char* e = getenv("KX_SLOTCAP");
-  const long long forced = e ? atoll(e) : -1;
+  const long long forced = kx_knob(KXK_SLOTCAP);
   const uint64_t full = ((uint64_t)TILE + 1 + 63) & ~63ull;
   uint64_t cap = full;
   if (forced > 0) {
@@ -4273,23 +4049,18 @@ void launch_emit(dim3 grid, hipStream_t stream, const DecParams& dp) {
   hipLaunchKernelGGL((emit_kernel<NV, MODE>), grid, dim3(NT), 0, stream, dp);
 }
 
-template <int NV, int MODE>
-void launch_combo(unsigned grid, hipStream_t stream, const ComboParams& cp, uint32_t nlist) {
-  if constexpr (is_thrift(MODE) && NV > 0) {
-    if (KX_EMIT_COOP && nlist) {
-      hipLaunchKernelGGL((combo_kernel<NV, MODE, true>), dim3(grid), dim3(NT), 0, stream, cp);
-      return;
-    }
-  }
-  hipLaunchKernelGGL((combo_kernel<NV, MODE, false>), dim3(grid), dim3(NT), 0, stream, cp);
+// compute units of the current device (the resident redo grids' size; 64 when the runtime cannot tell)
+static int resident_cus() {
+  int dev = 0;
+  const int n = hipGetDevice(&dev) == hipSuccess ? kx_device_cus(dev) : 0;
+  return n > 0 ? n : 64;
 }
 
 // the chain pass: chain_fast_kernel, then chain_kernel gated on its fallback flag (ws header word
-// redo_n[3]); KX_CHAIN_FAST=0 (read per call) launches chain_kernel alone
+// redo_n[3]); KX_CHAIN_FAST=0 launches chain_kernel alone
 template <int NV, int MODE>
 int launch_chain(const DecParams& dp, hipStream_t stream) {
-  const char* e = getenv("KX_CHAIN_FAST");
-  if (dp.gate || (e && !atoi(e))) {
+  if (dp.gate || !kx_knob(KXK_CHAIN_FAST)) {
     hipLaunchKernelGGL((chain_kernel<NV, MODE>), dim3(1), dim3(CT), 0, stream, dp);
     return hipGetLastError() != hipSuccess ? KX_ERR_HIP : KX_OK;
   }
@@ -4304,32 +4075,22 @@ int launch_chain(const DecParams& dp, hipStream_t stream) {
 
 // the split fast emit pass (emit_fast_kernel + emit_redo_kernel) when it applies: 1 launched, 0 not, -1 error.
 // It needs the fast index pass's T_CANON tiles (concatenated Thrift with a canonical plan) and a plan in emit
-// form (strings and fixed scalars only); KX_EMIT_FAST=0 keeps the general emit pass (A/B, read per call)
+// form (strings and fixed scalars only); KX_EMIT_FAST=0 keeps the general emit pass (A/B)
 template <int NV, int MODE>
 int launch_fast_emit(const DecParams& dp, unsigned grid, hipStream_t stream) {
   if constexpr (MODE != M_THRIFT) {
     return 0;
   } else {
-    const char* e = getenv("KX_EMIT_FAST");
-    if ((e && !atoi(e)) || !dp.fast || dp.offsets || !dp.ep.ok || dp.diag || dp.split_out) return 0;
-    static int ncu_dev[64];
-    int dev = 0, ncu = 64;
-    if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64) {
-      int v = 0;
-      if (!ncu_dev[dev] && hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
-        ncu_dev[dev] = v + 1;
-      if (ncu_dev[dev] > 1) ncu = ncu_dev[dev] - 1;
-    }
-    const char* ne = getenv("KX_FAST_NARROW");
-    const bool narrow = (!ne || atoi(ne)) && dp.winb <= (uint32_t)FWINB;
+    if (!kx_knob(KXK_EMIT_FAST) || !dp.fast || dp.offsets || !dp.ep.ok || dp.diag || dp.split_out) return 0;
+    const int ncu = resident_cus();
+    const bool narrow = kx_knob(KXK_FAST_NARROW) && dp.winb <= (uint32_t)FWINB;
     const unsigned tiles = (unsigned)(dp.t_hi - dp.t_lo);
     if (narrow)
       hipLaunchKernelGGL((emit_fast_kernel<NV, true>), dim3((tiles + FWAVES - 1) / FWAVES), dim3(FNT), 0, stream, dp);
     else
       hipLaunchKernelGGL((emit_fast_kernel<NV, false>), dim3((tiles + WAVES - 1) / WAVES), dim3(NT), 0, stream, dp);
     if (hipGetLastError() != hipSuccess) return -1;
-    const char* rg = getenv("KX_REDO_WG");   // workgroups per CU of the queue kernels (A/B; default 4)
-    const unsigned rgrid = (unsigned)kmin64(grid, (uint64_t)ncu * (rg ? (uint64_t)kmax64(1, atoi(rg)) : 4));
+    const unsigned rgrid = (unsigned)kmin64(grid, (uint64_t)ncu * (uint64_t)kmax64(1, kx_knob(KXK_REDO_WG)));
     if (KX_EMIT_COOP && dp.nlist)
       hipLaunchKernelGGL((emit_redo_kernel<NV, MODE, true>), dim3(rgrid), dim3(NT), 0, stream, dp);
     else
@@ -4344,19 +4105,10 @@ int launch_fast_index(const DecParams& dp, unsigned grid, hipStream_t stream) {
   if constexpr (MODE != M_THRIFT) {
     return 0;
   } else {
-    static int split_env = -1, ncu = -1;
-    if (split_env < 0) { const char* e = getenv("KX_FAST_SPLIT"); split_env = e ? atoi(e) : 1; }
-    if (!split_env || !dp.fast || dp.offsets || (dp.diag & ~(64 | 256 | 1024 | 2048 | 4096))) return 0;
-    if (ncu < 0) {
-      int dev = 0;
-      if (hipGetDevice(&dev) != hipSuccess ||
-          hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-        ncu = 0;
-    }
-    static int narrow_env = -1;
-    if (narrow_env < 0) { const char* e = getenv("KX_FAST_NARROW"); narrow_env = e ? atoi(e) : 1; }
+    if (!kx_knob(KXK_FAST_SPLIT) || !dp.fast || dp.offsets || (dp.diag & ~(64 | 256 | 1024 | 2048 | 4096))) return 0;
+    const int ncu = resident_cus();
     const uint64_t tiles = dp.t_hi - dp.t_lo;
-    if (narrow_env && dp.winb <= (uint32_t)FWINB) {
+    if (kx_knob(KXK_FAST_NARROW) && dp.winb <= (uint32_t)FWINB) {
       const unsigned fgrid = (unsigned)((tiles + FWAVES - 1) / FWAVES);
       hipLaunchKernelGGL((index_fast_kernel<NV, true>), dim3(fgrid), dim3(FNT), 0, stream, dp);
     } else {
@@ -4365,8 +4117,7 @@ int launch_fast_index(const DecParams& dp, unsigned grid, hipStream_t stream) {
     }
     if (hipGetLastError() != hipSuccess) return -1;
     // the queued tiles: one resident grid's worth of waves at most (4 workgroups per CU)
-    const char* rg = getenv("KX_REDO_WG");   // workgroups per CU of the queue kernels (A/B; default 4)
-    const unsigned rgrid = (unsigned)kmin64(grid, (uint64_t)(ncu > 0 ? ncu : 64) * (rg ? (uint64_t)kmax64(1, atoi(rg)) : 4));
+    const unsigned rgrid = (unsigned)kmin64(grid, (uint64_t)ncu * (uint64_t)kmax64(1, kx_knob(KXK_REDO_WG)));
     hipLaunchKernelGGL((redo_kernel<NV, MODE>), dim3(rgrid), dim3(NT), 0, stream, dp);
     return hipGetLastError() != hipSuccess ? -1 : 1;
   }
@@ -4399,38 +4150,6 @@ int launch_t(const DecParams& dp0, const WsLayout& L, void* ws, hipStream_t stre
     const int lr = launch_fast_index<NV, MODE>(dp, grid, stream);
     if (lr < 0) return KX_ERR_HIP;
     if (lr == 0) hipLaunchKernelGGL((index_kernel<NV, MODE>), dim3(grid), dim3(NT), 0, stream, dp);
-    return KX_OK;
-  }
-  const uint64_t cbt = pp ? pp->combo_tiles : 0;
-  if (!dp.direct && cbt && dp.ntiles >= 2 * cbt && !dp.diag) {
-    // one stream: launch s = index(s) + emit(s - 1), then group(s) + chain(s); the emit of chunk s - 1
-    // reads the bases chain(s - 1) wrote one launch earlier
-    const uint64_t nch = (dp.ntiles + cbt - 1) / cbt;
-    for (uint64_t s = 0; s <= nch; s++) {
-      ComboParams cp{};
-      uint64_t ni = 0, ne = 0;
-      if (s < nch) {
-        cp.ix = chunk_params(dp, s, nch, cbt);
-        ni = (cp.ix.t_hi - cp.ix.t_lo + WAVES - 1) / WAVES;
-      }
-      if (s >= 1) {
-        cp.em = chunk_params(dp, s - 1, nch, cbt);
-        ne = (cp.em.t_hi - cp.em.t_lo + WAVES - 1) / WAVES;
-      }
-      cp.nib = (uint32_t)ni;
-      launch_combo<NV, MODE>((unsigned)(ni + ne), stream, cp, dp.nlist);
-      KX_HIP_CHECK(hipGetLastError());
-      if (s < nch) {
-        const unsigned gg = (unsigned)((cp.ix.g_hi - cp.ix.g_lo + WAVES - 1) / WAVES);
-        hipLaunchKernelGGL((group_kernel<NV, MODE>), dim3(gg), dim3(NT), 0, stream, cp.ix);
-        KX_HIP_CHECK(hipGetLastError());
-        hipLaunchKernelGGL((chain_kernel<NV, MODE>), dim3(1), dim3(CT), 0, stream, cp.ix);
-        KX_HIP_CHECK(hipGetLastError());
-      }
-    }
-    hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(64), 0, stream, dp.status, dp.errkey, dp.overflow, dp.nstop,
-                       dp.offsets, dp.n, dp.redo_n);
-    KX_HIP_CHECK(hipGetLastError());
     return KX_OK;
   }
   const uint64_t cht = pp && pp->aux ? pp->chunk_tiles : 0;
@@ -4490,66 +4209,11 @@ int launch_t(const DecParams& dp0, const WsLayout& L, void* ws, hipStream_t stre
     KX_HIP_CHECK(hipGetLastError());
     return KX_OK;
   }
-  if constexpr (MODE == M_THRIFT && NV > 0) {
-    // known offsets, canonical plan: the length gather instead of the index pass's window, checked by the
-    // emit pass; on any difference the gated repair pass (index -> group -> chain -> emit) runs
-    // opt-in (KX_GATHER=1, read per call): measured no faster than the index pass (0.47 vs 0.60 ms for 16 M
-    // R2 records) while its emit pass must validate every record, where the index pass lets the emit pass
-    // of an all-canonical tile use the plan alone
-    const char* genv = getenv("KX_GATHER");
-    if (genv && atoi(genv) && !dp.direct && dp.offsets && dp.fast && dp.fp.ok && !dp.diag) {
-      DecParams c = dp;
-      c.gcheck = dp.redo_n + 1;
-      hipLaunchKernelGGL((gather_kernel<NV>), dim3(grid), dim3(NT), 0, stream, c);
-      KX_HIP_CHECK(hipGetLastError());
-      hipLaunchKernelGGL((group_kernel<NV, MODE>), dim3(ggrid), dim3(NT), 0, stream, c);
-      KX_HIP_CHECK(hipGetLastError());
-      hipLaunchKernelGGL((chain_kernel<NV, MODE>), dim3(1), dim3(CT), 0, stream, c);
-      KX_HIP_CHECK(hipGetLastError());
-      launch_emit<NV, MODE>(dim3(grid), stream, c);
-      KX_HIP_CHECK(hipGetLastError());
-      DecParams rp = dp;
-      rp.gate = dp.redo_n + 1;
-      hipLaunchKernelGGL(gate_rearm_kernel, dim3(1), dim3(64), 0, stream, rp.gate, dp.overflow);
-      KX_HIP_CHECK(hipGetLastError());
-      hipLaunchKernelGGL((index_kernel<NV, MODE>), dim3(grid), dim3(NT), 0, stream, rp);
-      KX_HIP_CHECK(hipGetLastError());
-      hipLaunchKernelGGL((group_kernel<NV, MODE>), dim3(ggrid), dim3(NT), 0, stream, rp);
-      KX_HIP_CHECK(hipGetLastError());
-      hipLaunchKernelGGL((chain_kernel<NV, MODE>), dim3(1), dim3(CT), 0, stream, rp);
-      KX_HIP_CHECK(hipGetLastError());
-      launch_emit<NV, MODE>(dim3(grid), stream, rp);
-      KX_HIP_CHECK(hipGetLastError());
-      hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(64), 0, stream, dp.status, dp.errkey, dp.overflow, dp.nstop,
-                         dp.offsets, dp.n, dp.redo_n);
-      KX_HIP_CHECK(hipGetLastError());
-      return KX_OK;
-    }
-  }
   if (!dp.direct) {
-    static int ncu_dev[64];   // CU count + 1 per device ordinal (0: not yet asked)
-    const char* e = getenv("KX_INDEX_PF");
-    const int pf = e ? atoi(e) : 0;
-    int ncu = 0;
-    if (pf > 0) {
-      int dev = 0, v = 0;
-      if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64) {
-        if (!ncu_dev[dev] && hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
-          ncu_dev[dev] = v + 1;
-        ncu = ncu_dev[dev] ? ncu_dev[dev] - 1 : 0;
-      }
-    }
-    int lr = launch_fast_index<NV, MODE>(dp, grid, stream);
+    const int lr = launch_fast_index<NV, MODE>(dp, grid, stream);
     if (lr < 0) return KX_ERR_HIP;
-    if (lr > 0) goto indexed;
-    if (pf > 0 && !dp.offsets && ncu > 0 && !dp.diag) {
-      const unsigned pgrid = (unsigned)kmin64(grid, (uint64_t)ncu * (uint64_t)pf);
-      hipLaunchKernelGGL((index_kernel_pf<NV, MODE>), dim3(pgrid), dim3(NT), 0, stream, dp);
-    } else {
-      hipLaunchKernelGGL((index_kernel<NV, MODE>), dim3(grid), dim3(NT), 0, stream, dp);
-    }
+    if (lr == 0) hipLaunchKernelGGL((index_kernel<NV, MODE>), dim3(grid), dim3(NT), 0, stream, dp);
     KX_HIP_CHECK(hipGetLastError());
-  indexed:
     hipLaunchKernelGGL((group_kernel<NV, MODE>), dim3(ggrid), dim3(NT), 0, stream, dp);
     KX_HIP_CHECK(hipGetLastError());
     if (int rc = launch_chain<NV, MODE>(dp, stream)) return rc;
@@ -4578,10 +4242,8 @@ done:
 unsigned long long* kx_phase_buf(int diag);
 namespace {
 void fill_diag_flags(DecParams& dp) {
-  static int nolds = -1, diag = -1;
-  if (nolds < 0) { const char* e = getenv("KX_NOLDS"); nolds = e && e[0] == '1'; }
-  if (diag < 0) { const char* e = getenv("KX_DIAG"); diag = e ? atoi(e) : 0; }
-  dp.nolds = nolds;
+  const int diag = kx_knob(KXK_DIAG);
+  dp.nolds = kx_knob(KXK_NOLDS) == 1;
   dp.diag = diag;
   dp.phase = kx_phase_buf(diag);
 }
@@ -4640,9 +4302,9 @@ KX_DEF(16, M_THRIFT_LS)
 KX_EXT(16, M_THRIFT_LS)
 #endif
 #if KX_OWNS(4)
-KX_DEF(0, M_PB) KX_DEF(1, M_PB) KX_DEF(2, M_PB)
+KX_DEF(0, M_PB) KX_DEF(1, M_PB) KX_DEF(2, M_PB) KX_DEF(0, M_PBB)
 #else
-KX_EXT(0, M_PB) KX_EXT(1, M_PB) KX_EXT(2, M_PB)
+KX_EXT(0, M_PB) KX_EXT(1, M_PB) KX_EXT(2, M_PB) KX_EXT(0, M_PBB)
 #endif
 #if KX_OWNS(5)
 KX_DEF(4, M_PB) KX_DEF(8, M_PB)
@@ -4728,13 +4390,9 @@ int kx_launch_decode(const KxProgram* dprog, const KxProgram& hprog, const uint8
   dp.all_view = 1;
   for (uint32_t v = 0; v < hprog.nvar; v++) dp.all_view &= (int)((cols.view >> hprog.var_col[v]) & 1);
   {
-    static int fast_env = -1;
-    if (fast_env < 0) { const char* e = getenv("KX_FAST"); fast_env = e ? atoi(e) : 1; }
     // concatenated: the fast index path; known offsets: the fast record measure (index) pass
-    dp.fast = fast_env && !pb && hprog.nsteps && (offsets || hprog.sig_len == 3);
-    static int fp_env = -1;
-    if (fp_env < 0) { const char* e = getenv("KX_FASTPLAN"); fp_env = e ? atoi(e) : 1; }
-    if (dp.fast && fp_env) kxp_fast_plan(hprog, dp.fp);
+    dp.fast = kx_knob(KXK_FAST) && !pb && hprog.nsteps && (offsets || hprog.sig_len == 3);
+    if (dp.fast && kx_knob(KXK_FASTPLAN)) kxp_fast_plan(hprog, dp.fp);
     if (dp.fast && !pb && !offsets) {
       kxp_emit_plan(hprog, dp.ep);
       // every var slot is a string, or a numeric list absent from the plan (its records hold none): the
@@ -4777,9 +4435,7 @@ int kx_launch_split(const KxProgram* dprog, const KxProgram* hprog, const uint8_
   }
   dp.prog = (const KAS KxProgram*)dprog;
   dp.winb = win_bytes(in_len, n);
-  static int fast_env = -1;
-  if (fast_env < 0) { const char* e = getenv("KX_FAST"); fast_env = e ? atoi(e) : 1; }
-  dp.fast = fast_env && hprog->nsteps && hprog->sig_len == 3;
+  dp.fast = kx_knob(KXK_FAST) && hprog->nsteps && hprog->sig_len == 3;
   bool ls = false;
   for (uint32_t f = 0; f < hprog->nfields; f++) ls |= hprog->f[f].kind == KXP_K_LSTRUCT;
   return ls ? launch_nv<M_THRIFT_LS>(dp, L, ws, stream, hprog->nvar, nullptr)
@@ -4811,7 +4467,7 @@ int kx_launch_pb_frames(const uint8_t* in, uint64_t in_len, uint64_t n, uint64_t
   dp.winb = TILE + HALO + 16;
   const WsLayout L = ws_layout(1, in_len, nullptr, n);
   if (ws_size < L.total) return KX_ERR_INVALID_ARG;
-  return kx_dec_launch<0, M_FRAME>(&dp, &L, ws, stream, nullptr);
+  return kx_dec_launch<0, M_PBB>(&dp, &L, ws, stream, nullptr);
 }
 
 int kx_launch_frames(const uint8_t* in, uint64_t in_len, uint64_t n, uint64_t max_payload, uint64_t* frame_offsets,

@@ -1018,20 +1018,15 @@ int kx_launch_encode(const KxProgram* dprog, const KxProgram& hprog, const KxLau
   ep.prog = dprog; ep.cols = cols; ep.n = n; ep.out = out; ep.out_cap = out_cap;
   ep.sizes_out = sizes_out; ep.offsets_out = offsets_out; ep.status = status;
   ep.nblocks = (n + RB - 1) / RB;
-  {
-    const char* e = getenv("KX_ENC_DIRECT");
-    ep.direct = e ? atoi(e) : 0;
-    const char* w = getenv("KX_ENC_WCU");
-    ep.wcu = w ? atoi(w) : 16;
-  }
+  ep.direct = kx_knob(KXK_ENC_DIRECT);
+  ep.wcu = kx_knob(KXK_ENC_WCU);
   if (ws_size < kx_encode_ws_bytes(n)) return KX_ERR_INVALID_ARG;
   ep.block_tot = (uint64_t*)ws;
   if (status) KX_HIP_CHECK(hipMemsetAsync(status, 0, sizeof(kx_status), stream));
   bool ls = false;
   for (uint32_t f = 0; f < hprog.nfields; f++) ls |= hprog.f[f].kind == KXP_K_LSTRUCT;
-  static int canon_env = -1;  // KX_ENC_CANON=0: the generic sizes and writer for every record (A/B)
-  if (canon_env < 0) { const char* e = getenv("KX_ENC_CANON"); canon_env = e ? atoi(e) : 1; }
-  const bool canon = canon_env && !pb && !ls && hprog.nsteps > 0;
+  // KX_ENC_CANON=0: the generic sizes and writer for every record (A/B)
+  const bool canon = kx_knob(KXK_ENC_CANON) && !pb && !ls && hprog.nsteps > 0;
   if (ls) hipLaunchKernelGGL((size_kernel<true, false>), dim3((unsigned)ep.nblocks), dim3(NT), 0, stream, ep);
   else if (canon) hipLaunchKernelGGL((size_kernel<false, true>), dim3((unsigned)ep.nblocks), dim3(NT), 0, stream, ep);
   else hipLaunchKernelGGL((size_kernel<false, false>), dim3((unsigned)ep.nblocks), dim3(NT), 0, stream, ep);

@@ -7,6 +7,7 @@
 
 #include "../../include/kxcodec.h"
 #include "kx_program.h"
+#include "kx_knobs.h"
 
 // 64-bit min/max (HIP's min()/max() on mixed unsigned long / unsigned long long picks a double overload)
 __host__ __device__ __forceinline__ uint64_t kmin64(uint64_t a, uint64_t b) { return a < b ? a : b; }
@@ -32,8 +33,6 @@ struct kx_schema {
 // emit of chunk k - 1 run on the caller's stream, so emit re-reads a chunk the index pass has just
 // pulled through the Infinity Cache. Events order the two streams (rings of KX_PIPE_EV).
 #define KX_PIPE_EV 8
-#define KX_COMBO_MB_DEFAULT 0  // KX_COMBO_MB: chunk MiB of the one-stream index(k) + emit(k - 1) schedule
-#define KX_CHUNK_MB_DEFAULT 0  // measured: chunking is slower at every size
 struct KxPipe {
   hipStream_t aux = nullptr;
   hipEvent_t fork = nullptr;
@@ -41,7 +40,6 @@ struct KxPipe {
   hipEvent_t ev_emit[KX_PIPE_EV] = {};  // chunk k emitted (caller's stream) -> throttles aux
   uint64_t chunk_tiles = 0;             // tiles per chunk (a multiple of 64), 0 = one chunk
   int ahead = 1;                        // chunks the index pass may run ahead of emit
-  uint64_t combo_tiles = 0;             // one-stream schedule: index(k) + emit(k - 1) per launch (0: off)
 };
 
 #define KX_HOST_CH 16   // record-range chunks of the kx_host_* pipelines

@@ -559,36 +559,3 @@ def case_coop_lists(dec, oracle, et, w, mode, n=1000):
     assert_columns_equal(cols, cs, infos, n, check_presence=False)
 
 
-# ---- known offsets: the length gather (kx_decode.hip gather_kernel) and its checked repair ----
-GATHER_CASES = ["r2", "r3", "noncanonical", "error"]
-
-
-def case_offsets_gather(dec, oracle, case, n=3000):
-    import os
-    os.environ["KX_GATHER"] = "1"   # opt-in, read per call
-    try:
-        _case_offsets_gather(dec, oracle, case, n)
-    finally:
-        del os.environ["KX_GATHER"]
-
-
-def _case_offsets_gather(dec, oracle, case, n):
-    """known offsets on a canonical plan: the length gather replaces the index window (kx_status.diag[2] = 2);
-    records off the plan make the checking emit pass run the gated repair (diag[2] = 3); parity either way.
-    A failing record counts as empty both ways, so it needs no repair."""
-    if case in ("r2", "r3"):
-        sch = S.SCHEMAS[case]()
-        cs = synth.GENERATORS[case](n, start=5)
-        rc, wire, offs = oracle.encode(sch, cs)
-    else:
-        sch = S.schema_r2()
-        rng = np.random.default_rng(3)
-        if case == "noncanonical":
-            recs = [r2_record(oracle, rng, order=list(rng.permutation(10)) if i == n // 2 else None)
-                    for i in range(n)]
-        else:
-            recs = [r2_record(oracle, rng) for _ in range(n)]
-            recs[n // 3] = rec_bytes(oracle, [(A.T_STRING, 9, bytes.fromhex("fffffff0"))])
-        wire, offs = concat(recs)
-    cols, st = check_decode(dec, oracle, sch, wire, n, offsets=offs)
-    assert st.diag[2] == (3 if case == "noncanonical" else 2), (case, st.diag[0], st.diag[1], st.diag[2])

@@ -12,14 +12,11 @@ sed -e 's/^#define LDS __attribute__((address_space(3)))/#define LDS/' \
     -e 's/^#define GLB __attribute__((address_space(1)))/#define GLB/' \
     -e 's/^#define KAS __attribute__((address_space(4))).*/#define KAS/' \
     -e 's/^#define KX_PARAMS() .*/#define KX_PARAMS() (dp_)/' \
-    -e 's/^#define KX_CPARAMS() .*/#define KX_CPARAMS() (cp_)/' \
     -e 's/__attribute__((amdgpu_waves_per_eu([0-9]*))) //' \
     -e 's/asm volatile("s_waitcnt vmcnt(0)" ::: "memory");/emu_wait_vmcnt0();/' \
     -e 's/asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");/emu_wait_vmcnt0();/' \
     -e 's/asm volatile("s_mov_b32 %0, 0" : "=s"(z));/z = 0;/' \
     -e 's|^  return \*(const GLB uint32_t\*)A;  // input tail dword$|  return emu_gdword(A, end);|' \
-    -e 's/asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WIN_LOADS) : "memory");/emu_wait_vmcnt0();/' \
-    -e 's/^  asm volatile("s_mov_b32 m0, %0.*offen lds".*$/  emu_dma_lds16(rs, dst, voff, soff); (void)m0v;/' \
     $ROOT/kitex_amd/csrc/kx_decode.hip > $OUT/kx_decode_emu.cpp
 CXX=${CXX:-/opt/rocm/lib/llvm/bin/clang++}
 FLAGS="-std=c++17 -O1 -g -fPIC -Wno-unknown-attributes -Wno-unused-function -I. -I$ROOT/kitex_amd/csrc ${EMU_EXTRA:-}"
@@ -27,6 +24,7 @@ $CXX $FLAGS -c $OUT/kx_decode_emu.cpp -o $OUT/kx_decode_emu.o
 cp $ROOT/kitex_amd/csrc/kx_crc.hip $OUT/kx_crc_emu.cpp
 $CXX $FLAGS -c $OUT/kx_crc_emu.cpp -o $OUT/kx_crc_emu.o
 $CXX $FLAGS -c $ROOT/kitex_amd/csrc/kx_schema.cpp -o $OUT/kx_schema.o
+$CXX $FLAGS -c $ROOT/kitex_amd/csrc/kx_knobs.cpp -o $OUT/kx_knobs.o
 $CXX $FLAGS -c $ROOT/kitex_amd/csrc/kx_nested_schema.cpp -o $OUT/kx_nested_schema.o
 $CXX $FLAGS -c nested_host.cpp -o $OUT/nested_host.o
 $CXX $FLAGS -c emu_rt.cpp -o $OUT/emu_rt.o

@@ -30,7 +30,8 @@ def lib():
     if _lib is None:
         csrc = os.path.join(HERE, "..", "..", "kitex_amd", "csrc")
         srcs = [os.path.join(csrc, f) for f in ("kx_decode.hip", "kx_crc.hip", "kx_nested.h", "kx_nested_schema.cpp",
-                                                "kx_schema.cpp", "kx_internal.h")] + \
+                                                "kx_schema.cpp", "kx_internal.h", "kx_knobs.cpp",
+                                                "kx_knobs.h")] + \
             [os.path.join(HERE, f) for f in ("emu_driver.cpp", "emu_rt.cpp", "nested_host.cpp",
                                              os.path.join("hip", "hip_runtime.h"))]
         import fcntl

@@ -54,9 +54,6 @@ extern "C" int emu_decode(const kx_struct_desc* structs, uint32_t nstructs, cons
     const char* a = getenv("KX_EMU_AHEAD");
     pipe.ahead = a ? atoi(a) : 1;
     pipe.aux = (hipStream_t)&pipe;  // any non-null handle
-    // KX_EMU_COMBO = tiles per chunk of the one-stream index(k) + emit(k - 1) schedule
-    const char* cb = getenv("KX_EMU_COMBO");
-    pipe.combo_tiles = cb ? strtoull(cb, nullptr, 10) : 0;
     rc = kx_launch_decode(&s.prog, s.prog, in, in_len, offsets, n, lc, record_status, status, ws, ws_cap, epoch,
                           nullptr, mode == 2, nullptr, nullptr, &pipe);
   }

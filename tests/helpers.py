@@ -4,6 +4,25 @@ import numpy as np
 from kitex_amd import _abi as A
 
 
+def knob(L, name: str, value: int, default: int):
+    """set one of the library's tuning switches (kx_knobs.h, read from the environment once per process) for
+    the duration of a `with` block, through the test-only kx_debug_set_knob of library L (libkxcodec or
+    the emulator)"""
+    import contextlib
+    import ctypes as C
+
+    @contextlib.contextmanager
+    def cm():
+        L.kx_debug_set_knob.argtypes = [C.c_char_p, C.c_int]
+        L.kx_debug_set_knob.restype = C.c_int
+        assert L.kx_debug_set_knob(name.encode(), value) == 0, name
+        try:
+            yield
+        finally:
+            L.kx_debug_set_knob(name.encode(), default)
+    return cm()
+
+
 def to_np(x):
     if isinstance(x, np.ndarray):
         return x

@@ -74,10 +74,15 @@ def test_emu_slot_overflow(edec, oracle):
 
 
 @pytest.mark.parametrize("case", ["r1", "r2", "r3", "pb", "containers", "noncanonical", "empty", "ragged", "skip"])
-def test_emu_slotcap_64(edec, oracle, case, monkeypatch):
+def test_emu_slotcap_64(edec, oracle, case):
     """64 record-start slots per tile (KX_SLOTCAP): every record past a tile's first 64 is emitted one per
     round from the previous record's end"""
-    monkeypatch.setenv("KX_SLOTCAP", "64")
+    from tests.helpers import knob
+    with knob(emu.lib(), "KX_SLOTCAP", 64, 0):
+        _slotcap_case(edec, oracle, case)
+
+
+def _slotcap_case(edec, oracle, case):
     if case in ("r1", "r2", "r3"):
         DC.case_concat(edec, oracle, case, 3000)
     elif case == "pb":
@@ -208,13 +213,6 @@ def test_emu_chunked(edec, oracle, case, ahead, monkeypatch):
     DC.case_chunked(edec, oracle, case)
 
 
-@pytest.mark.parametrize("case", DC.CHUNK_CASES)
-def test_emu_combo(edec, oracle, case, monkeypatch):
-    """the one-stream schedule: index of chunk k and emit of chunk k - 1 in one launch (64-tile chunks)"""
-    monkeypatch.setenv("KX_EMU_COMBO", "64")
-    DC.case_chunked(edec, oracle, case)
-
-
 # ---- framing sniff (M_FRAME walker, kx_launch_frames) ----
 def _emu_scan(threads=8):
     def scan(wire, n, mx):
@@ -234,14 +232,6 @@ def test_emu_views(edec, oracle, case):
     DC.case_views(edec, oracle, case)
 
 
-@pytest.mark.parametrize("case", ["r2", "r3", "error", "truncated", "noncanonical", "pb", "containers"])
-def test_emu_index_prefetch(edec, oracle, case, monkeypatch):
-    """the persistent double-buffered index pass (KX_INDEX_PF=2: 2 workgroups per emulated CU, each
-    wave walking many tiles while the next one's DMA is in flight)"""
-    monkeypatch.setenv("KX_INDEX_PF", "2")
-    DC.case_chunked(edec, oracle, case)
-
-
 @pytest.mark.parametrize("name,n", [("r1", 20000), ("r2", 15000), ("r3", 4000)])
 def test_emu_fast_index_path_taken(edec, oracle, name, n):
     """canonical batches: every tile but the last few takes the fast index path (status diag[2] counts
@@ -256,11 +246,6 @@ def test_emu_fast_index_path_taken(edec, oracle, name, n):
     assert st.diag[2] <= 2, (st.diag[2], tiles)
     rc, exp, est, _ = oracle.decode(sch, wire, n)
     assert_columns_equal(cols, exp, infos, n)
-
-
-@pytest.mark.parametrize("case", DC.GATHER_CASES)
-def test_emu_offsets_length_gather(edec, oracle, case):
-    DC.case_offsets_gather(edec, oracle, case)
 
 
 def test_emu_long_strings(edec, oracle):

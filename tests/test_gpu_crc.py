@@ -105,12 +105,13 @@ def test_decode_frames_with_crc32_check(torch, oracle, form, monkeypatch):
     n = 6000
     sch, recs, frames, wire, fo, exp = CC.crc_batch(n, CC.MODES_PASS + CC.MODES_FAIL)
     assert int(np.nonzero(exp)[0][0]) < 8
-    if form == "separate_no_fo":
-        monkeypatch.setenv("KX_CRC_FUSED", "0")
+    from kitex_amd._lib import lib
+    from tests.helpers import knob
     cdc = ThriftCodec(sch)
     buf = torch.from_numpy(wire).to("cuda:0")
-    res = cdc.UnmarshalFrames(buf, n, raise_on_error=False, crc32_check=True,
-                              frame_offsets=form == "fused")
+    with knob(lib(), "KX_CRC_FUSED", 0 if form == "separate_no_fo" else 1, 1):
+        res = cdc.UnmarshalFrames(buf, n, raise_on_error=False, crc32_check=True,
+                                  frame_offsets=form == "fused")
     st = res.read_status()
     rs = to_np(res.record_status)[:n]
     assert np.array_equal(rs, exp)
