@@ -54,6 +54,10 @@
 #define KXN_STACK 32          // walker frames (struct nesting + containers)
 #define KXN_SKIP_DEPTH 64     // codec_apache.go:167
 #define KXN_FMAP 32           // field ids 0 .. 31: direct lookup per struct (KxnProgram.fmap)
+// A walk without snapshots (snap == nullptr: the common, canonical record) met a field a second time in one
+// instance: the record needs the careful walk (snapshots, and in the write pass clipping at the record's
+// extents). Internal to the walker's callers, never a status code.
+#define KXN_REPEAT 0x7e
 
 enum : uint8_t { KN_SCALAR = 1, KN_STRING = 2, KN_RAW = 3, KN_STRUCT = 4, KN_LIST = 5, KN_MAP = 6 };
 
@@ -437,8 +441,16 @@ struct KxnState {
   uint64_t seen[3];   // seen masks per level
   uint64_t pres[3];   // presence words per level
   bool live[3];       // the open instance lies inside the record's extent of its domain (writes allowed)
-  const uint64_t* lim;  // W: per cursor, the end of the record's extent
+  const uint64_t* lim;  // W, careful walk: per cursor, the end of the record's extent (nullptr: the walk
+                        // has no repeated field, so it never leaves the extents the measure pass found)
 };
+
+// units of cursor k a write at cursor value c may fill (all of n without clipping)
+KXN_HD uint64_t kxn_room(const KxnState& S, int k, uint64_t c, uint64_t n) {
+  if (!S.lim) return n;
+  const uint64_t room = S.lim[k] > c ? S.lim[k] - c : 0;
+  return n < room ? n : room;
+}
 
 // an instance of root R at index e starts: offsets entries, scalar defaults
 template <bool W>
@@ -449,7 +461,7 @@ KXN_HD void kxn_inst_start(const KxnProgram& P, const KxnCols& C, int R, uint64_
   S.seen[RT.level] = 0;
   S.pres[RT.level] = 0;
   if (!W) return;
-  S.live[RT.level] = RT.level == 0 || e < S.lim[RT.dcur];
+  S.live[RT.level] = RT.level == 0 || !S.lim || e < S.lim[RT.dcur];
   if (!S.live[RT.level]) return;
   for (int k = RT.ent_lo; k < RT.ent_hi; k++) {
     const KxnEntry& E = P.ent[k];
@@ -468,7 +480,7 @@ KXN_HD void kxn_inst_end(const KxnProgram& P, const KxnCols& C, int R, uint64_t*
     if ((S.seen[L] >> D.sbit) & 1) continue;
     if (W)
       for (uint32_t j = 0; j < D.len; j++)
-        if (cur[D.cur] + j < S.lim[D.cur]) ((KXN_G(uint8_t)*)C.data[D.col])[cur[D.cur] + j] = P.defb[D.off + j];
+        if (!S.lim || cur[D.cur] + j < S.lim[D.cur]) ((KXN_G(uint8_t)*)C.data[D.col])[cur[D.cur] + j] = P.defb[D.off + j];
     cur[D.cur] += D.len;
   }
   if (!W || !S.live[L]) return;
@@ -490,12 +502,7 @@ KXN_HD int kxn_value(const KxnProgram& P, const KxnCols& C, B b, uint64_t len, u
     uint64_t e = *q;
     const int rc = kxn_skip(b, len, &e, KX_T_STRUCT, KXN_SKIP_DEPTH);
     if (rc) return rc;
-    if (W) {
-      uint8_t* dst = (uint8_t*)C.data[N.col] + cur[N.cur];
-      const uint64_t room = S.lim[N.cur] > cur[N.cur] ? S.lim[N.cur] - cur[N.cur] : 0;
-      const uint64_t m = e - *q < room ? e - *q : room;
-      kxn_copy(dst, b + *q, m);
-    }
+    if (W) kxn_copy((uint8_t*)C.data[N.col] + cur[N.cur], b + *q, kxn_room(S, N.cur, cur[N.cur], e - *q));
     cur[N.cur] += e - *q;
     *q = e;
     return KX_OK;
@@ -516,11 +523,7 @@ KXN_HD int kxn_value(const KxnProgram& P, const KxnCols& C, B b, uint64_t len, u
   if (kind == KN_STRING) {                                   // ReadString: a copy
     const uint64_t l = (uint64_t)c;
     if (*q + 4 + l > len) return KX_ERR_EOF;
-    if (W) {
-      uint8_t* dst = (uint8_t*)C.data[N.col] + cur[N.cur];
-      const uint64_t room = S.lim[N.cur] > cur[N.cur] ? S.lim[N.cur] - cur[N.cur] : 0;
-      kxn_copy(dst, b + *q + 4, l < room ? l : room);
-    }
+    if (W) kxn_copy((uint8_t*)C.data[N.col] + cur[N.cur], b + *q + 4, kxn_room(S, N.cur, cur[N.cur], l));
     cur[N.cur] += l;
     *q += 4 + l;
     return KX_OK;
@@ -534,7 +537,9 @@ KXN_HD int kxn_value(const KxnProgram& P, const KxnCols& C, B b, uint64_t len, u
 }
 
 // FastRead of record r = b[0 .. len). cur: cursors (measure: from 0, write: at the record's bases);
-// lim (write): the ends of the record's extents; snap: KXN_MAX_SNAP slots. *used = bytes of the struct.
+// lim (write, careful walk): the ends of the record's extents; snap: KXN_MAX_SNAP slots, or nullptr for the
+// fast walk, which returns KXN_REPEAT at a field's second occurrence in one instance (the caller then walks
+// the record again with snapshots, and in the write pass with lim). *used = bytes of the struct.
 template <bool W, class B>
 KXN_HD int kxn_read_record(const KxnProgram& P, const KxnCols& C, B b, uint64_t len, uint64_t r,
                            uint64_t* cur, uint64_t* snap, uint64_t* used, const uint64_t* lim = nullptr) {
@@ -589,7 +594,9 @@ KXN_HD int kxn_read_record(const KxnProgram& P, const KxnCols& C, B b, uint64_t 
       const uint64_t bit = 1ull << G.sbit;
       const bool again = (S.seen[L] & bit) != 0;
       if (G.snap >= 0) {
-        if (again) {                                            // repeated: keep only this occurrence
+        if (!snap) {                                            // fast walk: no snapshot was taken
+          if (again) { rc = KXN_REPEAT; break; }
+        } else if (again) {                                     // repeated: keep only this occurrence
           for (int k = N.cur_lo; k < N.cur_hi; k++) cur[k] = snap[G.snap + k - N.cur_lo];
         } else {
           for (int k = N.cur_lo; k < N.cur_hi; k++) snap[G.snap + k - N.cur_lo] = cur[k];
@@ -906,12 +913,7 @@ KXN_HD int kxn_pb_value(const KxnProgram& P, const KxnCols& C, B b, uint64_t end
       if (rc) return rc;
       if (l > end - *q) return KX_ERR_EOF;
       if (N.kind == KN_STRING && N.pbk != KX_PB_BYTES && !kxn_utf8(b + *q, l)) return KX_ERR_INVALID_DATA;
-      if (W) {
-        uint8_t* dst = (uint8_t*)C.data[N.col] + cur[N.cur];
-        const uint64_t room = S.lim[N.cur] > cur[N.cur] ? S.lim[N.cur] - cur[N.cur] : 0;
-        const uint64_t m = l < room ? l : room;
-        kxn_copy(dst, b + *q, m);
-      }
+      if (W) kxn_copy((uint8_t*)C.data[N.col] + cur[N.cur], b + *q, kxn_room(S, N.cur, cur[N.cur], l));
       cur[N.cur] += l;
       *q += l;
       break;
@@ -933,7 +935,7 @@ KXN_HD int kxn_pb_value(const KxnProgram& P, const KxnCols& C, B b, uint64_t end
   return KX_OK;
 }
 
-// proto.Unmarshal of record r = b[0 .. len): same cursors / snapshots / clipping as kxn_read_record
+// proto.Unmarshal of record r = b[0 .. len): same cursors / snapshots / clipping / fast walk as kxn_read_record
 template <bool W, class B>
 KXN_HD int kxn_pb_read_record(const KxnProgram& P, const KxnCols& C, B b, uint64_t len, uint64_t r,
                               uint64_t* cur, uint64_t* snap, uint64_t* used, const uint64_t* lim = nullptr) {
@@ -982,8 +984,12 @@ KXN_HD int kxn_pb_read_record(const KxnProgram& P, const KxnCols& C, B b, uint64
       const KxnNode& V = P.node[Xm];
       const int k = num == 1 ? 0 : 1;
       if (V.kind == KN_STRING || V.kind == KN_RAW) {    // a repeated key / value string: the last one wins
-        if (F.seen & (1 << k)) cur[V.cur] = F.c0[k];
-        else F.c0[k] = cur[V.cur];
+        if (F.seen & (1 << k)) {
+          if (!snap) { rc = KXN_REPEAT; break; }        // fast walk: the careful one clips the first copy
+          cur[V.cur] = F.c0[k];
+        } else {
+          F.c0[k] = cur[V.cur];
+        }
       }
       F.seen |= (uint8_t)(1 << k);
       xend = F.end;
@@ -1055,8 +1061,13 @@ KXN_HD int kxn_pb_read_record(const KxnProgram& P, const KxnCols& C, B b, uint64
       continue;
     }
     if (N.kind == KN_STRING && G.snap >= 0) {           // singular string: the last occurrence wins
-      if (S.seen[L] & bit) cur[N.cur] = snap[G.snap];
-      else snap[G.snap] = cur[N.cur];
+      if (!snap) {
+        if (S.seen[L] & bit) { rc = KXN_REPEAT; break; }
+      } else if (S.seen[L] & bit) {
+        cur[N.cur] = snap[G.snap];
+      } else {
+        snap[G.snap] = cur[N.cur];
+      }
     }
     S.seen[L] |= bit;
     if (G.pbit >= 0) S.pres[L] |= 1ull << G.pbit;

@@ -72,8 +72,13 @@ __device__ __forceinline__ int extent(const NParams& p, uint64_t r, uint64_t* a,
   return (*a > *b || *b > p.in_len) ? KX_ERR_INVALID_ARG : 0;
 }
 
+// rcode[r]: the record's code, | RC_CAREFUL when it repeats a field (its walks need snapshots, and the write
+// walk clipping at its extents); RC_NONE: not decoded (concatenated, past the failing record)
+constexpr uint8_t RC_CAREFUL = 0x40, RC_NONE = 0xff;
+
 // the walk of record [a, b) (a per-lane LDS window over the record's bytes, refilled 32 bytes at a time,
-// measured slower: 7.8 / 21.0 ms for the measure / write passes against 7.2 / 15.6 ms)
+// measured slower: 7.8 / 21.0 ms for the measure / write passes against 7.2 / 15.6 ms).
+// snap == nullptr: the fast walk (KXN_REPEAT at a repeated field)
 template <bool W>
 __device__ __forceinline__ int walk(const NParams& p, const KxnProgram& P, uint64_t a, uint64_t b, uint64_t r,
                                    uint64_t* cur, uint64_t* snap, uint64_t* lim) {
@@ -89,13 +94,21 @@ __device__ __forceinline__ void measure_record(const NParams& p, const KxnProgra
   int rc = extent(p, r, &a, &b);
   if (rc < 0) {
     rc = 0;  // not decoded: empty
-    p.rcode[r] = 0xff;
+    p.rcode[r] = RC_NONE;
   } else {
     // (a per-lane 16-byte read-ahead block in registers measured slower: 55.7 vs 41.7 ms for 1 M Nesting
     // records, divergent refills and 164 VGPRs in the write pass)
-    if (!rc) rc = walk<false>(p, P, a, b, r, cur, snap, nullptr);
+    uint8_t careful = 0;
+    if (!rc) {
+      rc = walk<false>(p, P, a, b, r, cur, nullptr, nullptr);   // no snapshot stores: the common record
+      if (rc == KXN_REPEAT) {                                   // a repeated field: again, with snapshots
+        for (uint32_t k = 0; k < p.ncur; k++) cur[k] = 0;
+        rc = walk<false>(p, P, a, b, r, cur, snap, nullptr);
+        careful = RC_CAREFUL;
+      }
+    }
     if (!rc && p.concat && r < p.n && p.skip_st->code && r == p.skip_st->n_records) rc = p.skip_st->code;
-    p.rcode[r] = (uint8_t)rc;
+    p.rcode[r] = (uint8_t)rc | careful;
     if (rc) atomicMin(p.errkey, (unsigned long long)((r << 8) | (uint64_t)(rc & 0xff)));
   }
   for (uint32_t k = 0; k < p.ncur; k++) p.counts[(uint64_t)k * p.n + r] = rc ? 0u : (uint32_t)cur[k];
@@ -227,23 +240,31 @@ __global__ void check_kernel(NParams p) {
 // record r (of block b), lane = record
 __device__ __forceinline__ void write_record(const NParams& p, const KxnProgram& P, uint64_t b, uint64_t r,
                                              uint64_t* cur, uint64_t* lim, uint64_t* snap) {
-  const uint64_t rb1 = kmin64((b + 1) * RB, p.n);   // the block's end
-  // the record's cursor bases: the block base + the in-block prefix (bsum_kernel); its extent ends at the
-  // next record's prefix, or at the next block's base
-  for (uint32_t k = 0; k < p.ncur; k++) {
-    const uint64_t base = p.bsum[(uint64_t)k * p.nblk + b];
-    const uint32_t* c = p.counts + (uint64_t)k * p.n;
-    cur[k] = base + c[r];
-    lim[k] = r + 1 < rb1 ? base + c[r + 1] : (b + 1 < p.nblk ? p.bsum[(uint64_t)k * p.nblk + b + 1] : p.totals[k]);
-  }
-  const uint8_t rc = p.rcode[r];
+  // the record's cursor bases: the block base + the in-block prefix (bsum_kernel)
+  for (uint32_t k = 0; k < p.ncur; k++)
+    cur[k] = p.bsum[(uint64_t)k * p.nblk + b] + p.counts[(uint64_t)k * p.n + r];
+  const uint8_t raw = p.rcode[r];
+  const uint8_t rc = raw == RC_NONE ? RC_NONE : (uint8_t)(raw & ~RC_CAREFUL);
   uint64_t a = 0, e = 0;
   if (rc == 0 && extent(p, r, &a, &e) == 0) {
-    (void)walk<true>(p, P, a, e, r, cur, snap, lim);
+    if (raw & RC_CAREFUL) {
+      // a record that repeats a field: its extents end at the next record's prefix, or at the next block's
+      // base, and every write is clipped to them (what a replaced occurrence wrote past them is the next
+      // record's)
+      const uint64_t rb1 = kmin64((b + 1) * RB, p.n);   // the block's end
+      for (uint32_t k = 0; k < p.ncur; k++) {
+        const uint64_t base = p.bsum[(uint64_t)k * p.nblk + b];
+        lim[k] = r + 1 < rb1 ? base + p.counts[(uint64_t)k * p.n + r + 1]
+                             : (b + 1 < p.nblk ? p.bsum[(uint64_t)k * p.nblk + b + 1] : p.totals[k]);
+      }
+      (void)walk<true>(p, P, a, e, r, cur, snap, lim);
+    } else {   // the fast walk writes only inside the record's extents
+      (void)walk<true>(p, P, a, e, r, cur, nullptr, nullptr);
+    }
   } else {
     kxn_failed_record(P, *p.C, r, cur);
   }
-  if (p.record_status && !p.concat) p.record_status[r] = rc == 0xff ? 0 : rc;
+  if (p.record_status && !p.concat) p.record_status[r] = rc == RC_NONE ? 0 : rc;
 }
 
 // one record per thread: workgroup w holds records [w·NTD, (w + 1)·NTD) of block w / (RB / NTD) (a workgroup

@@ -77,16 +77,24 @@ extern "C" int emu_nested_decode(const kx_struct_desc* structs, uint32_t ns, con
   }
   // measure
   std::vector<uint64_t> cnt((size_t)P.ncur * n, 0);
-  std::vector<uint8_t> code(n, 0);
+  std::vector<uint8_t> code(n, 0), careful(n, 0);
   std::vector<uint64_t> cur(KXN_MAX_CUR), lim(KXN_MAX_CUR), snap(KXN_MAX_SNAP);
   uint64_t first = n;
   for (uint64_t r = 0; r < n; r++) {
     if (!offsets && (r > nok || (r == nok && !skip_rc))) { code[r] = 0xff; continue; }
     for (uint32_t k = 0; k < P.ncur; k++) cur[k] = 0;
     uint64_t used = 0;
-    int e = (a[r] > b[r] || b[r] > in_len) ? KX_ERR_INVALID_ARG
-            : P.pb ? kxn_pb_read_record<false>(P, C, in + a[r], b[r] - a[r], r, cur.data(), snap.data(), &used)
-                   : kxn_read_record<false>(P, C, in + a[r], b[r] - a[r], r, cur.data(), snap.data(), &used);
+    // as the device: the fast walk (no snapshots), and for a record that repeats a field the careful walk
+    auto walk = [&](uint64_t* sn) {
+      return P.pb ? kxn_pb_read_record<false>(P, C, in + a[r], b[r] - a[r], r, cur.data(), sn, &used)
+                  : kxn_read_record<false>(P, C, in + a[r], b[r] - a[r], r, cur.data(), sn, &used);
+    };
+    int e = (a[r] > b[r] || b[r] > in_len) ? KX_ERR_INVALID_ARG : walk(nullptr);
+    if (e == KXN_REPEAT) {
+      for (uint32_t k = 0; k < P.ncur; k++) cur[k] = 0;
+      e = walk(snap.data());
+      careful[r] = 1;
+    }
     if (!e && !offsets && skip_rc && r == nok) e = skip_rc;
     code[r] = (uint8_t)e;
     if (e) { if (r < first) first = r; continue; }
@@ -112,10 +120,12 @@ extern "C" int emu_nested_decode(const kx_struct_desc* structs, uint32_t ns, con
       lim[k] = cur[k] + cnt[(size_t)k * n + r];
     }
     uint64_t used = 0;
+    uint64_t* sn = careful[r] ? snap.data() : nullptr;   // the fast walk stays inside the record's extents
+    const uint64_t* li = careful[r] ? lim.data() : nullptr;
     if (code[r] == 0 && P.pb)
-      (void)kxn_pb_read_record<true>(P, C, in + a[r], b[r] - a[r], r, cur.data(), snap.data(), &used, lim.data());
+      (void)kxn_pb_read_record<true>(P, C, in + a[r], b[r] - a[r], r, cur.data(), sn, &used, li);
     else if (code[r] == 0)
-      (void)kxn_read_record<true>(P, C, in + a[r], b[r] - a[r], r, cur.data(), snap.data(), &used, lim.data());
+      (void)kxn_read_record<true>(P, C, in + a[r], b[r] - a[r], r, cur.data(), sn, &used, li);
     else kxn_failed_record(P, C, r, cur.data());
     if (rstat && offsets) rstat[r] = code[r] == 0xff ? 0 : code[r];
   }
