@@ -19,7 +19,7 @@ const KnobDef kDefs[KXK_N] = {
     {"KX_CHAIN_FAST", 1}, {"KX_EMIT_FAST", 1}, {"KX_FAST_NARROW", 1}, {"KX_FAST_SPLIT", 1}, {"KX_REDO_WG", 4},
     {"KX_FAST", 1},       {"KX_FASTPLAN", 1},  {"KX_SLOTCAP", 0},     {"KX_NOLDS", 0},      {"KX_DIAG", 0},
     {"KX_CRC_FUSED", 1},  {"KX_CRC_BLK", 8},   {"KX_ENC_DIRECT", 0},  {"KX_ENC_WCU", 16},   {"KX_ENC_CANON", 1},
-    {"KX_CHUNK_MB", 0},   {"KX_CHUNK_AHEAD", 1}};
+    {"KX_CHUNK_MB", 0},   {"KX_CHUNK_AHEAD", 1}, {"KX_NESTED_LDS", 1}};
 
 std::atomic<int> g_knob[KXK_N];
 std::once_flag g_once;

@@ -25,6 +25,7 @@ enum KxKnob {
   KXK_ENC_CANON,    // KX_ENC_CANON (1): canonical-plan sizes and writer
   KXK_CHUNK_MB,     // KX_CHUNK_MB (0): chunked two-stream decode pipeline
   KXK_CHUNK_AHEAD,  // KX_CHUNK_AHEAD (1)
+  KXK_NESTED_LDS,   // KX_NESTED_LDS (1): the nested walker's cursors in LDS (0: in scratch)
   KXK_N
 };
 

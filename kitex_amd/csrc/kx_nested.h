@@ -28,8 +28,10 @@
 
 #if defined(__HIPCC__)
 #define KXN_HD __host__ __device__ __forceinline__
+#define KXN_MHD __host__ __device__ __forceinline__   // member functions
 #else
 #define KXN_HD static inline
+#define KXN_MHD inline
 #endif
 // global memory through address-space-1 pointers on the device pass (column arrays, the input and the
 // output are all global): the column pointers come out of the KxnCols struct in device memory, which the
@@ -184,6 +186,17 @@ struct KxnCols {
   uint64_t cap[KX_MAX_COLUMNS][4];  // units of data, arr0 (n), arr1, arr2 (entries - 1)
   uint64_t owide;                 // bit c: 8-byte offsets
   uint64_t* presence;
+};
+
+// The walker's cursors, behind a small interface so that they can live where the caller wants them: a
+// plain array here (the host harness, the device's scratch fallback); on the device a per-lane column of
+// the workgroup's LDS (kx_nested.hip KxnCurL), which keeps them out of scratch.
+struct KxnCurP {
+  uint64_t* p;
+  KXN_MHD uint64_t operator[](int k) const { return p[k]; }
+  KXN_MHD void set(int k, uint64_t v) const { p[k] = v; }
+  KXN_MHD void add(int k, uint64_t d) const { p[k] += d; }
+  KXN_MHD uint64_t post_inc(int k) const { return p[k]++; }
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -453,9 +466,8 @@ KXN_HD uint64_t kxn_room(const KxnState& S, int k, uint64_t c, uint64_t n) {
 }
 
 // an instance of root R at index e starts: offsets entries, scalar defaults
-template <bool W>
-KXN_HD void kxn_inst_start(const KxnProgram& P, const KxnCols& C, int R, uint64_t e, const uint64_t* cur,
-                           KxnState& S) {
+template <bool W, class CU>
+KXN_HD void kxn_inst_start(const KxnProgram& P, const KxnCols& C, int R, uint64_t e, CU cur, KxnState& S) {
   const KxnRoot& RT = P.root[R];
   S.idx[RT.level] = e;
   S.seen[RT.level] = 0;
@@ -471,8 +483,8 @@ KXN_HD void kxn_inst_start(const KxnProgram& P, const KxnCols& C, int R, uint64_
 }
 
 // the instance ends: absent string fields take their defaults, the presence word is stored
-template <bool W>
-KXN_HD void kxn_inst_end(const KxnProgram& P, const KxnCols& C, int R, uint64_t* cur, KxnState& S) {
+template <bool W, class CU>
+KXN_HD void kxn_inst_end(const KxnProgram& P, const KxnCols& C, int R, CU cur, KxnState& S) {
   const KxnRoot& RT = P.root[R];
   const int L = RT.level;
   for (int k = RT.sdf_lo; k < RT.sdf_hi; k++) {
@@ -481,7 +493,7 @@ KXN_HD void kxn_inst_end(const KxnProgram& P, const KxnCols& C, int R, uint64_t*
     if (W)
       for (uint32_t j = 0; j < D.len; j++)
         if (!S.lim || cur[D.cur] + j < S.lim[D.cur]) ((KXN_G(uint8_t)*)C.data[D.col])[cur[D.cur] + j] = P.defb[D.off + j];
-    cur[D.cur] += D.len;
+    cur.add(D.cur, D.len);
   }
   if (!W || !S.live[L]) return;
   if (L == 0) {
@@ -493,9 +505,9 @@ KXN_HD void kxn_inst_end(const KxnProgram& P, const KxnCols& C, int R, uint64_t*
 
 // read one value of node X at b[*q] (scalars, strings, raw structs directly; structs / containers push a
 // frame). Element instances of containers are opened by the caller.
-template <bool W, class B>
+template <bool W, class B, class CU>
 KXN_HD int kxn_value(const KxnProgram& P, const KxnCols& C, B b, uint64_t len, uint64_t* q, int X,
-                     uint64_t* cur, KxnState& S, KxnFrame* stk, int* sp) {
+                     CU cur, KxnState& S, KxnFrame* stk, int* sp) {
   const KxnNode& N = P.node[X];
   const uint32_t kind = N.kind;
   if (kind == KN_RAW) {                                      // a recursive struct: its encoded bytes
@@ -503,7 +515,7 @@ KXN_HD int kxn_value(const KxnProgram& P, const KxnCols& C, B b, uint64_t len, u
     const int rc = kxn_skip(b, len, &e, KX_T_STRUCT, KXN_SKIP_DEPTH);
     if (rc) return rc;
     if (W) kxn_copy((uint8_t*)C.data[N.col] + cur[N.cur], b + *q, kxn_room(S, N.cur, cur[N.cur], e - *q));
-    cur[N.cur] += e - *q;
+    cur.add(N.cur, e - *q);
     *q = e;
     return KX_OK;
   }
@@ -524,7 +536,7 @@ KXN_HD int kxn_value(const KxnProgram& P, const KxnCols& C, B b, uint64_t len, u
     const uint64_t l = (uint64_t)c;
     if (*q + 4 + l > len) return KX_ERR_EOF;
     if (W) kxn_copy((uint8_t*)C.data[N.col] + cur[N.cur], b + *q + 4, kxn_room(S, N.cur, cur[N.cur], l));
-    cur[N.cur] += l;
+    cur.add(N.cur, l);
     *q += 4 + l;
     return KX_OK;
   }
@@ -540,9 +552,9 @@ KXN_HD int kxn_value(const KxnProgram& P, const KxnCols& C, B b, uint64_t len, u
 // lim (write, careful walk): the ends of the record's extents; snap: KXN_MAX_SNAP slots, or nullptr for the
 // fast walk, which returns KXN_REPEAT at a field's second occurrence in one instance (the caller then walks
 // the record again with snapshots, and in the write pass with lim). *used = bytes of the struct.
-template <bool W, class B>
+template <bool W, class B, class CU>
 KXN_HD int kxn_read_record(const KxnProgram& P, const KxnCols& C, B b, uint64_t len, uint64_t r,
-                           uint64_t* cur, uint64_t* snap, uint64_t* used, const uint64_t* lim = nullptr) {
+                           CU cur, uint64_t* snap, uint64_t* used, const uint64_t* lim = nullptr) {
   KxnFrame stk[KXN_STACK];
   KxnState S;
   S.lim = lim;
@@ -597,7 +609,7 @@ KXN_HD int kxn_read_record(const KxnProgram& P, const KxnCols& C, B b, uint64_t 
         if (!snap) {                                            // fast walk: no snapshot was taken
           if (again) { rc = KXN_REPEAT; break; }
         } else if (again) {                                     // repeated: keep only this occurrence
-          for (int k = N.cur_lo; k < N.cur_hi; k++) cur[k] = snap[G.snap + k - N.cur_lo];
+          for (int k = N.cur_lo; k < N.cur_hi; k++) cur.set(k, snap[G.snap + k - N.cur_lo]);
         } else {
           for (int k = N.cur_lo; k < N.cur_hi; k++) snap[G.snap + k - N.cur_lo] = cur[k];
         }
@@ -624,7 +636,7 @@ KXN_HD int kxn_read_record(const KxnProgram& P, const KxnCols& C, B b, uint64_t 
     if (N.kind == KN_LIST || F.phase == 0) {
       if (F.rem == 0) { sp--; continue; }
       F.rem--;
-      const uint64_t e = cur[N.cur]++;
+      const uint64_t e = cur.post_inc(N.cur);
       kxn_inst_start<W>(P, C, N.root, e, cur, S);
       F.open = 1;
       if (N.kind == KN_MAP) F.phase = 1;
@@ -641,7 +653,8 @@ KXN_HD int kxn_read_record(const KxnProgram& P, const KxnCols& C, B b, uint64_t 
 }
 
 // the instance of record r of a record that failed: defaults, empty extents, presence 0
-KXN_HD void kxn_failed_record(const KxnProgram& P, const KxnCols& C, uint64_t r, const uint64_t* cur) {
+template <class CU>
+KXN_HD void kxn_failed_record(const KxnProgram& P, const KxnCols& C, uint64_t r, CU cur) {
   const KxnRoot& RT = P.root[0];
   for (int k = RT.ent_lo; k < RT.ent_hi; k++) kxn_put_arr(C, P.ent[k].col, P.ent[k].arr, r, cur[P.ent[k].cur]);
   for (int k = RT.dfl_lo; k < RT.dfl_hi; k++) kxn_put_val(C, P.dfl[k].col, P.dfl[k].width, r, (uint64_t)P.dfl[k].v);
@@ -895,9 +908,9 @@ struct KxnPFrame {      // an open message (its fields) or map entry (fields 1 /
 
 // one value of node X (wire type matched) into the open instance of its level; a message value pushes a
 // frame (close: the root to end with it), a scalar / string value ends `close` at once
-template <bool W, class B>
+template <bool W, class B, class CU>
 KXN_HD int kxn_pb_value(const KxnProgram& P, const KxnCols& C, B b, uint64_t end, uint64_t* q, int X,
-                        uint64_t* cur, KxnState& S, KxnPFrame* stk, int* sp, int close) {
+                        CU cur, KxnState& S, KxnPFrame* stk, int* sp, int close) {
   const KxnNode& N = P.node[X];
   switch (N.kind) {
     case KN_SCALAR: {
@@ -914,7 +927,7 @@ KXN_HD int kxn_pb_value(const KxnProgram& P, const KxnCols& C, B b, uint64_t end
       if (l > end - *q) return KX_ERR_EOF;
       if (N.kind == KN_STRING && N.pbk != KX_PB_BYTES && !kxn_utf8(b + *q, l)) return KX_ERR_INVALID_DATA;
       if (W) kxn_copy((uint8_t*)C.data[N.col] + cur[N.cur], b + *q, kxn_room(S, N.cur, cur[N.cur], l));
-      cur[N.cur] += l;
+      cur.add(N.cur, l);
       *q += l;
       break;
     }
@@ -936,9 +949,9 @@ KXN_HD int kxn_pb_value(const KxnProgram& P, const KxnCols& C, B b, uint64_t end
 }
 
 // proto.Unmarshal of record r = b[0 .. len): same cursors / snapshots / clipping / fast walk as kxn_read_record
-template <bool W, class B>
+template <bool W, class B, class CU>
 KXN_HD int kxn_pb_read_record(const KxnProgram& P, const KxnCols& C, B b, uint64_t len, uint64_t r,
-                              uint64_t* cur, uint64_t* snap, uint64_t* used, const uint64_t* lim = nullptr) {
+                              CU cur, uint64_t* snap, uint64_t* used, const uint64_t* lim = nullptr) {
   KxnPFrame stk[KXN_STACK];
   KxnState S;
   S.lim = lim;
@@ -986,7 +999,7 @@ KXN_HD int kxn_pb_read_record(const KxnProgram& P, const KxnCols& C, B b, uint64
       if (V.kind == KN_STRING || V.kind == KN_RAW) {    // a repeated key / value string: the last one wins
         if (F.seen & (1 << k)) {
           if (!snap) { rc = KXN_REPEAT; break; }        // fast walk: the careful one clips the first copy
-          cur[V.cur] = F.c0[k];
+          cur.set(V.cur, F.c0[k]);
         } else {
           F.c0[k] = cur[V.cur];
         }
@@ -1014,7 +1027,7 @@ KXN_HD int kxn_pb_read_record(const KxnProgram& P, const KxnCols& C, B b, uint64
       if (wt == ewt) {
         S.seen[L] |= bit;
         if (G.pbit >= 0) S.pres[L] |= 1ull << G.pbit;
-        const uint64_t e = cur[N.cur]++;
+        const uint64_t e = cur.post_inc(N.cur);
         kxn_inst_start<W>(P, C, N.root, e, cur, S);
         xend = fend;
         xclose = N.root;
@@ -1027,7 +1040,7 @@ KXN_HD int kxn_pb_read_record(const KxnProgram& P, const KxnCols& C, B b, uint64
         if (G.pbit >= 0) S.pres[L] |= 1ull << G.pbit;
         const uint64_t pend = q + l;
         while (q < pend) {
-          const uint64_t e = cur[N.cur]++;
+          const uint64_t e = cur.post_inc(N.cur);
           kxn_inst_start<W>(P, C, N.root, e, cur, S);
           uint64_t v;
           if ((rc = kxn_pb_scalar(E, b, pend, &q, &v))) break;
@@ -1051,7 +1064,7 @@ KXN_HD int kxn_pb_read_record(const KxnProgram& P, const KxnCols& C, B b, uint64
       if (sp >= KXN_STACK) { rc = KX_ERR_DEPTH_LIMIT; break; }
       S.seen[L] |= bit;
       if (G.pbit >= 0) S.pres[L] |= 1ull << G.pbit;
-      const uint64_t e = cur[N.cur]++;
+      const uint64_t e = cur.post_inc(N.cur);
       kxn_inst_start<W>(P, C, N.root, e, cur, S);
       stk[sp++] = KxnPFrame{1, 0, G.node, N.root, 0, q + l, {0, 0}};
       continue;
@@ -1064,7 +1077,7 @@ KXN_HD int kxn_pb_read_record(const KxnProgram& P, const KxnCols& C, B b, uint64
       if (!snap) {
         if (S.seen[L] & bit) { rc = KXN_REPEAT; break; }
       } else if (S.seen[L] & bit) {
-        cur[N.cur] = snap[G.snap];
+        cur.set(N.cur, snap[G.snap]);
       } else {
         snap[G.snap] = cur[N.cur];
       }

@@ -76,20 +76,41 @@ __device__ __forceinline__ int extent(const NParams& p, uint64_t r, uint64_t* a,
 // walk clipping at its extents); RC_NONE: not decoded (concatenated, past the failing record)
 constexpr uint8_t RC_CAREFUL = 0x40, RC_NONE = 0xff;
 
+// The cursors of a workgroup's lanes in LDS, cursor k of lane t at [k * NTD + t] (a wave's accesses to one
+// cursor are 64 adjacent dwords): u32 values relative to a per-cursor base the workgroup shares (0 in the
+// measure pass; the 1024-record block's base in the write pass, whose in-block prefixes are u32 already,
+// bsum_kernel). In scratch, with 1 M lanes' walks in flight, every cursor access missed the caches: the
+// measure and write passes fetched 11 and 18 GB per call for 0.76 GB of input (round 5 PMC).
+#define KXN_LDS __attribute__((address_space(3)))
+constexpr int NTD = 512;   // threads per workgroup of the walker's passes
+struct KxnCurL {
+  KXN_LDS uint32_t* p;             // this lane's cursor 0
+  const KXN_LDS uint64_t* base;    // per cursor
+  __device__ uint64_t operator[](int k) const { return base[k] + p[k * NTD]; }
+  __device__ void set(int k, uint64_t v) const { p[k * NTD] = (uint32_t)(v - base[k]); }
+  __device__ void add(int k, uint64_t d) const { p[k * NTD] += (uint32_t)d; }
+  __device__ uint64_t post_inc(int k) const {
+    const uint32_t x = p[k * NTD];
+    p[k * NTD] = x + 1;
+    return base[k] + x;
+  }
+};
+
 // the walk of record [a, b) (a per-lane LDS window over the record's bytes, refilled 32 bytes at a time,
 // measured slower: 7.8 / 21.0 ms for the measure / write passes against 7.2 / 15.6 ms).
 // snap == nullptr: the fast walk (KXN_REPEAT at a repeated field)
-template <bool W>
+template <bool W, class CU>
 __device__ __forceinline__ int walk(const NParams& p, const KxnProgram& P, uint64_t a, uint64_t b, uint64_t r,
-                                   uint64_t* cur, uint64_t* snap, uint64_t* lim) {
+                                   CU cur, uint64_t* snap, uint64_t* lim) {
   uint64_t used = 0;
   return P.pb ? kxn_pb_read_record<W>(P, *p.C, p.in + a, b - a, r, cur, snap, &used, lim)
               : kxn_read_record<W>(P, *p.C, p.in + a, b - a, r, cur, snap, &used, lim);
 }
 
-__device__ __forceinline__ void measure_record(const NParams& p, const KxnProgram& P, uint64_t r, uint64_t* cur,
+template <class CU>
+__device__ __forceinline__ void measure_record(const NParams& p, const KxnProgram& P, uint64_t r, CU cur,
                                                uint64_t* snap) {
-  for (uint32_t k = 0; k < p.ncur; k++) cur[k] = 0;
+  for (uint32_t k = 0; k < p.ncur; k++) cur.set(k, 0);
   uint64_t a = 0, b = 0;
   int rc = extent(p, r, &a, &b);
   if (rc < 0) {
@@ -102,7 +123,7 @@ __device__ __forceinline__ void measure_record(const NParams& p, const KxnProgra
     if (!rc) {
       rc = walk<false>(p, P, a, b, r, cur, nullptr, nullptr);   // no snapshot stores: the common record
       if (rc == KXN_REPEAT) {                                   // a repeated field: again, with snapshots
-        for (uint32_t k = 0; k < p.ncur; k++) cur[k] = 0;
+        for (uint32_t k = 0; k < p.ncur; k++) cur.set(k, 0);
         rc = walk<false>(p, P, a, b, r, cur, snap, nullptr);
         careful = RC_CAREFUL;
       }
@@ -118,8 +139,7 @@ __device__ __forceinline__ void measure_record(const NParams& p, const KxnProgra
 // workgroup, measured slower on the MI355X: 62.8 vs 43.7 ms for 1 M Nesting records)
 // The program in LDS: the walk's table reads (nodes, fields, structs, roots, entries, defaults: a dozen
 // dependent reads per field) at LDS latency instead of through the vector L1 / L2. One copy per 512-thread
-// workgroup (31 KB: 5 workgroups fit a CU's LDS, more than the registers allow).
-constexpr int NTD = 512;
+// workgroup (31 KB).
 __device__ __forceinline__ const KxnProgram& lds_program(const KxnProgram* g, KxnProgram* s) {
   static_assert(sizeof(KxnProgram) % 4 == 0, "dword copy");
   const uint32_t* src = (const uint32_t*)g;
@@ -129,13 +149,24 @@ __device__ __forceinline__ const KxnProgram& lds_program(const KxnProgram* g, Kx
   return *s;
 }
 
+// LC: the cursors in LDS (dynamic shared memory: ncur bases, then ncur x NTD u32), else in scratch
+template <bool LC>
 __global__ void __launch_bounds__(NTD) measure_kernel(NParams p) {
   __shared__ KxnProgram sP;
-  const KxnProgram& P = lds_program(p.P, &sP);
+  extern __shared__ uint64_t dyn[];
+  if (LC)
+    for (uint32_t k = threadIdx.x; k < p.ncur; k += NTD) dyn[k] = 0;
+  const KxnProgram& P = lds_program(p.P, &sP);   // (its barrier also publishes the bases)
   const uint64_t r = (uint64_t)blockIdx.x * NTD + threadIdx.x;
   if (r >= p.n) return;
-  uint64_t cur[CUR], snap[SNAP];
-  measure_record(p, P, r, cur, snap);
+  uint64_t snap[SNAP];
+  if constexpr (LC) {
+    measure_record(p, P, r, KxnCurL{(KXN_LDS uint32_t*)(dyn + p.ncur) + threadIdx.x, (const KXN_LDS uint64_t*)dyn},
+                   snap);
+  } else {
+    uint64_t cur[CUR];
+    measure_record(p, P, r, KxnCurP{cur}, snap);
+  }
 }
 
 
@@ -237,12 +268,11 @@ __global__ void check_kernel(NParams p) {
   if (over) *p.flag = 1u;
 }
 
-// record r (of block b), lane = record
+// record r (of block b), lane = record; cur holds the record's cursor bases: the block base + the in-block
+// prefix (bsum_kernel)
+template <class CU>
 __device__ __forceinline__ void write_record(const NParams& p, const KxnProgram& P, uint64_t b, uint64_t r,
-                                             uint64_t* cur, uint64_t* lim, uint64_t* snap) {
-  // the record's cursor bases: the block base + the in-block prefix (bsum_kernel)
-  for (uint32_t k = 0; k < p.ncur; k++)
-    cur[k] = p.bsum[(uint64_t)k * p.nblk + b] + p.counts[(uint64_t)k * p.n + r];
+                                             CU cur, uint64_t* lim, uint64_t* snap) {
   const uint8_t raw = p.rcode[r];
   const uint8_t rc = raw == RC_NONE ? RC_NONE : (uint8_t)(raw & ~RC_CAREFUL);
   uint64_t a = 0, e = 0;
@@ -269,14 +299,27 @@ __device__ __forceinline__ void write_record(const NParams& p, const KxnProgram&
 
 // one record per thread: workgroup w holds records [w·NTD, (w + 1)·NTD) of block w / (RB / NTD) (a workgroup
 // per block looping over its quarters left 4 waves per SIMD: DESIGN §3.10)
+template <bool LC>
 __global__ void __launch_bounds__(NTD) write_kernel(NParams p) {
   if (*p.flag) return;
   __shared__ KxnProgram sP;
+  extern __shared__ uint64_t dyn[];
+  const uint64_t b = blockIdx.x / (RB / NTD);
+  if (LC)   // the block's base per cursor, shared by the workgroup's lanes
+    for (uint32_t k = threadIdx.x; k < p.ncur; k += NTD) dyn[k] = p.bsum[(uint64_t)k * p.nblk + b];
   const KxnProgram& P = lds_program(p.P, &sP);
   const uint64_t r = (uint64_t)blockIdx.x * NTD + threadIdx.x;
   if (r >= p.n) return;
-  uint64_t cur[CUR], lim[CUR], snap[SNAP];
-  write_record(p, P, blockIdx.x / (RB / NTD), r, cur, lim, snap);
+  uint64_t lim[CUR], snap[SNAP];
+  if constexpr (LC) {
+    KXN_LDS uint32_t* c = (KXN_LDS uint32_t*)(dyn + p.ncur) + threadIdx.x;
+    for (uint32_t k = 0; k < p.ncur; k++) c[k * NTD] = p.counts[(uint64_t)k * p.n + r];   // in-block prefixes
+    write_record(p, P, b, r, KxnCurL{c, (const KXN_LDS uint64_t*)dyn}, lim, snap);
+  } else {
+    uint64_t cur[CUR];
+    for (uint32_t k = 0; k < p.ncur; k++) cur[k] = p.bsum[(uint64_t)k * p.nblk + b] + p.counts[(uint64_t)k * p.n + r];
+    write_record(p, P, b, r, KxnCurP{cur}, lim, snap);
+  }
 }
 
 
@@ -497,7 +540,13 @@ int kx_launch_nested_decode(const KxnProgram* dprog, const KxnProgram& hprog, co
   } else {
     p.offsets = offsets;
   }
-  hipLaunchKernelGGL(measure_kernel, dim3((unsigned)((n + NTD - 1) / NTD)), dim3(NTD), 0, stream, p);
+  // the cursors in LDS when they fit beside the program at two workgroups per CU (KX_NESTED_LDS=0: scratch)
+  const size_t curl = (size_t)hprog.ncur * (8 + 4 * NTD);
+  const bool lc = kx_knob(KXK_NESTED_LDS) && sizeof(KxnProgram) + curl <= 80 * 1024;
+  if (lc)
+    hipLaunchKernelGGL(measure_kernel<true>, dim3((unsigned)((n + NTD - 1) / NTD)), dim3(NTD), curl, stream, p);
+  else
+    hipLaunchKernelGGL(measure_kernel<false>, dim3((unsigned)((n + NTD - 1) / NTD)), dim3(NTD), 0, stream, p);
   KX_HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(bsum_kernel, dim3((unsigned)p.nblk, hprog.ncur), dim3(NT), 0, stream, p);
   KX_HIP_CHECK(hipGetLastError());
@@ -512,7 +561,10 @@ int kx_launch_nested_decode(const KxnProgram* dprog, const KxnProgram& hprog, co
   }
   hipLaunchKernelGGL(check_kernel, dim3(1), dim3(64), 0, stream, p);
   KX_HIP_CHECK(hipGetLastError());
-  hipLaunchKernelGGL(write_kernel, dim3((unsigned)((n + NTD - 1) / NTD)), dim3(NTD), 0, stream, p);
+  if (lc)
+    hipLaunchKernelGGL(write_kernel<true>, dim3((unsigned)((n + NTD - 1) / NTD)), dim3(NTD), curl, stream, p);
+  else
+    hipLaunchKernelGGL(write_kernel<false>, dim3((unsigned)((n + NTD - 1) / NTD)), dim3(NTD), 0, stream, p);
   KX_HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(64), 0, stream, p);
   KX_HIP_CHECK(hipGetLastError());

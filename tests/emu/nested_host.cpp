@@ -86,8 +86,8 @@ extern "C" int emu_nested_decode(const kx_struct_desc* structs, uint32_t ns, con
     uint64_t used = 0;
     // as the device: the fast walk (no snapshots), and for a record that repeats a field the careful walk
     auto walk = [&](uint64_t* sn) {
-      return P.pb ? kxn_pb_read_record<false>(P, C, in + a[r], b[r] - a[r], r, cur.data(), sn, &used)
-                  : kxn_read_record<false>(P, C, in + a[r], b[r] - a[r], r, cur.data(), sn, &used);
+      return P.pb ? kxn_pb_read_record<false>(P, C, in + a[r], b[r] - a[r], r, KxnCurP{cur.data()}, sn, &used)
+                  : kxn_read_record<false>(P, C, in + a[r], b[r] - a[r], r, KxnCurP{cur.data()}, sn, &used);
     };
     int e = (a[r] > b[r] || b[r] > in_len) ? KX_ERR_INVALID_ARG : walk(nullptr);
     if (e == KXN_REPEAT) {
@@ -123,10 +123,10 @@ extern "C" int emu_nested_decode(const kx_struct_desc* structs, uint32_t ns, con
     uint64_t* sn = careful[r] ? snap.data() : nullptr;   // the fast walk stays inside the record's extents
     const uint64_t* li = careful[r] ? lim.data() : nullptr;
     if (code[r] == 0 && P.pb)
-      (void)kxn_pb_read_record<true>(P, C, in + a[r], b[r] - a[r], r, cur.data(), sn, &used, li);
+      (void)kxn_pb_read_record<true>(P, C, in + a[r], b[r] - a[r], r, KxnCurP{cur.data()}, sn, &used, li);
     else if (code[r] == 0)
-      (void)kxn_read_record<true>(P, C, in + a[r], b[r] - a[r], r, cur.data(), sn, &used, li);
-    else kxn_failed_record(P, C, r, cur.data());
+      (void)kxn_read_record<true>(P, C, in + a[r], b[r] - a[r], r, KxnCurP{cur.data()}, sn, &used, li);
+    else kxn_failed_record(P, C, r, KxnCurP{cur.data()});
     if (rstat && offsets) rstat[r] = code[r] == 0xff ? 0 : code[r];
   }
   for (uint32_t c = 0; c < P.ncols; c++) {
