@@ -449,11 +449,34 @@ struct KxnFrame {
 // an occurrence that a later one of the same field replaces may have been longer, and what it wrote
 // past the record's final extent belongs to the next record (another lane). Inside the extent every
 // byte / element is written again by a later, final occurrence.
+// A value per container level (0 .. 2) as three named members, read and written with selects: an array
+// indexed by the level a program node names would live in scratch (device), one memory round trip per use
+template <class T>
+struct KxnL3 {
+  T v0, v1, v2;
+  struct Ref {
+    KxnL3* s;
+    int L;
+    KXN_MHD operator T() const { return s->get(L); }
+    KXN_MHD Ref& operator=(T x) { s->put(L, x); return *this; }
+    KXN_MHD Ref& operator|=(T x) { s->put(L, s->get(L) | x); return *this; }
+    KXN_MHD Ref& operator&=(T x) { s->put(L, s->get(L) & x); return *this; }
+  };
+  KXN_MHD T get(int L) const { return L == 0 ? v0 : L == 1 ? v1 : v2; }
+  KXN_MHD void put(int L, T x) {
+    v0 = L == 0 ? x : v0;
+    v1 = L == 1 ? x : v1;
+    v2 = L == 2 ? x : v2;
+  }
+  KXN_MHD void fill(T x) { v0 = v1 = v2 = x; }
+  KXN_MHD Ref operator[](int L) { return Ref{this, L}; }
+};
+
 struct KxnState {
-  uint64_t idx[3];    // index of the open instance per level
-  uint64_t seen[3];   // seen masks per level
-  uint64_t pres[3];   // presence words per level
-  bool live[3];       // the open instance lies inside the record's extent of its domain (writes allowed)
+  KxnL3<uint64_t> idx;   // index of the open instance per level
+  KxnL3<uint64_t> seen;  // seen masks per level
+  KxnL3<uint64_t> pres;  // presence words per level
+  KxnL3<bool> live;      // the open instance lies inside the record's extent of its domain (writes allowed)
   const uint64_t* lim;  // W, careful walk: per cursor, the end of the record's extent (nullptr: the walk
                         // has no repeated field, so it never leaves the extents the measure pass found)
 };
@@ -558,10 +581,10 @@ KXN_HD int kxn_read_record(const KxnProgram& P, const KxnCols& C, B b, uint64_t 
   KxnFrame stk[KXN_STACK];
   KxnState S;
   S.lim = lim;
-  S.live[0] = S.live[1] = S.live[2] = true;
-  S.idx[0] = S.idx[1] = S.idx[2] = 0;
-  S.seen[0] = S.seen[1] = S.seen[2] = 0;
-  S.pres[0] = S.pres[1] = S.pres[2] = 0;
+  S.live.fill(true);
+  S.idx.fill(0);
+  S.seen.fill(0);
+  S.pres.fill(0);
   int sp = 0;
   uint64_t q = 0;
   kxn_inst_start<W>(P, C, 0, r, cur, S);
@@ -955,10 +978,10 @@ KXN_HD int kxn_pb_read_record(const KxnProgram& P, const KxnCols& C, B b, uint64
   KxnPFrame stk[KXN_STACK];
   KxnState S;
   S.lim = lim;
-  S.live[0] = S.live[1] = S.live[2] = true;
-  S.idx[0] = S.idx[1] = S.idx[2] = 0;
-  S.seen[0] = S.seen[1] = S.seen[2] = 0;
-  S.pres[0] = S.pres[1] = S.pres[2] = 0;
+  S.live.fill(true);
+  S.idx.fill(0);
+  S.seen.fill(0);
+  S.pres.fill(0);
   int sp = 0;
   uint64_t q = 0;
   int rc = KX_OK;
