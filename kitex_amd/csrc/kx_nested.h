@@ -826,6 +826,31 @@ KXN_HD int kxn_uvarint(B b, uint64_t end, uint64_t* q, uint64_t* v) {  // protow
   return KX_ERR_INVALID_DATA;
 }
 
+// the input itself (the device's walk over global memory): with 10 bytes left, the whole varint from one
+// unaligned 8-byte load and a 2-byte one, branch-free (terminator = the first byte with bit 7 clear, the 7-bit
+// groups compacted in three shift / mask steps), instead of a chain of dependent byte loads
+KXN_HD int kxn_uvarint(const uint8_t* b, uint64_t end, uint64_t* q, uint64_t* v) {
+  if (end - *q < 10) return kxn_uvarint<const uint8_t*>(b, end, q, v);
+  uint64_t lo;
+  uint16_t hi;
+  __builtin_memcpy(&lo, b + *q, 8);
+  __builtin_memcpy(&hi, b + *q + 8, 2);
+  const uint32_t b8 = hi & 0xffu, b9 = hi >> 8;
+  const uint64_t stop = ~lo & 0x8080808080808080ull;
+  const uint32_t k = stop ? (uint32_t)__builtin_ctzll(stop) >> 3 : b8 < 0x80 ? 8u : 9u;
+  if (k == 9 && b9 > 1) return KX_ERR_INVALID_DATA;   // more than 64 bits (or no terminator in 10 bytes)
+  const uint64_t keep = k >= 7 ? ~0ull : (2ull << (8 * k + 7)) - 1;   // bytes 0..k
+  uint64_t x = lo & keep & 0x7f7f7f7f7f7f7f7full;
+  x = (x & 0x007f007f007f007full) | ((x & 0x7f007f007f007f00ull) >> 1);
+  x = (x & 0x00003fff00003fffull) | ((x & 0x3fff00003fff0000ull) >> 2);
+  x = (x & 0x000000000fffffffull) | ((x & 0x0fffffff00000000ull) >> 4);
+  if (k >= 8) x |= (uint64_t)(b8 & 0x7f) << 56;
+  if (k >= 9) x |= (uint64_t)(b9 & 0x01) << 63;
+  *v = x;
+  *q += k + 1;
+  return KX_OK;
+}
+
 KXN_HD uint32_t kxn_uvlen(uint64_t v) {
   uint32_t n = 1;
   while (v >= 0x80) { v >>= 7; n++; }
@@ -864,6 +889,16 @@ KXN_HD uint64_t kxn_le(B p, int n) {
   for (int k = n - 1; k >= 0; k--) v = (v << 8) | p[k];
   return v;
 }
+KXN_HD uint64_t kxn_le(const uint8_t* p, int n) {   // the input itself: one unaligned load
+  if (n == 8) {
+    uint64_t v;
+    __builtin_memcpy(&v, p, 8);
+    return v;
+  }
+  uint32_t v;
+  __builtin_memcpy(&v, p, 4);
+  return v;
+}
 
 // one scalar of node N at b[*q] (its wire type already matched), in the column's host form
 template <class B>
@@ -893,10 +928,22 @@ KXN_HD int kxn_pb_scalar(const KxnNode& N, B b, uint64_t end, uint64_t* q, uint6
   return KX_OK;
 }
 
-// utf8.Valid, as protobuf-go checks proto3 `string` fields
+// utf8.Valid, as protobuf-go checks proto3 `string` fields; over the input itself 8 bytes per step while they
+// are ASCII (one unaligned load each)
+template <class B>
+KXN_HD uint64_t kxn_ascii_prefix(B s, uint64_t n) { (void)s; (void)n; return 0; }
+KXN_HD uint64_t kxn_ascii_prefix(const uint8_t* s, uint64_t n) {
+  uint64_t i = 0;
+  for (; i + 8 <= n; i += 8) {
+    uint64_t x;
+    __builtin_memcpy(&x, s + i, 8);
+    if (x & 0x8080808080808080ull) break;
+  }
+  return i;
+}
 template <class B>
 KXN_HD bool kxn_utf8(B s, uint64_t n) {
-  uint64_t i = 0;
+  uint64_t i = kxn_ascii_prefix(s, n);
   while (i < n) {
     const uint32_t c = s[i];
     if (c < 0x80) { i++; continue; }

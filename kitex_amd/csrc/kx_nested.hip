@@ -100,11 +100,11 @@ struct KxnCurL {
 // measured slower: 7.8 / 21.0 ms for the measure / write passes against 7.2 / 15.6 ms).
 // snap == nullptr: the fast walk (KXN_REPEAT at a repeated field)
 template <bool W, class CU>
-__device__ __forceinline__ int walk(const NParams& p, const KxnProgram& P, uint64_t a, uint64_t b, uint64_t r,
-                                   CU cur, uint64_t* snap, uint64_t* lim) {
+__device__ __forceinline__ int walk(const NParams& p, const KxnProgram& P, const KxnCols& C, uint64_t a, uint64_t b,
+                                   uint64_t r, CU cur, uint64_t* snap, uint64_t* lim) {
   uint64_t used = 0;
-  return P.pb ? kxn_pb_read_record<W>(P, *p.C, p.in + a, b - a, r, cur, snap, &used, lim)
-              : kxn_read_record<W>(P, *p.C, p.in + a, b - a, r, cur, snap, &used, lim);
+  return P.pb ? kxn_pb_read_record<W>(P, C, p.in + a, b - a, r, cur, snap, &used, lim)
+              : kxn_read_record<W>(P, C, p.in + a, b - a, r, cur, snap, &used, lim);
 }
 
 template <class CU>
@@ -121,10 +121,10 @@ __device__ __forceinline__ void measure_record(const NParams& p, const KxnProgra
     // records, divergent refills and 164 VGPRs in the write pass)
     uint8_t careful = 0;
     if (!rc) {
-      rc = walk<false>(p, P, a, b, r, cur, nullptr, nullptr);   // no snapshot stores: the common record
+      rc = walk<false>(p, P, *p.C, a, b, r, cur, nullptr, nullptr);   // no snapshot stores: the common record
       if (rc == KXN_REPEAT) {                                   // a repeated field: again, with snapshots
         for (uint32_t k = 0; k < p.ncur; k++) cur.set(k, 0);
-        rc = walk<false>(p, P, a, b, r, cur, snap, nullptr);
+        rc = walk<false>(p, P, *p.C, a, b, r, cur, snap, nullptr);
         careful = RC_CAREFUL;
       }
     }
@@ -147,6 +147,14 @@ __device__ __forceinline__ const KxnProgram& lds_program(const KxnProgram* g, Kx
   for (uint32_t i = threadIdx.x; i < sizeof(KxnProgram) / 4; i += blockDim.x) dst[i] = src[i];
   __syncthreads();
   return *s;
+}
+// the call's column table in LDS too (4 KB), for the passes that store: every store's column pointer, width
+// and offset size is then an LDS read instead of a dependent global load (publish with lds_program's barrier)
+__device__ __forceinline__ void lds_cols(const KxnCols* g, KxnCols* s) {
+  static_assert(sizeof(KxnCols) % 4 == 0, "dword copy");
+  const uint32_t* src = (const uint32_t*)g;
+  uint32_t* dst = (uint32_t*)s;
+  for (uint32_t i = threadIdx.x; i < sizeof(KxnCols) / 4; i += blockDim.x) dst[i] = src[i];
 }
 
 // LC: the cursors in LDS (dynamic shared memory: ncur bases, then ncur x NTD u32), else in scratch
@@ -271,8 +279,8 @@ __global__ void check_kernel(NParams p) {
 // record r (of block b), lane = record; cur holds the record's cursor bases: the block base + the in-block
 // prefix (bsum_kernel)
 template <class CU>
-__device__ __forceinline__ void write_record(const NParams& p, const KxnProgram& P, uint64_t b, uint64_t r,
-                                             CU cur, uint64_t* lim, uint64_t* snap) {
+__device__ __forceinline__ void write_record(const NParams& p, const KxnProgram& P, const KxnCols& C, uint64_t b,
+                                             uint64_t r, CU cur, uint64_t* lim, uint64_t* snap) {
   const uint8_t raw = p.rcode[r];
   const uint8_t rc = raw == RC_NONE ? RC_NONE : (uint8_t)(raw & ~RC_CAREFUL);
   uint64_t a = 0, e = 0;
@@ -287,12 +295,12 @@ __device__ __forceinline__ void write_record(const NParams& p, const KxnProgram&
         lim[k] = r + 1 < rb1 ? base + p.counts[(uint64_t)k * p.n + r + 1]
                              : (b + 1 < p.nblk ? p.bsum[(uint64_t)k * p.nblk + b + 1] : p.totals[k]);
       }
-      (void)walk<true>(p, P, a, e, r, cur, snap, lim);
+      (void)walk<true>(p, P, C, a, e, r, cur, snap, lim);
     } else {   // the fast walk writes only inside the record's extents
-      (void)walk<true>(p, P, a, e, r, cur, nullptr, nullptr);
+      (void)walk<true>(p, P, C, a, e, r, cur, nullptr, nullptr);
     }
   } else {
-    kxn_failed_record(P, *p.C, r, cur);
+    kxn_failed_record(P, C, r, cur);
   }
   if (p.record_status && !p.concat) p.record_status[r] = rc == RC_NONE ? 0 : rc;
 }
@@ -308,17 +316,20 @@ __global__ void __launch_bounds__(NTD) write_kernel(NParams p) {
   if (LC)   // the block's base per cursor, shared by the workgroup's lanes
     for (uint32_t k = threadIdx.x; k < p.ncur; k += NTD) dyn[k] = p.bsum[(uint64_t)k * p.nblk + b];
   const KxnProgram& P = lds_program(p.P, &sP);
+  // (the column table stays in global memory here: 4 KB more LDS per workgroup measured slower, 10.3 vs 9.0 ms
+  // for 1 M Nesting records, the cursors' two workgroups per CU no longer fitting)
+  const KxnCols& C = *p.C;
   const uint64_t r = (uint64_t)blockIdx.x * NTD + threadIdx.x;
   if (r >= p.n) return;
   uint64_t lim[CUR], snap[SNAP];
   if constexpr (LC) {
     KXN_LDS uint32_t* c = (KXN_LDS uint32_t*)(dyn + p.ncur) + threadIdx.x;
     for (uint32_t k = 0; k < p.ncur; k++) c[k * NTD] = p.counts[(uint64_t)k * p.n + r];   // in-block prefixes
-    write_record(p, P, b, r, KxnCurL{c, (const KXN_LDS uint64_t*)dyn}, lim, snap);
+    write_record(p, P, C, b, r, KxnCurL{c, (const KXN_LDS uint64_t*)dyn}, lim, snap);
   } else {
     uint64_t cur[CUR];
     for (uint32_t k = 0; k < p.ncur; k++) cur[k] = p.bsum[(uint64_t)k * p.nblk + b] + p.counts[(uint64_t)k * p.n + r];
-    write_record(p, P, b, r, KxnCurP{cur}, lim, snap);
+    write_record(p, P, C, b, r, KxnCurP{cur}, lim, snap);
   }
 }
 
@@ -383,11 +394,14 @@ constexpr int ERB = NT;
 __global__ void __launch_bounds__(NT) esize_kernel(EParams p) {
   __shared__ uint64_t sh[NT / 64];
   __shared__ KxnProgram sP;
+  __shared__ KxnCols sC;
+  lds_cols(p.C, &sC);
   const KxnProgram& P = lds_program(p.P, &sP);   // the walk's table reads at LDS latency (as decode)
+  const KxnCols& C = sC;
   const uint64_t r = (uint64_t)blockIdx.x * ERB + threadIdx.x;
   uint64_t sz = 0;
   if (r < p.n) {   // Kitex-PB: the record's Batch frame (0x0A, uvarint body length, body)
-    sz = P.pb ? kxn_pb_frame_size(P, *p.C, r) : kxn_write_record<false>(P, *p.C, r, nullptr, 0);
+    sz = P.pb ? kxn_pb_frame_size(P, C, r) : kxn_write_record<false>(P, C, r, nullptr, 0);
     p.sizes[r] = sz;
   }
   uint64_t tot;
@@ -424,14 +438,17 @@ __global__ void __launch_bounds__(NT) ewrite_kernel(EParams p) {
   __shared__ uint64_t sh[NT / 64];
   __shared__ KxnProgram sP;
   if (p.status->code != 0) return;
+  __shared__ KxnCols sC;
+  lds_cols(p.C, &sC);
   const KxnProgram& P = lds_program(p.P, &sP);
+  const KxnCols& C = sC;
   const uint64_t r = (uint64_t)blockIdx.x * ERB + threadIdx.x;
   const uint64_t sz = r < p.n ? p.sizes[r] : 0;
   uint64_t tot;
   const uint64_t at = p.bsum[blockIdx.x] + wg_excl(sz, &tot, sh);
   if (r < p.n) {
-    if (P.pb) kxn_pb_write_frame(P, *p.C, r, p.out, at, sz);
-    else (void)kxn_write_record<true>(P, *p.C, r, p.out, at);
+    if (P.pb) kxn_pb_write_frame(P, C, r, p.out, at, sz);
+    else (void)kxn_write_record<true>(P, C, r, p.out, at);
     if (p.offsets_out) p.offsets_out[r] = at;
   }
 }
@@ -542,7 +559,7 @@ int kx_launch_nested_decode(const KxnProgram* dprog, const KxnProgram& hprog, co
   }
   // the cursors in LDS when they fit beside the program at two workgroups per CU (KX_NESTED_LDS=0: scratch)
   const size_t curl = (size_t)hprog.ncur * (8 + 4 * NTD);
-  const bool lc = kx_knob(KXK_NESTED_LDS) && sizeof(KxnProgram) + curl <= 80 * 1024;
+  const bool lc = kx_knob(KXK_NESTED_LDS) && sizeof(KxnProgram) + curl <= 160 * 1024;
   if (lc)
     hipLaunchKernelGGL(measure_kernel<true>, dim3((unsigned)((n + NTD - 1) / NTD)), dim3(NTD), curl, stream, p);
   else
