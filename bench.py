@@ -549,7 +549,9 @@ def extras(args, r2, dev, local):
         avg = sum(per) / len(per) / 1e3
         ok = b.verify()
         st = b.status()
-        traffic, tnote = pmc_traffic(f"{b.cfg}_{b.mode}") if not getattr(b, "views", False) else (None, None)
+        views = getattr(b, "views", False)
+        traffic, tnote = pmc_traffic(f"{b.cfg}_{b.mode}") if not views else \
+            pmc_traffic(f"{b.cfg}_views") if b.mode == "concat" else (None, "no profile of this workload")
         return {"records_per_s": b.n * steps / t, "ms_per_step": t / steps * 1e3, "verified": ok,
                 "decode_diag": {"tile_rewalks": st.diag[0], "group_rescans": st.diag[1]},
                 "roofline": roofline(b.in_bytes + b.out_bytes_per_record() * b.n, avg, "decode", traffic, tnote)}
@@ -630,7 +632,8 @@ def extras(args, r2, dev, local):
                "schema": "PN (tests/pbn_cases.py), Batch-framed" if pb else "Nesting (baseline.thrift)",
                "decode": {"records_per_s": n * steps / t, "ms_per_step": t / steps * 1e3, "verified": ok,
                           "mode": "concatenated (skip pass + measure + write)", "sizes_pass_ms": sizes_ms,
-                          "roofline": roofline(wire.numel() + out_bytes, avg, "nested decode (measure + write)")}}
+                          "roofline": roofline(wire.numel() + out_bytes, avg, "nested decode (measure + write)",
+                                               *pmc_traffic("pb_nested" if pb else "nested_concat"))}}
         if not pb:
             # with message lengths known (dataLen, codec_fast.go:60-71): measure + write only, the form the CPU
             # baseline below runs (it is given every record's extent)
@@ -644,7 +647,8 @@ def extras(args, r2, dev, local):
             res["decode_offsets"] = {"records_per_s": n * steps / t3, "ms_per_step": t3 / steps * 1e3,
                                      "verified": s3.code == 0 and s3.n_records == n,
                                      "roofline": roofline(wire.numel() + out_bytes + 8 * (n + 1),
-                                                          sum(per3) / len(per3) / 1e3, "nested decode, offsets known")}
+                                                          sum(per3) / len(per3) / 1e3, "nested decode, offsets known",
+                                                          *pmc_traffic("nested_offsets"))}
             note(f"  nested decode with offsets timed: {t3 / steps * 1e3:.2f} ms")
         w2, _ = cdc.Marshal(outc)
         note("  nested encode: first Marshal done")
@@ -714,7 +718,8 @@ def extras(args, r2, dev, local):
             res["crc32_check_on" if chk else "crc32_check_off"] = {
                 "ms_per_step": t / steps * 1e3, "frames_per_s": n * steps / t, "verified": ok,
                 "roofline": roofline(wire.numel() + 8 * 8 * n, sum(per) / len(per) / 1e3,
-                                     "frame scan + message decode" + (" + fused CRC32C check" if chk else ""))}
+                                     "frame scan + message decode" + (" + fused CRC32C check" if chk else ""),
+                                     *pmc_traffic("frames_on" if chk else "frames_off"))}
         res["check_overhead"] = res["crc32_check_on"]["ms_per_step"] / res["crc32_check_off"]["ms_per_step"] - 1
         bad = wire.clone()
         bad[(n // 2) * (H + M) + H + M - 3] ^= 1   # one payload byte of frame n/2

@@ -5,6 +5,8 @@ WRITE_SIZE are in KiB; gfx950 FETCH_SIZE counts half of a wide streaming read ->
   python scripts/pmc_summary.py <gpurun_out/prof_TAG> <cfg> <mode>  -> profiles/pmc_<cfg>_<mode>.json
   mode "encode": the encode kernels (size pass, scan, write pass) of scripts/run_encode.py instead
   mode "crc": the CRC32C Generate kernels of scripts/run_crc.py
+  python scripts/pmc_summary.py <dir> <name> all <calls>  -> profiles/pmc_<name>.json: every codec kernel of a
+  scripts/run_workload.py run (it launches no other), per call of `calls`
 """
 import csv
 import glob
@@ -21,6 +23,11 @@ KERNELS = DECODE
 
 
 def short(name):
+    if KERNELS is None:   # mode "all": every codec kernel (they all live in anonymous namespaces)
+        if "(anonymous namespace)::" not in name:
+            return None
+        k = name.split("(anonymous namespace)::", 1)[1]
+        return k.split("(", 1)[0]
     for k in KERNELS:
         if "namespace)::" + k in name:
             return k
@@ -41,18 +48,22 @@ def counter_sums(path, counter):
 def main():
     global KERNELS
     d, cfg, mode = sys.argv[1], sys.argv[2], sys.argv[3]
-    KERNELS = ENCODE if mode == "encode" else CRC if mode == "crc" else DECODE
+    KERNELS = None if mode == "all" else ENCODE if mode == "encode" else CRC if mode == "crc" else DECODE
     last = "write_kernel" if mode == "encode" else "crc_kernel" if mode == "crc" else "emit_kernel"
     fetch = counter_sums(os.path.join(d, "fetch"), "FETCH_SIZE")
     write = counter_sums(os.path.join(d, "write"), "WRITE_SIZE")
-    # one launch of every kernel of the pipeline per call: the most-launched one counts the calls (the
-    # fast-path kernels replace emit_kernel / chain_kernel on the headline)
-    calls = max([len(fetch.get(last, []))] + [len(v) for v in fetch.values()]) or 1
+    if mode == "all":
+        calls = int(sys.argv[4])
+    else:
+        # one launch of every kernel of the pipeline per call: the most-launched one counts the calls (the
+        # fast-path kernels replace emit_kernel / chain_kernel on the headline)
+        calls = max([len(fetch.get(last, []))] + [len(v) for v in fetch.values()]) or 1
     kib = 1024.0
     fetch_b = sum(sum(v) for v in fetch.values()) * kib * 2 / calls
     write_b = sum(sum(v) for v in write.values()) * kib / calls
+    names = sorted(set(fetch) | set(write)) if KERNELS is None else KERNELS
     per_kernel = {k: {"fetch_bytes": sum(fetch.get(k, [])) * kib * 2 / calls,
-                      "write_bytes": sum(write.get(k, [])) * kib / calls} for k in KERNELS}
+                      "write_bytes": sum(write.get(k, [])) * kib / calls} for k in names}
     dur = defaultdict(list)
     for f in glob.glob(os.path.join(d, "stats", "**", "*kernel_trace.csv"), recursive=True):
         with open(f) as fh:
@@ -66,7 +77,8 @@ def main():
             sha = fh.read().strip()
     except OSError:
         pass
-    res = {"workload": f"{cfg}_{mode}" if mode in ("encode", "crc") else f"{cfg}_decode_{mode}", "calls": calls, "lib_sha256": sha,
+    res = {"workload": cfg if mode == "all" else f"{cfg}_{mode}" if mode in ("encode", "crc") else f"{cfg}_decode_{mode}",
+           "calls": calls, "lib_sha256": sha,
            "hbm_bytes_per_launch": fetch_b + write_b, "fetch_bytes_per_call": fetch_b,
            "write_bytes_per_call": write_b, "per_kernel": per_kernel,
            "avg_ms": {k: sum(v) / len(v) for k, v in dur.items() if v},
@@ -75,7 +87,7 @@ def main():
                    "uses it only when lib_sha256 matches the library it times"}
     odir = os.environ.get("PMC_OUT") or os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                                      "profiles")
-    out = os.path.join(odir, f"pmc_{cfg}_{mode}.json")
+    out = os.path.join(odir, f"pmc_{cfg}.json" if mode == "all" else f"pmc_{cfg}_{mode}.json")
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1)
     print(json.dumps(res, indent=1))
