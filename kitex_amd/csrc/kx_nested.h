@@ -526,14 +526,12 @@ KXN_HD void kxn_inst_end(const KxnProgram& P, const KxnCols& C, int R, CU cur, K
   }
 }
 
-// read one value of node X at b[*q] (scalars, strings, raw structs directly; structs / containers push a
-// frame). Element instances of containers are opened by the caller.
+// read one leaf value (SCALAR / STRING / RAW) of node X at b[*q]
 template <bool W, class B, class CU>
-KXN_HD int kxn_value(const KxnProgram& P, const KxnCols& C, B b, uint64_t len, uint64_t* q, int X,
-                     CU cur, KxnState& S, KxnFrame* stk, int* sp) {
+KXN_HD int kxn_leaf(const KxnProgram& P, const KxnCols& C, B b, uint64_t len, uint64_t* q, int X, CU cur,
+                    KxnState& S) {
   const KxnNode& N = P.node[X];
-  const uint32_t kind = N.kind;
-  if (kind == KN_RAW) {                                      // a recursive struct: its encoded bytes
+  if (N.kind == KN_RAW) {                                    // a recursive struct: its encoded bytes
     uint64_t e = *q;
     const int rc = kxn_skip(b, len, &e, KX_T_STRUCT, KXN_SKIP_DEPTH);
     if (rc) return rc;
@@ -542,28 +540,51 @@ KXN_HD int kxn_value(const KxnProgram& P, const KxnCols& C, B b, uint64_t len, u
     *q = e;
     return KX_OK;
   }
-  // Every other kind in one straight line (lanes of a wave reading different kinds stay together): the
-  // bytes it starts with (a scalar's value, a string's length, ReadListBegin's type + count, ReadMapBegin's
-  // two types + count: struct_tpl.go:425-625) and, for strings and containers, the one length word
-  const uint32_t hl = kind == KN_SCALAR ? N.width : kind == KN_STRING ? 4u : kind == KN_LIST ? 5u : kind == KN_MAP ? 6u : 0u;
-  if (*q + hl > len) return KX_ERR_EOF;
-  const bool word = kind == KN_STRING || kind == KN_LIST || kind == KN_MAP;
-  const int32_t c = word ? (int32_t)kxn_be32(b + *q + (kind == KN_LIST ? 1u : kind == KN_MAP ? 2u : 0u)) : 0;
-  if (c < 0) return KX_ERR_NEGATIVE_SIZE;
-  if (kind == KN_SCALAR) {
+  if (N.kind == KN_SCALAR) {
+    if (*q + N.width > len) return KX_ERR_EOF;
     if (W && S.live[N.level]) kxn_put_val(C, N.col, N.width, S.idx[N.level], kxn_scalar(N.ttype, b + *q));
+    *q += N.width;
+    return KX_OK;
+  }
+  if (*q + 4 > len) return KX_ERR_EOF;                       // ReadString: a copy
+  const int32_t c = (int32_t)kxn_be32(b + *q);
+  if (c < 0) return KX_ERR_NEGATIVE_SIZE;
+  const uint64_t l = (uint64_t)c;
+  if (*q + 4 + l > len) return KX_ERR_EOF;
+  if (W) kxn_copy((uint8_t*)C.data[N.col] + cur[N.cur], b + *q + 4, kxn_room(S, N.cur, cur[N.cur], l));
+  cur.add(N.cur, l);
+  *q += 4 + l;
+  return KX_OK;
+}
+
+// read one value of node X at b[*q] (scalars, strings, raw structs directly; structs / containers push a
+// frame, except a list / map whose elements are leaves: its elements are read here, the frame loop's order
+// of instance starts / ends kept, with no frame stored and updated per element). Element instances of the
+// containers that push a frame are opened by the caller.
+template <bool W, class B, class CU>
+KXN_HD int kxn_value(const KxnProgram& P, const KxnCols& C, B b, uint64_t len, uint64_t* q, int X,
+                     CU cur, KxnState& S, KxnFrame* stk, int* sp) {
+  const KxnNode& N = P.node[X];
+  const uint32_t kind = N.kind;
+  if (kind <= KN_RAW) return kxn_leaf<W>(P, C, b, len, q, X, cur, S);
+  // STRUCT / LIST / SET / MAP: ReadListBegin's type + count, ReadMapBegin's two types + count
+  // (struct_tpl.go:425-625)
+  const uint32_t hl = kind == KN_LIST ? 5u : kind == KN_MAP ? 6u : 0u;
+  if (*q + hl > len) return KX_ERR_EOF;
+  const int32_t c = hl ? (int32_t)kxn_be32(b + *q + (kind == KN_LIST ? 1u : 2u)) : 0;
+  if (c < 0) return KX_ERR_NEGATIVE_SIZE;
+  if (hl && P.node[N.a].kind <= KN_RAW && (kind == KN_LIST || P.node[N.b].kind <= KN_RAW)) {
     *q += hl;
+    for (int32_t i = 0; i < c; i++) {
+      const uint64_t e = cur.post_inc(N.cur);
+      kxn_inst_start<W>(P, C, N.root, e, cur, S);
+      int rc = kxn_leaf<W>(P, C, b, len, q, N.a, cur, S);
+      if (!rc && kind == KN_MAP) rc = kxn_leaf<W>(P, C, b, len, q, N.b, cur, S);
+      if (rc) return rc;
+      kxn_inst_end<W>(P, C, N.root, cur, S);
+    }
     return KX_OK;
   }
-  if (kind == KN_STRING) {                                   // ReadString: a copy
-    const uint64_t l = (uint64_t)c;
-    if (*q + 4 + l > len) return KX_ERR_EOF;
-    if (W) kxn_copy((uint8_t*)C.data[N.col] + cur[N.cur], b + *q + 4, kxn_room(S, N.cur, cur[N.cur], l));
-    cur.add(N.cur, l);
-    *q += 4 + l;
-    return KX_OK;
-  }
-  // STRUCT / LIST / SET / MAP: a frame (a struct's fields, a container's elements)
   if (*sp >= KXN_STACK) return KX_ERR_DEPTH_LIMIT;
   stk[*sp] = KxnFrame{(uint8_t)kind, 0, 0, 0, (int16_t)(kind == KN_STRUCT ? N.a : X), 0, (int64_t)c};
   (*sp)++;
@@ -709,46 +730,57 @@ KXN_HD uint64_t kxn_pres_word(const KxnProgram& P, const KxnCols& C, int R, uint
   return RT.pres_col >= 0 ? ((const KXN_G(uint64_t)*)C.data[RT.pres_col])[e] : 0;
 }
 
-// one value of node X at instance index e (level X.level); structs / containers push a frame
+// one leaf value (SCALAR / STRING / RAW) of node X at instance index e
+template <bool W>
+KXN_HD void kxn_wleaf(const KxnProgram& P, const KxnCols& C, int X, uint64_t e, uint8_t* out, uint64_t* pos) {
+  const KxnNode& N = P.node[X];
+  if (N.kind == KN_SCALAR) {
+    uint64_t v = kxn_get_val(C, N.col, N.width, e);
+    if (N.ttype == KX_T_BOOL) v = (v & 0xff) ? 1 : 0;
+    kxn_out<W>(out, pos, v, N.width);
+    return;
+  }
+  const uint64_t a = kxn_get_arr(C, N.col, N.level, e), z = kxn_get_arr(C, N.col, N.level, e + 1);
+  const uint64_t l = z - a;
+  if (N.kind == KN_STRING) kxn_out<W>(out, pos, l, 4);
+  else if (l == 0) { kxn_out<W>(out, pos, KX_T_STOP, 1); return; }  // an empty raw struct: STOP
+  if (W)
+    kxn_copy(out + *pos, (const uint8_t*)C.data[N.col] + a, l);
+  *pos += l;
+}
+
+// one value of node X at instance index e (level X.level); structs / containers push a frame, except a
+// list / map of leaves, whose elements are written here
 template <bool W>
 KXN_HD void kxn_wvalue(const KxnProgram& P, const KxnCols& C, int X, uint64_t e, uint8_t* out, uint64_t* pos,
                        KxnEFrame* stk, int* sp) {
   const KxnNode& N = P.node[X];
-  switch (N.kind) {
-    case KN_SCALAR: {
-      uint64_t v = kxn_get_val(C, N.col, N.width, e);
-      if (N.ttype == KX_T_BOOL) v = (v & 0xff) ? 1 : 0;
-      kxn_out<W>(out, pos, v, N.width);
-      return;
-    }
-    case KN_STRING: case KN_RAW: {
-      const uint64_t a = kxn_get_arr(C, N.col, N.level, e), z = kxn_get_arr(C, N.col, N.level, e + 1);
-      const uint64_t l = z - a;
-      if (N.kind == KN_STRING) kxn_out<W>(out, pos, l, 4);
-      else if (l == 0) { kxn_out<W>(out, pos, KX_T_STOP, 1); return; }  // an empty raw struct: STOP
-      if (W)
-        kxn_copy(out + *pos, (const uint8_t*)C.data[N.col] + a, l);
-      *pos += l;
-      return;
-    }
-    case KN_STRUCT:
-      stk[*sp] = KxnEFrame{KN_STRUCT, 0, N.a, P.st[N.a].enc_first, P.st[N.a].root, 0, 0, e};
-      (*sp)++;
-      return;
-    default: {
-      const uint64_t a = kxn_get_arr(C, N.rep_col, N.level, e), z = kxn_get_arr(C, N.rep_col, N.level, e + 1);
-      if (N.kind == KN_LIST) {
-        kxn_out<W>(out, pos, N.etype, 1);
-      } else {
-        kxn_out<W>(out, pos, N.etype, 1);
-        kxn_out<W>(out, pos, N.vtype, 1);
-      }
-      kxn_out<W>(out, pos, z - a, 4);
-      stk[*sp] = KxnEFrame{N.kind, 0, (int16_t)X, 0, 0, a, z, 0};
-      (*sp)++;
-      return;
-    }
+  if (N.kind <= KN_RAW) {
+    kxn_wleaf<W>(P, C, X, e, out, pos);
+    return;
   }
+  if (N.kind == KN_STRUCT) {
+    stk[*sp] = KxnEFrame{KN_STRUCT, 0, N.a, P.st[N.a].enc_first, P.st[N.a].root, 0, 0, e};
+    (*sp)++;
+    return;
+  }
+  const uint64_t a = kxn_get_arr(C, N.rep_col, N.level, e), z = kxn_get_arr(C, N.rep_col, N.level, e + 1);
+  if (N.kind == KN_LIST) {
+    kxn_out<W>(out, pos, N.etype, 1);
+  } else {
+    kxn_out<W>(out, pos, N.etype, 1);
+    kxn_out<W>(out, pos, N.vtype, 1);
+  }
+  kxn_out<W>(out, pos, z - a, 4);
+  if (P.node[N.a].kind <= KN_RAW && (N.kind == KN_LIST || P.node[N.b].kind <= KN_RAW)) {
+    for (uint64_t i = a; i < z; i++) {
+      kxn_wleaf<W>(P, C, N.a, i, out, pos);
+      if (N.kind == KN_MAP) kxn_wleaf<W>(P, C, N.b, i, out, pos);
+    }
+    return;
+  }
+  stk[*sp] = KxnEFrame{N.kind, 0, (int16_t)X, 0, 0, a, z, 0};
+  (*sp)++;
 }
 
 template <bool W>
