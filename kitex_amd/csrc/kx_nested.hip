@@ -98,16 +98,17 @@ struct KxnCurL {
 
 // the walk of record [a, b) (a per-lane LDS window over the record's bytes, refilled 32 bytes at a time,
 // measured slower: 7.8 / 21.0 ms for the measure / write passes against 7.2 / 15.6 ms).
-// snap == nullptr: the fast walk (KXN_REPEAT at a repeated field)
-template <bool W, class CU>
+// snap == nullptr: the fast walk (KXN_REPEAT at a repeated field). PB: the program is Kitex-Protobuf's (every
+// walker kernel is built once per wire format, so that neither walker's registers bound the other's occupancy)
+template <bool W, bool PB, class CU>
 __device__ __forceinline__ int walk(const NParams& p, const KxnProgram& P, const KxnCols& C, uint64_t a, uint64_t b,
                                    uint64_t r, CU cur, uint64_t* snap, uint64_t* lim) {
   uint64_t used = 0;
-  return P.pb ? kxn_pb_read_record<W>(P, C, p.in + a, b - a, r, cur, snap, &used, lim)
-              : kxn_read_record<W>(P, C, p.in + a, b - a, r, cur, snap, &used, lim);
+  if constexpr (PB) return kxn_pb_read_record<W>(P, C, p.in + a, b - a, r, cur, snap, &used, lim);
+  else return kxn_read_record<W>(P, C, p.in + a, b - a, r, cur, snap, &used, lim);
 }
 
-template <class CU>
+template <bool PB, class CU>
 __device__ __forceinline__ void measure_record(const NParams& p, const KxnProgram& P, uint64_t r, CU cur,
                                                uint64_t* snap) {
   for (uint32_t k = 0; k < p.ncur; k++) cur.set(k, 0);
@@ -121,10 +122,10 @@ __device__ __forceinline__ void measure_record(const NParams& p, const KxnProgra
     // records, divergent refills and 164 VGPRs in the write pass)
     uint8_t careful = 0;
     if (!rc) {
-      rc = walk<false>(p, P, *p.C, a, b, r, cur, nullptr, nullptr);   // no snapshot stores: the common record
+      rc = walk<false, PB>(p, P, *p.C, a, b, r, cur, nullptr, nullptr);   // no snapshot stores: the common record
       if (rc == KXN_REPEAT) {                                   // a repeated field: again, with snapshots
         for (uint32_t k = 0; k < p.ncur; k++) cur.set(k, 0);
-        rc = walk<false>(p, P, *p.C, a, b, r, cur, snap, nullptr);
+        rc = walk<false, PB>(p, P, *p.C, a, b, r, cur, snap, nullptr);
         careful = RC_CAREFUL;
       }
     }
@@ -158,7 +159,7 @@ __device__ __forceinline__ void lds_cols(const KxnCols* g, KxnCols* s) {
 }
 
 // LC: the cursors in LDS (dynamic shared memory: ncur bases, then ncur x NTD u32), else in scratch
-template <bool LC>
+template <bool LC, bool PB>
 __global__ void __launch_bounds__(NTD) measure_kernel(NParams p) {
   __shared__ KxnProgram sP;
   extern __shared__ uint64_t dyn[];
@@ -169,11 +170,11 @@ __global__ void __launch_bounds__(NTD) measure_kernel(NParams p) {
   if (r >= p.n) return;
   uint64_t snap[SNAP];
   if constexpr (LC) {
-    measure_record(p, P, r, KxnCurL{(KXN_LDS uint32_t*)(dyn + p.ncur) + threadIdx.x, (const KXN_LDS uint64_t*)dyn},
+    measure_record<PB>(p, P, r, KxnCurL{(KXN_LDS uint32_t*)(dyn + p.ncur) + threadIdx.x, (const KXN_LDS uint64_t*)dyn},
                    snap);
   } else {
     uint64_t cur[CUR];
-    measure_record(p, P, r, KxnCurP{cur}, snap);
+    measure_record<PB>(p, P, r, KxnCurP{cur}, snap);
   }
 }
 
@@ -278,7 +279,7 @@ __global__ void check_kernel(NParams p) {
 
 // record r (of block b), lane = record; cur holds the record's cursor bases: the block base + the in-block
 // prefix (bsum_kernel)
-template <class CU>
+template <bool PB, class CU>
 __device__ __forceinline__ void write_record(const NParams& p, const KxnProgram& P, const KxnCols& C, uint64_t b,
                                              uint64_t r, CU cur, uint64_t* lim, uint64_t* snap) {
   const uint8_t raw = p.rcode[r];
@@ -295,9 +296,9 @@ __device__ __forceinline__ void write_record(const NParams& p, const KxnProgram&
         lim[k] = r + 1 < rb1 ? base + p.counts[(uint64_t)k * p.n + r + 1]
                              : (b + 1 < p.nblk ? p.bsum[(uint64_t)k * p.nblk + b + 1] : p.totals[k]);
       }
-      (void)walk<true>(p, P, C, a, e, r, cur, snap, lim);
+      (void)walk<true, PB>(p, P, C, a, e, r, cur, snap, lim);
     } else {   // the fast walk writes only inside the record's extents
-      (void)walk<true>(p, P, C, a, e, r, cur, nullptr, nullptr);
+      (void)walk<true, PB>(p, P, C, a, e, r, cur, nullptr, nullptr);
     }
   } else {
     kxn_failed_record(P, C, r, cur);
@@ -307,7 +308,7 @@ __device__ __forceinline__ void write_record(const NParams& p, const KxnProgram&
 
 // one record per thread: workgroup w holds records [w·NTD, (w + 1)·NTD) of block w / (RB / NTD) (a workgroup
 // per block looping over its quarters left 4 waves per SIMD: DESIGN §3.10)
-template <bool LC>
+template <bool LC, bool PB>
 __global__ void __launch_bounds__(NTD) write_kernel(NParams p) {
   if (*p.flag) return;
   __shared__ KxnProgram sP;
@@ -325,11 +326,11 @@ __global__ void __launch_bounds__(NTD) write_kernel(NParams p) {
   if constexpr (LC) {
     KXN_LDS uint32_t* c = (KXN_LDS uint32_t*)(dyn + p.ncur) + threadIdx.x;
     for (uint32_t k = 0; k < p.ncur; k++) c[k * NTD] = p.counts[(uint64_t)k * p.n + r];   // in-block prefixes
-    write_record(p, P, C, b, r, KxnCurL{c, (const KXN_LDS uint64_t*)dyn}, lim, snap);
+    write_record<PB>(p, P, C, b, r, KxnCurL{c, (const KXN_LDS uint64_t*)dyn}, lim, snap);
   } else {
     uint64_t cur[CUR];
     for (uint32_t k = 0; k < p.ncur; k++) cur[k] = p.bsum[(uint64_t)k * p.nblk + b] + p.counts[(uint64_t)k * p.n + r];
-    write_record(p, P, C, b, r, KxnCurP{cur}, lim, snap);
+    write_record<PB>(p, P, C, b, r, KxnCurP{cur}, lim, snap);
   }
 }
 
@@ -391,6 +392,7 @@ struct EParams {
 // encode blocks: ERB = NT records, one per thread (a workgroup per 1024 records looping over its quarters
 // left 4 waves per SIMD)
 constexpr int ERB = NT;
+template <bool PB>
 __global__ void __launch_bounds__(NT) esize_kernel(EParams p) {
   __shared__ uint64_t sh[NT / 64];
   __shared__ KxnProgram sP;
@@ -401,7 +403,8 @@ __global__ void __launch_bounds__(NT) esize_kernel(EParams p) {
   const uint64_t r = (uint64_t)blockIdx.x * ERB + threadIdx.x;
   uint64_t sz = 0;
   if (r < p.n) {   // Kitex-PB: the record's Batch frame (0x0A, uvarint body length, body)
-    sz = P.pb ? kxn_pb_frame_size(P, C, r) : kxn_write_record<false>(P, C, r, nullptr, 0);
+    if constexpr (PB) sz = kxn_pb_frame_size(P, C, r);
+    else sz = kxn_write_record<false>(P, C, r, nullptr, 0);
     p.sizes[r] = sz;
   }
   uint64_t tot;
@@ -434,6 +437,7 @@ __global__ void __launch_bounds__(1024) escan_kernel(EParams p) {
   }
 }
 
+template <bool PB>
 __global__ void __launch_bounds__(NT) ewrite_kernel(EParams p) {
   __shared__ uint64_t sh[NT / 64];
   __shared__ KxnProgram sP;
@@ -447,7 +451,7 @@ __global__ void __launch_bounds__(NT) ewrite_kernel(EParams p) {
   uint64_t tot;
   const uint64_t at = p.bsum[blockIdx.x] + wg_excl(sz, &tot, sh);
   if (r < p.n) {
-    if (P.pb) kxn_pb_write_frame(P, C, r, p.out, at, sz);
+    if constexpr (PB) kxn_pb_write_frame(P, C, r, p.out, at, sz);
     else (void)kxn_write_record<true>(P, C, r, p.out, at);
     if (p.offsets_out) p.offsets_out[r] = at;
   }
@@ -560,10 +564,10 @@ int kx_launch_nested_decode(const KxnProgram* dprog, const KxnProgram& hprog, co
   // the cursors in LDS when they fit beside the program at two workgroups per CU (KX_NESTED_LDS=0: scratch)
   const size_t curl = (size_t)hprog.ncur * (8 + 4 * NTD);
   const bool lc = kx_knob(KXK_NESTED_LDS) && sizeof(KxnProgram) + curl <= 160 * 1024;
-  if (lc)
-    hipLaunchKernelGGL(measure_kernel<true>, dim3((unsigned)((n + NTD - 1) / NTD)), dim3(NTD), curl, stream, p);
-  else
-    hipLaunchKernelGGL(measure_kernel<false>, dim3((unsigned)((n + NTD - 1) / NTD)), dim3(NTD), 0, stream, p);
+  const dim3 gw((unsigned)((n + NTD - 1) / NTD));
+  auto mk = hprog.pb ? (lc ? measure_kernel<true, true> : measure_kernel<false, true>)
+                     : (lc ? measure_kernel<true, false> : measure_kernel<false, false>);
+  hipLaunchKernelGGL(mk, gw, dim3(NTD), lc ? curl : 0, stream, p);
   KX_HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(bsum_kernel, dim3((unsigned)p.nblk, hprog.ncur), dim3(NT), 0, stream, p);
   KX_HIP_CHECK(hipGetLastError());
@@ -578,10 +582,9 @@ int kx_launch_nested_decode(const KxnProgram* dprog, const KxnProgram& hprog, co
   }
   hipLaunchKernelGGL(check_kernel, dim3(1), dim3(64), 0, stream, p);
   KX_HIP_CHECK(hipGetLastError());
-  if (lc)
-    hipLaunchKernelGGL(write_kernel<true>, dim3((unsigned)((n + NTD - 1) / NTD)), dim3(NTD), curl, stream, p);
-  else
-    hipLaunchKernelGGL(write_kernel<false>, dim3((unsigned)((n + NTD - 1) / NTD)), dim3(NTD), 0, stream, p);
+  auto wk = hprog.pb ? (lc ? write_kernel<true, true> : write_kernel<false, true>)
+                     : (lc ? write_kernel<true, false> : write_kernel<false, false>);
+  hipLaunchKernelGGL(wk, gw, dim3(NTD), lc ? curl : 0, stream, p);
   KX_HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(64), 0, stream, p);
   KX_HIP_CHECK(hipGetLastError());
@@ -594,7 +597,6 @@ int kx_launch_nested_encode(const KxnProgram* dprog, const KxnProgram& hprog, co
                             uint8_t* out, uint64_t out_cap, uint64_t* sizes_out, uint64_t* offsets_out,
                             kx_status* status, void* ws, size_t ws_size, hipStream_t stream, bool sizes_only,
                             const uint64_t* out_base) {
-  (void)hprog;
   if (ws_size < kx_nested_enc_ws_bytes(n)) return KX_ERR_INVALID_ARG;
   EParams p{};
   p.P = dprog;
@@ -609,12 +611,12 @@ int kx_launch_nested_encode(const KxnProgram* dprog, const KxnProgram& hprog, co
   p.status = status;
   p.out_base = out_base;
   if (status) KX_HIP_CHECK(hipMemsetAsync(status, 0, sizeof(kx_status), stream));
-  hipLaunchKernelGGL(esize_kernel, dim3((unsigned)p.nblk), dim3(NT), 0, stream, p);
+  hipLaunchKernelGGL(hprog.pb ? esize_kernel<true> : esize_kernel<false>, dim3((unsigned)p.nblk), dim3(NT), 0, stream, p);
   KX_HIP_CHECK(hipGetLastError());
   if (sizes_only) return KX_OK;
   hipLaunchKernelGGL(escan_kernel, dim3(1), dim3(1024), 0, stream, p);
   KX_HIP_CHECK(hipGetLastError());
-  hipLaunchKernelGGL(ewrite_kernel, dim3((unsigned)p.nblk), dim3(NT), 0, stream, p);
+  hipLaunchKernelGGL(hprog.pb ? ewrite_kernel<true> : ewrite_kernel<false>, dim3((unsigned)p.nblk), dim3(NT), 0, stream, p);
   KX_HIP_CHECK(hipGetLastError());
   return KX_OK;
 }
