@@ -286,6 +286,29 @@ __device__ __forceinline__ uint32_t canon_t(uint32_t t) {
   }
 }
 
+// Strings, and lists / sets / maps whose elements are strings or fixed-size, are skipped where they are met
+// (at a depth that leaves their elements inside the limit) instead of through a frame each: the frame stack
+// lives in scratch, and a store + load per string field / element was most of the skip pass's memory traffic
+// on nested records
+__device__ __forceinline__ int dskip_str(const Src& w, uint64_t& pos, uint64_t limit) {
+  if (limit - pos < 4) return KX_ERR_EOF;
+  const int32_t l = (int32_t)be32(w, pos);
+  if (l < 0) return KX_ERR_INVALID_DATA;
+  if (limit - pos - 4 < (uint64_t)l) return KX_ERR_EOF;
+  pos += 4 + (uint64_t)l;
+  return KX_OK;
+}
+
+// a leaf element (a string or fixed-size type, the caller checked which)
+__device__ __forceinline__ int dskip_leaf(const Src& w, uint64_t& pos, uint64_t limit, int sz) {
+  if (sz > 0) {
+    if (limit - pos < (uint64_t)sz) return KX_ERR_EOF;
+    pos += (uint64_t)sz;
+    return KX_OK;
+  }
+  return dskip_str(w, pos, limit);
+}
+
 __device__ __forceinline__ int dskip_body(const Src& w, uint64_t& pos, uint64_t limit, uint32_t t0, int md0) {
   uint64_t stk[66];
   int sp = 0;
@@ -326,6 +349,15 @@ __device__ __forceinline__ int dskip_body(const Src& w, uint64_t& pos, uint64_t 
             pos += 6 + b; sp--; continue;
           }
           pos += 6;
+          if (md > 1 && (ks > 0 || k == KX_T_STRING) && (vs > 0 || v == KX_T_STRING)) {
+            for (int32_t i = 0; i < cnt; i++) {
+              int rc = dskip_leaf(w, pos, limit, ks);
+              if (!rc) rc = dskip_leaf(w, pos, limit, vs);
+              if (rc) return rc;
+            }
+            sp--;
+            continue;
+          }
           stk[sp - 1] = (uint64_t)t | ((uint64_t)canon_t(k) << 4) | ((uint64_t)canon_t(v) << 8) |
                         (3ull << 12) | ((uint64_t)md << 15) | ((uint64_t)(uint32_t)cnt << 32);
           continue;
@@ -342,6 +374,14 @@ __device__ __forceinline__ int dskip_body(const Src& w, uint64_t& pos, uint64_t 
             pos += 5 + b; sp--; continue;
           }
           pos += 5;
+          if (md > 1 && v == KX_T_STRING) {
+            for (int32_t i = 0; i < cnt; i++) {
+              const int rc = dskip_str(w, pos, limit);
+              if (rc) return rc;
+            }
+            sp--;
+            continue;
+          }
           stk[sp - 1] = (uint64_t)t | ((uint64_t)canon_t(v) << 8) | (2ull << 12) | ((uint64_t)md << 15) |
                         ((uint64_t)(uint32_t)cnt << 32);
           continue;
@@ -361,6 +401,11 @@ __device__ __forceinline__ int dskip_body(const Src& w, uint64_t& pos, uint64_t 
       }
       if (limit - pos < 2) return KX_ERR_EOF;
       pos += 2;
+      if (tp == KX_T_STRING && md > 1) {
+        const int rc = dskip_str(w, pos, limit);
+        if (rc) return rc;
+        continue;
+      }
       stk[sp++] = mk(tp, md - 1);
     } else if (st == 2) {  // list / set elements
       if (rem == 0) { sp--; continue; }
