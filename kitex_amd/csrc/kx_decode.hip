@@ -309,13 +309,45 @@ __device__ __forceinline__ int dskip_leaf(const Src& w, uint64_t& pos, uint64_t 
   return dskip_str(w, pos, limit);
 }
 
+// a list / set / map field whose elements are leaves, skipped whole (*done); else nothing is consumed and the
+// frame path takes it (also for a header past the limit, so that its error is the frame path's)
+__device__ __forceinline__ int dskip_flat(const Src& w, uint64_t& pos, uint64_t limit, uint32_t t, bool& done) {
+  done = false;
+  const bool map = t == KX_T_MAP;
+  const uint64_t hl = map ? 6 : 5;
+  if (limit - pos < hl) return KX_OK;
+  const uint32_t h = ld4(w, pos);
+  const uint32_t k = h & 0xff, v = map ? (h >> 8) & 0xff : k;
+  const int ks = tsize(k), vs = tsize(v);
+  if (!(ks > 0 || k == KX_T_STRING) || !(vs > 0 || v == KX_T_STRING)) return KX_OK;
+  const int32_t cnt = (int32_t)be32(w, pos + (map ? 2 : 1));
+  if (cnt < 0) return KX_ERR_INVALID_DATA;
+  done = true;
+  pos += hl;
+  if (map ? ks > 0 && vs > 0 : ks > 0) {
+    const uint64_t b = (uint64_t)cnt * (uint64_t)(map ? ks + vs : ks);
+    if (limit - pos < b) return KX_ERR_EOF;
+    pos += b;
+    return KX_OK;
+  }
+  for (int32_t i = 0; i < cnt; i++) {
+    int rc = dskip_leaf(w, pos, limit, ks);
+    if (!rc && map) rc = dskip_leaf(w, pos, limit, vs);
+    if (rc) return rc;
+  }
+  return KX_OK;
+}
+
 __device__ __forceinline__ int dskip_body(const Src& w, uint64_t& pos, uint64_t limit, uint32_t t0, int md0) {
   uint64_t stk[66];
   int sp = 0;
   auto mk = [](uint32_t t, uint32_t md) -> uint64_t { return (uint64_t)(canon_t(t) | (md << 15)); };
-  stk[sp++] = mk(t0, (uint32_t)md0);
+  // the top frame in a register (stk holds the frames below it): the field loop of a struct reads and the
+  // element loops update it at every step
+  uint64_t top = mk(t0, (uint32_t)md0);
+  sp = 1;
   while (sp > 0) {
-    uint64_t fr = stk[sp - 1];
+    uint64_t fr = top;
     uint32_t t = fr & 15, kt = (fr >> 4) & 15, vt = (fr >> 8) & 15, st = (fr >> 12) & 3;
     uint32_t ph = (fr >> 14) & 1, md = (fr >> 15) & 127;
     uint32_t rem = (uint32_t)(fr >> 32);
@@ -324,7 +356,7 @@ __device__ __forceinline__ int dskip_body(const Src& w, uint64_t& pos, uint64_t 
       int sz = tsize(t);
       if (sz > 0) {
         if (limit - pos < (uint64_t)sz) return KX_ERR_EOF;
-        pos += sz; sp--; continue;
+        pos += sz; if (--sp) top = stk[sp - 1]; continue;
       }
       switch (t) {
         case KX_T_STRING: {
@@ -332,10 +364,10 @@ __device__ __forceinline__ int dskip_body(const Src& w, uint64_t& pos, uint64_t 
           int32_t l = (int32_t)be32(w, pos);
           if (l < 0) return KX_ERR_INVALID_DATA;
           if (limit - pos - 4 < (uint64_t)l) return KX_ERR_EOF;
-          pos += 4 + (uint64_t)l; sp--; continue;
+          pos += 4 + (uint64_t)l; if (--sp) top = stk[sp - 1]; continue;
         }
         case KX_T_STRUCT:
-          stk[sp - 1] = (fr & ~(3ull << 12)) | (1ull << 12); continue;
+          top = (fr & ~(3ull << 12)) | (1ull << 12); continue;
         case KX_T_MAP: {
           if (limit - pos < 6) return KX_ERR_EOF;
           uint32_t h = ld4(w, pos);
@@ -346,7 +378,7 @@ __device__ __forceinline__ int dskip_body(const Src& w, uint64_t& pos, uint64_t 
           if (ks > 0 && vs > 0) {
             uint64_t b = (uint64_t)cnt * (uint64_t)(ks + vs);
             if (limit - pos - 6 < b) return KX_ERR_EOF;
-            pos += 6 + b; sp--; continue;
+            pos += 6 + b; if (--sp) top = stk[sp - 1]; continue;
           }
           pos += 6;
           if (md > 1 && (ks > 0 || k == KX_T_STRING) && (vs > 0 || v == KX_T_STRING)) {
@@ -355,10 +387,10 @@ __device__ __forceinline__ int dskip_body(const Src& w, uint64_t& pos, uint64_t 
               if (!rc) rc = dskip_leaf(w, pos, limit, vs);
               if (rc) return rc;
             }
-            sp--;
+            if (--sp) top = stk[sp - 1];
             continue;
           }
-          stk[sp - 1] = (uint64_t)t | ((uint64_t)canon_t(k) << 4) | ((uint64_t)canon_t(v) << 8) |
+          top = (uint64_t)t | ((uint64_t)canon_t(k) << 4) | ((uint64_t)canon_t(v) << 8) |
                         (3ull << 12) | ((uint64_t)md << 15) | ((uint64_t)(uint32_t)cnt << 32);
           continue;
         }
@@ -371,7 +403,7 @@ __device__ __forceinline__ int dskip_body(const Src& w, uint64_t& pos, uint64_t 
           if (vs > 0) {
             uint64_t b = (uint64_t)cnt * (uint64_t)vs;
             if (limit - pos - 5 < b) return KX_ERR_EOF;
-            pos += 5 + b; sp--; continue;
+            pos += 5 + b; if (--sp) top = stk[sp - 1]; continue;
           }
           pos += 5;
           if (md > 1 && v == KX_T_STRING) {
@@ -379,10 +411,10 @@ __device__ __forceinline__ int dskip_body(const Src& w, uint64_t& pos, uint64_t 
               const int rc = dskip_str(w, pos, limit);
               if (rc) return rc;
             }
-            sp--;
+            if (--sp) top = stk[sp - 1];
             continue;
           }
-          stk[sp - 1] = (uint64_t)t | ((uint64_t)canon_t(v) << 8) | (2ull << 12) | ((uint64_t)md << 15) |
+          top = (uint64_t)t | ((uint64_t)canon_t(v) << 8) | (2ull << 12) | ((uint64_t)md << 15) |
                         ((uint64_t)(uint32_t)cnt << 32);
           continue;
         }
@@ -393,7 +425,7 @@ __device__ __forceinline__ int dskip_body(const Src& w, uint64_t& pos, uint64_t 
       if (limit - pos < 1) return KX_ERR_EOF;
       uint32_t tp = ld1(w, pos);
       pos += 1;
-      if (tp == KX_T_STOP) { sp--; continue; }
+      if (tp == KX_T_STOP) { if (--sp) top = stk[sp - 1]; continue; }
       int fsz = tsize(tp);
       if (fsz > 0) {
         if (limit - pos < 2 + (uint64_t)fsz) return KX_ERR_EOF;
@@ -406,23 +438,29 @@ __device__ __forceinline__ int dskip_body(const Src& w, uint64_t& pos, uint64_t 
         if (rc) return rc;
         continue;
       }
-      stk[sp++] = mk(tp, md - 1);
+      if ((tp == KX_T_LIST || tp == KX_T_SET || tp == KX_T_MAP) && md > 2) {
+        bool done;
+        const int rc = dskip_flat(w, pos, limit, tp, done);
+        if (rc) return rc;
+        if (done) continue;
+      }
+      stk[sp - 1] = top; top = mk(tp, md - 1); sp++;
     } else if (st == 2) {  // list / set elements
-      if (rem == 0) { sp--; continue; }
-      stk[sp - 1] = (fr & 0xffffffffull) | ((uint64_t)(rem - 1) << 32);
-      stk[sp++] = mk(vt, md - 1);
+      if (rem == 0) { if (--sp) top = stk[sp - 1]; continue; }
+      top = (fr & 0xffffffffull) | ((uint64_t)(rem - 1) << 32);
+      stk[sp - 1] = top; top = mk(vt, md - 1); sp++;
     } else {  // map: key then value
-      if (rem == 0) { sp--; continue; }
+      if (rem == 0) { if (--sp) top = stk[sp - 1]; continue; }
       uint32_t et = ph ? vt : kt;
       uint64_t nf = ph ? ((fr & ~(1ull << 14)) & 0xffffffffull) | ((uint64_t)(rem - 1) << 32)
                        : (fr | (1ull << 14));
-      stk[sp - 1] = nf;
+      top = nf;
       int es = tsize(et);
       if (es > 0) {  // fixed-size element: skipn (only reached when the other side is not)
         if (limit - pos < (uint64_t)es) return KX_ERR_EOF;
         pos += es;
       } else {
-        stk[sp++] = mk(et, md - 1);
+        stk[sp - 1] = top; top = mk(et, md - 1); sp++;
       }
     }
   }
