@@ -1027,7 +1027,8 @@ KXN_HD int kxn_pb_value(const KxnProgram& P, const KxnCols& C, B b, uint64_t end
       const int rc = kxn_uvarint(b, end, q, &l);
       if (rc) return rc;
       if (l > end - *q) return KX_ERR_EOF;
-      if (N.kind == KN_STRING && N.pbk != KX_PB_BYTES && !kxn_utf8(b + *q, l)) return KX_ERR_INVALID_DATA;
+      // (the write walk reads only records its measure walk validated)
+      if (!W && N.kind == KN_STRING && N.pbk != KX_PB_BYTES && !kxn_utf8(b + *q, l)) return KX_ERR_INVALID_DATA;
       if (W) kxn_copy((uint8_t*)C.data[N.col] + cur[N.cur], b + *q, kxn_room(S, N.cur, cur[N.cur], l));
       cur.add(N.cur, l);
       *q += l;
