@@ -974,7 +974,8 @@ KXN_HD uint64_t kxn_ascii_prefix(const uint8_t* s, uint64_t n) {
   return i;
 }
 template <class B>
-KXN_HD bool kxn_utf8(B s, uint64_t n) {
+KXN_HD bool kxn_utf8(B s, uint64_t n, B lo) {
+  (void)lo;
   uint64_t i = kxn_ascii_prefix(s, n);
   while (i < n) {
     const uint32_t c = s[i];
@@ -996,6 +997,47 @@ KXN_HD bool kxn_utf8(B s, uint64_t n) {
     i += (uint64_t)k + 1;
   }
   return true;
+}
+
+// the input itself: 8 bytes per load into a register and the sequence checked there (a multi-byte character
+// was a chain of dependent byte loads per byte); the last < 8 bytes come from one load ending at the string's
+// end, when the record holds 8 bytes there ([lo, s + n) is readable)
+KXN_HD bool kxn_utf8(const uint8_t* s, uint64_t n, const uint8_t* lo) {
+  uint64_t i = 0;
+  uint32_t need = 0, k = 0, cp = 0;
+  while (i < n) {
+    const uint64_t m = n - i < 8 ? n - i : 8;
+    uint64_t x = 0;
+    if (m == 8) {
+      __builtin_memcpy(&x, s + i, 8);
+    } else if ((uint64_t)(s + n - lo) >= 8) {
+      __builtin_memcpy(&x, s + n - 8, 8);
+      x >>= 8 * (8 - m);
+    } else {
+      for (uint64_t j = 0; j < m; j++) x |= (uint64_t)s[i + j] << (8 * j);
+    }
+    i += m;
+    if (need == 0 && !(x & 0x8080808080808080ull)) continue;   // ASCII (x's bytes past m are 0)
+    for (uint64_t j = 0; j < m; j++, x >>= 8) {
+      const uint32_t c = (uint32_t)(x & 0xff);
+      if (need == 0) {
+        if (c < 0x80) continue;
+        if ((c & 0xe0) == 0xc0) { k = 1; cp = c & 0x1f; }
+        else if ((c & 0xf0) == 0xe0) { k = 2; cp = c & 0x0f; }
+        else if ((c & 0xf8) == 0xf0) { k = 3; cp = c & 0x07; }
+        else return false;
+        need = k;
+        continue;
+      }
+      if ((c & 0xc0) != 0x80) return false;
+      cp = (cp << 6) | (c & 0x3f);
+      if (--need == 0) {
+        if ((k == 1 && cp < 0x80) || (k == 2 && cp < 0x800) || (k == 3 && cp < 0x10000)) return false;
+        if (cp > 0x10ffff || (cp >= 0xd800 && cp <= 0xdfff)) return false;
+      }
+    }
+  }
+  return need == 0;
 }
 
 struct KxnPFrame {      // an open message (its fields) or map entry (fields 1 / 2) (32 B)
@@ -1028,7 +1070,7 @@ KXN_HD int kxn_pb_value(const KxnProgram& P, const KxnCols& C, B b, uint64_t end
       if (rc) return rc;
       if (l > end - *q) return KX_ERR_EOF;
       // (the write walk reads only records its measure walk validated)
-      if (!W && N.kind == KN_STRING && N.pbk != KX_PB_BYTES && !kxn_utf8(b + *q, l)) return KX_ERR_INVALID_DATA;
+      if (!W && N.kind == KN_STRING && N.pbk != KX_PB_BYTES && !kxn_utf8(b + *q, l, b)) return KX_ERR_INVALID_DATA;
       if (W) kxn_copy((uint8_t*)C.data[N.col] + cur[N.cur], b + *q, kxn_room(S, N.cur, cur[N.cur], l));
       cur.add(N.cur, l);
       *q += l;
