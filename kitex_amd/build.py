@@ -62,7 +62,11 @@ def build(force: bool = False, verbose: bool = False, extra=(), variant: str = "
     for src, obj, flags in _units(libdir):
         if only_objs is not None and os.path.basename(obj) not in only_objs:
             import shutil
-            shutil.copy2(os.path.join(LIBDIR, os.path.basename(obj)), obj)
+            dflt = os.path.join(LIBDIR, os.path.basename(obj))
+            if not os.path.exists(dflt) or os.path.getmtime(dflt) < max(os.path.getmtime(src), newest_hdr):
+                raise RuntimeError(f"KX_VARIANT_PARTS: the default build's {os.path.basename(obj)} is missing or "
+                                   "older than its sources; run `python -m kitex_amd.build` first")
+            shutil.copy2(dflt, obj)
             continue
         fresh = (not force and not extra and not variant and os.path.exists(obj)
                  and os.path.getmtime(obj) > max(os.path.getmtime(src), newest_hdr))

@@ -401,6 +401,16 @@ KXN_HD uint64_t kxn_scalar(uint32_t t, B p) {  // host order; BOOL is `b == 1` (
     default: return kxn_be64(p);
   }
 }
+// the same from the value's first 8 bytes in a register (little-endian load of the big-endian value)
+KXN_HD uint64_t kxn_scalar_pre(uint32_t t, uint64_t lo) {
+  switch (t) {
+    case KX_T_BOOL: return (lo & 0xff) == 1;
+    case KX_T_BYTE: return lo & 0xff;
+    case KX_T_I16: return (uint32_t)__builtin_bswap16((uint16_t)lo);
+    case KX_T_I32: return __builtin_bswap32((uint32_t)lo);
+    default: return __builtin_bswap64(lo);
+  }
+}
 
 // byte copy in blocks of 16: a block's loads are all issued before its stores (the compiler may not
 // reorder them itself: source and destination could alias), so a lane waits once per 16 bytes rather
@@ -526,10 +536,60 @@ KXN_HD void kxn_inst_end(const KxnProgram& P, const KxnCols& C, int R, CU cur, K
   }
 }
 
+// 16 bytes of the input at a field's tag, in registers: the tag and, from the bytes after it, the field's value
+// (a varint, a fixed word or a length) decode without a second dependent load (av: bytes valid; 0 = none)
+struct KxnPre {
+  uint64_t lo, hi;
+  uint32_t av;
+};
+template <class B>
+KXN_HD bool kxn_pre_load(B b, uint64_t q, KxnPre* p) {
+  (void)b; (void)q; (void)p;
+  return false;
+}
+KXN_HD bool kxn_pre_load(const uint8_t* b, uint64_t q, KxnPre* p) {
+  __builtin_memcpy(&p->lo, b + q, 8);
+  __builtin_memcpy(&p->hi, b + q + 8, 8);
+  p->av = 16;
+  return true;
+}
+// the varint at the window's start as kxn_uvarint reads it with 10 bytes left (false: not decodable here —
+// fewer than 10 bytes valid, or malformed — and the caller reads it from memory, which finds the error)
+KXN_HD bool kxn_uvarint_pre(const KxnPre& p, uint64_t* v, uint32_t* used) {
+  if (p.av < 10) return false;
+  const uint64_t lo = p.lo;
+  const uint32_t b8 = (uint32_t)p.hi & 0xffu, b9 = (uint32_t)(p.hi >> 8) & 0xffu;
+  const uint64_t stop = ~lo & 0x8080808080808080ull;
+  const uint32_t k = stop ? (uint32_t)__builtin_ctzll(stop) >> 3 : b8 < 0x80 ? 8u : 9u;
+  if (k == 9 && b9 > 1) return false;
+  const uint64_t keep = k >= 7 ? ~0ull : (2ull << (8 * k + 7)) - 1;
+  uint64_t x = lo & keep & 0x7f7f7f7f7f7f7f7full;
+  x = (x & 0x007f007f007f007full) | ((x & 0x7f007f007f007f00ull) >> 1);
+  x = (x & 0x00003fff00003fffull) | ((x & 0x3fff00003fff0000ull) >> 2);
+  x = (x & 0x000000000fffffffull) | ((x & 0x0fffffff00000000ull) >> 4);
+  if (k >= 8) x |= (uint64_t)(b8 & 0x7f) << 56;
+  if (k >= 9) x |= (uint64_t)(b9 & 0x01) << 63;
+  *v = x;
+  *used = k + 1;
+  return true;
+}
+// the window advanced by u (1 .. 10) bytes
+KXN_HD void kxn_pre_skip(KxnPre* p, uint32_t u) {
+  if (u < 8) {
+    p->lo = (p->lo >> (8 * u)) | (p->hi << (64 - 8 * u));
+    p->hi >>= 8 * u;
+  } else {
+    p->lo = p->hi >> (8 * (u - 8));
+    p->hi = 0;
+  }
+  p->av = p->av > u ? p->av - u : 0;
+}
+
 // read one leaf value (SCALAR / STRING / RAW) of node X at b[*q]
+// (pre: the value's first bytes in registers, Thrift byte order, when av > 0)
 template <bool W, class B, class CU>
 KXN_HD int kxn_leaf(const KxnProgram& P, const KxnCols& C, B b, uint64_t len, uint64_t* q, int X, CU cur,
-                    KxnState& S) {
+                    KxnState& S, const KxnPre* pre = nullptr) {
   const KxnNode& N = P.node[X];
   if (N.kind == KN_RAW) {                                    // a recursive struct: its encoded bytes
     uint64_t e = *q;
@@ -540,14 +600,16 @@ KXN_HD int kxn_leaf(const KxnProgram& P, const KxnCols& C, B b, uint64_t len, ui
     *q = e;
     return KX_OK;
   }
+  const bool pr = pre && pre->av >= 8;
   if (N.kind == KN_SCALAR) {
     if (*q + N.width > len) return KX_ERR_EOF;
-    if (W && S.live[N.level]) kxn_put_val(C, N.col, N.width, S.idx[N.level], kxn_scalar(N.ttype, b + *q));
+    if (W && S.live[N.level])
+      kxn_put_val(C, N.col, N.width, S.idx[N.level], pr ? kxn_scalar_pre(N.ttype, pre->lo) : kxn_scalar(N.ttype, b + *q));
     *q += N.width;
     return KX_OK;
   }
   if (*q + 4 > len) return KX_ERR_EOF;                       // ReadString: a copy
-  const int32_t c = (int32_t)kxn_be32(b + *q);
+  const int32_t c = (int32_t)(pr ? __builtin_bswap32((uint32_t)pre->lo) : kxn_be32(b + *q));
   if (c < 0) return KX_ERR_NEGATIVE_SIZE;
   const uint64_t l = (uint64_t)c;
   if (*q + 4 + l > len) return KX_ERR_EOF;
@@ -563,15 +625,17 @@ KXN_HD int kxn_leaf(const KxnProgram& P, const KxnCols& C, B b, uint64_t len, ui
 // containers that push a frame are opened by the caller.
 template <bool W, class B, class CU>
 KXN_HD int kxn_value(const KxnProgram& P, const KxnCols& C, B b, uint64_t len, uint64_t* q, int X,
-                     CU cur, KxnState& S, KxnFrame* stk, int* sp) {
+                     CU cur, KxnState& S, KxnFrame* stk, int* sp, const KxnPre& pre) {
   const KxnNode& N = P.node[X];
   const uint32_t kind = N.kind;
-  if (kind <= KN_RAW) return kxn_leaf<W>(P, C, b, len, q, X, cur, S);
+  if (kind <= KN_RAW) return kxn_leaf<W>(P, C, b, len, q, X, cur, S, &pre);
   // STRUCT / LIST / SET / MAP: ReadListBegin's type + count, ReadMapBegin's two types + count
   // (struct_tpl.go:425-625)
   const uint32_t hl = kind == KN_LIST ? 5u : kind == KN_MAP ? 6u : 0u;
   if (*q + hl > len) return KX_ERR_EOF;
-  const int32_t c = hl ? (int32_t)kxn_be32(b + *q + (kind == KN_LIST ? 1u : 2u)) : 0;
+  const uint32_t ho = kind == KN_LIST ? 1u : 2u;
+  const int32_t c = !hl ? 0 : pre.av >= 8 ? (int32_t)__builtin_bswap32((uint32_t)(pre.lo >> (8 * ho)))
+                                          : (int32_t)kxn_be32(b + *q + ho);
   if (c < 0) return KX_ERR_NEGATIVE_SIZE;
   if (hl && P.node[N.a].kind <= KN_RAW && (kind == KN_LIST || P.node[N.b].kind <= KN_RAW)) {
     *q += hl;
@@ -615,10 +679,12 @@ KXN_HD int kxn_read_record(const KxnProgram& P, const KxnCols& C, B b, uint64_t 
   // one record tiled, DESIGN §3.10, most of it divergence)
   int rc = KX_OK;
   int X = P.rec_node;
+  KxnPre pre{0, 0, 0};   // a field's value bytes, loaded with its header (consumed by the next value read)
   for (;;) {
     if (X >= 0) {
-      rc = kxn_value<W>(P, C, b, len, &q, X, cur, S, stk, &sp);
+      rc = kxn_value<W>(P, C, b, len, &q, X, cur, S, stk, &sp, pre);
       X = -1;
+      pre.av = 0;
       if (rc) break;
     }
     if (sp == 0) break;
@@ -626,9 +692,12 @@ KXN_HD int kxn_read_record(const KxnProgram& P, const KxnCols& C, B b, uint64_t 
     if (F.kind == KN_STRUCT) {
       const KxnStruct& T = P.st[F.id];
       if (q + 1 > len) { rc = KX_ERR_EOF; break; }             // ReadFieldBegin
-      // type and id in one load where 4 bytes remain (all but a record's final STOP)
-      const bool h4 = q + 4 <= len;
-      const uint32_t hw = h4 ? kxn_be32(b + q) : 0u;
+      // header and value from one 16-byte load where the record holds it, else type and id in one load where
+      // 4 bytes remain (all but a record's final STOP)
+      pre.av = 0;
+      const bool h16 = len - q >= 16 && kxn_pre_load(b, q, &pre);
+      const bool h4 = h16 || q + 4 <= len;
+      const uint32_t hw = h16 ? __builtin_bswap32((uint32_t)pre.lo) : h4 ? kxn_be32(b + q) : 0u;
       const uint32_t t = h4 ? hw >> 24 : (uint32_t)b[q];
       const int L = T.level;
       if (t == KX_T_STOP) {
@@ -640,6 +709,7 @@ KXN_HD int kxn_read_record(const KxnProgram& P, const KxnCols& C, B b, uint64_t 
       if (q + 3 > len) { rc = KX_ERR_EOF; break; }
       const int16_t id = h4 ? (int16_t)(uint16_t)(hw >> 8) : (int16_t)kxn_be16(b + q + 1);
       q += 3;
+      kxn_pre_skip(&pre, 3);
       const int fi = kxn_field(P, F.id, T, id);
       if (fi < 0 || P.f[fi].ttype != t) {                       // default: / mismatched type -> Skip
         if ((rc = kxn_skip(b, len, &q, t, KXN_SKIP_DEPTH))) break;
@@ -671,7 +741,8 @@ KXN_HD int kxn_read_record(const KxnProgram& P, const KxnCols& C, B b, uint64_t 
       X = G.node;
       continue;
     }
-    // LIST / MAP: close the open element, then open the next one
+    // LIST / MAP: close the open element, then open the next one (its value is read from memory)
+    pre.av = 0;
     const KxnNode& N = P.node[F.id];
     if (F.open && (N.kind == KN_LIST || F.phase == 0)) {
       kxn_inst_end<W>(P, C, N.root, cur, S);
@@ -934,12 +1005,18 @@ KXN_HD uint64_t kxn_le(const uint8_t* p, int n) {   // the input itself: one una
 
 // one scalar of node N at b[*q] (its wire type already matched), in the column's host form
 template <class B>
-KXN_HD int kxn_pb_scalar(const KxnNode& N, B b, uint64_t end, uint64_t* q, uint64_t* out) {
+KXN_HD int kxn_pb_scalar(const KxnNode& N, B b, uint64_t end, uint64_t* q, uint64_t* out,
+                         const KxnPre* pre = nullptr) {
   const uint32_t wt = kxn_pb_wt(N);
   uint64_t v;
   if (wt == 0) {
-    const int rc = kxn_uvarint(b, end, q, &v);
-    if (rc) return rc;
+    uint32_t u;
+    if (pre && kxn_uvarint_pre(*pre, &v, &u)) {
+      *q += u;
+    } else {
+      const int rc = kxn_uvarint(b, end, q, &v);
+      if (rc) return rc;
+    }
     if (N.ttype == KX_T_BOOL) {
       v = v != 0;
     } else if (N.pbk == KX_PB_SINT) {   // protowire.DecodeZigZag (sint32: of the low 32 bits)
@@ -953,7 +1030,7 @@ KXN_HD int kxn_pb_scalar(const KxnNode& N, B b, uint64_t end, uint64_t* q, uint6
   } else {
     const int n = wt == 1 ? 8 : 4;
     if (end - *q < (uint64_t)n) return KX_ERR_EOF;
-    v = kxn_le(b + *q, n);
+    v = pre && pre->av >= (uint32_t)n ? (n == 8 ? pre->lo : (uint64_t)(uint32_t)pre->lo) : kxn_le(b + *q, n);
     *q += (uint64_t)n;
   }
   *out = v;
@@ -1054,20 +1131,25 @@ struct KxnPFrame {      // an open message (its fields) or map entry (fields 1 /
 // frame (close: the root to end with it), a scalar / string value ends `close` at once
 template <bool W, class B, class CU>
 KXN_HD int kxn_pb_value(const KxnProgram& P, const KxnCols& C, B b, uint64_t end, uint64_t* q, int X,
-                        CU cur, KxnState& S, KxnPFrame* stk, int* sp, int close) {
+                        CU cur, KxnState& S, KxnPFrame* stk, int* sp, int close, const KxnPre& pre) {
   const KxnNode& N = P.node[X];
   switch (N.kind) {
     case KN_SCALAR: {
       uint64_t v;
-      const int rc = kxn_pb_scalar(N, b, end, q, &v);
+      const int rc = kxn_pb_scalar(N, b, end, q, &v, &pre);
       if (rc) return rc;
       if (W && S.live[N.level]) kxn_put_val(C, N.col, N.width, S.idx[N.level], v);
       break;
     }
     case KN_STRING: case KN_RAW: {   // string / bytes; a recursive message keeps its bytes (they merge)
       uint64_t l;
-      const int rc = kxn_uvarint(b, end, q, &l);
-      if (rc) return rc;
+      uint32_t u;
+      if (kxn_uvarint_pre(pre, &l, &u)) {
+        *q += u;
+      } else {
+        const int rc = kxn_uvarint(b, end, q, &l);
+        if (rc) return rc;
+      }
       if (l > end - *q) return KX_ERR_EOF;
       // (the write walk reads only records its measure walk validated)
       if (!W && N.kind == KN_STRING && N.pbk != KX_PB_BYTES && !kxn_utf8(b + *q, l, b)) return KX_ERR_INVALID_DATA;
@@ -1078,8 +1160,13 @@ KXN_HD int kxn_pb_value(const KxnProgram& P, const KxnCols& C, B b, uint64_t end
     }
     case KN_STRUCT: {
       uint64_t l;
-      const int rc = kxn_uvarint(b, end, q, &l);
-      if (rc) return rc;
+      uint32_t u;
+      if (kxn_uvarint_pre(pre, &l, &u)) {
+        *q += u;
+      } else {
+        const int rc = kxn_uvarint(b, end, q, &l);
+        if (rc) return rc;
+      }
       if (l > end - *q) return KX_ERR_EOF;
       if (*sp >= KXN_STACK) return KX_ERR_DEPTH_LIMIT;
       stk[*sp] = KxnPFrame{0, 0, N.a, (int16_t)close, 0, *q + l, {0, 0}};
@@ -1111,12 +1198,14 @@ KXN_HD int kxn_pb_read_record(const KxnProgram& P, const KxnCols& C, B b, uint64
   stk[sp++] = KxnPFrame{0, 0, P.node[P.rec_node].a, -1, 0, len, {0, 0}};
   // one value read per iteration at a single call site (as kxn_read_record): X, its frame's end and the
   // root its instance closes are chosen by the field logic below
+  KxnPre pre{0, 0, 0};   // the bytes after the last tag (the value read at the loop's top consumes them)
   int X = -1, xclose = -1;
   uint64_t xend = 0;
   for (;;) {
     if (X >= 0) {
-      rc = kxn_pb_value<W>(P, C, b, xend, &q, X, cur, S, stk, &sp, xclose);
+      rc = kxn_pb_value<W>(P, C, b, xend, &q, X, cur, S, stk, &sp, xclose, pre);
       X = -1;
+      pre.av = 0;
       if (rc) break;
     }
     if (sp == 0) break;
@@ -1128,7 +1217,14 @@ KXN_HD int kxn_pb_read_record(const KxnProgram& P, const KxnCols& C, B b, uint64
       continue;
     }
     uint64_t tag;
-    if ((rc = kxn_uvarint(b, F.end, &q, &tag))) break;
+    uint32_t tu;
+    if (F.end - q >= 16 && kxn_pre_load(b, q, &pre) && kxn_uvarint_pre(pre, &tag, &tu)) {
+      q += tu;
+      kxn_pre_skip(&pre, tu);
+    } else {
+      pre.av = 0;
+      if ((rc = kxn_uvarint(b, F.end, &q, &tag))) break;
+    }
     const uint64_t num = tag >> 3;
     const uint32_t wt = (uint32_t)(tag & 7);
     if (num == 0 || num > 536870911ull) { rc = KX_ERR_INVALID_DATA; break; }   // protowire.MaxValidNumber
