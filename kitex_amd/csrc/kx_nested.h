@@ -183,10 +183,12 @@ KXN_HD int kxn_field(const KxnProgram& P, int si, const KxnStruct& T, int64_t id
 struct KxnCols {
   void* data[KX_MAX_COLUMNS];
   void* arr[KX_MAX_COLUMNS][3];   // offsets, elem_offsets, sub_offsets
-  uint64_t cap[KX_MAX_COLUMNS][4];  // units of data, arr0 (n), arr1, arr2 (entries - 1)
   uint64_t owide;                 // bit c: 8-byte offsets
   uint64_t* presence;
+  uint64_t cap[KX_MAX_COLUMNS][4];  // units of data, arr0 (n), arr1, arr2 (entries - 1): the capacity check only
 };
+// the part of KxnCols the walkers read (everything before cap): the decode write pass keeps this much in LDS
+constexpr unsigned KXN_COLS_HEAD = (unsigned)__builtin_offsetof(KxnCols, cap);
 
 // The walker's cursors, behind a small interface so that they can live where the caller wants them: a
 // plain array here (the host harness, the device's scratch fallback); on the device a per-lane column of

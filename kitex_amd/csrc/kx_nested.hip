@@ -308,7 +308,10 @@ __device__ __forceinline__ void write_record(const NParams& p, const KxnProgram&
 
 // one record per thread: workgroup w holds records [w·NTD, (w + 1)·NTD) of block w / (RB / NTD) (a workgroup
 // per block looping over its quarters left 4 waves per SIMD: DESIGN §3.10)
-template <bool LC, bool PB>
+// CL: the walker's part of the column table (KXN_COLS_HEAD bytes) in LDS after the cursors, when two workgroups
+// per CU still fit (the whole 4 KB table measured slower, 10.3 vs 9.0 ms for 1 M Nesting records: one
+// workgroup per CU)
+template <bool LC, bool PB, bool CL>
 __global__ void __launch_bounds__(NTD) write_kernel(NParams p) {
   if (*p.flag) return;
   __shared__ KxnProgram sP;
@@ -316,10 +319,13 @@ __global__ void __launch_bounds__(NTD) write_kernel(NParams p) {
   const uint64_t b = blockIdx.x / (RB / NTD);
   if (LC)   // the block's base per cursor, shared by the workgroup's lanes
     for (uint32_t k = threadIdx.x; k < p.ncur; k += NTD) dyn[k] = p.bsum[(uint64_t)k * p.nblk + b];
+  KxnCols* sc = (KxnCols*)(dyn + (size_t)p.ncur * (1 + NTD / 2));
+  if (CL) {   // (published by lds_program's barrier)
+    static_assert(KXN_COLS_HEAD % 4 == 0, "dword copy");
+    for (uint32_t i = threadIdx.x; i < KXN_COLS_HEAD / 4; i += NTD) ((uint32_t*)sc)[i] = ((const uint32_t*)p.C)[i];
+  }
   const KxnProgram& P = lds_program(p.P, &sP);
-  // (the column table stays in global memory here: 4 KB more LDS per workgroup measured slower, 10.3 vs 9.0 ms
-  // for 1 M Nesting records, the cursors' two workgroups per CU no longer fitting)
-  const KxnCols& C = *p.C;
+  const KxnCols& C = CL ? *sc : *p.C;
   const uint64_t r = (uint64_t)blockIdx.x * NTD + threadIdx.x;
   if (r >= p.n) return;
   uint64_t lim[CUR], snap[SNAP];
@@ -582,9 +588,10 @@ int kx_launch_nested_decode(const KxnProgram* dprog, const KxnProgram& hprog, co
   }
   hipLaunchKernelGGL(check_kernel, dim3(1), dim3(64), 0, stream, p);
   KX_HIP_CHECK(hipGetLastError());
-  auto wk = hprog.pb ? (lc ? write_kernel<true, true> : write_kernel<false, true>)
-                     : (lc ? write_kernel<true, false> : write_kernel<false, false>);
-  hipLaunchKernelGGL(wk, gw, dim3(NTD), lc ? curl : 0, stream, p);
+  const bool cl = lc && 2 * (sizeof(KxnProgram) + curl + KXN_COLS_HEAD) <= 160 * 1024;
+  auto wk = hprog.pb ? (cl ? write_kernel<true, true, true> : lc ? write_kernel<true, true, false> : write_kernel<false, true, false>)
+                     : (cl ? write_kernel<true, false, true> : lc ? write_kernel<true, false, false> : write_kernel<false, false, false>);
+  hipLaunchKernelGGL(wk, gw, dim3(NTD), cl ? curl + KXN_COLS_HEAD : lc ? curl : 0, stream, p);
   KX_HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(64), 0, stream, p);
   KX_HIP_CHECK(hipGetLastError());
