@@ -1584,13 +1584,13 @@ __device__ __forceinline__ bool pb_frame_at(const Src& w, uint64_t p, uint64_t l
 // 0x0A bytes inside nested messages through (a map<string, V> entry, a repeated field-1 message): their
 // false chains merged into the true one a record late, and the chain pass re-scanned group after group
 // (1 M PN records: 61 ms of the 77 ms decode in the chain kernel before this, round 5).
-// The candidate's body must also open with up to 8 well-formed fields (tag varint with a field number and a
+// The candidate's body must also open with up to 2 well-formed fields (tag varint with a field number and a
 // wire type of 0 / 1 / 2 / 5, its value inside the body): a 0x0A inside a record whose next byte happens to
 // be the length to the next record's start passed the frame checks, and the chain pass re-scanned its group
 // (1 M PN records tiled from 4 096: 28 groups, 0.58 ms of a 10.4 ms decode, round 6).
 __device__ __forceinline__ bool pb_body_plausible(const Src& w, uint64_t b, uint64_t e) {
   uint64_t q = b;
-  for (int k = 0; k < 8 && q < e; k++) {
+  for (int k = 0; k < 2 && q < e; k++) {
     uint64_t tag, v;
     uint32_t u;
     if (pb_varint(w, q, e - q, tag, u) || u > 5 || (tag >> 3) == 0) return false;
@@ -1615,12 +1615,12 @@ __device__ __forceinline__ bool pb_body_plausible(const Src& w, uint64_t b, uint
 __device__ __forceinline__ bool pb_frame_ok(const Src& w, uint64_t p, uint64_t len) {
   uint64_t e, e2;
   if (!pb_frame_at(w, p, len, &e)) return false;
+  if (e != len && !(ld1(w, e) == 0x0Au && pb_frame_at(w, e, len, &e2) && (e2 == len || ld1(w, e2) == 0x0Au)))
+    return false;
   uint64_t l;
   uint32_t u;
   (void)pb_varint(w, p + 1, len - p - 1, l, u);   // (pb_frame_at checked it)
-  if (!pb_body_plausible(w, p + 1 + u, e)) return false;
-  if (e == len) return true;
-  return ld1(w, e) == 0x0Au && pb_frame_at(w, e, len, &e2) && (e2 == len || ld1(w, e2) == 0x0Au);
+  return pb_body_plausible(w, p + 1 + u, e);   // last: true frames all reach it
 }
 
 // Kitex-Protobuf candidate in a lane's segment [seg_lo, seg_hi): the rotated, conflict-free scan
