@@ -1584,13 +1584,13 @@ __device__ __forceinline__ bool pb_frame_at(const Src& w, uint64_t p, uint64_t l
 // 0x0A bytes inside nested messages through (a map<string, V> entry, a repeated field-1 message): their
 // false chains merged into the true one a record late, and the chain pass re-scanned group after group
 // (1 M PN records: 61 ms of the 77 ms decode in the chain kernel before this, round 5).
-// The candidate's body must also open with up to 2 well-formed fields (tag varint with a field number and a
+// The candidate's body must also open with up to 3 well-formed fields (tag varint with a field number and a
 // wire type of 0 / 1 / 2 / 5, its value inside the body): a 0x0A inside a record whose next byte happens to
 // be the length to the next record's start passed the frame checks, and the chain pass re-scanned its group
 // (1 M PN records tiled from 4 096: 28 groups, 0.58 ms of a 10.4 ms decode, round 6).
 __device__ __forceinline__ bool pb_body_plausible(const Src& w, uint64_t b, uint64_t e) {
   uint64_t q = b;
-  for (int k = 0; k < 2 && q < e; k++) {
+  for (int k = 0; k < 3 && q < e; k++) {
     uint64_t tag, v;
     uint32_t u;
     if (pb_varint(w, q, e - q, tag, u) || u > 5 || (tag >> 3) == 0) return false;
