@@ -9,7 +9,7 @@ from collections import defaultdict
 d = sys.argv[1]
 KS = ("index_kernel<", "index_fast_kernel<", "redo_kernel<", "group_kernel<", "chain_kernel<", "chain_fast_kernel<",
       "emit_kernel<", "emit_fast_kernel<", "emit_redo_kernel<", "combo_kernel<", "write_kernel<", "size_kernel<",
-      "crc_kernel(")
+      "crc_kernel(", "measure_kernel<", "esize_kernel<", "ewrite_kernel<")
 agg = defaultdict(lambda: defaultdict(list))
 for p in ("p1", "p2"):
     for f in glob.glob(f"{d}/{p}/**/*counter_collection.csv", recursive=True):
