@@ -338,6 +338,9 @@ __device__ __forceinline__ int dskip_flat(const Src& w, uint64_t& pos, uint64_t 
   return KX_OK;
 }
 
+// LEAF: the in-place skips above (the skip decoder's record walk and the field loops' unknown fields); the frame
+// walker's PurePayload skip keeps the plain form, whose registers and scratch its TTHeader index kernel shares
+template <bool LEAF = true>
 __device__ __forceinline__ int dskip_body(const Src& w, uint64_t& pos, uint64_t limit, uint32_t t0, int md0) {
   uint64_t stk[66];
   int sp = 0;
@@ -381,7 +384,7 @@ __device__ __forceinline__ int dskip_body(const Src& w, uint64_t& pos, uint64_t 
             pos += 6 + b; if (--sp) top = stk[sp - 1]; continue;
           }
           pos += 6;
-          if (md > 1 && (ks > 0 || k == KX_T_STRING) && (vs > 0 || v == KX_T_STRING)) {
+          if (LEAF && md > 1 && (ks > 0 || k == KX_T_STRING) && (vs > 0 || v == KX_T_STRING)) {
             for (int32_t i = 0; i < cnt; i++) {
               int rc = dskip_leaf(w, pos, limit, ks);
               if (!rc) rc = dskip_leaf(w, pos, limit, vs);
@@ -406,7 +409,7 @@ __device__ __forceinline__ int dskip_body(const Src& w, uint64_t& pos, uint64_t 
             pos += 5 + b; if (--sp) top = stk[sp - 1]; continue;
           }
           pos += 5;
-          if (md > 1 && v == KX_T_STRING) {
+          if (LEAF && md > 1 && v == KX_T_STRING) {
             for (int32_t i = 0; i < cnt; i++) {
               const int rc = dskip_str(w, pos, limit);
               if (rc) return rc;
@@ -433,12 +436,12 @@ __device__ __forceinline__ int dskip_body(const Src& w, uint64_t& pos, uint64_t 
       }
       if (limit - pos < 2) return KX_ERR_EOF;
       pos += 2;
-      if (tp == KX_T_STRING && md > 1) {
+      if (LEAF && tp == KX_T_STRING && md > 1) {
         const int rc = dskip_str(w, pos, limit);
         if (rc) return rc;
         continue;
       }
-      if ((tp == KX_T_LIST || tp == KX_T_SET || tp == KX_T_MAP) && md > 2) {
+      if (LEAF && (tp == KX_T_LIST || tp == KX_T_SET || tp == KX_T_MAP) && md > 2) {
         bool done;
         const int rc = dskip_flat(w, pos, limit, tp, done);
         if (rc) return rc;
@@ -1815,7 +1818,7 @@ __device__ __forceinline__ int frame_one(const Src& w, uint64_t pos, uint64_t li
       if (nl < 0) return KX_ERR_NEGATIVE_SIZE;
       if (len - p < 12 + (uint64_t)nl) return KX_ERR_EOF;
       uint64_t q = pos + p + 12 + (uint64_t)nl;
-      const int rc = dskip_body(w, q, lim, KX_T_STRUCT, 64);
+      const int rc = dskip_body<false>(w, q, lim, KX_T_STRUCT, 64);
       if (rc) return rc;
       ps = p; pe = q - pos;
       fend = pe;
