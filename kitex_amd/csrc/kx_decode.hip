@@ -1615,11 +1615,15 @@ __device__ __forceinline__ bool pb_body_plausible(const Src& w, uint64_t b, uint
   }
   return true;
 }
+// BODY: also the body check (M_PBB, nested messages; flat M_PB records keep the two frame checks alone: the
+// body check cost the PF index pass 1.7 ms for nothing)
+template <bool BODY>
 __device__ __forceinline__ bool pb_frame_ok(const Src& w, uint64_t p, uint64_t len) {
   uint64_t e, e2;
   if (!pb_frame_at(w, p, len, &e)) return false;
   if (e != len && !(ld1(w, e) == 0x0Au && pb_frame_at(w, e, len, &e2) && (e2 == len || ld1(w, e2) == 0x0Au)))
     return false;
+  if (!BODY) return true;
   uint64_t l;
   uint32_t u;
   (void)pb_varint(w, p + 1, len - p - 1, l, u);   // (pb_frame_at checked it)
@@ -1631,6 +1635,7 @@ __device__ __forceinline__ bool pb_frame_ok(const Src& w, uint64_t p, uint64_t l
 // headers. Frame validation is a varint decode plus two probes, far too costly to run for every
 // 0x0A byte inside the scan loop (a divergent branch taken by the whole wave). If neither validates
 // the lane has no candidate and takes its entry from the chain below (speculation only).
+template <bool BODY>
 __device__ __forceinline__ uint64_t pb_scan_segment(const Src& w, uint64_t seg_lo, uint64_t seg_hi, uint64_t len,
                                                     int lane) {
   const int32_t q0 = wofs(w, seg_lo, SEG + 8);
@@ -1659,9 +1664,9 @@ __device__ __forceinline__ uint64_t pb_scan_segment(const Src& w, uint64_t seg_l
         else { c2 = rel; break; }
       }
   }
-  if (c1 < n && pb_frame_ok(w, seg_lo + c1, len)) return seg_lo + c1;
+  if (c1 < n && pb_frame_ok<BODY>(w, seg_lo + c1, len)) return seg_lo + c1;
   if (c2 >= n) return X_NONE;
-  if (pb_frame_ok(w, seg_lo + c2, len)) return seg_lo + c2;
+  if (pb_frame_ok<BODY>(w, seg_lo + c2, len)) return seg_lo + c2;
   // both lowest were false (0x0A bytes in the previous record's tail): the segment's later 0x0A bytes in
   // order, so the tile's first frame is still its entry (a later one would send the group to the chain
   // pass's serial re-scan)
@@ -1674,13 +1679,13 @@ __device__ __forceinline__ uint64_t pb_scan_segment(const Src& w, uint64_t seg_l
         const uint32_t rel = 4 * d + first_hit(m) - sh0;
         m &= m - 1;
         if (rel <= c2 || rel >= n) continue;
-        if (pb_frame_ok(w, seg_lo + rel, len)) return seg_lo + rel;
+        if (pb_frame_ok<BODY>(w, seg_lo + rel, len)) return seg_lo + rel;
       }
     }
     return X_NONE;
   }
   for (uint32_t rel = c2 + 1; rel < n; rel++)
-    if (ld1(w, seg_lo + rel) == 0x0Au && pb_frame_ok(w, seg_lo + rel, len)) return seg_lo + rel;
+    if (ld1(w, seg_lo + rel) == 0x0Au && pb_frame_ok<BODY>(w, seg_lo + rel, len)) return seg_lo + rel;
   return X_NONE;
 }
 
@@ -2167,7 +2172,7 @@ __device__ __forceinline__ Cand lane_candidate(KParams& dp, const Src& w, uint64
   cd.ent = X_NONE; cd.plim = seg_lo; cd.sig = 0; cd.smask = 0xffu; cd.s2o = 0; cd.s2 = 0; cd.strict = false;
   if (seg_lo >= seg_hi) return cd;
   if (MODE == M_PB || MODE == M_PBB) {   // Kitex-PB Batch frames
-    cd.ent = pb_scan_segment(w, seg_lo, seg_hi, dp.in_len, lane);
+    cd.ent = pb_scan_segment<MODE == M_PBB>(w, seg_lo, seg_hi, dp.in_len, lane);
     return cd;
   }
   if (MODE == M_FRAME) {
