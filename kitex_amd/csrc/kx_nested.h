@@ -1315,9 +1315,7 @@ KXN_HD void kxn_pb_put_uv(uint8_t* out, uint64_t* pos, uint64_t v) {
 }
 
 // the scalar of node N at instance e: *wire = its varint value, or its fixed bytes (*fixed = 4 / 8)
-KXN_HD uint64_t kxn_pb_wire_scalar(const KxnProgram& P, const KxnCols& C, const KxnNode& N, uint64_t e, int* fixed,
-                                   bool* zero) {
-  (void)P;
+KXN_HD uint64_t kxn_pb_wire_scalar_c(const KxnCols& C, const KxnNode& N, uint64_t e, int* fixed, bool* zero) {
   const uint64_t v = kxn_get_val(C, N.col, N.width, e);
   const uint32_t wt = kxn_pb_wt(N);
   *zero = (N.ttype == KX_T_BOOL ? (v & 0xff) : v) == 0;
@@ -1335,6 +1333,11 @@ KXN_HD uint64_t kxn_pb_wire_scalar(const KxnProgram& P, const KxnCols& C, const 
   }
   return N.pbk == KX_PB_SINT ? ((v << 1) ^ (uint64_t)((int64_t)v >> 63)) : v;
 }
+KXN_HD uint64_t kxn_pb_wire_scalar(const KxnProgram& P, const KxnCols& C, const KxnNode& N, uint64_t e, int* fixed,
+                                   bool* zero) {
+  (void)P;
+  return kxn_pb_wire_scalar_c(C, N, e, fixed, zero);
+}
 
 template <bool W>
 KXN_HD void kxn_pb_put_scalar(uint8_t* out, uint64_t* pos, uint64_t v, int fixed) {
@@ -1345,6 +1348,35 @@ KXN_HD void kxn_pb_put_scalar(uint8_t* out, uint64_t* pos, uint64_t v, int fixed
   } else {
     kxn_pb_put_uv<W>(out, pos, v);
   }
+}
+
+// a map entry's key (field 1) or value (field 2) that is a leaf: its tag + value bytes, and the writer
+KXN_HD uint64_t kxn_pb_leaf_size(const KxnCols& C, const KxnNode& V, int fnum, uint64_t e) {
+  const uint64_t tag = ((uint64_t)fnum << 3) | kxn_pb_wt(V);
+  if (V.kind == KN_SCALAR) {
+    int fixed;
+    bool zero;
+    const uint64_t v = kxn_pb_wire_scalar_c(C, V, e, &fixed, &zero);
+    return kxn_uvlen(tag) + (fixed ? (uint64_t)fixed : kxn_uvlen(v));
+  }
+  const uint64_t l = kxn_get_arr(C, V.col, V.level, e + 1) - kxn_get_arr(C, V.col, V.level, e);
+  return kxn_uvlen(tag) + kxn_uvlen(l) + l;
+}
+template <bool W>
+KXN_HD void kxn_pb_put_leaf(const KxnCols& C, const KxnNode& V, int fnum, uint64_t e, uint8_t* out, uint64_t* pos) {
+  const uint64_t tag = ((uint64_t)fnum << 3) | kxn_pb_wt(V);
+  kxn_pb_put_uv<W>(out, pos, tag);
+  if (V.kind == KN_SCALAR) {
+    int fixed;
+    bool zero;
+    const uint64_t v = kxn_pb_wire_scalar_c(C, V, e, &fixed, &zero);
+    kxn_pb_put_scalar<W>(out, pos, v, fixed);
+    return;
+  }
+  const uint64_t a = kxn_get_arr(C, V.col, V.level, e), z = kxn_get_arr(C, V.col, V.level, e + 1);
+  kxn_pb_put_uv<W>(out, pos, z - a);
+  if (W) kxn_copy(out + *pos, (const uint8_t*)C.data[V.col] + a, z - a);
+  *pos += z - a;
 }
 
 struct KxnPEFrame {     // encode: a message's fields, a repeated message's elements, a map's entries (48 B)
@@ -1472,6 +1504,20 @@ KXN_HD uint64_t kxn_pb_walk(const KxnProgram& P, const KxnCols& C, KxnPEFrame st
               pos += l;
             } else {
               sz += kxn_uvlen(tag) + kxn_uvlen(l) + l;
+            }
+          }
+        } else if (N.kind == KN_MAP && P.node[N.a].kind <= KN_RAW && P.node[N.b].kind <= KN_RAW) {
+          // entries of leaves: each entry's size from its key and value here, no entry frame and no size walk
+          const uint64_t tag = ((uint64_t)(uint16_t)G.id << 3) | 2u;
+          for (uint64_t j = a; j < z; j++) {
+            uint64_t body = 0;
+            for (int k = 0; k < 2; k++) body += kxn_pb_leaf_size(C, P.node[k == 0 ? N.a : N.b], k + 1, j);
+            if (W) {
+              kxn_pb_put_uv<W>(out, &pos, tag);
+              kxn_pb_put_uv<W>(out, &pos, body);
+              for (int k = 0; k < 2; k++) kxn_pb_put_leaf<W>(C, P.node[k == 0 ? N.a : N.b], k + 1, j, out, &pos);
+            } else {
+              sz += kxn_uvlen(tag) + kxn_uvlen(body) + body;
             }
           }
         } else {                                       // repeated messages / map entries: a frame
