@@ -551,7 +551,7 @@ def extras(args, r2, dev, local):
         st = b.status()
         views = getattr(b, "views", False)
         traffic, tnote = pmc_traffic(f"{b.cfg}_{b.mode}") if not views else \
-            pmc_traffic(f"{b.cfg}_views") if b.mode == "concat" else (None, "no profile of this workload")
+            pmc_traffic(f"{b.cfg}_views") if b.mode == "concat" else pmc_traffic(f"{b.cfg}_offsets_views")
         return {"records_per_s": b.n * steps / t, "ms_per_step": t / steps * 1e3, "verified": ok,
                 "decode_diag": {"tile_rewalks": st.diag[0], "group_rescans": st.diag[1]},
                 "roofline": roofline(b.in_bytes + b.out_bytes_per_record() * b.n, avg, "decode", traffic, tnote)}

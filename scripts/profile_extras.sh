@@ -7,7 +7,7 @@ set -u
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 TAG=$1; shift
-WL=${*:-frames_off frames_on nested_concat nested_offsets pb_nested r2_views}
+WL=${*:-frames_off frames_on nested_concat nested_offsets pb_nested r2_views r2_offsets r2_offsets_views}
 LIB=kitex_amd/lib/libkxcodec.so
 S=gpurun_out/${TAG}_summ
 mkdir -p $S

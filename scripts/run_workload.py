@@ -8,7 +8,8 @@ capacities too), so `scripts/pmc_summary.py DIR NAME all CALLS+1` can sum every 
 NAME: frames_off, frames_on (16 M TTHeader frames of R1 messages, CRC32Check off / on: bench.py
 frames_crc32c), nested_concat, nested_offsets (1 M baseline.thrift Nesting records, 4096 distinct tiled:
 bench.py nested_decode_encode), pb_nested (1 M PN records, Batch-framed: bench.py pb_nested), r2_views
-(16 M R2 records, string views: bench.py r2_decode_views)."""
+(16 M R2 records, string views: bench.py r2_decode_views), r2_offsets / r2_offsets_views (the same records
+with their offsets known, copies / views: bench.py r2_decode_offsets / r2_decode_offsets_views)."""
 import os
 import sys
 
@@ -65,12 +66,12 @@ def prep(name):
         units = cdc.DecodeSizes(buf, n)
         offs = cdc.Skip(buf, n).cpu().numpy() if name == "nested_offsets" else np.zeros(1, np.int64)
         np.savez(path(name), wire=wire, n=np.array([n]), units=np.array(units, dtype=np.int64), offs=offs)
-    elif name == "r2_views":
+    elif name in ("r2_views", "r2_offsets", "r2_offsets_views"):
         n = 16 << 20
         cdc = ThriftCodec(S.schema_r2())
         src = synth.TORCH_GENERATORS["r2"](n, dev)
-        wire, _ = cdc.Marshal(src)
-        np.savez(path(name), wire=wire.cpu().numpy(), n=np.array([n]))
+        wire, offs = cdc.Marshal(src)
+        np.savez(path(name), wire=wire.cpu().numpy(), n=np.array([n]), offs=offs.cpu().numpy())
     else:
         raise SystemExit(f"unknown workload {name}")
 
@@ -109,15 +110,16 @@ def run(name, calls):
 
         def call():
             cdc.Unmarshal(wire, n, offsets=offs, out=out, var_caps=vc, raise_on_error=False, status=st)
-    elif name == "r2_views":
+    elif name in ("r2_views", "r2_offsets", "r2_offsets_views"):
         cdc = ThriftCodec(S.schema_r2())
         ds = cdc.dschema
         caps = [0 if ci.kind == A.COL_FIXED else max(1, wire.numel()) for ci in ds.infos]
-        out = alloc_device(ds.infos, n, caps, ds.npresence, dev, views=True)
+        out = alloc_device(ds.infos, n, caps, ds.npresence, dev, views=name != "r2_offsets")
+        offs = torch.from_numpy(d["offs"]).to(dev) if name != "r2_views" else None
         st = status_tensor(dev)
 
         def call():
-            cdc.Unmarshal(wire, n, out=out, var_caps=caps, raise_on_error=False, status=st)
+            cdc.Unmarshal(wire, n, offsets=offs, out=out, var_caps=caps, raise_on_error=False, status=st)
     else:
         raise SystemExit(f"unknown workload {name}")
     for _ in range(calls + 1):
