@@ -763,7 +763,7 @@ def extras(args, r2, dev, local):
             e = decode_entry(bo)
             avg = e["roofline"]["avg_launch_ms"] / 1e3
             e["roofline"] = roofline(bo.in_bytes + 8 * (bo.n + 1) + bo.out_bytes_per_record() * bo.n, avg,
-                                     "decode (known offsets)")
+                                     "decode (known offsets)", *pmc_traffic("r2_offsets"))
             out["r2_decode_offsets"] = {"records": bo.n, **e}
             del bo
             torch.cuda.empty_cache()
@@ -772,7 +772,7 @@ def extras(args, r2, dev, local):
             e = decode_entry(bov)
             avg = e["roofline"]["avg_launch_ms"] / 1e3
             e["roofline"] = roofline(bov.in_bytes + 8 * (bov.n + 1) + bov.out_bytes_per_record() * bov.n, avg,
-                                     "decode (known offsets, views: emit pass alone)")
+                                     "decode (known offsets, views: emit pass alone)", *pmc_traffic("r2_offsets_views"))
             e["roofline"]["read_only_frac"] = bov.in_bytes / avg / 1e9 / HBM_PEAK_GBS
             out["r2_decode_offsets_views"] = {"records": bov.n, "out_bytes_per_record": bov.out_bytes_per_record(),
                                               **e}
