@@ -666,7 +666,8 @@ def extras(args, r2, dev, local):
         eq = all(bool(torch.equal(a, b)) for a, b in zip(tensors(outc), tensors(back.columns)))
         res["encode"] = {"records_per_s": n * steps / t, "ms_per_step": t / steps * 1e3,
                          "round_trip_equal": eq and bool(torch.equal(buf, w2)),
-                         "roofline": roofline(out_bytes + buf.numel(), avg, "nested encode (size + write)")}
+                         "roofline": roofline(out_bytes + buf.numel(), avg, "nested encode (size + write)",
+                                              *pmc_traffic("pb_nested_encode" if pb else "nested_encode"))}
         note("  nested round trip compared; cpu baseline")
         if not args.no_cpu:
             cb = nested_cpu_baseline(sch, cpu_recs, n, pb)

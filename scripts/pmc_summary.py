@@ -7,6 +7,7 @@ WRITE_SIZE are in KiB; gfx950 FETCH_SIZE counts half of a wide streaming read ->
   mode "crc": the CRC32C Generate kernels of scripts/run_crc.py
   python scripts/pmc_summary.py <dir> <name> all <calls>  -> profiles/pmc_<name>.json: every codec kernel of a
   scripts/run_workload.py run (it launches no other), per call of `calls`
+  mode "nenc" (same arguments): the nested encoder's kernels only (its run decodes the columns once first)
 """
 import csv
 import glob
@@ -19,6 +20,7 @@ DECODE = ("index_kernel", "index_fast_kernel", "redo_kernel", "group_kernel", "c
           "emit_fast_kernel", "emit_redo_kernel", "finalize_kernel")
 ENCODE = ("size_kernel", "scan_kernel", "write_kernel")
 CRC = ("crc_kernel", "crc_final_kernel")
+NENC = ("esize_kernel", "escan_kernel", "ewrite_kernel")   # the nested encoder
 KERNELS = DECODE
 
 
@@ -48,11 +50,12 @@ def counter_sums(path, counter):
 def main():
     global KERNELS
     d, cfg, mode = sys.argv[1], sys.argv[2], sys.argv[3]
-    KERNELS = None if mode == "all" else ENCODE if mode == "encode" else CRC if mode == "crc" else DECODE
+    KERNELS = None if mode == "all" else NENC if mode == "nenc" else ENCODE if mode == "encode" else CRC if mode == "crc" \
+        else DECODE
     last = "write_kernel" if mode == "encode" else "crc_kernel" if mode == "crc" else "emit_kernel"
     fetch = counter_sums(os.path.join(d, "fetch"), "FETCH_SIZE")
     write = counter_sums(os.path.join(d, "write"), "WRITE_SIZE")
-    if mode == "all":
+    if mode in ("all", "nenc"):
         calls = int(sys.argv[4])
     else:
         # one launch of every kernel of the pipeline per call: the most-launched one counts the calls (the
@@ -77,7 +80,7 @@ def main():
             sha = fh.read().strip()
     except OSError:
         pass
-    res = {"workload": cfg if mode == "all" else f"{cfg}_{mode}" if mode in ("encode", "crc") else f"{cfg}_decode_{mode}",
+    res = {"workload": cfg if mode in ("all", "nenc") else f"{cfg}_{mode}" if mode in ("encode", "crc") else f"{cfg}_decode_{mode}",
            "calls": calls, "lib_sha256": sha,
            "hbm_bytes_per_launch": fetch_b + write_b, "fetch_bytes_per_call": fetch_b,
            "write_bytes_per_call": write_b, "per_kernel": per_kernel,
@@ -87,7 +90,7 @@ def main():
                    "uses it only when lib_sha256 matches the library it times"}
     odir = os.environ.get("PMC_OUT") or os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                                      "profiles")
-    out = os.path.join(odir, f"pmc_{cfg}.json" if mode == "all" else f"pmc_{cfg}_{mode}.json")
+    out = os.path.join(odir, f"pmc_{cfg}.json" if mode in ("all", "nenc") else f"pmc_{cfg}_{mode}.json")
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1)
     print(json.dumps(res, indent=1))

@@ -27,7 +27,8 @@ for w in $WL; do
     echo "$w $pass rc=$rc"
     [ $rc = 0 ] || exit $rc
   done
-  PMC_OUT=$S python3 scripts/pmc_summary.py $OUT $w all 4 > /dev/null || exit 1
+  M=all; case $w in *_encode) M=nenc;; esac
+  PMC_OUT=$S python3 scripts/pmc_summary.py $OUT $w $M 4 > /dev/null || exit 1
   f=$(find $OUT/stats -name "*kernel_stats.csv" | head -1)
   cp "$f" $S/${w}_kernel_stats.csv
   rm -rf $OUT /tmp/kxw_$w.npz

@@ -8,7 +8,8 @@ capacities too), so `scripts/pmc_summary.py DIR NAME all CALLS+1` can sum every 
 NAME: frames_off, frames_on (16 M TTHeader frames of R1 messages, CRC32Check off / on: bench.py
 frames_crc32c), nested_concat, nested_offsets (1 M baseline.thrift Nesting records, 4096 distinct tiled:
 bench.py nested_decode_encode), pb_nested (1 M PN records, Batch-framed: bench.py pb_nested), r2_views
-(16 M R2 records, string views: bench.py r2_decode_views), r2_offsets / r2_offsets_views (the same records
+(16 M R2 records, string views: bench.py r2_decode_views), nested_encode / pb_nested_encode (the columns of
+one decode, encoded: bench.py nested_decode_encode.encode / pb_nested.encode; summarise with mode "nenc"), r2_offsets / r2_offsets_views (the same records
 with their offsets known, copies / views: bench.py r2_decode_offsets / r2_decode_offsets_views)."""
 import os
 import sys
@@ -46,9 +47,9 @@ def prep(name):
         fr[:, H - len(info) + 15:H - len(info) + 23] = torch.where(nib < 10, nib + 48, nib + 87).to(torch.uint8)
         fr[:, H:] = msgs.view(n, M)
         np.savez(path(name), wire=fr.view(-1).cpu().numpy(), n=np.array([n]))
-    elif name.startswith("nested") or name == "pb_nested":
+    elif name.startswith("nested") or name.startswith("pb_nested"):
         n, k = 1 << 20, 4096
-        if name == "pb_nested":
+        if name.startswith("pb_nested"):
             from tests import pbn_cases as PB
             sch = PB.schema_pn()
             cdc = ProtobufCodec(sch)
@@ -93,8 +94,8 @@ def run(name, calls):
 
         def call():
             cdc.UnmarshalFrames(wire, n, raise_on_error=False, crc32_check=name == "frames_on")
-    elif name.startswith("nested") or name == "pb_nested":
-        if name == "pb_nested":
+    elif name.startswith("nested") or name.startswith("pb_nested"):
+        if name.startswith("pb_nested"):
             from tests import pbn_cases as PB
             cdc = ProtobufCodec(PB.schema_pn())
         else:
@@ -110,6 +111,15 @@ def run(name, calls):
 
         def call():
             cdc.Unmarshal(wire, n, offsets=offs, out=out, var_caps=vc, raise_on_error=False, status=st)
+        if name.endswith("_encode"):   # the columns of one decode; the first Marshal is the warm-up
+            call()
+            w2, _ = cdc.Marshal(out)
+            buf = torch.empty_like(w2)
+            st2 = status_tensor(dev)
+
+            def call():
+                cdc.Marshal(out, with_offsets=False, out=buf, status=st2, check_status=False)
+            calls -= 1
     elif name in ("r2_views", "r2_offsets", "r2_offsets_views"):
         cdc = ThriftCodec(S.schema_r2())
         ds = cdc.dschema
